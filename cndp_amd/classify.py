@@ -1,0 +1,144 @@
+"""Python host API of the MI355X classify path (include/cndp_gpu.h).
+
+    c = Classifier(device=0)
+    c.set_rss(key=None, reta=None, nb_queues=16)
+    c.set_fib(fib4, fib6)
+    out = c.classify(frames, mode=CNDP_MODE_L3FWD)      # device-resident
+    out = c.classify_host(np_slab, n, ...)              # host buffers (PCIe)
+
+Frames carry torch tensors (the slab lives in HBM when they are on cuda);
+outputs are allocated as torch tensors on the same device unless given.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import native as N
+
+
+class Classifier:
+    def __init__(self, device: int = -1):
+        self._L = N.lib()
+        h = ctypes.c_void_p()
+        N.check(self._L.cndp_gpu_init(device, ctypes.byref(h)), "cndp_gpu_init")
+        self.h = h
+        self.device = self._L.cndp_gpu_device(h)
+        self.reta_size = 128
+        self.fib4 = None
+        self.fib6 = None
+
+    def close(self):
+        if self.h:
+            self._L.cndp_gpu_fini(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_rss(self, key: bytes | None = None, reta=None, nb_queues: int = 16):
+        rarr = None
+        size = 0
+        if reta is not None:
+            rarr = np.ascontiguousarray(reta, dtype=np.uint16)
+            size = len(rarr)
+        N.check(self._L.cndp_gpu_set_rss(self.h, key, len(key) if key else 0,
+                                         rarr.ctypes.data if rarr is not None else None, size,
+                                         nb_queues), "cndp_gpu_set_rss")
+        self.reta_size = size or 128
+
+    def set_fib(self, fib4=None, fib6=None):
+        N.check(self._L.cndp_gpu_set_fib(self.h, fib4.h if fib4 else None, fib6.h if fib6 else None),
+                "cndp_gpu_set_fib")
+        self.fib4, self.fib6 = fib4, fib6
+
+    def alloc_outputs(self, n: int, n_bins: int = 64, device=None, edge: bool = True):
+        import torch
+        dev = device if device is not None else f"cuda:{self.device}"
+        return {
+            "nh": torch.empty(n, dtype=torch.int32, device=dev),
+            "hash": torch.empty(n, dtype=torch.int32, device=dev),
+            "queue": torch.empty(n, dtype=torch.int16, device=dev),
+            "edge": torch.empty(n, dtype=torch.uint8, device=dev) if edge else None,
+            "bins": torch.zeros(n_bins + 2, dtype=torch.int64, device=dev),
+            "n_bins": n_bins,
+        }
+
+    @staticmethod
+    def _ptr(t):
+        return t.data_ptr() if t is not None else None
+
+    def batch(self, frames, mode: int, out: dict, buf_len: int = 1984, offsets_t=None) -> "N.Batch":
+        b = N.Batch()
+        b.mode = mode
+        b.n = frames.n
+        b.slab = frames.slab.data_ptr()
+        b.slab_len = frames.slab.numel()
+        b.stride = frames.stride
+        off = offsets_t if offsets_t is not None else frames.offsets
+        b.offsets = off.data_ptr() if off is not None else None
+        b.data_off = frames.data_off
+        b.buf_len = buf_len
+        b.nh = self._ptr(out.get("nh"))
+        b.hash = self._ptr(out.get("hash"))
+        b.queue = self._ptr(out.get("queue"))
+        b.edge = self._ptr(out.get("edge"))
+        b.bins = self._ptr(out.get("bins"))
+        b.n_bins = out.get("n_bins", 64)
+        return b
+
+    def classify(self, frames, mode: int = N.CNDP_MODE_L3FWD, out: dict | None = None,
+                 n_bins: int = 64, buf_len: int = 1984, stream: int | None = None) -> dict:
+        """Enqueue one classify pass on `stream` (default: torch's current
+        stream of the device).  Returns the output dict (torch tensors)."""
+        import torch
+        if out is None:
+            out = self.alloc_outputs(frames.n, n_bins, device=frames.slab.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.slab.device).cuda_stream
+        b = self.batch(frames, mode, out, buf_len)
+        N.check(self._L.cndp_gpu_classify(self.h, ctypes.byref(b), stream or None), "cndp_gpu_classify")
+        return out
+
+    def classify_host(self, slab: np.ndarray, n: int, mode: int, stride: int = 64, offsets=None,
+                      data_off: int = 0, buf_len: int = 1984, n_bins: int = 64) -> dict:
+        """Host buffers in, host results out (H2D + kernel + D2H, PCIe-bound)."""
+        slab = np.ascontiguousarray(slab, dtype=np.uint8)
+        out = {"nh": np.zeros(n, np.uint32), "hash": np.zeros(n, np.uint32),
+               "queue": np.zeros(n, np.uint16), "edge": np.zeros(n, np.uint8),
+               "bins": np.zeros(n_bins + 2, np.uint64)}
+        off = np.ascontiguousarray(offsets, dtype=np.uint64) if offsets is not None else None
+        b = N.Batch()
+        b.mode, b.n, b.slab, b.slab_len = mode, n, slab.ctypes.data, slab.nbytes
+        b.stride, b.offsets, b.data_off, b.buf_len = stride, off.ctypes.data if off is not None else None, data_off, buf_len
+        b.nh, b.hash, b.queue = out["nh"].ctypes.data, out["hash"].ctypes.data, out["queue"].ctypes.data
+        b.edge, b.bins, b.n_bins = out["edge"].ctypes.data, out["bins"].ctypes.data, n_bins
+        N.check(self._L.cndp_gpu_classify_host(self.h, ctypes.byref(b)), "cndp_gpu_classify_host")
+        return out
+
+    def bin_partition(self, bin_of, n_bins: int, stream: int | None = None):
+        """Stable partition of packet indices by bin id (per-edge streams)."""
+        import torch
+        n = bin_of.numel()
+        start = torch.empty(n_bins + 3, dtype=torch.int32, device=bin_of.device)
+        order = torch.empty(max(n, 1), dtype=torch.int32, device=bin_of.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(bin_of.device).cuda_stream
+        N.check(self._L.cndp_gpu_bin_partition(self.h, bin_of.data_ptr(), n, n_bins, start.data_ptr(),
+                                               order.data_ptr(), stream or None), "cndp_gpu_bin_partition")
+        return start, order[:n]
+
+    def bin_ids(self, mode: int, out: dict, n: int, n_bins: int, stream: int | None = None):
+        import torch
+        dev = out["queue"].device
+        bins = torch.empty(n, dtype=torch.int16, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        N.check(self._L.cndp_gpu_bin_ids(self.h, mode, self._ptr(out.get("nh")), self._ptr(out.get("edge")),
+                                         self._ptr(out.get("queue")), n, n_bins, bins.data_ptr(),
+                                         stream or None), "cndp_gpu_bin_ids")
+        return bins

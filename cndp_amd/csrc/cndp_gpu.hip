@@ -1,0 +1,1284 @@
+// cndp_gpu.hip -- MI355X (gfx950) device runtime and kernels of libcndp_gpu.so.
+//
+// Kernels (one packet per lane, wave64, no MFMA -- pure integer/byte work):
+//   k_classify_fast<MODE>  l3fwd / hash modes: fixed-offset header fields
+//                          (Eth + IPv4 at 14) loaded straight into VGPRs,
+//                          Toeplitz by byte-sliced tables in LDS, DIR-24-8
+//                          gather, per-block LDS bin counters.
+//   k_classify_cnet        cnet mode: each lane's 64-byte header window is
+//                          staged in LDS (17-dword rows: conflict-free for
+//                          equal offsets across lanes), cne_get_ptype parse
+//                          from LDS with variable offsets, IPv4 checksum,
+//                          DIR-24-8 / trie gathers.
+//   k_lookup4<W>/k_lookup6<W>  bulk FIB lookups (cne_fib[6]_lookup_bulk).
+//   k_bin_ids, k_part_*    stable partition into per-edge streams.
+// Reference behaviour each kernel restates is cited inline (CNDP v25.08.0).
+
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fib_internal.h"
+#include "../../include/cndp_gpu.h"
+
+#define CNDP_VERSION "cndp_amd 0.1 (gfx950)"
+
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) {                                                                  \
+            fprintf(stderr, "cndp_gpu: %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(e_),   \
+                    __FILE__, __LINE__);                                                         \
+            return e_ == hipErrorNoDevice || e_ == hipErrorInvalidDevice ? -ENODEV : -EIO;       \
+        }                                                                                        \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+__device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
+{
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+
+// bounded global byte read (bytes past the slab end read as 0)
+__device__ __forceinline__ uint32_t gbyte(const uint8_t *p, uint64_t avail, uint64_t o)
+{
+    return o < avail ? (uint32_t)p[o] : 0u;
+}
+// 4 bytes at o assembled little-endian, bounded
+__device__ __forceinline__ uint32_t gld32(const uint8_t *p, uint64_t avail, uint64_t o)
+{
+    return gbyte(p, avail, o) | (gbyte(p, avail, o + 1) << 8) | (gbyte(p, avail, o + 2) << 16) |
+           (gbyte(p, avail, o + 3) << 24);
+}
+
+// DIR-24-8 4B lookup, dir24_8.h:131-135
+__device__ __forceinline__ uint32_t lpm4(const uint32_t *__restrict__ t24,
+                                         const uint32_t *__restrict__ t8, uint32_t ip)
+{
+    uint32_t e = t24[ip >> 8];
+    if (e & 1u)
+        e = t8[(e >> 1) * 256u + (ip & 0xffu)];
+    return e >> 1;
+}
+
+// Toeplitz byte table access: T[b][v] at tab[b * 256 + v]
+__device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_t x)
+{
+    // the 4 stream bytes b..b+3 held little-endian in x (byte b = x & 0xff)
+    return tab[(b + 0) * 256 + (x & 0xffu)] ^ tab[(b + 1) * 256 + ((x >> 8) & 0xffu)] ^
+           tab[(b + 2) * 256 + ((x >> 16) & 0xffu)] ^ tab[(b + 3) * 256 + (x >> 24)];
+}
+
+struct KArgs {
+    const uint8_t *slab;
+    uint64_t slab_len;
+    uint64_t stride;
+    const uint64_t *offsets;
+    uint32_t data_off;
+    uint32_t n;
+    uint32_t buf_len;
+    uint32_t reta_mask;
+    const uint32_t *tbl24;
+    const uint32_t *tbl8;
+    const uint32_t *tbl24_6;
+    const uint32_t *tbl8_6;
+    const uint32_t *ttab; // 36 x 256 Toeplitz byte tables (global)
+    const uint16_t *reta;
+    uint32_t *nh;
+    uint32_t *hash;
+    uint16_t *queue;
+    uint8_t *edge;
+    unsigned long long *bins;
+    uint32_t n_bins;
+};
+
+#define FAST_THREADS 256
+#define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
+#define TAB_POS 36  /* ... for the IPv6 L4 tuple */
+
+// Bins (identical to oracle.c classify_one)
+template <int MODE>
+__device__ __forceinline__ uint32_t bin_of(uint32_t nh, uint32_t edge, uint32_t q, uint32_t nb)
+{
+    if (MODE == CNDP_MODE_HASH)
+        return q < nb ? q : nb + 1;
+    if (MODE == CNDP_MODE_L3FWD) {
+        if (edge == 0)
+            return (nh & 0xffffu) < nb ? (nh & 0xffffu) : nb + 1;
+        return (edge == 1 || edge == 0xFFu) ? nb : nb + 1;
+    }
+    if (edge == 1)
+        return (nh & 0xffffffu) < nb ? (nh & 0xffffffu) : nb + 1;
+    return (edge == 0 || edge == 0x80u) ? nb : nb + 1;
+}
+
+// IPv6 flow hash when the tables are not all in LDS (l3fwd/hash modes);
+// addresses at ip+8 / ip+24, ports at ip+40 (no extension headers there).
+__device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip, bool l4,
+                                   const uint32_t *__restrict__ ttab)
+{
+    uint32_t h = 0;
+    for (uint32_t k = 0; k < 8; k++)
+        h ^= tz4(ttab, 4 * k, gld32(p, avail, ip + 8 + 4 * k));
+    if (l4)
+        h ^= tz4(ttab, 32, gld32(p, avail, ip + 40));
+    return h;
+}
+
+// ---------------------------------------------------------------------------
+// l3fwd / hash classify: pktdev_rx.c:24-34 + pkt_cls.c:19-31 + ip4_lookup.c
+// :108-154 (+ build-defined Toeplitz / RSS queue).  Header fields sit at fixed
+// offsets (Ethernet 14 B, no VLAN parse in this chain), so each lane loads
+// bytes 12..39 of its frame into 7 VGPRs and never touches them again.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
+{
+    __shared__ uint32_t s_t[TAB4_POS * 256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB4_POS * 256; k += FAST_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += FAST_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint64_t step = (uint64_t)gridDim.x * FAST_THREADS;
+    for (uint64_t i = (uint64_t)blockIdx.x * FAST_THREADS + tid; i < a.n; i += step) {
+        const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
+        const uint8_t *p = a.slab + base;
+        const uint64_t avail = base < a.slab_len ? a.slab_len - base : 0;
+        uint32_t w3, w4, w5, w6, w7, w8, w9;
+        if (avail >= 48 && (base & 15u) == 0) {
+            const uint4 q0 = *(const uint4 *)(p + 0);
+            const uint4 q1 = *(const uint4 *)(p + 16);
+            const uint2 q2 = *(const uint2 *)(p + 32);
+            w3 = q0.w;
+            w4 = q1.x;
+            w5 = q1.y;
+            w6 = q1.z;
+            w7 = q1.w;
+            w8 = q2.x;
+            w9 = q2.y;
+        } else if (avail >= 40 && (base & 3u) == 0) {
+            const uint32_t *d = (const uint32_t *)p;
+            w3 = d[3];
+            w4 = d[4];
+            w5 = d[5];
+            w6 = d[6];
+            w7 = d[7];
+            w8 = d[8];
+            w9 = d[9];
+        } else {
+            w3 = gld32(p, avail, 12);
+            w4 = gld32(p, avail, 16);
+            w5 = gld32(p, avail, 20);
+            w6 = gld32(p, avail, 24);
+            w7 = gld32(p, avail, 28);
+            w8 = gld32(p, avail, 32);
+            w9 = gld32(p, avail, 36);
+        }
+        (void)w4;
+        const uint32_t et = bswap16(w3 & 0xffffu);
+        uint32_t h = 0, nh = CNDP_NH_INVALID, edge;
+        if (et == 0x0800u) {
+            const uint32_t ihl = (w3 >> 16) & 0xfu;
+            const uint32_t proto = w5 >> 24;
+            const uint32_t frag = bswap16(w5 & 0xffffu) & 0x3fffu;
+            const uint32_t src = alignb(w7, w6, 2);
+            const uint32_t dst = alignb(w8, w7, 2);
+            h = tz4(s_t, 0, src) ^ tz4(s_t, 4, dst);
+            if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
+                const uint32_t ports = ihl == 5 ? alignb(w9, w8, 2) : gld32(p, avail, 14 + 4 * ihl);
+                h ^= tz4(s_t, 8, ports);
+            }
+            if (MODE == CNDP_MODE_L3FWD)
+                nh = lpm4(a.tbl24, a.tbl8, bswap32(dst));
+        } else if (et == 0x86DDu) {
+            const uint32_t nx = w5 & 0xffu; // ip6 next header: frame byte 20
+            h = hash_v6_global(p, avail, 14, nx == 6u || nx == 17u, a.ttab);
+        }
+        if (MODE == CNDP_MODE_HASH)
+            edge = 0;
+        else
+            edge = et == 0x0800u ? ((nh >> 16) & 0xffu) : 0xFFu;
+        const uint32_t q = s_reta[h & a.reta_mask];
+        if (a.nh)
+            a.nh[i] = nh;
+        if (a.hash)
+            a.hash[i] = h;
+        if (a.queue)
+            a.queue[i] = (uint16_t)q;
+        if (a.edge)
+            a.edge[i] = (uint8_t)edge;
+        if (count)
+            atomicAdd(&s_bins[bin_of<MODE>(nh, edge, q, a.n_bins)], 1u);
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// cnet classify: eth_rx (cne_get_ptype) -> ptype -> ip4_input / ip6_input.
+// ---------------------------------------------------------------------------
+#define CNET_THREADS 512
+#define WIN_DW 16      /* 64-byte window per lane */
+#define ROW_DW 17      /* padded row: lane L dword k sits in bank (L + k) % 32 */
+
+struct Win {
+    const uint32_t *row; // LDS row, bytes 0..63 of the frame (zero past avail)
+    const uint8_t *g;
+    uint64_t avail;
+    __device__ __forceinline__ uint32_t ld32(uint32_t o) const
+    {
+        if (o + 4 <= 64) {
+            const uint32_t lo = row[o >> 2], hi = row[(o >> 2) + 1];
+            return alignb(hi, lo, o & 3u);
+        }
+        return gld32(g, avail, o);
+    }
+    __device__ __forceinline__ uint32_t b8(uint32_t o) const
+    {
+        return o < 64 ? (row[o >> 2] >> ((o & 3u) * 8)) & 0xffu : gbyte(g, avail, o);
+    }
+    __device__ __forceinline__ uint32_t raw16(uint32_t o) const { return ld32(o) & 0xffffu; }
+    __device__ __forceinline__ uint32_t be16(uint32_t o) const { return bswap16(ld32(o) & 0xffffu); }
+    __device__ __forceinline__ uint32_t be32(uint32_t o) const { return bswap32(ld32(o)); }
+};
+
+#define BE16C(x) ((uint32_t)((((x) & 0xffu) << 8) | (((x) >> 8) & 0xffu)))
+
+struct Lens {
+    uint32_t l2, l3;
+};
+
+__device__ __forceinline__ uint32_t pt_l3_ip(uint32_t vihl)
+{
+    return vihl == 0x45u ? 0x10u : (vihl >= 0x46u && vihl <= 0x4fu) ? 0x30u : 0u;
+}
+__device__ __forceinline__ uint32_t pt_l4(uint32_t p)
+{
+    return p == 17u ? 0x200u : p == 6u ? 0x100u : p == 132u ? 0x400u : 0u;
+}
+__device__ __forceinline__ bool v6_ext(uint32_t p)
+{
+    return p == 0u || p == 43u || p == 44u || p == 50u || p == 51u || p == 60u;
+}
+
+// pktmbuf_ptype.c:426-468 (skip_ip6_ext); returns -1 past 5 headers
+__device__ int skip_v6_ext(const Win &w, uint32_t proto, uint32_t &off, int &frag)
+{
+    frag = 0;
+    for (int i = 0; i < 5; i++) {
+        if (proto == 0u || proto == 43u || proto == 60u) {
+            const uint32_t x = w.ld32(off);
+            proto = x & 0xffu;
+            off += (((x >> 8) & 0xffu) + 1u) * 8u;
+        } else if (proto == 44u) {
+            proto = w.b8(off);
+            off += 8;
+            frag = 1;
+            return (int)proto;
+        } else if (proto == 59u) {
+            return 0;
+        } else {
+            return (int)proto;
+        }
+    }
+    return -1;
+}
+
+// cne_get_ptype, pktmbuf_ptype.c:472-744, all layers (CNE_PTYPE_ALL_MASK).
+// Only l2_len / l3_len are consumed downstream (eth_rx.c:56-60 + the input
+// nodes), so the inner-header lengths are not tracked; the ptype bits are.
+__device__ uint32_t get_ptype(const Win &w, Lens &ln)
+{
+    uint32_t pt = 0x1u, off = 14, proto = w.raw16(12);
+    int ret;
+    ln.l2 = 14;
+    ln.l3 = 0;
+    if (proto == BE16C(0x0806u))
+        return 0x3u;
+    if (proto != BE16C(0x0800u)) {
+        if (proto == BE16C(0x8100u)) {
+            pt = 0x6u;
+            proto = w.raw16(off + 2);
+            off += 4;
+            ln.l2 += 4;
+        } else if (proto == BE16C(0x88A8u)) {
+            pt = 0x7u;
+            proto = w.raw16(off + 6);
+            off += 8;
+            ln.l2 += 8;
+        } else if (proto == BE16C(0x8847u) || proto == BE16C(0x8848u)) {
+            return pt; // :541-556 never sets the MPLS bits
+        }
+    }
+    if (proto == BE16C(0x0800u)) {
+        const uint32_t ip = off;
+        const uint32_t x0 = w.ld32(ip);
+        pt |= pt_l3_ip(x0 & 0xffu);
+        ln.l3 = (x0 & 0xfu) * 4u;
+        off += ln.l3;
+        const uint32_t x6 = w.ld32(ip + 6);
+        if ((x6 & 0xffffu) & BE16C(0x3fffu))
+            return pt | 0x300u;
+        proto = (x6 >> 24) & 0xffu; // byte ip+9
+        pt |= pt_l4(proto);
+    } else if (proto == BE16C(0x86DDu)) {
+        int frag = 0;
+        proto = w.b8(off + 6);
+        ln.l3 = 40;
+        off += 40;
+        pt |= v6_ext(proto) ? 0xc0u : 0x40u;
+        if ((pt & 0xf0u) == 0xc0u) {
+            ret = skip_v6_ext(w, proto, off, frag);
+            if (ret < 0)
+                return pt;
+            proto = (uint32_t)ret;
+            ln.l3 = off - ln.l2;
+        }
+        if (proto == 0u)
+            return pt;
+        if (frag)
+            return pt | 0x300u;
+        pt |= pt_l4(proto);
+    }
+    const uint32_t l4t = pt & 0xf00u;
+    if (l4t == 0x200u) {
+        const uint32_t dport = w.raw16(ln.l2 + ln.l3 + 2);
+        if (dport == BE16C(2152u))
+            pt |= 0x8000u;
+        else if (dport == BE16C(2123u))
+            pt |= 0x7000u;
+        return pt;
+    }
+    if (l4t == 0x100u || l4t == 0x400u)
+        return pt;
+
+    // tunnels (:372-411)
+    if (proto == 47u) {
+        const uint32_t x = w.ld32(off);
+        const uint32_t flags = bswap16(x & 0xffffu) >> 12;
+        const uint32_t olen = flags == 0 ? 4 : (flags == 1 || flags == 2 || flags == 8) ? 8
+                            : (flags == 3 || flags == 9 || flags == 10)           ? 12
+                            : flags == 11                                         ? 16
+                                                                                  : 0;
+        if (olen) {
+            proto = x >> 16;
+            off += olen;
+            pt |= proto == BE16C(0x6558u) ? 0x4000u : 0x2000u;
+        }
+    } else if (proto == 4u) {
+        proto = BE16C(0x0800u);
+        pt |= 0x1000u;
+    } else if (proto == 41u) {
+        proto = BE16C(0x86DDu);
+        pt |= 0x1000u;
+    }
+    // inner headers (:617-744); note the reference compares IP protocol
+    // numbers against htobe16() ethertypes here, so proto 8 / 129 alias
+    // IPv4 / VLAN -- reproduced as is.
+    if (proto == BE16C(0x6558u)) {
+        pt |= 0x10000u;
+        proto = w.raw16(off + 12);
+        off += 14;
+    }
+    if (proto == BE16C(0x8100u)) {
+        pt = (pt & ~0xf0000u) | 0x20000u;
+        proto = w.raw16(off + 2);
+        off += 4;
+    } else if (proto == BE16C(0x88A8u)) {
+        pt = (pt & ~0xf0000u) | 0x30000u;
+        proto = w.raw16(off + 6);
+        off += 8;
+    }
+    if (proto == BE16C(0x0800u)) {
+        const uint32_t x0 = w.ld32(off);
+        const uint32_t v = x0 & 0xffu;
+        pt |= v == 0x45u ? 0x100000u : (v >= 0x46u && v <= 0x4fu) ? 0x200000u : 0u;
+        const uint32_t x6 = w.ld32(off + 6);
+        off += (x0 & 0xfu) * 4u;
+        if ((x6 & 0xffffu) & BE16C(0x3fffu))
+            return pt | 0x3000000u;
+        const uint32_t p4 = (x6 >> 24) & 0xffu;
+        pt |= p4 == 17u ? 0x2000000u : p4 == 6u ? 0x1000000u : p4 == 132u ? 0x4000000u : 0u;
+    } else if (proto == BE16C(0x86DDu)) {
+        int frag = 0;
+        proto = w.b8(off + 6);
+        off += 40;
+        pt |= v6_ext(proto) ? 0x500000u : 0x300000u;
+        if ((pt & 0xf00000u) == 0x500000u) {
+            ret = skip_v6_ext(w, proto, off, frag);
+            if (ret < 0)
+                return pt;
+            proto = (uint32_t)ret;
+        }
+        if (proto == 0u)
+            return pt;
+        if (frag)
+            return pt | 0x3000000u;
+        pt |= proto == 17u ? 0x2000000u : proto == 6u ? 0x1000000u : proto == 132u ? 0x4000000u : 0u;
+    }
+    return pt;
+}
+
+// lib/cnet/ptype/ptype.c:32-46 (indexed by ptype & 0xffff)
+__device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
+{
+    switch (pt & 0xffffu) {
+    case 0x0003u:
+        return 2u; // FRAME_PUNT
+    case 0x0211u:
+    case 0x0111u:
+    case 0x0231u:
+    case 0x0291u:
+        return 3u; // IP4_INPUT
+    case 0x0241u:
+    case 0x0141u:
+    case 0x02c1u:
+    case 0x02e1u:
+        return 4u; // IP6_INPUT
+    case 0x8211u:
+    case 0x8241u:
+        return 5u; // GTPU_INPUT
+    default:
+        return 0u; // PKT_DROP
+    }
+}
+
+__global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
+{
+    __shared__ uint32_t s_t[TAB_POS * 256];
+    __shared__ uint32_t s_win[CNET_THREADS * ROW_DW];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB_POS * 256; k += CNET_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += CNET_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CNET_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    uint32_t *row = s_win + tid * ROW_DW;
+    row[WIN_DW] = 0;
+    const uint64_t step = (uint64_t)gridDim.x * CNET_THREADS;
+    for (uint64_t i = (uint64_t)blockIdx.x * CNET_THREADS + tid; i < a.n; i += step) {
+        const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
+        const uint8_t *p = a.slab + base;
+        const uint64_t avail = base < a.slab_len ? a.slab_len - base : 0;
+        // stage the 64-byte header window (bounded) into this lane's LDS row
+        if (avail >= 64 && (base & 15u) == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint4 q = *(const uint4 *)(p + 16 * k);
+                row[4 * k + 0] = q.x;
+                row[4 * k + 1] = q.y;
+                row[4 * k + 2] = q.z;
+                row[4 * k + 3] = q.w;
+            }
+        } else {
+            for (int k = 0; k < WIN_DW; k++)
+                row[k] = gld32(p, avail, 4u * (uint32_t)k);
+        }
+        const Win w{row, p, avail};
+        Lens ln;
+        const uint32_t pt = get_ptype(w, ln);
+        const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
+        const uint32_t ip = ln.l2;
+        const bool l4ok = l4t == 0x100u || l4t == 0x200u;
+        uint32_t h = 0, nh = CNDP_NH_INVALID, edge;
+        if (l3 != 0u && !(l3 & 0x40u)) {
+            h = tz4(s_t, 0, w.ld32(ip + 12)) ^ tz4(s_t, 4, w.ld32(ip + 16));
+            if (l4ok)
+                h ^= tz4(s_t, 8, w.ld32(ip + ln.l3));
+        } else if (l3 & 0x40u) {
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++)
+                h ^= tz4(s_t, 4 * k, w.ld32(ip + 8 + 4 * k));
+            if (l4ok)
+                h ^= tz4(s_t, 32, w.ld32(ip + ln.l3));
+        }
+        const uint32_t pe = cnet_edge(pt);
+        if (pe == 3u) {
+            // ip4_input.c:121-140: total_length < buf_len && cksum == 0
+            const uint32_t x0 = w.ld32(ip);
+            const uint32_t hl = (x0 & 0xfu);
+            uint32_t sum = 0;
+            for (uint32_t k = 0; k < hl; k++) {
+                const uint32_t x = k == 0 ? x0 : w.ld32(ip + 4 * k);
+                sum += (x & 0xffffu) + (x >> 16);
+            }
+            sum = (sum >> 16) + (sum & 0xffffu);
+            sum = (sum >> 16) + (sum & 0xffffu);
+            const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
+            const uint32_t dip = ok ? w.be32(ip + 16) : 0u;
+            nh = lpm4(a.tbl24, a.tbl8, dip);
+            edge = nh >> 24;
+        } else if (pe == 4u) {
+            // ip6_input.c:115-135: payload_len < buf_len, else dip = ::
+            const bool ok = w.be16(ip + 4) < a.buf_len;
+            uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+            if (ok) {
+                d0 = w.ld32(ip + 24);
+                d1 = w.ld32(ip + 28);
+                d2 = w.ld32(ip + 32);
+                d3 = w.ld32(ip + 36);
+            }
+            // trie.h:126-134
+            uint32_t e = a.tbl24_6[((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu)];
+            uint32_t j = 3;
+            while ((e & 1u) && j < 16) {
+                const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
+                const uint32_t byte = (wd >> ((j & 3u) * 8)) & 0xffu;
+                e = a.tbl8_6[(e >> 1) * 256u + byte];
+                j++;
+            }
+            nh = e >> 1;
+            edge = nh >> 24;
+        } else {
+            edge = 0x80u | pe;
+        }
+        const uint32_t q = s_reta[h & a.reta_mask];
+        if (a.nh)
+            a.nh[i] = nh;
+        if (a.hash)
+            a.hash[i] = h;
+        if (a.queue)
+            a.queue[i] = (uint16_t)q;
+        if (a.edge)
+            a.edge[i] = (uint8_t)edge;
+        if (count)
+            atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CNET_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// bulk lookups (cne_fib_lookup_bulk / cne_fib6_lookup_bulk semantics)
+// ---------------------------------------------------------------------------
+template <typename E>
+__global__ __launch_bounds__(256) void k_lookup4(const E *__restrict__ t24, const E *__restrict__ t8,
+                                                 const uint32_t *__restrict__ ips,
+                                                 uint64_t *__restrict__ nh, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t ip = ips[i];
+    uint64_t e = (uint64_t)t24[ip >> 8];
+    if (e & 1u)
+        e = (uint64_t)t8[(e >> 1) * 256u + (ip & 0xffu)];
+    nh[i] = e >> 1;
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void k_lookup6(const E *__restrict__ t24, const E *__restrict__ t8,
+                                                 const uint8_t *__restrict__ ips,
+                                                 uint64_t *__restrict__ nh, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint8_t *ip = ips + (uint64_t)i * 16u;
+    uint64_t e = (uint64_t)t24[((uint32_t)ip[0] << 16) | ((uint32_t)ip[1] << 8) | ip[2]];
+    uint32_t j = 3;
+    while ((e & 1u) && j < 16)
+        e = (uint64_t)t8[(e >> 1) * 256u + ip[j++]];
+    nh[i] = e >> 1;
+}
+
+// ---------------------------------------------------------------------------
+// per-packet bin ids and the stable partition (per-edge streams)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bin_ids(uint32_t mode, const uint32_t *__restrict__ nh,
+                                                 const uint8_t *__restrict__ edge,
+                                                 const uint16_t *__restrict__ queue, uint32_t n,
+                                                 uint32_t nb, uint16_t *__restrict__ out)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    uint32_t b;
+    if (mode == CNDP_MODE_HASH)
+        b = bin_of<CNDP_MODE_HASH>(0, 0, queue[i], nb);
+    else if (mode == CNDP_MODE_L3FWD)
+        b = bin_of<CNDP_MODE_L3FWD>(nh[i], edge[i], 0, nb);
+    else
+        b = bin_of<CNDP_MODE_CNET>(nh[i], edge[i], 0, nb);
+    out[i] = (uint16_t)b;
+}
+
+#define PART_TILE 1024u
+#define PART_THREADS 256u
+
+// pass 1: per-tile histogram, stored bin-major: hist[bin * tiles + tile]
+__global__ __launch_bounds__(PART_THREADS) void k_part_hist(const uint16_t *__restrict__ bin_of,
+                                                            uint32_t n, uint32_t nbt,
+                                                            uint32_t tiles, uint32_t *hist)
+{
+    __shared__ uint32_t h[CNDP_BINS_MAX + 2];
+    for (uint32_t k = threadIdx.x; k < nbt; k += PART_THREADS)
+        h[k] = 0;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * PART_TILE;
+    for (uint32_t k = threadIdx.x; k < PART_TILE; k += PART_THREADS) {
+        const uint32_t i = t0 + k;
+        if (i < n)
+            atomicAdd(&h[bin_of[i]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nbt; k += PART_THREADS)
+        hist[(uint64_t)k * tiles + blockIdx.x] = h[k];
+}
+
+// pass 2: exclusive scan of hist (bin-major) -> tile offsets; bin_start
+__global__ __launch_bounds__(1024) void k_part_scan(uint32_t *hist, uint32_t total,
+                                                    uint32_t tiles, uint32_t nbt,
+                                                    uint32_t *bin_start)
+{
+    __shared__ uint32_t s_carry;
+    __shared__ uint32_t s_wave[16];
+    if (threadIdx.x == 0)
+        s_carry = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint32_t base = 0; base < total; base += 1024u) {
+        const uint32_t k = base + threadIdx.x;
+        const uint32_t v = k < total ? hist[k] : 0u;
+        // inclusive wave scan
+        uint32_t x = v;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d)
+                x += y;
+        }
+        if (lane == 63)
+            s_wave[wv] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int q = 0; q < 16; q++) {
+                const uint32_t t = s_wave[q];
+                s_wave[q] = acc;
+                acc += t;
+            }
+        }
+        __syncthreads();
+        const uint32_t excl = s_carry + s_wave[wv] + x - v;
+        if (k < total) {
+            hist[k] = excl;
+            if (k % tiles == 0)
+                bin_start[k / tiles] = excl;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023)
+            s_carry = excl + v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        bin_start[nbt] = s_carry;
+}
+
+// pass 3: stable scatter.  Within a tile, waves go in order; within a wave
+// the rank among same-bin lanes comes from ballots over the lane's peers.
+__global__ __launch_bounds__(PART_THREADS) void k_part_scatter(const uint16_t *__restrict__ bin_of,
+                                                               uint32_t n, uint32_t nbt,
+                                                               uint32_t tiles,
+                                                               const uint32_t *__restrict__ off,
+                                                               uint32_t *__restrict__ order)
+{
+    __shared__ uint32_t cur[CNDP_BINS_MAX + 2];
+    for (uint32_t k = threadIdx.x; k < nbt; k += PART_THREADS)
+        cur[k] = off[(uint64_t)k * tiles + blockIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t lt_mask = lane ? (~0ULL >> (64 - lane)) : 0ULL;
+    const uint32_t t0 = blockIdx.x * PART_TILE;
+    for (uint32_t chunk = 0; chunk < PART_TILE; chunk += PART_THREADS) {
+        // process the 4 waves of this chunk strictly in order
+        for (uint32_t turn = 0; turn < PART_THREADS / 64u; turn++) {
+            if (wv == turn) {
+                const uint32_t i = t0 + chunk + threadIdx.x;
+                const bool valid = i < n;
+                const uint32_t b = valid ? bin_of[i] : 0xFFFFFFFFu;
+                uint64_t todo = __ballot(valid);
+                uint32_t dst = 0;
+                while (todo) {
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+                    const uint32_t lb = __shfl(b, leader, 64);
+                    const uint64_t peers = __ballot(valid && b == lb);
+                    const uint32_t cnt = (uint32_t)__builtin_popcountll(peers);
+                    uint32_t basev = 0;
+                    if (lane == leader)
+                        basev = cur[lb];
+                    basev = __shfl(basev, leader, 64);
+                    if (b == lb && valid)
+                        dst = basev + (uint32_t)__builtin_popcountll(peers & lt_mask);
+                    if (lane == leader)
+                        cur[lb] = basev + cnt;
+                    todo &= ~peers;
+                }
+                if (valid)
+                    order[dst] = i;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct cndp_gpu_ctx {
+    int dev;
+    uint8_t key[CNDP_RSS_KEY_LEN];
+    uint32_t *d_ttab;     // 36 x 256
+    uint16_t *d_reta;
+    uint32_t reta_size;
+    struct cne_fib *fib4;
+    struct cne_fib6 *fib6;
+    uint32_t *d_part;     // partition scratch
+    size_t part_cap;
+    int num_cu;
+};
+
+static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
+    0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+    0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+    0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+
+// 32-bit key window starting at key bit s (MSB-first bit order)
+static uint32_t key_window(const uint8_t *key, uint32_t s)
+{
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < 5; k++) {
+        const uint32_t byte = s / 8 + k;
+        v = (v << 8) | (byte < CNDP_RSS_KEY_LEN ? key[byte] : 0u);
+    }
+    return (uint32_t)(v >> (8 - (s % 8)));
+}
+
+// T[b][v] = XOR of the windows of the set bits of byte v at stream byte b
+// (linearity of cne_softrss, cne_thash.h:150-163)
+static void build_ttab(const uint8_t *key, uint32_t *tab)
+{
+    for (uint32_t b = 0; b < TAB_POS; b++) {
+        uint32_t wbit[8];
+        for (uint32_t k = 0; k < 8; k++)
+            wbit[k] = key_window(key, 8 * b + k);
+        for (uint32_t v = 0; v < 256; v++) {
+            uint32_t h = 0;
+            for (uint32_t k = 0; k < 8; k++)
+                if (v & (0x80u >> k))
+                    h ^= wbit[k];
+            tab[b * 256 + v] = h;
+        }
+    }
+}
+
+static int set_device(int dev)
+{
+    HIP_TRY(hipSetDevice(dev));
+    return 0;
+}
+
+extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
+{
+    if (!out)
+        return -EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return -ENODEV;
+    if (device < 0)
+        HIP_TRY(hipGetDevice(&device));
+    if (device >= ndev)
+        return -ENODEV;
+    int r = set_device(device);
+    if (r)
+        return r;
+    cndp_gpu_ctx_t *c = (cndp_gpu_ctx_t *)calloc(1, sizeof(*c));
+    if (!c)
+        return -ENOMEM;
+    c->dev = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess)
+        c->num_cu = prop.multiProcessorCount;
+    if (c->num_cu <= 0)
+        c->num_cu = 256;
+    if (hipMalloc((void **)&c->d_ttab, TAB_POS * 256 * 4) != hipSuccess ||
+        hipMalloc((void **)&c->d_reta, CNDP_RETA_MAX * 2) != hipSuccess) {
+        cndp_gpu_fini(c);
+        return -ENOMEM;
+    }
+    r = cndp_gpu_set_rss(c, nullptr, 0, nullptr, 0, 16);
+    if (r) {
+        cndp_gpu_fini(c);
+        return r;
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
+{
+    if (!c)
+        return;
+    hipSetDevice(c->dev);
+    if (c->d_ttab)
+        hipFree(c->d_ttab);
+    if (c->d_reta)
+        hipFree(c->d_reta);
+    if (c->d_part)
+        hipFree(c->d_part);
+    free(c);
+}
+
+extern "C" int cndp_gpu_device(const cndp_gpu_ctx_t *c) { return c ? c->dev : -EINVAL; }
+
+extern "C" int cndp_gpu_set_rss(cndp_gpu_ctx_t *c, const uint8_t *key, uint32_t key_len,
+                                const uint16_t *reta, uint32_t reta_size, uint32_t nb_queues)
+{
+    if (!c)
+        return -EINVAL;
+    if (key && key_len != CNDP_RSS_KEY_LEN)
+        return -EINVAL;
+    uint16_t rt[CNDP_RETA_MAX];
+    if (reta) {
+        if (reta_size == 0 || reta_size > CNDP_RETA_MAX || (reta_size & (reta_size - 1)))
+            return -EINVAL;
+        memcpy(rt, reta, reta_size * 2);
+    } else {
+        if (nb_queues == 0)
+            return -EINVAL;
+        reta_size = 128;
+        for (uint32_t i = 0; i < reta_size; i++)
+            rt[i] = (uint16_t)(i % nb_queues);
+    }
+    memcpy(c->key, key ? key : ms_default_key, CNDP_RSS_KEY_LEN);
+    uint32_t *tab = (uint32_t *)malloc(TAB_POS * 256 * 4);
+    if (!tab)
+        return -ENOMEM;
+    build_ttab(c->key, tab);
+    int r = set_device(c->dev);
+    if (!r && (hipMemcpy(c->d_ttab, tab, TAB_POS * 256 * 4, hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(c->d_reta, rt, reta_size * 2, hipMemcpyHostToDevice) != hipSuccess))
+        r = -EIO;
+    free(tab);
+    if (!r)
+        c->reta_size = reta_size;
+    return r;
+}
+
+extern "C" int cndp_gpu_set_fib(cndp_gpu_ctx_t *c, struct cne_fib *f4, struct cne_fib6 *f6)
+{
+    if (!c)
+        return -EINVAL;
+    if (f4 && f4->t.nh_sz != 2)
+        return -ENOTSUP;
+    if (f6 && f6->t.nh_sz != 2)
+        return -ENOTSUP;
+    c->fib4 = f4;
+    c->fib6 = f6;
+    return 0;
+}
+
+// ---- table mirror -----------------------------------------------------------
+extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
+{
+    if (!t || t->dev_id < 0)
+        return;
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(t->dev_id);
+    if (t->dev_tbl24)
+        hipFree(t->dev_tbl24);
+    if (t->dev_tbl8)
+        hipFree(t->dev_tbl8);
+    hipSetDevice(cur);
+    t->dev_tbl24 = t->dev_tbl8 = nullptr;
+    t->dev_id = -1;
+    t->dev_groups = 0;
+}
+
+extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
+{
+    if (!t || !t->tbl24)
+        return -EINVAL;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return -ENODEV;
+    const size_t esz = (size_t)1 << t->nh_sz;
+    const uint32_t groups = t->cap_groups + 1;
+    if (t->dev_id >= 0 && t->dev_id != dev)
+        return -EXDEV; // a FIB mirror lives on one device
+    hipStream_t s = (hipStream_t)stream;
+    if (t->dev_id < 0) {
+        HIP_TRY(hipMalloc(&t->dev_tbl24, (size_t)CNDP_TBL24_ENT * esz));
+        HIP_TRY(hipMalloc(&t->dev_tbl8, (size_t)groups * CNDP_TBL8_GRP * esz));
+        t->dev_id = dev;
+        t->dev_groups = groups;
+        t->d24_lo = 0;
+        t->d24_hi = CNDP_TBL24_ENT;
+        t->d8_lo = 0;
+        t->d8_hi = (uint64_t)groups * CNDP_TBL8_GRP;
+    } else if (t->dev_groups != groups) { // pool grew (DUMMY FIBs)
+        void *n8 = nullptr;
+        HIP_TRY(hipMalloc(&n8, (size_t)groups * CNDP_TBL8_GRP * esz));
+        HIP_TRY(hipFree(t->dev_tbl8));
+        t->dev_tbl8 = n8;
+        t->dev_groups = groups;
+        t->d8_lo = 0;
+        t->d8_hi = (uint64_t)groups * CNDP_TBL8_GRP;
+    }
+    if (t->d24_hi > t->d24_lo) {
+        HIP_TRY(hipMemcpyAsync((uint8_t *)t->dev_tbl24 + t->d24_lo * esz, t->tbl24 + t->d24_lo * esz,
+                               (t->d24_hi - t->d24_lo) * esz, hipMemcpyHostToDevice, s));
+    }
+    if (t->d8_hi > t->d8_lo) {
+        HIP_TRY(hipMemcpyAsync((uint8_t *)t->dev_tbl8 + t->d8_lo * esz, t->tbl8 + t->d8_lo * esz,
+                               (t->d8_hi - t->d8_lo) * esz, hipMemcpyHostToDevice, s));
+    }
+    // the host image may change right after we return: finish the copies
+    if (t->d24_hi > t->d24_lo || t->d8_hi > t->d8_lo)
+        HIP_TRY(hipStreamSynchronize(s));
+    t->d24_lo = t->d8_lo = ~0ULL;
+    t->d24_hi = t->d8_hi = 0;
+    return 0;
+}
+
+static inline uint32_t blocks_for(uint64_t n, uint32_t threads)
+{
+    return (uint32_t)((n + threads - 1) / threads);
+}
+
+extern "C" int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh,
+                                    uint32_t n, void *stream)
+{
+    int r = cndp_tbl_dev_sync(t, stream);
+    if (r)
+        return r;
+    if (n == 0)
+        return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t g = blocks_for(n, 256);
+    switch (t->nh_sz) {
+    case 0:
+        hipLaunchKernelGGL(k_lookup4<uint8_t>, dim3(g), dim3(256), 0, s, (const uint8_t *)t->dev_tbl24,
+                           (const uint8_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_lookup4<uint16_t>, dim3(g), dim3(256), 0, s,
+                           (const uint16_t *)t->dev_tbl24, (const uint16_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_lookup4<uint32_t>, dim3(g), dim3(256), 0, s,
+                           (const uint32_t *)t->dev_tbl24, (const uint32_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    default:
+        hipLaunchKernelGGL(k_lookup4<uint64_t>, dim3(g), dim3(256), 0, s,
+                           (const uint64_t *)t->dev_tbl24, (const uint64_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n,
+                                    void *stream)
+{
+    int r = cndp_tbl_dev_sync(t, stream);
+    if (r)
+        return r;
+    if (n == 0)
+        return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t g = blocks_for(n, 256);
+    switch (t->nh_sz) {
+    case 1:
+        hipLaunchKernelGGL(k_lookup6<uint16_t>, dim3(g), dim3(256), 0, s,
+                           (const uint16_t *)t->dev_tbl24, (const uint16_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_lookup6<uint32_t>, dim3(g), dim3(256), 0, s,
+                           (const uint32_t *)t->dev_tbl24, (const uint32_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    default:
+        hipLaunchKernelGGL(k_lookup6<uint64_t>, dim3(g), dim3(256), 0, s,
+                           (const uint64_t *)t->dev_tbl24, (const uint64_t *)t->dev_tbl8, ips, nh, n);
+        break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+// host-array lookups: stage through device scratch on the current device
+static int lookup_host_common(struct cndp_tbl *t, const void *ips, size_t ip_bytes, uint64_t *nh,
+                              uint32_t n, int v6)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return -ENODEV;
+    void *d_ip = nullptr;
+    uint64_t *d_nh = nullptr;
+    HIP_TRY(hipMalloc(&d_ip, ip_bytes));
+    if (hipMalloc((void **)&d_nh, (size_t)n * 8) != hipSuccess) {
+        hipFree(d_ip);
+        return -ENOMEM;
+    }
+    int r = 0;
+    if (hipMemcpy(d_ip, ips, ip_bytes, hipMemcpyHostToDevice) != hipSuccess)
+        r = -EIO;
+    if (!r)
+        r = v6 ? cndp_tbl_lookup6_dev(t, (const uint8_t *)d_ip, d_nh, n, nullptr)
+               : cndp_tbl_lookup4_dev(t, (const uint32_t *)d_ip, d_nh, n, nullptr);
+    if (!r && hipMemcpy(nh, d_nh, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        r = -EIO;
+    hipFree(d_ip);
+    hipFree(d_nh);
+    return r;
+}
+
+extern "C" int cndp_tbl_lookup4_host(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n)
+{
+    return lookup_host_common(t, ips, (size_t)n * 4, nh, n, 0);
+}
+
+extern "C" int cndp_tbl_lookup6_host(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n)
+{
+    return lookup_host_common(t, ips, (size_t)n * 16, nh, n, 1);
+}
+
+// ---- classify ---------------------------------------------------------------
+static int validate_batch(const cndp_gpu_ctx_t *c, const struct cndp_batch *b)
+{
+    if (!c || !b)
+        return -EINVAL;
+    if (b->mode != CNDP_MODE_L3FWD && b->mode != CNDP_MODE_CNET && b->mode != CNDP_MODE_HASH)
+        return -EINVAL;
+    if (b->n && !b->slab)
+        return -EINVAL;
+    if (b->bins && b->n_bins > CNDP_BINS_MAX)
+        return -EINVAL;
+    if (b->mode != CNDP_MODE_HASH && !c->fib4)
+        return -EINVAL;
+    if (b->mode == CNDP_MODE_CNET && !c->fib6)
+        return -EINVAL;
+    return 0;
+}
+
+extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream)
+{
+    int r = validate_batch(c, b);
+    if (r)
+        return r;
+    r = set_device(c->dev);
+    if (r)
+        return r;
+    if (b->mode != CNDP_MODE_HASH && (r = cndp_tbl_dev_sync(&c->fib4->t, stream)))
+        return r;
+    if (b->mode == CNDP_MODE_CNET && (r = cndp_tbl_dev_sync(&c->fib6->t, stream)))
+        return r;
+    if (b->n == 0)
+        return 0;
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    a.slab = (const uint8_t *)b->slab;
+    a.slab_len = b->slab_len;
+    a.stride = b->stride;
+    a.offsets = b->offsets;
+    a.data_off = b->data_off;
+    a.n = b->n;
+    a.buf_len = b->buf_len;
+    a.reta_mask = c->reta_size - 1;
+    if (c->fib4) {
+        a.tbl24 = (const uint32_t *)c->fib4->t.dev_tbl24;
+        a.tbl8 = (const uint32_t *)c->fib4->t.dev_tbl8;
+    }
+    if (c->fib6) {
+        a.tbl24_6 = (const uint32_t *)c->fib6->t.dev_tbl24;
+        a.tbl8_6 = (const uint32_t *)c->fib6->t.dev_tbl8;
+    }
+    a.ttab = c->d_ttab;
+    a.reta = c->d_reta;
+    a.nh = b->nh;
+    a.hash = b->hash;
+    a.queue = b->queue;
+    a.edge = b->edge;
+    a.bins = (unsigned long long *)b->bins;
+    a.n_bins = b->n_bins;
+    hipStream_t s = (hipStream_t)stream;
+    if (b->mode == CNDP_MODE_CNET) {
+        uint32_t g = blocks_for(b->n, CNET_THREADS);
+        const uint32_t cap = (uint32_t)c->num_cu * 2u;
+        if (g > cap)
+            g = cap;
+        hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
+    } else {
+        uint32_t g = blocks_for(b->n, FAST_THREADS);
+        const uint32_t cap = (uint32_t)c->num_cu * 8u;
+        if (g > cap)
+            g = cap;
+        if (b->mode == CNDP_MODE_L3FWD)
+            hipLaunchKernelGGL(k_classify_fast<CNDP_MODE_L3FWD>, dim3(g), dim3(FAST_THREADS), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_classify_fast<CNDP_MODE_HASH>, dim3(g), dim3(FAST_THREADS), 0, s, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch *hb)
+{
+    int r = validate_batch(c, hb);
+    if (r)
+        return r;
+    if ((r = set_device(c->dev)))
+        return r;
+    struct cndp_batch db = *hb;
+    const uint64_t n = hb->n;
+    void *d_slab = nullptr, *d_off = nullptr, *d_out = nullptr;
+    const size_t o_nh = 0, o_hash = o_nh + n * 4, o_q = o_hash + n * 4, o_e = o_q + ((n * 2 + 15) & ~15ull),
+                 o_b = o_e + ((n + 15) & ~15ull), out_bytes = o_b + ((uint64_t)hb->n_bins + 2) * 8;
+    hipStream_t s = nullptr;
+    r = -EIO;
+    if (hipStreamCreate(&s) != hipSuccess)
+        return -EIO;
+    if (hipMalloc(&d_slab, hb->slab_len ? hb->slab_len : 1) != hipSuccess ||
+        hipMalloc(&d_out, out_bytes) != hipSuccess)
+        goto out;
+    if (hb->offsets && hipMalloc(&d_off, n * 8) != hipSuccess)
+        goto out;
+    if (hipMemcpyAsync(d_slab, hb->slab, hb->slab_len, hipMemcpyHostToDevice, s) != hipSuccess)
+        goto out;
+    if (hb->offsets && hipMemcpyAsync(d_off, hb->offsets, n * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+        goto out;
+    if (hb->bins && hipMemcpyAsync((uint8_t *)d_out + o_b, hb->bins, ((uint64_t)hb->n_bins + 2) * 8,
+                                   hipMemcpyHostToDevice, s) != hipSuccess)
+        goto out;
+    db.slab = d_slab;
+    db.offsets = (const uint64_t *)d_off;
+    db.nh = hb->nh ? (uint32_t *)((uint8_t *)d_out + o_nh) : nullptr;
+    db.hash = hb->hash ? (uint32_t *)((uint8_t *)d_out + o_hash) : nullptr;
+    db.queue = hb->queue ? (uint16_t *)((uint8_t *)d_out + o_q) : nullptr;
+    db.edge = hb->edge ? (uint8_t *)d_out + o_e : nullptr;
+    db.bins = hb->bins ? (uint64_t *)((uint8_t *)d_out + o_b) : nullptr;
+    if ((r = cndp_gpu_classify(c, &db, s)))
+        goto out;
+    r = -EIO;
+    if (hb->nh && hipMemcpyAsync(hb->nh, db.nh, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        goto out;
+    if (hb->hash && hipMemcpyAsync(hb->hash, db.hash, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        goto out;
+    if (hb->queue && hipMemcpyAsync(hb->queue, db.queue, n * 2, hipMemcpyDeviceToHost, s) != hipSuccess)
+        goto out;
+    if (hb->edge && hipMemcpyAsync(hb->edge, db.edge, n, hipMemcpyDeviceToHost, s) != hipSuccess)
+        goto out;
+    if (hb->bins && hipMemcpyAsync(hb->bins, db.bins, ((uint64_t)hb->n_bins + 2) * 8,
+                                   hipMemcpyDeviceToHost, s) != hipSuccess)
+        goto out;
+    if (hipStreamSynchronize(s) != hipSuccess)
+        goto out;
+    r = 0;
+out:
+    if (s)
+        hipStreamSynchronize(s);
+    if (d_slab)
+        hipFree(d_slab);
+    if (d_off)
+        hipFree(d_off);
+    if (d_out)
+        hipFree(d_out);
+    if (s)
+        hipStreamDestroy(s);
+    return r;
+}
+
+extern "C" int cndp_gpu_bin_ids(cndp_gpu_ctx_t *c, uint32_t mode, const uint32_t *nh,
+                                const uint8_t *edge, const uint16_t *queue, uint32_t n,
+                                uint32_t n_bins, uint16_t *bin_of_out, void *stream)
+{
+    if (!c || !bin_of_out || n_bins > CNDP_BINS_MAX)
+        return -EINVAL;
+    if (mode == CNDP_MODE_HASH ? !queue : (!nh || !edge))
+        return -EINVAL;
+    if (mode > CNDP_MODE_HASH)
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    if (n == 0)
+        return 0;
+    hipLaunchKernelGGL(k_bin_ids, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, mode,
+                       nh, edge, queue, n, n_bins, bin_of_out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of, uint32_t n,
+                                      uint32_t n_bins, uint32_t *bin_start, uint32_t *order,
+                                      void *stream)
+{
+    if (!c || !bin_start || n_bins > CNDP_BINS_MAX || (n && (!bin_of || !order)))
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    const uint32_t nbt = n_bins + 2;
+    const uint32_t tiles = n ? blocks_for(n, PART_TILE) : 1;
+    const size_t need = (size_t)nbt * tiles;
+    if (need > c->part_cap) {
+        if (c->d_part)
+            HIP_TRY(hipFree(c->d_part));
+        c->d_part = nullptr;
+        c->part_cap = 0;
+        HIP_TRY(hipMalloc((void **)&c->d_part, need * 4));
+        c->part_cap = need;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(bin_start, 0, (size_t)(nbt + 1) * 4, s));
+        return 0;
+    }
+    hipLaunchKernelGGL(k_part_hist, dim3(tiles), dim3(PART_THREADS), 0, s, bin_of, n, nbt, tiles,
+                       c->d_part);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, c->d_part, (uint32_t)need, tiles, nbt,
+                       bin_start);
+    hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(PART_THREADS), 0, s, bin_of, n, nbt, tiles,
+                       c->d_part, order);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" const char *cndp_gpu_version(void) { return CNDP_VERSION; }

@@ -1,0 +1,79 @@
+/*
+ * fib_internal.h -- table images shared by the host control plane (fib.c)
+ * and the device runtime (cndp_gpu.hip).
+ *
+ * One struct cndp_tbl holds a DIR-24-8 (IPv4) or trie (IPv6) image in the
+ * reference's entry encoding (dir24_8.h:27-46 / trie.h:26-40):
+ *   tbl24[1<<24]        entry = nh << 1, or (group << 1) | 1 when extended
+ *   tbl8[groups*256]    DIR-24-8: (nh << 1) | 1 ; trie: like tbl24 (chains)
+ * Entry width is 1 << nh_sz bytes.  The device mirror is a byte-for-byte copy
+ * in HBM, refreshed from the dirty entry ranges on sync.
+ */
+#ifndef CNDP_FIB_INTERNAL_H
+#define CNDP_FIB_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rib.h"
+#include "../../include/cndp_fib.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CNDP_TBL24_ENT (1u << 24)
+#define CNDP_TBL8_GRP 256u
+
+struct cndp_tbl {
+    uint32_t nh_sz;     /* log2(entry bytes) */
+    uint32_t is_trie;   /* 0 = DIR-24-8, 1 = IPv6 trie */
+    uint8_t *tbl24;
+    uint8_t *tbl8;      /* (cap_groups + 1) groups */
+    uint64_t *used;     /* bitmap over cap_groups */
+    uint32_t num_tbl8;  /* allocatable groups (0 = unlimited, growable) */
+    uint32_t cap_groups;
+    uint32_t cur_tbl8s;
+    /* dirty entry ranges [lo, hi) pending upload */
+    uint64_t d24_lo, d24_hi, d8_lo, d8_hi;
+    /* device mirror */
+    int dev_id;
+    void *dev_tbl24;
+    void *dev_tbl8;
+    uint32_t dev_groups; /* groups allocated on the device */
+};
+
+struct cne_fib {
+    char name[64];
+    enum cne_fib_type type;
+    uint64_t def_nh;
+    int lookup_type;
+    uint32_t rsvd_tbl8s;
+    struct cndp_rib rib;
+    struct cndp_tbl t;
+};
+
+struct cne_fib6 {
+    char name[64];
+    enum cne_fib_type type;
+    uint64_t def_nh;
+    int lookup_type;
+    uint32_t rsvd_tbl8s;
+    struct cndp_rib rib;
+    struct cndp_tbl t;
+};
+
+/* implemented in cndp_gpu.hip (device side of the mirror) */
+int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream);
+void cndp_tbl_dev_free(struct cndp_tbl *t);
+int cndp_tbl_lookup4_host(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n);
+int cndp_tbl_lookup6_host(struct cndp_tbl *t, const uint8_t *ips16, uint64_t *nh, uint32_t n);
+int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n,
+                         void *stream);
+int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips16, uint64_t *nh, uint32_t n,
+                         void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

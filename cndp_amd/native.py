@@ -1,0 +1,150 @@
+"""ctypes binding of libcndp_gpu.so (the C-ABI declared in include/cndp_fib.h
+and include/cndp_gpu.h).
+
+The library is built in-tree (cndp_amd/lib/libcndp_gpu.so, see build.py).
+There is no fallback: if the shared object is missing, importing the
+product API raises, so a test or bench can never silently run a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, Union, c_char_p, c_int, c_uint8, c_uint16,
+                    c_uint32, c_uint64, c_void_p)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcndp_gpu.so")
+
+# cne_fib.h:34-38, :53-58, :60, :63-73 (+ CNE_FIB_LOOKUP_GPU)
+CNE_FIB_DUMMY, CNE_FIB_DIR24_8, CNE_FIB_TRIE = 0, 1, 2
+CNE_FIB_DIR24_8_1B, CNE_FIB_DIR24_8_2B, CNE_FIB_DIR24_8_4B, CNE_FIB_DIR24_8_8B = 0, 1, 2, 3
+CNE_FIB_TRIE_2B, CNE_FIB_TRIE_4B, CNE_FIB_TRIE_8B = 1, 2, 3
+(CNE_FIB_LOOKUP_DEFAULT, CNE_FIB_LOOKUP_DIR24_8_SCALAR_MACRO, CNE_FIB_LOOKUP_DIR24_8_SCALAR_INLINE,
+ CNE_FIB_LOOKUP_DIR24_8_SCALAR_UNI, CNE_FIB_LOOKUP_DIR24_8_VECTOR_AVX512, CNE_FIB_LOOKUP_TRIE_SCALAR,
+ CNE_FIB_LOOKUP_TRIE_VECTOR_AVX512, CNE_FIB_LOOKUP_GPU) = range(8)
+CNE_FIB_MAXDEPTH = 32
+CNE_FIB6_MAXDEPTH = 128
+
+# cndp_gpu.h
+CNDP_MODE_L3FWD, CNDP_MODE_CNET, CNDP_MODE_HASH = 0, 1, 2
+CNDP_NH_INVALID = 0xFFFFFFFF
+CNDP_EDGE_CLS_DROP = 0xFF
+CNDP_RSS_KEY_LEN = 40
+CNDP_RETA_MAX = 512
+CNDP_BINS_MAX = 1024
+
+# l3fwd edges (node_ip4_api.h:28-34) and cnet edges (ip4_input_priv.h:26-31)
+IP4_LOOKUP_NEXT_REWRITE, IP4_LOOKUP_NEXT_PKT_DROP = 0, 1
+IP4_INPUT_NEXT_PKT_DROP, IP4_INPUT_NEXT_FORWARD, IP4_INPUT_NEXT_PROTO = 0, 1, 2
+
+MS_RSS_KEY = bytes.fromhex(
+    "6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
+
+
+class _Dir24(Structure):
+    _fields_ = [("nh_sz", c_int), ("num_tbl8", c_uint32)]
+
+
+class _ConfU(Union):
+    _fields_ = [("dir24_8", _Dir24), ("trie", _Dir24)]
+
+
+class FibConf(Structure):
+    """struct cne_fib_conf (cne_fib.h:76-91)."""
+    _anonymous_ = ("u",)
+    _fields_ = [("type", c_int), ("default_nh", c_uint64), ("max_routes", c_int), ("u", _ConfU)]
+
+
+class FibImage(Structure):
+    _fields_ = [("nh_sz", c_uint32), ("tbl8_groups", c_uint32), ("tbl24", c_void_p),
+                ("tbl8", c_void_p), ("def_nh", c_uint64)]
+
+
+class Batch(Structure):
+    """struct cndp_batch (cndp_gpu.h)."""
+    _fields_ = [("mode", c_uint32), ("n", c_uint32), ("slab", c_void_p), ("slab_len", c_uint64),
+                ("stride", c_uint64), ("offsets", c_void_p), ("data_off", c_uint32),
+                ("buf_len", c_uint32), ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p),
+                ("edge", c_void_p), ("bins", c_void_p), ("n_bins", c_uint32)]
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the native library; raise if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        # cndp_fib.h
+        "cne_fib_create": (c_void_p, [c_char_p, POINTER(FibConf)]),
+        "cne_fib_free": (None, [c_void_p]),
+        "cne_fib_add": (c_int, [c_void_p, c_uint32, c_uint8, c_uint64]),
+        "cne_fib_delete": (c_int, [c_void_p, c_uint32, c_uint8]),
+        "cne_fib_lookup_bulk": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+        "cne_fib_get_dp": (c_void_p, [c_void_p]),
+        "cne_fib_get_rib": (c_void_p, [c_void_p]),
+        "cne_fib_select_lookup": (c_int, [c_void_p, c_int]),
+        "cne_fib6_create": (c_void_p, [c_char_p, POINTER(FibConf)]),
+        "cne_fib6_free": (None, [c_void_p]),
+        "cne_fib6_add": (c_int, [c_void_p, c_void_p, c_uint8, c_uint64]),
+        "cne_fib6_delete": (c_int, [c_void_p, c_void_p, c_uint8]),
+        "cne_fib6_lookup_bulk": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+        "cne_fib6_get_dp": (c_void_p, [c_void_p]),
+        "cne_fib6_select_lookup": (c_int, [c_void_p, c_int]),
+        "cndp_fib_image": (c_int, [c_void_p, POINTER(FibImage)]),
+        "cndp_fib6_image": (c_int, [c_void_p, POINTER(FibImage)]),
+        "cndp_fib_sync": (c_int, [c_void_p, c_void_p]),
+        "cndp_fib6_sync": (c_int, [c_void_p, c_void_p]),
+        "cndp_fib_lookup_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+        "cndp_fib6_lookup_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+        "cndp_fib_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+        "cndp_fib6_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+        # cndp_gpu.h
+        "cndp_gpu_init": (c_int, [c_int, POINTER(c_void_p)]),
+        "cndp_gpu_fini": (None, [c_void_p]),
+        "cndp_gpu_device": (c_int, [c_void_p]),
+        "cndp_gpu_set_rss": (c_int, [c_void_p, c_char_p, c_uint32, c_void_p, c_uint32, c_uint32]),
+        "cndp_gpu_set_fib": (c_int, [c_void_p, c_void_p, c_void_p]),
+        "cndp_gpu_classify": (c_int, [c_void_p, POINTER(Batch), c_void_p]),
+        "cndp_gpu_classify_host": (c_int, [c_void_p, POINTER(Batch)]),
+        "cndp_gpu_bin_partition": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p,
+                                           c_void_p, c_void_p]),
+        "cndp_gpu_bin_ids": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32,
+                                     c_uint32, c_void_p, c_void_p]),
+        "cndp_gpu_version": (c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names the C-ABI headers declare (checked against the .so by tests)."""
+    import re
+    names = []
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    for h in ("cndp_fib.h", "cndp_gpu.h"):
+        with open(os.path.join(inc, h)) as f:
+            txt = f.read()
+        names += re.findall(r"^[A-Za-z_][\w \*]*?\b((?:cne|cndp)_\w+)\s*\(", txt, re.M)
+    return sorted(set(n for n in names if not n.endswith("_fn_t")))
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise OSError(-rc, f"{what} failed: {os.strerror(-rc)}")
+    return rc

@@ -1,0 +1,155 @@
+/*
+ * cndp_fib.h -- drop-in FIB API of libcndp_gpu.so (IPv4 DIR-24-8 + IPv6 trie).
+ *
+ * Each entry point keeps the exact name, signature, argument meaning and
+ * error behaviour of the reference call it replaces, so code written against
+ * CNDP's lib/usr/clib/fib/cne_fib.h and cne_fib6.h builds and links against
+ * this library unchanged.  The control plane (RIB + table build) runs on the
+ * host; every lookup runs on the MI355X (the tables are mirrored to HBM and
+ * kept in sync incrementally).  There is no CPU lookup path: without a usable
+ * GPU, cne_fib_lookup_bulk / cne_fib6_lookup_bulk return -ENODEV.
+ *
+ *   reference (CNDP v25.08.0)                    this library
+ *   cne_fib.h:103   cne_fib_create               same
+ *   cne_fib.h:113   cne_fib_free                 same
+ *   cne_fib.h:129   cne_fib_add                  same
+ *   cne_fib.h:143   cne_fib_delete               same
+ *   cne_fib.h:162   cne_fib_lookup_bulk          same, GPU-backed (host arrays)
+ *   cne_fib.h:173   cne_fib_get_dp               same (host table image)
+ *   cne_fib.h:183   cne_fib_get_rib              returns the build's RIB
+ *   cne_fib.h:197   cne_fib_select_lookup        same (+ CNE_FIB_LOOKUP_GPU)
+ *   cne_fib6.h:41-138  cne_fib6_*                same set for IPv6
+ * Extensions (device-resident batches, no reference counterpart):
+ *   cndp_fib_lookup_dev / cndp_fib6_lookup_dev, cndp_fib_sync / cndp_fib6_sync.
+ */
+#ifndef CNDP_FIB_H
+#define CNDP_FIB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CNE_FIB_MAXDEPTH 32   /* cne_fib.h:31 */
+#define CNE_FIB6_MAXDEPTH 128 /* private_fib6.h:28 */
+#define IPV6_ADDR_LEN 16
+
+struct cne_fib;
+struct cne_fib6;
+struct cne_rib;
+
+/* cne_fib.h:34-38 */
+enum cne_fib_type {
+    CNE_FIB_DUMMY,
+    CNE_FIB_DIR24_8,
+    CNE_FIB_TRIE
+};
+
+/* cne_fib.h:41-45 */
+typedef int (*cne_fib_modify_fn_t)(struct cne_fib *fib, uint32_t ip, uint8_t depth,
+                                   uint64_t next_hop, int op);
+typedef void (*cne_fib_lookup_fn_t)(void *fib, const uint32_t *ips, uint64_t *next_hops,
+                                    const unsigned int n);
+
+/* cne_fib.h:47-50 */
+enum cne_fib_op {
+    CNE_FIB_ADD,
+    CNE_FIB_DEL,
+};
+
+/* cne_fib.h:53-58: entry width is (1 << nh_sz) bytes */
+enum cne_fib_dir24_8_nh_sz {
+    CNE_FIB_DIR24_8_1B,
+    CNE_FIB_DIR24_8_2B,
+    CNE_FIB_DIR24_8_4B,
+    CNE_FIB_DIR24_8_8B,
+};
+
+/* cne_fib.h:60 */
+enum cne_fib_trie_nh_sz { CNE_FIB_TRIE_2B = 1, CNE_FIB_TRIE_4B, CNE_FIB_TRIE_8B };
+
+/* cne_fib.h:63-73, plus CNE_FIB_LOOKUP_GPU appended (every DIR-24-8 / trie
+ * selector resolves to the GPU lookup of the same table) */
+enum cne_fib_lookup_type {
+    CNE_FIB_LOOKUP_DEFAULT,
+    CNE_FIB_LOOKUP_DIR24_8_SCALAR_MACRO,
+    CNE_FIB_LOOKUP_DIR24_8_SCALAR_INLINE,
+    CNE_FIB_LOOKUP_DIR24_8_SCALAR_UNI,
+    CNE_FIB_LOOKUP_DIR24_8_VECTOR_AVX512,
+    CNE_FIB_LOOKUP_TRIE_SCALAR,
+    CNE_FIB_LOOKUP_TRIE_VECTOR_AVX512,
+    CNE_FIB_LOOKUP_GPU
+};
+
+/* cne_fib.h:76-91 (same layout) */
+struct cne_fib_conf {
+    enum cne_fib_type type;
+    uint64_t default_nh;
+    int max_routes;
+    union {
+        struct {
+            enum cne_fib_dir24_8_nh_sz nh_sz;
+            uint32_t num_tbl8;
+        } dir24_8;
+        struct {
+            enum cne_fib_trie_nh_sz nh_sz;
+            uint32_t num_tbl8;
+        } trie;
+    };
+};
+
+/* ---- IPv4 (lib/usr/clib/fib/cne_fib.h) ---------------------------------- */
+struct cne_fib *cne_fib_create(const char *name, struct cne_fib_conf *conf);
+void cne_fib_free(struct cne_fib *fib);
+int cne_fib_add(struct cne_fib *fib, uint32_t ip, uint8_t depth, uint64_t next_hop);
+int cne_fib_delete(struct cne_fib *fib, uint32_t ip, uint8_t depth);
+int cne_fib_lookup_bulk(struct cne_fib *fib, uint32_t *ips, uint64_t *next_hops, int n);
+void *cne_fib_get_dp(struct cne_fib *fib);
+struct cne_rib *cne_fib_get_rib(struct cne_fib *fib);
+int cne_fib_select_lookup(struct cne_fib *fib, enum cne_fib_lookup_type type);
+
+/* ---- IPv6 (lib/usr/clib/fib/cne_fib6.h) --------------------------------- */
+struct cne_fib6 *cne_fib6_create(const char *name, struct cne_fib_conf *conf);
+void cne_fib6_free(struct cne_fib6 *fib);
+int cne_fib6_add(struct cne_fib6 *fib, const uint8_t ip[IPV6_ADDR_LEN], uint8_t depth,
+                 uint64_t next_hop);
+int cne_fib6_delete(struct cne_fib6 *fib, const uint8_t ip[IPV6_ADDR_LEN], uint8_t depth);
+int cne_fib6_lookup_bulk(struct cne_fib6 *fib, uint8_t ips[][IPV6_ADDR_LEN], uint64_t *next_hops,
+                         int n);
+void *cne_fib6_get_dp(struct cne_fib6 *fib);
+int cne_fib6_select_lookup(struct cne_fib6 *fib, enum cne_fib_lookup_type type);
+
+/* ---- build extensions ---------------------------------------------------
+ * Host table image as mirrored to HBM (entry width 1 << nh_sz bytes).
+ * tbl24: 1<<24 entries; tbl8: (tbl8_groups) * 256 entries. */
+struct cndp_fib_image {
+    uint32_t nh_sz;
+    uint32_t tbl8_groups;
+    const void *tbl24;
+    const void *tbl8;
+    uint64_t def_nh;
+};
+int cndp_fib_image(struct cne_fib *fib, struct cndp_fib_image *out);
+int cndp_fib6_image(struct cne_fib6 *fib, struct cndp_fib_image *out);
+
+/* Upload pending table changes to the current HIP device (stream may be
+ * NULL for the null stream).  Lookups and classify call this themselves. */
+int cndp_fib_sync(struct cne_fib *fib, void *stream);
+int cndp_fib6_sync(struct cne_fib6 *fib, void *stream);
+
+/* Device-resident bulk lookups: ips / next_hops are device pointers;
+ * asynchronous on `stream`. */
+int cndp_fib_lookup_dev(struct cne_fib *fib, const uint32_t *ips, uint64_t *next_hops, uint32_t n,
+                        void *stream);
+int cndp_fib6_lookup_dev(struct cne_fib6 *fib, const uint8_t *ips16, uint64_t *next_hops,
+                         uint32_t n, void *stream);
+
+/* counters: tbl8 groups in use / reserved (cne_fib internal state) */
+int cndp_fib_stats(struct cne_fib *fib, uint32_t *routes, uint32_t *tbl8_used, uint32_t *rsvd);
+int cndp_fib6_stats(struct cne_fib6 *fib, uint32_t *routes, uint32_t *tbl8_used, uint32_t *rsvd);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,121 @@
+/*
+ * cndp_gpu.h -- batch parse + flow-hash + LPM classify on MI355X (libcndp_gpu.so).
+ *
+ * This is the data-plane half of the drop-in boundary.  It replaces, for a
+ * batch of many bursts at once, the per-burst arithmetic of these reference
+ * graph nodes (CNDP v25.08.0):
+ *
+ *   mode CNDP_MODE_L3FWD  (examples/l3fwd-graph chain)
+ *     pktdev_rx soft parse   lib/usr/clib/nodes/pktdev_rx.c:24-34,37-103
+ *     pkt_cls  classify      lib/usr/clib/nodes/pkt_cls.c:19-31,34-182
+ *     ip4_lookup             lib/usr/clib/nodes/ip4_lookup.c:48-256
+ *       -> cne_fib_lookup_bulk (DIR-24-8 4B) lib/usr/clib/fib/dir24_8.h:118-148
+ *   mode CNDP_MODE_CNET   (examples/cnet-graph chain)
+ *     eth_rx  (cne_get_ptype) lib/cnet/eth/eth_rx.c:35-63,
+ *                             lib/core/pktmbuf/pktmbuf_ptype.c:472-744
+ *     ptype                   lib/cnet/ptype/ptype.c:32-46,48-210
+ *     ip4_input (len+cksum)   lib/cnet/ipv4/ip4_input.c:50-260
+ *     ip6_input               lib/cnet/ipv6/ip6_input.c:52-260
+ *       -> cne_fib6_lookup_bulk (trie 4B) lib/usr/clib/fib/trie.h:119-138
+ *   mode CNDP_MODE_HASH   parse + Toeplitz + RSS queue only (config 2)
+ *   flow hash in every mode: cne_softrss (lib/core/hash/cne_thash.h:150-163)
+ *   over the NIC-style 5-tuple (cne_ipv4_tuple / cne_ipv6_tuple, :68-97).
+ *
+ * Packet i lives at slab + (offsets ? offsets[i] : i * stride) + data_off,
+ * i.e. a frame slab indexed like an AF_XDP UMEM (2 KiB frames, data at
+ * +256) or a packed slab (64-B slots).  Bytes at or past slab + slab_len
+ * read as zero.  All batch pointers are DEVICE pointers (hipMalloc / torch);
+ * work is enqueued on `stream` (a hipStream_t, NULL = null stream) and the
+ * call returns without waiting.  Errors are negative errno values.
+ *
+ * Per-packet outputs (SoA, any may be NULL except as noted):
+ *   nh[i]    u32 FIB value (l3fwd: edge<<16 | nh id; cnet: edge<<24 | idx),
+ *            CNDP_NH_INVALID when the packet never reached a lookup
+ *   hash[i]  u32 Toeplitz flow hash (0 for non-IP)
+ *   queue[i] u16 RSS queue = reta[hash & (reta_size - 1)]
+ *   edge[i]  u8  final graph edge
+ *   bins[n_bins + 2] u64 counters, accumulated (+=): next-hop bins
+ *            [0, n_bins), drops at n_bins, everything else at n_bins + 1.
+ */
+#ifndef CNDP_GPU_H
+#define CNDP_GPU_H
+
+#include <stdint.h>
+
+#include "cndp_fib.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CNDP_MODE_L3FWD 0u
+#define CNDP_MODE_CNET 1u
+#define CNDP_MODE_HASH 2u
+
+#define CNDP_NH_INVALID 0xFFFFFFFFu
+#define CNDP_EDGE_CLS_DROP 0xFFu /* l3fwd: pkt_cls sent the packet to pkt_drop */
+#define CNDP_RSS_KEY_LEN 40u
+#define CNDP_RETA_MAX 512u
+#define CNDP_BINS_MAX 1024u
+
+typedef struct cndp_gpu_ctx cndp_gpu_ctx_t;
+
+struct cndp_batch {
+    uint32_t mode;          /* CNDP_MODE_* */
+    uint32_t n;             /* packets */
+    const void *slab;       /* device */
+    uint64_t slab_len;      /* bytes readable from slab */
+    uint64_t stride;        /* used when offsets == NULL */
+    const uint64_t *offsets; /* device, optional: byte offset of frame i */
+    uint32_t data_off;      /* added to every frame offset (pktmbuf data_off) */
+    uint32_t buf_len;       /* pktmbuf buf_len (cnet length checks), e.g. 1984 */
+    uint32_t *nh;           /* device outputs, see above */
+    uint32_t *hash;
+    uint16_t *queue;
+    uint8_t *edge;
+    uint64_t *bins;
+    uint32_t n_bins;        /* <= CNDP_BINS_MAX */
+};
+
+/* Create / destroy a context bound to HIP device `device` (-1 = current). */
+int cndp_gpu_init(int device, cndp_gpu_ctx_t **out);
+void cndp_gpu_fini(cndp_gpu_ctx_t *ctx);
+int cndp_gpu_device(const cndp_gpu_ctx_t *ctx);
+
+/* RSS configuration: 40-byte Toeplitz key in NIC byte order (NULL keeps the
+ * Microsoft default key) and a redirection table (NULL = reta[i] = i % nb_q
+ * with reta_size 128).  reta_size must be a power of two <= CNDP_RETA_MAX. */
+int cndp_gpu_set_rss(cndp_gpu_ctx_t *ctx, const uint8_t *key, uint32_t key_len,
+                     const uint16_t *reta, uint32_t reta_size, uint32_t nb_queues);
+
+/* Bind the FIBs used by classify (fib6 may be NULL unless mode CNET).
+ * The tables must be DIR-24-8 4B / trie 4B (the l3fwd and cnet layouts). */
+int cndp_gpu_set_fib(cndp_gpu_ctx_t *ctx, struct cne_fib *fib4, struct cne_fib6 *fib6);
+
+/* Enqueue one classify pass over a device-resident batch. */
+int cndp_gpu_classify(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *stream);
+
+/* Same over HOST buffers (pinned or pageable): copies the slab (and
+ * offsets) in, classifies, copies the outputs back and waits.  This is the
+ * path a pktdev/AF_XDP consumer uses; it is PCIe-bound. */
+int cndp_gpu_classify_host(cndp_gpu_ctx_t *ctx, const struct cndp_batch *host_batch);
+
+/* Stable partition of packet indices by bin (the per-edge streams a graph
+ * walk would build): bin_of[i] in [0, n_bins+2) (device), outputs
+ * bin_start[n_bins+3] (exclusive prefix, device) and order[n] (device).
+ * The result equals a stable counting sort of i by bin_of[i]. */
+int cndp_gpu_bin_partition(cndp_gpu_ctx_t *ctx, const uint16_t *bin_of, uint32_t n,
+                           uint32_t n_bins, uint32_t *bin_start, uint32_t *order, void *stream);
+
+/* Bin id per packet as counted in cndp_batch.bins, from classify outputs. */
+int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, const uint8_t *edge,
+                     const uint16_t *queue, uint32_t n, uint32_t n_bins, uint16_t *bin_of,
+                     void *stream);
+
+/* Version / build info string. */
+const char *cndp_gpu_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,216 @@
+"""ctypes wrapper of oracle/liboracle.so (and oracle/_ref/libcndp_ref.so).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product (cndp_amd/).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, Structure, c_double, c_int, c_uint8, c_uint16, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libcndp_ref.so")
+
+MODE_L3FWD, MODE_CNET, MODE_HASH = 0, 1, 2
+
+
+class Route4(Structure):
+    _fields_ = [("ip", c_uint32), ("depth", c_uint8), ("nh", c_uint64)]
+
+
+class Route6(Structure):
+    _fields_ = [("ip", c_uint8 * 16), ("depth", c_uint8), ("nh", c_uint64)]
+
+
+class HdrLens(Structure):
+    _fields_ = [("l2_len", c_uint8), ("inner_l2_len", c_uint8), ("l3_len", c_uint16),
+                ("inner_l3_len", c_uint16), ("tunnel_len", c_uint16), ("l4_len", c_uint8),
+                ("inner_l4_len", c_uint8)]
+
+
+class ClassifyArgs(Structure):
+    _fields_ = [("mode", c_uint32), ("slab", c_void_p), ("slab_len", c_uint64), ("stride", c_uint64),
+                ("offsets", c_void_p), ("data_off", c_uint32), ("n", c_uint32), ("buf_len", c_uint32),
+                ("tbl24", c_void_p), ("tbl8", c_void_p), ("tbl24_6", c_void_p), ("tbl8_6", c_void_p),
+                ("rss_key", c_void_p), ("reta", c_void_p), ("reta_size", c_uint32), ("n_bins", c_uint32),
+                ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p), ("edge", c_void_p),
+                ("bins", c_void_p)]
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-s", "-C", HERE, os.path.join(HERE, "liboracle.so")], check=True)
+        L = ctypes.CDLL(LIB)
+        L.orc_softrss.restype = c_uint32
+        L.orc_softrss.argtypes = [c_void_p, c_uint32, c_void_p]
+        L.orc_softrss_be.restype = c_uint32
+        L.orc_softrss_be.argtypes = [c_void_p, c_uint32, c_void_p]
+        L.orc_convert_rss_key.argtypes = [c_void_p, c_void_p, c_int]
+        L.orc_ipv4_cksum.restype = c_uint16
+        L.orc_ipv4_cksum.argtypes = [c_void_p]
+        L.orc_lpm4_bruteforce.argtypes = [c_void_p, c_uint32, c_uint64, c_void_p, c_uint32, c_void_p]
+        L.orc_lpm6_bruteforce.argtypes = [c_void_p, c_uint32, c_uint64, c_void_p, c_uint32, c_void_p]
+        L.orc_dir24_8_build.restype = c_int
+        L.orc_dir24_8_build.argtypes = [c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p]
+        L.orc_dir24_8_lookup.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
+        L.orc_trie_build.restype = c_int
+        L.orc_trie_build.argtypes = [c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p]
+        L.orc_trie_lookup.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
+        L.orc_get_ptype.restype = c_uint32
+        L.orc_get_ptype.argtypes = [c_void_p, c_uint64, POINTER(HdrLens), c_uint32]
+        L.orc_classify.restype = c_int
+        L.orc_classify.argtypes = [POINTER(ClassifyArgs)]
+        L.orc_l3fwd_burst_bench.restype = c_double
+        L.orc_l3fwd_burst_bench.argtypes = [POINTER(ClassifyArgs), c_int, c_int]
+        _lib = L
+    return _lib
+
+
+def ref():
+    """The reference's own cne_softrss / cne_ipv4_cksum (None if not built)."""
+    global _ref
+    if _ref is None and os.path.exists(REF_LIB):
+        R = ctypes.CDLL(REF_LIB)
+        R.ref_softrss.restype = c_uint32
+        R.ref_softrss.argtypes = [c_void_p, c_uint32, c_void_p]
+        R.ref_softrss_be.restype = c_uint32
+        R.ref_softrss_be.argtypes = [c_void_p, c_uint32, c_void_p]
+        R.ref_convert_rss_key.argtypes = [c_void_p, c_void_p, c_int]
+        R.ref_ipv4_cksum.restype = c_uint16
+        R.ref_ipv4_cksum.argtypes = [c_void_p]
+        R.ref_thash_load_v6.argtypes = [c_void_p, c_void_p]
+        _ref = R
+    return _ref
+
+
+def _p(a):
+    return a.ctypes.data if a is not None else None
+
+
+def softrss(tuple_dw, key: bytes) -> int:
+    t = np.ascontiguousarray(tuple_dw, dtype=np.uint32)
+    return lib().orc_softrss(_p(t), len(t), key)
+
+
+def ipv4_cksum(hdr: bytes) -> int:
+    b = np.frombuffer(bytes(hdr) + bytes(64), dtype=np.uint8)
+    return lib().orc_ipv4_cksum(_p(b))
+
+
+def _routes4(routes):
+    arr = (Route4 * max(1, len(routes)))()
+    for i, (ip, d, nh) in enumerate(routes):
+        arr[i].ip, arr[i].depth, arr[i].nh = ip & 0xFFFFFFFF, d, nh
+    return arr
+
+
+def _routes6(routes):
+    arr = (Route6 * max(1, len(routes)))()
+    for i, (ip, d, nh) in enumerate(routes):
+        b = ip.to_bytes(16, "big") if isinstance(ip, int) else bytes(ip)
+        arr[i].ip[:] = list(b)
+        arr[i].depth, arr[i].nh = d, nh
+    return arr
+
+
+def lpm4_bruteforce(routes, def_nh, ips) -> np.ndarray:
+    ips = np.ascontiguousarray(ips, dtype=np.uint32)
+    out = np.zeros(len(ips), np.uint64)
+    lib().orc_lpm4_bruteforce(_routes4(routes), len(routes), def_nh, _p(ips), len(ips), _p(out))
+    return out
+
+
+def lpm6_bruteforce(routes, def_nh, ips) -> np.ndarray:
+    ips = np.ascontiguousarray(ips, dtype=np.uint8).reshape(-1, 16)
+    out = np.zeros(len(ips), np.uint64)
+    lib().orc_lpm6_bruteforce(_routes6(routes), len(routes), def_nh, _p(ips), len(ips), _p(out))
+    return out
+
+
+def dir24_8_build(routes, def_nh, num_tbl8=1024):
+    t24 = np.empty(1 << 24, np.uint32)
+    t8 = np.zeros((num_tbl8 + 1) * 256, np.uint32)
+    rc = lib().orc_dir24_8_build(_routes4(routes), len(routes), def_nh, num_tbl8, _p(t24), _p(t8))
+    if rc < 0:
+        raise OSError(-rc, "orc_dir24_8_build")
+    return t24, t8
+
+
+def dir24_8_lookup(t24, t8, ips) -> np.ndarray:
+    ips = np.ascontiguousarray(ips, dtype=np.uint32)
+    out = np.zeros(len(ips), np.uint64)
+    lib().orc_dir24_8_lookup(_p(t24), _p(t8), _p(ips), len(ips), _p(out))
+    return out
+
+
+def trie_build(routes, def_nh, num_tbl8=1 << 15):
+    t24 = np.empty(1 << 24, np.uint32)
+    t8 = np.zeros((num_tbl8 + 1) * 256, np.uint32)
+    rc = lib().orc_trie_build(_routes6(routes), len(routes), def_nh, num_tbl8, _p(t24), _p(t8))
+    if rc < 0:
+        raise OSError(-rc, "orc_trie_build")
+    return t24, t8
+
+
+def trie_lookup(t24, t8, ips) -> np.ndarray:
+    ips = np.ascontiguousarray(ips, dtype=np.uint8).reshape(-1, 16)
+    out = np.zeros(len(ips), np.uint64)
+    lib().orc_trie_lookup(_p(t24), _p(t8), _p(ips), len(ips), _p(out))
+    return out
+
+
+def get_ptype(pkt: bytes):
+    b = np.frombuffer(bytes(pkt), dtype=np.uint8)
+    hl = HdrLens()
+    pt = lib().orc_get_ptype(_p(b), len(b), ctypes.byref(hl), 0x0FFFFFFF)
+    return pt, hl
+
+
+def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, tables4=None,
+              tables6=None, key=None, reta=None, n_bins=64):
+    from cndp_amd.native import MS_RSS_KEY
+    key = np.frombuffer(key or MS_RSS_KEY, dtype=np.uint8).copy()
+    reta = np.ascontiguousarray(reta if reta is not None else (np.arange(128) % 16), dtype=np.uint16)
+    out = {"nh": np.zeros(n, np.uint32), "hash": np.zeros(n, np.uint32), "queue": np.zeros(n, np.uint16),
+           "edge": np.zeros(n, np.uint8), "bins": np.zeros(n_bins + 2, np.uint64)}
+    slab = np.ascontiguousarray(slab, dtype=np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64) if offsets is not None else None
+    a = ClassifyArgs()
+    a.mode, a.slab, a.slab_len, a.stride = mode, _p(slab), slab.nbytes, stride
+    a.offsets, a.data_off, a.n, a.buf_len = _p(off), data_off, n, buf_len
+    if tables4 is not None:
+        a.tbl24, a.tbl8 = _p(tables4[0]), _p(tables4[1])
+    if tables6 is not None:
+        a.tbl24_6, a.tbl8_6 = _p(tables6[0]), _p(tables6[1])
+    a.rss_key, a.reta, a.reta_size, a.n_bins = _p(key), _p(reta), len(reta), n_bins
+    a.nh, a.hash, a.queue, a.edge, a.bins = (_p(out["nh"]), _p(out["hash"]), _p(out["queue"]),
+                                            _p(out["edge"]), _p(out["bins"]))
+    keep = (slab, off, key, reta, tables4, tables6)  # keep buffers alive with the struct
+    return a, out, keep
+
+
+def classify(mode, slab, n, **kw) -> dict:
+    a, out, keep = make_args(mode, slab, n, **kw)
+    rc = lib().orc_classify(ctypes.byref(a))
+    if rc < 0:
+        raise OSError(-rc, "orc_classify")
+    del keep
+    return out
+
+
+def l3fwd_burst_bench(slab, n, stride, tables4, nthreads=1, iters=1, **kw) -> float:
+    a, out, keep = make_args(MODE_L3FWD, slab, n, stride=stride, tables4=tables4, **kw)
+    t = lib().orc_l3fwd_burst_bench(ctypes.byref(a), nthreads, iters)
+    del keep
+    return t

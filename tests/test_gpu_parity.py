@@ -1,0 +1,244 @@
+"""GPU parity: every kernel of libcndp_gpu.so against the oracle (bit-exact).
+
+All calls go through the C-ABI (ctypes).  Sizes are chosen so the oracle
+finishes in seconds, plus one full-size (16M packet) C3 run compared
+against the C oracle in full."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cndp_amd import native as N
+from cndp_amd import pktgen
+from oracle import oracle as O
+
+from helpers import (CNET_DEF, L3FWD_DEF, assert_same, cnet_fibs, l3fwd_fib, l3fwd_oracle_tables,
+                     oracle_classify)
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def l3(gpu):
+    from cndp_amd.classify import Classifier
+    fib, vals = l3fwd_fib()
+    cl = Classifier(0)
+    cl.set_fib(fib)
+    return cl, fib, l3fwd_oracle_tables(vals)
+
+
+@pytest.fixture(scope="module")
+def cnet(gpu):
+    from cndp_amd.classify import Classifier
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    cl = Classifier(0)
+    cl.set_fib(fib, fib6)
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    return cl, routes, v6, t4, t6
+
+
+def run_gpu(cl, frames, mode, n_bins=64, buf_len=1984):
+    out = cl.classify(frames, mode, n_bins=n_bins, buf_len=buf_len)
+    torch.cuda.synchronize()
+    return {k: v for k, v in out.items() if k != "n_bins"}
+
+
+def test_l3fwd_c3_parity(l3, gpu):
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(1 << 20, routes=pktgen.l3fwd_routes(), device=gpu)
+    got = run_gpu(cl, fr, N.CNDP_MODE_L3FWD)
+    ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+    assert_same(got, ref)
+    assert ref["bins"].sum() == fr.n
+
+
+def test_hash_c2_parity(l3, gpu):
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(1 << 20, device=gpu, seed=77)
+    got = run_gpu(cl, fr, N.CNDP_MODE_HASH)
+    ref = oracle_classify(O.MODE_HASH, fr)
+    assert_same(got, ref)
+
+
+def test_umem_layout_parity(l3, gpu):
+    """2 KiB AF_XDP UMEM frames with data at +256 (pktmbuf.c:60-80)."""
+    cl, fib, t4 = l3
+    fr = pktgen.umem_ipv4(1 << 16, routes=pktgen.l3fwd_routes(), device=gpu)
+    assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
+
+
+def test_custom_rss_key_and_reta(l3, gpu):
+    cl, fib, t4 = l3
+    rng = np.random.default_rng(5)
+    key = rng.integers(0, 256, 40, dtype=np.uint8).tobytes()
+    reta = rng.integers(0, 8, 256).astype(np.uint16)
+    cl.set_rss(key=key, reta=reta)
+    try:
+        fr = pktgen.packed_ipv4(1 << 16, routes=pktgen.l3fwd_routes(), device=gpu, seed=3)
+        got = run_gpu(cl, fr, N.CNDP_MODE_L3FWD)
+        ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4, key=key, reta=reta)
+        assert_same(got, ref)
+    finally:
+        cl.set_rss()
+
+
+@pytest.mark.parametrize("mode", [N.CNDP_MODE_L3FWD, N.CNDP_MODE_HASH])
+def test_fuzz_frames_l3fwd(l3, gpu, mode):
+    """Random frames (every ethertype / IHL / proto branch, ragged slab end)."""
+    cl, fib, t4 = l3
+    fr = pktgen.fuzz_frames(50000, seed=21, slot=96, device=gpu)
+    assert_same(run_gpu(cl, fr, mode), oracle_classify(mode, fr, tables4=t4))
+
+
+def test_fuzz_unaligned_offsets(l3, gpu):
+    """Frame offsets that are not 4/16-byte aligned take the byte-read path."""
+    cl, fib, t4 = l3
+    fr = pktgen.fuzz_frames(20000, seed=4, slot=97, device=gpu)
+    fr.data_off = 3
+    assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
+
+
+def test_cnet_imix_c4_parity(cnet, gpu):
+    cl, routes, v6, t4, t6 = cnet
+    fr = pktgen.imix(1 << 18, v4routes=routes, v6routes=v6, device=gpu)
+    got = run_gpu(cl, fr, N.CNDP_MODE_CNET)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+    assert_same(got, ref)
+    # both families forwarded somewhere
+    assert (ref["edge"] == 1).mean() > 0.5
+
+
+def test_cnet_fuzz_parity(cnet, gpu):
+    """cne_get_ptype over random structures (parity vs the unpinned restatement)."""
+    cl, routes, v6, t4, t6 = cnet
+    for seed in (1, 2, 3):
+        fr = pktgen.fuzz_frames(40000, seed=seed, slot=128, device=gpu)
+        assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6))
+
+
+def test_cnet_c5_checksum_verify(cnet, gpu):
+    """1500-B frames, 1/1024 with a corrupted IPv4 checksum (ip4_input.c:121-140)."""
+    cl, routes, v6, t4, t6 = cnet
+    fr = pktgen.packed_ipv4(1 << 17, slot=1536, frame_len=1500, routes=routes, device=gpu)
+    bad = pktgen.corrupt_cksum(fr, 1024)
+    assert bad > 50
+    got = run_gpu(cl, fr, N.CNDP_MODE_CNET)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+    assert_same(got, ref)
+
+
+def test_cnet_buf_len_check(cnet, gpu):
+    """total_length >= buf_len sends the packet to the lookup of 0.0.0.0."""
+    cl, routes, v6, t4, t6 = cnet
+    fr = pktgen.packed_ipv4(4096, slot=1536, frame_len=1500, routes=routes, device=gpu)
+    got = run_gpu(cl, fr, N.CNDP_MODE_CNET, buf_len=1000)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6, buf_len=1000)
+    assert_same(got, ref)
+
+
+def test_empty_and_single(l3, gpu):
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(1, routes=pktgen.l3fwd_routes(), device=gpu)
+    assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
+    fr0 = pktgen.Frames(torch.zeros(64, dtype=torch.uint8, device=gpu), 0, stride=64)
+    out = run_gpu(cl, fr0, N.CNDP_MODE_L3FWD)
+    assert int(out["bins"].sum()) == 0
+
+
+def test_classify_host_path(l3, gpu):
+    """Host buffers through H2D + kernel + D2H give the same answers."""
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(1 << 16, routes=pktgen.l3fwd_routes())
+    got = cl.classify_host(fr.slab.numpy(), fr.n, N.CNDP_MODE_L3FWD, stride=64)
+    assert_same(got, oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
+
+
+@pytest.mark.parametrize("nh_sz", [0, 1, 2, 3])
+def test_fib_lookup_bulk_gpu_vs_bruteforce(gpu, nh_sz):
+    from cndp_amd.fib import Fib
+    rng = np.random.default_rng(nh_sz)
+    maxnh = (1 << ((8 << nh_sz) - 1)) - 1
+    f = Fib("b", N.CNE_FIB_DIR24_8, default_nh=min(7, maxnh), max_routes=4096, nh_sz=nh_sz,
+            num_tbl8=min(127, maxnh) if nh_sz == 0 else 512)
+    routes = {}
+    for _ in range(400):
+        d = int(rng.integers(8, 33))
+        ip = int(rng.integers(0, 2**32)) & (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+        ip = 0x0A000000 | (ip & 0x00FFFFFF) if rng.random() < 0.7 else ip
+        ip &= (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+        nh = int(rng.integers(0, maxnh + 1))
+        if f.add(ip, d, nh) == 0:
+            routes[(ip, d)] = nh
+    ips = rng.integers(0, 2**32, size=20000, dtype=np.uint64).astype(np.uint32)
+    ips[::2] = 0x0A000000 | (ips[::2] & 0x00FFFFFF)
+    got = f.lookup_bulk(ips)
+    exp = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], min(7, maxnh), ips)
+    assert np.array_equal(got, exp)
+
+
+def test_fib_ladder_gpu():
+    """fib_test.c check_fib through the GPU-backed cne_fib_lookup_bulk."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_oracle_golden import _ladder4
+    from cndp_amd.fib import Fib
+    for t, nh_sz, ntbl8 in ((N.CNE_FIB_DUMMY, 0, 127), (N.CNE_FIB_DIR24_8, 0, 127), (N.CNE_FIB_DIR24_8, 1, 255),
+                            (N.CNE_FIB_DIR24_8, 2, 256), (N.CNE_FIB_DIR24_8, 3, 256)):
+        f = Fib("lad", t, default_nh=100, max_routes=1 << 16, nh_sz=nh_sz, num_tbl8=ntbl8)
+        _ladder4(f.lookup_bulk, f.add, f.delete)
+
+
+def test_lpm6_1000_rules_gpu(gpu):
+    from cndp_amd.fib import Fib6
+    g = np.load(os.path.join(GOLD, "lpm6_1000.npz"))
+    for nh_sz in (N.CNE_FIB_TRIE_2B, N.CNE_FIB_TRIE_4B, N.CNE_FIB_TRIE_8B):
+        f6 = Fib6("l6", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=nh_sz, num_tbl8=1 << 15)
+        for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
+            assert f6.add(bytes(ip), int(d), int(nh)) == 0
+        assert np.array_equal(f6.lookup_bulk(g["ip"]), g["nh"].astype(np.uint64))
+    d6 = Fib6("d6", N.CNE_FIB_DUMMY, default_nh=0, max_routes=2000)
+    for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
+        assert d6.add(bytes(ip), int(d), int(nh)) == 0
+    assert np.array_equal(d6.lookup_bulk(g["ip"]), g["nh"].astype(np.uint64))
+
+
+def test_fib_incremental_sync_gpu(gpu):
+    """Routes changed after the first GPU lookup are visible to the next one."""
+    from cndp_amd.fib import Fib
+    f = Fib("inc", N.CNE_FIB_DIR24_8, default_nh=1, max_routes=64, num_tbl8=64)
+    ips = np.array([0x0A000001, 0x0A000081, 0x0B000001], np.uint32)
+    assert list(f.lookup_bulk(ips)) == [1, 1, 1]
+    f.add(0x0A000000, 8, 5)
+    f.add(0x0A000080, 25, 6)
+    assert list(f.lookup_bulk(ips)) == [5, 6, 1]
+    f.delete(0x0A000080, 25)
+    assert list(f.lookup_bulk(ips)) == [5, 5, 1]
+
+
+def test_bin_partition_stable(l3, gpu):
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(300000, routes=pktgen.l3fwd_routes(), device=gpu, seed=9)
+    out = cl.classify(fr, N.CNDP_MODE_L3FWD, n_bins=64)
+    bins = cl.bin_ids(N.CNDP_MODE_L3FWD, out, fr.n, 64)
+    start, order = cl.bin_partition(bins, 64)
+    torch.cuda.synchronize()
+    b = bins.cpu().numpy().astype(np.int64)
+    exp_order = np.argsort(b, kind="stable")
+    assert np.array_equal(order.cpu().numpy(), exp_order)
+    counts = np.bincount(b, minlength=66)
+    assert np.array_equal(start.cpu().numpy()[:-1], np.concatenate([[0], np.cumsum(counts)[:-1]]))
+    assert np.array_equal(counts, out["bins"].cpu().numpy())
+
+
+@pytest.mark.slow
+def test_full_size_c3_16M(l3, gpu):
+    """BASELINE C3 at full size (16M packets) bit-exact against the C oracle."""
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(1 << 24, routes=pktgen.l3fwd_routes(), device=gpu)
+    got = run_gpu(cl, fr, N.CNDP_MODE_L3FWD)
+    ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+    assert_same(got, ref)
+    assert int(ref["bins"].sum()) == 1 << 24

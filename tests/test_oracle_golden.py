@@ -1,0 +1,173 @@
+"""Pin the oracle (CPU restatement) against the reference's own outputs:
+the committed golden fixtures (tests/golden/, made by tools/gen_golden.py
+from the reference's cne_softrss / cne_ipv4_cksum / lpm6_data_test.h) and
+the public Microsoft RSS KAT.  Also the reference fib_test.c / fib6_test.c
+LPM ladders against the oracle's table painter.  CPU only."""
+import json
+import os
+import socket
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kat():
+    with open(os.path.join(GOLD, "rss_kat.json")) as f:
+        return json.load(f)
+
+
+def test_rss_kat_ipv4():
+    k = _kat()
+    key = bytes.fromhex(k["key"])
+    for d, dp, s, sp, l3, l4 in k["ipv4"]:
+        t = [struct.unpack(">I", socket.inet_aton(s))[0], struct.unpack(">I", socket.inet_aton(d))[0],
+             (sp << 16) | dp]
+        assert O.softrss(t[:2], key) == l3
+        assert O.softrss(t, key) == l4
+
+
+def test_rss_kat_ipv6():
+    k = _kat()
+    key = bytes.fromhex(k["key"])
+    for d, dp, s, sp, l3, l4 in k["ipv6"]:
+        sa, da = socket.inet_pton(socket.AF_INET6, s), socket.inet_pton(socket.AF_INET6, d)
+        t = list(struct.unpack(">4I", sa)) + list(struct.unpack(">4I", da)) + [(sp << 16) | dp]
+        assert O.softrss(t[:8], key) == l3
+        assert O.softrss(t, key) == l4
+
+
+def test_softrss_matches_reference_vectors():
+    g = np.load(os.path.join(GOLD, "thash_ref.npz"))
+    L = O.lib()
+    for i in range(len(g["lens"])):
+        t = np.ascontiguousarray(g["tuples"][i])
+        key = np.ascontiguousarray(g["keys"][g["kidx"][i]])
+        assert L.orc_softrss(t.ctypes.data, int(g["lens"][i]), key.ctypes.data) == g["expected"][i]
+        kc = np.ascontiguousarray(g["keys_converted"][g["kidx"][i]])
+        assert L.orc_softrss_be(t.ctypes.data, int(g["lens"][i]), kc.ctypes.data) == g["expected_be"][i]
+
+
+def test_convert_key_matches_reference():
+    g = np.load(os.path.join(GOLD, "thash_ref.npz"))
+    for k in range(len(g["keys"])):
+        src = np.ascontiguousarray(g["keys"][k])
+        dst = np.zeros(40, np.uint8)
+        O.lib().orc_convert_rss_key(src.ctypes.data, dst.ctypes.data, 40)
+        assert np.array_equal(dst, g["keys_converted"][k])
+
+
+def test_v6_tuple_loading_matches_reference():
+    g = np.load(os.path.join(GOLD, "thash_ref.npz"))
+    for h, exp in zip(g["v6_hdr"], g["v6_loaded"]):
+        got = [int.from_bytes(bytes(h[8 + 4 * k: 12 + 4 * k]), "big") for k in range(8)]
+        assert got == [int(x) for x in exp]
+
+
+def test_ipv4_cksum_matches_reference():
+    g = np.load(os.path.join(GOLD, "cksum_ref.npz"))
+    for h, exp in zip(g["hdrs"], g["expected"]):
+        assert O.ipv4_cksum(bytes(h)) == exp
+
+
+def _ladder4(lookup, add, delete, def_nh=100):
+    """test/testcne/fib_test.c:239-288 check_fib, expressed against callables."""
+    ip_add = 128 << 24
+    ip_arr = [(ip_add + (1 << i) - 1) & 0xFFFFFFFF for i in range(32)]
+    missing = (127 << 24) | 0xFFFFFF
+
+    def asc(n):
+        got = lookup(ip_arr + [missing])
+        exp = [n] * (32 - n + 1) + [n - 1 - k for k in range(n - 1)] + [def_nh]
+        assert list(got) == exp, (n, list(got))
+
+    def desc(n):
+        got = lookup(ip_arr + [missing])
+        exp = [32 - i for i in range(n)] + [def_nh] * (32 - n) + [def_nh]
+        assert list(got) == exp, (n, list(got))
+
+    desc(0)
+    for i in range(1, 33):
+        assert add(ip_add, i, i) == 0
+        asc(i)
+    for i in range(32, 1, -1):
+        assert delete(ip_add, i) == 0
+        asc(i - 1)
+    assert delete(ip_add, 1) == 0
+    desc(0)
+    for i in range(32):
+        assert add(ip_add, 32 - i, 32 - i) == 0
+        desc(i + 1)
+    for i in range(1, 33):
+        assert delete(ip_add, i) == 0
+        desc(32 - i)
+
+
+def test_ladder4_oracle_painter():
+    routes = {}
+
+    def add(ip, d, nh):
+        routes[(ip & (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF, d)] = nh
+        return 0
+
+    def delete(ip, d):
+        routes.pop((ip & (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF, d))
+        return 0
+
+    def lookup(ips):
+        rl = [(ip, d, nh) for (ip, d), nh in routes.items()]
+        t24, t8 = O.dir24_8_build(rl, 100, 64)
+        a = O.dir24_8_lookup(t24, t8, ips)
+        b = O.lpm4_bruteforce(rl, 100, ips)
+        assert np.array_equal(a, b)
+        return a
+
+    _ladder4(lookup, add, delete)
+
+
+def test_lpm6_1000_rules_oracle():
+    g = np.load(os.path.join(GOLD, "lpm6_1000.npz"))
+    routes = [(bytes(ip), int(d), int(nh)) for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"])]
+    t24, t8 = O.trie_build(routes, 0, 1 << 16)
+    got = O.trie_lookup(t24, t8, g["ip"])
+    assert np.array_equal(got, g["nh"].astype(np.uint64))
+    bf = O.lpm6_bruteforce(routes, 0, g["ip"][:2000])
+    assert np.array_equal(bf, g["nh"][:2000].astype(np.uint64))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_dir24_8_painter_vs_bruteforce(seed):
+    rng = np.random.default_rng(seed)
+    routes = []
+    for _ in range(300):
+        d = int(rng.integers(0, 33))
+        ip = int(rng.integers(0, 2**32)) & ((0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF if d else 0)
+        routes.append((ip, d, int(rng.integers(0, 2**31 - 1))))
+    # concentrate some addresses inside the prefixes
+    ips = rng.integers(0, 2**32, size=4096, dtype=np.uint64).astype(np.uint32)
+    for i in range(0, 4096, 2):
+        ip, d, _ = routes[i % len(routes)]
+        ips[i] = (ip | (int(ips[i]) & ((1 << (32 - d)) - 1))) & 0xFFFFFFFF
+    t24, t8 = O.dir24_8_build(routes, 7, 1024)
+    assert np.array_equal(O.dir24_8_lookup(t24, t8, ips), O.lpm4_bruteforce(routes, 7, ips))
+
+
+def test_trie_painter_vs_bruteforce():
+    rng = np.random.default_rng(9)
+    routes = []
+    for _ in range(200):
+        d = int(rng.integers(0, 129))
+        ip = int.from_bytes(rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), "big")
+        ip &= ((1 << 128) - 1) ^ ((1 << (128 - d)) - 1)
+        routes.append((ip.to_bytes(16, "big"), d, int(rng.integers(0, 2**31 - 1))))
+    ips = rng.integers(0, 256, size=(2048, 16), dtype=np.uint8)
+    for i in range(0, 2048, 2):
+        ip, d, _ = routes[i % len(routes)]
+        v = int.from_bytes(ip, "big") | (int.from_bytes(ips[i].tobytes(), "big") & ((1 << (128 - d)) - 1))
+        ips[i] = np.frombuffer(v.to_bytes(16, "big"), np.uint8)
+    t24, t8 = O.trie_build(routes, 3, 1 << 14)
+    assert np.array_equal(O.trie_lookup(t24, t8, ips), O.lpm6_bruteforce(routes, 3, ips))
