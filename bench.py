@@ -46,16 +46,9 @@ def log(*a):
 
 
 def setup_dist():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(local)
+    from cndp_amd import dist as D
+    world, rank, local = D.init_from_env("nccl")
+    torch.cuda.set_device(local)
     return world, rank, local
 
 
@@ -100,7 +93,10 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None):
             fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed, device=dev)
             pktgen.corrupt_cksum(fr, 1024, seed)
             state["frames"] = fr
-    state["out"] = cl.alloc_outputs(n, 64, device=dev)
+    # l3fwd / hash: the graph edge is nh >> 16 (no separate edge stream);
+    # cnet keeps the edge output (its drop/forward/proto edge is not in nh
+    # for packets the ptype node sends elsewhere)
+    state["out"] = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
     return state
 
 
@@ -127,6 +123,8 @@ def parity_sample(state, k: int = 1 << 16) -> bool:
     torch.cuda.synchronize()
     ok = True
     for key, dt in (("nh", np.uint32), ("hash", np.uint32), ("queue", np.uint16), ("edge", np.uint8)):
+        if out.get(key) is None:
+            continue
         g = out[key][:k].cpu().numpy().view(dt)
         ok &= bool(np.array_equal(g, ref[key]))
     return ok
@@ -153,6 +151,36 @@ def cpu_baseline(state, budget_s: float = 10.0):
                        f"{single:.1f} Mpps")}
 
 
+def sweep(st, stream, cfg):
+    """Kernel-variant sweep (performance only; every variant is parity-tested)."""
+    cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
+    rows = []
+    for nt in (0, 1):
+        for unroll in (1, 2):
+            for bpc in (4, 8, 16):
+                cl.set_tuning(nt=nt, unroll=unroll, blocks_per_cu=bpc)
+                for _ in range(3):
+                    cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+                evs = []
+                for _ in range(20):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(stream)
+                    cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+                    b.record(stream)
+                    evs.append((a, b))
+                torch.cuda.synchronize()
+                ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+                gbs = st["algo"] * st["n"] / (ms * 1e-3) / 1e9
+                rows.append({"nt": nt, "unroll": unroll, "bpc": bpc, "kernel_ms": ms, "algo_GBs": gbs,
+                             "Mpps": st["n"] / ms / 1e3})
+                log(f"[sweep {cfg}] nt={nt} unroll={unroll} bpc={bpc:2d}: {ms:.4f} ms "
+                    f"{gbs:7.1f} GB/s {st['n'] / ms / 1e3:9.1f} Mpps")
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
+        json.dump(rows, f, indent=1)
+    cl.set_tuning(nt=1, unroll=1, blocks_per_cu=8)
+
+
 def load_traffic(cfg: str):
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
@@ -174,8 +202,13 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr + gpurun_out)")
+    ap.add_argument("--nt", type=int, default=None)
+    ap.add_argument("--unroll", type=int, default=None)
+    ap.add_argument("--bpc", type=int, default=None)
     args = ap.parse_args()
 
+    from cndp_amd import dist as D
     world, rank, local = setup_dist()
     dev = torch.device(f"cuda:{local}")
     t0 = time.time()
@@ -185,6 +218,9 @@ def main():
         log(f"[bench] setup {time.time() - t0:.1f}s: {st['desc']}")
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     stream = torch.cuda.current_stream(dev)
+    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc)
+    if args.sweep and rank == 0:
+        sweep(st, stream, args.config)
 
     for _ in range(args.warmup):
         cl.classify(fr, mode, out=out)
@@ -206,9 +242,7 @@ def main():
         evs[s][0].record(stream)
         cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
         evs[s][1].record(stream)
-    if world > 1:
-        import torch.distributed as dist
-        dist.all_reduce(out["bins"])  # final per-bin (next hop / port) count reduce over RCCL
+    D.final_count_reduce(out["bins"])  # the one RCCL collective: per-bin counts
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -216,10 +250,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], dev)
 
     n = st["n"]
     total_pkts = n * world * args.steps

@@ -51,6 +51,14 @@ class Classifier:
                                          nb_queues), "cndp_gpu_set_rss")
         self.reta_size = size or 128
 
+    def set_tuning(self, nt: int | None = None, unroll: int | None = None,
+                   blocks_per_cu: int | None = None):
+        """Kernel variant knobs (cndp_gpu_set_tuning); never change results."""
+        for key, v in ((N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),
+                       (N.CNDP_TUNE_BLOCKS_PER_CU, blocks_per_cu)):
+            if v is not None:
+                N.check(self._L.cndp_gpu_set_tuning(self.h, key, int(v)), "cndp_gpu_set_tuning")
+
     def set_fib(self, fib4=None, fib6=None):
         N.check(self._L.cndp_gpu_set_fib(self.h, fib4.h if fib4 else None, fib6.h if fib6 else None),
                 "cndp_gpu_set_fib")

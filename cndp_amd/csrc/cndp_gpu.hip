@@ -138,9 +138,122 @@ __device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip
 // l3fwd / hash classify: pktdev_rx.c:24-34 + pkt_cls.c:19-31 + ip4_lookup.c
 // :108-154 (+ build-defined Toeplitz / RSS queue).  Header fields sit at fixed
 // offsets (Ethernet 14 B, no VLAN parse in this chain), so each lane loads
-// bytes 12..39 of its frame into 7 VGPRs and never touches them again.
+// bytes 12..39 of its frame into VGPRs and never touches them again.
+// Variants (runtime-selected, see cndp_gpu_set_tuning):
+//   NT  frames read / outputs written with the non-temporal hint, so the
+//       once-touched stream does not evict the DIR-24-8 table from the
+//       Infinity Cache / L2 (the random 10% of lookups then stay on-die);
+//   U   packets per lane per loop trip (U = 2 issues both frames' loads
+//       before the first dependent LPM gather: more bytes in flight).
 // ---------------------------------------------------------------------------
-template <int MODE>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ldg4(const uint8_t *p)
+{
+    if (NT)
+        return __builtin_nontemporal_load((const u32x4 *)p);
+    return *(const u32x4 *)p;
+}
+template <bool NT>
+__device__ __forceinline__ u32x2 ldg2(const uint8_t *p)
+{
+    if (NT)
+        return __builtin_nontemporal_load((const u32x2 *)p);
+    return *(const u32x2 *)p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void stg(T *p, T v)
+{
+    if (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+struct FastHdr {
+    const uint8_t *p;
+    uint64_t avail;
+    uint32_t w3, w5, w6, w7, w8, w9;
+};
+
+template <bool NT>
+__device__ __forceinline__ void fast_load(const KArgs &a, uint64_t i, FastHdr &h)
+{
+    const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
+    h.p = a.slab + base;
+    h.avail = base < a.slab_len ? a.slab_len - base : 0;
+    if (h.avail >= 48 && (base & 15u) == 0) {
+        const u32x4 q0 = ldg4<NT>(h.p + 0);
+        const u32x4 q1 = ldg4<NT>(h.p + 16);
+        const u32x2 q2 = ldg2<NT>(h.p + 32);
+        h.w3 = q0.w;
+        h.w5 = q1.y;
+        h.w6 = q1.z;
+        h.w7 = q1.w;
+        h.w8 = q2.x;
+        h.w9 = q2.y;
+    } else if (h.avail >= 40 && (base & 3u) == 0) {
+        const uint32_t *d = (const uint32_t *)h.p;
+        h.w3 = d[3];
+        h.w5 = d[5];
+        h.w6 = d[6];
+        h.w7 = d[7];
+        h.w8 = d[8];
+        h.w9 = d[9];
+    } else {
+        h.w3 = gld32(h.p, h.avail, 12);
+        h.w5 = gld32(h.p, h.avail, 20);
+        h.w6 = gld32(h.p, h.avail, 24);
+        h.w7 = gld32(h.p, h.avail, 28);
+        h.w8 = gld32(h.p, h.avail, 32);
+        h.w9 = gld32(h.p, h.avail, 36);
+    }
+}
+
+template <int MODE, bool NT>
+__device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const FastHdr &h,
+                                            const uint32_t *s_t, const uint16_t *s_reta,
+                                            uint32_t *s_bins, bool count)
+{
+    const uint32_t et = bswap16(h.w3 & 0xffffu);
+    uint32_t hs = 0, nh = CNDP_NH_INVALID, edge;
+    if (et == 0x0800u) {
+        const uint32_t ihl = (h.w3 >> 16) & 0xfu;
+        const uint32_t proto = h.w5 >> 24;
+        const uint32_t frag = bswap16(h.w5 & 0xffffu) & 0x3fffu;
+        const uint32_t src = alignb(h.w7, h.w6, 2);
+        const uint32_t dst = alignb(h.w8, h.w7, 2);
+        if (MODE == CNDP_MODE_L3FWD)
+            nh = lpm4(a.tbl24, a.tbl8, bswap32(dst)); // issue the gather first
+        hs = tz4(s_t, 0, src) ^ tz4(s_t, 4, dst);
+        if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
+            const uint32_t ports = ihl == 5 ? alignb(h.w9, h.w8, 2) : gld32(h.p, h.avail, 14 + 4 * ihl);
+            hs ^= tz4(s_t, 8, ports);
+        }
+    } else if (et == 0x86DDu) {
+        const uint32_t nx = h.w5 & 0xffu; // ip6 next header: frame byte 20
+        hs = hash_v6_global(h.p, h.avail, 14, nx == 6u || nx == 17u, a.ttab);
+    }
+    if (MODE == CNDP_MODE_HASH)
+        edge = 0;
+    else
+        edge = et == 0x0800u ? ((nh >> 16) & 0xffu) : 0xFFu;
+    const uint32_t q = s_reta[hs & a.reta_mask];
+    if (a.nh)
+        stg<NT>(a.nh + i, nh);
+    if (a.hash)
+        stg<NT>(a.hash + i, hs);
+    if (a.queue)
+        stg<NT>(a.queue + i, (uint16_t)q);
+    if (a.edge)
+        stg<NT>(a.edge + i, (uint8_t)edge);
+    if (count)
+        atomicAdd(&s_bins[bin_of<MODE>(nh, edge, q, a.n_bins)], 1u);
+}
+
+template <int MODE, bool NT, int U>
 __global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
 {
     __shared__ uint32_t s_t[TAB4_POS * 256];
@@ -159,75 +272,20 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
     __syncthreads();
 
     const uint64_t step = (uint64_t)gridDim.x * FAST_THREADS;
-    for (uint64_t i = (uint64_t)blockIdx.x * FAST_THREADS + tid; i < a.n; i += step) {
-        const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
-        const uint8_t *p = a.slab + base;
-        const uint64_t avail = base < a.slab_len ? a.slab_len - base : 0;
-        uint32_t w3, w4, w5, w6, w7, w8, w9;
-        if (avail >= 48 && (base & 15u) == 0) {
-            const uint4 q0 = *(const uint4 *)(p + 0);
-            const uint4 q1 = *(const uint4 *)(p + 16);
-            const uint2 q2 = *(const uint2 *)(p + 32);
-            w3 = q0.w;
-            w4 = q1.x;
-            w5 = q1.y;
-            w6 = q1.z;
-            w7 = q1.w;
-            w8 = q2.x;
-            w9 = q2.y;
-        } else if (avail >= 40 && (base & 3u) == 0) {
-            const uint32_t *d = (const uint32_t *)p;
-            w3 = d[3];
-            w4 = d[4];
-            w5 = d[5];
-            w6 = d[6];
-            w7 = d[7];
-            w8 = d[8];
-            w9 = d[9];
-        } else {
-            w3 = gld32(p, avail, 12);
-            w4 = gld32(p, avail, 16);
-            w5 = gld32(p, avail, 20);
-            w6 = gld32(p, avail, 24);
-            w7 = gld32(p, avail, 28);
-            w8 = gld32(p, avail, 32);
-            w9 = gld32(p, avail, 36);
+    uint64_t i = (uint64_t)blockIdx.x * FAST_THREADS + tid;
+    if (U == 2) {
+        for (; i + step < a.n; i += 2 * step) {
+            FastHdr h0, h1;
+            fast_load<NT>(a, i, h0);
+            fast_load<NT>(a, i + step, h1);
+            fast_finish<MODE, NT>(a, i, h0, s_t, s_reta, s_bins, count);
+            fast_finish<MODE, NT>(a, i + step, h1, s_t, s_reta, s_bins, count);
         }
-        (void)w4;
-        const uint32_t et = bswap16(w3 & 0xffffu);
-        uint32_t h = 0, nh = CNDP_NH_INVALID, edge;
-        if (et == 0x0800u) {
-            const uint32_t ihl = (w3 >> 16) & 0xfu;
-            const uint32_t proto = w5 >> 24;
-            const uint32_t frag = bswap16(w5 & 0xffffu) & 0x3fffu;
-            const uint32_t src = alignb(w7, w6, 2);
-            const uint32_t dst = alignb(w8, w7, 2);
-            h = tz4(s_t, 0, src) ^ tz4(s_t, 4, dst);
-            if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
-                const uint32_t ports = ihl == 5 ? alignb(w9, w8, 2) : gld32(p, avail, 14 + 4 * ihl);
-                h ^= tz4(s_t, 8, ports);
-            }
-            if (MODE == CNDP_MODE_L3FWD)
-                nh = lpm4(a.tbl24, a.tbl8, bswap32(dst));
-        } else if (et == 0x86DDu) {
-            const uint32_t nx = w5 & 0xffu; // ip6 next header: frame byte 20
-            h = hash_v6_global(p, avail, 14, nx == 6u || nx == 17u, a.ttab);
-        }
-        if (MODE == CNDP_MODE_HASH)
-            edge = 0;
-        else
-            edge = et == 0x0800u ? ((nh >> 16) & 0xffu) : 0xFFu;
-        const uint32_t q = s_reta[h & a.reta_mask];
-        if (a.nh)
-            a.nh[i] = nh;
-        if (a.hash)
-            a.hash[i] = h;
-        if (a.queue)
-            a.queue[i] = (uint16_t)q;
-        if (a.edge)
-            a.edge[i] = (uint8_t)edge;
-        if (count)
-            atomicAdd(&s_bins[bin_of<MODE>(nh, edge, q, a.n_bins)], 1u);
+    }
+    for (; i < a.n; i += step) {
+        FastHdr h0;
+        fast_load<NT>(a, i, h0);
+        fast_finish<MODE, NT>(a, i, h0, s_t, s_reta, s_bins, count);
     }
     if (count) {
         __syncthreads();
@@ -771,6 +829,9 @@ struct cndp_gpu_ctx {
     uint32_t *d_part;     // partition scratch
     size_t part_cap;
     int num_cu;
+    int tune_nt;          // CNDP_TUNE_NT
+    int tune_unroll;      // CNDP_TUNE_UNROLL
+    int tune_bpc;         // CNDP_TUNE_BLOCKS_PER_CU
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -832,6 +893,9 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     if (!c)
         return -ENOMEM;
     c->dev = device;
+    c->tune_nt = 1;
+    c->tune_unroll = 1;
+    c->tune_bpc = 8;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -1147,13 +1211,23 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
         hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
-        const uint32_t cap = (uint32_t)c->num_cu * 8u;
+        const uint32_t cap = (uint32_t)c->num_cu * (uint32_t)c->tune_bpc;
         if (g > cap)
             g = cap;
-        if (b->mode == CNDP_MODE_L3FWD)
-            hipLaunchKernelGGL(k_classify_fast<CNDP_MODE_L3FWD>, dim3(g), dim3(FAST_THREADS), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_classify_fast<CNDP_MODE_HASH>, dim3(g), dim3(FAST_THREADS), 0, s, a);
+#define LAUNCH_FAST(M, NTV, UV) \
+    hipLaunchKernelGGL((k_classify_fast<M, NTV, UV>), dim3(g), dim3(FAST_THREADS), 0, s, a)
+        const int v = (b->mode == CNDP_MODE_L3FWD ? 0 : 4) | (c->tune_nt ? 2 : 0) | (c->tune_unroll == 2 ? 1 : 0);
+        switch (v) {
+        case 0: LAUNCH_FAST(CNDP_MODE_L3FWD, false, 1); break;
+        case 1: LAUNCH_FAST(CNDP_MODE_L3FWD, false, 2); break;
+        case 2: LAUNCH_FAST(CNDP_MODE_L3FWD, true, 1); break;
+        case 3: LAUNCH_FAST(CNDP_MODE_L3FWD, true, 2); break;
+        case 4: LAUNCH_FAST(CNDP_MODE_HASH, false, 1); break;
+        case 5: LAUNCH_FAST(CNDP_MODE_HASH, false, 2); break;
+        case 6: LAUNCH_FAST(CNDP_MODE_HASH, true, 1); break;
+        default: LAUNCH_FAST(CNDP_MODE_HASH, true, 2); break;
+        }
+#undef LAUNCH_FAST
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -1279,6 +1353,29 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
                        c->d_part, order);
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
+{
+    if (!c)
+        return -EINVAL;
+    switch (key) {
+    case CNDP_TUNE_NT:
+        c->tune_nt = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_UNROLL:
+        if (value != 1 && value != 2)
+            return -EINVAL;
+        c->tune_unroll = value;
+        return 0;
+    case CNDP_TUNE_BLOCKS_PER_CU:
+        if (value < 1 || value > 64)
+            return -EINVAL;
+        c->tune_bpc = value;
+        return 0;
+    default:
+        return -EINVAL;
+    }
 }
 
 extern "C" const char *cndp_gpu_version(void) { return CNDP_VERSION; }

@@ -65,15 +65,13 @@ static inline uint32_t key_dw_be(const uint8_t *key, uint32_t j)
 
 uint32_t orc_softrss(const uint32_t *tuple, uint32_t len_dw, const uint8_t *key)
 {
+    /* visits the set bits lowest first, like the map &= map - 1 loop */
     uint32_t h = 0;
     for (uint32_t j = 0; j < len_dw; j++) {
         uint32_t hi = key_dw_be(key, j), lo = key_dw_be(key, j + 1);
-        for (int i = 31; i >= 0; i--) {
-            if (!(tuple[j] >> i & 1u))
-                continue;
-            uint32_t w = hi << (31 - i);
-            w |= (uint32_t)((uint64_t)lo >> (i + 1));
-            h ^= w;
+        for (uint32_t map = tuple[j]; map; map &= map - 1) {
+            uint32_t i = (uint32_t)__builtin_ctz(map);
+            h ^= (hi << (31 - i)) | (uint32_t)((uint64_t)lo >> (i + 1));
         }
     }
     return h;
@@ -88,9 +86,8 @@ uint32_t orc_softrss_be(const uint32_t *tuple, uint32_t len_dw, const uint8_t *k
         uint32_t hi, lo;
         memcpy(&hi, k + j, 4);
         memcpy(&lo, k + j + 1, 4);
-        for (int i = 31; i >= 0; i--) {
-            if (!(tuple[j] >> i & 1u))
-                continue;
+        for (uint32_t map = tuple[j]; map; map &= map - 1) {
+            uint32_t i = (uint32_t)__builtin_ctz(map);
             h ^= (hi << (31 - i)) | (uint32_t)((uint64_t)lo >> (i + 1));
         }
     }

@@ -1,0 +1,79 @@
+"""world_size-2 gloo rehearsal of the multi-GPU path on CPU: each rank
+classifies its own contiguous shard (here with the oracle standing in for
+the device, since this container has no GPU), then the per-bin counters are
+all-reduced once; the result must equal the counters of the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    from cndp_amd import dist as D
+    from cndp_amd import pktgen
+    from oracle import oracle as O
+    import helpers
+    w, r, _ = D.init_from_env("gloo")
+    assert (w, r) == (world, rank)
+    vals = [(ip, d, nh) for ip, d, nh in pktgen.l3fwd_routes()]
+    t4 = O.dir24_8_build(vals, helpers.L3FWD_DEF, 256)
+    lo, hi = D.shard(n, rank, world)
+    fr = pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes())
+    slab = fr.slab.numpy()[lo * 64: hi * 64]
+    out = O.classify(O.MODE_L3FWD, slab, hi - lo, stride=64, tables4=t4)
+    bins = torch.from_numpy(out["bins"].astype(np.int64))
+    D.final_count_reduce(bins)
+    mx = D.max_over_ranks([float(rank)], "cpu")
+    if rank == 0:
+        q.put((bins.numpy().copy(), mx))
+    torch.distributed.destroy_process_group()
+
+
+def test_two_rank_count_reduce():
+    n = 40000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    bins, mx = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from cndp_amd import pktgen
+    from oracle import oracle as O
+    import helpers
+    vals = [(ip, d, nh) for ip, d, nh in pktgen.l3fwd_routes()]
+    t4 = O.dir24_8_build(vals, helpers.L3FWD_DEF, 256)
+    fr = pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes())
+    full = O.classify(O.MODE_L3FWD, fr.slab.numpy(), n, stride=64, tables4=t4)
+    assert np.array_equal(bins.astype(np.uint64), full["bins"])
+    assert mx == [1.0]
+
+
+def test_shard_covers_everything():
+    from cndp_amd.dist import shard
+    for n in (0, 1, 7, 1000, 16777216):
+        for w in (1, 2, 3, 8):
+            parts = [shard(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            for (a, b), (c, d) in zip(parts, parts[1:]):
+                assert b == c and a <= b

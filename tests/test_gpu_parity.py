@@ -195,7 +195,7 @@ def test_lpm6_1000_rules_gpu(gpu):
     from cndp_amd.fib import Fib6
     g = np.load(os.path.join(GOLD, "lpm6_1000.npz"))
     for nh_sz in (N.CNE_FIB_TRIE_2B, N.CNE_FIB_TRIE_4B, N.CNE_FIB_TRIE_8B):
-        f6 = Fib6("l6", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=nh_sz, num_tbl8=1 << 15)
+        f6 = Fib6("l6", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=nh_sz, num_tbl8=1 << 14)
         for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
             assert f6.add(bytes(ip), int(d), int(nh)) == 0
         assert np.array_equal(f6.lookup_bulk(g["ip"]), g["nh"].astype(np.uint64))
@@ -242,3 +242,19 @@ def test_full_size_c3_16M(l3, gpu):
     ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
     assert_same(got, ref)
     assert int(ref["bins"].sum()) == 1 << 24
+
+
+@pytest.mark.parametrize("mode", [N.CNDP_MODE_L3FWD, N.CNDP_MODE_HASH])
+def test_tuning_variants_identical(l3, gpu, mode):
+    """Every kernel variant (nt / unroll / grid) produces the same bits."""
+    cl, fib, t4 = l3
+    fr = pktgen.packed_ipv4(300001, routes=pktgen.l3fwd_routes(), device=gpu, seed=12)
+    ref = oracle_classify(mode, fr, tables4=t4)
+    try:
+        for nt in (0, 1):
+            for unroll in (1, 2):
+                for bpc in (1, 8, 16):
+                    cl.set_tuning(nt=nt, unroll=unroll, blocks_per_cu=bpc)
+                    assert_same(run_gpu(cl, fr, mode), ref)
+    finally:
+        cl.set_tuning(nt=1, unroll=1, blocks_per_cu=8)
