@@ -155,30 +155,29 @@ def sweep(st, stream, cfg):
     """Kernel-variant sweep (performance only; every variant is parity-tested)."""
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     rows = []
-    for nt in (0, 1):
-        for unroll in (1, 2):
-            for bpc in (4, 8, 16):
-                cl.set_tuning(nt=nt, unroll=unroll, blocks_per_cu=bpc)
-                for _ in range(3):
-                    cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
-                evs = []
-                for _ in range(20):
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record(stream)
-                    cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
-                    b.record(stream)
-                    evs.append((a, b))
-                torch.cuda.synchronize()
-                ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
-                gbs = st["algo"] * st["n"] / (ms * 1e-3) / 1e9
-                rows.append({"nt": nt, "unroll": unroll, "bpc": bpc, "kernel_ms": ms, "algo_GBs": gbs,
-                             "Mpps": st["n"] / ms / 1e3})
-                log(f"[sweep {cfg}] nt={nt} unroll={unroll} bpc={bpc:2d}: {ms:.4f} ms "
-                    f"{gbs:7.1f} GB/s {st['n'] / ms / 1e3:9.1f} Mpps")
+    variants = [dict(tile=0, nt=0, unroll=1, blocks_per_cu=4), dict(tile=0, nt=0, unroll=1, blocks_per_cu=8),
+                dict(tile=0, nt=1, unroll=1, blocks_per_cu=4), dict(tile=0, nt=0, unroll=2, blocks_per_cu=4)]
+    variants += [dict(tile=t, nt=0, unroll=1, blocks_per_cu=b) for t in (1, 2) for b in (2, 4, 8)]
+    for v in variants:
+        cl.set_tuning(**v)
+        for _ in range(3):
+            cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+        evs = []
+        for _ in range(20):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+            b.record(stream)
+            evs.append((a, b))
+        torch.cuda.synchronize()
+        ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+        gbs = st["algo"] * st["n"] / (ms * 1e-3) / 1e9
+        rows.append(dict(v, kernel_ms=ms, algo_GBs=gbs, Mpps=st["n"] / ms / 1e3))
+        log(f"[sweep {cfg}] {v}: {ms:.4f} ms {gbs:7.1f} GB/s {st['n'] / ms / 1e3:9.1f} Mpps")
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(nt=1, unroll=1, blocks_per_cu=8)
+    cl.set_tuning(tile=1, nt=0, unroll=1, blocks_per_cu=4)
 
 
 def load_traffic(cfg: str):

@@ -212,20 +212,32 @@ __device__ __forceinline__ void fast_load(const KArgs &a, uint64_t i, FastHdr &h
     }
 }
 
-template <int MODE, bool NT>
+// ip4_lookup.c:109-145 for one frame: the FIB value, or CNDP_NH_INVALID when
+// pkt_cls would not send the frame to ip4_lookup (ethertype != IPv4)
+template <int MODE>
+__device__ __forceinline__ uint32_t fast_lpm(const KArgs &a, const FastHdr &h)
+{
+    if (MODE != CNDP_MODE_L3FWD || bswap16(h.w3 & 0xffffu) != 0x0800u)
+        return CNDP_NH_INVALID;
+    return lpm4(a.tbl24, a.tbl8, bswap32(alignb(h.w8, h.w7, 2)));
+}
+
+template <int MODE, bool NT, bool PRE = false>
 __device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const FastHdr &h,
                                             const uint32_t *s_t, const uint16_t *s_reta,
-                                            uint32_t *s_bins, bool count)
+                                            uint32_t *s_bins, bool count, uint32_t nh_pre = 0)
 {
     const uint32_t et = bswap16(h.w3 & 0xffffu);
     uint32_t hs = 0, nh = CNDP_NH_INVALID, edge;
+    if (PRE)
+        nh = nh_pre;
     if (et == 0x0800u) {
         const uint32_t ihl = (h.w3 >> 16) & 0xfu;
         const uint32_t proto = h.w5 >> 24;
         const uint32_t frag = bswap16(h.w5 & 0xffffu) & 0x3fffu;
         const uint32_t src = alignb(h.w7, h.w6, 2);
         const uint32_t dst = alignb(h.w8, h.w7, 2);
-        if (MODE == CNDP_MODE_L3FWD)
+        if (MODE == CNDP_MODE_L3FWD && !PRE)
             nh = lpm4(a.tbl24, a.tbl8, bswap32(dst)); // issue the gather first
         hs = tz4(s_t, 0, src) ^ tz4(s_t, 4, dst);
         if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
@@ -286,6 +298,117 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
         FastHdr h0;
         fast_load<NT>(a, i, h0);
         fast_finish<MODE, NT>(a, i, h0, s_t, s_reta, s_bins, count);
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Wave-tile variant for packed 64-byte slots (stride 64): each wave owns a
+// tile of 64 consecutive frames = 4 KiB of contiguous HBM.  The wave reads
+// it with 4 fully coalesced 1-KiB loads (16 B/lane), writes the 16-B chunks
+// to its LDS tile with the row swizzle  part' = part ^ ((frame >> 2) & 3),
+// and each lane then reads its own frame's parts 0..2 with ds_read_b128 /
+// ds_read_b64 -- conflict-free for the b128 lane groups.  The next tile's
+// four loads are issued before the current tile is parsed, so each wave
+// keeps 4 KiB in flight while it computes.
+// ---------------------------------------------------------------------------
+#define TILE_WAVES (FAST_THREADS / 64)
+
+template <int MODE, int SCHED>
+__global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_t n_tiles)
+{
+    __shared__ uint32_t s_t[TAB4_POS * 256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[TILE_WAVES][256];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB4_POS * 256; k += FAST_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += FAST_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint8_t *base = a.slab + a.data_off;
+    const uint64_t wstep = (uint64_t)gridDim.x * TILE_WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * TILE_WAVES + wv;
+    // swizzled destination of the chunk this lane loads in instruction k:
+    // chunk c = 64k + lane -> frame c>>2 (= 16k + lane>>2), part c&3
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    u32x4 r0, r1, r2, r3;
+    if (t < n_tiles) {
+        const u32x4 *g = (const u32x4 *)(base + t * 4096u);
+        r0 = g[lane];
+        r1 = g[64 + lane];
+        r2 = g[128 + lane];
+        r3 = g[192 + lane];
+    }
+    for (; t < n_tiles; t += wstep) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t f = 16u * k + fr_in_k;
+            const u32x4 v = k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r3;
+            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t tn = t + wstep;
+        if (SCHED == 0 && tn < n_tiles) { // prefetch the next tile while this one is parsed
+            const u32x4 *g = (const u32x4 *)(base + tn * 4096u);
+            r0 = g[lane];
+            r1 = g[64 + lane];
+            r2 = g[128 + lane];
+            r3 = g[192 + lane];
+        }
+        const uint32_t sw = (lane >> 2) & 3u;
+        const u32x4 p0 = tile[lane * 4u + (0u ^ sw)];
+        const u32x4 p1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t i = t * 64u + lane;
+        FastHdr h;
+        h.p = base + i * 64u;
+        h.avail = a.slab_len - (a.data_off + i * 64u);
+        h.w3 = p0.w;
+        h.w5 = p1.y;
+        h.w6 = p1.z;
+        h.w7 = p1.w;
+        h.w8 = p2.x;
+        h.w9 = p2.y;
+        if (SCHED == 0) {
+            fast_finish<MODE, false>(a, i, h, s_t, s_reta, s_bins, count);
+        } else {
+            // finish the dependent tbl24 -> tbl8 gathers first: vmcnt drains in
+            // issue order, so a prefetch issued before them would be waited for
+            const uint32_t nh = fast_lpm<MODE>(a, h);
+            if (tn < n_tiles) {
+                const u32x4 *g = (const u32x4 *)(base + tn * 4096u);
+                r0 = g[lane];
+                r1 = g[64 + lane];
+                r2 = g[128 + lane];
+                r3 = g[192 + lane];
+            }
+            fast_finish<MODE, false, true>(a, i, h, s_t, s_reta, s_bins, count, nh);
+        }
+    }
+    // ragged tail (frames past the last whole tile): per-lane path
+    const uint64_t done = n_tiles * 64u;
+    for (uint64_t i = done + (uint64_t)blockIdx.x * FAST_THREADS + tid; i < a.n;
+         i += (uint64_t)gridDim.x * FAST_THREADS) {
+        FastHdr h;
+        fast_load<false>(a, i, h);
+        fast_finish<MODE, false>(a, i, h, s_t, s_reta, s_bins, count);
     }
     if (count) {
         __syncthreads();
@@ -832,6 +955,7 @@ struct cndp_gpu_ctx {
     int tune_nt;          // CNDP_TUNE_NT
     int tune_unroll;      // CNDP_TUNE_UNROLL
     int tune_bpc;         // CNDP_TUNE_BLOCKS_PER_CU
+    int tune_tile;        // CNDP_TUNE_TILE
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -893,9 +1017,10 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     if (!c)
         return -ENOMEM;
     c->dev = device;
-    c->tune_nt = 1;
+    c->tune_nt = 0;
     c->tune_unroll = 1;
-    c->tune_bpc = 8;
+    c->tune_bpc = 4;
+    c->tune_tile = 1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -1214,6 +1339,37 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
         const uint32_t cap = (uint32_t)c->num_cu * (uint32_t)c->tune_bpc;
         if (g > cap)
             g = cap;
+        // wave-tile path: packed 64-B slots, 16-B aligned, whole tiles in bounds
+        const uint64_t n_tiles = b->n / 64u;
+        const bool tile_ok = c->tune_tile && !b->offsets && b->stride == 64 &&
+                             (((uintptr_t)b->slab + b->data_off) & 15u) == 0 && n_tiles > 0 &&
+                             b->data_off + n_tiles * 4096u <= b->slab_len;
+        if (tile_ok) {
+            uint32_t gt = (uint32_t)((n_tiles + TILE_WAVES - 1) / TILE_WAVES);
+            if (gt > cap)
+                gt = cap;
+            const int tv = (b->mode == CNDP_MODE_L3FWD ? 0 : 2) | (c->tune_tile == 2 ? 1 : 0);
+            switch (tv) {
+            case 0:
+                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_L3FWD, 0>), dim3(gt), dim3(FAST_THREADS), 0, s,
+                                   a, n_tiles);
+                break;
+            case 1:
+                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_L3FWD, 1>), dim3(gt), dim3(FAST_THREADS), 0, s,
+                                   a, n_tiles);
+                break;
+            case 2:
+                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_HASH, 0>), dim3(gt), dim3(FAST_THREADS), 0, s,
+                                   a, n_tiles);
+                break;
+            default:
+                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_HASH, 1>), dim3(gt), dim3(FAST_THREADS), 0, s,
+                                   a, n_tiles);
+                break;
+            }
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
 #define LAUNCH_FAST(M, NTV, UV) \
     hipLaunchKernelGGL((k_classify_fast<M, NTV, UV>), dim3(g), dim3(FAST_THREADS), 0, s, a)
         const int v = (b->mode == CNDP_MODE_L3FWD ? 0 : 4) | (c->tune_nt ? 2 : 0) | (c->tune_unroll == 2 ? 1 : 0);
@@ -1372,6 +1528,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 1 || value > 64)
             return -EINVAL;
         c->tune_bpc = value;
+        return 0;
+    case CNDP_TUNE_TILE:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_tile = value;
         return 0;
     default:
         return -EINVAL;

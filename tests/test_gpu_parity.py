@@ -254,7 +254,23 @@ def test_tuning_variants_identical(l3, gpu, mode):
         for nt in (0, 1):
             for unroll in (1, 2):
                 for bpc in (1, 8, 16):
-                    cl.set_tuning(nt=nt, unroll=unroll, blocks_per_cu=bpc)
+                    cl.set_tuning(tile=0, nt=nt, unroll=unroll, blocks_per_cu=bpc)
                     assert_same(run_gpu(cl, fr, mode), ref)
+        for tile in (1, 2):
+            for bpc in (1, 2, 4, 16):
+                cl.set_tuning(tile=tile, blocks_per_cu=bpc)
+                assert_same(run_gpu(cl, fr, mode), ref)
     finally:
-        cl.set_tuning(nt=1, unroll=1, blocks_per_cu=8)
+        cl.set_tuning(tile=1, nt=0, unroll=1, blocks_per_cu=4)
+
+
+def test_tile_path_ragged_and_offset(l3, gpu):
+    """Wave-tile path with a 16-B data_off and n not a multiple of 64."""
+    cl, fib, t4 = l3
+    n = 64 * 1000 + 37
+    fr = pktgen.packed_ipv4(n + 1, routes=pktgen.l3fwd_routes(), device=gpu, seed=14)
+    fr2 = pktgen.Frames(fr.slab, n, stride=64, data_off=16)
+    for tile in (0, 1, 2):
+        cl.set_tuning(tile=tile)
+        assert_same(run_gpu(cl, fr2, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr2, tables4=t4))
+    cl.set_tuning(tile=1)

@@ -29,6 +29,9 @@ if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
     step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
     step pytest_gpu 1200 python3 -m pytest tests -m gpu -q -p no:cacheprovider -x
 fi
+if [ "$WHAT" = all ] || [ "$WHAT" = sweep ]; then
+    step sweep_$CFG 600 python3 bench.py --config $CFG --sweep --steps 5 --warmup 2 --no-cpu-baseline --no-parity
+fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
     step bench 600 python3 bench.py --config $CFG --steps 50 --warmup 5
     grep '^{' $OUT/bench.log > $OUT/bench_$CFG.json || true
