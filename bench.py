@@ -52,7 +52,7 @@ def setup_dist():
     return world, rank, local
 
 
-def build_state(cfg: str, dev, rank: int, n_override: int | None):
+def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac: float = 0.9):
     from cndp_amd import native as N
     from cndp_amd import pktgen
     from cndp_amd.classify import Classifier
@@ -73,7 +73,8 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None):
         cl.set_fib(fib)
         state["fib"] = fib
         state["mode"] = N.CNDP_MODE_HASH if cfg == "c2" else N.CNDP_MODE_L3FWD
-        state["frames"] = pktgen.packed_ipv4(n, routes=routes, seed=seed, device=dev)
+        state["frames"] = pktgen.packed_ipv4(n, routes=routes, seed=seed, device=dev,
+                                             in_route_frac=in_route_frac)
     else:
         nr = 1024
         fib = Fib("rt4-fib", N.CNE_FIB_DIR24_8, default_nh=(0 << 24) | (nr + 1), max_routes=nr,
@@ -158,6 +159,7 @@ def sweep(st, stream, cfg):
     variants = [dict(tile=0, nt=0, unroll=1, blocks_per_cu=4), dict(tile=0, nt=0, unroll=1, blocks_per_cu=8),
                 dict(tile=0, nt=1, unroll=1, blocks_per_cu=4), dict(tile=0, nt=0, unroll=2, blocks_per_cu=4)]
     variants += [dict(tile=t, nt=0, unroll=1, blocks_per_cu=b) for t in (1, 2) for b in (2, 4, 8)]
+    variants += [dict(tile=3, nt=0, unroll=1, blocks_per_cu=b) for b in (2, 4, 8, 16)]
     for v in variants:
         cl.set_tuning(**v)
         for _ in range(3):
@@ -202,6 +204,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr + gpurun_out)")
+    ap.add_argument("--in-route-frac", type=float, default=0.9,
+                    help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
+    ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
     ap.add_argument("--unroll", type=int, default=None)
     ap.add_argument("--bpc", type=int, default=None)
@@ -211,13 +216,13 @@ def main():
     world, rank, local = setup_dist()
     dev = torch.device(f"cuda:{local}")
     t0 = time.time()
-    st = build_state(args.config, dev, rank, args.packets or None)
+    st = build_state(args.config, dev, rank, args.packets or None, args.in_route_frac)
     torch.cuda.synchronize()
     if rank == 0:
         log(f"[bench] setup {time.time() - t0:.1f}s: {st['desc']}")
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     stream = torch.cuda.current_stream(dev)
-    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc)
+    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 

@@ -418,6 +418,125 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Software-pipelined per-lane variant (any layout).  vmcnt retires loads in
+// issue order, so in every loop trip the loads go out oldest-dependency
+// first:  tbl8 of packet k-1 (its tbl24 entry arrived last trip), tbl24 of
+// packet k (its frame arrived last trip), then the frame of packet k+1.
+// Each wait therefore leaves the younger loads in flight: the frame stream
+// never stops while the FIB gathers resolve.  The tbl8 / tbl24 loads are
+// issued unconditionally (index 0 when unused) so no branch splits the
+// counter bookkeeping.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(FAST_THREADS) void k_classify_pipe(KArgs a)
+{
+    __shared__ uint32_t s_t[TAB4_POS * 256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB4_POS * 256; k += FAST_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += FAST_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint64_t step = (uint64_t)gridDim.x * FAST_THREADS;
+    uint64_t i = (uint64_t)blockIdx.x * FAST_THREADS + tid;
+    bool have_cur = i < a.n, have_prev = false;
+    FastHdr cur;
+    if (have_cur)
+        fast_load<false>(a, i, cur);
+    uint64_t ip = 0;
+    uint32_t e_prev = 0, lo_prev = 0, q_prev = 0;
+    bool is4_prev = false;
+    while (have_cur || have_prev) {
+        // (1) tbl8 of the previous packet (dir24_8.h:132-134)
+        uint32_t e8 = 0;
+        if (MODE == CNDP_MODE_L3FWD && have_prev)
+            e8 = a.tbl8[(e_prev & 1u) ? (e_prev >> 1) * 256u + lo_prev : 0u];
+        // (2) tbl24 of the current packet (dir24_8.h:131)
+        uint32_t e24 = 0, dip = 0;
+        bool is4 = false;
+        if (have_cur) {
+            is4 = bswap16(cur.w3 & 0xffffu) == 0x0800u;
+            dip = bswap32(alignb(cur.w8, cur.w7, 2));
+            if (MODE == CNDP_MODE_L3FWD)
+                e24 = a.tbl24[is4 ? dip >> 8 : 0u];
+        }
+        // (3) frame of the next packet
+        const uint64_t in = i + step;
+        const bool have_nxt = have_cur && in < a.n;
+        FastHdr nxt;
+        if (have_nxt)
+            fast_load<false>(a, in, nxt);
+        // (4) flow hash + RSS queue of the current packet
+        uint32_t q = 0;
+        if (have_cur) {
+            const uint32_t et = bswap16(cur.w3 & 0xffffu);
+            uint32_t hs = 0;
+            if (et == 0x0800u) {
+                const uint32_t ihl = (cur.w3 >> 16) & 0xfu;
+                const uint32_t proto = cur.w5 >> 24;
+                const uint32_t frag = bswap16(cur.w5 & 0xffffu) & 0x3fffu;
+                hs = tz4(s_t, 0, alignb(cur.w7, cur.w6, 2)) ^ tz4(s_t, 4, alignb(cur.w8, cur.w7, 2));
+                if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
+                    const uint32_t ports =
+                        ihl == 5 ? alignb(cur.w9, cur.w8, 2) : gld32(cur.p, cur.avail, 14 + 4 * ihl);
+                    hs ^= tz4(s_t, 8, ports);
+                }
+            } else if (et == 0x86DDu) {
+                const uint32_t nx = cur.w5 & 0xffu;
+                hs = hash_v6_global(cur.p, cur.avail, 14, nx == 6u || nx == 17u, a.ttab);
+            }
+            q = s_reta[hs & a.reta_mask];
+            if (a.hash)
+                a.hash[i] = hs;
+            if (a.queue)
+                a.queue[i] = (uint16_t)q;
+        }
+        // (5) next hop, edge and bin of the previous packet
+        if (have_prev) {
+            uint32_t nh = CNDP_NH_INVALID, edge;
+            if (MODE == CNDP_MODE_L3FWD) {
+                if (is4_prev)
+                    nh = ((e_prev & 1u) ? e8 : e_prev) >> 1;
+                edge = is4_prev ? ((nh >> 16) & 0xffu) : 0xFFu;
+            } else {
+                edge = 0;
+            }
+            if (a.nh)
+                a.nh[ip] = nh;
+            if (a.edge)
+                a.edge[ip] = (uint8_t)edge;
+            if (count)
+                atomicAdd(&s_bins[bin_of<MODE>(nh, edge, q_prev, a.n_bins)], 1u);
+        }
+        // (6) shift the pipeline
+        have_prev = have_cur;
+        ip = i;
+        e_prev = e24;
+        lo_prev = dip & 0xffu;
+        is4_prev = is4;
+        q_prev = q;
+        have_cur = have_nxt;
+        cur = nxt;
+        i = in;
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // cnet classify: eth_rx (cne_get_ptype) -> ptype -> ip4_input / ip6_input.
 // ---------------------------------------------------------------------------
@@ -1339,6 +1458,14 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
         const uint32_t cap = (uint32_t)c->num_cu * (uint32_t)c->tune_bpc;
         if (g > cap)
             g = cap;
+        if (c->tune_tile == 3) {
+            if (b->mode == CNDP_MODE_L3FWD)
+                hipLaunchKernelGGL(k_classify_pipe<CNDP_MODE_L3FWD>, dim3(g), dim3(FAST_THREADS), 0, s, a);
+            else
+                hipLaunchKernelGGL(k_classify_pipe<CNDP_MODE_HASH>, dim3(g), dim3(FAST_THREADS), 0, s, a);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
         // wave-tile path: packed 64-B slots, 16-B aligned, whole tiles in bounds
         const uint64_t n_tiles = b->n / 64u;
         const bool tile_ok = c->tune_tile && !b->offsets && b->stride == 64 &&
@@ -1530,7 +1657,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_bpc = value;
         return 0;
     case CNDP_TUNE_TILE:
-        if (value < 0 || value > 2)
+        if (value < 0 || value > 3)
             return -EINVAL;
         c->tune_tile = value;
         return 0;

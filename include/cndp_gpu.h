@@ -116,8 +116,9 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_NT            1 = non-temporal frame loads / output stores (default 0)
  *   CNDP_TUNE_UNROLL        packets per lane per loop trip, 1 or 2 (default 1)
  *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 4)
- *   CNDP_TUNE_TILE          wave-tile LDS staging for packed 64-B slots: 0 off, 1 prefetch
- *                           before the FIB gathers, 2 after them (default 1) */
+ *   CNDP_TUNE_TILE          l3fwd/hash kernel: 0 per-lane, 1 / 2 wave-tile LDS staging
+ *                           (packed 64-B slots; prefetch before / after the FIB gathers),
+ *                           3 software-pipelined per-lane (default 1) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3

@@ -90,7 +90,11 @@ def test_fuzz_frames_l3fwd(l3, gpu, mode):
     """Random frames (every ethertype / IHL / proto branch, ragged slab end)."""
     cl, fib, t4 = l3
     fr = pktgen.fuzz_frames(50000, seed=21, slot=96, device=gpu)
-    assert_same(run_gpu(cl, fr, mode), oracle_classify(mode, fr, tables4=t4))
+    ref = oracle_classify(mode, fr, tables4=t4)
+    for tile in (0, 3):
+        cl.set_tuning(tile=tile)
+        assert_same(run_gpu(cl, fr, mode), ref)
+    cl.set_tuning(tile=1)
 
 
 def test_fuzz_unaligned_offsets(l3, gpu):
@@ -256,7 +260,7 @@ def test_tuning_variants_identical(l3, gpu, mode):
                 for bpc in (1, 8, 16):
                     cl.set_tuning(tile=0, nt=nt, unroll=unroll, blocks_per_cu=bpc)
                     assert_same(run_gpu(cl, fr, mode), ref)
-        for tile in (1, 2):
+        for tile in (1, 2, 3):
             for bpc in (1, 2, 4, 16):
                 cl.set_tuning(tile=tile, blocks_per_cu=bpc)
                 assert_same(run_gpu(cl, fr, mode), ref)
@@ -270,7 +274,7 @@ def test_tile_path_ragged_and_offset(l3, gpu):
     n = 64 * 1000 + 37
     fr = pktgen.packed_ipv4(n + 1, routes=pktgen.l3fwd_routes(), device=gpu, seed=14)
     fr2 = pktgen.Frames(fr.slab, n, stride=64, data_off=16)
-    for tile in (0, 1, 2):
+    for tile in (0, 1, 2, 3):
         cl.set_tuning(tile=tile)
         assert_same(run_gpu(cl, fr2, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr2, tables4=t4))
     cl.set_tuning(tile=1)
