@@ -4,6 +4,7 @@
 //   copy     : float4 read+write of the slab size (calibration, like the guide's 6.29 TB/s)
 //   read     : tile-pattern read of 16M x 64-B slots, one u32 per wave written
 //   rw10     : tile read + 10 B/pkt SoA writes (u32, u32, u16) of values derived from the frames
+//   rw10lane : the same traffic with per-lane strided frame loads (bytes 0..39 of each slot)
 //   rw10lds  : rw10 with the frames staged through a swizzled LDS tile (the classify layout)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -38,8 +39,8 @@ __global__ __launch_bounds__(256) void k_tile(const uint8_t *slab, uint64_t n_ti
         }
         uint32_t w3, w5, w6, w7, w8;
         if (MODE == 1) {
-            // lane holds chunks of 4 different frames: use them as-is
-            w3 = r0.w; w5 = r1.y; w6 = r1.z; w7 = r1.w; w8 = r2.x;
+            // lane holds chunks of 4 different frames: use all of them (no dead loads)
+            w3 = r0.w ^ r3.x; w5 = r1.y ^ r3.y; w6 = r1.z ^ r3.z; w7 = r1.w ^ r3.w; w8 = r2.x;
         } else {
             const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
 #pragma unroll
