@@ -160,6 +160,9 @@ def sweep(st, stream, cfg):
                 dict(tile=0, nt=1, unroll=1, blocks_per_cu=4), dict(tile=0, nt=0, unroll=2, blocks_per_cu=4)]
     variants += [dict(tile=t, nt=0, unroll=1, blocks_per_cu=b) for t in (1, 2) for b in (2, 4, 8)]
     variants += [dict(tile=3, nt=0, unroll=1, blocks_per_cu=b) for b in (2, 4, 8, 16)]
+    variants = [dict(v, dir16=1) for v in variants] + [dict(v, dir16=0) for v in variants
+                                                       if v["tile"] in (0, 1) and v["nt"] == 0
+                                                       and v["unroll"] == 1 and v["blocks_per_cu"] == 4]
     for v in variants:
         cl.set_tuning(**v)
         for _ in range(3):
@@ -179,7 +182,7 @@ def sweep(st, stream, cfg):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=1, nt=0, unroll=1, blocks_per_cu=4)
+    cl.set_tuning(tile=1, nt=0, unroll=1, blocks_per_cu=4, dir16=1)
 
 
 def load_traffic(cfg: str):
@@ -207,6 +210,7 @@ def main():
     ap.add_argument("--in-route-frac", type=float, default=0.9,
                     help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
     ap.add_argument("--tile", type=int, default=None)
+    ap.add_argument("--dir16", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
     ap.add_argument("--unroll", type=int, default=None)
     ap.add_argument("--bpc", type=int, default=None)
@@ -222,7 +226,7 @@ def main():
         log(f"[bench] setup {time.time() - t0:.1f}s: {st['desc']}")
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     stream = torch.cuda.current_stream(dev)
-    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile)
+    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 

@@ -70,6 +70,19 @@ __device__ __forceinline__ uint32_t lpm4(const uint32_t *__restrict__ t24,
     return e >> 1;
 }
 
+// DIR-24-8 4B lookup through the /16 directory (same result as lpm4)
+__device__ __forceinline__ uint32_t lpm4d(const uint32_t *__restrict__ d16,
+                                          const uint32_t *__restrict__ pages,
+                                          const uint32_t *__restrict__ t8, uint32_t ip)
+{
+    uint32_t e = d16[ip >> 16];
+    if (e & 1u)
+        e = pages[(e >> 1) * 256u + ((ip >> 8) & 0xffu)];
+    if (e & 1u)
+        e = t8[(e >> 1) * 256u + (ip & 0xffu)];
+    return e >> 1;
+}
+
 // Toeplitz byte table access: T[b][v] at tab[b * 256 + v]
 __device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_t x)
 {
@@ -91,6 +104,8 @@ struct KArgs {
     const uint32_t *tbl8;
     const uint32_t *tbl24_6;
     const uint32_t *tbl8_6;
+    const uint32_t *dir16; // /16 directory (nullptr = plain tbl24 path)
+    const uint32_t *pages;
     const uint32_t *ttab; // 36 x 256 Toeplitz byte tables (global)
     const uint16_t *reta;
     uint32_t *nh;
@@ -219,7 +234,8 @@ __device__ __forceinline__ uint32_t fast_lpm(const KArgs &a, const FastHdr &h)
 {
     if (MODE != CNDP_MODE_L3FWD || bswap16(h.w3 & 0xffffu) != 0x0800u)
         return CNDP_NH_INVALID;
-    return lpm4(a.tbl24, a.tbl8, bswap32(alignb(h.w8, h.w7, 2)));
+    const uint32_t ip = bswap32(alignb(h.w8, h.w7, 2));
+    return a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, ip) : lpm4(a.tbl24, a.tbl8, ip);
 }
 
 template <int MODE, bool NT, bool PRE = false>
@@ -237,8 +253,8 @@ __device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const Fa
         const uint32_t frag = bswap16(h.w5 & 0xffffu) & 0x3fffu;
         const uint32_t src = alignb(h.w7, h.w6, 2);
         const uint32_t dst = alignb(h.w8, h.w7, 2);
-        if (MODE == CNDP_MODE_L3FWD && !PRE)
-            nh = lpm4(a.tbl24, a.tbl8, bswap32(dst)); // issue the gather first
+        if (MODE == CNDP_MODE_L3FWD && !PRE) // issue the gather first
+            nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, bswap32(dst)) : lpm4(a.tbl24, a.tbl8, bswap32(dst));
         hs = tz4(s_t, 0, src) ^ tz4(s_t, 4, dst);
         if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
             const uint32_t ports = ihl == 5 ? alignb(h.w9, h.w8, 2) : gld32(h.p, h.avail, 14 + 4 * ihl);
@@ -837,7 +853,7 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
             sum = (sum >> 16) + (sum & 0xffffu);
             const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
             const uint32_t dip = ok ? w.be32(ip + 16) : 0u;
-            nh = lpm4(a.tbl24, a.tbl8, dip);
+            nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, dip) : lpm4(a.tbl24, a.tbl8, dip);
             edge = nh >> 24;
         } else if (pe == 4u) {
             // ip6_input.c:115-135: payload_len < buf_len, else dip = ::
@@ -1075,6 +1091,7 @@ struct cndp_gpu_ctx {
     int tune_unroll;      // CNDP_TUNE_UNROLL
     int tune_bpc;         // CNDP_TUNE_BLOCKS_PER_CU
     int tune_tile;        // CNDP_TUNE_TILE
+    int tune_dir16;       // CNDP_TUNE_DIR16
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -1140,6 +1157,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_unroll = 1;
     c->tune_bpc = 4;
     c->tune_tile = 1;
+    c->tune_dir16 = 1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -1234,10 +1252,129 @@ extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
         hipFree(t->dev_tbl24);
     if (t->dev_tbl8)
         hipFree(t->dev_tbl8);
+    if (t->dev_dir16)
+        hipFree(t->dev_dir16);
+    if (t->dev_pages)
+        hipFree(t->dev_pages);
     hipSetDevice(cur);
+    t->dev_dir16 = t->dev_pages = nullptr;
+    t->dev_cap_pages = 0;
     t->dev_tbl24 = t->dev_tbl8 = nullptr;
     t->dev_id = -1;
     t->dev_groups = 0;
+}
+
+// ---- /16 directory maintenance (host) ---------------------------------------
+static int dir16_page_alloc(struct cndp_tbl *t)
+{
+    if (t->n_free)
+        return (int)t->page_free[--t->n_free];
+    if (t->page_hwm == t->cap_pages) {
+        const uint32_t ncap = t->cap_pages ? t->cap_pages * 2 : 64;
+        uint32_t *np = (uint32_t *)realloc(t->pages, (size_t)ncap * 256 * 4);
+        uint32_t *nf = (uint32_t *)realloc(t->page_free, (size_t)ncap * 4);
+        if (!np || !nf) {
+            if (np)
+                t->pages = np;
+            if (nf)
+                t->page_free = nf;
+            return -ENOMEM;
+        }
+        t->pages = np;
+        t->page_free = nf;
+        t->cap_pages = ncap;
+    }
+    return (int)t->page_hwm++;
+}
+
+// refresh the directory entries of /16 blocks [k0, k1]
+static int dir16_update(struct cndp_tbl *t, uint32_t k0, uint32_t k1)
+{
+    if (!t->dir16) {
+        t->dir16 = (uint32_t *)calloc(65536, 4);
+        t->page_of = (int32_t *)malloc(65536 * 4);
+        if (!t->dir16 || !t->page_of)
+            return -ENOMEM;
+        for (uint32_t k = 0; k < 65536; k++)
+            t->page_of[k] = -1;
+        k0 = 0;
+        k1 = 65535;
+        t->dd_lo = t->dp_lo = ~0ULL;
+        t->dd_hi = t->dp_hi = 0;
+    }
+    const uint32_t *t24 = (const uint32_t *)t->tbl24;
+    for (uint32_t k = k0; k <= k1; k++) {
+        const uint32_t *e = t24 + (size_t)k * 256;
+        const uint32_t v = e[0];
+        bool uni = !(v & 1u);
+        for (uint32_t b = 1; uni && b < 256; b++)
+            uni = e[b] == v;
+        uint32_t nd;
+        if (uni) {
+            if (t->page_of[k] >= 0) {
+                t->page_free[t->n_free++] = (uint32_t)t->page_of[k];
+                t->page_of[k] = -1;
+                t->n_pages_used--;
+            }
+            nd = v;
+        } else {
+            if (t->page_of[k] < 0) {
+                const int pg = dir16_page_alloc(t);
+                if (pg < 0)
+                    return pg;
+                t->page_of[k] = pg;
+                t->n_pages_used++;
+            }
+            const uint64_t pe = (uint64_t)t->page_of[k] * 256;
+            memcpy(t->pages + pe, e, 256 * 4);
+            if (pe < t->dp_lo)
+                t->dp_lo = pe;
+            if (pe + 256 > t->dp_hi)
+                t->dp_hi = pe + 256;
+            nd = ((uint32_t)t->page_of[k] << 1) | 1u;
+        }
+        if (t->dir16[k] != nd || t->dd_hi == 0) {
+            t->dir16[k] = nd;
+            if (k < t->dd_lo)
+                t->dd_lo = k;
+            if ((uint64_t)k + 1 > t->dd_hi)
+                t->dd_hi = (uint64_t)k + 1;
+        }
+    }
+    return 0;
+}
+
+static int dir16_sync(struct cndp_tbl *t, hipStream_t s, uint64_t d24_lo, uint64_t d24_hi)
+{
+    if (d24_hi > d24_lo || !t->dir16) {
+        int r = dir16_update(t, (uint32_t)(d24_lo >> 8), (uint32_t)((d24_hi ? d24_hi - 1 : 0) >> 8));
+        if (r)
+            return r;
+    }
+    if (!t->dev_dir16) {
+        HIP_TRY(hipMalloc(&t->dev_dir16, 65536 * 4));
+        t->dd_lo = 0;
+        t->dd_hi = 65536;
+    }
+    if (!t->dev_pages || t->dev_cap_pages < t->cap_pages) {
+        if (t->dev_pages)
+            HIP_TRY(hipFree(t->dev_pages));
+        t->dev_pages = nullptr;
+        const uint32_t cap = t->cap_pages > 64 ? t->cap_pages : 64;
+        HIP_TRY(hipMalloc(&t->dev_pages, (size_t)cap * 256 * 4));
+        t->dev_cap_pages = cap;
+        t->dp_lo = 0;
+        t->dp_hi = (uint64_t)t->page_hwm * 256;
+    }
+    if (t->dd_hi > t->dd_lo)
+        HIP_TRY(hipMemcpyAsync((uint32_t *)t->dev_dir16 + t->dd_lo, t->dir16 + t->dd_lo,
+                               (t->dd_hi - t->dd_lo) * 4, hipMemcpyHostToDevice, s));
+    if (t->dp_hi > t->dp_lo)
+        HIP_TRY(hipMemcpyAsync((uint32_t *)t->dev_pages + t->dp_lo, t->pages + t->dp_lo,
+                               (t->dp_hi - t->dp_lo) * 4, hipMemcpyHostToDevice, s));
+    t->dd_lo = t->dp_lo = ~0ULL;
+    t->dd_hi = t->dp_hi = 0;
+    return 0;
 }
 
 extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
@@ -1278,8 +1415,14 @@ extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
         HIP_TRY(hipMemcpyAsync((uint8_t *)t->dev_tbl8 + t->d8_lo * esz, t->tbl8 + t->d8_lo * esz,
                                (t->d8_hi - t->d8_lo) * esz, hipMemcpyHostToDevice, s));
     }
+    const bool dirty = t->d24_hi > t->d24_lo || t->d8_hi > t->d8_lo || !t->dev_dir16;
+    if (!t->is_trie && t->nh_sz == 2) {
+        int r = dir16_sync(t, s, t->d24_lo, t->d24_hi);
+        if (r)
+            return r;
+    }
     // the host image may change right after we return: finish the copies
-    if (t->d24_hi > t->d24_lo || t->d8_hi > t->d8_lo)
+    if (dirty)
         HIP_TRY(hipStreamSynchronize(s));
     t->d24_lo = t->d8_lo = ~0ULL;
     t->d24_hi = t->d8_hi = 0;
@@ -1433,6 +1576,10 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
     if (c->fib4) {
         a.tbl24 = (const uint32_t *)c->fib4->t.dev_tbl24;
         a.tbl8 = (const uint32_t *)c->fib4->t.dev_tbl8;
+        if (c->tune_dir16 && c->fib4->t.dev_dir16 && c->fib4->t.dev_pages) {
+            a.dir16 = (const uint32_t *)c->fib4->t.dev_dir16;
+            a.pages = (const uint32_t *)c->fib4->t.dev_pages;
+        }
     }
     if (c->fib6) {
         a.tbl24_6 = (const uint32_t *)c->fib6->t.dev_tbl24;
@@ -1660,6 +1807,9 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 3)
             return -EINVAL;
         c->tune_tile = value;
+        return 0;
+    case CNDP_TUNE_DIR16:
+        c->tune_dir16 = value ? 1 : 0;
         return 0;
     default:
         return -EINVAL;

@@ -126,6 +126,10 @@ static void tbl_fini(struct cndp_tbl *t)
     free(t->tbl24);
     free(t->tbl8);
     free(t->used);
+    free(t->dir16);
+    free(t->page_of);
+    free(t->pages);
+    free(t->page_free);
     memset(t, 0, sizeof(*t));
 }
 

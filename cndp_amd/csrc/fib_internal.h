@@ -41,6 +41,21 @@ struct cndp_tbl {
     void *dev_tbl24;
     void *dev_tbl8;
     uint32_t dev_groups; /* groups allocated on the device */
+    /* /16 directory in front of tbl24 (DIR-24-8 4-B images, device side):
+     * dir16[k] = tbl24 value shared by all 256 entries of /16 block k (bit0
+     * clear), or (page << 1) | 1 with pages[page*256 + b] = tbl24[k*256 + b].
+     * Built on the host at sync time from the dirty tbl24 range. */
+    uint32_t *dir16;     /* 65536 entries */
+    int32_t *page_of;    /* page id per /16 block, -1 = uniform */
+    uint32_t *pages;     /* cap_pages * 256 entries */
+    uint32_t cap_pages;
+    uint32_t *page_free;
+    uint32_t n_free, n_pages_used, page_hwm;
+    uint64_t dd_lo, dd_hi; /* dirty dir16 entries */
+    uint64_t dp_lo, dp_hi; /* dirty page entries */
+    void *dev_dir16;
+    void *dev_pages;
+    uint32_t dev_cap_pages;
 };
 
 struct cne_fib {

@@ -118,11 +118,14 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 4)
  *   CNDP_TUNE_TILE          l3fwd/hash kernel: 0 per-lane, 1 / 2 wave-tile LDS staging
  *                           (packed 64-B slots; prefetch before / after the FIB gathers),
- *                           3 software-pipelined per-lane (default 1) */
+ *                           3 software-pipelined per-lane (default 1)
+ *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
+ *                           kept in front of tbl24 (default 1) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
 #define CNDP_TUNE_TILE 4
+#define CNDP_TUNE_DIR16 5
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

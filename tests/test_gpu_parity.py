@@ -278,3 +278,57 @@ def test_tile_path_ragged_and_offset(l3, gpu):
         cl.set_tuning(tile=tile)
         assert_same(run_gpu(cl, fr2, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr2, tables4=t4))
     cl.set_tuning(tile=1)
+
+
+def test_dir16_on_off_identical(l3, cnet, gpu):
+    """The /16 directory in front of tbl24 changes no output bit (l3fwd + cnet)."""
+    cl, fib, t4 = l3
+    for frac in (0.0, 0.9):
+        fr = pktgen.packed_ipv4(200000, routes=pktgen.l3fwd_routes(), device=gpu, seed=31,
+                                in_route_frac=frac)
+        ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+        for d in (0, 1):
+            for tile in (0, 1, 3):
+                cl.set_tuning(dir16=d, tile=tile)
+                assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), ref)
+    cl.set_tuning(dir16=1, tile=1)
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = pktgen.imix(1 << 16, v4routes=routes, v6routes=v6, device=gpu, seed=5)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
+    for d in (0, 1):
+        ccl.set_tuning(dir16=d)
+        assert_same(run_gpu(ccl, fr, N.CNDP_MODE_CNET), ref)
+    ccl.set_tuning(dir16=1)
+
+
+def test_route_churn_between_batches(gpu):
+    """Routes added / deleted between classify calls: the mirror (tbl24, tbl8,
+    /16 directory and its pages) follows incrementally, results == oracle."""
+    from cndp_amd.classify import Classifier
+    from cndp_amd.fib import Fib
+    rng = np.random.default_rng(77)
+    fib = Fib("churn", N.CNE_FIB_DIR24_8, default_nh=1 << 16, max_routes=4096, nh_sz=N.CNE_FIB_DIR24_8_4B,
+              num_tbl8=512)
+    cl = Classifier(0)
+    cl.set_fib(fib)
+    live = {}
+    fr = pktgen.packed_ipv4(1 << 17, routes=pktgen.l3fwd_routes(), device=gpu, seed=8, in_route_frac=0.5)
+    for rnd_ in range(6):
+        for _ in range(150):
+            if live and rng.random() < 0.4:
+                key = list(live)[int(rng.integers(0, len(live)))]
+                assert fib.delete(*key) == 0
+                del live[key]
+            else:
+                d = int(rng.integers(8, 33))
+                base = (10 << 24) if rng.random() < 0.7 else int(rng.integers(0, 2**32))
+                ip = (base | int(rng.integers(0, 1 << 22))) & ((0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF)
+                nh = int(rng.integers(0, 64))
+                rc = fib.add(ip, d, nh)
+                if rc == 0:
+                    live[(ip, d)] = nh
+        vals = [(ip, d, nh) for (ip, d), nh in live.items()]
+        t4 = O.dir24_8_build(vals, 1 << 16, 4096)
+        for d16 in (1, 0):
+            cl.set_tuning(dir16=d16)
+            assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
