@@ -238,23 +238,19 @@ __device__ __forceinline__ uint32_t fast_lpm(const KArgs &a, const FastHdr &h)
     return a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, ip) : lpm4(a.tbl24, a.tbl8, ip);
 }
 
-template <int MODE, bool NT, bool PRE = false>
-__device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const FastHdr &h,
-                                            const uint32_t *s_t, const uint16_t *s_reta,
-                                            uint32_t *s_bins, bool count, uint32_t nh_pre = 0)
+// 5-tuple Toeplitz of one frame (build-defined: L4 tuple for TCP/UDP
+// non-fragments, else L3), tables T[b][v] in LDS for the IPv4 tuple
+template <int MODE>
+__device__ __forceinline__ uint32_t fast_hash(const KArgs &a, const FastHdr &h, const uint32_t *s_t)
 {
     const uint32_t et = bswap16(h.w3 & 0xffffu);
-    uint32_t hs = 0, nh = CNDP_NH_INVALID, edge;
-    if (PRE)
-        nh = nh_pre;
+    uint32_t hs = 0;
     if (et == 0x0800u) {
         const uint32_t ihl = (h.w3 >> 16) & 0xfu;
         const uint32_t proto = h.w5 >> 24;
         const uint32_t frag = bswap16(h.w5 & 0xffffu) & 0x3fffu;
         const uint32_t src = alignb(h.w7, h.w6, 2);
         const uint32_t dst = alignb(h.w8, h.w7, 2);
-        if (MODE == CNDP_MODE_L3FWD && !PRE) // issue the gather first
-            nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, bswap32(dst)) : lpm4(a.tbl24, a.tbl8, bswap32(dst));
         hs = tz4(s_t, 0, src) ^ tz4(s_t, 4, dst);
         if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
             const uint32_t ports = ihl == 5 ? alignb(h.w9, h.w8, 2) : gld32(h.p, h.avail, 14 + 4 * ihl);
@@ -264,6 +260,15 @@ __device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const Fa
         const uint32_t nx = h.w5 & 0xffu; // ip6 next header: frame byte 20
         hs = hash_v6_global(h.p, h.avail, 14, nx == 6u || nx == 17u, a.ttab);
     }
+    return hs;
+}
+
+// queue, bins and the output stores of one frame
+template <int MODE, bool NT>
+__device__ __forceinline__ void fast_emit(const KArgs &a, uint64_t i, uint32_t et, uint32_t nh, uint32_t hs,
+                                          const uint16_t *s_reta, uint32_t *s_bins, bool count)
+{
+    uint32_t edge;
     if (MODE == CNDP_MODE_HASH)
         edge = 0;
     else
@@ -279,6 +284,21 @@ __device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const Fa
         stg<NT>(a.edge + i, (uint8_t)edge);
     if (count)
         atomicAdd(&s_bins[bin_of<MODE>(nh, edge, q, a.n_bins)], 1u);
+}
+
+template <int MODE, bool NT, bool PRE = false>
+__device__ __forceinline__ void fast_finish(const KArgs &a, uint64_t i, const FastHdr &h,
+                                            const uint32_t *s_t, const uint16_t *s_reta,
+                                            uint32_t *s_bins, bool count, uint32_t nh_pre = 0)
+{
+    const uint32_t et = bswap16(h.w3 & 0xffffu);
+    uint32_t nh = PRE ? nh_pre : CNDP_NH_INVALID;
+    if (MODE == CNDP_MODE_L3FWD && !PRE && et == 0x0800u) { // issue the gather first
+        const uint32_t ip = bswap32(alignb(h.w8, h.w7, 2));
+        nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, ip) : lpm4(a.tbl24, a.tbl8, ip);
+    }
+    const uint32_t hs = fast_hash<MODE>(a, h, s_t);
+    fast_emit<MODE, NT>(a, i, et, nh, hs, s_reta, s_bins, count);
 }
 
 template <int MODE, bool NT, int U>
@@ -336,7 +356,7 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
 // ---------------------------------------------------------------------------
 #define TILE_WAVES (FAST_THREADS / 64)
 
-template <int MODE, int SCHED>
+template <int MODE, int SCHED, bool NTS>
 __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB4_POS * 256];
@@ -403,7 +423,55 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
         h.w8 = p2.x;
         h.w9 = p2.y;
         if (SCHED == 0) {
-            fast_finish<MODE, false>(a, i, h, s_t, s_reta, s_bins, count);
+            fast_finish<MODE, NTS>(a, i, h, s_t, s_reta, s_bins, count);
+        } else if (SCHED == 2) {
+            // first FIB gather (directory or tbl24) issued before the next
+            // tile's loads, the second after them: the wave waits for
+            // max(frame latency, both gathers) instead of their sum, and the
+            // Toeplitz work runs while all three are in flight.  Both the
+            // gather and the prefetch are unconditional (any ip indexes the
+            // directory / tbl24 in bounds; the last tile re-reads itself), so
+            // the compiler's in-order vmcnt bookkeeping can leave the prefetch
+            // in flight when it waits for the gather.  Frames needing global
+            // byte loads for the hash (IPv6, IPv4 options) are hashed after.
+            const uint32_t et = bswap16(h.w3 & 0xffffu);
+            const uint32_t dst = alignb(h.w8, h.w7, 2), ip = bswap32(dst);
+            uint32_t e = 0;
+            if (MODE == CNDP_MODE_L3FWD)
+                e = a.dir16 ? a.dir16[ip >> 16] : a.tbl24[ip >> 8];
+            {
+                const uint64_t tp = tn < n_tiles ? tn : t;
+                const u32x4 *g = (const u32x4 *)(base + tp * 4096u);
+                r0 = g[lane];
+                r1 = g[64 + lane];
+                r2 = g[128 + lane];
+                r3 = g[192 + lane];
+            }
+            uint32_t hs = 0;
+            bool slow = et == 0x86DDu;
+            if (et == 0x0800u) {
+                const uint32_t ihl = (h.w3 >> 16) & 0xfu;
+                const uint32_t proto = h.w5 >> 24;
+                const uint32_t frag = bswap16(h.w5 & 0xffffu) & 0x3fffu;
+                hs = tz4(s_t, 0, alignb(h.w7, h.w6, 2)) ^ tz4(s_t, 4, dst);
+                if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
+                    if (ihl == 5)
+                        hs ^= tz4(s_t, 8, alignb(h.w9, h.w8, 2));
+                    else
+                        slow = true;
+                }
+            }
+            uint32_t nh = CNDP_NH_INVALID;
+            if (MODE == CNDP_MODE_L3FWD && et == 0x0800u) {
+                if (a.dir16 && (e & 1u))
+                    e = a.pages[(e >> 1) * 256u + ((ip >> 8) & 0xffu)];
+                if (e & 1u)
+                    e = a.tbl8[(e >> 1) * 256u + (ip & 0xffu)];
+                nh = e >> 1;
+            }
+            if (slow)
+                hs = fast_hash<MODE>(a, h, s_t);
+            fast_emit<MODE, NTS>(a, i, et, nh, hs, s_reta, s_bins, count);
         } else {
             // finish the dependent tbl24 -> tbl8 gathers first: vmcnt drains in
             // issue order, so a prefetch issued before them would be waited for
@@ -415,7 +483,7 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
                 r2 = g[128 + lane];
                 r3 = g[192 + lane];
             }
-            fast_finish<MODE, false, true>(a, i, h, s_t, s_reta, s_bins, count, nh);
+            fast_finish<MODE, NTS, true>(a, i, h, s_t, s_reta, s_bins, count, nh);
         }
     }
     // ragged tail (frames past the last whole tile): per-lane path
@@ -1153,10 +1221,10 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     if (!c)
         return -ENOMEM;
     c->dev = device;
-    c->tune_nt = 0;
+    c->tune_nt = 1;
     c->tune_unroll = 1;
     c->tune_bpc = 4;
-    c->tune_tile = 1;
+    c->tune_tile = 4;
     c->tune_dir16 = 1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
@@ -1622,25 +1690,18 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
             uint32_t gt = (uint32_t)((n_tiles + TILE_WAVES - 1) / TILE_WAVES);
             if (gt > cap)
                 gt = cap;
-            const int tv = (b->mode == CNDP_MODE_L3FWD ? 0 : 2) | (c->tune_tile == 2 ? 1 : 0);
-            switch (tv) {
-            case 0:
-                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_L3FWD, 0>), dim3(gt), dim3(FAST_THREADS), 0, s,
-                                   a, n_tiles);
-                break;
-            case 1:
-                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_L3FWD, 1>), dim3(gt), dim3(FAST_THREADS), 0, s,
-                                   a, n_tiles);
-                break;
-            case 2:
-                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_HASH, 0>), dim3(gt), dim3(FAST_THREADS), 0, s,
-                                   a, n_tiles);
-                break;
-            default:
-                hipLaunchKernelGGL((k_classify_tile<CNDP_MODE_HASH, 1>), dim3(gt), dim3(FAST_THREADS), 0, s,
-                                   a, n_tiles);
-                break;
-            }
+            // tile 1: gathers then prefetch; 2: prefetch then gathers; 4: split
+            const int sched = c->tune_tile == 2 ? 0 : c->tune_tile == 4 ? 2 : 1;
+            typedef void (*tile_fn)(KArgs, uint64_t);
+            static const tile_fn fns[2][3][2] = {
+                {{k_classify_tile<CNDP_MODE_L3FWD, 0, false>, k_classify_tile<CNDP_MODE_L3FWD, 0, true>},
+                 {k_classify_tile<CNDP_MODE_L3FWD, 1, false>, k_classify_tile<CNDP_MODE_L3FWD, 1, true>},
+                 {k_classify_tile<CNDP_MODE_L3FWD, 2, false>, k_classify_tile<CNDP_MODE_L3FWD, 2, true>}},
+                {{k_classify_tile<CNDP_MODE_HASH, 0, false>, k_classify_tile<CNDP_MODE_HASH, 0, true>},
+                 {k_classify_tile<CNDP_MODE_HASH, 1, false>, k_classify_tile<CNDP_MODE_HASH, 1, true>},
+                 {k_classify_tile<CNDP_MODE_HASH, 2, false>, k_classify_tile<CNDP_MODE_HASH, 2, true>}}};
+            const tile_fn fn = fns[b->mode == CNDP_MODE_L3FWD ? 0 : 1][sched][c->tune_nt ? 1 : 0];
+            hipLaunchKernelGGL(fn, dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
             HIP_TRY(hipGetLastError());
             return 0;
         }
@@ -1804,7 +1865,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_bpc = value;
         return 0;
     case CNDP_TUNE_TILE:
-        if (value < 0 || value > 3)
+        if (value < 0 || value > 4)
             return -EINVAL;
         c->tune_tile = value;
         return 0;

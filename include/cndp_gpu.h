@@ -113,12 +113,15 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
                      void *stream);
 
 /* Kernel variant knobs (performance only; results never change):
- *   CNDP_TUNE_NT            1 = non-temporal frame loads / output stores (default 0)
+ *   CNDP_TUNE_NT            1 = non-temporal hint on the once-touched streams: frame loads
+ *                           and output stores (per-lane kernels), output stores only
+ *                           (wave-tile kernels) (default 1)
  *   CNDP_TUNE_UNROLL        packets per lane per loop trip, 1 or 2 (default 1)
  *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 4)
  *   CNDP_TUNE_TILE          l3fwd/hash kernel: 0 per-lane, 1 / 2 wave-tile LDS staging
  *                           (packed 64-B slots; prefetch before / after the FIB gathers),
- *                           3 software-pipelined per-lane (default 1)
+ *                           3 software-pipelined per-lane, 4 wave-tile with the next
+ *                           tile's loads issued between the two FIB gathers (default 4)
  *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
  *                           kept in front of tbl24 (default 1) */
 #define CNDP_TUNE_NT 1

@@ -94,7 +94,15 @@ def test_fuzz_frames_l3fwd(l3, gpu, mode):
     for tile in (0, 3):
         cl.set_tuning(tile=tile)
         assert_same(run_gpu(cl, fr, mode), ref)
-    cl.set_tuning(tile=1)
+    # packed 64-B slots: the wave-tile kernels, including their slow-hash
+    # paths (IPv6, IPv4 options read past the 48 staged bytes)
+    fr = pktgen.fuzz_frames(64 * 800 + 5, seed=22, slot=64, device=gpu)
+    ref = oracle_classify(mode, fr, tables4=t4)
+    for tile in (0, 1, 2, 3, 4):
+        for nt in (0, 1):
+            cl.set_tuning(tile=tile, nt=nt)
+            assert_same(run_gpu(cl, fr, mode), ref)
+    cl.set_tuning(tile=4, nt=1)
 
 
 def test_fuzz_unaligned_offsets(l3, gpu):
@@ -260,12 +268,13 @@ def test_tuning_variants_identical(l3, gpu, mode):
                 for bpc in (1, 8, 16):
                     cl.set_tuning(tile=0, nt=nt, unroll=unroll, blocks_per_cu=bpc)
                     assert_same(run_gpu(cl, fr, mode), ref)
-        for tile in (1, 2, 3):
+        for tile in (1, 2, 3, 4):
             for bpc in (1, 2, 4, 16):
-                cl.set_tuning(tile=tile, blocks_per_cu=bpc)
-                assert_same(run_gpu(cl, fr, mode), ref)
+                for nt in (0, 1):
+                    cl.set_tuning(tile=tile, blocks_per_cu=bpc, nt=nt)
+                    assert_same(run_gpu(cl, fr, mode), ref)
     finally:
-        cl.set_tuning(tile=1, nt=0, unroll=1, blocks_per_cu=4)
+        cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4)
 
 
 def test_tile_path_ragged_and_offset(l3, gpu):
@@ -274,10 +283,10 @@ def test_tile_path_ragged_and_offset(l3, gpu):
     n = 64 * 1000 + 37
     fr = pktgen.packed_ipv4(n + 1, routes=pktgen.l3fwd_routes(), device=gpu, seed=14)
     fr2 = pktgen.Frames(fr.slab, n, stride=64, data_off=16)
-    for tile in (0, 1, 2, 3):
+    for tile in (0, 1, 2, 3, 4):
         cl.set_tuning(tile=tile)
         assert_same(run_gpu(cl, fr2, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr2, tables4=t4))
-    cl.set_tuning(tile=1)
+    cl.set_tuning(tile=4)
 
 
 def test_dir16_on_off_identical(l3, cnet, gpu):
@@ -288,10 +297,10 @@ def test_dir16_on_off_identical(l3, cnet, gpu):
                                 in_route_frac=frac)
         ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
         for d in (0, 1):
-            for tile in (0, 1, 3):
+            for tile in (0, 1, 3, 4):
                 cl.set_tuning(dir16=d, tile=tile)
                 assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), ref)
-    cl.set_tuning(dir16=1, tile=1)
+    cl.set_tuning(dir16=1, tile=4)
     ccl, routes, v6, ct4, ct6 = cnet
     fr = pktgen.imix(1 << 16, v4routes=routes, v6routes=v6, device=gpu, seed=5)
     ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
