@@ -154,6 +154,7 @@ def cpu_baseline(state, budget_s: float = 10.0):
 
 def sweep(st, stream, cfg):
     """Kernel-variant sweep (performance only; every variant is parity-tested)."""
+    from cndp_amd import native as N
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     rows = []
     variants = [dict(tile=0, nt=0, unroll=1, blocks_per_cu=4), dict(tile=0, nt=1, unroll=1, blocks_per_cu=4),
@@ -161,6 +162,8 @@ def sweep(st, stream, cfg):
     variants += [dict(tile=t, nt=nt, unroll=1, blocks_per_cu=b) for t in (1, 4) for nt in (0, 1) for b in (2, 4, 8)]
     variants += [dict(tile=2, nt=1, unroll=1, blocks_per_cu=4), dict(tile=3, nt=0, unroll=1, blocks_per_cu=4)]
     variants = [dict(v, dir16=1) for v in variants] + [dict(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=0)]
+    if mode == N.CNDP_MODE_CNET:
+        variants = [dict(cnet_tile=ct, dir16=d) for ct in (1, 0) for d in (1, 0)]
     for v in variants:
         cl.set_tuning(**v)
         for _ in range(3):
@@ -180,7 +183,7 @@ def sweep(st, stream, cfg):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1)
+    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1)
 
 
 def load_traffic(cfg: str):

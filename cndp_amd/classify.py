@@ -53,11 +53,11 @@ class Classifier:
 
     def set_tuning(self, nt: int | None = None, unroll: int | None = None,
                    blocks_per_cu: int | None = None, tile: int | None = None,
-                   dir16: int | None = None):
+                   dir16: int | None = None, cnet_tile: int | None = None):
         """Kernel variant knobs (cndp_gpu_set_tuning); never change results."""
         for key, v in ((N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),
                        (N.CNDP_TUNE_BLOCKS_PER_CU, blocks_per_cu), (N.CNDP_TUNE_TILE, tile),
-                       (N.CNDP_TUNE_DIR16, dir16)):
+                       (N.CNDP_TUNE_DIR16, dir16), (N.CNDP_TUNE_CNET_TILE, cnet_tile)):
             if v is not None:
                 N.check(self._L.cndp_gpu_set_tuning(self.h, key, int(v)), "cndp_gpu_set_tuning")
 

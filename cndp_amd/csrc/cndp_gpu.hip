@@ -668,8 +668,41 @@ __device__ __forceinline__ bool v6_ext(uint32_t p)
     return p == 0u || p == 43u || p == 44u || p == 50u || p == 51u || p == 60u;
 }
 
+// The same 64-byte window held in a wave's swizzled LDS frame tile (the
+// layout k_classify_tile uses): dword d of frame slot f sits at
+// tile[(f*4 + ((d>>2) ^ ((f>>2)&3)))*4 + (d&3)].
+struct TWin {
+    const uint32_t *t; // wave tile, as dwords
+    uint32_t f4, sw;   // f*4, swizzle of frame slot f
+    const uint8_t *g;
+    uint64_t avail;
+    __device__ __forceinline__ uint32_t dw(uint32_t d) const
+    {
+        return t[((f4 + ((d >> 2) ^ sw)) << 2) | (d & 3u)];
+    }
+    __device__ __forceinline__ uint32_t ld32(uint32_t o) const
+    {
+        if (o + 4 <= 64) {
+            const uint32_t d = o >> 2;
+            const uint32_t lo = dw(d);
+            if ((o & 3u) == 0)
+                return lo;
+            return alignb(dw(d + 1), lo, o & 3u);
+        }
+        return gld32(g, avail, o);
+    }
+    __device__ __forceinline__ uint32_t b8(uint32_t o) const
+    {
+        return o < 64 ? (dw(o >> 2) >> ((o & 3u) * 8)) & 0xffu : gbyte(g, avail, o);
+    }
+    __device__ __forceinline__ uint32_t raw16(uint32_t o) const { return ld32(o) & 0xffffu; }
+    __device__ __forceinline__ uint32_t be16(uint32_t o) const { return bswap16(ld32(o) & 0xffffu); }
+    __device__ __forceinline__ uint32_t be32(uint32_t o) const { return bswap32(ld32(o)); }
+};
+
 // pktmbuf_ptype.c:426-468 (skip_ip6_ext); returns -1 past 5 headers
-__device__ int skip_v6_ext(const Win &w, uint32_t proto, uint32_t &off, int &frag)
+template <class W>
+__device__ int skip_v6_ext(const W &w, uint32_t proto, uint32_t &off, int &frag)
 {
     frag = 0;
     for (int i = 0; i < 5; i++) {
@@ -694,7 +727,8 @@ __device__ int skip_v6_ext(const Win &w, uint32_t proto, uint32_t &off, int &fra
 // cne_get_ptype, pktmbuf_ptype.c:472-744, all layers (CNE_PTYPE_ALL_MASK).
 // Only l2_len / l3_len are consumed downstream (eth_rx.c:56-60 + the input
 // nodes), so the inner-header lengths are not tracked; the ptype bits are.
-__device__ uint32_t get_ptype(const Win &w, Lens &ln)
+template <class W>
+__device__ uint32_t get_ptype(const W &w, Lens &ln)
 {
     uint32_t pt = 0x1u, off = 14, proto = w.raw16(12);
     int ret;
@@ -968,6 +1002,315 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// cnet classify, wave-tile form (default for CNDP_MODE_CNET).  Same outputs as
+// k_classify_cnet, restructured for latency:
+//  * a wave owns 64 consecutive packets; their 64-B windows are fetched 4
+//    lanes per frame (one 16-B load each, so a wave instruction covers 16
+//    whole windows) into the swizzled LDS tile, for any stride / offsets;
+//  * per tile: parse from LDS, issue the first FIB gather (/16 directory,
+//    tbl24 or IPv6 tbl24), then the next tile's window loads, then the
+//    Toeplitz hash from the LDS tables while both are in flight, then the
+//    rest of the gather chain;
+//  * IPv4 and IPv6 lanes share one hash loop and one gather-chain loop, so
+//    a mixed wave pays max(v4, v6) steps instead of their sum.
+// Frames that are not 16-B aligned or have < 64 bytes before the slab end
+// are staged with bounded byte loads (zero past the end), like Win.
+// ---------------------------------------------------------------------------
+#define CT_THREADS 512
+#define CT_WAVES (CT_THREADS / 64)
+
+// frame base (bytes from slab) of packet i, or ~0 when i >= n
+__device__ __forceinline__ uint64_t ct_base(const KArgs &a, uint64_t i, uint64_t off_i)
+{
+    if (i >= a.n)
+        return ~0ull;
+    return (a.offsets ? off_i : i * a.stride) + a.data_off;
+}
+
+__device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
+{
+    return base != ~0ull && base < a.slab_len && a.slab_len - base >= 64 &&
+           (((uintptr_t)a.slab + base) & 15u) == 0;
+}
+
+__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_classify_cnet_tile(KArgs a, uint64_t n_tiles)
+{
+    __shared__ uint32_t s_t[TAB_POS * 256];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint32_t *tdw = (const uint32_t *)tile;
+    const uint64_t wstep = (uint64_t)gridDim.x * CT_WAVES;
+    // quad lane geometry: in load k, this lane fetches part (lane&3) of frame
+    // slot 16k + lane/4, written to slot*4 + (part ^ swizzle(slot))
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+
+    uint64_t t = (uint64_t)blockIdx.x * CT_WAVES + wv;
+    // this lane's own frame offset, one tile ahead of the loads
+    uint64_t off_cur = 0, off_nxt = 0;
+    if (a.offsets) {
+        const uint64_t i0 = t * 64u + lane, i1 = (t + wstep) * 64u + lane;
+        off_cur = t < n_tiles && i0 < a.n ? a.offsets[i0] : 0;
+        off_nxt = t + wstep < n_tiles && i1 < a.n ? a.offsets[i1] : 0;
+    }
+    // frame bases of the 4 frames this lane loads parts of, and the loads
+    uint64_t qb[4];
+    u32x4 r[4];
+    {
+        const uint64_t my_base = ct_base(a, t * 64u + lane, off_cur);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            qb[k] = __shfl(my_base, 16 * k + (int)fr_in_k);
+            // frames off the fast path load a dummy chunk of the (aligned,
+            // 36 KiB) Toeplitz table instead, so every load is unconditional
+            const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u
+                                                   : (const uint8_t *)a.ttab + part * 16u;
+            r[k] = t < n_tiles ? *(const u32x4 *)src : (u32x4){0, 0, 0, 0};
+        }
+    }
+    for (; t < n_tiles; t += wstep) {
+        const uint64_t i = t * 64u + lane;
+        // (1) stage the tile: fast frames from the loads, others bounded
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t f = 16u * k + fr_in_k;
+            u32x4 v = r[k];
+            if (!ct_fast(a, qb[k])) {
+                v = (u32x4){0, 0, 0, 0};
+                if (qb[k] != ~0ull) {
+                    const uint8_t *p = a.slab + qb[k];
+                    const uint64_t avail = qb[k] < a.slab_len ? a.slab_len - qb[k] : 0;
+                    v.x = gld32(p, avail, part * 16u + 0);
+                    v.y = gld32(p, avail, part * 16u + 4);
+                    v.z = gld32(p, avail, part * 16u + 8);
+                    v.w = gld32(p, avail, part * 16u + 12);
+                }
+            }
+            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+
+        // (2) parse this lane's frame.  Fast path from 16 registers for the
+        // common shapes -- Ethernet + IPv4 IHL 5 unfragmented or IPv6 without
+        // extension headers, carrying TCP / UDP / SCTP -- where every field
+        // sits at a fixed offset inside the window; everything else runs the
+        // general cne_get_ptype restatement against the LDS window.
+        const bool live = i < a.n;
+        const uint64_t base = ct_base(a, i, off_cur);
+        const uint32_t sw = (lane >> 2) & 3u;
+        uint32_t W[16];
+        {
+            const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
+            const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
+            W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
+            W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
+            W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
+            W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
+        }
+        const uint32_t et = W[3] & 0xffffu;         // raw bytes 12..13
+        const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
+        const bool l4p4 = p4 == 6u || p4 == 17u || p4 == 132u, l4p6 = p6 == 6u || p6 == 17u || p6 == 132u;
+        const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
+                        ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
+        const bool f6 = et == BE16C(0x86DDu) && l4p6;
+        uint32_t pt = 0, l3len = 0, pe = 0;
+        uint32_t hw[9];      // Toeplitz input words, nw of them + the L4 word
+        uint32_t nw = 0, hl4 = 0;
+        uint32_t dip = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+        bool do4 = false, do6 = false;
+#pragma unroll
+        for (int k = 0; k < 9; k++)
+            hw[k] = 0;
+        if (live && (f4 || f6)) {
+            const uint32_t proto = f4 ? p4 : p6;
+            pt = (f4 ? 0x11u : 0x41u) | pt_l4(proto);
+            if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
+                const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
+                pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
+            }
+            pe = cnet_edge(pt);
+            const bool l4ok = proto == 6u || proto == 17u;
+            if (f4) {
+                l3len = 20;
+                nw = 2;
+                hw[0] = alignb(W[7], W[6], 2);
+                hw[1] = alignb(W[8], W[7], 2);
+                hl4 = l4ok ? alignb(W[9], W[8], 2) : 0u;
+                if (pe == 3u) { // ip4_input.c:121-140
+                    uint32_t sum = 0;
+#pragma unroll
+                    for (int k = 0; k < 5; k++) {
+                        const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
+                        sum += (x & 0xffffu) + (x >> 16);
+                    }
+                    sum = (sum >> 16) + (sum & 0xffffu);
+                    sum = (sum >> 16) + (sum & 0xffffu);
+                    const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
+                    dip = ok ? bswap32(hw[1]) : 0u;
+                    do4 = true;
+                }
+            } else {
+                l3len = 40;
+                nw = 8;
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    hw[k] = alignb(W[6 + k], W[5 + k], 2);
+                hl4 = l4ok ? alignb(W[14], W[13], 2) : 0u;
+                if (pe == 4u) { // ip6_input.c:115-135
+                    if (bswap16(W[4] >> 16) < a.buf_len) {
+                        d0 = hw[4];
+                        d1 = hw[5];
+                        d2 = hw[6];
+                        d3 = hw[7];
+                    }
+                    do6 = true;
+                }
+            }
+            if (!l4ok)
+                hl4 = 0;
+            (void)l3len;
+        } else if (live) {
+            const TWin w{tdw, lane * 4u, sw, a.slab + base, base < a.slab_len ? a.slab_len - base : 0};
+            Lens ln{14u, 0u};
+            pt = get_ptype(w, ln);
+            const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
+            const uint32_t ip = ln.l2;
+            const bool l4ok = l4t == 0x100u || l4t == 0x200u;
+            pe = cnet_edge(pt);
+            if (l3 != 0u && !(l3 & 0x40u)) {
+                nw = 2;
+                hw[0] = w.ld32(ip + 12);
+                hw[1] = w.ld32(ip + 16);
+            } else if (l3 & 0x40u) {
+                nw = 8;
+                for (uint32_t k = 0; k < 8; k++)
+                    hw[k] = w.ld32(ip + 8 + 4 * k);
+            }
+            hl4 = nw && l4ok ? w.ld32(ip + ln.l3) : 0u;
+            if (pe == 3u) {
+                const uint32_t x0 = w.ld32(ip);
+                const uint32_t hl = x0 & 0xfu;
+                uint32_t sum = 0;
+                for (uint32_t k = 0; k < hl; k++) {
+                    const uint32_t x = k == 0 ? x0 : w.ld32(ip + 4 * k);
+                    sum += (x & 0xffffu) + (x >> 16);
+                }
+                sum = (sum >> 16) + (sum & 0xffffu);
+                sum = (sum >> 16) + (sum & 0xffffu);
+                const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
+                dip = ok ? w.be32(ip + 16) : 0u;
+                do4 = true;
+            } else if (pe == 4u) {
+                if (w.be16(ip + 4) < a.buf_len) {
+                    d0 = w.ld32(ip + 24);
+                    d1 = w.ld32(ip + 28);
+                    d2 = w.ld32(ip + 32);
+                    d3 = w.ld32(ip + 36);
+                }
+                do6 = true;
+            }
+        }
+        // (3) first FIB gather, unconditional (every lane indexes in bounds)
+        const uint32_t *tb0;
+        uint32_t idx0;
+        if (!do4) {
+            tb0 = a.tbl24_6;
+            idx0 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu); // trie.h:126
+        } else if (a.dir16) {
+            tb0 = a.dir16;
+            idx0 = dip >> 16;
+        } else {
+            tb0 = a.tbl24;
+            idx0 = dip >> 8;
+        }
+        uint32_t e = tb0[idx0];
+        // (4) next tile's window loads (and the offsets one tile further)
+        const uint64_t tn = t + wstep;
+        {
+            const uint64_t nb = ct_base(a, tn * 64u + lane, off_nxt);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                qb[k] = __shfl(nb, 16 * k + (int)fr_in_k);
+                const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u
+                                                       : (const uint8_t *)a.ttab + part * 16u;
+                r[k] = *(const u32x4 *)src;
+            }
+            off_cur = off_nxt;
+            if (a.offsets) {
+                const uint64_t i2 = (tn + wstep) * 64u + lane;
+                off_nxt = tn + wstep < n_tiles && i2 < a.n ? a.offsets[i2] : 0;
+            }
+        }
+        // (5) Toeplitz over the nw address words, then the L4 word
+        uint32_t h = 0;
+        for (uint32_t k = 0; k < 8; k++)
+            if (k < nw)
+                h ^= tz4(s_t, 4 * k, hw[k]);
+        if (nw && hl4 != 0u)
+            h ^= tz4(s_t, 4 * nw, hl4);
+        // (6) rest of the chain: v4 page / tbl8, v6 tbl8 levels (trie.h:127-134)
+        uint32_t j = do6 ? 3u : (a.dir16 ? 1u : 2u);
+        bool more = (do4 || do6) && (e & 1u);
+        while (__any(more)) {
+            if (more) {
+                uint32_t byte;
+                const uint32_t *tb;
+                if (do6) {
+                    const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
+                    byte = (wd >> ((j & 3u) * 8)) & 0xffu;
+                    tb = a.tbl8_6;
+                } else {
+                    byte = j == 1 ? (dip >> 8) & 0xffu : dip & 0xffu;
+                    tb = j == 1 ? a.pages : a.tbl8;
+                }
+                e = tb[(e >> 1) * 256u + byte];
+                j++;
+                more = (e & 1u) && (do6 ? j < 16 : j <= 2);
+            }
+        }
+        uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
+        if (do4 || do6) {
+            nh = e >> 1;
+            edge = nh >> 24;
+        }
+        __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
+        if (live) {
+            const uint32_t q = s_reta[h & a.reta_mask];
+            if (a.nh)
+                a.nh[i] = nh;
+            if (a.hash)
+                a.hash[i] = h;
+            if (a.queue)
+                a.queue[i] = (uint16_t)q;
+            if (a.edge)
+                a.edge[i] = (uint8_t)edge;
+            if (count)
+                atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
+        }
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // bulk lookups (cne_fib_lookup_bulk / cne_fib6_lookup_bulk semantics)
 // ---------------------------------------------------------------------------
 template <typename E>
@@ -1160,6 +1503,7 @@ struct cndp_gpu_ctx {
     int tune_bpc;         // CNDP_TUNE_BLOCKS_PER_CU
     int tune_tile;        // CNDP_TUNE_TILE
     int tune_dir16;       // CNDP_TUNE_DIR16
+    int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -1226,6 +1570,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_bpc = 4;
     c->tune_tile = 4;
     c->tune_dir16 = 1;
+    c->tune_cnet_tile = 1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -1667,7 +2012,15 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
         const uint32_t cap = (uint32_t)c->num_cu * 2u;
         if (g > cap)
             g = cap;
-        hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
+        if (c->tune_cnet_tile) {
+            const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
+            uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
+            if (gt > cap)
+                gt = cap;
+            hipLaunchKernelGGL(k_classify_cnet_tile, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+        } else {
+            hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
+        }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
         const uint32_t cap = (uint32_t)c->num_cu * (uint32_t)c->tune_bpc;
@@ -1871,6 +2224,9 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return 0;
     case CNDP_TUNE_DIR16:
         c->tune_dir16 = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_CNET_TILE:
+        c->tune_cnet_tile = value ? 1 : 0;
         return 0;
     default:
         return -EINVAL;

@@ -33,6 +33,7 @@ CNDP_RSS_KEY_LEN = 40
 CNDP_RETA_MAX = 512
 CNDP_BINS_MAX = 1024
 CNDP_TUNE_NT, CNDP_TUNE_UNROLL, CNDP_TUNE_BLOCKS_PER_CU, CNDP_TUNE_TILE, CNDP_TUNE_DIR16 = 1, 2, 3, 4, 5
+CNDP_TUNE_CNET_TILE = 6
 
 # l3fwd edges (node_ip4_api.h:28-34) and cnet edges (ip4_input_priv.h:26-31)
 IP4_LOOKUP_NEXT_REWRITE, IP4_LOOKUP_NEXT_PKT_DROP = 0, 1

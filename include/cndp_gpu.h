@@ -123,12 +123,15 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           3 software-pipelined per-lane, 4 wave-tile with the next
  *                           tile's loads issued between the two FIB gathers (default 4)
  *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
- *                           kept in front of tbl24 (default 1) */
+ *                           kept in front of tbl24 (default 1)
+ *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = wave-tile staging with the next tile's loads
+ *                           overlapping the FIB gathers (default), 0 = per-lane rows */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
 #define CNDP_TUNE_TILE 4
 #define CNDP_TUNE_DIR16 5
+#define CNDP_TUNE_CNET_TILE 6
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

@@ -17,6 +17,7 @@ from helpers import (CNET_DEF, L3FWD_DEF, assert_same, cnet_fibs, l3fwd_fib, l3f
                      oracle_classify)
 
 pytestmark = pytest.mark.gpu
+CNET_KERNELS = (0, 1)  # per-lane rows, wave tile (default, set last)
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
@@ -116,9 +117,10 @@ def test_fuzz_unaligned_offsets(l3, gpu):
 def test_cnet_imix_c4_parity(cnet, gpu):
     cl, routes, v6, t4, t6 = cnet
     fr = pktgen.imix(1 << 18, v4routes=routes, v6routes=v6, device=gpu)
-    got = run_gpu(cl, fr, N.CNDP_MODE_CNET)
     ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
-    assert_same(got, ref)
+    for ct in CNET_KERNELS:
+        cl.set_tuning(cnet_tile=ct)
+        assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
     # both families forwarded somewhere
     assert (ref["edge"] == 1).mean() > 0.5
 
@@ -128,7 +130,19 @@ def test_cnet_fuzz_parity(cnet, gpu):
     cl, routes, v6, t4, t6 = cnet
     for seed in (1, 2, 3):
         fr = pktgen.fuzz_frames(40000, seed=seed, slot=128, device=gpu)
-        assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6))
+        ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+        for ct in CNET_KERNELS:
+            cl.set_tuning(cnet_tile=ct)
+            assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
+    # 64-B slots (windows reach into the next frame), unaligned frames, ragged ends
+    for slot, doff, n in ((64, 0, 64 * 300 + 7), (97, 3, 20001), (128, 16, 63), (80, 0, 1)):
+        fr = pktgen.fuzz_frames(n, seed=slot, slot=slot, device=gpu)
+        fr.data_off = doff
+        ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+        for ct in CNET_KERNELS:
+            cl.set_tuning(cnet_tile=ct)
+            assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
+    cl.set_tuning(cnet_tile=1)
 
 
 def test_cnet_c5_checksum_verify(cnet, gpu):
@@ -137,18 +151,20 @@ def test_cnet_c5_checksum_verify(cnet, gpu):
     fr = pktgen.packed_ipv4(1 << 17, slot=1536, frame_len=1500, routes=routes, device=gpu)
     bad = pktgen.corrupt_cksum(fr, 1024)
     assert bad > 50
-    got = run_gpu(cl, fr, N.CNDP_MODE_CNET)
     ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
-    assert_same(got, ref)
+    for ct in CNET_KERNELS:
+        cl.set_tuning(cnet_tile=ct)
+        assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
 
 
 def test_cnet_buf_len_check(cnet, gpu):
     """total_length >= buf_len sends the packet to the lookup of 0.0.0.0."""
     cl, routes, v6, t4, t6 = cnet
     fr = pktgen.packed_ipv4(4096, slot=1536, frame_len=1500, routes=routes, device=gpu)
-    got = run_gpu(cl, fr, N.CNDP_MODE_CNET, buf_len=1000)
     ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6, buf_len=1000)
-    assert_same(got, ref)
+    for ct in CNET_KERNELS:
+        cl.set_tuning(cnet_tile=ct)
+        assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET, buf_len=1000), ref)
 
 
 def test_empty_and_single(l3, gpu):
