@@ -186,6 +186,61 @@ def sweep(st, stream, cfg):
     cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1)
 
 
+def e2e_host(st, reps: int = 5):
+    """Host-memory rates (rank 0, N=1): the frames start in host memory and
+    the results end there (SURVEY §8(d) 'End to end').  Two paths, same
+    kernel, same batch:
+      pinned_stream : pinned host slab -> cndp_gpu_classify_host (64 MiB
+                      H2D segments overlapped with classify and D2H of the
+                      results, three streams) -> pinned host results;
+      zero_copy     : the slab registered in place (cndp_gpu_host_register,
+                      as an AF_XDP UMEM would be) and read by the kernel over
+                      PCIe; results to HBM."""
+    import mmap
+    fr, cl, mode, n = st["frames"], st["cl"], st["mode"], st["n"]
+    res = {}
+    host = fr.slab.cpu().pin_memory()
+    offs = fr.offsets.cpu().pin_memory() if fr.offsets is not None else None
+    out = {k: torch.zeros(n, dtype=d).pin_memory() for k, d in
+           (("nh", torch.int32), ("hash", torch.int32), ("queue", torch.int16))}
+    if mode == 1:
+        out["edge"] = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    out["bins"] = torch.zeros(66, dtype=torch.int64).pin_memory()
+    kw = dict(stride=fr.stride, offsets=offs, data_off=fr.data_off, out=out)
+    cl.classify_host(host, n, mode, **kw)
+    t = time.perf_counter()
+    for _ in range(reps):
+        cl.classify_host(host, n, mode, **kw)
+    dt = (time.perf_counter() - t) / reps
+    in_bytes = host.numel() + (n * 8 if offs is not None else 0)
+    res["pinned_stream"] = {"Mpps": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 3),
+                            "h2d_bytes": in_bytes, "h2d_GBs": round(in_bytes / dt / 1e9, 1)}
+    del host, offs, out
+    # zero-copy from a registered, page-aligned buffer
+    buf = mmap.mmap(-1, fr.slab.numel())
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    arr[:] = fr.slab.cpu().numpy()
+    dptr = cl.host_register(arr)
+    try:
+        dout = cl.alloc_outputs(n, 64, device=fr.slab.device, edge=mode == 1)
+        offs_d = fr.offsets.data_ptr() if fr.offsets is not None else None
+        args = (mode, n, dptr, arr.nbytes, dout)
+        kw = dict(stride=fr.stride, data_off=fr.data_off, offsets=offs_d)
+        cl.classify_ptrs(*args, **kw)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            cl.classify_ptrs(*args, **kw)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / reps
+        res["zero_copy"] = {"Mpps": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 3)}
+    finally:
+        cl.host_unregister(arr)
+        del arr
+        buf.close()
+    return res
+
+
 def load_traffic(cfg: str):
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
@@ -207,6 +262,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) rates")
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr + gpurun_out)")
     ap.add_argument("--in-route-frac", type=float, default=0.9,
                     help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
@@ -270,8 +326,13 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
             cpu = cpu_baseline(st, args.cpu_budget)
-        elif world == 1 and not args.no_cpu_baseline:
-            cpu = None
+        e2e = None
+        if world == 1 and not args.no_e2e:
+            try:
+                e2e = e2e_host(st)
+                log(f"[bench] host-memory rates: {e2e}")
+            except Exception as ex:  # reported, never fatal for the headline line
+                e2e = {"error": repr(ex)}
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -298,6 +359,7 @@ def main():
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_pkt": st["algo"]},
             "cpu_baseline": cpu,
+            "host_memory_e2e": e2e,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -53,11 +53,13 @@ class Classifier:
 
     def set_tuning(self, nt: int | None = None, unroll: int | None = None,
                    blocks_per_cu: int | None = None, tile: int | None = None,
-                   dir16: int | None = None, cnet_tile: int | None = None):
+                   dir16: int | None = None, cnet_tile: int | None = None,
+                   host_chunk: int | None = None):
         """Kernel variant knobs (cndp_gpu_set_tuning); never change results."""
         for key, v in ((N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),
                        (N.CNDP_TUNE_BLOCKS_PER_CU, blocks_per_cu), (N.CNDP_TUNE_TILE, tile),
-                       (N.CNDP_TUNE_DIR16, dir16), (N.CNDP_TUNE_CNET_TILE, cnet_tile)):
+                       (N.CNDP_TUNE_DIR16, dir16), (N.CNDP_TUNE_CNET_TILE, cnet_tile),
+                       (N.CNDP_TUNE_HOST_CHUNK, host_chunk)):
             if v is not None:
                 N.check(self._L.cndp_gpu_set_tuning(self.h, key, int(v)), "cndp_gpu_set_tuning")
 
@@ -114,20 +116,66 @@ class Classifier:
         N.check(self._L.cndp_gpu_classify(self.h, ctypes.byref(b), stream or None), "cndp_gpu_classify")
         return out
 
-    def classify_host(self, slab: np.ndarray, n: int, mode: int, stride: int = 64, offsets=None,
-                      data_off: int = 0, buf_len: int = 1984, n_bins: int = 64) -> dict:
-        """Host buffers in, host results out (H2D + kernel + D2H, PCIe-bound)."""
-        slab = np.ascontiguousarray(slab, dtype=np.uint8)
-        out = {"nh": np.zeros(n, np.uint32), "hash": np.zeros(n, np.uint32),
-               "queue": np.zeros(n, np.uint16), "edge": np.zeros(n, np.uint8),
-               "bins": np.zeros(n_bins + 2, np.uint64)}
-        off = np.ascontiguousarray(offsets, dtype=np.uint64) if offsets is not None else None
+    @staticmethod
+    def _hptr(x):
+        """Address of a host buffer (numpy array or CPU torch tensor)."""
+        if x is None:
+            return None
+        if isinstance(x, np.ndarray):
+            return x.ctypes.data
+        return x.data_ptr()
+
+    def classify_host(self, slab, n: int, mode: int, stride: int = 64, offsets=None,
+                      data_off: int = 0, buf_len: int = 1984, n_bins: int = 64, out: dict | None = None,
+                      slab_len: int | None = None) -> dict:
+        """Host buffers in, host results out (streamed H2D / classify / D2H,
+        PCIe-bound).  `slab`, `offsets` and the arrays of `out` may be numpy
+        arrays or CPU torch tensors (pinned ones give full DMA rate)."""
+        if isinstance(slab, np.ndarray):
+            slab = np.ascontiguousarray(slab, dtype=np.uint8)
+            nbytes = slab.nbytes
+        else:
+            nbytes = slab.numel() * slab.element_size()
+        if out is None:
+            out = {"nh": np.zeros(n, np.uint32), "hash": np.zeros(n, np.uint32),
+                   "queue": np.zeros(n, np.uint16), "edge": np.zeros(n, np.uint8),
+                   "bins": np.zeros(n_bins + 2, np.uint64)}
+        if offsets is not None and isinstance(offsets, np.ndarray):
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         b = N.Batch()
-        b.mode, b.n, b.slab, b.slab_len = mode, n, slab.ctypes.data, slab.nbytes
-        b.stride, b.offsets, b.data_off, b.buf_len = stride, off.ctypes.data if off is not None else None, data_off, buf_len
-        b.nh, b.hash, b.queue = out["nh"].ctypes.data, out["hash"].ctypes.data, out["queue"].ctypes.data
-        b.edge, b.bins, b.n_bins = out["edge"].ctypes.data, out["bins"].ctypes.data, n_bins
+        b.mode, b.n, b.slab = mode, n, self._hptr(slab)
+        b.slab_len = nbytes if slab_len is None else slab_len
+        b.stride, b.offsets, b.data_off, b.buf_len = stride, self._hptr(offsets), data_off, buf_len
+        b.nh, b.hash, b.queue = self._hptr(out.get("nh")), self._hptr(out.get("hash")), self._hptr(out.get("queue"))
+        b.edge, b.bins, b.n_bins = self._hptr(out.get("edge")), self._hptr(out.get("bins")), n_bins
         N.check(self._L.cndp_gpu_classify_host(self.h, ctypes.byref(b)), "cndp_gpu_classify_host")
+        return out
+
+    def host_register(self, buf) -> int:
+        """Pin + map a host buffer; returns its device address (zero-copy)."""
+        d = ctypes.c_void_p()
+        size = buf.nbytes if isinstance(buf, np.ndarray) else buf.numel() * buf.element_size()
+        N.check(self._L.cndp_gpu_host_register(self.h, self._hptr(buf), size, ctypes.byref(d)),
+                "cndp_gpu_host_register")
+        return d.value
+
+    def host_unregister(self, buf):
+        N.check(self._L.cndp_gpu_host_unregister(self.h, self._hptr(buf)), "cndp_gpu_host_unregister")
+
+    def classify_ptrs(self, mode: int, n: int, slab: int, slab_len: int, out: dict, stride: int = 64,
+                      data_off: int = 0, offsets: int | None = None, buf_len: int = 1984,
+                      n_bins: int = 64, stream: int | None = None):
+        """cndp_gpu_classify on raw device-visible addresses (e.g. a
+        host_register'd UMEM): outputs are torch device tensors."""
+        import torch
+        b = N.Batch()
+        b.mode, b.n, b.slab, b.slab_len = mode, n, slab, slab_len
+        b.stride, b.offsets, b.data_off, b.buf_len = stride, offsets, data_off, buf_len
+        b.nh, b.hash, b.queue = self._ptr(out.get("nh")), self._ptr(out.get("hash")), self._ptr(out.get("queue"))
+        b.edge, b.bins, b.n_bins = self._ptr(out.get("edge")), self._ptr(out.get("bins")), n_bins
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        N.check(self._L.cndp_gpu_classify(self.h, ctypes.byref(b), stream or None), "cndp_gpu_classify")
         return out
 
     def bin_partition(self, bin_of, n_bins: int, stream: int | None = None):

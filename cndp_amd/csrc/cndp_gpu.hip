@@ -1504,6 +1504,19 @@ struct cndp_gpu_ctx {
     int tune_tile;        // CNDP_TUNE_TILE
     int tune_dir16;       // CNDP_TUNE_DIR16
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
+    uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
+    // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
+    hipStream_t hs[3];    // copy-in, classify, copy-out
+    uint8_t *h_slab;      // device mirror of the host slab (same byte offsets)
+    uint64_t h_slab_cap;
+    uint64_t *h_off;
+    uint64_t h_off_cap;
+    uint8_t *h_out;       // nh | hash | queue | edge | bins
+    uint64_t h_out_cap;
+    // mbuf shim staging: pinned host windows / results and their device twins
+    uint8_t *m_hwin, *m_dwin;
+    uint32_t *m_hres, *m_dres; // nh[cap] | hash[cap]
+    uint32_t m_cap;
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -1571,6 +1584,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_tile = 4;
     c->tune_dir16 = 1;
     c->tune_cnet_tile = 1;
+    c->host_chunk = 1u << 20;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -1595,6 +1609,23 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
     if (!c)
         return;
     hipSetDevice(c->dev);
+    for (int k = 0; k < 3; k++)
+        if (c->hs[k])
+            hipStreamDestroy(c->hs[k]);
+    if (c->h_slab)
+        hipFree(c->h_slab);
+    if (c->h_off)
+        hipFree(c->h_off);
+    if (c->h_out)
+        hipFree(c->h_out);
+    if (c->m_hwin)
+        hipHostFree(c->m_hwin);
+    if (c->m_hres)
+        hipHostFree(c->m_hres);
+    if (c->m_dwin)
+        hipFree(c->m_dwin);
+    if (c->m_dres)
+        hipFree(c->m_dres);
     if (c->d_ttab)
         hipFree(c->d_ttab);
     if (c->d_reta)
@@ -2077,6 +2108,33 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
     return 0;
 }
 
+// grow a device buffer to at least `need` bytes (contents not kept)
+static int grow(void **buf, uint64_t *cap, uint64_t need)
+{
+    if (*cap >= need && *buf)
+        return 0;
+    if (*buf)
+        HIP_TRY(hipFree(*buf));
+    *buf = nullptr;
+    *cap = 0;
+    const uint64_t sz = need + (need >> 3) + 4096;
+    HIP_TRY(hipMalloc(buf, sz));
+    *cap = sz;
+    return 0;
+}
+
+// Host-memory batch (AF_XDP UMEM / loopback socket buffers).  The slab is
+// mirrored into device memory at the same byte offsets, streamed in 64 MiB
+// segments in byte order on the copy-in stream; packet chunk k is classified
+// on the compute stream as soon as every segment it can read has landed --
+// its frame bases plus CNDP_HOST_REACH bytes, the farthest any parse reads
+// (Ethernet + 2 VLAN tags + IPv4 options + tunnel + inner headers + 5 IPv6
+// extension headers of at most 2 KiB each) -- and its results go back on the
+// copy-out stream.  The kernel therefore sees exactly the bytes the device-
+// resident path sees: results are identical to cndp_gpu_classify.
+#define CNDP_HOST_SEG (64ull << 20)
+#define CNDP_HOST_REACH (16ull << 10)
+
 extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch *hb)
 {
     int r = validate_batch(c, hb);
@@ -2084,63 +2142,253 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
         return r;
     if ((r = set_device(c->dev)))
         return r;
-    struct cndp_batch db = *hb;
     const uint64_t n = hb->n;
-    void *d_slab = nullptr, *d_off = nullptr, *d_out = nullptr;
-    const size_t o_nh = 0, o_hash = o_nh + n * 4, o_q = o_hash + n * 4, o_e = o_q + ((n * 2 + 15) & ~15ull),
-                 o_b = o_e + ((n + 15) & ~15ull), out_bytes = o_b + ((uint64_t)hb->n_bins + 2) * 8;
-    hipStream_t s = nullptr;
+    const uint64_t o_nh = 0, o_hash = o_nh + n * 4, o_q = o_hash + n * 4, o_e = o_q + ((n * 2 + 15) & ~15ull),
+                   o_b = o_e + ((n + 15) & ~15ull), out_bytes = o_b + ((uint64_t)hb->n_bins + 2) * 8;
+    for (int k = 0; k < 3; k++)
+        if (!c->hs[k])
+            HIP_TRY(hipStreamCreateWithFlags(&c->hs[k], hipStreamNonBlocking));
+    hipStream_t cs = c->hs[0], ks = c->hs[1], ds = c->hs[2];
+    if ((r = grow((void **)&c->h_slab, &c->h_slab_cap, hb->slab_len ? hb->slab_len : 1)) ||
+        (r = grow((void **)&c->h_out, &c->h_out_cap, out_bytes)) ||
+        (hb->offsets && (r = grow((void **)&c->h_off, &c->h_off_cap, n * 8 + 8))))
+        return r;
+    uint64_t *d_bins = hb->bins ? (uint64_t *)(c->h_out + o_b) : nullptr;
+    if (hb->bins)
+        HIP_TRY(hipMemcpyAsync(d_bins, hb->bins, ((uint64_t)hb->n_bins + 2) * 8, hipMemcpyHostToDevice, cs));
+    const uint64_t C = c->host_chunk;
+    const uint64_t n_chunks = n ? (n + C - 1) / C : 0;
+    const uint64_t n_segs = (hb->slab_len + CNDP_HOST_SEG - 1) / CNDP_HOST_SEG;
+    uint64_t seg_done = 0; // segments issued so far
+    hipEvent_t ev_in = nullptr, ev_k = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ev_k, hipEventDisableTiming));
     r = -EIO;
-    if (hipStreamCreate(&s) != hipSuccess)
-        return -EIO;
-    if (hipMalloc(&d_slab, hb->slab_len ? hb->slab_len : 1) != hipSuccess ||
-        hipMalloc(&d_out, out_bytes) != hipSuccess)
-        goto out;
-    if (hb->offsets && hipMalloc(&d_off, n * 8) != hipSuccess)
-        goto out;
-    if (hipMemcpyAsync(d_slab, hb->slab, hb->slab_len, hipMemcpyHostToDevice, s) != hipSuccess)
-        goto out;
-    if (hb->offsets && hipMemcpyAsync(d_off, hb->offsets, n * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-        goto out;
-    if (hb->bins && hipMemcpyAsync((uint8_t *)d_out + o_b, hb->bins, ((uint64_t)hb->n_bins + 2) * 8,
-                                   hipMemcpyHostToDevice, s) != hipSuccess)
-        goto out;
-    db.slab = d_slab;
-    db.offsets = (const uint64_t *)d_off;
-    db.nh = hb->nh ? (uint32_t *)((uint8_t *)d_out + o_nh) : nullptr;
-    db.hash = hb->hash ? (uint32_t *)((uint8_t *)d_out + o_hash) : nullptr;
-    db.queue = hb->queue ? (uint16_t *)((uint8_t *)d_out + o_q) : nullptr;
-    db.edge = hb->edge ? (uint8_t *)d_out + o_e : nullptr;
-    db.bins = hb->bins ? (uint64_t *)((uint8_t *)d_out + o_b) : nullptr;
-    if ((r = cndp_gpu_classify(c, &db, s)))
-        goto out;
-    r = -EIO;
-    if (hb->nh && hipMemcpyAsync(hb->nh, db.nh, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
-        goto out;
-    if (hb->hash && hipMemcpyAsync(hb->hash, db.hash, n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
-        goto out;
-    if (hb->queue && hipMemcpyAsync(hb->queue, db.queue, n * 2, hipMemcpyDeviceToHost, s) != hipSuccess)
-        goto out;
-    if (hb->edge && hipMemcpyAsync(hb->edge, db.edge, n, hipMemcpyDeviceToHost, s) != hipSuccess)
-        goto out;
-    if (hb->bins && hipMemcpyAsync(hb->bins, db.bins, ((uint64_t)hb->n_bins + 2) * 8,
-                                   hipMemcpyDeviceToHost, s) != hipSuccess)
-        goto out;
-    if (hipStreamSynchronize(s) != hipSuccess)
+    for (uint64_t k = 0; k < n_chunks; k++) {
+        const uint64_t i0 = k * C, cnt = (n - i0) < C ? (n - i0) : C;
+        // byte span this chunk's parse can reach
+        uint64_t hi;
+        if (hb->offsets) {
+            hi = 0;
+            for (uint64_t i = i0; i < i0 + cnt; i++)
+                hi = hb->offsets[i] > hi ? hb->offsets[i] : hi;
+        } else {
+            hi = (i0 + cnt - 1) * hb->stride;
+        }
+        hi += (uint64_t)hb->data_off + CNDP_HOST_REACH;
+        const uint64_t seg_need = hi / CNDP_HOST_SEG + 1 < n_segs ? hi / CNDP_HOST_SEG + 1 : n_segs;
+        for (; seg_done < seg_need; seg_done++) {
+            const uint64_t lo = seg_done * CNDP_HOST_SEG;
+            const uint64_t len = hb->slab_len - lo < CNDP_HOST_SEG ? hb->slab_len - lo : CNDP_HOST_SEG;
+            if (hipMemcpyAsync(c->h_slab + lo, (const uint8_t *)hb->slab + lo, len, hipMemcpyHostToDevice, cs) !=
+                hipSuccess)
+                goto out;
+        }
+        if (hb->offsets && hipMemcpyAsync(c->h_off + i0, hb->offsets + i0, cnt * 8, hipMemcpyHostToDevice, cs) !=
+                               hipSuccess)
+            goto out;
+        if (hipEventRecord(ev_in, cs) != hipSuccess || hipStreamWaitEvent(ks, ev_in, 0) != hipSuccess)
+            goto out;
+        struct cndp_batch cb = *hb;
+        cb.n = (uint32_t)cnt;
+        cb.slab = c->h_slab;
+        if (hb->offsets)
+            cb.offsets = c->h_off + i0;
+        else
+            cb.data_off = hb->data_off; // packet i0 sits at i0 * stride: shift the slab view instead
+        cb.nh = hb->nh ? (uint32_t *)(c->h_out + o_nh) + i0 : nullptr;
+        cb.hash = hb->hash ? (uint32_t *)(c->h_out + o_hash) + i0 : nullptr;
+        cb.queue = hb->queue ? (uint16_t *)(c->h_out + o_q) + i0 : nullptr;
+        cb.edge = hb->edge ? c->h_out + o_e + i0 : nullptr;
+        cb.bins = d_bins;
+        if (!hb->offsets) {
+            // frames of this chunk start at byte i0 * stride of the mirror
+            cb.slab = c->h_slab + i0 * hb->stride;
+            cb.slab_len = hb->slab_len > i0 * hb->stride ? hb->slab_len - i0 * hb->stride : 0;
+        }
+        if ((r = cndp_gpu_classify(c, &cb, ks)))
+            goto out;
+        r = -EIO;
+        if (hipEventRecord(ev_k, ks) != hipSuccess || hipStreamWaitEvent(ds, ev_k, 0) != hipSuccess)
+            goto out;
+        if (hb->nh && hipMemcpyAsync(hb->nh + i0, cb.nh, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
+            goto out;
+        if (hb->hash && hipMemcpyAsync(hb->hash + i0, cb.hash, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
+            goto out;
+        if (hb->queue && hipMemcpyAsync(hb->queue + i0, cb.queue, cnt * 2, hipMemcpyDeviceToHost, ds) != hipSuccess)
+            goto out;
+        if (hb->edge && hipMemcpyAsync(hb->edge + i0, cb.edge, cnt, hipMemcpyDeviceToHost, ds) != hipSuccess)
+            goto out;
+    }
+    if (n_chunks == 0) { // still bind / sync the FIB images like the device path
+        struct cndp_batch cb = *hb;
+        cb.n = 0;
+        if ((r = cndp_gpu_classify(c, &cb, ks)))
+            goto out;
+        r = -EIO;
+    }
+    if (hb->bins) {
+        if (hipEventRecord(ev_k, ks) != hipSuccess || hipStreamWaitEvent(ds, ev_k, 0) != hipSuccess)
+            goto out;
+        if (hipMemcpyAsync(hb->bins, d_bins, ((uint64_t)hb->n_bins + 2) * 8, hipMemcpyDeviceToHost, ds) !=
+            hipSuccess)
+            goto out;
+    }
+    if (hipStreamSynchronize(ds) != hipSuccess || hipStreamSynchronize(ks) != hipSuccess ||
+        hipStreamSynchronize(cs) != hipSuccess)
         goto out;
     r = 0;
 out:
-    if (s)
-        hipStreamSynchronize(s);
-    if (d_slab)
-        hipFree(d_slab);
-    if (d_off)
-        hipFree(d_off);
-    if (d_out)
-        hipFree(d_out);
-    if (s)
-        hipStreamDestroy(s);
+    if (r) {
+        hipStreamSynchronize(cs);
+        hipStreamSynchronize(ks);
+        hipStreamSynchronize(ds);
+    }
+    hipEventDestroy(ev_in);
+    hipEventDestroy(ev_k);
     return r;
+}
+
+// ---------------------------------------------------------------------------
+// pktmbuf shim: the l3fwd-graph chain pktdev_rx (ptype) -> pkt_cls ->
+// ip4_lookup over an array of pktmbuf_t pointers (host memory), with every
+// field those nodes write into the mbuf written back the same way.
+// pktmbuf_t layout (pktmbuf.h:102-204): buf_addr @8, hash @16, data_off @24,
+// buf_len @28, data_len @30, packet_type @32, udata64 @56.
+// ---------------------------------------------------------------------------
+#define MB_BUF_ADDR 8
+#define MB_HASH 16
+#define MB_DATA_OFF 24
+#define MB_BUF_LEN 28
+#define MB_PTYPE 32
+#define MB_UDATA64 56
+
+static int mbuf_stage_grow(cndp_gpu_ctx_t *c, uint32_t n)
+{
+    if (c->m_cap >= n)
+        return 0;
+    const uint32_t cap = n < 4096 ? 4096 : n + (n >> 2);
+    if (c->m_hwin)
+        hipHostFree(c->m_hwin);
+    if (c->m_hres)
+        hipHostFree(c->m_hres);
+    if (c->m_dwin)
+        hipFree(c->m_dwin);
+    if (c->m_dres)
+        hipFree(c->m_dres);
+    c->m_hwin = nullptr;
+    c->m_hres = c->m_dres = nullptr;
+    c->m_dwin = nullptr;
+    c->m_cap = 0;
+    HIP_TRY(hipHostMalloc((void **)&c->m_hwin, (size_t)cap * 64, 0));
+    HIP_TRY(hipHostMalloc((void **)&c->m_hres, (size_t)cap * 8, 0));
+    HIP_TRY(hipMalloc((void **)&c->m_dwin, (size_t)cap * 64));
+    HIP_TRY(hipMalloc((void **)&c->m_dres, (size_t)cap * 8));
+    c->m_cap = cap;
+    return 0;
+}
+
+extern "C" int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *c, void *const *mbufs, uint32_t n, uint16_t *edges,
+                                    void *stream)
+{
+    if (!c || (n && (!mbufs || !edges)) || !c->fib4)
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    if (n == 0)
+        return 0;
+    if ((r = mbuf_stage_grow(c, n)))
+        return r;
+    // gather the 64-byte header window of each frame (bytes past the
+    // segment buffer are zero, like the slab-end rule of the device path)
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *m = (const uint8_t *)mbufs[i];
+        const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
+        const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
+        const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+        uint8_t *w = c->m_hwin + (size_t)i * 64;
+        const uint32_t avail = blen > doff ? (uint32_t)(blen - doff) : 0u;
+        if (avail >= 64) {
+            memcpy(w, buf + doff, 64);
+        } else {
+            memcpy(w, buf + doff, avail);
+            memset(w + avail, 0, 64 - avail);
+        }
+    }
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(c->m_dwin, c->m_hwin, (size_t)n * 64, hipMemcpyHostToDevice, s));
+    struct cndp_batch b;
+    memset(&b, 0, sizeof(b));
+    b.mode = CNDP_MODE_L3FWD;
+    b.n = n;
+    b.slab = c->m_dwin;
+    b.slab_len = (uint64_t)n * 64;
+    b.stride = 64;
+    b.buf_len = 1984;
+    b.nh = c->m_dres;
+    b.hash = c->m_dres + c->m_cap;
+    if ((r = cndp_gpu_classify(c, &b, s)))
+        return r;
+    HIP_TRY(hipMemcpyAsync(c->m_hres, c->m_dres, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(c->m_hres + c->m_cap, c->m_dres + c->m_cap, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t *m = (uint8_t *)mbufs[i];
+        const uint8_t *w = c->m_hwin + (size_t)i * 64;
+        const uint32_t et = ((uint32_t)w[12] << 8) | w[13];
+        // pktdev_rx.c:24-34 l3_ptype
+        *(uint32_t *)(m + MB_PTYPE) = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
+        *(uint32_t *)(m + MB_HASH) = c->m_hres[c->m_cap + i];
+        const uint32_t val = c->m_hres[i];
+        if (val == CNDP_NH_INVALID) { // pkt_cls.c: not IPv4 -> pkt_drop
+            edges[i] = CNDP_MBUF_EDGE_CLS_DROP;
+            continue;
+        }
+        // ip4_lookup.c:108-154: priv1 {nh, ttl, cksum} in udata64, edge = val >> 16
+        const uint64_t nh16 = val & 0xffffu, ttl = w[22], cksum = (uint64_t)w[24] | ((uint64_t)w[25] << 8);
+        *(uint64_t *)(m + MB_UDATA64) = nh16 | (ttl << 16) | (cksum << 32);
+        edges[i] = (uint16_t)(val >> 16);
+    }
+    return 0;
+}
+
+// Pin + map host memory (an AF_XDP UMEM region, a socket buffer pool) so the
+// device reads frames from it in place (zero-copy ingest) and DMA runs at
+// full rate.  *dev_ptr is the device-side address of `ptr`.
+extern "C" int cndp_gpu_host_register(cndp_gpu_ctx_t *c, void *ptr, uint64_t len, void **dev_ptr)
+{
+    if (!c || !ptr || !len)
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    hipError_t e = hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e == hipErrorHostMemoryAlreadyRegistered)
+        return -EEXIST;
+    if (e != hipSuccess) {
+        fprintf(stderr, "cndp_gpu: hipHostRegister failed: %s\n", hipGetErrorString(e));
+        return -ENOMEM;
+    }
+    if (dev_ptr) {
+        void *d = nullptr;
+        if (hipHostGetDevicePointer(&d, ptr, 0) != hipSuccess) {
+            hipHostUnregister(ptr);
+            return -EIO;
+        }
+        *dev_ptr = d;
+    }
+    return 0;
+}
+
+extern "C" int cndp_gpu_host_unregister(cndp_gpu_ctx_t *c, void *ptr)
+{
+    if (!c || !ptr)
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    return hipHostUnregister(ptr) == hipSuccess ? 0 : -ENOENT;
 }
 
 extern "C" int cndp_gpu_bin_ids(cndp_gpu_ctx_t *c, uint32_t mode, const uint32_t *nh,
@@ -2227,6 +2475,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return 0;
     case CNDP_TUNE_CNET_TILE:
         c->tune_cnet_tile = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_HOST_CHUNK:
+        if (value < 1024)
+            return -EINVAL;
+        c->host_chunk = (uint32_t)value;
         return 0;
     default:
         return -EINVAL;

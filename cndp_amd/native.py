@@ -34,6 +34,8 @@ CNDP_RETA_MAX = 512
 CNDP_BINS_MAX = 1024
 CNDP_TUNE_NT, CNDP_TUNE_UNROLL, CNDP_TUNE_BLOCKS_PER_CU, CNDP_TUNE_TILE, CNDP_TUNE_DIR16 = 1, 2, 3, 4, 5
 CNDP_TUNE_CNET_TILE = 6
+CNDP_TUNE_HOST_CHUNK = 7
+CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF
 
 # l3fwd edges (node_ip4_api.h:28-34) and cnet edges (ip4_input_priv.h:26-31)
 IP4_LOOKUP_NEXT_REWRITE, IP4_LOOKUP_NEXT_PKT_DROP = 0, 1
@@ -120,6 +122,9 @@ def lib():
         "cndp_gpu_set_fib": (c_int, [c_void_p, c_void_p, c_void_p]),
         "cndp_gpu_classify": (c_int, [c_void_p, POINTER(Batch), c_void_p]),
         "cndp_gpu_classify_host": (c_int, [c_void_p, POINTER(Batch)]),
+        "cndp_gpu_host_register": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_void_p)]),
+        "cndp_gpu_host_unregister": (c_int, [c_void_p, c_void_p]),
+        "cndp_gpu_l3fwd_mbufs": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
         "cndp_gpu_bin_partition": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p,
                                            c_void_p, c_void_p]),
         "cndp_gpu_bin_ids": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32,

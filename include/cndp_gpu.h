@@ -95,10 +95,33 @@ int cndp_gpu_set_fib(cndp_gpu_ctx_t *ctx, struct cne_fib *fib4, struct cne_fib6 
 /* Enqueue one classify pass over a device-resident batch. */
 int cndp_gpu_classify(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *stream);
 
-/* Same over HOST buffers (pinned or pageable): copies the slab (and
- * offsets) in, classifies, copies the outputs back and waits.  This is the
- * path a pktdev/AF_XDP consumer uses; it is PCIe-bound. */
+/* Same over HOST buffers (an AF_XDP UMEM, socket buffers): the slab is
+ * streamed into a device mirror in 64 MiB segments while earlier packet
+ * chunks are classified and their results copied back (three streams), and
+ * the call waits.  Results equal cndp_gpu_classify on a device copy.  Pinned
+ * memory (cndp_gpu_host_register, hipHostMalloc) gives full PCIe rate;
+ * pageable memory works at the driver's staging rate. */
 int cndp_gpu_classify_host(cndp_gpu_ctx_t *ctx, const struct cndp_batch *host_batch);
+
+/* pktmbuf shim for l3fwd-graph: one call per graph burst (or batch of
+ * bursts) of pktmbuf_t pointers in host memory.  Runs pktdev_rx's ptype
+ * parse (pktdev_rx.c:24-34), pkt_cls (pkt_cls.c:19-31) and ip4_lookup
+ * (ip4_lookup.c:48-256) on the GPU and writes back what those nodes write:
+ * m->packet_type, m->udata64 = node_mbuf_priv1 {nh, ttl, cksum}
+ * (node_private.h:24-35), plus m->hash (the flow hash, build-defined).
+ * edges[i] = the ip4_lookup next edge (val >> 16: 0 rewrite, 1 drop), or
+ * CNDP_MBUF_EDGE_CLS_DROP when pkt_cls sends the frame to pkt_drop.  Header
+ * windows are gathered into pinned staging, classified, and the call waits
+ * on `stream`.  mbufs: pktmbuf_t layout of pktmbuf.h:102-204. */
+#define CNDP_MBUF_EDGE_CLS_DROP 0xFFFFu
+int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, uint16_t *edges,
+                         void *stream);
+
+/* Pin and map host memory for the device (zero-copy ingest: pass *dev_ptr
+ * as cndp_batch.slab to cndp_gpu_classify and the kernel reads the frames
+ * over PCIe in place).  -EEXIST if already registered. */
+int cndp_gpu_host_register(cndp_gpu_ctx_t *ctx, void *ptr, uint64_t len, void **dev_ptr);
+int cndp_gpu_host_unregister(cndp_gpu_ctx_t *ctx, void *ptr);
 
 /* Stable partition of packet indices by bin (the per-edge streams a graph
  * walk would build): bin_of[i] in [0, n_bins+2) (device), outputs
@@ -125,13 +148,16 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
  *                           kept in front of tbl24 (default 1)
  *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = wave-tile staging with the next tile's loads
- *                           overlapping the FIB gathers (default), 0 = per-lane rows */
+ *                           overlapping the FIB gathers (default), 0 = per-lane rows
+ *   CNDP_TUNE_HOST_CHUNK    packets per pipelined chunk of cndp_gpu_classify_host
+ *                           (>= 1024, default 1M) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
 #define CNDP_TUNE_TILE 4
 #define CNDP_TUNE_DIR16 5
 #define CNDP_TUNE_CNET_TILE 6
+#define CNDP_TUNE_HOST_CHUNK 7
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

@@ -184,6 +184,56 @@ def test_classify_host_path(l3, gpu):
     assert_same(got, oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
 
 
+def test_classify_host_chunked(l3, cnet, gpu):
+    """The streamed host path with small chunks (many segments / chunk
+    boundaries, pinned and pageable buffers) equals the oracle: strided,
+    offset (IMIX) and deep-header fuzz layouts."""
+    cl, fib, t4 = l3
+    ccl, routes, v6, ct4, ct6 = cnet
+    try:
+        for c in (cl, ccl):
+            c.set_tuning(host_chunk=1024)
+        fr = pktgen.packed_ipv4(100003, routes=pktgen.l3fwd_routes(), seed=9)
+        ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+        pinned = fr.slab.pin_memory()
+        out = {k: torch.zeros(fr.n, dtype=d).pin_memory() for k, d in
+               (("nh", torch.int32), ("hash", torch.int32), ("queue", torch.int16), ("edge", torch.uint8))}
+        out["bins"] = torch.zeros(66, dtype=torch.int64).pin_memory()
+        got = cl.classify_host(pinned, fr.n, N.CNDP_MODE_L3FWD, stride=64, out=out)
+        assert_same({k: v.numpy() for k, v in got.items()}, ref)
+        for fr in (pktgen.imix(30011, v4routes=routes, v6routes=v6, seed=3),
+                   pktgen.fuzz_frames(20000, seed=8, slot=128)):
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
+            offs = fr.offsets.numpy().astype(np.uint64) if fr.offsets is not None else None
+            got = ccl.classify_host(fr.slab.numpy(), fr.n, N.CNDP_MODE_CNET, stride=fr.stride, offsets=offs,
+                                    data_off=fr.data_off)
+            assert_same(got, ref)
+    finally:
+        for c in (cl, ccl):
+            c.set_tuning(host_chunk=1 << 20)
+
+
+def test_zero_copy_registered_host(l3, gpu):
+    """Frames left in registered host memory (a UMEM), read in place by the kernel."""
+    cl, fib, t4 = l3
+    fr = pktgen.umem_ipv4(20000, routes=pktgen.l3fwd_routes(), seed=6)
+    ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+    import mmap
+    buf = mmap.mmap(-1, fr.slab.numel())
+    host = np.frombuffer(buf, dtype=np.uint8)
+    host[:] = fr.slab.numpy()
+    dptr = cl.host_register(host)
+    try:
+        out = cl.alloc_outputs(fr.n, 64, device=gpu)
+        cl.classify_ptrs(N.CNDP_MODE_L3FWD, fr.n, dptr, host.nbytes, out, stride=fr.stride, data_off=fr.data_off)
+        torch.cuda.synchronize()
+        assert_same({k: v for k, v in out.items() if k != "n_bins"}, ref)
+    finally:
+        cl.host_unregister(host)
+        del host
+        buf.close()
+
+
 @pytest.mark.parametrize("nh_sz", [0, 1, 2, 3])
 def test_fib_lookup_bulk_gpu_vs_bruteforce(gpu, nh_sz):
     from cndp_amd.fib import Fib
@@ -357,3 +407,43 @@ def test_route_churn_between_batches(gpu):
         for d16 in (1, 0):
             cl.set_tuning(dir16=d16)
             assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr, tables4=t4))
+
+
+def test_l3fwd_mbuf_shim(l3, gpu):
+    """pktmbuf_t pointer arrays in host memory (the node-process boundary):
+    packet_type, udata64 (node_mbuf_priv1), hash and the next edges written
+    back exactly as pktdev_rx + pkt_cls + ip4_lookup would."""
+    import ctypes
+    cl, fib, t4 = l3
+    n = 3000
+    fr = pktgen.fuzz_frames(n, seed=17, slot=64)
+    win = fr.slab.numpy()
+    win = np.concatenate([win, np.zeros(n * 64 - win.size, np.uint8)]).reshape(n, 64)
+    ref = O.classify(O.MODE_L3FWD, win.reshape(-1).copy(), n, stride=64, tables4=t4)
+    # mbuf headers (64 B each) and 2 KiB buffers with data at +256 (pktmbuf.c:60-80)
+    hdrs = np.zeros((n, 64), np.uint8)
+    bufs = np.zeros((n, 2048), np.uint8)
+    bufs[:, 256:320] = win
+    base = bufs.ctypes.data
+    for i in range(n):
+        h = hdrs[i]
+        h[8:16] = np.frombuffer(np.uint64(base + i * 2048).tobytes(), np.uint8)
+        h[24:26] = np.frombuffer(np.uint16(256).tobytes(), np.uint8)   # data_off
+        h[28:30] = np.frombuffer(np.uint16(2048).tobytes(), np.uint8)  # buf_len
+        h[56:64] = 0xAB                                                # udata64 sentinel
+    ptrs = (ctypes.c_void_p * n)(*[hdrs.ctypes.data + 64 * i for i in range(n)])
+    edges = np.zeros(n, np.uint16)
+    N.check(cl._L.cndp_gpu_l3fwd_mbufs(cl.h, ptrs, n, edges.ctypes.data, None), "l3fwd_mbufs")
+    et = (win[:, 12].astype(np.uint32) << 8) | win[:, 13]
+    ptype = hdrs[:, 32:36].copy().view(np.uint32).ravel()
+    assert np.array_equal(ptype, np.where(et == 0x0800, 0x90, np.where(et == 0x86DD, 0xE0, 0)))
+    assert np.array_equal(hdrs[:, 16:20].copy().view(np.uint32).ravel(), ref["hash"])
+    is4 = ref["nh"] != 0xFFFFFFFF
+    assert np.array_equal(is4, et == 0x0800)
+    assert np.array_equal(edges[~is4], np.full((~is4).sum(), N.CNDP_MBUF_EDGE_CLS_DROP))
+    assert np.array_equal(edges[is4], (ref["nh"][is4] >> 16).astype(np.uint16))
+    u = hdrs[:, 56:64].copy().view(np.uint64).ravel()
+    cks = win[:, 24].astype(np.uint64) | (win[:, 25].astype(np.uint64) << 8)
+    want = (ref["nh"].astype(np.uint64) & 0xFFFF) | (win[:, 22].astype(np.uint64) << 16) | (cks << 32)
+    assert np.array_equal(u[is4], want[is4])
+    assert np.all(u[~is4] == np.uint64(0xABABABABABABABAB))

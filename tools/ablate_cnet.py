@@ -28,7 +28,7 @@ def main():
     torch.cuda.set_device(dev)
     st = bench.build_state("c4", dev, 0, 1 << 20)   # FIBs + classifier (small batch, replaced below)
     cl, routes, v6 = st["cl"], st["routes"], st["v6routes"]
-    n = 1 << 24
+    n = 1 << 22
     stream = torch.cuda.Stream(dev)
     inputs = [
         ("imix v6=0.5", lambda: pktgen.imix(n, v4routes=routes, v6routes=v6, device=dev, v6_frac=0.5)),
@@ -36,9 +36,10 @@ def main():
         ("imix v6=1", lambda: pktgen.imix(n, v4routes=routes, v6routes=v6, device=dev, v6_frac=1.0)),
         ("packed64 v4", lambda: pktgen.packed_ipv4(n, routes=routes, device=dev)),
     ]
-    for name, make in inputs:
-        fr = make()
-        full = cl.alloc_outputs(n, 64, device=dev, edge=True)
+    made = [(name, make()) for name, make in inputs]   # all generated up front
+    torch.cuda.synchronize()
+    full = cl.alloc_outputs(n, 64, device=dev, edge=True)
+    for name, fr in made:
         cases = [("full", dict(full)), ("nh+edge", dict(full, hash=None, queue=None, bins=None))]
         for ct in (1, 0):
             cl.set_tuning(cnet_tile=ct)
@@ -46,8 +47,6 @@ def main():
                 ms = timeit(cl, fr, N.CNDP_MODE_CNET, out, stream)
                 print(f"[ablate-cnet {name:12s} cnet_tile={ct}] {cname:8s} {ms:.4f} ms {n / ms / 1e3:9.1f} Mpps",
                       flush=True)
-        del fr, full
-        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
