@@ -178,6 +178,45 @@ class Classifier:
         N.check(self._L.cndp_gpu_classify(self.h, ctypes.byref(b), stream or None), "cndp_gpu_classify")
         return out
 
+    # -- ip4_rewrite / cndpfwd loopback (in place on the device slab) -------
+    def rewrite_set_next(self, port_id: int, next_index: int):
+        """ip4_rewrite_set_next (ip4_rewrite.c:252-263)."""
+        N.check(self._L.cndp_gpu_ip4_rewrite_set_next(self.h, port_id, next_index), "ip4_rewrite_set_next")
+
+    def rewrite_add(self, next_hop: int, rewrite_data: bytes, dst_port: int) -> int:
+        """cne_node_ip4_rewrite_add (ip4_rewrite.c:265-295); returns its rc."""
+        buf = ctypes.create_string_buffer(bytes(rewrite_data), max(1, len(rewrite_data)))
+        return self._L.cndp_gpu_ip4_rewrite_add(self.h, next_hop, buf, len(rewrite_data), dst_port)
+
+    def ip4_rewrite(self, frames, nh, burst: int = 256, tx_edge=None, stream: int | None = None):
+        """Rewrite the frames routed to ip4_rewrite (l3fwd classify value
+        `nh` with edge 0) in place; returns the tx edge per packet (u16 as
+        int16 tensor, 0xFFFF = not rewritten)."""
+        import torch
+        if tx_edge is None:
+            tx_edge = torch.empty(frames.n, dtype=torch.int16, device=frames.slab.device)
+        b = N.Batch()
+        b.mode, b.n, b.slab, b.slab_len = N.CNDP_MODE_L3FWD, frames.n, frames.slab.data_ptr(), frames.slab.numel()
+        b.stride, b.data_off = frames.stride, frames.data_off
+        b.offsets = frames.offsets.data_ptr() if frames.offsets is not None else None
+        b.nh = nh.data_ptr()
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.slab.device).cuda_stream
+        N.check(self._L.cndp_gpu_ip4_rewrite(self.h, ctypes.byref(b), burst, tx_edge.data_ptr(), stream or None),
+                "cndp_gpu_ip4_rewrite")
+        return tx_edge
+
+    def mac_swap(self, frames, stream: int | None = None):
+        """cndpfwd loopback MAC swap on every frame (in place)."""
+        import torch
+        b = N.Batch()
+        b.n, b.slab, b.slab_len = frames.n, frames.slab.data_ptr(), frames.slab.numel()
+        b.stride, b.data_off = frames.stride, frames.data_off
+        b.offsets = frames.offsets.data_ptr() if frames.offsets is not None else None
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.slab.device).cuda_stream
+        N.check(self._L.cndp_gpu_mac_swap(self.h, ctypes.byref(b), stream or None), "cndp_gpu_mac_swap")
+
     def bin_partition(self, bin_of, n_bins: int, stream: int | None = None):
         """Stable partition of packet indices by bin id (per-edge streams)."""
         import torch

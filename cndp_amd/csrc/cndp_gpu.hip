@@ -1487,6 +1487,18 @@ __global__ __launch_bounds__(PART_THREADS) void k_part_scatter(const uint16_t *_
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+#define CNDP_RW_MAX_NH 64     // CNE_GRAPH_IP4_REWRITE_MAX_NH
+#define CNDP_RW_MAX_LEN 56    // CNE_GRAPH_IP4_REWRITE_MAX_LEN
+#define CNDP_RW_MAX_PORTS 32  // CNE_MAX_ETHPORTS
+// struct ip4_rewrite_nh_header (ip4_rewrite_priv.h:24-38)
+struct cndp_rw_nh {
+    uint16_t rewrite_len;
+    uint16_t tx_node;
+    uint16_t enabled;
+    uint16_t rsvd;
+    uint8_t rewrite_data[CNDP_RW_MAX_LEN];
+};
+
 struct cndp_gpu_ctx {
     int dev;
     uint8_t key[CNDP_RSS_KEY_LEN];
@@ -1517,6 +1529,11 @@ struct cndp_gpu_ctx {
     uint8_t *m_hwin, *m_dwin;
     uint32_t *m_hres, *m_dres; // nh[cap] | hash[cap]
     uint32_t m_cap;
+    // ip4_rewrite node state (ip4_rewrite_priv.h:15-51)
+    struct cndp_rw_nh rw_tbl[CNDP_RW_MAX_NH];
+    uint16_t rw_next[CNDP_RW_MAX_PORTS];
+    struct cndp_rw_nh *d_rw_tbl;
+    int rw_dirty;
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -1626,6 +1643,8 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         hipFree(c->m_dwin);
     if (c->m_dres)
         hipFree(c->m_dres);
+    if (c->d_rw_tbl)
+        hipFree(c->d_rw_tbl);
     if (c->d_ttab)
         hipFree(c->d_ttab);
     if (c->d_reta)
@@ -2250,6 +2269,167 @@ out:
 }
 
 // ---------------------------------------------------------------------------
+// ip4_rewrite (ip4_rewrite.c:40-247) and the cndpfwd loopback MAC swap
+// (examples/cndpfwd/main.h:303-315), in place on the device frame slab.
+// A block owns whole graph bursts: the rewrite stream of a burst is its
+// edge-0 packets in order; the first (count & ~3) of them take the 4-wide
+// loop's checksum update (end-around carry, :97-104), the rest the tail
+// loop's (:214-216).  Frames whose first 28 bytes are 4-B aligned and in
+// the slab are rewritten as 7 dwords; others byte by byte.
+// ---------------------------------------------------------------------------
+struct RwArgs {
+    uint8_t *slab;
+    uint64_t slab_len, stride;
+    const uint64_t *offsets;
+    uint32_t data_off, n, burst;
+    const uint32_t *nh;
+    const struct cndp_rw_nh *tbl;
+    uint16_t *tx_edge;
+};
+
+__device__ __forceinline__ bool rw_bound(uint32_t v) { return v != CNDP_NH_INVALID && (v >> 16) == 0u; }
+
+// block-wide count of `f` and this thread's exclusive prefix (256 threads)
+__device__ __forceinline__ uint32_t block_scan(bool f, uint32_t *s_w, uint32_t &total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(f);
+    const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();
+    if (lane == 0)
+        s_w[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0;
+    total = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+        pre += k < wv ? s_w[k] : 0u;
+        total += s_w[k];
+    }
+    return pre + below;
+}
+
+__device__ __forceinline__ void rw_byte(uint8_t *slab, uint64_t len, uint64_t o, uint32_t v)
+{
+    if (o < len)
+        slab[o] = (uint8_t)v;
+}
+
+__global__ __launch_bounds__(256) void k_ip4_rewrite(RwArgs a)
+{
+    __shared__ struct cndp_rw_nh s_tbl[CNDP_RW_MAX_NH];
+    __shared__ uint32_t s_w[4];
+    for (uint32_t k = threadIdx.x; k < sizeof(s_tbl) / 4; k += 256)
+        ((uint32_t *)s_tbl)[k] = ((const uint32_t *)a.tbl)[k];
+    __syncthreads();
+    const uint64_t n_bursts = ((uint64_t)a.n + a.burst - 1) / a.burst;
+    for (uint64_t b = blockIdx.x; b < n_bursts; b += gridDim.x) {
+        const uint64_t b0 = b * a.burst, b1 = b0 + a.burst < a.n ? b0 + a.burst : a.n;
+        uint32_t cnt = 0;
+        for (uint64_t c0 = b0; c0 < b1; c0 += 256) {
+            const uint64_t i = c0 + threadIdx.x;
+            uint32_t tot;
+            block_scan(i < b1 && rw_bound(a.nh[i]), s_w, tot);
+            cnt += tot;
+        }
+        const uint32_t vec = cnt & ~3u;
+        uint32_t run = 0;
+        for (uint64_t c0 = b0; c0 < b1; c0 += 256) {
+            const uint64_t i = c0 + threadIdx.x;
+            const uint32_t v = i < b1 ? a.nh[i] : CNDP_NH_INVALID;
+            const bool f = i < b1 && rw_bound(v);
+            uint32_t tot;
+            const uint32_t pos = run + block_scan(f, s_w, tot);
+            run += tot;
+            if (i >= b1)
+                continue;
+            if (!f) {
+                if (a.tx_edge)
+                    a.tx_edge[i] = 0xFFFFu;
+                continue;
+            }
+            const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
+            const uint32_t nh16 = v & 0xffffu;
+            const uint32_t len = nh16 < CNDP_RW_MAX_NH ? s_tbl[nh16].rewrite_len : 0u;
+            const uint32_t tx = nh16 < CNDP_RW_MAX_NH ? s_tbl[nh16].tx_node : 0u;
+            const uint8_t *data = s_tbl[nh16 < CNDP_RW_MAX_NH ? nh16 : 0].rewrite_data;
+            const uint32_t lenc = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
+            uint8_t *p = a.slab + base;
+            const bool fast = base + 28 <= a.slab_len && (((uintptr_t)p) & 3u) == 0;
+            uint32_t ttl, ck;
+            if (fast) {
+                uint32_t d[7];
+#pragma unroll
+                for (int k = 0; k < 7; k++)
+                    d[k] = ((const uint32_t *)p)[k];
+                ttl = (d[5] >> 16) & 0xffu;
+                ck = d[6] & 0xffffu;
+                for (uint32_t k = 0; k < lenc && k < 28; k++) {
+                    const uint32_t sh = (k & 3u) * 8u;
+                    d[k >> 2] = (d[k >> 2] & ~(0xffu << sh)) | ((uint32_t)data[k] << sh);
+                }
+                uint32_t nck;
+                if (pos < vec) {
+                    const uint32_t c32 = ck + 1u;
+                    nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
+                } else {
+                    uint32_t c16 = (ck + 1u) & 0xffffu;
+                    nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
+                }
+                d[5] = (d[5] & 0xff00ffffu) | (((ttl - 1u) & 0xffu) << 16);
+                d[6] = (d[6] & 0xffff0000u) | nck;
+#pragma unroll
+                for (int k = 0; k < 7; k++)
+                    ((uint32_t *)p)[k] = d[k];
+                for (uint32_t k = 28; k < lenc; k++)
+                    rw_byte(a.slab, a.slab_len, base + k, data[k]);
+            } else {
+                ttl = base + 22 < a.slab_len ? p[22] : 0u;
+                ck = (base + 24 < a.slab_len ? p[24] : 0u) | ((base + 25 < a.slab_len ? (uint32_t)p[25] : 0u) << 8);
+                for (uint32_t k = 0; k < lenc; k++)
+                    rw_byte(a.slab, a.slab_len, base + k, data[k]);
+                uint32_t nck;
+                if (pos < vec) {
+                    const uint32_t c32 = ck + 1u;
+                    nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
+                } else {
+                    uint32_t c16 = (ck + 1u) & 0xffffu;
+                    nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
+                }
+                rw_byte(a.slab, a.slab_len, base + 22, ttl - 1u);
+                rw_byte(a.slab, a.slab_len, base + 24, nck & 0xffu);
+                rw_byte(a.slab, a.slab_len, base + 25, nck >> 8);
+            }
+            if (a.tx_edge)
+                a.tx_edge[i] = (uint16_t)tx;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mac_swap(uint8_t *slab, uint64_t slab_len, uint64_t stride,
+                                                  const uint64_t *offsets, uint32_t data_off, uint32_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t base = (offsets ? offsets[i] : i * stride) + data_off;
+        if (base + 12 > slab_len)
+            continue;
+        uint8_t *p = slab + base;
+        if ((((uintptr_t)p) & 3u) == 0) {
+            uint32_t *d = (uint32_t *)p;
+            const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+            d[0] = alignb(d2, d1, 2);          // bytes 6..9
+            d[1] = (d2 >> 16) | (d0 << 16);    // bytes 10, 11, 0, 1
+            d[2] = alignb(d1, d0, 2);          // bytes 2..5
+        } else {
+            for (int k = 0; k < 6; k++) {
+                const uint8_t t = p[k];
+                p[k] = p[6 + k];
+                p[6 + k] = t;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // pktmbuf shim: the l3fwd-graph chain pktdev_rx (ptype) -> pkt_cls ->
 // ip4_lookup over an array of pktmbuf_t pointers (host memory), with every
 // field those nodes write into the mbuf written back the same way.
@@ -2350,6 +2530,99 @@ extern "C" int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *c, void *const *mbufs, uint3
         *(uint64_t *)(m + MB_UDATA64) = nh16 | (ttl << 16) | (cksum << 32);
         edges[i] = (uint16_t)(val >> 16);
     }
+    return 0;
+}
+
+// ip4_rewrite_set_next (ip4_rewrite.c:252-263)
+extern "C" int cndp_gpu_ip4_rewrite_set_next(cndp_gpu_ctx_t *c, uint16_t port_id, uint16_t next_index)
+{
+    if (!c || port_id >= CNDP_RW_MAX_PORTS)
+        return -EINVAL;
+    c->rw_next[port_id] = next_index;
+    return 0;
+}
+
+// cne_node_ip4_rewrite_add (ip4_rewrite.c:265-295): same checks, same order
+extern "C" int cndp_gpu_ip4_rewrite_add(cndp_gpu_ctx_t *c, uint16_t next_hop, const uint8_t *rewrite_data,
+                                        uint8_t rewrite_len, uint16_t dst_port)
+{
+    if (!c)
+        return -EINVAL;
+    if (next_hop >= CNDP_RW_MAX_NH)
+        return -EINVAL;
+    if (rewrite_len > CNDP_RW_MAX_LEN)
+        return -EINVAL;
+    if (dst_port >= CNDP_RW_MAX_PORTS || !c->rw_next[dst_port])
+        return -EINVAL;
+    if (rewrite_len && !rewrite_data)
+        return -EINVAL;
+    struct cndp_rw_nh *e = &c->rw_tbl[next_hop];
+    if (rewrite_len)
+        memcpy(e->rewrite_data, rewrite_data, rewrite_len);
+    e->tx_node = c->rw_next[dst_port];
+    e->rewrite_len = rewrite_len;
+    e->enabled = 1;
+    c->rw_dirty = 1;
+    return 0;
+}
+
+extern "C" int cndp_gpu_ip4_rewrite(cndp_gpu_ctx_t *c, const struct cndp_batch *b, uint32_t burst,
+                                    uint16_t *tx_edge, void *stream)
+{
+    if (!c || !b || burst == 0 || (b->n && (!b->slab || !b->nh)))
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    hipStream_t s = (hipStream_t)stream;
+    if (!c->d_rw_tbl) {
+        HIP_TRY(hipMalloc((void **)&c->d_rw_tbl, sizeof(c->rw_tbl)));
+        c->rw_dirty = 1;
+    }
+    if (c->rw_dirty) {
+        HIP_TRY(hipMemcpyAsync(c->d_rw_tbl, c->rw_tbl, sizeof(c->rw_tbl), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s)); // the host table may change after we return
+        c->rw_dirty = 0;
+    }
+    if (b->n == 0)
+        return 0;
+    RwArgs a;
+    a.slab = (uint8_t *)b->slab;
+    a.slab_len = b->slab_len;
+    a.stride = b->stride;
+    a.offsets = b->offsets;
+    a.data_off = b->data_off;
+    a.n = b->n;
+    a.burst = burst;
+    a.nh = b->nh;
+    a.tbl = c->d_rw_tbl;
+    a.tx_edge = tx_edge;
+    const uint64_t n_bursts = ((uint64_t)b->n + burst - 1) / burst;
+    uint64_t g = n_bursts;
+    const uint64_t cap = (uint64_t)c->num_cu * 8u;
+    if (g > cap)
+        g = cap;
+    hipLaunchKernelGGL(k_ip4_rewrite, dim3((uint32_t)g), dim3(256), 0, s, a);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int cndp_gpu_mac_swap(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream)
+{
+    if (!c || !b || (b->n && !b->slab))
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    if (b->n == 0)
+        return 0;
+    uint32_t g = blocks_for(b->n, 256);
+    const uint32_t cap = (uint32_t)c->num_cu * 8u;
+    if (g > cap)
+        g = cap;
+    hipLaunchKernelGGL(k_mac_swap, dim3(g), dim3(256), 0, (hipStream_t)stream, (uint8_t *)b->slab, b->slab_len,
+                       b->stride, b->offsets, b->data_off, b->n);
+    HIP_TRY(hipGetLastError());
     return 0;
 }
 

@@ -117,6 +117,25 @@ int cndp_gpu_classify_host(cndp_gpu_ctx_t *ctx, const struct cndp_batch *host_ba
 int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, uint16_t *edges,
                          void *stream);
 
+/* ip4_rewrite node on the device (ip4_rewrite.c).  Control plane mirrors
+ * ip4_rewrite_set_next (:252-263) and cne_node_ip4_rewrite_add (:265-295):
+ * next_hop < 64, rewrite_len <= 56, the dst_port must have a next index,
+ * else -EINVAL.  cndp_gpu_ip4_rewrite rewrites the device slab of `b` IN
+ * PLACE for the packets whose l3fwd classify value b->nh[i] has edge 0:
+ * rewrite data at the frame start, TTL - 1, checksum + 0x0100 with the
+ * reference's 4-wide / tail loop rules inside each graph burst of `burst`
+ * packets; tx_edge[i] (device, may be NULL) = the next hop's tx node, or
+ * 0xFFFF for packets that do not go through ip4_rewrite. */
+int cndp_gpu_ip4_rewrite_set_next(cndp_gpu_ctx_t *ctx, uint16_t port_id, uint16_t next_index);
+int cndp_gpu_ip4_rewrite_add(cndp_gpu_ctx_t *ctx, uint16_t next_hop, const uint8_t *rewrite_data,
+                             uint8_t rewrite_len, uint16_t dst_port);
+int cndp_gpu_ip4_rewrite(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, uint32_t burst,
+                         uint16_t *tx_edge, void *stream);
+
+/* cndpfwd loopback (examples/cndpfwd/main.c:317-339): swap the Ethernet
+ * destination and source addresses of every frame of the device slab. */
+int cndp_gpu_mac_swap(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *stream);
+
 /* Pin and map host memory for the device (zero-copy ingest: pass *dev_ptr
  * as cndp_batch.slab to cndp_gpu_classify and the kernel reads the frames
  * over PCIe in place).  -EEXIST if already registered. */

@@ -898,3 +898,78 @@ double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, in
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---------------------------------------------------------------------------
+ * ip4_rewrite (ip4_rewrite.c:40-247) and the cndpfwd MAC swap
+ * ------------------------------------------------------------------------- */
+static uint64_t frame_base(uint64_t stride, const uint64_t *offsets, uint32_t data_off, uint32_t i)
+{
+    return (offsets ? offsets[i] : (uint64_t)i * stride) + data_off;
+}
+
+static void put8(uint8_t *slab, uint64_t slab_len, uint64_t o, uint8_t v)
+{
+    if (o < slab_len)
+        slab[o] = v;
+}
+
+void orc_ip4_rewrite(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint64_t *offsets,
+                     uint32_t data_off, uint32_t n, const uint32_t *nh, uint32_t burst,
+                     const struct orc_rewrite_nh *tbl, uint16_t *tx_edge)
+{
+    static const struct orc_rewrite_nh unset; /* calloc'ed entry (ip4_rewrite.c:258) */
+    if (burst == 0)
+        burst = 1;
+    for (uint32_t b0 = 0; b0 < n; b0 += burst) {
+        const uint32_t b1 = b0 + burst < n ? b0 + burst : n;
+        uint32_t cnt = 0;
+        for (uint32_t i = b0; i < b1; i++)
+            cnt += nh[i] != 0xFFFFFFFFu && (nh[i] >> 16) == 0;
+        const uint32_t vec = cnt & ~3u; /* packets handled by the 4-wide loop */
+        uint32_t p = 0;
+        for (uint32_t i = b0; i < b1; i++) {
+            if (!(nh[i] != 0xFFFFFFFFu && (nh[i] >> 16) == 0)) {
+                tx_edge[i] = 0xFFFF;
+                continue;
+            }
+            const uint64_t base = frame_base(stride, offsets, data_off, i);
+            /* priv1 as ip4_lookup left it: nh, ttl, cksum from the frame */
+            const uint32_t nh16 = nh[i] & 0xFFFFu;
+            const uint32_t ttl = base + 22 < slab_len ? slab[base + 22] : 0;
+            const uint32_t ck = (base + 24 < slab_len ? slab[base + 24] : 0) |
+                                ((base + 25 < slab_len ? (uint32_t)slab[base + 25] : 0) << 8);
+            const struct orc_rewrite_nh *e = nh16 < 64 ? &tbl[nh16] : &unset;
+            for (uint32_t k = 0; k < e->rewrite_len && k < 56; k++)
+                put8(slab, slab_len, base + k, e->rewrite_data[k]);
+            uint16_t nck;
+            if (p < vec) { /* priv.u32[1] += htons(0x0100); cksum = u16[2] + u16[3] */
+                const uint32_t c32 = ck + 0x0001u;
+                nck = (uint16_t)((c32 & 0xFFFFu) + (c32 >> 16));
+            } else { /* chksum = cksum + htons(0x0100); chksum += chksum >= 0xffff */
+                uint16_t c16 = (uint16_t)(ck + 0x0001u);
+                c16 = (uint16_t)(c16 + (c16 >= 0xffff));
+                nck = c16;
+            }
+            put8(slab, slab_len, base + 22, (uint8_t)(ttl - 1));
+            put8(slab, slab_len, base + 24, (uint8_t)(nck & 0xFF));
+            put8(slab, slab_len, base + 25, (uint8_t)(nck >> 8));
+            tx_edge[i] = e->tx_node;
+            p++;
+        }
+    }
+}
+
+void orc_mac_swap(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint64_t *offsets,
+                  uint32_t data_off, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t base = frame_base(stride, offsets, data_off, i);
+        if (base + 12 > slab_len)
+            continue; /* build-defined: frames without a whole Ethernet address pair stay */
+        for (int k = 0; k < 6; k++) {
+            const uint8_t t = slab[base + k];
+            slab[base + k] = slab[base + 6 + k];
+            slab[base + 6 + k] = t;
+        }
+    }
+}

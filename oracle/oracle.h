@@ -121,6 +121,31 @@ int orc_classify(const struct orc_classify_args *a);
  * Multi-threaded over nthreads contiguous shards; returns elapsed seconds. */
 double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, int iters);
 
+/* ip4_rewrite node (ip4_rewrite.c:40-247) over a batch cut into graph
+ * bursts of `burst` packets.  nh[i] is the l3fwd classify output (edge << 16
+ * | nh, CNDP_NH_INVALID for non-IPv4); packets with edge 0 form the
+ * rewrite stream of their burst, in order.  For each: memcpy of the next
+ * hop's rewrite data to the frame start, TTL - 1, checksum + 0x0100 with
+ * the 4-wide loop's end-around carry (:97-100,104) for the first
+ * (cnt & ~3) packets of the stream and the tail loop's rule (:214-216) for
+ * the rest; tx_edge[i] = the next hop's tx node (0xFFFF when the packet is
+ * not in a rewrite stream).  Next hops >= 64 behave as unset entries. */
+struct orc_rewrite_nh {
+    uint16_t rewrite_len;
+    uint16_t tx_node;
+    uint16_t enabled;
+    uint16_t rsvd;
+    uint8_t rewrite_data[56];
+};
+void orc_ip4_rewrite(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint64_t *offsets,
+                     uint32_t data_off, uint32_t n, const uint32_t *nh, uint32_t burst,
+                     const struct orc_rewrite_nh *tbl, uint16_t *tx_edge);
+
+/* cndpfwd loopback: swap_mac_addresses (examples/cndpfwd/main.h:303-315)
+ * on every frame of the batch. */
+void orc_mac_swap(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint64_t *offsets,
+                  uint32_t data_off, uint32_t n);
+
 /* splitmix64 packet generator shared by tests and bench (seed 0x43444E50). */
 uint64_t orc_splitmix64(uint64_t *state);
 

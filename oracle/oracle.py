@@ -73,6 +73,9 @@ def lib():
         L.orc_classify.argtypes = [POINTER(ClassifyArgs)]
         L.orc_l3fwd_burst_bench.restype = c_double
         L.orc_l3fwd_burst_bench.argtypes = [POINTER(ClassifyArgs), c_int, c_int]
+        L.orc_ip4_rewrite.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32, c_void_p,
+                                      c_uint32, c_void_p, c_void_p]
+        L.orc_mac_swap.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]
         _lib = L
     return _lib
 
@@ -214,3 +217,26 @@ def l3fwd_burst_bench(slab, n, stride, tables4, nthreads=1, iters=1, **kw) -> fl
     t = lib().orc_l3fwd_burst_bench(ctypes.byref(a), nthreads, iters)
     del keep
     return t
+
+
+REWRITE_NH = np.dtype([("rewrite_len", "<u2"), ("tx_node", "<u2"), ("enabled", "<u2"), ("rsvd", "<u2"),
+                       ("rewrite_data", "u1", (56,))])
+
+
+def ip4_rewrite(slab: np.ndarray, n: int, nh: np.ndarray, table: np.ndarray, burst: int = 256,
+                stride: int = 64, offsets=None, data_off: int = 0):
+    """In-place ip4_rewrite restatement; returns tx_edge (u16)."""
+    assert slab.dtype == np.uint8 and slab.flags.c_contiguous
+    nh = np.ascontiguousarray(nh, dtype=np.uint32)
+    table = np.ascontiguousarray(table, dtype=REWRITE_NH)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64) if offsets is not None else None
+    tx = np.zeros(n, np.uint16)
+    lib().orc_ip4_rewrite(slab.ctypes.data, slab.nbytes, stride, offs.ctypes.data if offs is not None else None,
+                          data_off, n, nh.ctypes.data, burst, table.ctypes.data, tx.ctypes.data)
+    return tx
+
+
+def mac_swap(slab: np.ndarray, n: int, stride: int = 64, offsets=None, data_off: int = 0):
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64) if offsets is not None else None
+    lib().orc_mac_swap(slab.ctypes.data, slab.nbytes, stride, offs.ctypes.data if offs is not None else None,
+                       data_off, n)

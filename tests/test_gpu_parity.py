@@ -447,3 +447,77 @@ def test_l3fwd_mbuf_shim(l3, gpu):
     want = (ref["nh"].astype(np.uint64) & 0xFFFF) | (win[:, 22].astype(np.uint64) << 16) | (cks << 32)
     assert np.array_equal(u[is4], want[is4])
     assert np.all(u[~is4] == np.uint64(0xABABABABABABABAB))
+
+
+def _rewrite_setup(cl):
+    """Ports 0..3 with next indexes 1..4; next hops 0..47 rewrite 12-B MAC
+    pairs (some longer: 30 and 56 bytes), 48..63 left unset."""
+    tbl = np.zeros(64, O.REWRITE_NH)
+    for p in range(4):
+        cl.rewrite_set_next(p, p + 1)
+    rng = np.random.default_rng(5)
+    for nh in range(48):
+        ln = 56 if nh == 7 else 30 if nh == 9 else 12
+        data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        assert cl.rewrite_add(nh, data, nh % 4) == 0
+        tbl[nh]["rewrite_len"] = ln
+        tbl[nh]["tx_node"] = nh % 4 + 1
+        tbl[nh]["enabled"] = 1
+        tbl[nh]["rewrite_data"][:ln] = np.frombuffer(data, np.uint8)
+    return tbl
+
+
+def test_ip4_rewrite_control_plane_errors(l3, gpu):
+    cl, fib, t4 = l3
+    cl.rewrite_set_next(5, 0)
+    assert cl.rewrite_add(64, b"\x00" * 12, 0) < 0      # next_hop >= 64
+    assert cl.rewrite_add(1, b"\x00" * 57, 0) < 0       # rewrite_len > 56
+    assert cl.rewrite_add(1, b"\x00" * 12, 5) < 0       # no next index for the port
+
+
+@pytest.mark.parametrize("burst", [256, 7, 1000])
+def test_ip4_rewrite_parity(l3, gpu, burst):
+    """classify -> ip4_rewrite on the GPU == oracle classify -> rewrite
+    restatement, byte for byte over the whole slab (incl. the 4-wide / tail
+    checksum quirk at 0xFFFE / 0xFFFF and TTL 0)."""
+    cl, fib, t4 = l3
+    tbl = _rewrite_setup(cl)
+    for fr in (pktgen.packed_ipv4(50000, routes=pktgen.l3fwd_routes(), seed=burst),
+               pktgen.fuzz_frames(20011, seed=burst, slot=64),
+               pktgen.umem_ipv4(6000, routes=pktgen.l3fwd_routes(), seed=2)):
+        slab = fr.slab.clone()
+        k = torch.arange(fr.n)
+        base = (fr.offsets if fr.offsets is not None else k * fr.stride) + fr.data_off
+        sel = base[(k % 5 == 0) & (base + 26 <= slab.numel())]
+        slab[sel + 24] = 0xFE
+        slab[sel[::2] + 24] = 0xFF
+        slab[sel + 25] = 0xFF
+        slab[sel[::3] + 22] = 0
+        fr = pktgen.Frames(slab, fr.n, stride=fr.stride, data_off=fr.data_off, offsets=fr.offsets)
+        ref_cls = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+        host = fr.slab.numpy().copy()
+        ref_tx = O.ip4_rewrite(host, fr.n, ref_cls["nh"], tbl, burst=burst, stride=fr.stride,
+                               offsets=fr.offsets.numpy() if fr.offsets is not None else None, data_off=fr.data_off)
+        dfr = pktgen.Frames(fr.slab.to(gpu), fr.n, stride=fr.stride, data_off=fr.data_off,
+                            offsets=fr.offsets.to(gpu) if fr.offsets is not None else None)
+        out = cl.classify(dfr, N.CNDP_MODE_L3FWD)
+        tx = cl.ip4_rewrite(dfr, out["nh"], burst=burst)
+        torch.cuda.synchronize()
+        assert np.array_equal(tx.cpu().numpy().view(np.uint16), ref_tx)
+        got = dfr.slab.cpu().numpy()
+        bad = np.nonzero(got != host)[0]
+        assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+
+
+def test_mac_swap_loopback(l3, gpu):
+    """cndpfwd _loopback_test: MAC swap of every frame (aligned and not)."""
+    cl, fib, t4 = l3
+    for fr, doff in ((pktgen.packed_ipv4(512, routes=pktgen.l3fwd_routes()), 0),
+                     (pktgen.fuzz_frames(3001, seed=3, slot=97), 1)):
+        fr.data_off = doff
+        host = fr.slab.numpy().copy()
+        O.mac_swap(host, fr.n, stride=fr.stride, data_off=doff)
+        dfr = pktgen.Frames(fr.slab.to(gpu), fr.n, stride=fr.stride, data_off=doff)
+        cl.mac_swap(dfr)
+        torch.cuda.synchronize()
+        assert np.array_equal(dfr.slab.cpu().numpy(), host)

@@ -171,3 +171,44 @@ def test_trie_painter_vs_bruteforce():
         ips[i] = np.frombuffer(v.to_bytes(16, "big"), np.uint8)
     t24, t8 = O.trie_build(routes, 3, 1 << 14)
     assert np.array_equal(O.trie_lookup(t24, t8, ips), O.lpm6_bruteforce(routes, 3, ips))
+
+
+def test_oracle_ip4_rewrite_known_answers():
+    """ip4_rewrite restatement: TTL 64 -> 63 and checksum + 0x0100 (what the
+    reference chain produced when run), the header still
+    verifies, and the 4-wide / tail checksum rules at 0xFFFE / 0xFFFF."""
+    import numpy as np
+    from cndp_amd import pktgen
+    fr = pktgen.packed_ipv4(8, routes=pktgen.l3fwd_routes())
+    slab = fr.slab.numpy().copy()
+    tbl = np.zeros(64, O.REWRITE_NH)
+    tbl[:]["rewrite_len"] = 12
+    tbl[:]["tx_node"] = 3
+    nh = np.zeros(8, np.uint32)          # all to ip4_rewrite, next hop 0
+    before = slab.reshape(8, 64).copy()
+    tx = O.ip4_rewrite(slab, 8, nh, tbl, burst=8)
+    after = slab.reshape(8, 64)
+    assert (tx == 3).all()
+    assert (before[:, 22] == 64).all() and (after[:, 22] == 63).all()
+    ck0 = before[:, 24].astype(int) << 8 | before[:, 25]
+    ck1 = after[:, 24].astype(int) << 8 | after[:, 25]
+    assert ((ck0 + 0x100) & 0xFFFF == ck1).all()
+    for r in after:
+        assert O.ipv4_cksum(bytes(r[14:34])) == 0   # still a valid header
+    # quirk table: raw little-endian checksum word -> result, per loop
+    cases = {0xFFFE: (0xFFFF, 0x0000), 0xFFFF: (0x0001, 0x0000), 0x1234: (0x1235, 0x1235)}
+    for raw, (vec, tail) in cases.items():
+        s = np.zeros(64 * 5, np.uint8)
+        s[24::64] = raw & 0xFF
+        s[25::64] = raw >> 8
+        O.ip4_rewrite(s, 5, np.zeros(5, np.uint32), tbl, burst=5)   # 4 in the 4-wide loop, 1 tail
+        w = s[24::64].astype(int) | (s[25::64].astype(int) << 8)
+        assert list(w) == [vec] * 4 + [tail], (hex(raw), [hex(x) for x in w])
+
+
+def test_oracle_mac_swap():
+    import numpy as np
+    s = np.arange(128, dtype=np.uint8)
+    O.mac_swap(s, 2, stride=64)
+    assert list(s[:12]) == [6, 7, 8, 9, 10, 11, 0, 1, 2, 3, 4, 5]
+    assert list(s[64:76]) == [70, 71, 72, 73, 74, 75, 64, 65, 66, 67, 68, 69]
