@@ -34,6 +34,10 @@ CONFIGS = {
            1 << 24, 64 + 4 + 2),
     "c3": ("C3 l3fwd-graph: 64B IPv4/UDP, 1024-prefix DIR-24-8 LPM + Toeplitz + RSS queue, "
            "16M pkts/GPU device-resident", 1 << 24, 64 + 4 + 4 + 2),
+    # the full l3fwd-graph chain: C3's classify then ip4_rewrite in place
+    # (read nh 4 + frame bytes 0..27, write 28 + tx edge 2 on top of C3's 74)
+    "c3rw": ("C3 + ip4_rewrite: l3fwd-graph classify then MAC rewrite / TTL / checksum in place, "
+             "16M pkts/GPU device-resident", 1 << 24, 74 + 4 + 28 + 28 + 2),
     "c4": ("C4 IMIX 64/570/1500 (7:4:1) IPv4+IPv6 cnet parse + DIR-24-8/trie LPM + Toeplitz, "
            "16M pkts/GPU device-resident", 1 << 24, 64 + 4 + 4 + 2),
     "c5": ("C5 1500B IPv4/UDP cnet parse + IPv4 checksum verify + LPM, 32M pkts/GPU "
@@ -65,7 +69,7 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     cl = Classifier(dev.index)
     routes = pktgen.l3fwd_routes()
     state = {"desc": desc, "n": n, "algo": algo, "cl": cl, "routes": routes}
-    if cfg in ("c2", "c3"):
+    if cfg in ("c2", "c3", "c3rw"):
         fib = Fib("rt4", N.CNE_FIB_DIR24_8, default_nh=N.IP4_LOOKUP_NEXT_PKT_DROP << 16, max_routes=1024,
                   nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=256)
         for ip, d, nh in routes:
@@ -98,7 +102,25 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     # cnet keeps the edge output (its drop/forward/proto edge is not in nh
     # for packets the ptype node sends elsewhere)
     state["out"] = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
+    if cfg == "c3rw":
+        import random
+        rnd_ = random.Random(7)
+        for p in range(4):
+            cl.rewrite_set_next(p, p + 1)
+        for nh in range(64):  # 12-B dst/src MAC rewrite per next hop (l3fwd-graph main.c)
+            assert cl.rewrite_add(nh, bytes(rnd_.randrange(256) for _ in range(12)), nh % 4) == 0
+        state["tx"] = torch.empty(n, dtype=torch.int16, device=dev)
     return state
+
+
+def run_step(st, stream=None):
+    """One step of the configured workload (what the timed loop repeats)."""
+    cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
+    sid = stream.cuda_stream if stream is not None else None
+    if "tx" in st:
+        cl.classify_rewrite(fr, out=out, burst=256, tx_edge=st["tx"], stream=sid)
+    else:
+        cl.classify(fr, mode, out=out, stream=sid)
 
 
 def parity_sample(state, k: int = 1 << 16) -> bool:
@@ -288,7 +310,7 @@ def main():
         sweep(st, stream, args.config)
 
     for _ in range(args.warmup):
-        cl.classify(fr, mode, out=out)
+        run_step(st)
     torch.cuda.synchronize()
     parity = None
     if rank == 0 and not args.no_parity:
@@ -305,7 +327,7 @@ def main():
     t_start = time.perf_counter()
     for s in range(args.steps):
         evs[s][0].record(stream)
-        cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+        run_step(st, stream)
         evs[s][1].record(stream)
     D.final_count_reduce(out["bins"])  # the one RCCL collective: per-bin counts
     torch.cuda.synchronize()
@@ -327,7 +349,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
             cpu = cpu_baseline(st, args.cpu_budget)
         e2e = None
-        if world == 1 and not args.no_e2e:
+        if world == 1 and not args.no_e2e and args.config != "c3rw":
             try:
                 e2e = e2e_host(st)
                 log(f"[bench] host-memory rates: {e2e}")

@@ -206,6 +206,21 @@ class Classifier:
                 "cndp_gpu_ip4_rewrite")
         return tx_edge
 
+    def classify_rewrite(self, frames, out: dict | None = None, burst: int = 256, tx_edge=None,
+                         stream: int | None = None):
+        """l3fwd classify + ip4_rewrite (fused for packed 64-B slots, 256-bursts)."""
+        import torch
+        if out is None:
+            out = self.alloc_outputs(frames.n, 64, device=frames.slab.device, edge=False)
+        if tx_edge is None:
+            tx_edge = torch.empty(frames.n, dtype=torch.int16, device=frames.slab.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(frames.slab.device).cuda_stream
+        b = self.batch(frames, N.CNDP_MODE_L3FWD, out)
+        N.check(self._L.cndp_gpu_classify_rewrite(self.h, ctypes.byref(b), burst, tx_edge.data_ptr(),
+                                                  stream or None), "cndp_gpu_classify_rewrite")
+        return out, tx_edge
+
     def mac_swap(self, frames, stream: int | None = None):
         """cndpfwd loopback MAC swap on every frame (in place)."""
         import torch

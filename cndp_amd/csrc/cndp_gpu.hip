@@ -91,6 +91,18 @@ __device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_
            tab[(b + 2) * 256 + ((x >> 16) & 0xffu)] ^ tab[(b + 3) * 256 + (x >> 24)];
 }
 
+#define CNDP_RW_MAX_NH 64     // CNE_GRAPH_IP4_REWRITE_MAX_NH
+#define CNDP_RW_MAX_LEN 56    // CNE_GRAPH_IP4_REWRITE_MAX_LEN
+#define CNDP_RW_MAX_PORTS 32  // CNE_MAX_ETHPORTS
+// struct ip4_rewrite_nh_header (ip4_rewrite_priv.h:24-38)
+struct cndp_rw_nh {
+    uint16_t rewrite_len;
+    uint16_t tx_node;
+    uint16_t enabled;
+    uint16_t rsvd;
+    uint8_t rewrite_data[CNDP_RW_MAX_LEN];
+};
+
 struct KArgs {
     const uint8_t *slab;
     uint64_t slab_len;
@@ -114,9 +126,15 @@ struct KArgs {
     uint8_t *edge;
     unsigned long long *bins;
     uint32_t n_bins;
+    // fused ip4_rewrite (k_classify_tile<..., RW = true>)
+    const struct cndp_rw_nh *rw_tbl;
+    uint16_t *tx_edge;
+    uint32_t rw_parts; // 16-B parts of each rewritten frame written back
 };
 
 #define FAST_THREADS 256
+// a packet ip4_lookup hands to ip4_rewrite (edge 0, ip4_lookup.c:150)
+__device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
 #define TAB_POS 36  /* ... for the IPv6 L4 tuple */
 
@@ -356,15 +374,21 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
 // ---------------------------------------------------------------------------
 #define TILE_WAVES (FAST_THREADS / 64)
 
-template <int MODE, int SCHED, bool NTS>
+template <int MODE, int SCHED, bool NTS, bool RW = false>
 __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB4_POS * 256];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
     __shared__ __attribute__((aligned(16))) u32x4 s_tile[TILE_WAVES][256];
+    __shared__ struct cndp_rw_nh s_rw[RW ? CNDP_RW_MAX_NH : 1];
+    __shared__ uint32_t s_rwc[2][TILE_WAVES];
 
     const uint32_t tid = threadIdx.x;
+    if (RW)
+        for (uint32_t k = tid; k < sizeof(s_rw) / 4; k += FAST_THREADS)
+            ((uint32_t *)s_rw)[k] = ((const uint32_t *)a.rw_tbl)[k];
+    uint32_t rw_par = 0;
     for (uint32_t k = tid; k < TAB4_POS * 256; k += FAST_THREADS)
         s_t[k] = a.ttab[k];
     for (uint32_t k = tid; k <= a.reta_mask; k += FAST_THREADS)
@@ -471,6 +495,66 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
             }
             if (slow)
                 hs = fast_hash<MODE>(a, h, s_t);
+            if (RW) {
+                // ip4_rewrite fused (ip4_rewrite.c:40-247): the block's 4 waves
+                // hold the 4 tiles of one 256-packet graph burst; the burst's
+                // rewrite stream is its edge-0 packets in order
+                const bool f = nh_ready_rw(nh);
+                const unsigned long long m = __ballot(f);
+                const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                uint32_t *cw = s_rwc[rw_par];
+                rw_par ^= 1u;
+                if (lane == 0)
+                    cw[wv] = (uint32_t)__popcll(m);
+                __syncthreads();
+                uint32_t pre = 0, tot = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < TILE_WAVES; k++) {
+                    pre += k < wv ? cw[k] : 0u;
+                    tot += cw[k];
+                }
+                uint32_t tx = 0xFFFFu;
+                if (f) {
+                    const uint32_t pos = pre + below, nh16 = nh & 0xffffu;
+                    const struct cndp_rw_nh *e = &s_rw[nh16 < CNDP_RW_MAX_NH ? nh16 : 0];
+                    const uint32_t len = nh16 < CNDP_RW_MAX_NH ? e->rewrite_len : 0u;
+                    const uint32_t lenc = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
+                    tx = nh16 < CNDP_RW_MAX_NH ? e->tx_node : 0u;
+                    uint32_t *fd = (uint32_t *)tile;
+                    const uint32_t sw = (lane >> 2) & 3u;
+#define RW_DW(d) fd[((lane * 4u + (((d) >> 2) ^ sw)) << 2) | ((d) & 3u)]
+                    const uint32_t d5 = RW_DW(5u), d6 = RW_DW(6u);
+                    const uint32_t ttl = (d5 >> 16) & 0xffu, ck = d6 & 0xffffu;
+                    const uint32_t *src = (const uint32_t *)e->rewrite_data;
+                    for (uint32_t d = 0; d * 4 < lenc; d++) {
+                        const uint32_t nb = lenc - d * 4;
+                        const uint32_t keep = nb >= 4 ? 0u : (0xffffffffu << (nb * 8));
+                        RW_DW(d) = (RW_DW(d) & keep) | (src[d] & ~keep);
+                    }
+                    uint32_t nck;
+                    if (pos < (tot & ~3u)) {
+                        const uint32_t c32 = ck + 1u;
+                        nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
+                    } else {
+                        const uint32_t c16 = (ck + 1u) & 0xffffu;
+                        nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
+                    }
+                    RW_DW(5u) = (RW_DW(5u) & 0xff00ffffu) | (((ttl - 1u) & 0xffu) << 16);
+                    RW_DW(6u) = (RW_DW(6u) & 0xffff0000u) | nck;
+#undef RW_DW
+                }
+                __builtin_amdgcn_wave_barrier();
+                // write back the rewritten frames' first rw_parts 16-B parts
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    const uint32_t fk = 16u * k + fr_in_k;
+                    if (part < a.rw_parts && ((m >> fk) & 1ull))
+                        *(u32x4 *)(const_cast<uint8_t *>(base) + (t * 64u + fk) * 64u + part * 16u) =
+                            tile[fk * 4u + (part ^ ((fk >> 2) & 3u))];
+                }
+                __builtin_amdgcn_wave_barrier();
+                a.tx_edge[i] = (uint16_t)tx;
+            }
             fast_emit<MODE, NTS>(a, i, et, nh, hs, s_reta, s_bins, count);
         } else {
             // finish the dependent tbl24 -> tbl8 gathers first: vmcnt drains in
@@ -1487,18 +1571,6 @@ __global__ __launch_bounds__(PART_THREADS) void k_part_scatter(const uint16_t *_
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-#define CNDP_RW_MAX_NH 64     // CNE_GRAPH_IP4_REWRITE_MAX_NH
-#define CNDP_RW_MAX_LEN 56    // CNE_GRAPH_IP4_REWRITE_MAX_LEN
-#define CNDP_RW_MAX_PORTS 32  // CNE_MAX_ETHPORTS
-// struct ip4_rewrite_nh_header (ip4_rewrite_priv.h:24-38)
-struct cndp_rw_nh {
-    uint16_t rewrite_len;
-    uint16_t tx_node;
-    uint16_t enabled;
-    uint16_t rsvd;
-    uint8_t rewrite_data[CNDP_RW_MAX_LEN];
-};
-
 struct cndp_gpu_ctx {
     int dev;
     uint8_t key[CNDP_RSS_KEY_LEN];
@@ -1534,6 +1606,7 @@ struct cndp_gpu_ctx {
     uint16_t rw_next[CNDP_RW_MAX_PORTS];
     struct cndp_rw_nh *d_rw_tbl;
     int rw_dirty;
+    uint32_t rw_parts;    // 16-B parts a rewrite touches: ceil(max(26, longest rewrite) / 16)
 };
 
 static const uint8_t ms_default_key[CNDP_RSS_KEY_LEN] = {
@@ -2012,7 +2085,10 @@ static int validate_batch(const cndp_gpu_ctx_t *c, const struct cndp_batch *b)
     return 0;
 }
 
-extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream)
+// rw_tx != nullptr asks for ip4_rewrite fused into the wave-tile kernel
+// (256-packet bursts); *fused says whether that kernel ran
+static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream, uint16_t *rw_tx,
+                         bool *fused)
 {
     int r = validate_batch(c, b);
     if (r)
@@ -2103,7 +2179,15 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
                 {{k_classify_tile<CNDP_MODE_HASH, 0, false>, k_classify_tile<CNDP_MODE_HASH, 0, true>},
                  {k_classify_tile<CNDP_MODE_HASH, 1, false>, k_classify_tile<CNDP_MODE_HASH, 1, true>},
                  {k_classify_tile<CNDP_MODE_HASH, 2, false>, k_classify_tile<CNDP_MODE_HASH, 2, true>}}};
-            const tile_fn fn = fns[b->mode == CNDP_MODE_L3FWD ? 0 : 1][sched][c->tune_nt ? 1 : 0];
+            tile_fn fn = fns[b->mode == CNDP_MODE_L3FWD ? 0 : 1][sched][c->tune_nt ? 1 : 0];
+            if (rw_tx && b->mode == CNDP_MODE_L3FWD && sched == 2 && b->n % 256u == 0 && c->d_rw_tbl) {
+                fn = c->tune_nt ? k_classify_tile<CNDP_MODE_L3FWD, 2, true, true>
+                                : k_classify_tile<CNDP_MODE_L3FWD, 2, false, true>;
+                a.rw_tbl = c->d_rw_tbl;
+                a.tx_edge = rw_tx;
+                a.rw_parts = c->rw_parts;
+                *fused = true;
+            }
             hipLaunchKernelGGL(fn, dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
             HIP_TRY(hipGetLastError());
             return 0;
@@ -2125,6 +2209,11 @@ extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
     }
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream)
+{
+    return classify_impl(c, b, stream, nullptr, nullptr);
 }
 
 // grow a device buffer to at least `need` bytes (contents not kept)
@@ -2566,6 +2655,24 @@ extern "C" int cndp_gpu_ip4_rewrite_add(cndp_gpu_ctx_t *c, uint16_t next_hop, co
     return 0;
 }
 
+static int rw_sync(cndp_gpu_ctx_t *c, hipStream_t s)
+{
+    if (!c->d_rw_tbl) {
+        HIP_TRY(hipMalloc((void **)&c->d_rw_tbl, sizeof(c->rw_tbl)));
+        c->rw_dirty = 1;
+    }
+    if (c->rw_dirty) {
+        uint32_t mx = 26; // TTL and checksum end at byte 26
+        for (int k = 0; k < CNDP_RW_MAX_NH; k++)
+            mx = c->rw_tbl[k].rewrite_len > mx ? c->rw_tbl[k].rewrite_len : mx;
+        c->rw_parts = (mx + 15) / 16;
+        HIP_TRY(hipMemcpyAsync(c->d_rw_tbl, c->rw_tbl, sizeof(c->rw_tbl), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s)); // the host table may change after we return
+        c->rw_dirty = 0;
+    }
+    return 0;
+}
+
 extern "C" int cndp_gpu_ip4_rewrite(cndp_gpu_ctx_t *c, const struct cndp_batch *b, uint32_t burst,
                                     uint16_t *tx_edge, void *stream)
 {
@@ -2575,15 +2682,8 @@ extern "C" int cndp_gpu_ip4_rewrite(cndp_gpu_ctx_t *c, const struct cndp_batch *
     if (r)
         return r;
     hipStream_t s = (hipStream_t)stream;
-    if (!c->d_rw_tbl) {
-        HIP_TRY(hipMalloc((void **)&c->d_rw_tbl, sizeof(c->rw_tbl)));
-        c->rw_dirty = 1;
-    }
-    if (c->rw_dirty) {
-        HIP_TRY(hipMemcpyAsync(c->d_rw_tbl, c->rw_tbl, sizeof(c->rw_tbl), hipMemcpyHostToDevice, s));
-        HIP_TRY(hipStreamSynchronize(s)); // the host table may change after we return
-        c->rw_dirty = 0;
-    }
+    if ((r = rw_sync(c, s)))
+        return r;
     if (b->n == 0)
         return 0;
     RwArgs a;
@@ -2605,6 +2705,24 @@ extern "C" int cndp_gpu_ip4_rewrite(cndp_gpu_ctx_t *c, const struct cndp_batch *
     hipLaunchKernelGGL(k_ip4_rewrite, dim3((uint32_t)g), dim3(256), 0, s, a);
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+// classify (l3fwd) + ip4_rewrite: one fused wave-tile kernel for packed
+// 64-B slots in 256-packet bursts, otherwise the two kernels back to back
+extern "C" int cndp_gpu_classify_rewrite(cndp_gpu_ctx_t *c, const struct cndp_batch *b, uint32_t burst,
+                                         uint16_t *tx_edge, void *stream)
+{
+    if (!c || !b || b->mode != CNDP_MODE_L3FWD || burst == 0 || (b->n && (!b->nh || !tx_edge)))
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    if ((r = rw_sync(c, (hipStream_t)stream)))
+        return r;
+    bool fused = false;
+    if ((r = classify_impl(c, b, stream, burst == 256 ? tx_edge : nullptr, &fused)))
+        return r;
+    return fused ? 0 : cndp_gpu_ip4_rewrite(c, b, burst, tx_edge, stream);
 }
 
 extern "C" int cndp_gpu_mac_swap(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream)

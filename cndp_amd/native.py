@@ -129,6 +129,7 @@ def lib():
         "cndp_gpu_ip4_rewrite_add": (c_int, [c_void_p, c_uint16, c_void_p, c_uint8, c_uint16]),
         "cndp_gpu_ip4_rewrite": (c_int, [c_void_p, POINTER(Batch), c_uint32, c_void_p, c_void_p]),
         "cndp_gpu_mac_swap": (c_int, [c_void_p, POINTER(Batch), c_void_p]),
+        "cndp_gpu_classify_rewrite": (c_int, [c_void_p, POINTER(Batch), c_uint32, c_void_p, c_void_p]),
         "cndp_gpu_bin_partition": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p,
                                            c_void_p, c_void_p]),
         "cndp_gpu_bin_ids": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32,

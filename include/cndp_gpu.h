@@ -132,6 +132,13 @@ int cndp_gpu_ip4_rewrite_add(cndp_gpu_ctx_t *ctx, uint16_t next_hop, const uint8
 int cndp_gpu_ip4_rewrite(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, uint32_t burst,
                          uint16_t *tx_edge, void *stream);
 
+/* The whole l3fwd-graph data path in one call: classify (CNDP_MODE_L3FWD,
+ * b->nh required) then ip4_rewrite as above.  Packed 64-B slots in
+ * 256-packet bursts run as ONE fused kernel (the rewrite is applied to the
+ * frame tile already staged in LDS); other layouts run the two kernels. */
+int cndp_gpu_classify_rewrite(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, uint32_t burst,
+                              uint16_t *tx_edge, void *stream);
+
 /* cndpfwd loopback (examples/cndpfwd/main.c:317-339): swap the Ethernet
  * destination and source addresses of every frame of the device slab. */
 int cndp_gpu_mac_swap(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *stream);

@@ -521,3 +521,33 @@ def test_mac_swap_loopback(l3, gpu):
         cl.mac_swap(dfr)
         torch.cuda.synchronize()
         assert np.array_equal(dfr.slab.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("n,burst", [(256 * 300, 256), (256 * 300 + 77, 256), (5000, 7)])
+def test_classify_rewrite(l3, gpu, n, burst):
+    """cndp_gpu_classify_rewrite: the fused wave-tile kernel (packed slots,
+    n % 256 == 0, burst 256) and the two-kernel fallback both equal the
+    oracle chain (classify -> ip4_rewrite), incl. 30- and 56-byte rewrites."""
+    cl, fib, t4 = l3
+    tbl = _rewrite_setup(cl)
+    fr = pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=n)
+    slab = fr.slab.clone()
+    sel = torch.arange(0, n, 3) * 64
+    slab[sel + 24] = 0xFE
+    slab[sel + 25] = 0xFF
+    fr = pktgen.Frames(slab, n, stride=64)
+    ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+    host = fr.slab.numpy().copy()
+    ref_tx = O.ip4_rewrite(host, n, ref["nh"], tbl, burst=burst)
+    dfr = pktgen.Frames(fr.slab.to(gpu), n, stride=64)
+    for nt in (1, 0):
+        cl.set_tuning(nt=nt)
+        d2 = pktgen.Frames(dfr.slab.clone(), n, stride=64)
+        out, tx = cl.classify_rewrite(d2, burst=burst)
+        torch.cuda.synchronize()
+        assert_same({k: v for k, v in out.items() if k != "n_bins"}, ref, keys=("nh", "hash", "queue", "bins"))
+        assert np.array_equal(tx.cpu().numpy().view(np.uint16), ref_tx)
+        got = d2.slab.cpu().numpy()
+        bad = np.nonzero(got != host)[0]
+        assert bad.size == 0, f"nt={nt}: {bad.size} bytes differ, first at {bad[:8]}"
+    cl.set_tuning(nt=1)
