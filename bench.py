@@ -186,15 +186,17 @@ def sweep(st, stream, cfg):
     variants = [dict(v, dir16=1) for v in variants] + [dict(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=0)]
     if mode == N.CNDP_MODE_CNET:
         variants = [dict(cnet_tile=ct, dir16=d) for ct in (1, 0) for d in (1, 0)]
+    if "tx" in st:
+        variants = [dict(rw_wb=w, nt=nt, tile=4) for w in (0, 1, 2) for nt in (1, 0)] + [dict(tile=1, rw_wb=0)]
     for v in variants:
         cl.set_tuning(**v)
         for _ in range(3):
-            cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+            run_step(st, stream)
         evs = []
         for _ in range(20):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
-            cl.classify(fr, mode, out=out, stream=stream.cuda_stream)
+            run_step(st, stream)
             b.record(stream)
             evs.append((a, b))
         torch.cuda.synchronize()
@@ -205,7 +207,7 @@ def sweep(st, stream, cfg):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1)
+    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1, rw_wb=0)
 
 
 def e2e_host(st, reps: int = 5):

@@ -54,12 +54,12 @@ class Classifier:
     def set_tuning(self, nt: int | None = None, unroll: int | None = None,
                    blocks_per_cu: int | None = None, tile: int | None = None,
                    dir16: int | None = None, cnet_tile: int | None = None,
-                   host_chunk: int | None = None):
+                   host_chunk: int | None = None, rw_wb: int | None = None):
         """Kernel variant knobs (cndp_gpu_set_tuning); never change results."""
         for key, v in ((N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),
                        (N.CNDP_TUNE_BLOCKS_PER_CU, blocks_per_cu), (N.CNDP_TUNE_TILE, tile),
                        (N.CNDP_TUNE_DIR16, dir16), (N.CNDP_TUNE_CNET_TILE, cnet_tile),
-                       (N.CNDP_TUNE_HOST_CHUNK, host_chunk)):
+                       (N.CNDP_TUNE_HOST_CHUNK, host_chunk), (N.CNDP_TUNE_RW_WB, rw_wb)):
             if v is not None:
                 N.check(self._L.cndp_gpu_set_tuning(self.h, key, int(v)), "cndp_gpu_set_tuning")
 
@@ -68,10 +68,10 @@ class Classifier:
                 "cndp_gpu_set_fib")
         self.fib4, self.fib6 = fib4, fib6
 
-    def alloc_outputs(self, n: int, n_bins: int = 64, device=None, edge: bool = True):
+    def alloc_outputs(self, n: int, n_bins: int = 64, device=None, edge: bool = True, meta: bool = False):
         import torch
         dev = device if device is not None else f"cuda:{self.device}"
-        return {
+        out = {
             "nh": torch.empty(n, dtype=torch.int32, device=dev),
             "hash": torch.empty(n, dtype=torch.int32, device=dev),
             "queue": torch.empty(n, dtype=torch.int16, device=dev),
@@ -79,6 +79,10 @@ class Classifier:
             "bins": torch.zeros(n_bins + 2, dtype=torch.int64, device=dev),
             "n_bins": n_bins,
         }
+        if meta:
+            out["ptype"] = torch.empty(n, dtype=torch.int32, device=dev)
+            out["rxmeta"] = torch.empty(n, dtype=torch.int32, device=dev)
+        return out
 
     @staticmethod
     def _ptr(t):
@@ -101,6 +105,8 @@ class Classifier:
         b.edge = self._ptr(out.get("edge"))
         b.bins = self._ptr(out.get("bins"))
         b.n_bins = out.get("n_bins", 64)
+        b.ptype = self._ptr(out.get("ptype"))
+        b.rxmeta = self._ptr(out.get("rxmeta"))
         return b
 
     def classify(self, frames, mode: int = N.CNDP_MODE_L3FWD, out: dict | None = None,
@@ -148,6 +154,7 @@ class Classifier:
         b.stride, b.offsets, b.data_off, b.buf_len = stride, self._hptr(offsets), data_off, buf_len
         b.nh, b.hash, b.queue = self._hptr(out.get("nh")), self._hptr(out.get("hash")), self._hptr(out.get("queue"))
         b.edge, b.bins, b.n_bins = self._hptr(out.get("edge")), self._hptr(out.get("bins")), n_bins
+        b.ptype, b.rxmeta = self._hptr(out.get("ptype")), self._hptr(out.get("rxmeta"))
         N.check(self._L.cndp_gpu_classify_host(self.h, ctypes.byref(b)), "cndp_gpu_classify_host")
         return out
 
@@ -173,6 +180,7 @@ class Classifier:
         b.stride, b.offsets, b.data_off, b.buf_len = stride, offsets, data_off, buf_len
         b.nh, b.hash, b.queue = self._ptr(out.get("nh")), self._ptr(out.get("hash")), self._ptr(out.get("queue"))
         b.edge, b.bins, b.n_bins = self._ptr(out.get("edge")), self._ptr(out.get("bins")), n_bins
+        b.ptype, b.rxmeta = self._ptr(out.get("ptype")), self._ptr(out.get("rxmeta"))
         if stream is None:
             stream = torch.cuda.current_stream(self.device).cuda_stream
         N.check(self._L.cndp_gpu_classify(self.h, ctypes.byref(b), stream or None), "cndp_gpu_classify")

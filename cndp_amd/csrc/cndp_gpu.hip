@@ -126,6 +126,8 @@ struct KArgs {
     uint8_t *edge;
     unsigned long long *bins;
     uint32_t n_bins;
+    uint32_t *ptype;   // optional: packet_type per frame
+    uint32_t *rxmeta;  // optional (cnet): eth_rx lengths + ol_flags, packed (cndp_gpu.h)
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -292,6 +294,8 @@ __device__ __forceinline__ void fast_emit(const KArgs &a, uint64_t i, uint32_t e
     else
         edge = et == 0x0800u ? ((nh >> 16) & 0xffu) : 0xFFu;
     const uint32_t q = s_reta[hs & a.reta_mask];
+    if (a.ptype) // pktdev_rx.c:24-34 l3_ptype
+        stg<NT>(a.ptype + i, et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u);
     if (a.nh)
         stg<NT>(a.nh + i, nh);
     if (a.hash)
@@ -545,10 +549,14 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
                 }
                 __builtin_amdgcn_wave_barrier();
                 // write back the rewritten frames' first rw_parts 16-B parts
+                // rw_parts == 4 with whole-tile write-back (CNDP_TUNE_RW_WB):
+                // every frame of a tile holding a rewrite goes back as full
+                // coalesced 1-KiB stores (unchanged frames rewrite their own bytes)
+                const bool whole = a.rw_parts > 4u && m != 0ull;
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
                     const uint32_t fk = 16u * k + fr_in_k;
-                    if (part < a.rw_parts && ((m >> fk) & 1ull))
+                    if (whole || (part < a.rw_parts && ((m >> fk) & 1ull)))
                         *(u32x4 *)(const_cast<uint8_t *>(base) + (t * 64u + fk) * 64u + part * 16u) =
                             tile[fk * 4u + (part ^ ((fk >> 2) & 3u))];
                 }
@@ -668,6 +676,8 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_pipe(KArgs a)
                 a.hash[i] = hs;
             if (a.queue)
                 a.queue[i] = (uint16_t)q;
+            if (a.ptype) // pktdev_rx.c:24-34 l3_ptype
+                a.ptype[i] = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
         }
         // (5) next hop, edge and bin of the previous packet
         if (have_prev) {
@@ -736,7 +746,7 @@ struct Win {
 #define BE16C(x) ((uint32_t)((((x) & 0xffu) << 8) | (((x) >> 8) & 0xffu)))
 
 struct Lens {
-    uint32_t l2, l3;
+    uint32_t l2, l3, l4; // outer lengths (cne_net_hdr_lens); unset ones stay 0
 };
 
 __device__ __forceinline__ uint32_t pt_l3_ip(uint32_t vihl)
@@ -818,6 +828,7 @@ __device__ uint32_t get_ptype(const W &w, Lens &ln)
     int ret;
     ln.l2 = 14;
     ln.l3 = 0;
+    ln.l4 = 0;
     if (proto == BE16C(0x0806u))
         return 0x3u;
     if (proto != BE16C(0x0800u)) {
@@ -867,6 +878,7 @@ __device__ uint32_t get_ptype(const W &w, Lens &ln)
     }
     const uint32_t l4t = pt & 0xf00u;
     if (l4t == 0x200u) {
+        ln.l4 = 8;
         const uint32_t dport = w.raw16(ln.l2 + ln.l3 + 2);
         if (dport == BE16C(2152u))
             pt |= 0x8000u;
@@ -874,8 +886,14 @@ __device__ uint32_t get_ptype(const W &w, Lens &ln)
             pt |= 0x7000u;
         return pt;
     }
-    if (l4t == 0x100u || l4t == 0x400u)
+    if (l4t == 0x100u) {
+        ln.l4 = (w.b8(ln.l2 + ln.l3 + 12) & 0xf0u) >> 2; // TCP data offset
         return pt;
+    }
+    if (l4t == 0x400u) {
+        ln.l4 = 12;
+        return pt;
+    }
 
     // tunnels (:372-411)
     if (proto == 47u) {
@@ -944,6 +962,19 @@ __device__ uint32_t get_ptype(const W &w, Lens &ln)
     return pt;
 }
 
+// eth_rx.c:43-60 packed: tx_offload l2:7 | l3:9 | l4:8, ol_flags >> 32 in bits 29..31
+__device__ __forceinline__ uint32_t rx_meta(const Lens &ln, uint32_t w0, uint32_t w1, uint32_t et_raw)
+{
+    uint32_t m = (ln.l2 & 0x7fu) | ((ln.l3 & 0x1ffu) << 7) | ((ln.l4 & 0xffu) << 16);
+    if (et_raw == BE16C(0x86DDu))
+        m |= 1u << 31;                                   // CNE_MBUF_TYPE_IPv6
+    if (w0 == 0xffffffffu && (w1 & 0xffffu) == 0xffffu)
+        m |= 1u << 30;                                   // CNE_MBUF_TYPE_BCAST
+    else if (w0 & 1u)
+        m |= 1u << 29;                                   // CNE_MBUF_TYPE_MCAST
+    return m;
+}
+
 // lib/cnet/ptype/ptype.c:32-46 (indexed by ptype & 0xffff)
 __device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
 {
@@ -1010,6 +1041,10 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
         const Win w{row, p, avail};
         Lens ln;
         const uint32_t pt = get_ptype(w, ln);
+        if (a.ptype)
+            a.ptype[i] = pt;
+        if (a.rxmeta)
+            a.rxmeta[i] = rx_meta(ln, row[0], row[1], row[3] & 0xffffu);
         const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
         const uint32_t ip = ln.l2;
         const bool l4ok = l4t == 0x100u || l4t == 0x200u;
@@ -1211,7 +1246,8 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
         const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
                         ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
         const bool f6 = et == BE16C(0x86DDu) && l4p6;
-        uint32_t pt = 0, l3len = 0, pe = 0;
+        uint32_t pt = 0, pe = 0;
+        Lens lens{14u, 0u, 0u};
         uint32_t hw[9];      // Toeplitz input words, nw of them + the L4 word
         uint32_t nw = 0, hl4 = 0;
         uint32_t dip = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0;
@@ -1228,8 +1264,12 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             }
             pe = cnet_edge(pt);
             const bool l4ok = proto == 6u || proto == 17u;
+            lens.l3 = f4 ? 20u : 40u;
+            if (a.rxmeta) // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
+                lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
+                        : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
+                             : (gbyte(a.slab + base, base < a.slab_len ? a.slab_len - base : 0, 66) & 0xf0u) >> 2;
             if (f4) {
-                l3len = 20;
                 nw = 2;
                 hw[0] = alignb(W[7], W[6], 2);
                 hw[1] = alignb(W[8], W[7], 2);
@@ -1248,7 +1288,6 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                     do4 = true;
                 }
             } else {
-                l3len = 40;
                 nw = 8;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
@@ -1266,11 +1305,11 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             }
             if (!l4ok)
                 hl4 = 0;
-            (void)l3len;
         } else if (live) {
             const TWin w{tdw, lane * 4u, sw, a.slab + base, base < a.slab_len ? a.slab_len - base : 0};
-            Lens ln{14u, 0u};
+            Lens ln{14u, 0u, 0u};
             pt = get_ptype(w, ln);
+            lens = ln;
             const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
             const uint32_t ip = ln.l2;
             const bool l4ok = l4t == 0x100u || l4t == 0x200u;
@@ -1374,6 +1413,10 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
         __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
         if (live) {
             const uint32_t q = s_reta[h & a.reta_mask];
+            if (a.ptype)
+                a.ptype[i] = pt;
+            if (a.rxmeta)
+                a.rxmeta[i] = rx_meta(lens, W[0], W[1], et);
             if (a.nh)
                 a.nh[i] = nh;
             if (a.hash)
@@ -1589,6 +1632,7 @@ struct cndp_gpu_ctx {
     int tune_dir16;       // CNDP_TUNE_DIR16
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
+    int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
     hipStream_t hs[3];    // copy-in, classify, copy-out
     uint8_t *h_slab;      // device mirror of the host slab (same byte offsets)
@@ -2132,6 +2176,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
     a.edge = b->edge;
     a.bins = (unsigned long long *)b->bins;
     a.n_bins = b->n_bins;
+    a.ptype = b->ptype;
+    a.rxmeta = b->mode == CNDP_MODE_CNET ? b->rxmeta : nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (b->mode == CNDP_MODE_CNET) {
         uint32_t g = blocks_for(b->n, CNET_THREADS);
@@ -2185,7 +2231,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                 : k_classify_tile<CNDP_MODE_L3FWD, 2, false, true>;
                 a.rw_tbl = c->d_rw_tbl;
                 a.tx_edge = rw_tx;
-                a.rw_parts = c->rw_parts;
+                a.rw_parts = c->tune_rw_wb == 1 ? 4u : c->tune_rw_wb == 2 ? 5u : c->rw_parts;
                 *fused = true;
             }
             hipLaunchKernelGGL(fn, dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
@@ -2252,7 +2298,8 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
         return r;
     const uint64_t n = hb->n;
     const uint64_t o_nh = 0, o_hash = o_nh + n * 4, o_q = o_hash + n * 4, o_e = o_q + ((n * 2 + 15) & ~15ull),
-                   o_b = o_e + ((n + 15) & ~15ull), out_bytes = o_b + ((uint64_t)hb->n_bins + 2) * 8;
+                   o_b = o_e + ((n + 15) & ~15ull), o_pt = o_b + ((uint64_t)hb->n_bins + 2) * 8,
+                   o_rm = o_pt + n * 4, out_bytes = o_rm + n * 4;
     for (int k = 0; k < 3; k++)
         if (!c->hs[k])
             HIP_TRY(hipStreamCreateWithFlags(&c->hs[k], hipStreamNonBlocking));
@@ -2309,6 +2356,8 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
         cb.queue = hb->queue ? (uint16_t *)(c->h_out + o_q) + i0 : nullptr;
         cb.edge = hb->edge ? c->h_out + o_e + i0 : nullptr;
         cb.bins = d_bins;
+        cb.ptype = hb->ptype ? (uint32_t *)(c->h_out + o_pt) + i0 : nullptr;
+        cb.rxmeta = hb->rxmeta ? (uint32_t *)(c->h_out + o_rm) + i0 : nullptr;
         if (!hb->offsets) {
             // frames of this chunk start at byte i0 * stride of the mirror
             cb.slab = c->h_slab + i0 * hb->stride;
@@ -2326,6 +2375,11 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
         if (hb->queue && hipMemcpyAsync(hb->queue + i0, cb.queue, cnt * 2, hipMemcpyDeviceToHost, ds) != hipSuccess)
             goto out;
         if (hb->edge && hipMemcpyAsync(hb->edge + i0, cb.edge, cnt, hipMemcpyDeviceToHost, ds) != hipSuccess)
+            goto out;
+        if (hb->ptype && hipMemcpyAsync(hb->ptype + i0, cb.ptype, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
+            goto out;
+        if (hb->rxmeta &&
+            hipMemcpyAsync(hb->rxmeta + i0, cb.rxmeta, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
             goto out;
     }
     if (n_chunks == 0) { // still bind / sync the FIB images like the device path
@@ -2866,6 +2920,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return 0;
     case CNDP_TUNE_CNET_TILE:
         c->tune_cnet_tile = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_RW_WB:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_rw_wb = value;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

@@ -35,6 +35,7 @@ CNDP_BINS_MAX = 1024
 CNDP_TUNE_NT, CNDP_TUNE_UNROLL, CNDP_TUNE_BLOCKS_PER_CU, CNDP_TUNE_TILE, CNDP_TUNE_DIR16 = 1, 2, 3, 4, 5
 CNDP_TUNE_CNET_TILE = 6
 CNDP_TUNE_HOST_CHUNK = 7
+CNDP_TUNE_RW_WB = 8
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF
 
 # l3fwd edges (node_ip4_api.h:28-34) and cnet edges (ip4_input_priv.h:26-31)
@@ -69,7 +70,8 @@ class Batch(Structure):
     _fields_ = [("mode", c_uint32), ("n", c_uint32), ("slab", c_void_p), ("slab_len", c_uint64),
                 ("stride", c_uint64), ("offsets", c_void_p), ("data_off", c_uint32),
                 ("buf_len", c_uint32), ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p),
-                ("edge", c_void_p), ("bins", c_void_p), ("n_bins", c_uint32)]
+                ("edge", c_void_p), ("bins", c_void_p), ("n_bins", c_uint32), ("ptype", c_void_p),
+                ("rxmeta", c_void_p)]
 
 
 class NativeLibraryMissing(RuntimeError):

@@ -75,7 +75,17 @@ struct cndp_batch {
     uint8_t *edge;
     uint64_t *bins;
     uint32_t n_bins;        /* <= CNDP_BINS_MAX */
+    uint32_t *ptype;        /* optional out: m->packet_type -- cnet: cne_get_ptype
+                             * (eth_rx.c:41); l3fwd / hash: pktdev_rx's l3_ptype */
+    uint32_t *rxmeta;       /* optional out (cnet): the rest of eth_rx's mbuf_update
+                             * (eth_rx.c:43-60): bits 0-23 = tx_offload's l2_len:7 |
+                             * l3_len:9 | l4_len:8, bits 29-31 = ol_flags >> 32
+                             * (MCAST, BCAST, IPv6); lengths the reference leaves
+                             * unset are 0 */
 };
+#define CNDP_RXMETA_L2(m) ((m) & 0x7fu)
+#define CNDP_RXMETA_L3(m) (((m) >> 7) & 0x1ffu)
+#define CNDP_RXMETA_L4(m) (((m) >> 16) & 0xffu)
 
 /* Create / destroy a context bound to HIP device `device` (-1 = current). */
 int cndp_gpu_init(int device, cndp_gpu_ctx_t **out);
@@ -176,7 +186,10 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = wave-tile staging with the next tile's loads
  *                           overlapping the FIB gathers (default), 0 = per-lane rows
  *   CNDP_TUNE_HOST_CHUNK    packets per pipelined chunk of cndp_gpu_classify_host
- *                           (>= 1024, default 1M) */
+ *                           (>= 1024, default 1M)
+ *   CNDP_TUNE_RW_WB         fused classify+rewrite write-back: 0 = the 16-B parts the
+ *                           rewrite touches of rewritten frames (default), 1 = whole
+ *                           rewritten frames, 2 = whole tiles holding a rewrite */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -184,6 +197,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_DIR16 5
 #define CNDP_TUNE_CNET_TILE 6
 #define CNDP_TUNE_HOST_CHUNK 7
+#define CNDP_TUNE_RW_WB 8
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

@@ -720,6 +720,8 @@ static void classify_one(const struct orc_classify_args *a, uint32_t i)
             int l4ok = nx == 6 || nx == 17;
             hash = hash_v6(v, 14, l4ok, 14 + 40, a->rss_key);
         }
+        if (a->ptype) /* pktdev_rx.c:24-34 l3_ptype */
+            a->ptype[i] = et == 0x0800 ? 0x90u : et == 0x86DD ? 0xE0u : 0u;
         if (a->mode == MODE_HASH) {
             edge = 0;
         } else if (et == 0x0800) {
@@ -735,6 +737,24 @@ static void classify_one(const struct orc_classify_args *a, uint32_t i)
         struct orc_hdr_lens hl;
         memset(&hl, 0, sizeof(hl));
         uint32_t pt = orc_get_ptype(v.p, v.avail, &hl, 0x0fffffffu);
+        if (a->ptype)
+            a->ptype[i] = pt;
+        if (a->rxmeta) {
+            /* eth_rx.c:43-60: ol_flags IPv6 / BCAST / MCAST, tx_offload
+             * l2_len:7 l3_len:9 l4_len:8 (pktmbuf_offload.h:396-400) */
+            uint32_t m = (hl.l2_len & 0x7fu) | ((uint32_t)(hl.l3_len & 0x1ffu) << 7) |
+                         ((uint32_t)hl.l4_len << 16);
+            if (vraw16(v, 12) == BE(ET_IPV6))
+                m |= 1u << 31;
+            int bc = 1;
+            for (int k = 0; k < 6; k++)
+                bc &= v8(v, (uint32_t)k) == 0xFF;
+            if (bc)
+                m |= 1u << 30;
+            else if (v8(v, 0) & 1u)
+                m |= 1u << 29;
+            a->rxmeta[i] = m;
+        }
         uint32_t l3 = pt & 0xf0u;
         uint32_t l4t = pt & 0xf00u;
         uint32_t ip = hl.l2_len;

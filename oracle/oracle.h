@@ -113,6 +113,9 @@ struct orc_classify_args {
     uint16_t *queue;
     uint8_t *edge;              /* may be NULL */
     uint64_t *bins;             /* may be NULL */
+    uint32_t *ptype;            /* may be NULL: m->packet_type (eth_rx.c:41 / pktdev_rx.c:24-34) */
+    uint32_t *rxmeta;           /* may be NULL (cnet): eth_rx.c:43-60 lengths + ol_flags, packed
+                                 * as in cndp_gpu.h */
 };
 int orc_classify(const struct orc_classify_args *a);
 

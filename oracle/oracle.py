@@ -39,7 +39,7 @@ class ClassifyArgs(Structure):
                 ("tbl24", c_void_p), ("tbl8", c_void_p), ("tbl24_6", c_void_p), ("tbl8_6", c_void_p),
                 ("rss_key", c_void_p), ("reta", c_void_p), ("reta_size", c_uint32), ("n_bins", c_uint32),
                 ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p), ("edge", c_void_p),
-                ("bins", c_void_p)]
+                ("bins", c_void_p), ("ptype", c_void_p), ("rxmeta", c_void_p)]
 
 
 _lib = None
@@ -186,7 +186,8 @@ def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, 
     key = np.frombuffer(key or MS_RSS_KEY, dtype=np.uint8).copy()
     reta = np.ascontiguousarray(reta if reta is not None else (np.arange(128) % 16), dtype=np.uint16)
     out = {"nh": np.zeros(n, np.uint32), "hash": np.zeros(n, np.uint32), "queue": np.zeros(n, np.uint16),
-           "edge": np.zeros(n, np.uint8), "bins": np.zeros(n_bins + 2, np.uint64)}
+           "edge": np.zeros(n, np.uint8), "bins": np.zeros(n_bins + 2, np.uint64),
+           "ptype": np.zeros(n, np.uint32), "rxmeta": np.zeros(n, np.uint32)}
     slab = np.ascontiguousarray(slab, dtype=np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64) if offsets is not None else None
     a = ClassifyArgs()
@@ -199,6 +200,7 @@ def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, 
     a.rss_key, a.reta, a.reta_size, a.n_bins = _p(key), _p(reta), len(reta), n_bins
     a.nh, a.hash, a.queue, a.edge, a.bins = (_p(out["nh"]), _p(out["hash"]), _p(out["queue"]),
                                             _p(out["edge"]), _p(out["bins"]))
+    a.ptype, a.rxmeta = _p(out["ptype"]), _p(out["rxmeta"])
     keep = (slab, off, key, reta, tables4, tables6)  # keep buffers alive with the struct
     return a, out, keep
 

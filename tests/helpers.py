@@ -56,7 +56,8 @@ def oracle_classify(mode, frames, tables4=None, tables6=None, n_bins=64, reta=No
                       buf_len=buf_len)
 
 
-DT = {"nh": np.uint32, "hash": np.uint32, "queue": np.uint16, "edge": np.uint8, "bins": np.uint64}
+DT = {"nh": np.uint32, "hash": np.uint32, "queue": np.uint16, "edge": np.uint8, "bins": np.uint64,
+      "ptype": np.uint32, "rxmeta": np.uint32}
 
 
 def assert_same(got: dict, ref: dict, keys=("nh", "hash", "queue", "edge", "bins")):

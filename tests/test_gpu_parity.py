@@ -540,8 +540,8 @@ def test_classify_rewrite(l3, gpu, n, burst):
     host = fr.slab.numpy().copy()
     ref_tx = O.ip4_rewrite(host, n, ref["nh"], tbl, burst=burst)
     dfr = pktgen.Frames(fr.slab.to(gpu), n, stride=64)
-    for nt in (1, 0):
-        cl.set_tuning(nt=nt)
+    for nt, wb in ((1, 0), (0, 0), (1, 1), (1, 2)):
+        cl.set_tuning(nt=nt, rw_wb=wb)
         d2 = pktgen.Frames(dfr.slab.clone(), n, stride=64)
         out, tx = cl.classify_rewrite(d2, burst=burst)
         torch.cuda.synchronize()
@@ -549,5 +549,33 @@ def test_classify_rewrite(l3, gpu, n, burst):
         assert np.array_equal(tx.cpu().numpy().view(np.uint16), ref_tx)
         got = d2.slab.cpu().numpy()
         bad = np.nonzero(got != host)[0]
-        assert bad.size == 0, f"nt={nt}: {bad.size} bytes differ, first at {bad[:8]}"
-    cl.set_tuning(nt=1)
+        assert bad.size == 0, f"nt={nt} wb={wb}: {bad.size} bytes differ, first at {bad[:8]}"
+    cl.set_tuning(nt=1, rw_wb=0)
+
+
+def test_cnet_ptype_and_rxmeta(cnet, l3, gpu):
+    """m->packet_type and the eth_rx mbuf_update fields (lengths, ol_flags)
+    from both cnet kernels, and pktdev_rx's l3_ptype in l3fwd mode."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    cl, fib, t4 = l3
+    keys = ("nh", "hash", "queue", "edge", "bins", "ptype", "rxmeta")
+    for fr in (pktgen.fuzz_frames(30000, seed=11, slot=128, device=gpu),
+               pktgen.fuzz_frames(64 * 200, seed=12, slot=64, device=gpu),
+               pktgen.imix(20000, v4routes=routes, v6routes=v6, device=gpu, seed=4)):
+        ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
+        for ct in CNET_KERNELS:
+            ccl.set_tuning(cnet_tile=ct)
+            out = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+            ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
+            torch.cuda.synchronize()
+            assert_same(out, ref, keys=keys)
+    ccl.set_tuning(cnet_tile=1)
+    fr = pktgen.fuzz_frames(64 * 300, seed=13, slot=64, device=gpu)
+    ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+    for tile in (0, 3, 4):
+        cl.set_tuning(tile=tile)
+        out = cl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+        cl.classify(fr, N.CNDP_MODE_L3FWD, out=out)
+        torch.cuda.synchronize()
+        assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    cl.set_tuning(tile=4)

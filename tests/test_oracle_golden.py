@@ -212,3 +212,26 @@ def test_oracle_mac_swap():
     O.mac_swap(s, 2, stride=64)
     assert list(s[:12]) == [6, 7, 8, 9, 10, 11, 0, 1, 2, 3, 4, 5]
     assert list(s[64:76]) == [70, 71, 72, 73, 74, 75, 64, 65, 66, 67, 68, 69]
+
+
+def test_oracle_rxmeta_known_answers():
+    """eth_rx mbuf_update fields for hand-built frames (eth_rx.c:35-63)."""
+    import numpy as np
+    def frame(et, ip=b"", dst=b"\x02" * 6):
+        f = dst + b"\x02" * 6 + et.to_bytes(2, "big") + ip
+        return np.frombuffer(f + bytes(128 - len(f)), np.uint8)
+    v4 = bytes([0x45, 0, 0, 40, 0, 0, 0, 0, 64, 6]) + bytes(10)          # TCP
+    tcp = bytes(12) + bytes([0x80]) + bytes(7)                         # data offset 8 words -> 32 B
+    v6 = bytes([0x60, 0, 0, 0, 0, 8, 17, 64]) + bytes(32)                 # UDP
+    frames = [frame(0x0800, v4 + tcp), frame(0x86DD, v6), frame(0x0806, dst=b"\xff" * 6),
+              frame(0x0800, v4 + tcp, dst=b"\x01\x00\x5e\x00\x00\x01")]
+    slab = np.concatenate(frames)
+    r = O.classify(O.MODE_CNET, slab, 4, stride=128, tables4=O.dir24_8_build([], 0, 16),
+                   tables6=O.trie_build([], 0, 16))
+    m = r["rxmeta"]
+    l2, l3, l4 = m & 0x7F, (m >> 7) & 0x1FF, (m >> 16) & 0xFF
+    assert list(l2) == [14, 14, 14, 14]
+    assert list(l3[:2]) == [20, 40] and l3[2] == 0
+    assert list(l4) == [32, 8, 0, 32]
+    assert [(x >> 29) & 7 for x in m] == [0, 4, 2, 1]      # IPv6, BCAST, MCAST bits
+    assert list(r["ptype"][:3]) == [0x111, 0x241, 0x3]
