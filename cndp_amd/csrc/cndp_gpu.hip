@@ -128,6 +128,8 @@ struct KArgs {
     uint32_t n_bins;
     uint32_t *ptype;   // optional: packet_type per frame
     uint32_t *rxmeta;  // optional (cnet): eth_rx lengths + ol_flags, packed (cndp_gpu.h)
+    uint32_t *spec_nh; // cnet speculation model: input-node result of every frame a
+                       // ptype-node group could send to ip4/ip6_input (else ~0)
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -1274,7 +1276,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 hw[0] = alignb(W[7], W[6], 2);
                 hw[1] = alignb(W[8], W[7], 2);
                 hl4 = l4ok ? alignb(W[9], W[8], 2) : 0u;
-                if (pe == 3u) { // ip4_input.c:121-140
+                if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
                     uint32_t sum = 0;
 #pragma unroll
                     for (int k = 0; k < 5; k++) {
@@ -1293,7 +1295,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 for (int k = 0; k < 8; k++)
                     hw[k] = alignb(W[6 + k], W[5 + k], 2);
                 hl4 = l4ok ? alignb(W[14], W[13], 2) : 0u;
-                if (pe == 4u) { // ip6_input.c:115-135
+                if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
                     if (bswap16(W[4] >> 16) < a.buf_len) {
                         d0 = hw[4];
                         d1 = hw[5];
@@ -1324,7 +1326,13 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                     hw[k] = w.ld32(ip + 8 + 4 * k);
             }
             hl4 = nw && l4ok ? w.ld32(ip + ln.l3) : 0u;
-            if (pe == 3u) {
+            // with the speculation model, frames of the types a quiet 4-group can
+            // carry into ip4/ip6_input (L2 ether + IPv4 / IPv6 variants) get the
+            // input node's result computed as well
+            const uint32_t lb = pt & 0xffu;
+            const bool alt4 = a.spec_nh && (lb == 0x11u || lb == 0x31u || lb == 0x91u);
+            const bool alt6 = a.spec_nh && (lb == 0x41u || lb == 0xc1u || lb == 0xe1u);
+            if (pe == 3u || alt4) {
                 const uint32_t x0 = w.ld32(ip);
                 const uint32_t hl = x0 & 0xfu;
                 uint32_t sum = 0;
@@ -1337,7 +1345,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
                 dip = ok ? w.be32(ip + 16) : 0u;
                 do4 = true;
-            } else if (pe == 4u) {
+            } else if (pe == 4u || alt6) {
                 if (w.be16(ip + 4) < a.buf_len) {
                     d0 = w.ld32(ip + 24);
                     d1 = w.ld32(ip + 28);
@@ -1406,10 +1414,12 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             }
         }
         uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
-        if (do4 || do6) {
+        if ((do4 || do6) && (pe == 3u || pe == 4u)) {
             nh = e >> 1;
             edge = nh >> 24;
         }
+        if (a.spec_nh && live)
+            a.spec_nh[i] = do4 || do6 ? e >> 1 : CNDP_NH_INVALID;
         __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
         if (live) {
             const uint32_t q = s_reta[h & a.reta_mask];
@@ -1434,6 +1444,199 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
         for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
             if (s_bins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// cnet ptype-node speculation (ptype.c:48-210) as a post-pass over the
+// per-packet ptypes the classify kernel wrote.  In each graph burst of B
+// packets the node walks 4-packet groups against its state last_type: a
+// group whose four low bytes equal last_type's (the uint8_t fix_spec,
+// :109-110) goes whole to p_nxt[last_type]; any other group goes packet by
+// packet to p_nxt[type] and moves last_type to the group's 4th type when the
+// 3rd equals it or p_nxt agrees; the tail goes per packet.  The state only
+// matters through its signature sig = (low byte, p_nxt), and a group either
+// keeps it or replaces it by its 4th type, so each burst is a map
+// sig -> {unchanged | new state}.  Bursts are resolved with a chunked scan of
+// those maps over the signatures present in the batch (<= SPEC_KMAX; more
+// falls back to one sequential thread), then every burst is replayed from
+// its true start state and the frames whose node edge differs from
+// p_nxt[own type] get that edge's result (spec_nh) and their bins moved.
+// ---------------------------------------------------------------------------
+#define SPEC_KMAX 64
+#define SPEC_UNCH 0xFFFFFFFFu
+#define SPEC_SCAN_THREADS 1024
+
+__device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
+
+__global__ __launch_bounds__(256) void k_spec_flags(const uint32_t *__restrict__ pt, uint32_t n,
+                                                    uint32_t *flags, const uint32_t *state)
+{
+    __shared__ uint32_t s_f[64];
+    if (threadIdx.x < 64)
+        s_f[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t g = spec_sig(pt[i] & 0xffffu);
+        atomicOr(&s_f[g >> 5], 1u << (g & 31u));
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint32_t g = spec_sig(*state & 0xffffu);
+        atomicOr(&s_f[g >> 5], 1u << (g & 31u));
+    }
+    __syncthreads();
+    if (threadIdx.x < 64 && s_f[threadIdx.x])
+        atomicOr(&flags[threadIdx.x], s_f[threadIdx.x]);
+}
+
+// meta[0] = K, meta[1 + k] = signature of class k; class_id[sig] = k or 0xFF
+__global__ void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0)
+        return;
+    uint32_t k = 0;
+    for (uint32_t g = 0; g < 2048; g++) {
+        const bool on = (flags[g >> 5] >> (g & 31u)) & 1u;
+        class_id[g] = on && k < SPEC_KMAX ? (uint8_t)k : (uint8_t)0xFF;
+        if (on) {
+            if (k < SPEC_KMAX)
+                meta[1 + k] = g;
+            k++;
+        }
+    }
+    meta[0] = k;
+}
+
+// one burst's effect on a state of signature sig: SPEC_UNCH or the new state
+__device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0, uint32_t cnt, uint32_t sig)
+{
+    uint32_t low = sig >> 3, E = sig & 7u, c = SPEC_UNCH;
+    for (uint32_t g = 0; g + 4 <= cnt; g += 4) {
+        const uint32_t l0 = pt[b0 + g] & 0xffffu, l1 = pt[b0 + g + 1] & 0xffffu;
+        const uint32_t l2 = pt[b0 + g + 2] & 0xffffu, l3 = pt[b0 + g + 3] & 0xffffu;
+        const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low && (l3 & 0xffu) == low;
+        if (!quiet && (l2 == l3 || E == cnet_edge(l3))) {
+            c = l3;
+            low = l3 & 0xffu;
+            E = cnet_edge(l3);
+        }
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                     uint64_t nb, const uint32_t *meta, uint32_t *T)
+{
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t K = meta[0];
+    if (b >= nb || K > SPEC_KMAX)
+        return;
+    const uint64_t b0 = b * B;
+    const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
+    for (uint32_t k = 0; k < K; k++)
+        T[b * SPEC_KMAX + k] = spec_burst_map(pt, b0, cnt, meta[1 + k]);
+}
+
+__global__ __launch_bounds__(SPEC_SCAN_THREADS) void k_spec_scan(const uint32_t *__restrict__ pt, uint32_t n,
+                                                                uint32_t B, uint64_t nb, const uint32_t *meta,
+                                                                const uint8_t *class_id, const uint32_t *T,
+                                                                uint32_t *U, uint32_t *S, uint32_t *state)
+{
+    __shared__ uint32_t s_start[SPEC_SCAN_THREADS];
+    const uint32_t tid = threadIdx.x, K = meta[0];
+    if (K > SPEC_KMAX) { // too many signatures: one sequential walk
+        if (tid == 0) {
+            uint32_t st = *state & 0xffffu;
+            for (uint64_t b = 0; b < nb; b++) {
+                S[b] = st;
+                const uint64_t b0 = b * B;
+                const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
+                const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st));
+                if (c != SPEC_UNCH)
+                    st = c;
+            }
+            *state = st;
+        }
+        return;
+    }
+    const uint64_t C = (nb + SPEC_SCAN_THREADS - 1) / SPEC_SCAN_THREADS;
+    const uint64_t lo = tid * C < nb ? tid * C : nb, hi = lo + C < nb ? lo + C : nb;
+    uint32_t *u = U + (uint64_t)tid * SPEC_KMAX;
+    for (uint32_t k = 0; k < K; k++)
+        u[k] = SPEC_UNCH;
+    for (uint64_t b = lo; b < hi; b++) {
+        const uint32_t *t = T + b * SPEC_KMAX;
+        for (uint32_t k = 0; k < K; k++) {
+            const uint32_t cur = u[k];
+            if (cur == SPEC_UNCH) {
+                u[k] = t[k];
+            } else {
+                const uint32_t nx = t[class_id[spec_sig(cur)]];
+                if (nx != SPEC_UNCH)
+                    u[k] = nx;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t st = *state & 0xffffu;
+        for (uint32_t w = 0; w < SPEC_SCAN_THREADS; w++) {
+            s_start[w] = st;
+            const uint32_t nx = U[(uint64_t)w * SPEC_KMAX + class_id[spec_sig(st)]];
+            if (nx != SPEC_UNCH)
+                st = nx;
+        }
+        *state = st;
+    }
+    __syncthreads();
+    uint32_t st = s_start[tid];
+    for (uint64_t b = lo; b < hi; b++) {
+        S[b] = st;
+        const uint32_t nx = T[b * SPEC_KMAX + class_id[spec_sig(st)]];
+        if (nx != SPEC_UNCH)
+            st = nx;
+    }
+}
+
+__device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
+{
+    const uint32_t own = cnet_edge(own_l);
+    const uint32_t old_nh = own == 3u || own == 4u ? a.spec_nh[i] : CNDP_NH_INVALID;
+    const uint32_t old_edge = own == 3u || own == 4u ? old_nh >> 24 : 0x80u | own;
+    const uint32_t nh = dst == 3u || dst == 4u ? a.spec_nh[i] : CNDP_NH_INVALID;
+    const uint32_t edge = dst == 3u || dst == 4u ? nh >> 24 : 0x80u | dst;
+    if (a.nh)
+        a.nh[i] = nh;
+    if (a.edge)
+        a.edge[i] = (uint8_t)edge;
+    if (a.bins) {
+        atomicAdd(&a.bins[bin_of<CNDP_MODE_CNET>(old_nh, old_edge, 0, a.n_bins)], ~0ull); // -1
+        atomicAdd(&a.bins[bin_of<CNDP_MODE_CNET>(nh, edge, 0, a.n_bins)], 1ull);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *S)
+{
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= nb)
+        return;
+    const uint64_t b0 = b * B;
+    const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
+    uint32_t st = S[b], low = st & 0xffu, E = cnet_edge(st);
+    for (uint32_t g = 0; g + 4 <= cnt; g += 4) {
+        uint32_t l[4];
+        for (int j = 0; j < 4; j++)
+            l[j] = a.ptype[b0 + g + j] & 0xffffu;
+        const bool quiet = (l[0] & 0xffu) == low && (l[1] & 0xffu) == low && (l[2] & 0xffu) == low &&
+                           (l[3] & 0xffu) == low;
+        if (quiet) {
+            for (int j = 0; j < 4; j++)
+                if (cnet_edge(l[j]) != E)
+                    spec_fix(a, b0 + g + j, l[j], E);
+        } else if (l[2] == l[3] || E == cnet_edge(l[3])) {
+            low = l[3] & 0xffu;
+            E = cnet_edge(l[3]);
+        }
     }
 }
 
@@ -1633,6 +1836,11 @@ struct cndp_gpu_ctx {
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
+    uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
+    uint32_t *sp_small;   // [0] last_type, [1..65] class meta, [66..129] signature flags
+    uint8_t *sp_class;    // class id per signature (2048)
+    uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U;
+    uint64_t sp_n_cap, sp_b_cap;
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
     hipStream_t hs[3];    // copy-in, classify, copy-out
     uint8_t *h_slab;      // device mirror of the host slab (same byte offsets)
@@ -1719,6 +1927,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_dir16 = 1;
     c->tune_cnet_tile = 1;
     c->host_chunk = 1u << 20;
+    c->spec_burst = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -1762,6 +1971,10 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         hipFree(c->m_dres);
     if (c->d_rw_tbl)
         hipFree(c->d_rw_tbl);
+    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt, c->sp_nh, c->sp_S, c->sp_T, c->sp_U};
+    for (void *q : sp)
+        if (q)
+            hipFree(q);
     if (c->d_ttab)
         hipFree(c->d_ttab);
     if (c->d_reta)
@@ -2129,6 +2342,42 @@ static int validate_batch(const cndp_gpu_ctx_t *c, const struct cndp_batch *b)
     return 0;
 }
 
+// scratch of the ptype-speculation pass, grown on demand
+static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
+{
+    if (!c->sp_small) {
+        HIP_TRY(hipMalloc((void **)&c->sp_small, 256 * 4));
+        HIP_TRY(hipMemset(c->sp_small, 0, 256 * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_class, 2048));
+        HIP_TRY(hipMalloc((void **)&c->sp_U, (size_t)SPEC_SCAN_THREADS * SPEC_KMAX * 4));
+    }
+    if (n > c->sp_n_cap) {
+        if (c->sp_pt)
+            HIP_TRY(hipFree(c->sp_pt));
+        if (c->sp_nh)
+            HIP_TRY(hipFree(c->sp_nh));
+        c->sp_pt = c->sp_nh = nullptr;
+        c->sp_n_cap = 0;
+        const uint64_t cap = n + (n >> 3) + 1024;
+        HIP_TRY(hipMalloc((void **)&c->sp_pt, cap * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_nh, cap * 4));
+        c->sp_n_cap = cap;
+    }
+    if (nb > c->sp_b_cap) {
+        if (c->sp_S)
+            HIP_TRY(hipFree(c->sp_S));
+        if (c->sp_T)
+            HIP_TRY(hipFree(c->sp_T));
+        c->sp_S = c->sp_T = nullptr;
+        c->sp_b_cap = 0;
+        const uint64_t cap = nb + (nb >> 3) + 64;
+        HIP_TRY(hipMalloc((void **)&c->sp_S, cap * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
+        c->sp_b_cap = cap;
+    }
+    return 0;
+}
+
 // rw_tx != nullptr asks for ip4_rewrite fused into the wave-tile kernel
 // (256-packet bursts); *fused says whether that kernel ran
 static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream, uint16_t *rw_tx,
@@ -2184,7 +2433,15 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         const uint32_t cap = (uint32_t)c->num_cu * 2u;
         if (g > cap)
             g = cap;
-        if (c->tune_cnet_tile) {
+        const uint32_t B = c->spec_burst;
+        if (B && (r = spec_scratch(c, b->n, ((uint64_t)b->n + B - 1) / B)))
+            return r;
+        if (B) {
+            if (!a.ptype)
+                a.ptype = c->sp_pt;
+            a.spec_nh = c->sp_nh;
+        }
+        if (c->tune_cnet_tile || B) {
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
             uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
             if (gt > cap)
@@ -2192,6 +2449,24 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             hipLaunchKernelGGL(k_classify_cnet_tile, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
         } else {
             hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
+        }
+        if (B) {
+            const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
+            uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
+            HIP_TRY(hipMemsetAsync(flags, 0, 64 * 4, s));
+            uint32_t gf = blocks_for(b->n, 256);
+            if (gf > (uint32_t)c->num_cu * 4u)
+                gf = (uint32_t)c->num_cu * 4u;
+            hipLaunchKernelGGL(k_spec_flags, dim3(gf), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, flags,
+                               (const uint32_t *)state);
+            hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta);
+            const uint32_t gb = (uint32_t)((nb + 255) / 256);
+            hipLaunchKernelGGL(k_spec_tables, dim3(gb), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, B, nb,
+                               (const uint32_t *)meta, c->sp_T);
+            hipLaunchKernelGGL(k_spec_scan, dim3(1), dim3(SPEC_SCAN_THREADS), 0, s, (const uint32_t *)a.ptype, b->n,
+                               B, nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)c->sp_T,
+                               c->sp_U, c->sp_S, state);
+            hipLaunchKernelGGL(k_spec_emit, dim3(gb), dim3(256), 0, s, a, B, nb, (const uint32_t *)c->sp_S);
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
@@ -2311,7 +2586,9 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
     uint64_t *d_bins = hb->bins ? (uint64_t *)(c->h_out + o_b) : nullptr;
     if (hb->bins)
         HIP_TRY(hipMemcpyAsync(d_bins, hb->bins, ((uint64_t)hb->n_bins + 2) * 8, hipMemcpyHostToDevice, cs));
-    const uint64_t C = c->host_chunk;
+    uint64_t C = c->host_chunk;
+    if (hb->mode == CNDP_MODE_CNET && c->spec_burst) // chunks hold whole graph bursts
+        C = C < c->spec_burst ? c->spec_burst : C - C % c->spec_burst;
     const uint64_t n_chunks = n ? (n + C - 1) / C : 0;
     const uint64_t n_segs = (hb->slab_len + CNDP_HOST_SEG - 1) / CNDP_HOST_SEG;
     uint64_t seg_done = 0; // segments issued so far
@@ -2925,6 +3202,13 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 2)
             return -EINVAL;
         c->tune_rw_wb = value;
+        return 0;
+    case CNDP_TUNE_CNET_SPEC:
+        if (value < 0)
+            return -EINVAL;
+        c->spec_burst = (uint32_t)value;
+        if (c->sp_small) // a new graph: ctx->last_type starts at 0 again
+            HIP_TRY(hipMemset(c->sp_small, 0, 4));
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

@@ -187,6 +187,11 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           overlapping the FIB gathers (default), 0 = per-lane rows
  *   CNDP_TUNE_HOST_CHUNK    packets per pipelined chunk of cndp_gpu_classify_host
  *                           (>= 1024, default 1M)
+ *   CNDP_TUNE_CNET_SPEC     cnet: graph burst size B of the ptype node's speculative
+ *                           4-wide loop (ptype.c:48-210, uint8_t fix_spec quirk
+ *                           included); the node state (last_type) persists across calls
+ *                           and is reset to 0 by setting this key.  0 = route every
+ *                           frame by p_nxt[its type] instead (default 256)
  *   CNDP_TUNE_RW_WB         fused classify+rewrite write-back: 0 = the 16-B parts the
  *                           rewrite touches of rewritten frames (default), 1 = whole
  *                           rewritten frames, 2 = whole tiles holding a rewrite */
@@ -198,6 +203,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_CNET_TILE 6
 #define CNDP_TUNE_HOST_CHUNK 7
 #define CNDP_TUNE_RW_WB 8
+#define CNDP_TUNE_CNET_SPEC 9
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

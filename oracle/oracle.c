@@ -699,6 +699,50 @@ static uint32_t hash_v6(struct pv v, uint32_t ip6, int l4ok, uint32_t l4, const 
     return orc_softrss(t, 8, key);
 }
 
+/* ip4_input.c:121-140 / ip6_input.c:115-135 for a frame the ptype node
+ * sends to edge pe (ip = its L3 offset); other edges: 0x80 | pe */
+static void cnet_input(const struct orc_classify_args *a, struct pv v, uint32_t ip, uint8_t pe, uint32_t *nh,
+                       uint8_t *edge)
+{
+    if (pe == PTN_IP4) {
+        uint8_t hdr[60]; /* cksum over the bounded view */
+        for (int k = 0; k < 60; k++)
+            hdr[k] = v8(v, ip + (uint32_t)k);
+        uint32_t tl = vbe16(v, ip + 2);
+        uint32_t dip = 0;
+        if (tl < a->buf_len && orc_ipv4_cksum(hdr) == 0)
+            dip = vbe32(v, ip + 16);
+        *nh = lookup4(a->tbl24, a->tbl8, dip);
+        *edge = (uint8_t)(*nh >> 24);
+    } else if (pe == PTN_IP6) {
+        uint8_t dip[16];
+        memset(dip, 0, 16);
+        if ((uint32_t)vbe16(v, ip + 4) < a->buf_len)
+            for (int k = 0; k < 16; k++)
+                dip[k] = v8(v, ip + 24 + (uint32_t)k);
+        *nh = lookup6(a->tbl24_6, a->tbl8_6, dip);
+        *edge = (uint8_t)(*nh >> 24);
+    } else {
+        *nh = NH_INVALID;
+        *edge = (uint8_t)(0x80u | pe);
+    }
+}
+
+static uint32_t bin_for(const struct orc_classify_args *a, uint32_t nh, uint8_t edge, uint32_t q)
+{
+    const uint32_t nb = a->n_bins;
+    if (a->mode == MODE_HASH)
+        return q < nb ? q : nb + 1;
+    if (a->mode == MODE_L3FWD) {
+        if (edge == 0)
+            return (nh & 0xffffu) < nb ? (nh & 0xffffu) : nb + 1;
+        return (edge == 1 || edge == 0xFF) ? nb : nb + 1;
+    }
+    if (edge == 1)
+        return (nh & 0xffffffu) < nb ? (nh & 0xffffffu) : nb + 1;
+    return (edge == 0 || edge == (0x80u | PTN_DROP)) ? nb : nb + 1;
+}
+
 static void classify_one(const struct orc_classify_args *a, uint32_t i)
 {
     uint64_t base = (a->offsets ? a->offsets[i] : (uint64_t)i * a->stride) + a->data_off;
@@ -764,29 +808,7 @@ static void classify_one(const struct orc_classify_args *a, uint32_t i)
         else if (l3 & 0x40u)
             hash = hash_v6(v, ip, l4ok, ip + hl.l3_len, a->rss_key);
         uint8_t pe = cnet_ptype_edge(pt);
-        if (pe == PTN_IP4) {
-            /* ip4_input.c:121-140 (cksum over the bounded view) */
-            uint8_t hdr[60];
-            for (int k = 0; k < 60; k++)
-                hdr[k] = v8(v, ip + (uint32_t)k);
-            uint32_t tl = vbe16(v, ip + 2);
-            uint32_t dip = 0;
-            if (tl < a->buf_len && orc_ipv4_cksum(hdr) == 0)
-                dip = vbe32(v, ip + 16);
-            nh = lookup4(a->tbl24, a->tbl8, dip);
-            edge = (uint8_t)(nh >> 24);
-        } else if (pe == PTN_IP6) {
-            /* ip6_input.c:115-135 */
-            uint8_t dip[16];
-            memset(dip, 0, 16);
-            if ((uint32_t)vbe16(v, ip + 4) < a->buf_len)
-                for (int k = 0; k < 16; k++)
-                    dip[k] = v8(v, ip + 24 + (uint32_t)k);
-            nh = lookup6(a->tbl24_6, a->tbl8_6, dip);
-            edge = (uint8_t)(nh >> 24);
-        } else {
-            edge = (uint8_t)(0x80u | pe);
-        }
+        cnet_input(a, v, ip, pe, &nh, &edge);
     }
 
     uint32_t q = a->reta[hash & (a->reta_size - 1)];
@@ -818,6 +840,89 @@ static void classify_one(const struct orc_classify_args *a, uint32_t i)
         a->bins[bin]++;
 }
 
+/* cnet with the ptype node's speculation (ptype.c:48-210), restated loop
+ * for loop: per graph burst of B packets, 4-wide groups compared against
+ * last_type with the uint8_t fix_spec (:109-110) -- a group whose four low
+ * bytes equal last_type's goes whole to the speculated edge p_nxt[last_type]
+ * -- then the per-packet tail.  last_type persists across bursts (and across
+ * calls through spec_state; ctx->last_type starts at 0).  A frame sent to an
+ * input node other than its own then gets that node's result. */
+static int classify_cnet_spec(const struct orc_classify_args *a)
+{
+    const uint32_t n = a->n, B = a->spec_burst;
+    uint16_t *l = malloc((size_t)(n ? n : 1) * sizeof(uint16_t));
+    uint8_t *dst = malloc(n ? n : 1);
+    uint32_t *pts = a->ptype ? NULL : malloc((size_t)(n ? n : 1) * 4);
+    if (!l || !dst || (!a->ptype && !pts)) {
+        free(l);
+        free(dst);
+        free(pts);
+        return -ENOMEM;
+    }
+    struct orc_classify_args b = *a;
+    if (!b.ptype)
+        b.ptype = pts;
+    for (uint32_t i = 0; i < n; i++) {
+        classify_one(&b, i);
+        l[i] = (uint16_t)(b.ptype[i] & 0xffffu);
+    }
+    uint16_t last_type = a->spec_state ? *a->spec_state : 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += B) {
+        const uint32_t nb = n - b0 < B ? n - b0 : B;
+        uint16_t next_index = cnet_ptype_edge(last_type);
+        uint32_t k = 0;
+        for (; k + 4 <= nb; k += 4) {
+            const uint16_t *g = l + b0 + k;
+            uint8_t fix_spec = (uint8_t)((last_type ^ g[0]) | (last_type ^ g[1]) | (last_type ^ g[2]) |
+                                         (last_type ^ g[3]));
+            if (fix_spec) {
+                for (int j = 0; j < 4; j++)
+                    dst[b0 + k + j] = cnet_ptype_edge(g[j]);
+                if (last_type != g[3] && g[2] == g[3] && next_index != cnet_ptype_edge(g[3])) {
+                    next_index = cnet_ptype_edge(g[3]);
+                    last_type = g[3];
+                } else if (next_index == cnet_ptype_edge(g[3])) {
+                    last_type = g[3];
+                }
+            } else {
+                for (int j = 0; j < 4; j++)
+                    dst[b0 + k + j] = (uint8_t)next_index;
+            }
+        }
+        for (; k < nb; k++) /* tail (:184-200): every frame to p_nxt[its type] */
+            dst[b0 + k] = cnet_ptype_edge(l[b0 + k]);
+    }
+    if (a->spec_state)
+        *a->spec_state = last_type;
+    /* frames the speculation sent somewhere else than p_nxt[own type] */
+    for (uint32_t i = 0; i < n; i++) {
+        if (dst[i] == cnet_ptype_edge(l[i]))
+            continue;
+        uint64_t base = (a->offsets ? a->offsets[i] : (uint64_t)i * a->stride) + a->data_off;
+        struct pv v = {a->slab + base, base < a->slab_len ? a->slab_len - base : 0};
+        struct orc_hdr_lens hl;
+        memset(&hl, 0, sizeof(hl));
+        (void)orc_get_ptype(v.p, v.avail, &hl, 0x0fffffffu);
+        const uint8_t old_edge = (uint8_t)(a->nh[i] == NH_INVALID ? 0x80u | cnet_ptype_edge(l[i])
+                                                                   : (a->nh[i] >> 24));
+        const uint32_t old_nh = a->nh[i];
+        uint32_t nh;
+        uint8_t edge;
+        cnet_input(a, v, hl.l2_len, dst[i], &nh, &edge);
+        a->nh[i] = nh;
+        if (a->edge)
+            a->edge[i] = edge;
+        if (a->bins) {
+            a->bins[bin_for(a, old_nh, old_edge, a->queue[i])]--;
+            a->bins[bin_for(a, nh, edge, a->queue[i])]++;
+        }
+    }
+    free(l);
+    free(dst);
+    free(pts);
+    return 0;
+}
+
 int orc_classify(const struct orc_classify_args *a)
 {
     if (!a || !a->slab || !a->rss_key || !a->reta || !a->nh || !a->hash || !a->queue)
@@ -830,6 +935,8 @@ int orc_classify(const struct orc_classify_args *a)
         return -EINVAL;
     if (a->mode == MODE_CNET && (!a->tbl24_6 || !a->tbl8_6))
         return -EINVAL;
+    if (a->mode == MODE_CNET && a->spec_burst)
+        return classify_cnet_spec(a);
     for (uint32_t i = 0; i < a->n; i++)
         classify_one(a, i);
     return 0;

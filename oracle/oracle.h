@@ -116,6 +116,10 @@ struct orc_classify_args {
     uint32_t *ptype;            /* may be NULL: m->packet_type (eth_rx.c:41 / pktdev_rx.c:24-34) */
     uint32_t *rxmeta;           /* may be NULL (cnet): eth_rx.c:43-60 lengths + ol_flags, packed
                                  * as in cndp_gpu.h */
+    uint32_t spec_burst;        /* cnet: 0 = route by p_nxt[ptype] per packet; B > 0 = the
+                                 * ptype node's speculative 4-wide loop (ptype.c:48-210) over
+                                 * graph bursts of B packets, uint8_t fix_spec quirk included */
+    uint16_t *spec_state;       /* in/out: the node's ctx->last_type (NULL = start at 0) */
 };
 int orc_classify(const struct orc_classify_args *a);
 

@@ -39,7 +39,8 @@ class ClassifyArgs(Structure):
                 ("tbl24", c_void_p), ("tbl8", c_void_p), ("tbl24_6", c_void_p), ("tbl8_6", c_void_p),
                 ("rss_key", c_void_p), ("reta", c_void_p), ("reta_size", c_uint32), ("n_bins", c_uint32),
                 ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p), ("edge", c_void_p),
-                ("bins", c_void_p), ("ptype", c_void_p), ("rxmeta", c_void_p)]
+                ("bins", c_void_p), ("ptype", c_void_p), ("rxmeta", c_void_p), ("spec_burst", c_uint32),
+                ("spec_state", c_void_p)]
 
 
 _lib = None
@@ -181,7 +182,7 @@ def get_ptype(pkt: bytes):
 
 
 def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, tables4=None,
-              tables6=None, key=None, reta=None, n_bins=64):
+              tables6=None, key=None, reta=None, n_bins=64, spec_burst=0, spec_state=None):
     from cndp_amd.native import MS_RSS_KEY
     key = np.frombuffer(key or MS_RSS_KEY, dtype=np.uint8).copy()
     reta = np.ascontiguousarray(reta if reta is not None else (np.arange(128) % 16), dtype=np.uint16)
@@ -201,7 +202,10 @@ def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, 
     a.nh, a.hash, a.queue, a.edge, a.bins = (_p(out["nh"]), _p(out["hash"]), _p(out["queue"]),
                                             _p(out["edge"]), _p(out["bins"]))
     a.ptype, a.rxmeta = _p(out["ptype"]), _p(out["rxmeta"])
-    keep = (slab, off, key, reta, tables4, tables6)  # keep buffers alive with the struct
+    a.spec_burst = spec_burst
+    if spec_state is not None:   # np.uint16 array of 1, updated in place
+        a.spec_state = _p(spec_state)
+    keep = (slab, off, key, reta, tables4, tables6, spec_state)  # keep buffers alive with the struct
     return a, out, keep
 
 

@@ -48,12 +48,17 @@ def cnet_fibs():
 
 
 def oracle_classify(mode, frames, tables4=None, tables6=None, n_bins=64, reta=None, key=None,
-                    buf_len=1984):
+                    buf_len=1984, spec_burst=None, spec_state=None):
+    """The oracle over a Frames batch.  cnet mode models the ptype node's
+    speculation over 256-packet bursts from state 0 (the library default
+    after a reset) unless spec_burst says otherwise."""
     slab = frames.slab.cpu().numpy()
     offs = frames.offsets.cpu().numpy().astype(np.uint64) if frames.offsets is not None else None
+    if spec_burst is None:
+        spec_burst = 256 if mode == O.MODE_CNET else 0
     return O.classify(mode, slab, frames.n, stride=frames.stride, offsets=offs, data_off=frames.data_off,
                       tables4=tables4, tables6=tables6, n_bins=n_bins, reta=reta, key=key,
-                      buf_len=buf_len)
+                      buf_len=buf_len, spec_burst=spec_burst, spec_state=spec_state)
 
 
 DT = {"nh": np.uint32, "hash": np.uint32, "queue": np.uint16, "edge": np.uint8, "bins": np.uint64,

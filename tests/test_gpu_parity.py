@@ -42,6 +42,8 @@ def cnet(gpu):
 
 
 def run_gpu(cl, frames, mode, n_bins=64, buf_len=1984):
+    if mode == N.CNDP_MODE_CNET:
+        cl.set_tuning(cnet_spec=256)   # fresh ptype-node state, like the oracle
     out = cl.classify(frames, mode, n_bins=n_bins, buf_len=buf_len)
     torch.cuda.synchronize()
     return {k: v for k, v in out.items() if k != "n_bins"}
@@ -205,6 +207,7 @@ def test_classify_host_chunked(l3, cnet, gpu):
                    pktgen.fuzz_frames(20000, seed=8, slot=128)):
             ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
             offs = fr.offsets.numpy().astype(np.uint64) if fr.offsets is not None else None
+            ccl.set_tuning(cnet_spec=256)
             got = ccl.classify_host(fr.slab.numpy(), fr.n, N.CNDP_MODE_CNET, stride=fr.stride, offsets=offs,
                                     data_off=fr.data_off)
             assert_same(got, ref)
@@ -564,7 +567,7 @@ def test_cnet_ptype_and_rxmeta(cnet, l3, gpu):
                pktgen.imix(20000, v4routes=routes, v6routes=v6, device=gpu, seed=4)):
         ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
         for ct in CNET_KERNELS:
-            ccl.set_tuning(cnet_tile=ct)
+            ccl.set_tuning(cnet_tile=ct, cnet_spec=256)
             out = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
             ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
             torch.cuda.synchronize()
@@ -579,3 +582,62 @@ def test_cnet_ptype_and_rxmeta(cnet, l3, gpu):
         torch.cuda.synchronize()
         assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
     cl.set_tuning(tile=4)
+
+
+def _gtp_mix(n, routes, v6, gpu, seed):
+    """IMIX with GTP-U (UDP dport 2152 / 2123) and TCP frames mixed into
+    runs of plain IPv4 UDP, so 4-groups share the low ptype byte but not
+    the next edge -- the case the uint8_t fix_spec mis-routes."""
+    fr = pktgen.imix(n, v4routes=routes, v6routes=v6, device="cpu", seed=seed, v6_frac=0.2)
+    g = torch.Generator().manual_seed(seed)
+    k = torch.arange(n)
+    base = fr.offsets + fr.data_off
+    is4 = (fr.slab[base + 12] == 0x08) & (fr.slab[base + 13] == 0x00)
+    pick = torch.rand(n, generator=g)
+    gtpu = is4 & (pick < 0.15)
+    gtpc = is4 & (pick >= 0.15) & (pick < 0.2)
+    tcp = is4 & (pick >= 0.2) & (pick < 0.25)
+    fr.slab[base[gtpu] + 36] = 2152 >> 8
+    fr.slab[base[gtpu] + 37] = 2152 & 0xFF
+    fr.slab[base[gtpc] + 36] = 2123 >> 8
+    fr.slab[base[gtpc] + 37] = 2123 & 0xFF
+    fr.slab[base[tcp] + 23] = 6
+    del k
+    return pktgen.Frames(fr.slab.to(gpu), n, offsets=fr.offsets.to(gpu))
+
+
+@pytest.mark.parametrize("burst", [256, 7, 64])
+def test_cnet_ptype_speculation(cnet, gpu, burst):
+    """ptype.c:48-210 speculation incl. the uint8_t fix_spec quirk: GPU ==
+    the restated node loop, across bursts and across calls (state kept)."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = _gtp_mix(40000, routes, v6, gpu, seed=burst)
+    plain = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=burst)
+    assert (plain["edge"] != ref["edge"]).sum() > 0, "input does not exercise the quirk"
+    ccl.set_tuning(cnet_spec=burst)
+    out = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+    ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
+    torch.cuda.synchronize()
+    assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    # two calls over halves (cut on a burst boundary) == one call: the node state persists
+    cut = (fr.n // 2) // burst * burst
+    st = np.zeros(1, np.uint16)
+    ccl.set_tuning(cnet_spec=burst)
+    for lo, hi in ((0, cut), (cut, fr.n)):
+        part = pktgen.Frames(fr.slab, hi - lo, offsets=fr.offsets[lo:hi].contiguous())
+        r = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=burst, spec_state=st)
+        o = ccl.alloc_outputs(part.n, 64, device=gpu)
+        ccl.classify(part, N.CNDP_MODE_CNET, out=o)
+        torch.cuda.synchronize()
+        assert_same(o, r)
+    ccl.set_tuning(cnet_spec=256)
+
+
+def test_cnet_speculation_many_signatures(cnet, gpu):
+    """More distinct ptype signatures than the scan handles (fuzz): the
+    sequential fallback gives the same answer as the node loop."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    for seed in (5, 6):
+        fr = pktgen.fuzz_frames(30000, seed=seed, slot=128, device=gpu)
+        assert_same(run_gpu(ccl, fr, N.CNDP_MODE_CNET), oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6))
