@@ -134,6 +134,11 @@ def parity_sample(state, k: int = 1 << 16) -> bool:
     kw = dict(tables4=(t24, t8))
     if state["mode"] == N.CNDP_MODE_CNET:
         kw["tables6"] = tuple(x.copy() for x in state["fib6"].image())
+        # the ptype-node model is stateful: restart it (last_type = 0), redo
+        # one pass, and compare with the node loop from the same state
+        kw["spec_burst"] = 256
+        cl.set_tuning(cnet_spec=256)
+        cl.classify(fr, state["mode"], out=state["out"])
     if fr.offsets is not None:
         offs = fr.offsets[:k].cpu().numpy().astype(np.uint64)
         end = int(offs[-1]) + 2048

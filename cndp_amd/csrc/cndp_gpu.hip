@@ -1507,13 +1507,33 @@ __global__ void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_
     meta[0] = k;
 }
 
+// the 4 types of the group at packet j (16-B load when the burst size keeps
+// groups 16-B aligned)
+__device__ __forceinline__ void spec_group(const uint32_t *__restrict__ pt, uint64_t j, bool vec, uint32_t &l0,
+                                           uint32_t &l1, uint32_t &l2, uint32_t &l3)
+{
+    if (vec) {
+        const u32x4 q = *(const u32x4 *)(pt + j);
+        l0 = q.x & 0xffffu;
+        l1 = q.y & 0xffffu;
+        l2 = q.z & 0xffffu;
+        l3 = q.w & 0xffffu;
+    } else {
+        l0 = pt[j] & 0xffffu;
+        l1 = pt[j + 1] & 0xffffu;
+        l2 = pt[j + 2] & 0xffffu;
+        l3 = pt[j + 3] & 0xffffu;
+    }
+}
+
 // one burst's effect on a state of signature sig: SPEC_UNCH or the new state
-__device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0, uint32_t cnt, uint32_t sig)
+__device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0, uint32_t cnt, uint32_t sig,
+                                   bool vec)
 {
     uint32_t low = sig >> 3, E = sig & 7u, c = SPEC_UNCH;
     for (uint32_t g = 0; g + 4 <= cnt; g += 4) {
-        const uint32_t l0 = pt[b0 + g] & 0xffffu, l1 = pt[b0 + g + 1] & 0xffffu;
-        const uint32_t l2 = pt[b0 + g + 2] & 0xffffu, l3 = pt[b0 + g + 3] & 0xffffu;
+        uint32_t l0, l1, l2, l3;
+        spec_group(pt, b0 + g, vec, l0, l1, l2, l3);
         const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low && (l3 & 0xffu) == low;
         if (!quiet && (l2 == l3 || E == cnet_edge(l3))) {
             c = l3;
@@ -1525,7 +1545,7 @@ __device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0,
 }
 
 __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, const uint32_t *meta, uint32_t *T)
+                                                     uint64_t nb, const uint32_t *meta, uint32_t *T, bool vec)
 {
     const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t K = meta[0];
@@ -1534,7 +1554,7 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
     const uint64_t b0 = b * B;
     const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
     for (uint32_t k = 0; k < K; k++)
-        T[b * SPEC_KMAX + k] = spec_burst_map(pt, b0, cnt, meta[1 + k]);
+        T[b * SPEC_KMAX + k] = spec_burst_map(pt, b0, cnt, meta[1 + k], vec);
 }
 
 __global__ __launch_bounds__(SPEC_SCAN_THREADS) void k_spec_scan(const uint32_t *__restrict__ pt, uint32_t n,
@@ -1551,7 +1571,7 @@ __global__ __launch_bounds__(SPEC_SCAN_THREADS) void k_spec_scan(const uint32_t 
                 S[b] = st;
                 const uint64_t b0 = b * B;
                 const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
-                const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st));
+                const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
                 if (c != SPEC_UNCH)
                     st = c;
             }
@@ -1615,7 +1635,7 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
     }
 }
 
-__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *S)
+__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *S, bool vec)
 {
     const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (b >= nb)
@@ -1625,8 +1645,7 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
     uint32_t st = S[b], low = st & 0xffu, E = cnet_edge(st);
     for (uint32_t g = 0; g + 4 <= cnt; g += 4) {
         uint32_t l[4];
-        for (int j = 0; j < 4; j++)
-            l[j] = a.ptype[b0 + g + j] & 0xffffu;
+        spec_group(a.ptype, b0 + g, vec, l[0], l[1], l[2], l[3]);
         const bool quiet = (l[0] & 0xffu) == low && (l[1] & 0xffu) == low && (l[2] & 0xffu) == low &&
                            (l[3] & 0xffu) == low;
         if (quiet) {
@@ -2461,12 +2480,13 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                (const uint32_t *)state);
             hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta);
             const uint32_t gb = (uint32_t)((nb + 255) / 256);
+            const bool vec = (B & 3u) == 0 && (((uintptr_t)a.ptype) & 15u) == 0;
             hipLaunchKernelGGL(k_spec_tables, dim3(gb), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, B, nb,
-                               (const uint32_t *)meta, c->sp_T);
+                               (const uint32_t *)meta, c->sp_T, vec);
             hipLaunchKernelGGL(k_spec_scan, dim3(1), dim3(SPEC_SCAN_THREADS), 0, s, (const uint32_t *)a.ptype, b->n,
                                B, nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)c->sp_T,
                                c->sp_U, c->sp_S, state);
-            hipLaunchKernelGGL(k_spec_emit, dim3(gb), dim3(256), 0, s, a, B, nb, (const uint32_t *)c->sp_S);
+            hipLaunchKernelGGL(k_spec_emit, dim3(gb), dim3(256), 0, s, a, B, nb, (const uint32_t *)c->sp_S, vec);
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
