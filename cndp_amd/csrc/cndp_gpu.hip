@@ -1465,7 +1465,6 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
 // ---------------------------------------------------------------------------
 #define SPEC_KMAX 64
 #define SPEC_UNCH 0xFFFFFFFFu
-#define SPEC_SCAN_THREADS 1024
 
 __device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
 
@@ -1557,65 +1556,93 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
         T[b * SPEC_KMAX + k] = spec_burst_map(pt, b0, cnt, meta[1 + k], vec);
 }
 
-__global__ __launch_bounds__(SPEC_SCAN_THREADS) void k_spec_scan(const uint32_t *__restrict__ pt, uint32_t n,
-                                                                uint32_t B, uint64_t nb, const uint32_t *meta,
-                                                                const uint8_t *class_id, const uint32_t *T,
-                                                                uint32_t *U, uint32_t *S, uint32_t *state)
+// Burst maps are composed with a two-level LDS scan when at most
+// SPEC_KFAST signatures occur (a map is then SPEC_KFAST registers); the
+// composition "E then L" sends a class k through E, then through L.
+#define SPEC_KFAST 8
+#define SPEC_BLK 256
+
+__device__ __forceinline__ uint32_t spec_apply(const uint32_t *m, const uint8_t *cls, uint32_t st)
 {
-    __shared__ uint32_t s_start[SPEC_SCAN_THREADS];
-    const uint32_t tid = threadIdx.x, K = meta[0];
-    if (K > SPEC_KMAX) { // too many signatures: one sequential walk
-        if (tid == 0) {
-            uint32_t st = *state & 0xffffu;
-            for (uint64_t b = 0; b < nb; b++) {
-                S[b] = st;
-                const uint64_t b0 = b * B;
-                const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
-                const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
-                if (c != SPEC_UNCH)
-                    st = c;
-            }
-            *state = st;
-        }
+    const uint32_t nx = m[cls[spec_sig(st)]];
+    return nx == SPEC_UNCH ? st : nx;
+}
+
+// per block of SPEC_BLK bursts: inclusive scan of the burst maps (P), and the
+// block's total map (Bt)
+__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint8_t *class_id,
+                                                        const uint32_t *T, uint32_t *P, uint32_t *Bt)
+{
+    __shared__ uint8_t s_cls[2048];
+    __shared__ uint32_t s_m[SPEC_BLK][SPEC_KFAST];
+    const uint32_t K = meta[0];
+    if (K > SPEC_KFAST)
         return;
-    }
-    const uint64_t C = (nb + SPEC_SCAN_THREADS - 1) / SPEC_SCAN_THREADS;
-    const uint64_t lo = tid * C < nb ? tid * C : nb, hi = lo + C < nb ? lo + C : nb;
-    uint32_t *u = U + (uint64_t)tid * SPEC_KMAX;
-    for (uint32_t k = 0; k < K; k++)
-        u[k] = SPEC_UNCH;
-    for (uint64_t b = lo; b < hi; b++) {
-        const uint32_t *t = T + b * SPEC_KMAX;
-        for (uint32_t k = 0; k < K; k++) {
-            const uint32_t cur = u[k];
-            if (cur == SPEC_UNCH) {
-                u[k] = t[k];
-            } else {
-                const uint32_t nx = t[class_id[spec_sig(cur)]];
-                if (nx != SPEC_UNCH)
-                    u[k] = nx;
+    for (uint32_t k = threadIdx.x; k < 2048; k += SPEC_BLK)
+        s_cls[k] = class_id[k];
+    const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + threadIdx.x;
+    uint32_t m[SPEC_KFAST];
+#pragma unroll
+    for (uint32_t k = 0; k < SPEC_KFAST; k++)
+        m[k] = b < nb && k < K ? T[b * SPEC_KMAX + k] : SPEC_UNCH;
+    for (uint32_t d = 1; d < SPEC_BLK; d <<= 1) {
+#pragma unroll
+        for (uint32_t k = 0; k < SPEC_KFAST; k++)
+            s_m[threadIdx.x][k] = m[k];
+        __syncthreads();
+        if (threadIdx.x >= d) {
+            const uint32_t *e = s_m[threadIdx.x - d]; // earlier map, then ours
+            const uint32_t *l = s_m[threadIdx.x];
+#pragma unroll
+            for (uint32_t k = 0; k < SPEC_KFAST; k++) {
+                if (k >= K)
+                    break;
+                const uint32_t ek = e[k];
+                m[k] = ek == SPEC_UNCH ? l[k] : spec_apply(l, s_cls, ek);
             }
         }
+        __syncthreads();
     }
+    if (b < nb)
+        for (uint32_t k = 0; k < K; k++)
+            P[b * SPEC_KFAST + k] = m[k];
+    if (threadIdx.x == SPEC_BLK - 1)
+        for (uint32_t k = 0; k < K; k++)
+            Bt[(uint64_t)blockIdx.x * SPEC_KFAST + k] = m[k];
+}
+
+// start state of every block (walking the block totals) and the final state;
+// with more than SPEC_KFAST signatures: one sequential walk over the bursts
+__global__ __launch_bounds__(64) void k_spec_scan_b(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                   uint64_t nb, uint64_t nblk, const uint32_t *meta,
+                                                   const uint8_t *class_id, const uint32_t *Bt, uint32_t *Sblk,
+                                                   uint32_t *S, uint32_t *state)
+{
+    __shared__ uint8_t s_cls[2048];
+    for (uint32_t k = threadIdx.x; k < 2048; k += 64)
+        s_cls[k] = class_id[k];
     __syncthreads();
-    if (tid == 0) {
-        uint32_t st = *state & 0xffffu;
-        for (uint32_t w = 0; w < SPEC_SCAN_THREADS; w++) {
-            s_start[w] = st;
-            const uint32_t nx = U[(uint64_t)w * SPEC_KMAX + class_id[spec_sig(st)]];
-            if (nx != SPEC_UNCH)
-                st = nx;
+    if (threadIdx.x != 0)
+        return;
+    const uint32_t K = meta[0];
+    uint32_t st = *state & 0xffffu;
+    if (K > SPEC_KFAST) {
+        for (uint64_t b = 0; b < nb; b++) {
+            S[b] = st;
+            const uint64_t b0 = b * B;
+            const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
+            const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
+            if (c != SPEC_UNCH)
+                st = c;
         }
         *state = st;
+        return;
     }
-    __syncthreads();
-    uint32_t st = s_start[tid];
-    for (uint64_t b = lo; b < hi; b++) {
-        S[b] = st;
-        const uint32_t nx = T[b * SPEC_KMAX + class_id[spec_sig(st)]];
-        if (nx != SPEC_UNCH)
-            st = nx;
+    for (uint64_t k = 0; k < nblk; k++) {
+        Sblk[k] = st;
+        st = spec_apply(Bt + k * SPEC_KFAST, s_cls, st);
     }
+    *state = st;
 }
 
 __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
@@ -1635,14 +1662,25 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
     }
 }
 
-__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *S, bool vec)
+__global__ __launch_bounds__(SPEC_BLK) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *meta,
+                                                       const uint8_t *class_id, const uint32_t *P,
+                                                       const uint32_t *Sblk, const uint32_t *S, bool vec)
 {
-    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ uint8_t s_cls[2048];
+    for (uint32_t k = threadIdx.x; k < 2048; k += SPEC_BLK)
+        s_cls[k] = class_id[k];
+    __syncthreads();
+    const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + threadIdx.x;
     if (b >= nb)
         return;
     const uint64_t b0 = b * B;
     const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
-    uint32_t st = S[b], low = st & 0xffu, E = cnet_edge(st);
+    uint32_t st;
+    if (meta[0] > SPEC_KFAST)
+        st = S[b];
+    else // block start state through the block's earlier bursts (exclusive prefix)
+        st = threadIdx.x == 0 ? Sblk[blockIdx.x] : spec_apply(P + (b - 1) * SPEC_KFAST, s_cls, Sblk[blockIdx.x]);
+    uint32_t low = st & 0xffu, E = cnet_edge(st);
     for (uint32_t g = 0; g + 4 <= cnt; g += 4) {
         uint32_t l[4];
         spec_group(a.ptype, b0 + g, vec, l[0], l[1], l[2], l[3]);
@@ -2368,7 +2406,6 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
         HIP_TRY(hipMalloc((void **)&c->sp_small, 256 * 4));
         HIP_TRY(hipMemset(c->sp_small, 0, 256 * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_class, 2048));
-        HIP_TRY(hipMalloc((void **)&c->sp_U, (size_t)SPEC_SCAN_THREADS * SPEC_KMAX * 4));
     }
     if (n > c->sp_n_cap) {
         if (c->sp_pt)
@@ -2387,11 +2424,15 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
             HIP_TRY(hipFree(c->sp_S));
         if (c->sp_T)
             HIP_TRY(hipFree(c->sp_T));
-        c->sp_S = c->sp_T = nullptr;
+        if (c->sp_U)
+            HIP_TRY(hipFree(c->sp_U));
+        c->sp_S = c->sp_T = c->sp_U = nullptr;
         c->sp_b_cap = 0;
         const uint64_t cap = nb + (nb >> 3) + 64;
         HIP_TRY(hipMalloc((void **)&c->sp_S, cap * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
+        // inclusive burst prefixes + block totals + block start states
+        HIP_TRY(hipMalloc((void **)&c->sp_U, (cap * SPEC_KFAST + (cap / SPEC_BLK + 2) * (SPEC_KFAST + 1)) * 4));
         c->sp_b_cap = cap;
     }
     return 0;
@@ -2483,10 +2524,16 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             const bool vec = (B & 3u) == 0 && (((uintptr_t)a.ptype) & 15u) == 0;
             hipLaunchKernelGGL(k_spec_tables, dim3(gb), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, B, nb,
                                (const uint32_t *)meta, c->sp_T, vec);
-            hipLaunchKernelGGL(k_spec_scan, dim3(1), dim3(SPEC_SCAN_THREADS), 0, s, (const uint32_t *)a.ptype, b->n,
-                               B, nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)c->sp_T,
-                               c->sp_U, c->sp_S, state);
-            hipLaunchKernelGGL(k_spec_emit, dim3(gb), dim3(256), 0, s, a, B, nb, (const uint32_t *)c->sp_S, vec);
+            const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
+            uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
+            hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb, (const uint32_t *)meta,
+                               (const uint8_t *)c->sp_class, (const uint32_t *)c->sp_T, P, Bt);
+            hipLaunchKernelGGL(k_spec_scan_b, dim3(1), dim3(64), 0, s, (const uint32_t *)a.ptype, b->n, B, nb, nblk,
+                               (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk,
+                               c->sp_S, state);
+            hipLaunchKernelGGL(k_spec_emit, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, a, B, nb,
+                               (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
+                               (const uint32_t *)Sblk, (const uint32_t *)c->sp_S, vec);
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
