@@ -190,7 +190,8 @@ def sweep(st, stream, cfg):
     variants += [dict(tile=2, nt=1, unroll=1, blocks_per_cu=4), dict(tile=3, nt=0, unroll=1, blocks_per_cu=4)]
     variants = [dict(v, dir16=1) for v in variants] + [dict(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=0)]
     if mode == N.CNDP_MODE_CNET:
-        variants = [dict(cnet_tile=ct, dir16=d) for ct in (1, 0) for d in (1, 0)]
+        variants = [dict(cnet_tile=ct, dir16=d, cnet_spec=sp) for sp in (256, 0) for ct in (1, 0) for d in (1, 0)
+                    if sp == 256 or (ct == 1 and d == 1)]
     if "tx" in st:
         variants = [dict(rw_wb=w, nt=nt, tile=4) for w in (0, 1, 2) for nt in (1, 0)] + [dict(tile=1, rw_wb=0)]
     for v in variants:
@@ -212,7 +213,7 @@ def sweep(st, stream, cfg):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1, rw_wb=0)
+    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1, rw_wb=2)
 
 
 def e2e_host(st, reps: int = 5):

@@ -1475,9 +1475,23 @@ __global__ __launch_bounds__(256) void k_spec_flags(const uint32_t *__restrict__
     if (threadIdx.x < 64)
         s_f[threadIdx.x] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint32_t g = spec_sig(pt[i] & 0xffffu);
-        atomicOr(&s_f[g >> 5], 1u << (g & 31u));
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint32_t g = i < n ? spec_sig(pt[i] & 0xffffu) : 0u;
+        uint32_t w = g >> 5, bit = 1u << (g & 31u);
+        // one LDS atomic per distinct flag word in the wave (a batch holds few)
+        bool todo = i < n;
+        while (__any(todo)) {
+            const uint32_t lead = __shfl(w, __ffsll((unsigned long long)__ballot(todo)) - 1);
+            const bool mine = todo && w == lead;
+            const unsigned long long mm = __ballot(mine);
+            uint32_t v = mine ? bit : 0u;
+            for (int o = 32; o > 0; o >>= 1)
+                v |= __shfl_xor(v, o);
+            if (mine && (uint32_t)__lane_id() == (uint32_t)(__ffsll(mm) - 1))
+                atomicOr(&s_f[lead], v);
+            todo = todo && !mine;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const uint32_t g = spec_sig(*state & 0xffffu);
@@ -1489,21 +1503,31 @@ __global__ __launch_bounds__(256) void k_spec_flags(const uint32_t *__restrict__
 }
 
 // meta[0] = K, meta[1 + k] = signature of class k; class_id[sig] = k or 0xFF
-__global__ void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta)
+// (64 threads: thread t owns flag word t, classes numbered in signature order)
+__global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta)
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0)
-        return;
-    uint32_t k = 0;
-    for (uint32_t g = 0; g < 2048; g++) {
-        const bool on = (flags[g >> 5] >> (g & 31u)) & 1u;
-        class_id[g] = on && k < SPEC_KMAX ? (uint8_t)k : (uint8_t)0xFF;
-        if (on) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = flags[t], cnt = (uint32_t)__popc(w);
+    uint32_t pre = cnt; // inclusive wave prefix
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(pre, o);
+        if ((int)t >= o)
+            pre += v;
+    }
+    uint32_t k = pre - cnt;
+    for (uint32_t j = 0; j < 32; j++) {
+        const uint32_t g = t * 32 + j;
+        if ((w >> j) & 1u) {
+            class_id[g] = k < SPEC_KMAX ? (uint8_t)k : (uint8_t)0xFF;
             if (k < SPEC_KMAX)
                 meta[1 + k] = g;
             k++;
+        } else {
+            class_id[g] = 0xFF;
         }
     }
-    meta[0] = k;
+    if (t == 63)
+        meta[0] = pre;
 }
 
 // the 4 types of the group at packet j (16-B load when the burst size keeps
@@ -1626,7 +1650,9 @@ __global__ __launch_bounds__(64) void k_spec_scan_b(const uint32_t *__restrict__
         return;
     const uint32_t K = meta[0];
     uint32_t st = *state & 0xffffu;
-    if (K > SPEC_KFAST) {
+    if (K <= SPEC_KFAST)
+        return; // k_spec_scan_c walks the block totals
+    {
         for (uint64_t b = 0; b < nb; b++) {
             S[b] = st;
             const uint64_t b0 = b * B;
@@ -1638,11 +1664,34 @@ __global__ __launch_bounds__(64) void k_spec_scan_b(const uint32_t *__restrict__
         *state = st;
         return;
     }
-    for (uint64_t k = 0; k < nblk; k++) {
-        Sblk[k] = st;
-        st = spec_apply(Bt + k * SPEC_KFAST, s_cls, st);
+    *state = st; // overwritten below; keeps the K > SPEC_KFAST exit simple
+}
+
+// block start states: the block totals are walked from LDS in windows
+__global__ __launch_bounds__(256) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
+                                                    const uint32_t *Bt, uint32_t *Sblk, uint32_t *state)
+{
+    __shared__ uint8_t s_cls[2048];
+    __shared__ uint32_t s_bt[256 * SPEC_KFAST];
+    if (meta[0] > SPEC_KFAST)
+        return;
+    for (uint32_t k = threadIdx.x; k < 2048; k += 256)
+        s_cls[k] = class_id[k];
+    uint32_t st = *state & 0xffffu;
+    for (uint64_t w0 = 0; w0 < nblk; w0 += 256) {
+        const uint64_t cnt = nblk - w0 < 256 ? nblk - w0 : 256;
+        __syncthreads();
+        for (uint64_t k = threadIdx.x; k < cnt * SPEC_KFAST; k += 256)
+            s_bt[k] = Bt[w0 * SPEC_KFAST + k];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (uint64_t k = 0; k < cnt; k++) {
+                Sblk[w0 + k] = st;
+                st = spec_apply(s_bt + k * SPEC_KFAST, s_cls, st);
+            }
     }
-    *state = st;
+    if (threadIdx.x == 0)
+        *state = st;
 }
 
 __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
@@ -1985,6 +2034,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_cnet_tile = 1;
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
+    c->tune_rw_wb = 2;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess)
         c->num_cu = prop.multiProcessorCount;
@@ -2531,6 +2581,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             hipLaunchKernelGGL(k_spec_scan_b, dim3(1), dim3(64), 0, s, (const uint32_t *)a.ptype, b->n, B, nb, nblk,
                                (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk,
                                c->sp_S, state);
+            hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(256), 0, s, nblk, (const uint32_t *)meta,
+                               (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state);
             hipLaunchKernelGGL(k_spec_emit, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, a, B, nb,
                                (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
                                (const uint32_t *)Sblk, (const uint32_t *)c->sp_S, vec);

@@ -193,8 +193,9 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           and is reset to 0 by setting this key.  0 = route every
  *                           frame by p_nxt[its type] instead (default 256)
  *   CNDP_TUNE_RW_WB         fused classify+rewrite write-back: 0 = the 16-B parts the
- *                           rewrite touches of rewritten frames (default), 1 = whole
- *                           rewritten frames, 2 = whole tiles holding a rewrite */
+ *                           rewrite touches of rewritten frames, 1 = whole rewritten
+ *                           frames, 2 = whole tiles holding a rewrite (default: full
+ *                           coalesced lines beat partial-line writes on HBM) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3

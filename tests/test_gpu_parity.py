@@ -553,7 +553,7 @@ def test_classify_rewrite(l3, gpu, n, burst):
         got = d2.slab.cpu().numpy()
         bad = np.nonzero(got != host)[0]
         assert bad.size == 0, f"nt={nt} wb={wb}: {bad.size} bytes differ, first at {bad[:8]}"
-    cl.set_tuning(nt=1, rw_wb=0)
+    cl.set_tuning(nt=1, rw_wb=2)
 
 
 def test_cnet_ptype_and_rxmeta(cnet, l3, gpu):
