@@ -213,7 +213,7 @@ def sweep(st, stream, cfg):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1, rw_wb=2)
+    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1, rw_wb=2, cnet_spec=256)
 
 
 def e2e_host(st, reps: int = 5):
