@@ -130,6 +130,7 @@ struct KArgs {
     uint32_t *rxmeta;  // optional (cnet): eth_rx lengths + ol_flags, packed (cndp_gpu.h)
     uint32_t *spec_nh; // cnet speculation model: input-node result of every frame a
                        // ptype-node group could send to ip4/ip6_input (else ~0)
+    uint32_t *spec_flags; // 2048-bit set of the type signatures seen (speculation model)
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -1001,6 +1002,28 @@ __device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
     }
 }
 
+__device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
+
+// OR the signature bit of each active lane into a 64-word LDS bitmap with one
+// LDS atomic per distinct word in the wave
+__device__ __forceinline__ void spec_mark(uint32_t *s_f, bool on, uint32_t g)
+{
+    const uint32_t w = g >> 5, bit = 1u << (g & 31u);
+    bool todo = on;
+    while (__any(todo)) {
+        const uint32_t lead = __shfl(w, __ffsll((unsigned long long)__ballot(todo)) - 1);
+        const bool mine = todo && w == lead;
+        const unsigned long long mm = __ballot(mine);
+        uint32_t v = mine ? bit : 0u;
+        for (int o = 32; o > 0; o >>= 1)
+            v |= __shfl_xor(v, o);
+        if (mine && (uint32_t)__lane_id() == (uint32_t)(__ffsll(mm) - 1))
+            atomicOr(&s_f[lead], v);
+        todo = todo && !mine;
+    }
+}
+
+
 __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
@@ -1160,8 +1183,11 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
     __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ uint32_t s_sf[64]; // type signatures seen (speculation model)
 
     const uint32_t tid = threadIdx.x;
+    if (tid < 64)
+        s_sf[tid] = 0;
     for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
         s_t[k] = a.ttab[k];
     for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
@@ -1418,8 +1444,11 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             nh = e >> 1;
             edge = nh >> 24;
         }
-        if (a.spec_nh && live)
-            a.spec_nh[i] = do4 || do6 ? e >> 1 : CNDP_NH_INVALID;
+        if (a.spec_nh) {
+            if (live)
+                a.spec_nh[i] = do4 || do6 ? e >> 1 : CNDP_NH_INVALID;
+            spec_mark(s_sf, live, spec_sig(pt & 0xffffu));
+        }
         __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
         if (live) {
             const uint32_t q = s_reta[h & a.reta_mask];
@@ -1439,12 +1468,14 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
         }
     }
-    if (count) {
+    if (count || a.spec_flags)
         __syncthreads();
+    if (count)
         for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
             if (s_bins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    }
+    if (a.spec_flags && tid < 64 && s_sf[tid])
+        atomicOr(&a.spec_flags[tid], s_sf[tid]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1466,48 +1497,13 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
 #define SPEC_KMAX 64
 #define SPEC_UNCH 0xFFFFFFFFu
 
-__device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
-
-__global__ __launch_bounds__(256) void k_spec_flags(const uint32_t *__restrict__ pt, uint32_t n,
-                                                    uint32_t *flags, const uint32_t *state)
-{
-    __shared__ uint32_t s_f[64];
-    if (threadIdx.x < 64)
-        s_f[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < n; i0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t i = i0 + threadIdx.x;
-        const uint32_t g = i < n ? spec_sig(pt[i] & 0xffffu) : 0u;
-        uint32_t w = g >> 5, bit = 1u << (g & 31u);
-        // one LDS atomic per distinct flag word in the wave (a batch holds few)
-        bool todo = i < n;
-        while (__any(todo)) {
-            const uint32_t lead = __shfl(w, __ffsll((unsigned long long)__ballot(todo)) - 1);
-            const bool mine = todo && w == lead;
-            const unsigned long long mm = __ballot(mine);
-            uint32_t v = mine ? bit : 0u;
-            for (int o = 32; o > 0; o >>= 1)
-                v |= __shfl_xor(v, o);
-            if (mine && (uint32_t)__lane_id() == (uint32_t)(__ffsll(mm) - 1))
-                atomicOr(&s_f[lead], v);
-            todo = todo && !mine;
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const uint32_t g = spec_sig(*state & 0xffffu);
-        atomicOr(&s_f[g >> 5], 1u << (g & 31u));
-    }
-    __syncthreads();
-    if (threadIdx.x < 64 && s_f[threadIdx.x])
-        atomicOr(&flags[threadIdx.x], s_f[threadIdx.x]);
-}
-
 // meta[0] = K, meta[1 + k] = signature of class k; class_id[sig] = k or 0xFF
 // (64 threads: thread t owns flag word t, classes numbered in signature order)
 __global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta)
 {
     const uint32_t t = threadIdx.x;
-    const uint32_t w = flags[t], cnt = (uint32_t)__popc(w);
+    const uint32_t g0 = spec_sig(meta[-1] & 0xffffu); // the node state entering the batch
+    const uint32_t w = flags[t] | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
     uint32_t pre = cnt; // inclusive wave prefix
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t v = __shfl_up(pre, o);
@@ -1567,24 +1563,49 @@ __device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0,
     return c;
 }
 
+// one wave per burst: the burst's types are staged through LDS (1024 at a
+// time) and lane k runs the group walk for signature class k
+#define SPEC_STAGE 1024
 __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, const uint32_t *meta, uint32_t *T, bool vec)
+                                                     uint64_t nb, const uint32_t *meta, uint32_t *T)
 {
-    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ uint32_t s_pt[4][SPEC_STAGE];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t b = (uint64_t)blockIdx.x * 4 + wv;
     const uint32_t K = meta[0];
     if (b >= nb || K > SPEC_KMAX)
         return;
+    uint32_t *st = s_pt[wv];
     const uint64_t b0 = b * B;
     const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
-    for (uint32_t k = 0; k < K; k++)
-        T[b * SPEC_KMAX + k] = spec_burst_map(pt, b0, cnt, meta[1 + k], vec);
+    const uint32_t sig = lane < K ? meta[1 + lane] : 0u;
+    uint32_t low = sig >> 3, E = sig & 7u, c = SPEC_UNCH;
+    for (uint32_t c0 = 0; c0 + 4 <= cnt; c0 += SPEC_STAGE) {
+        const uint32_t m = cnt - c0 < SPEC_STAGE ? cnt - c0 : SPEC_STAGE;
+        for (uint32_t k = lane; k < m; k += 64)
+            st[k] = pt[b0 + c0 + k] & 0xffffu;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t g = 0; g + 4 <= m; g += 4) {
+            const uint32_t l0 = st[g], l1 = st[g + 1], l2 = st[g + 2], l3 = st[g + 3];
+            const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low &&
+                               (l3 & 0xffu) == low;
+            if (!quiet && (l2 == l3 || E == cnet_edge(l3))) {
+                c = l3;
+                low = l3 & 0xffu;
+                E = cnet_edge(l3);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < K)
+        T[b * SPEC_KMAX + lane] = c;
 }
 
 // Burst maps are composed with a two-level LDS scan when at most
 // SPEC_KFAST signatures occur (a map is then SPEC_KFAST registers); the
 // composition "E then L" sends a class k through E, then through L.
 #define SPEC_KFAST 8
-#define SPEC_BLK 256
+#define SPEC_BLK 1024
 
 __device__ __forceinline__ uint32_t spec_apply(const uint32_t *m, const uint8_t *cls, uint32_t st)
 {
@@ -1711,38 +1732,67 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
     }
 }
 
-__global__ __launch_bounds__(SPEC_BLK) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *meta,
-                                                       const uint8_t *class_id, const uint32_t *P,
-                                                       const uint32_t *Sblk, const uint32_t *S, bool vec)
+// one wave per burst: start state from the scan, types staged through LDS;
+// every lane walks the groups (uniform, broadcast LDS reads) and remembers
+// the state at the groups it owns (g % 64 == lane), then fixes those groups
+__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *meta,
+                                                   const uint8_t *class_id, const uint32_t *P, const uint32_t *Sblk,
+                                                   const uint32_t *S)
 {
     __shared__ uint8_t s_cls[2048];
-    for (uint32_t k = threadIdx.x; k < 2048; k += SPEC_BLK)
+    __shared__ uint32_t s_pt[4][SPEC_STAGE];
+    for (uint32_t k = threadIdx.x; k < 2048; k += 256)
         s_cls[k] = class_id[k];
     __syncthreads();
-    const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t b = (uint64_t)blockIdx.x * 4 + wv;
     if (b >= nb)
         return;
+    uint32_t *st = s_pt[wv];
     const uint64_t b0 = b * B;
     const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
-    uint32_t st;
-    if (meta[0] > SPEC_KFAST)
-        st = S[b];
-    else // block start state through the block's earlier bursts (exclusive prefix)
-        st = threadIdx.x == 0 ? Sblk[blockIdx.x] : spec_apply(P + (b - 1) * SPEC_KFAST, s_cls, Sblk[blockIdx.x]);
-    uint32_t low = st & 0xffu, E = cnet_edge(st);
-    for (uint32_t g = 0; g + 4 <= cnt; g += 4) {
-        uint32_t l[4];
-        spec_group(a.ptype, b0 + g, vec, l[0], l[1], l[2], l[3]);
-        const bool quiet = (l[0] & 0xffu) == low && (l[1] & 0xffu) == low && (l[2] & 0xffu) == low &&
-                           (l[3] & 0xffu) == low;
-        if (quiet) {
-            for (int j = 0; j < 4; j++)
-                if (cnet_edge(l[j]) != E)
-                    spec_fix(a, b0 + g + j, l[j], E);
-        } else if (l[2] == l[3] || E == cnet_edge(l[3])) {
-            low = l[3] & 0xffu;
-            E = cnet_edge(l[3]);
+    uint32_t s0;
+    if (meta[0] > SPEC_KFAST) {
+        s0 = S[b];
+    } else { // block start state through the block's earlier bursts (exclusive prefix)
+        const uint64_t blk = b / SPEC_BLK;
+        s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * SPEC_KFAST, s_cls, Sblk[blk]);
+    }
+    uint32_t low = s0 & 0xffu, E = cnet_edge(s0);
+    for (uint32_t c0 = 0; c0 + 4 <= cnt; c0 += SPEC_STAGE) {
+        const uint32_t m = cnt - c0 < SPEC_STAGE ? cnt - c0 : SPEC_STAGE;
+        for (uint32_t k = lane; k < m; k += 64)
+            st[k] = a.ptype[b0 + c0 + k] & 0xffffu;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t myE[SPEC_STAGE / 256], myq[SPEC_STAGE / 256];
+#pragma unroll
+        for (int r = 0; r < SPEC_STAGE / 256; r++)
+            myq[r] = myE[r] = 0;
+        for (uint32_t g = 0; g + 4 <= m; g += 4) {
+            const uint32_t l0 = st[g], l1 = st[g + 1], l2 = st[g + 2], l3 = st[g + 3];
+            const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low &&
+                               (l3 & 0xffu) == low;
+            const uint32_t gi = g >> 2;
+            if ((gi & 63u) == lane) {
+                myq[gi >> 6] = quiet;
+                myE[gi >> 6] = E;
+            }
+            if (!quiet && (l2 == l3 || E == cnet_edge(l3))) {
+                low = l3 & 0xffu;
+                E = cnet_edge(l3);
+            }
         }
+#pragma unroll
+        for (int r = 0; r < SPEC_STAGE / 256; r++) {
+            const uint32_t gi = (uint32_t)r * 64u + lane;
+            if (myq[r] && gi * 4 + 4 <= m)
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t l = st[gi * 4 + j];
+                    if (cnet_edge(l) != myE[r])
+                        spec_fix(a, b0 + c0 + gi * 4 + j, l, myE[r]);
+                }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -2550,6 +2600,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             if (!a.ptype)
                 a.ptype = c->sp_pt;
             a.spec_nh = c->sp_nh;
+            a.spec_flags = c->sp_small + 66;
+            HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
         }
         if (c->tune_cnet_tile || B) {
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
@@ -2563,17 +2615,10 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         if (B) {
             const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
             uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
-            HIP_TRY(hipMemsetAsync(flags, 0, 64 * 4, s));
-            uint32_t gf = blocks_for(b->n, 256);
-            if (gf > (uint32_t)c->num_cu * 4u)
-                gf = (uint32_t)c->num_cu * 4u;
-            hipLaunchKernelGGL(k_spec_flags, dim3(gf), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, flags,
-                               (const uint32_t *)state);
             hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta);
-            const uint32_t gb = (uint32_t)((nb + 255) / 256);
-            const bool vec = (B & 3u) == 0 && (((uintptr_t)a.ptype) & 15u) == 0;
-            hipLaunchKernelGGL(k_spec_tables, dim3(gb), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, B, nb,
-                               (const uint32_t *)meta, c->sp_T, vec);
+            const uint32_t gw = (uint32_t)((nb + 3) / 4); // one wave per burst
+            hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, B, nb,
+                               (const uint32_t *)meta, c->sp_T);
             const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
             uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
             hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb, (const uint32_t *)meta,
@@ -2583,9 +2628,9 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                c->sp_S, state);
             hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(256), 0, s, nblk, (const uint32_t *)meta,
                                (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state);
-            hipLaunchKernelGGL(k_spec_emit, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, a, B, nb,
-                               (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
-                               (const uint32_t *)Sblk, (const uint32_t *)c->sp_S, vec);
+            hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, (const uint32_t *)meta,
+                               (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
+                               (const uint32_t *)c->sp_S);
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
