@@ -1569,7 +1569,7 @@ __device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0,
 __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
                                                      uint64_t nb, const uint32_t *meta, uint32_t *T)
 {
-    __shared__ uint32_t s_pt[4][SPEC_STAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][SPEC_STAGE];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t b = (uint64_t)blockIdx.x * 4 + wv;
     const uint32_t K = meta[0];
@@ -1582,17 +1582,19 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
     uint32_t low = sig >> 3, E = sig & 7u, c = SPEC_UNCH;
     for (uint32_t c0 = 0; c0 + 4 <= cnt; c0 += SPEC_STAGE) {
         const uint32_t m = cnt - c0 < SPEC_STAGE ? cnt - c0 : SPEC_STAGE;
-        for (uint32_t k = lane; k < m; k += 64)
-            st[k] = pt[b0 + c0 + k] & 0xffffu;
+        for (uint32_t k = lane; k < m; k += 64) { // type | p_nxt << 16, computed in parallel
+            const uint32_t l = pt[b0 + c0 + k] & 0xffffu;
+            st[k] = l | (cnet_edge(l) << 16);
+        }
         __builtin_amdgcn_wave_barrier();
         for (uint32_t g = 0; g + 4 <= m; g += 4) {
-            const uint32_t l0 = st[g], l1 = st[g + 1], l2 = st[g + 2], l3 = st[g + 3];
-            const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low &&
-                               (l3 & 0xffu) == low;
-            if (!quiet && (l2 == l3 || E == cnet_edge(l3))) {
-                c = l3;
-                low = l3 & 0xffu;
-                E = cnet_edge(l3);
+            const u32x4 x = *(const u32x4 *)(st + g);
+            const bool quiet = (x.x & 0xffu) == low && (x.y & 0xffu) == low && (x.z & 0xffu) == low &&
+                               (x.w & 0xffu) == low;
+            if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || E == (x.w >> 16))) {
+                c = x.w & 0xffffu;
+                low = x.w & 0xffu;
+                E = x.w >> 16;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1640,10 +1642,9 @@ __global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uin
             const uint32_t *l = s_m[threadIdx.x];
 #pragma unroll
             for (uint32_t k = 0; k < SPEC_KFAST; k++) {
-                if (k >= K)
-                    break;
                 const uint32_t ek = e[k];
-                m[k] = ek == SPEC_UNCH ? l[k] : spec_apply(l, s_cls, ek);
+                if (k < K)
+                    m[k] = ek == SPEC_UNCH ? l[k] : spec_apply(l, s_cls, ek);
             }
         }
         __syncthreads();
@@ -1740,7 +1741,8 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
                                                    const uint32_t *S)
 {
     __shared__ uint8_t s_cls[2048];
-    __shared__ uint32_t s_pt[4][SPEC_STAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][SPEC_STAGE];
+    __shared__ uint8_t s_q[4][SPEC_STAGE / 4];
     for (uint32_t k = threadIdx.x; k < 2048; k += 256)
         s_cls[k] = class_id[k];
     __syncthreads();
@@ -1759,37 +1761,35 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
         s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * SPEC_KFAST, s_cls, Sblk[blk]);
     }
     uint32_t low = s0 & 0xffu, E = cnet_edge(s0);
+    uint8_t *sq = s_q[wv];
     for (uint32_t c0 = 0; c0 + 4 <= cnt; c0 += SPEC_STAGE) {
         const uint32_t m = cnt - c0 < SPEC_STAGE ? cnt - c0 : SPEC_STAGE;
-        for (uint32_t k = lane; k < m; k += 64)
-            st[k] = a.ptype[b0 + c0 + k] & 0xffffu;
+        for (uint32_t k = lane; k < m; k += 64) {
+            const uint32_t l = a.ptype[b0 + c0 + k] & 0xffffu;
+            st[k] = l | (cnet_edge(l) << 16);
+        }
         __builtin_amdgcn_wave_barrier();
-        uint32_t myE[SPEC_STAGE / 256], myq[SPEC_STAGE / 256];
-#pragma unroll
-        for (int r = 0; r < SPEC_STAGE / 256; r++)
-            myq[r] = myE[r] = 0;
+        // the node walk (uniform over the wave): per group, quiet under the
+        // state (0x80 | p_nxt[state]) or not (0)
         for (uint32_t g = 0; g + 4 <= m; g += 4) {
-            const uint32_t l0 = st[g], l1 = st[g + 1], l2 = st[g + 2], l3 = st[g + 3];
-            const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low &&
-                               (l3 & 0xffu) == low;
-            const uint32_t gi = g >> 2;
-            if ((gi & 63u) == lane) {
-                myq[gi >> 6] = quiet;
-                myE[gi >> 6] = E;
-            }
-            if (!quiet && (l2 == l3 || E == cnet_edge(l3))) {
-                low = l3 & 0xffu;
-                E = cnet_edge(l3);
+            const u32x4 x = *(const u32x4 *)(st + g);
+            const bool quiet = (x.x & 0xffu) == low && (x.y & 0xffu) == low && (x.z & 0xffu) == low &&
+                               (x.w & 0xffu) == low;
+            if (lane == 0)
+                sq[g >> 2] = quiet ? (uint8_t)(0x80u | E) : (uint8_t)0;
+            if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || E == (x.w >> 16))) {
+                low = x.w & 0xffu;
+                E = x.w >> 16;
             }
         }
-#pragma unroll
-        for (int r = 0; r < SPEC_STAGE / 256; r++) {
-            const uint32_t gi = (uint32_t)r * 64u + lane;
-            if (myq[r] && gi * 4 + 4 <= m)
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t gi = lane; gi * 4 + 4 <= m; gi += 64) {
+            const uint32_t q = sq[gi];
+            if (q & 0x80u)
                 for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t l = st[gi * 4 + j];
-                    if (cnet_edge(l) != myE[r])
-                        spec_fix(a, b0 + c0 + gi * 4 + j, l, myE[r]);
+                    const uint32_t x = st[gi * 4 + j];
+                    if ((x >> 16) != (q & 7u))
+                        spec_fix(a, b0 + c0 + gi * 4 + j, x & 0xffffu, q & 7u);
                 }
         }
         __builtin_amdgcn_wave_barrier();
