@@ -1563,9 +1563,58 @@ __device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0,
     return c;
 }
 
+#define SPEC_STAGE 1024
+// Wave-parallel shortcuts for a burst of <= 256 packets (lane g = group g),
+// types staged in st as type | p_nxt << 16:
+//  * a "universal" group (low bytes not all equal, 3rd type == 4th) moves
+//    every state to its 4th type, so after the last one the walk no longer
+//    depends on where it started;
+//  * a "uniform" burst (every group: equal low bytes v, 3rd == 4th) leaves a
+//    state with low byte v alone and sends any other to group 0's 4th type.
+struct SpecGroups {
+    unsigned long long U; // universal groups
+    bool uniform;
+    uint32_t v, first;    // uniform: the low byte, group 0's 4th type
+};
+
+__device__ __forceinline__ SpecGroups spec_groups(const uint32_t *st, uint32_t ng, uint32_t lane)
+{
+    SpecGroups r;
+    bool allq = true, eq23 = false;
+    uint32_t v = 0;
+    if (lane < ng) {
+        const u32x4 x = *(const u32x4 *)(st + 4 * lane);
+        v = x.x & 0xffu;
+        allq = (x.y & 0xffu) == v && (x.z & 0xffu) == v && (x.w & 0xffu) == v;
+        eq23 = (x.z & 0xffffu) == (x.w & 0xffffu);
+    }
+    r.U = __ballot(lane < ng && !allq && eq23);
+    const uint32_t v0 = __shfl(v, 0);
+    const unsigned long long ok = __ballot(lane >= ng || (allq && eq23 && v == v0));
+    r.uniform = ng > 0 && ok == ~0ull;
+    r.v = v0;
+    r.first = st[3] & 0xffffu;
+    return r;
+}
+
+// walk groups [g0, g1) from a state given as (low byte, p_nxt, type)
+__device__ __forceinline__ void spec_walk(const uint32_t *st, uint32_t g0, uint32_t g1, uint32_t &low, uint32_t &E,
+                                          uint32_t &cur)
+{
+    for (uint32_t g = g0; g < g1; g++) {
+        const u32x4 x = *(const u32x4 *)(st + 4 * g);
+        const bool quiet = (x.x & 0xffu) == low && (x.y & 0xffu) == low && (x.z & 0xffu) == low &&
+                           (x.w & 0xffu) == low;
+        if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || E == (x.w >> 16))) {
+            cur = x.w & 0xffffu;
+            low = x.w & 0xffu;
+            E = x.w >> 16;
+        }
+    }
+}
+
 // one wave per burst: the burst's types are staged through LDS (1024 at a
 // time) and lane k runs the group walk for signature class k
-#define SPEC_STAGE 1024
 __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
                                                      uint64_t nb, const uint32_t *meta, uint32_t *T)
 {
@@ -1587,16 +1636,24 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
             st[k] = l | (cnet_edge(l) << 16);
         }
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t g = 0; g + 4 <= m; g += 4) {
-            const u32x4 x = *(const u32x4 *)(st + g);
-            const bool quiet = (x.x & 0xffu) == low && (x.y & 0xffu) == low && (x.z & 0xffu) == low &&
-                               (x.w & 0xffu) == low;
-            if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || E == (x.w >> 16))) {
-                c = x.w & 0xffffu;
-                low = x.w & 0xffu;
-                E = x.w >> 16;
+        if (cnt <= 256) { // one stage holds the burst: try the shortcuts
+            const uint32_t ng = m >> 2;
+            const SpecGroups sg = spec_groups(st, ng, lane);
+            if (sg.U) { // every class ends where the walk from the last universal group ends
+                const uint32_t u = 63u - (uint32_t)__clzll(sg.U);
+                uint32_t cu = st[4 * u + 3] & 0xffffu, lu = cu & 0xffu, Eu = st[4 * u + 3] >> 16;
+                spec_walk(st, u + 1, ng, lu, Eu, cu);
+                c = cu;
+                break;
+            }
+            if (sg.uniform) {
+                c = low == sg.v ? SPEC_UNCH : sg.first;
+                break;
             }
         }
+        uint32_t cur = c;
+        spec_walk(st, 0, m >> 2, low, E, cur);
+        c = cur;
         __builtin_amdgcn_wave_barrier();
     }
     if (lane < K)
@@ -1769,17 +1826,46 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
             st[k] = l | (cnet_edge(l) << 16);
         }
         __builtin_amdgcn_wave_barrier();
-        // the node walk (uniform over the wave): per group, quiet under the
-        // state (0x80 | p_nxt[state]) or not (0)
-        for (uint32_t g = 0; g + 4 <= m; g += 4) {
-            const u32x4 x = *(const u32x4 *)(st + g);
-            const bool quiet = (x.x & 0xffu) == low && (x.y & 0xffu) == low && (x.z & 0xffu) == low &&
-                               (x.w & 0xffu) == low;
-            if (lane == 0)
-                sq[g >> 2] = quiet ? (uint8_t)(0x80u | E) : (uint8_t)0;
-            if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || E == (x.w >> 16))) {
-                low = x.w & 0xffu;
-                E = x.w >> 16;
+        if (cnt <= 256) {
+            // lane g finds the state entering group g on its own: from the last
+            // universal group before it, or (uniform burst) directly, or from
+            // the burst start -- then marks its group
+            const uint32_t ng = m >> 2;
+            const SpecGroups sg = spec_groups(st, ng, lane);
+            if (lane < ng) {
+                uint32_t l = low, e = E, cur = 0;
+                const unsigned long long before = sg.U & ((1ull << lane) - 1ull);
+                if (before) {
+                    const uint32_t u = 63u - (uint32_t)__clzll(before);
+                    l = st[4 * u + 3] & 0xffu;
+                    e = st[4 * u + 3] >> 16;
+                    spec_walk(st, u + 1, lane, l, e, cur);
+                } else if (sg.uniform) {
+                    if (lane > 0 && low != sg.v) {
+                        l = sg.first & 0xffu;
+                        e = st[3] >> 16;
+                    }
+                } else {
+                    spec_walk(st, 0, lane, l, e, cur);
+                }
+                const u32x4 x = *(const u32x4 *)(st + 4 * lane);
+                const bool quiet = (x.x & 0xffu) == l && (x.y & 0xffu) == l && (x.z & 0xffu) == l &&
+                                   (x.w & 0xffu) == l;
+                sq[lane] = quiet ? (uint8_t)(0x80u | e) : (uint8_t)0;
+            }
+        } else {
+            // the node walk (uniform over the wave): per group, quiet under the
+            // state (0x80 | p_nxt[state]) or not (0)
+            for (uint32_t g = 0; g + 4 <= m; g += 4) {
+                const u32x4 x = *(const u32x4 *)(st + g);
+                const bool quiet = (x.x & 0xffu) == low && (x.y & 0xffu) == low && (x.z & 0xffu) == low &&
+                                   (x.w & 0xffu) == low;
+                if (lane == 0)
+                    sq[g >> 2] = quiet ? (uint8_t)(0x80u | E) : (uint8_t)0;
+                if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || E == (x.w >> 16))) {
+                    low = x.w & 0xffu;
+                    E = x.w >> 16;
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
