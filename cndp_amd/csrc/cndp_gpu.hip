@@ -981,25 +981,14 @@ __device__ __forceinline__ uint32_t rx_meta(const Lens &ln, uint32_t w0, uint32_
 // lib/cnet/ptype/ptype.c:32-46 (indexed by ptype & 0xffff)
 __device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
 {
-    switch (pt & 0xffffu) {
-    case 0x0003u:
-        return 2u; // FRAME_PUNT
-    case 0x0211u:
-    case 0x0111u:
-    case 0x0231u:
-    case 0x0291u:
-        return 3u; // IP4_INPUT
-    case 0x0241u:
-    case 0x0141u:
-    case 0x02c1u:
-    case 0x02e1u:
-        return 4u; // IP6_INPUT
-    case 0x8211u:
-    case 0x8241u:
-        return 5u; // GTPU_INPUT
-    default:
-        return 0u; // PKT_DROP
-    }
+    // branch-free: bitwise ORs of the compares, selects (it runs in the
+    // speculation walks once per group)
+    const uint32_t l = pt & 0xffffu;
+    uint32_t e = l == 0x0003u ? 2u : 0u;                                             // FRAME_PUNT
+    e = ((l == 0x0211u) | (l == 0x0111u) | (l == 0x0231u) | (l == 0x0291u)) ? 3u : e; // IP4_INPUT
+    e = ((l == 0x0241u) | (l == 0x0141u) | (l == 0x02c1u) | (l == 0x02e1u)) ? 4u : e; // IP6_INPUT
+    e = ((l == 0x8211u) | (l == 0x8241u)) ? 5u : e;                                  // GTPU_INPUT
+    return e;                                                                         // else PKT_DROP
 }
 
 __device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
@@ -1664,7 +1653,7 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
 // SPEC_KFAST signatures occur (a map is then SPEC_KFAST registers); the
 // composition "E then L" sends a class k through E, then through L.
 #define SPEC_KFAST 8
-#define SPEC_BLK 1024
+#define SPEC_BLK 256
 
 __device__ __forceinline__ uint32_t spec_apply(const uint32_t *m, const uint8_t *cls, uint32_t st)
 {
@@ -1747,30 +1736,65 @@ __global__ __launch_bounds__(64) void k_spec_scan_b(const uint32_t *__restrict__
 }
 
 // block start states: the block totals are walked from LDS in windows
-__global__ __launch_bounds__(256) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
-                                                    const uint32_t *Bt, uint32_t *Sblk, uint32_t *state)
+// block start states: Hillis-Steele over the block totals, 1024 at a time
+// with the composed map of the earlier windows carried along
+__global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
+                                                     const uint32_t *Bt, uint32_t *Sblk, uint32_t *state)
 {
     __shared__ uint8_t s_cls[2048];
-    __shared__ uint32_t s_bt[256 * SPEC_KFAST];
-    if (meta[0] > SPEC_KFAST)
+    __shared__ uint32_t s_m[1024][SPEC_KFAST];
+    __shared__ uint32_t s_carry[SPEC_KFAST];
+    const uint32_t K = meta[0], t = threadIdx.x;
+    if (K > SPEC_KFAST)
         return;
-    for (uint32_t k = threadIdx.x; k < 2048; k += 256)
+    for (uint32_t k = t; k < 2048; k += 1024)
         s_cls[k] = class_id[k];
-    uint32_t st = *state & 0xffffu;
-    for (uint64_t w0 = 0; w0 < nblk; w0 += 256) {
-        const uint64_t cnt = nblk - w0 < 256 ? nblk - w0 : 256;
-        __syncthreads();
-        for (uint64_t k = threadIdx.x; k < cnt * SPEC_KFAST; k += 256)
-            s_bt[k] = Bt[w0 * SPEC_KFAST + k];
-        __syncthreads();
-        if (threadIdx.x == 0)
-            for (uint64_t k = 0; k < cnt; k++) {
-                Sblk[w0 + k] = st;
-                st = spec_apply(s_bt + k * SPEC_KFAST, s_cls, st);
+    if (t < SPEC_KFAST)
+        s_carry[t] = SPEC_UNCH;
+    const uint32_t s0 = *state & 0xffffu;
+    __syncthreads();
+    for (uint64_t w0 = 0; w0 < nblk; w0 += 1024) {
+        const uint64_t k0 = w0 + t;
+        uint32_t m[SPEC_KFAST];
+#pragma unroll
+        for (uint32_t k = 0; k < SPEC_KFAST; k++)
+            m[k] = k0 < nblk && k < K ? Bt[k0 * SPEC_KFAST + k] : SPEC_UNCH;
+        for (uint32_t d = 1; d < 1024; d <<= 1) {
+#pragma unroll
+            for (uint32_t k = 0; k < SPEC_KFAST; k++)
+                s_m[t][k] = m[k];
+            __syncthreads();
+            if (t >= d) {
+                const uint32_t *e = s_m[t - d], *l = s_m[t];
+#pragma unroll
+                for (uint32_t k = 0; k < SPEC_KFAST; k++) {
+                    const uint32_t ek = e[k];
+                    if (k < K)
+                        m[k] = ek == SPEC_UNCH ? l[k] : spec_apply(l, s_cls, ek);
+                }
             }
+            __syncthreads();
+        }
+        // state entering block k0: the carry, then this window's blocks before k0
+        uint32_t st = spec_apply(s_carry, s_cls, s0);
+        if (t > 0)
+            st = spec_apply(s_m[t - 1], s_cls, st);
+        if (k0 < nblk)
+            Sblk[k0] = st;
+        __syncthreads();
+        if (t == 1023) { // carry = carry then this window's total
+            uint32_t nc[SPEC_KFAST];
+            for (uint32_t k = 0; k < SPEC_KFAST; k++) {
+                const uint32_t ck = s_carry[k];
+                nc[k] = k >= K ? SPEC_UNCH : ck == SPEC_UNCH ? m[k] : spec_apply(m, s_cls, ck);
+            }
+            for (uint32_t k = 0; k < SPEC_KFAST; k++)
+                s_carry[k] = nc[k];
+        }
+        __syncthreads();
     }
-    if (threadIdx.x == 0)
-        *state = st;
+    if (t == 0)
+        *state = spec_apply(s_carry, s_cls, s0);
 }
 
 __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
@@ -2712,7 +2736,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             hipLaunchKernelGGL(k_spec_scan_b, dim3(1), dim3(64), 0, s, (const uint32_t *)a.ptype, b->n, B, nb, nblk,
                                (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk,
                                c->sp_S, state);
-            hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(256), 0, s, nblk, (const uint32_t *)meta,
+            hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
                                (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state);
             hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, (const uint32_t *)meta,
                                (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
