@@ -56,7 +56,8 @@ def setup_dist():
     return world, rank, local
 
 
-def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac: float = 0.9):
+def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac: float = 0.9,
+                ring: int = 0):
     from cndp_amd import native as N
     from cndp_amd import pktgen
     from cndp_amd.classify import Classifier
@@ -102,6 +103,27 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     # cnet keeps the edge output (its drop/forward/proto edge is not in nh
     # for packets the ptype node sends elsewhere)
     state["out"] = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
+    # Ring of batches: step k classifies batch k % R, as a NIC ring hands over
+    # fresh buffers.  R is sized so that the ring's frames and results are
+    # several times the 256 MiB Infinity Cache: no step is served results or
+    # frames a previous step left on-die.  The bin counters are shared.
+    fr0 = state["frames"]
+    batch_bytes = fr0.slab.numel() + sum(t.numel() * t.element_size() for t in state["out"].values()
+                                         if isinstance(t, torch.Tensor))
+    R = ring if ring > 0 else max(1, min(4, -(-(4 << 30) // batch_bytes)))
+    state["ring"] = [(fr0, state["out"])]
+    for r in range(1, R):
+        if cfg in ("c2", "c3", "c3rw"):
+            fr = pktgen.packed_ipv4(n, routes=routes, seed=seed + 1000 * r, device=dev,
+                                    in_route_frac=in_route_frac)
+        elif cfg == "c4":
+            fr = pktgen.imix(n, seed=seed + 1000 * r, v4routes=routes, v6routes=state["v6routes"], device=dev)
+        else:
+            fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed + 1000 * r, device=dev)
+            pktgen.corrupt_cksum(fr, 1024, seed + 1000 * r)
+        o = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
+        o["bins"] = state["out"]["bins"]
+        state["ring"].append((fr, o))
     if cfg == "c3rw":
         import random
         rnd_ = random.Random(7)
@@ -113,9 +135,11 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     return state
 
 
-def run_step(st, stream=None):
-    """One step of the configured workload (what the timed loop repeats)."""
-    cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
+def run_step(st, stream=None, k: int = 0):
+    """One step of the configured workload (what the timed loop repeats):
+    batch k % R of the ring."""
+    cl, mode = st["cl"], st["mode"]
+    fr, out = st["ring"][k % len(st["ring"])]
     sid = stream.cuda_stream if stream is not None else None
     if "tx" in st:
         cl.classify_rewrite(fr, out=out, burst=256, tx_edge=st["tx"], stream=sid)
@@ -188,7 +212,12 @@ def sweep(st, stream, cfg):
                 dict(tile=0, nt=0, unroll=2, blocks_per_cu=4)]
     variants += [dict(tile=t, nt=nt, unroll=1, blocks_per_cu=b) for t in (1, 4) for nt in (0, 1) for b in (2, 4, 8)]
     variants += [dict(tile=2, nt=1, unroll=1, blocks_per_cu=4), dict(tile=3, nt=0, unroll=1, blocks_per_cu=4)]
-    variants = [dict(v, dir16=1) for v in variants] + [dict(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=0)]
+    variants = [dict(v, dir16=1, load_nt=0) for v in variants] + [dict(tile=4, nt=1, unroll=1, blocks_per_cu=4,
+                                                                      dir16=0, load_nt=0)]
+    variants += [dict(tile=4, nt=nt, unroll=1, blocks_per_cu=b, dir16=1, load_nt=1) for nt in (1, 0)
+                 for b in (2, 3, 4, 6)]
+    variants += [dict(tile=5, nt=1, unroll=1, blocks_per_cu=b, dir16=d, load_nt=l) for l in (1, 0)
+                 for b in (1, 2, 3, 4) for d in (1, 0)]
     if mode == N.CNDP_MODE_CNET:
         variants = [dict(cnet_tile=ct, dir16=d, cnet_spec=sp) for sp in (256, 0) for ct in (1, 0) for d in (1, 0)
                     if sp == 256 or (ct == 1 and d == 1)]
@@ -196,24 +225,23 @@ def sweep(st, stream, cfg):
         variants = [dict(rw_wb=w, nt=nt, tile=4) for w in (0, 1, 2) for nt in (1, 0)] + [dict(tile=1, rw_wb=0)]
     for v in variants:
         cl.set_tuning(**v)
-        for _ in range(3):
-            run_step(st, stream)
-        evs = []
-        for _ in range(20):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            run_step(st, stream)
-            b.record(stream)
-            evs.append((a, b))
+        for k in range(3):
+            run_step(st, stream, k)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for k in range(20):
+            run_step(st, stream, k)
+        b.record(stream)
         torch.cuda.synchronize()
-        ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+        ms = a.elapsed_time(b) / 20
         gbs = st["algo"] * st["n"] / (ms * 1e-3) / 1e9
         rows.append(dict(v, kernel_ms=ms, algo_GBs=gbs, Mpps=st["n"] / ms / 1e3))
         log(f"[sweep {cfg}] {v}: {ms:.4f} ms {gbs:7.1f} GB/s {st['n'] / ms / 1e3:9.1f} Mpps")
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4, dir16=1, cnet_tile=1, rw_wb=2, cnet_spec=256)
+    cl.set_tuning(tile=5, nt=1, unroll=1, blocks_per_cu=0, dir16=1, cnet_tile=1, rw_wb=2, cnet_spec=256,
+                  load_nt=1)
 
 
 def e2e_host(st, reps: int = 5):
@@ -296,6 +324,9 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr + gpurun_out)")
     ap.add_argument("--in-route-frac", type=float, default=0.9,
                     help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
+    ap.add_argument("--ring", type=int, default=0,
+                    help="batches in the ring (0 = auto: >= 4 GiB of frames + results, at most 4)")
+    ap.add_argument("--load-nt", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--dir16", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
@@ -307,18 +338,19 @@ def main():
     world, rank, local = setup_dist()
     dev = torch.device(f"cuda:{local}")
     t0 = time.time()
-    st = build_state(args.config, dev, rank, args.packets or None, args.in_route_frac)
+    st = build_state(args.config, dev, rank, args.packets or None, args.in_route_frac, args.ring)
     torch.cuda.synchronize()
     if rank == 0:
         log(f"[bench] setup {time.time() - t0:.1f}s: {st['desc']}")
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     stream = torch.cuda.current_stream(dev)
-    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16)
+    cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16,
+                  load_nt=args.load_nt)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 
-    for _ in range(args.warmup):
-        run_step(st)
+    for k in range(args.warmup):
+        run_step(st, None, k)
     torch.cuda.synchronize()
     parity = None
     if rank == 0 and not args.no_parity:
@@ -330,20 +362,23 @@ def main():
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # One HIP event pair on the launch stream brackets the K back-to-back
+    # launches: kern_ms = their average duration including the kernel
+    # boundary (an event pair per launch adds ~10 us of marker overhead per
+    # step on ROCm and would understate the kernel).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_start = time.perf_counter()
+    ev0.record(stream)
     for s in range(args.steps):
-        evs[s][0].record(stream)
-        run_step(st, stream)
-        evs[s][1].record(stream)
+        run_step(st, stream, s)
+    ev1.record(stream)
     D.final_count_reduce(out["bins"])  # the one RCCL collective: per-bin counts
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], dev)
 
@@ -380,6 +415,7 @@ def main():
                        "frame_layout": "packed 64-B slots" if fr.offsets is None and fr.stride == 64
                        else ("IMIX packed at roundup(len,64)" if fr.offsets is not None
                              else f"{fr.stride}-B slots"),
+                       "ring_batches": len(st["ring"]),
                        "routes": len(st["routes"]), "parallelism": f"dp{world} (replicated FIB, sharded batches)",
                        "parity_sample_vs_oracle": parity,
                        "bins_total": int(bins.sum())},

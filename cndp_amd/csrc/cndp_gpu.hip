@@ -381,7 +381,7 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_fast(KArgs a)
 // ---------------------------------------------------------------------------
 #define TILE_WAVES (FAST_THREADS / 64)
 
-template <int MODE, int SCHED, bool NTS, bool RW = false>
+template <int MODE, int SCHED, bool NTS, bool RW = false, bool LNT = false>
 __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB4_POS * 256];
@@ -417,10 +417,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
     u32x4 r0, r1, r2, r3;
     if (t < n_tiles) {
         const u32x4 *g = (const u32x4 *)(base + t * 4096u);
-        r0 = g[lane];
-        r1 = g[64 + lane];
-        r2 = g[128 + lane];
-        r3 = g[192 + lane];
+        r0 = ldg4<LNT>((const uint8_t *)(g + lane));
+        r1 = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+        r2 = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+        r3 = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
     }
     for (; t < n_tiles; t += wstep) {
 #pragma unroll
@@ -433,10 +433,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
         const uint64_t tn = t + wstep;
         if (SCHED == 0 && tn < n_tiles) { // prefetch the next tile while this one is parsed
             const u32x4 *g = (const u32x4 *)(base + tn * 4096u);
-            r0 = g[lane];
-            r1 = g[64 + lane];
-            r2 = g[128 + lane];
-            r3 = g[192 + lane];
+            r0 = ldg4<LNT>((const uint8_t *)(g + lane));
+            r1 = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+            r2 = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+            r3 = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
         }
         const uint32_t sw = (lane >> 2) & 3u;
         const u32x4 p0 = tile[lane * 4u + (0u ^ sw)];
@@ -473,10 +473,10 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
             {
                 const uint64_t tp = tn < n_tiles ? tn : t;
                 const u32x4 *g = (const u32x4 *)(base + tp * 4096u);
-                r0 = g[lane];
-                r1 = g[64 + lane];
-                r2 = g[128 + lane];
-                r3 = g[192 + lane];
+                r0 = ldg4<LNT>((const uint8_t *)(g + lane));
+                r1 = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+                r2 = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+                r3 = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
             }
             uint32_t hs = 0;
             bool slow = et == 0x86DDu;
@@ -573,13 +573,198 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_tile(KArgs a, uint64_
             const uint32_t nh = fast_lpm<MODE>(a, h);
             if (tn < n_tiles) {
                 const u32x4 *g = (const u32x4 *)(base + tn * 4096u);
-                r0 = g[lane];
-                r1 = g[64 + lane];
-                r2 = g[128 + lane];
-                r3 = g[192 + lane];
+                r0 = ldg4<LNT>((const uint8_t *)(g + lane));
+                r1 = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+                r2 = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+                r3 = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
             }
             fast_finish<MODE, NTS, true>(a, i, h, s_t, s_reta, s_bins, count, nh);
         }
+    }
+    // ragged tail (frames past the last whole tile): per-lane path
+    const uint64_t done = n_tiles * 64u;
+    for (uint64_t i = done + (uint64_t)blockIdx.x * FAST_THREADS + tid; i < a.n;
+         i += (uint64_t)gridDim.x * FAST_THREADS) {
+        FastHdr h;
+        fast_load<false>(a, i, h);
+        fast_finish<MODE, false>(a, i, h, s_t, s_reta, s_bins, count);
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Streamed wave-tile kernel (CNDP_TUNE_TILE 5, l3fwd / hash, packed 64-B slots).
+// The per-tile work is cut into four stages that run one loop trip apart,
+// so every FIB gather has a whole trip to come back and nothing waits on
+// the newest frame loads:
+//   A  tile c    LDS-stage the frames, parse, Toeplitz; gather 1 (/16
+//                directory, or tbl24 without it)
+//   B  tile c-1  gather 2 (directory page, or tbl8 without the directory)
+//   C  tile c-2  gather 3 (tbl8 behind a page)
+//   D  tile c-3  queue, bins and the result stores
+// Frame tiles are loaded two trips ahead into two alternating register
+// sets (the trip is unrolled by two).  Each trip issues its loads in the
+// order  gathers(C, B, A) -> frame tile c+2 -> stores(D), so the vmcnt wait
+// at the top of the next trip -- for the gathers and tile c+1 -- leaves
+// tile c+2 and the stores in flight: a wave always has one to two 4-KiB
+// tiles outstanding and never idles on an L2 round trip.
+// ---------------------------------------------------------------------------
+struct StreamLane { // one lane's packet in flight between stages
+    uint32_t et, ip, hs;
+    uint32_t e;   // FIB entry so far
+    uint32_t raw; // the gather issued for it last trip (may still be in flight)
+    bool sel;     // raw replaces e (resolved by the consumer, not at issue)
+};
+
+template <int MODE, bool NTS, bool LNT, int P>
+__device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, uint64_t t0, uint64_t wstep,
+                                            uint64_t nt_w, uint64_t j, uint32_t lane, u32x4 *tile,
+                                            u32x4 (&r)[2][4], StreamLane &sb, StreamLane &sc, StreamLane &sd,
+                                            const uint32_t *s_t, const uint16_t *s_reta, uint32_t *s_bins,
+                                            bool count)
+{
+    // Every load below is issued unconditionally (a safe index when its
+    // result is not needed; past the wave's last tile the frame loads re-read
+    // the slab's last tile, an L2 hit): the compiler's static vmcnt
+    // bookkeeping then sees the same issue order on every path and waits only
+    // for what is older than the newest frame tile.
+    const uint8_t *base = a.slab + a.data_off;
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    const bool dD = j >= 3 && j - 3 < nt_w;
+    const uint64_t c = t0 + j * wstep;
+    // D: tile c-3 -- its final entry came back with last trip's gather 3
+    uint32_t nhD = CNDP_NH_INVALID;
+    const uint32_t etD = sd.et, hsD = sd.hs;
+    if (MODE == CNDP_MODE_L3FWD && etD == 0x0800u)
+        nhD = (sd.sel ? sd.raw : sd.e) >> 1;
+    StreamLane nd = sc, nc = sb, nb;
+    if (MODE == CNDP_MODE_L3FWD) {
+        // C: tile c-2 -- gather 3 (tbl8 behind a directory page)
+        const uint32_t ec = sc.sel ? sc.raw : sc.e;
+        nd.e = ec;
+        nd.sel = a.dir16 && (ec & 1u);
+        nd.raw = a.tbl8[nd.sel ? (ec >> 1) * 256u + (sc.ip & 0xffu) : 0u];
+        // B: tile c-1 -- gather 2 (directory page, or tbl8 without the directory)
+        const uint32_t eb = sb.sel ? sb.raw : 0u; // gather 1 was issued for IPv4 frames only
+        nc.e = eb;
+        nc.sel = (eb & 1u) != 0u;
+        const uint32_t *t2 = a.dir16 ? a.pages : a.tbl8;
+        const uint32_t i2 = a.dir16 ? (eb >> 1) * 256u + ((sb.ip >> 8) & 0xffu) : (eb >> 1) * 256u + (sb.ip & 0xffu);
+        nc.raw = t2[nc.sel ? i2 : 0u];
+    }
+    // A: tile c -- stage, parse, hash, gather 1
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t f = 16u * k + fr_in_k;
+        tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t sw = (lane >> 2) & 3u;
+    const u32x4 p0 = tile[lane * 4u + (0u ^ sw)];
+    const u32x4 p1 = tile[lane * 4u + (1u ^ sw)];
+    const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+    __builtin_amdgcn_wave_barrier();
+    FastHdr h;
+    const uint64_t i = (c < n_tiles ? c : n_tiles - 1u) * 64u + lane;
+    h.p = base + i * 64u;
+    h.avail = a.slab_len - (a.data_off + i * 64u);
+    h.w3 = p0.w;
+    h.w5 = p1.y;
+    h.w6 = p1.z;
+    h.w7 = p1.w;
+    h.w8 = p2.x;
+    h.w9 = p2.y;
+    const uint32_t et = bswap16(h.w3 & 0xffffu);
+    const uint32_t dst = alignb(h.w8, h.w7, 2);
+    nb.et = et;
+    nb.ip = bswap32(dst);
+    nb.e = 0;
+    nb.sel = et == 0x0800u; // non-IPv4: no lookup, no further gathers
+    nb.raw = 0;
+    if (MODE == CNDP_MODE_L3FWD)
+        nb.raw = a.dir16 ? a.dir16[nb.ip >> 16] : a.tbl24[nb.ip >> 8];
+    nb.hs = 0;
+    bool slow = et == 0x86DDu;
+    if (et == 0x0800u) {
+        const uint32_t ihl = (h.w3 >> 16) & 0xfu;
+        const uint32_t proto = h.w5 >> 24;
+        const uint32_t frag = bswap16(h.w5 & 0xffffu) & 0x3fffu;
+        nb.hs = tz4(s_t, 0, alignb(h.w7, h.w6, 2)) ^ tz4(s_t, 4, dst);
+        if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
+            if (ihl == 5)
+                nb.hs ^= tz4(s_t, 8, alignb(h.w9, h.w8, 2));
+            else
+                slow = true;
+        }
+    }
+    if (slow) // IPv6 tuple / IPv4 options: bytes past the staged 48
+        nb.hs = fast_hash<MODE>(a, h, s_t);
+    // frame tile c+2 into the register set just consumed
+    {
+        const uint64_t cn = c + 2u * wstep;
+        const u32x4 *g = (const u32x4 *)(base + (cn < n_tiles ? cn : n_tiles - 1u) * 4096u);
+        r[P][0] = ldg4<LNT>((const uint8_t *)(g + lane));
+        r[P][1] = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+        r[P][2] = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+        r[P][3] = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
+    }
+    // D: the stores of tile c-3
+    if (dD)
+        fast_emit<MODE, NTS>(a, (c - 3u * wstep) * 64u + lane, etD, nhD, hsD, s_reta, s_bins, count);
+    sd = nd;
+    sc = nc;
+    sb = nb;
+}
+
+template <int MODE, bool NTS, bool LNT>
+__global__ __launch_bounds__(FAST_THREADS) void k_classify_stream(KArgs a, uint64_t n_tiles)
+{
+    __shared__ uint32_t s_t[TAB4_POS * 256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[TILE_WAVES][256];
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB4_POS * 256; k += FAST_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += FAST_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint8_t *base = a.slab + a.data_off;
+    const uint64_t wstep = (uint64_t)gridDim.x * TILE_WAVES;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE_WAVES + wv;
+    const uint64_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0; // this wave's tiles
+    u32x4 r[2][4];
+#pragma unroll
+    for (uint32_t s = 0; s < 2; s++) {
+        const uint64_t ts = t0 + s * wstep;
+        const u32x4 *g = (const u32x4 *)(base + (ts < n_tiles ? ts : n_tiles - 1u) * 4096u);
+        r[s][0] = ldg4<LNT>((const uint8_t *)(g + lane));
+        r[s][1] = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+        r[s][2] = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+        r[s][3] = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
+    }
+    StreamLane sb = {0, 0, 0, 0, 0, false}, sc = sb, sd = sb;
+    const uint64_t trips = nt_w ? nt_w + 3 : 0;
+    for (uint64_t j = 0; j < trips; j += 2) {
+        stream_trip<MODE, NTS, LNT, 0>(a, n_tiles, t0, wstep, nt_w, j, lane, tile, r, sb, sc, sd, s_t, s_reta,
+                                       s_bins, count);
+        if (j + 1 < trips)
+            stream_trip<MODE, NTS, LNT, 1>(a, n_tiles, t0, wstep, nt_w, j + 1, lane, tile, r, sb, sc, sd, s_t,
+                                           s_reta, s_bins, count);
     }
     // ragged tail (frames past the last whole tile): per-lane path
     const uint64_t done = n_tiles * 64u;
@@ -2100,6 +2285,7 @@ struct cndp_gpu_ctx {
     int tune_tile;        // CNDP_TUNE_TILE
     int tune_dir16;       // CNDP_TUNE_DIR16
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
+    int tune_lnt;         // CNDP_TUNE_LOAD_NT
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
@@ -2188,10 +2374,11 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->dev = device;
     c->tune_nt = 1;
     c->tune_unroll = 1;
-    c->tune_bpc = 4;
-    c->tune_tile = 4;
+    c->tune_bpc = 0; // auto: 2 for the streamed tile kernel, 4 otherwise
+    c->tune_tile = 5;
     c->tune_dir16 = 1;
     c->tune_cnet_tile = 1;
+    c->tune_lnt = 1;
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
     c->tune_rw_wb = 2;
@@ -2744,7 +2931,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
-        const uint32_t cap = (uint32_t)c->num_cu * (uint32_t)c->tune_bpc;
+        const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : c->tune_tile == 5 ? 2u : 4u;
+        const uint32_t cap = (uint32_t)c->num_cu * bpc;
         if (g > cap)
             g = cap;
         if (c->tune_tile == 3) {
@@ -2764,8 +2952,20 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             uint32_t gt = (uint32_t)((n_tiles + TILE_WAVES - 1) / TILE_WAVES);
             if (gt > cap)
                 gt = cap;
+            if (c->tune_tile == 5 && !rw_tx) {
+                typedef void (*stream_fn)(KArgs, uint64_t);
+                static const stream_fn sfns[2][2][2] = {
+                    {{k_classify_stream<CNDP_MODE_L3FWD, false, false>, k_classify_stream<CNDP_MODE_L3FWD, false, true>},
+                     {k_classify_stream<CNDP_MODE_L3FWD, true, false>, k_classify_stream<CNDP_MODE_L3FWD, true, true>}},
+                    {{k_classify_stream<CNDP_MODE_HASH, false, false>, k_classify_stream<CNDP_MODE_HASH, false, true>},
+                     {k_classify_stream<CNDP_MODE_HASH, true, false>, k_classify_stream<CNDP_MODE_HASH, true, true>}}};
+                hipLaunchKernelGGL(sfns[b->mode == CNDP_MODE_L3FWD ? 0 : 1][c->tune_nt ? 1 : 0][c->tune_lnt ? 1 : 0],
+                                   dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
+                HIP_TRY(hipGetLastError());
+                return 0;
+            }
             // tile 1: gathers then prefetch; 2: prefetch then gathers; 4: split
-            const int sched = c->tune_tile == 2 ? 0 : c->tune_tile == 4 ? 2 : 1;
+            const int sched = c->tune_tile == 2 ? 0 : (c->tune_tile == 4 || c->tune_tile == 5) ? 2 : 1;
             typedef void (*tile_fn)(KArgs, uint64_t);
             static const tile_fn fns[2][3][2] = {
                 {{k_classify_tile<CNDP_MODE_L3FWD, 0, false>, k_classify_tile<CNDP_MODE_L3FWD, 0, true>},
@@ -2774,7 +2974,14 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                 {{k_classify_tile<CNDP_MODE_HASH, 0, false>, k_classify_tile<CNDP_MODE_HASH, 0, true>},
                  {k_classify_tile<CNDP_MODE_HASH, 1, false>, k_classify_tile<CNDP_MODE_HASH, 1, true>},
                  {k_classify_tile<CNDP_MODE_HASH, 2, false>, k_classify_tile<CNDP_MODE_HASH, 2, true>}}};
-            tile_fn fn = fns[b->mode == CNDP_MODE_L3FWD ? 0 : 1][sched][c->tune_nt ? 1 : 0];
+            // split schedule with non-temporal frame loads (CNDP_TUNE_LOAD_NT)
+            static const tile_fn fns_lnt[2][2] = {
+                {k_classify_tile<CNDP_MODE_L3FWD, 2, false, false, true>,
+                 k_classify_tile<CNDP_MODE_L3FWD, 2, true, false, true>},
+                {k_classify_tile<CNDP_MODE_HASH, 2, false, false, true>,
+                 k_classify_tile<CNDP_MODE_HASH, 2, true, false, true>}};
+            const int mi = b->mode == CNDP_MODE_L3FWD ? 0 : 1, nti = c->tune_nt ? 1 : 0;
+            tile_fn fn = sched == 2 && c->tune_lnt ? fns_lnt[mi][nti] : fns[mi][sched][nti];
             if (rw_tx && b->mode == CNDP_MODE_L3FWD && sched == 2 && b->n % 256u == 0 && c->d_rw_tbl) {
                 fn = c->tune_nt ? k_classify_tile<CNDP_MODE_L3FWD, 2, true, true>
                                 : k_classify_tile<CNDP_MODE_L3FWD, 2, false, true>;
@@ -3457,12 +3664,12 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_unroll = value;
         return 0;
     case CNDP_TUNE_BLOCKS_PER_CU:
-        if (value < 1 || value > 64)
+        if (value < 0 || value > 64)
             return -EINVAL;
         c->tune_bpc = value;
         return 0;
     case CNDP_TUNE_TILE:
-        if (value < 0 || value > 4)
+        if (value < 0 || value > 5)
             return -EINVAL;
         c->tune_tile = value;
         return 0;
@@ -3471,6 +3678,9 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return 0;
     case CNDP_TUNE_CNET_TILE:
         c->tune_cnet_tile = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_LOAD_NT:
+        c->tune_lnt = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_RW_WB:
         if (value < 0 || value > 2)

@@ -176,11 +176,14 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           and output stores (per-lane kernels), output stores only
  *                           (wave-tile kernels) (default 1)
  *   CNDP_TUNE_UNROLL        packets per lane per loop trip, 1 or 2 (default 1)
- *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 4)
+ *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 0 = auto:
+ *                           2 for the streamed wave-tile kernel, 4 for the others)
  *   CNDP_TUNE_TILE          l3fwd/hash kernel: 0 per-lane, 1 / 2 wave-tile LDS staging
  *                           (packed 64-B slots; prefetch before / after the FIB gathers),
  *                           3 software-pipelined per-lane, 4 wave-tile with the next
- *                           tile's loads issued between the two FIB gathers (default 4)
+ *                           tile's loads issued between the two FIB gathers, 5 streamed
+ *                           wave-tile: frames two tiles ahead, each FIB gather level one
+ *                           loop trip apart (default 5)
  *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
  *                           kept in front of tbl24 (default 1)
  *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = wave-tile staging with the next tile's loads
@@ -195,7 +198,11 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_RW_WB         fused classify+rewrite write-back: 0 = the 16-B parts the
  *                           rewrite touches of rewritten frames, 1 = whole rewritten
  *                           frames, 2 = whole tiles holding a rewrite (default: full
- *                           coalesced lines beat partial-line writes on HBM) */
+ *                           coalesced lines beat partial-line writes on HBM)
+ *   CNDP_TUNE_LOAD_NT       wave-tile kernels (tile 4): 1 = frame tiles loaded with the
+ *                           non-temporal hint, so the once-read stream neither allocates
+ *                           in L2 / the Infinity Cache nor evicts the FIB directory from
+ *                           them (default 1) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -205,6 +212,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_HOST_CHUNK 7
 #define CNDP_TUNE_RW_WB 8
 #define CNDP_TUNE_CNET_SPEC 9
+#define CNDP_TUNE_LOAD_NT 10
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

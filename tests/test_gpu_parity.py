@@ -101,11 +101,12 @@ def test_fuzz_frames_l3fwd(l3, gpu, mode):
     # paths (IPv6, IPv4 options read past the 48 staged bytes)
     fr = pktgen.fuzz_frames(64 * 800 + 5, seed=22, slot=64, device=gpu)
     ref = oracle_classify(mode, fr, tables4=t4)
-    for tile in (0, 1, 2, 3, 4):
+    for tile in (0, 1, 2, 3, 4, 5):
         for nt in (0, 1):
-            cl.set_tuning(tile=tile, nt=nt)
-            assert_same(run_gpu(cl, fr, mode), ref)
-    cl.set_tuning(tile=4, nt=1)
+            for lnt in ((0, 1) if tile >= 4 else (1,)):
+                cl.set_tuning(tile=tile, nt=nt, load_nt=lnt)
+                assert_same(run_gpu(cl, fr, mode), ref)
+    cl.set_tuning(tile=5, nt=1, load_nt=1)
 
 
 def test_fuzz_unaligned_offsets(l3, gpu):
@@ -337,13 +338,14 @@ def test_tuning_variants_identical(l3, gpu, mode):
                 for bpc in (1, 8, 16):
                     cl.set_tuning(tile=0, nt=nt, unroll=unroll, blocks_per_cu=bpc)
                     assert_same(run_gpu(cl, fr, mode), ref)
-        for tile in (1, 2, 3, 4):
+        for tile in (1, 2, 3, 4, 5):
             for bpc in (1, 2, 4, 16):
                 for nt in (0, 1):
-                    cl.set_tuning(tile=tile, blocks_per_cu=bpc, nt=nt)
-                    assert_same(run_gpu(cl, fr, mode), ref)
+                    for lnt in ((0, 1) if tile >= 4 else (1,)):
+                        cl.set_tuning(tile=tile, blocks_per_cu=bpc, nt=nt, load_nt=lnt)
+                        assert_same(run_gpu(cl, fr, mode), ref)
     finally:
-        cl.set_tuning(tile=4, nt=1, unroll=1, blocks_per_cu=4)
+        cl.set_tuning(tile=5, nt=1, unroll=1, blocks_per_cu=0, load_nt=1)
 
 
 def test_tile_path_ragged_and_offset(l3, gpu):
@@ -352,10 +354,10 @@ def test_tile_path_ragged_and_offset(l3, gpu):
     n = 64 * 1000 + 37
     fr = pktgen.packed_ipv4(n + 1, routes=pktgen.l3fwd_routes(), device=gpu, seed=14)
     fr2 = pktgen.Frames(fr.slab, n, stride=64, data_off=16)
-    for tile in (0, 1, 2, 3, 4):
+    for tile in (0, 1, 2, 3, 4, 5):
         cl.set_tuning(tile=tile)
         assert_same(run_gpu(cl, fr2, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr2, tables4=t4))
-    cl.set_tuning(tile=4)
+    cl.set_tuning(tile=5)
 
 
 def test_dir16_on_off_identical(l3, cnet, gpu):
@@ -366,10 +368,10 @@ def test_dir16_on_off_identical(l3, cnet, gpu):
                                 in_route_frac=frac)
         ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
         for d in (0, 1):
-            for tile in (0, 1, 3, 4):
+            for tile in (0, 1, 3, 4, 5):
                 cl.set_tuning(dir16=d, tile=tile)
                 assert_same(run_gpu(cl, fr, N.CNDP_MODE_L3FWD), ref)
-    cl.set_tuning(dir16=1, tile=4)
+    cl.set_tuning(dir16=1, tile=5)
     ccl, routes, v6, ct4, ct6 = cnet
     fr = pktgen.imix(1 << 16, v4routes=routes, v6routes=v6, device=gpu, seed=5)
     ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
@@ -575,13 +577,13 @@ def test_cnet_ptype_and_rxmeta(cnet, l3, gpu):
     ccl.set_tuning(cnet_tile=1)
     fr = pktgen.fuzz_frames(64 * 300, seed=13, slot=64, device=gpu)
     ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
-    for tile in (0, 3, 4):
+    for tile in (0, 3, 4, 5):
         cl.set_tuning(tile=tile)
         out = cl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
         cl.classify(fr, N.CNDP_MODE_L3FWD, out=out)
         torch.cuda.synchronize()
         assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
-    cl.set_tuning(tile=4)
+    cl.set_tuning(tile=5)
 
 
 def _gtp_mix(n, routes, v6, gpu, seed):
