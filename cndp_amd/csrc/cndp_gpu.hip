@@ -131,6 +131,7 @@ struct KArgs {
     uint32_t *spec_nh; // cnet speculation model: input-node result of every frame a
                        // ptype-node group could send to ip4/ip6_input (else ~0)
     uint32_t *spec_flags; // 2048-bit set of the type signatures seen (speculation model)
+    uint16_t *spec_t16;   // speculation model: packet_type & 0xFFFF of every frame
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -1178,6 +1179,14 @@ __device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
 
 __device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
 
+// Burst / chunk maps store their target states tagged with the target's
+// signature class (state | class << 16; SPEC_UNCH = keep the state), so map
+// composition never recomputes a signature.
+__device__ __forceinline__ uint32_t spec_tag(uint32_t st, const uint8_t *class_id)
+{
+    return st == 0xFFFFFFFFu ? st : (st & 0xffffu) | ((uint32_t)class_id[spec_sig(st)] << 16);
+}
+
 // OR the signature bit of each active lane into a 64-word LDS bitmap with one
 // LDS atomic per distinct word in the wave
 __device__ __forceinline__ void spec_mark(uint32_t *s_f, bool on, uint32_t g)
@@ -1351,6 +1360,7 @@ __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
            (((uintptr_t)a.slab + base) & 15u) == 0;
 }
 
+template <bool LNT>
 __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_classify_cnet_tile(KArgs a, uint64_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
@@ -1400,7 +1410,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             // 36 KiB) Toeplitz table instead, so every load is unconditional
             const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u
                                                    : (const uint8_t *)a.ttab + part * 16u;
-            r[k] = t < n_tiles ? *(const u32x4 *)src : (u32x4){0, 0, 0, 0};
+            r[k] = t < n_tiles ? ldg4<LNT>(src) : (u32x4){0, 0, 0, 0};
         }
     }
     for (; t < n_tiles; t += wstep) {
@@ -1578,7 +1588,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 qb[k] = __shfl(nb, 16 * k + (int)fr_in_k);
                 const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u
                                                        : (const uint8_t *)a.ttab + part * 16u;
-                r[k] = *(const u32x4 *)src;
+                r[k] = ldg4<LNT>(src);
             }
             off_cur = off_nxt;
             if (a.offsets) {
@@ -1619,8 +1629,12 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             edge = nh >> 24;
         }
         if (a.spec_nh) {
+            // the input-node result is kept for the frames whose own edge does
+            // not carry it in nh already (spec_fix reads nh for the others)
+            if (live && (do4 || do6) && (!a.nh || (pe != 3u && pe != 4u)))
+                a.spec_nh[i] = e >> 1;
             if (live)
-                a.spec_nh[i] = do4 || do6 ? e >> 1 : CNDP_NH_INVALID;
+                a.spec_t16[i] = (uint16_t)pt;
             spec_mark(s_sf, live, spec_sig(pt & 0xffffu));
         }
         __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
@@ -1702,25 +1716,25 @@ __global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint
 
 // the 4 types of the group at packet j (16-B load when the burst size keeps
 // groups 16-B aligned)
-__device__ __forceinline__ void spec_group(const uint32_t *__restrict__ pt, uint64_t j, bool vec, uint32_t &l0,
+__device__ __forceinline__ void spec_group(const uint16_t *__restrict__ pt, uint64_t j, bool vec, uint32_t &l0,
                                            uint32_t &l1, uint32_t &l2, uint32_t &l3)
 {
     if (vec) {
-        const u32x4 q = *(const u32x4 *)(pt + j);
+        const u32x2 q = *(const u32x2 *)(pt + j);
         l0 = q.x & 0xffffu;
-        l1 = q.y & 0xffffu;
-        l2 = q.z & 0xffffu;
-        l3 = q.w & 0xffffu;
+        l1 = q.x >> 16;
+        l2 = q.y & 0xffffu;
+        l3 = q.y >> 16;
     } else {
-        l0 = pt[j] & 0xffffu;
-        l1 = pt[j + 1] & 0xffffu;
-        l2 = pt[j + 2] & 0xffffu;
-        l3 = pt[j + 3] & 0xffffu;
+        l0 = pt[j];
+        l1 = pt[j + 1];
+        l2 = pt[j + 2];
+        l3 = pt[j + 3];
     }
 }
 
 // one burst's effect on a state of signature sig: SPEC_UNCH or the new state
-__device__ uint32_t spec_burst_map(const uint32_t *__restrict__ pt, uint64_t b0, uint32_t cnt, uint32_t sig,
+__device__ uint32_t spec_burst_map(const uint16_t *__restrict__ pt, uint64_t b0, uint32_t cnt, uint32_t sig,
                                    bool vec)
 {
     uint32_t low = sig >> 3, E = sig & 7u, c = SPEC_UNCH;
@@ -1789,8 +1803,9 @@ __device__ __forceinline__ void spec_walk(const uint32_t *st, uint32_t g0, uint3
 
 // one wave per burst: the burst's types are staged through LDS (1024 at a
 // time) and lane k runs the group walk for signature class k
-__global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, const uint32_t *meta, uint32_t *T)
+__global__ __launch_bounds__(256) void k_spec_tables(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                     uint64_t nb, const uint32_t *meta, const uint8_t *class_id,
+                                                     uint32_t *T)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][SPEC_STAGE];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -1806,7 +1821,7 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
     for (uint32_t c0 = 0; c0 + 4 <= cnt; c0 += SPEC_STAGE) {
         const uint32_t m = cnt - c0 < SPEC_STAGE ? cnt - c0 : SPEC_STAGE;
         for (uint32_t k = lane; k < m; k += 64) { // type | p_nxt << 16, computed in parallel
-            const uint32_t l = pt[b0 + c0 + k] & 0xffffu;
+            const uint32_t l = pt[b0 + c0 + k];
             st[k] = l | (cnet_edge(l) << 16);
         }
         __builtin_amdgcn_wave_barrier();
@@ -1831,7 +1846,7 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
         __builtin_amdgcn_wave_barrier();
     }
     if (lane < K)
-        T[b * SPEC_KMAX + lane] = c;
+        T[b * SPEC_KMAX + lane] = spec_tag(c, class_id);
 }
 
 // Burst maps are composed with a two-level LDS scan when at most
@@ -1840,24 +1855,36 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint32_t *__restrict_
 #define SPEC_KFAST 8
 #define SPEC_BLK 256
 
+// the 2 KiB class table into LDS with one 16-B load per thread (threads >= 128 idle)
+__device__ __forceinline__ void spec_cls_stage(uint8_t *s_cls, const uint8_t *class_id, uint32_t tid, uint32_t nthr)
+{
+    for (uint32_t k = tid; k < 128; k += nthr)
+        ((u32x4 *)s_cls)[k] = ((const u32x4 *)class_id)[k];
+}
+
+// plain state st after the tagged map m (in memory)
 __device__ __forceinline__ uint32_t spec_apply(const uint32_t *m, const uint8_t *cls, uint32_t st)
 {
     const uint32_t nx = m[cls[spec_sig(st)]];
+    return nx == SPEC_UNCH ? st : nx & 0xffffu;
+}
+
+// tagged state st after the tagged map m (an LDS row)
+__device__ __forceinline__ uint32_t spec_apply_t(const uint32_t *m, uint32_t st)
+{
+    const uint32_t nx = m[st >> 16];
     return nx == SPEC_UNCH ? st : nx;
 }
 
-// per block of SPEC_BLK bursts: inclusive scan of the burst maps (P), and the
-// block's total map (Bt)
-__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint8_t *class_id,
-                                                        const uint32_t *T, uint32_t *P, uint32_t *Bt)
+// per block of SPEC_BLK bursts or chunks: inclusive scan of their maps (P),
+// and the block's total map (Bt)
+__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint32_t *T,
+                                                        uint32_t *P, uint32_t *Bt)
 {
-    __shared__ uint8_t s_cls[2048];
-    __shared__ uint32_t s_m[SPEC_BLK][SPEC_KFAST];
+    __shared__ uint32_t s_m[SPEC_BLK][SPEC_KFAST + 1];
     const uint32_t K = meta[0];
     if (K > SPEC_KFAST)
         return;
-    for (uint32_t k = threadIdx.x; k < 2048; k += SPEC_BLK)
-        s_cls[k] = class_id[k];
     const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + threadIdx.x;
     uint32_t m[SPEC_KFAST];
 #pragma unroll
@@ -1874,8 +1901,7 @@ __global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uin
 #pragma unroll
             for (uint32_t k = 0; k < SPEC_KFAST; k++) {
                 const uint32_t ek = e[k];
-                if (k < K)
-                    m[k] = ek == SPEC_UNCH ? l[k] : spec_apply(l, s_cls, ek);
+                m[k] = k >= K ? SPEC_UNCH : ek == SPEC_UNCH ? l[k] : spec_apply_t(l, ek);
             }
         }
         __syncthreads();
@@ -1888,55 +1914,36 @@ __global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uin
             Bt[(uint64_t)blockIdx.x * SPEC_KFAST + k] = m[k];
 }
 
-// start state of every block (walking the block totals) and the final state;
-// with more than SPEC_KFAST signatures: one sequential walk over the bursts
-__global__ __launch_bounds__(64) void k_spec_scan_b(const uint32_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                   uint64_t nb, uint64_t nblk, const uint32_t *meta,
-                                                   const uint8_t *class_id, const uint32_t *Bt, uint32_t *Sblk,
-                                                   uint32_t *S, uint32_t *state)
-{
-    __shared__ uint8_t s_cls[2048];
-    for (uint32_t k = threadIdx.x; k < 2048; k += 64)
-        s_cls[k] = class_id[k];
-    __syncthreads();
-    if (threadIdx.x != 0)
-        return;
-    const uint32_t K = meta[0];
-    uint32_t st = *state & 0xffffu;
-    if (K <= SPEC_KFAST)
-        return; // k_spec_scan_c walks the block totals
-    {
-        for (uint64_t b = 0; b < nb; b++) {
-            S[b] = st;
-            const uint64_t b0 = b * B;
-            const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
-            const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
-            if (c != SPEC_UNCH)
-                st = c;
-        }
-        *state = st;
-        return;
-    }
-    *state = st; // overwritten below; keeps the K > SPEC_KFAST exit simple
-}
-
-// block start states: the block totals are walked from LDS in windows
 // block start states: Hillis-Steele over the block totals, 1024 at a time
-// with the composed map of the earlier windows carried along
+// with the composed map of the earlier windows carried along, and the final
+// state.  With more than SPEC_KFAST signatures: one thread walks the bursts
+// sequentially instead (S = the state entering every burst).
 __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
-                                                     const uint32_t *Bt, uint32_t *Sblk, uint32_t *state)
+                                                     const uint32_t *Bt, uint32_t *Sblk, uint32_t *state,
+                                                     const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                     uint64_t nb, uint32_t *S)
 {
-    __shared__ uint8_t s_cls[2048];
-    __shared__ uint32_t s_m[1024][SPEC_KFAST];
+    __shared__ uint32_t s_m[1024][SPEC_KFAST + 1];
     __shared__ uint32_t s_carry[SPEC_KFAST];
     const uint32_t K = meta[0], t = threadIdx.x;
-    if (K > SPEC_KFAST)
+    if (K > SPEC_KFAST) {
+        if (t == 0) {
+            uint32_t st = *state & 0xffffu;
+            for (uint64_t b = 0; b < nb; b++) {
+                S[b] = st;
+                const uint64_t b0 = b * B;
+                const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
+                const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
+                if (c != SPEC_UNCH)
+                    st = c;
+            }
+            *state = st;
+        }
         return;
-    for (uint32_t k = t; k < 2048; k += 1024)
-        s_cls[k] = class_id[k];
+    }
     if (t < SPEC_KFAST)
         s_carry[t] = SPEC_UNCH;
-    const uint32_t s0 = *state & 0xffffu;
+    const uint32_t s0 = spec_tag(*state & 0xffffu, class_id);
     __syncthreads();
     for (uint64_t w0 = 0; w0 < nblk; w0 += 1024) {
         const uint64_t k0 = w0 + t;
@@ -1944,7 +1951,8 @@ __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint3
 #pragma unroll
         for (uint32_t k = 0; k < SPEC_KFAST; k++)
             m[k] = k0 < nblk && k < K ? Bt[k0 * SPEC_KFAST + k] : SPEC_UNCH;
-        for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t dmax = nblk - w0 < 1024 ? (uint32_t)(nblk - w0) : 1024u;
+        for (uint32_t d = 1; d < dmax; d <<= 1) {
 #pragma unroll
             for (uint32_t k = 0; k < SPEC_KFAST; k++)
                 s_m[t][k] = m[k];
@@ -1954,24 +1962,28 @@ __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint3
 #pragma unroll
                 for (uint32_t k = 0; k < SPEC_KFAST; k++) {
                     const uint32_t ek = e[k];
-                    if (k < K)
-                        m[k] = ek == SPEC_UNCH ? l[k] : spec_apply(l, s_cls, ek);
+                    m[k] = k >= K ? SPEC_UNCH : ek == SPEC_UNCH ? l[k] : spec_apply_t(l, ek);
                 }
             }
             __syncthreads();
         }
-        // state entering block k0: the carry, then this window's blocks before k0
-        uint32_t st = spec_apply(s_carry, s_cls, s0);
-        if (t > 0)
-            st = spec_apply(s_m[t - 1], s_cls, st);
-        if (k0 < nblk)
-            Sblk[k0] = st;
+#pragma unroll
+        for (uint32_t k = 0; k < SPEC_KFAST; k++)
+            s_m[t][k] = m[k];
         __syncthreads();
-        if (t == 1023) { // carry = carry then this window's total
+        // state entering block k0: the carry, then this window's blocks before k0
+        uint32_t st = spec_apply_t(s_carry, s0);
+        if (t > 0)
+            st = spec_apply_t(s_m[t - 1], st);
+        if (k0 < nblk)
+            Sblk[k0] = st & 0xffffu;
+        __syncthreads();
+        if (t == 0) { // carry = carry then this window's total
+            const uint32_t *tot = s_m[dmax - 1];
             uint32_t nc[SPEC_KFAST];
             for (uint32_t k = 0; k < SPEC_KFAST; k++) {
                 const uint32_t ck = s_carry[k];
-                nc[k] = k >= K ? SPEC_UNCH : ck == SPEC_UNCH ? m[k] : spec_apply(m, s_cls, ck);
+                nc[k] = k >= K ? SPEC_UNCH : ck == SPEC_UNCH ? tot[k] : spec_apply_t(tot, ck);
             }
             for (uint32_t k = 0; k < SPEC_KFAST; k++)
                 s_carry[k] = nc[k];
@@ -1979,15 +1991,16 @@ __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint3
         __syncthreads();
     }
     if (t == 0)
-        *state = spec_apply(s_carry, s_cls, s0);
+        *state = spec_apply_t(s_carry, s0) & 0xffffu;
 }
 
 __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
 {
     const uint32_t own = cnet_edge(own_l);
-    const uint32_t old_nh = own == 3u || own == 4u ? a.spec_nh[i] : CNDP_NH_INVALID;
-    const uint32_t old_edge = own == 3u || own == 4u ? old_nh >> 24 : 0x80u | own;
-    const uint32_t nh = dst == 3u || dst == 4u ? a.spec_nh[i] : CNDP_NH_INVALID;
+    const bool own_in = own == 3u || own == 4u;
+    const uint32_t old_nh = own_in ? (a.nh ? a.nh[i] : a.spec_nh[i]) : CNDP_NH_INVALID;
+    const uint32_t old_edge = own_in ? old_nh >> 24 : 0x80u | own;
+    const uint32_t nh = dst == 3u || dst == 4u ? (own_in ? old_nh : a.spec_nh[i]) : CNDP_NH_INVALID;
     const uint32_t edge = dst == 3u || dst == 4u ? nh >> 24 : 0x80u | dst;
     if (a.nh)
         a.nh[i] = nh;
@@ -2002,16 +2015,12 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
 // one wave per burst: start state from the scan, types staged through LDS;
 // every lane walks the groups (uniform, broadcast LDS reads) and remembers
 // the state at the groups it owns (g % 64 == lane), then fixes those groups
-__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, const uint32_t *meta,
-                                                   const uint8_t *class_id, const uint32_t *P, const uint32_t *Sblk,
-                                                   const uint32_t *S)
+__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, uint32_t kseq,
+                                                   const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
+                                                   const uint32_t *Sblk, const uint32_t *S)
 {
-    __shared__ uint8_t s_cls[2048];
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][SPEC_STAGE];
     __shared__ uint8_t s_q[4][SPEC_STAGE / 4];
-    for (uint32_t k = threadIdx.x; k < 2048; k += 256)
-        s_cls[k] = class_id[k];
-    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t b = (uint64_t)blockIdx.x * 4 + wv;
     if (b >= nb)
@@ -2020,18 +2029,18 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
     const uint64_t b0 = b * B;
     const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
     uint32_t s0;
-    if (meta[0] > SPEC_KFAST) {
+    if (meta[0] > kseq) {
         s0 = S[b];
     } else { // block start state through the block's earlier bursts (exclusive prefix)
         const uint64_t blk = b / SPEC_BLK;
-        s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * SPEC_KFAST, s_cls, Sblk[blk]);
+        s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * SPEC_KFAST, class_id, Sblk[blk]);
     }
     uint32_t low = s0 & 0xffu, E = cnet_edge(s0);
     uint8_t *sq = s_q[wv];
     for (uint32_t c0 = 0; c0 + 4 <= cnt; c0 += SPEC_STAGE) {
         const uint32_t m = cnt - c0 < SPEC_STAGE ? cnt - c0 : SPEC_STAGE;
         for (uint32_t k = lane; k < m; k += 64) {
-            const uint32_t l = a.ptype[b0 + c0 + k] & 0xffffu;
+            const uint32_t l = a.spec_t16[b0 + c0 + k];
             st[k] = l | (cnet_edge(l) << 16);
         }
         __builtin_amdgcn_wave_barrier();
@@ -2088,6 +2097,185 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
                 }
         }
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Chunked speculation passes for graph bursts of B <= 256 packets (<= 64
+// groups, one group per lane): one wave per chunk of SPEC_CH bursts, the
+// chunk's types staged in LDS by one batch of loads.
+//   k_spec_ctables  the chunk's map (its bursts' maps composed), lane k =
+//                   signature class k -- the scans then run over chunks;
+//   k_spec_cemit    from the chunk's entering state, burst after burst: lane
+//                   g finds the state entering group g, fixes its frames if
+//                   the group is quiet under it, and lane ng-1 hands the
+//                   burst's exit state to the next burst.
+// ---------------------------------------------------------------------------
+#define SPEC_CH 4 // measured: 4 beats 1 and 16 (occupancy vs per-wave latency)
+
+// stage the types of bursts [c0, c1) as type | p_nxt << 16, burst j at
+// st + (j - c0) * spec_bstride(B) (16-B aligned groups for any B)
+__device__ __forceinline__ uint32_t spec_bstride(uint32_t B) { return (B + 3u) & ~3u; }
+
+template <int CH>
+__device__ __forceinline__ void spec_stage_chunk(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                 uint64_t c0, uint64_t c1, uint32_t lane, uint32_t *st)
+{
+    const uint32_t bs = spec_bstride(B);
+    if ((B & 7u) == 0) {
+        // bursts are contiguous in LDS too (bs == B): 16-B loads of 8 types,
+        // every load of the chunk issued before the first is used
+        const uint64_t p0 = c0 * B, p1 = c1 * B < n ? c1 * B : n;
+        const uint32_t m = (uint32_t)(p1 - p0);
+        constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+        u32x4 v[R];
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t idx = (r * 64u + lane) * 8u;
+            v[r] = idx + 8u <= m ? *(const u32x4 *)(pt + p0 + idx) : (u32x4){0, 0, 0, 0};
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t idx = (r * 64u + lane) * 8u;
+            if (idx >= m)
+                continue;
+            uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            if (idx + 8u > m) // the batch's last partial vector
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint32_t lo = idx + 2 * q < m ? pt[p0 + idx + 2 * q] : 0u;
+                    const uint32_t hi = idx + 2 * q + 1 < m ? pt[p0 + idx + 2 * q + 1] : 0u;
+                    w[q] = lo | (hi << 16);
+                }
+            u32x4 o0, o1;
+            o0.x = (w[0] & 0xffffu) | (cnet_edge(w[0]) << 16);
+            o0.y = (w[0] >> 16) | (cnet_edge(w[0] >> 16) << 16);
+            o0.z = (w[1] & 0xffffu) | (cnet_edge(w[1]) << 16);
+            o0.w = (w[1] >> 16) | (cnet_edge(w[1] >> 16) << 16);
+            o1.x = (w[2] & 0xffffu) | (cnet_edge(w[2]) << 16);
+            o1.y = (w[2] >> 16) | (cnet_edge(w[2] >> 16) << 16);
+            o1.z = (w[3] & 0xffffu) | (cnet_edge(w[3]) << 16);
+            o1.w = (w[3] >> 16) | (cnet_edge(w[3] >> 16) << 16);
+            *(u32x4 *)(st + idx) = o0;
+            *(u32x4 *)(st + idx + 4) = o1;
+        }
+    } else {
+        for (uint64_t j = c0; j < c1; j++) {
+            const uint64_t p0 = j * B;
+            const uint32_t cnt = (uint32_t)((uint64_t)n - p0 < B ? (uint64_t)n - p0 : B);
+            uint32_t *d = st + (j - c0) * bs;
+            for (uint32_t k = lane; k < cnt; k += 64) {
+                const uint32_t l = pt[p0 + k];
+                d[k] = l | (cnet_edge(l) << 16);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                      uint64_t nb, uint64_t nch, const uint32_t *meta,
+                                                      const uint8_t *class_id, uint32_t *T)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    const uint32_t K = meta[0];
+    if (c >= nch || K > SPEC_KMAX)
+        return;
+    uint32_t *st = s_pt[wv];
+    const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+    spec_stage_chunk<CH>(pt, n, B, c0, c1, lane, st);
+    const uint32_t sig = lane < K ? meta[1 + lane] : 0u;
+    uint32_t cm = SPEC_UNCH;
+    for (uint64_t bb = c0; bb < c1; bb++) {
+        const uint32_t *sb = st + (bb - c0) * spec_bstride(B);
+        const uint64_t b0 = bb * B;
+        const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
+        const uint32_t ng = cnt >> 2;
+        const SpecGroups sg = spec_groups(sb, ng, lane);
+        uint32_t mp = SPEC_UNCH;
+        if (sg.U) {
+            const uint32_t u = 63u - (uint32_t)__clzll(sg.U);
+            uint32_t cu = sb[4 * u + 3] & 0xffffu, lu = cu & 0xffu, Eu = sb[4 * u + 3] >> 16;
+            spec_walk(sb, u + 1, ng, lu, Eu, cu);
+            mp = cu;
+        } else if (sg.uniform) {
+            mp = (sig >> 3) == sg.v ? SPEC_UNCH : sg.first;
+        } else {
+            uint32_t low = sig >> 3, E = sig & 7u;
+            spec_walk(sb, 0, ng, low, E, mp);
+        }
+        // cm = this burst after the chunk so far (tagged states)
+        mp = lane < K ? spec_tag(mp, class_id) : SPEC_UNCH;
+        const uint32_t nx = __shfl(mp, (int)(cm == SPEC_UNCH ? 0u : cm >> 16));
+        cm = cm == SPEC_UNCH ? mp : nx == SPEC_UNCH ? cm : nx;
+    }
+    if (lane < K)
+        T[c * SPEC_KMAX + lane] = cm;
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_t nb, uint64_t nch,
+                                                    const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
+                                                    const uint32_t *Sblk, const uint32_t *S)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if (c >= nch)
+        return;
+    uint32_t *st = s_pt[wv];
+    const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+    uint32_t s0;
+    if (meta[0] > SPEC_KFAST) {
+        s0 = S[c0];
+    } else { // chunk start state: the block's start, then the block's earlier chunks
+        const uint64_t blk = c / SPEC_BLK;
+        s0 = c % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (c - 1) * SPEC_KFAST, class_id, Sblk[blk]);
+    }
+    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st);
+    for (uint64_t bb = c0; bb < c1; bb++) {
+        const uint32_t *sb = st + (bb - c0) * spec_bstride(B);
+        const uint64_t b0 = bb * B;
+        const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
+        const uint32_t ng = cnt >> 2;
+        const SpecGroups sg = spec_groups(sb, ng, lane);
+        const uint32_t low0 = s0 & 0xffu;
+        uint32_t nxt = s0; // the state after this lane's group
+        if (lane < ng) {
+            // the state entering group `lane`
+            uint32_t cur = s0, l = low0, e = cnet_edge(s0);
+            const unsigned long long before = sg.U & ((1ull << lane) - 1ull);
+            if (before) {
+                const uint32_t u = 63u - (uint32_t)__clzll(before);
+                cur = sb[4 * u + 3] & 0xffffu;
+                l = cur & 0xffu;
+                e = sb[4 * u + 3] >> 16;
+                spec_walk(sb, u + 1, lane, l, e, cur);
+            } else if (sg.uniform) {
+                if (lane > 0 && low0 != sg.v) {
+                    cur = sg.first;
+                    l = cur & 0xffu;
+                    e = sb[3] >> 16;
+                }
+            } else {
+                spec_walk(sb, 0, lane, l, e, cur);
+            }
+            const u32x4 x = *(const u32x4 *)(sb + 4 * lane);
+            const bool quiet = (x.x & 0xffu) == l && (x.y & 0xffu) == l && (x.z & 0xffu) == l && (x.w & 0xffu) == l;
+            nxt = cur;
+            if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || e == (x.w >> 16)))
+                nxt = x.w & 0xffffu;
+            if (quiet) { // the group goes whole to p_nxt[state]
+                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++)
+                    if ((xs[j] >> 16) != e)
+                        spec_fix(a, b0 + lane * 4u + j, xs[j] & 0xffffu, e);
+            }
+        }
+        s0 = ng ? __shfl(nxt, (int)ng - 1) : s0;
     }
 }
 
@@ -2291,7 +2479,7 @@ struct cndp_gpu_ctx {
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
     uint32_t *sp_small;   // [0] last_type, [1..65] class meta, [66..129] signature flags
     uint8_t *sp_class;    // class id per signature (2048)
-    uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U;
+    uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U; // sp_pt: the u16 types (speculation model)
     uint64_t sp_n_cap, sp_b_cap;
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
     hipStream_t hs[3];    // copy-in, classify, copy-out
@@ -2812,7 +3000,7 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
         c->sp_pt = c->sp_nh = nullptr;
         c->sp_n_cap = 0;
         const uint64_t cap = n + (n >> 3) + 1024;
-        HIP_TRY(hipMalloc((void **)&c->sp_pt, cap * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_pt, cap * 2));
         HIP_TRY(hipMalloc((void **)&c->sp_nh, cap * 4));
         c->sp_n_cap = cap;
     }
@@ -2894,8 +3082,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         if (B && (r = spec_scratch(c, b->n, ((uint64_t)b->n + B - 1) / B)))
             return r;
         if (B) {
-            if (!a.ptype)
-                a.ptype = c->sp_pt;
+            a.spec_t16 = (uint16_t *)c->sp_pt;
             a.spec_nh = c->sp_nh;
             a.spec_flags = c->sp_small + 66;
             HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
@@ -2905,7 +3092,10 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
             if (gt > cap)
                 gt = cap;
-            hipLaunchKernelGGL(k_classify_cnet_tile, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+            if (c->tune_lnt)
+                hipLaunchKernelGGL(k_classify_cnet_tile<true>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+            else
+                hipLaunchKernelGGL(k_classify_cnet_tile<false>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
         } else {
             hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
         }
@@ -2914,20 +3104,39 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
             hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta);
             const uint32_t gw = (uint32_t)((nb + 3) / 4); // one wave per burst
-            hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint32_t *)a.ptype, b->n, B, nb,
-                               (const uint32_t *)meta, c->sp_T);
-            const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
-            uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
-            hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb, (const uint32_t *)meta,
-                               (const uint8_t *)c->sp_class, (const uint32_t *)c->sp_T, P, Bt);
-            hipLaunchKernelGGL(k_spec_scan_b, dim3(1), dim3(64), 0, s, (const uint32_t *)a.ptype, b->n, B, nb, nblk,
-                               (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk,
-                               c->sp_S, state);
-            hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
-                               (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state);
-            hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, (const uint32_t *)meta,
-                               (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
-                               (const uint32_t *)c->sp_S);
+            if (B <= 256) { // chunked passes (SPEC_CH bursts per wave)
+                const uint64_t nch = (nb + SPEC_CH - 1) / SPEC_CH;
+                const uint32_t gc = (uint32_t)((nch + 3) / 4);
+                auto ct = k_spec_ctables<SPEC_CH>;
+                auto ce = k_spec_cemit<SPEC_CH>;
+                hipLaunchKernelGGL(ct, dim3(gc), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B, nb, nch,
+                                   (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
+                const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
+                uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
+                hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nch,
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P,
+                                   Bt);
+                hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
+                                   (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
+                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S);
+                hipLaunchKernelGGL(ce, dim3(gc), dim3(256), 0, s, a, B, nb, nch, (const uint32_t *)meta,
+                                   (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
+                                   (const uint32_t *)c->sp_S);
+            } else {
+                hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
+                                   nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
+                const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
+                uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
+                hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb,
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P,
+                                   Bt);
+                hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
+                                   (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
+                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S);
+                hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, (uint32_t)SPEC_KFAST,
+                                   (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
+                                   (const uint32_t *)Sblk, (const uint32_t *)c->sp_S);
+            }
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
