@@ -132,6 +132,10 @@ struct KArgs {
                        // ptype-node group could send to ip4/ip6_input (else ~0)
     uint32_t *spec_flags; // 2048-bit set of the type signatures seen (speculation model)
     uint16_t *spec_t16;   // speculation model: packet_type & 0xFFFF of every frame
+    // cnet fast / general split (k_cnet_stream -> k_classify_cnet): frames the
+    // fast kernel leaves to the general parse, and their count
+    uint32_t *wl;
+    uint32_t *wl_n;
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -1207,14 +1211,20 @@ __device__ __forceinline__ void spec_mark(uint32_t *s_f, bool on, uint32_t g)
 }
 
 
+template <bool WL>
 __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
     __shared__ uint32_t s_win[CNET_THREADS * ROW_DW];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ uint32_t s_sf[64]; // type signatures seen (speculation model)
 
     const uint32_t tid = threadIdx.x;
+    if (WL && (uint64_t)blockIdx.x * CNET_THREADS >= *a.wl_n)
+        return; // nothing left for this block
+    if (tid < 64)
+        s_sf[tid] = 0;
     for (uint32_t k = tid; k < TAB_POS * 256; k += CNET_THREADS)
         s_t[k] = a.ttab[k];
     for (uint32_t k = tid; k <= a.reta_mask; k += CNET_THREADS)
@@ -1228,7 +1238,10 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
     uint32_t *row = s_win + tid * ROW_DW;
     row[WIN_DW] = 0;
     const uint64_t step = (uint64_t)gridDim.x * CNET_THREADS;
-    for (uint64_t i = (uint64_t)blockIdx.x * CNET_THREADS + tid; i < a.n; i += step) {
+    // WL: the frames k_cnet_stream left to the general parse (a.wl[0 .. *a.wl_n))
+    const uint64_t n_it = WL ? (uint64_t)*a.wl_n : a.n;
+    for (uint64_t j = (uint64_t)blockIdx.x * CNET_THREADS + tid; j < n_it; j += step) {
+        const uint64_t i = WL ? (uint64_t)a.wl[j] : j;
         const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
         const uint8_t *p = a.slab + base;
         const uint64_t avail = base < a.slab_len ? a.slab_len - base : 0;
@@ -1269,7 +1282,13 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
                 h ^= tz4(s_t, 32, w.ld32(ip + ln.l3));
         }
         const uint32_t pe = cnet_edge(pt);
-        if (pe == 3u) {
+        // with the speculation model, frames of the types a quiet 4-group can
+        // carry into ip4/ip6_input get the input node's result as well
+        const uint32_t lb = pt & 0xffu;
+        const bool alt4 = a.spec_nh && (lb == 0x11u || lb == 0x31u || lb == 0x91u);
+        const bool alt6 = a.spec_nh && (lb == 0x41u || lb == 0xc1u || lb == 0xe1u);
+        bool has = false;
+        if (pe == 3u || alt4) {
             // ip4_input.c:121-140: total_length < buf_len && cksum == 0
             const uint32_t x0 = w.ld32(ip);
             const uint32_t hl = (x0 & 0xfu);
@@ -1283,8 +1302,8 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
             const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
             const uint32_t dip = ok ? w.be32(ip + 16) : 0u;
             nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, dip) : lpm4(a.tbl24, a.tbl8, dip);
-            edge = nh >> 24;
-        } else if (pe == 4u) {
+            has = true;
+        } else if (pe == 4u || alt6) {
             // ip6_input.c:115-135: payload_len < buf_len, else dip = ::
             const bool ok = w.be16(ip + 4) < a.buf_len;
             uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
@@ -1304,8 +1323,18 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
                 j++;
             }
             nh = e >> 1;
+            has = true;
+        }
+        if (a.spec_nh) {
+            if (has && (!a.nh || (pe != 3u && pe != 4u)))
+                a.spec_nh[i] = nh;
+            a.spec_t16[i] = (uint16_t)pt;
+            spec_mark(s_sf, true, spec_sig(pt & 0xffffu));
+        }
+        if (pe == 3u || pe == 4u) {
             edge = nh >> 24;
         } else {
+            nh = CNDP_NH_INVALID;
             edge = 0x80u | pe;
         }
         const uint32_t q = s_reta[h & a.reta_mask];
@@ -1320,12 +1349,14 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
         if (count)
             atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
     }
-    if (count) {
+    if (count || a.spec_flags)
         __syncthreads();
+    if (count)
         for (uint32_t k = tid; k < a.n_bins + 2; k += CNET_THREADS)
             if (s_bins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    }
+    if (a.spec_flags && tid < 64 && s_sf[tid])
+        atomicOr(&a.spec_flags[tid], s_sf[tid]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1655,6 +1686,286 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             if (count)
                 atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
         }
+    }
+    if (count || a.spec_flags)
+        __syncthreads();
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    if (a.spec_flags && tid < 64 && s_sf[tid])
+        atomicOr(&a.spec_flags[tid], s_sf[tid]);
+}
+
+// ---------------------------------------------------------------------------
+// Streamed cnet kernel (CNDP_TUNE_CNET_TILE 2): the wave-tile
+// kernel's fast path only -- Ethernet + IPv4 IHL 5 unfragmented or IPv6
+// without extension headers, carrying TCP / UDP / SCTP, 64 readable aligned
+// bytes -- with every other frame appended to a worklist that the general
+// per-lane kernel (k_classify_cnet<true>) finishes afterwards.  Without the
+// general parse the kernel is small enough to keep two window tiles in
+// flight: each loop trip resolves its whole FIB gather chain before it issues
+// the window loads of the tile two ahead, so the in-order vmcnt waits of the
+// chain only ever include loads issued a trip earlier.
+// ---------------------------------------------------------------------------
+struct CsOff { // this lane's frame offsets for tiles t, t+1, t+2 and the load for t+3
+    uint64_t o0, o1, o2, o3;
+};
+
+template <bool LNT>
+__device__ __forceinline__ void cs_issue(const KArgs &a, uint64_t tt, uint64_t n_tiles, uint64_t off,
+                                         uint32_t lane, u32x4 (&r)[4])
+{
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    const uint64_t my_base = tt < n_tiles ? ct_base(a, tt * 64u + lane, off) : ~0ull;
+    uint64_t qb[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        qb[k] = __shfl(my_base, 16 * k + (int)fr_in_k);
+        // frames off the fast path load a dummy chunk of the (aligned,
+        // 36 KiB) Toeplitz table instead, so every load is unconditional
+        const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u : (const uint8_t *)a.ttab + part * 16u;
+        r[k] = ldg4<LNT>(src);
+    }
+}
+
+template <bool LNT, int P>
+__device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wstep, uint64_t n_tiles, uint32_t lane,
+                                        u32x4 *tile, u32x4 (&r)[2][4], CsOff &off,
+                                        const uint32_t *s_t, const uint16_t *s_reta, uint32_t *s_bins,
+                                        uint32_t *s_sf, bool count)
+{
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    const uint64_t i = t * 64u + lane;
+    // (1) stage the tile (chunks of non-fast frames are never read)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t f = 16u * k + fr_in_k;
+        tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const bool live = i < a.n;
+    const uint64_t base = ct_base(a, i, off.o0);
+    const uint32_t sw = (lane >> 2) & 3u;
+    uint32_t W[16];
+    {
+        const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
+        W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
+        W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
+        W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
+        W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // (2) fast-path shape test (pktmbuf_ptype.c for these shapes); the rest go
+    // to the worklist
+    const uint32_t et = W[3] & 0xffffu; // raw bytes 12..13
+    const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
+    const bool l4p4 = p4 == 6u || p4 == 17u || p4 == 132u, l4p6 = p6 == 6u || p6 == 17u || p6 == 132u;
+    const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
+                    ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
+    const bool f6 = et == BE16C(0x86DDu) && l4p6;
+    const bool fast = live && ct_fast(a, base) && (f4 || f6);
+    {
+        const bool slow = live && !fast;
+        const unsigned long long m = __ballot(slow);
+        if (m) {
+            uint32_t w0 = 0;
+            if (lane == (uint32_t)(__ffsll(m) - 1))
+                w0 = atomicAdd(a.wl_n, (uint32_t)__popcll(m));
+            w0 = __shfl(w0, __ffsll(m) - 1);
+            if (slow)
+                a.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+        }
+    }
+    uint32_t pt = 0, pe = 0;
+    Lens lens{14u, 0u, 0u};
+    uint32_t hw[9];
+    uint32_t nw = 0, hl4 = 0;
+    uint32_t dip = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+    bool do4 = false, do6 = false;
+#pragma unroll
+    for (int k = 0; k < 9; k++)
+        hw[k] = 0;
+    if (fast) {
+        const uint32_t proto = f4 ? p4 : p6;
+        pt = (f4 ? 0x11u : 0x41u) | pt_l4(proto);
+        if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
+            const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
+            pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
+        }
+        pe = cnet_edge(pt);
+        const bool l4ok = proto == 6u || proto == 17u;
+        lens.l3 = f4 ? 20u : 40u;
+        if (a.rxmeta) // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
+            lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
+                    : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
+                         : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
+        if (f4) {
+            nw = 2;
+            hw[0] = alignb(W[7], W[6], 2);
+            hw[1] = alignb(W[8], W[7], 2);
+            hl4 = l4ok ? alignb(W[9], W[8], 2) : 0u;
+            if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
+                uint32_t sum = 0;
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
+                    sum += (x & 0xffffu) + (x >> 16);
+                }
+                sum = (sum >> 16) + (sum & 0xffffu);
+                sum = (sum >> 16) + (sum & 0xffffu);
+                const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
+                dip = ok ? bswap32(hw[1]) : 0u;
+                do4 = true;
+            }
+        } else {
+            nw = 8;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                hw[k] = alignb(W[6 + k], W[5 + k], 2);
+            hl4 = l4ok ? alignb(W[14], W[13], 2) : 0u;
+            if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
+                if (bswap16(W[4] >> 16) < a.buf_len) {
+                    d0 = hw[4];
+                    d1 = hw[5];
+                    d2 = hw[6];
+                    d3 = hw[7];
+                }
+                do6 = true;
+            }
+        }
+    }
+    // (3) the whole FIB gather chain of this tile (v4: directory or tbl24,
+    // page, tbl8; v6: tbl24 then tbl8 levels, trie.h:126-134)
+    const uint32_t *tb0;
+    uint32_t idx0;
+    if (!do4) {
+        tb0 = a.tbl24_6;
+        idx0 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu);
+    } else if (a.dir16) {
+        tb0 = a.dir16;
+        idx0 = dip >> 16;
+    } else {
+        tb0 = a.tbl24;
+        idx0 = dip >> 8;
+    }
+    uint32_t e = tb0[idx0];
+    {
+        uint32_t j = do6 ? 3u : (a.dir16 ? 1u : 2u);
+        bool more = (do4 || do6) && (e & 1u);
+        while (__any(more)) {
+            if (more) {
+                uint32_t byte;
+                const uint32_t *tb;
+                if (do6) {
+                    const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
+                    byte = (wd >> ((j & 3u) * 8)) & 0xffu;
+                    tb = a.tbl8_6;
+                } else {
+                    byte = j == 1 ? (dip >> 8) & 0xffu : dip & 0xffu;
+                    tb = j == 1 ? a.pages : a.tbl8;
+                }
+                e = tb[(e >> 1) * 256u + byte];
+                j++;
+                more = (e & 1u) && (do6 ? j < 16 : j <= 2);
+            }
+        }
+    }
+    // (4) the offsets one tile further, then the windows of tile t+2
+    {
+        const uint64_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
+        off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
+        cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
+    }
+    // (5) Toeplitz, results
+    uint32_t h = 0;
+    for (uint32_t k = 0; k < 8; k++)
+        if (k < nw)
+            h ^= tz4(s_t, 4 * k, hw[k]);
+    if (nw && hl4 != 0u)
+        h ^= tz4(s_t, 4 * nw, hl4);
+    uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
+    if ((do4 || do6) && (pe == 3u || pe == 4u)) {
+        nh = e >> 1;
+        edge = nh >> 24;
+    }
+    if (a.spec_nh) {
+        if (fast && (do4 || do6) && (!a.nh || (pe != 3u && pe != 4u)))
+            a.spec_nh[i] = e >> 1;
+        if (fast)
+            a.spec_t16[i] = (uint16_t)pt;
+        spec_mark(s_sf, fast, spec_sig(pt & 0xffffu));
+    }
+    if (fast) {
+        const uint32_t q = s_reta[h & a.reta_mask];
+        if (a.ptype)
+            a.ptype[i] = pt;
+        if (a.rxmeta)
+            a.rxmeta[i] = rx_meta(lens, W[0], W[1], et);
+        if (a.nh)
+            a.nh[i] = nh;
+        if (a.hash)
+            a.hash[i] = h;
+        if (a.queue)
+            a.queue[i] = (uint16_t)q;
+        if (a.edge)
+            a.edge[i] = (uint8_t)edge;
+        if (count)
+            atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
+    }
+    off.o0 = off.o1;
+    off.o1 = off.o2;
+    off.o2 = off.o3;
+}
+
+template <bool LNT>
+__global__ __launch_bounds__(CT_THREADS) void k_cnet_stream(KArgs a, uint64_t n_tiles)
+{
+    __shared__ uint32_t s_t[TAB_POS * 256];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ uint32_t s_sf[64];
+
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64)
+        s_sf[tid] = 0;
+    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint64_t wstep = (uint64_t)gridDim.x * CT_WAVES;
+    const uint64_t t0 = (uint64_t)blockIdx.x * CT_WAVES + wv;
+    CsOff off{0, 0, 0, 0};
+    if (a.offsets) {
+#pragma unroll
+        for (uint32_t s = 0; s < 3; s++) {
+            const uint64_t ts = t0 + s * wstep, is = ts * 64u + lane;
+            const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
+            if (s == 0)
+                off.o0 = o;
+            else if (s == 1)
+                off.o1 = o;
+            else
+                off.o2 = o;
+        }
+    }
+    u32x4 r[2][4];
+    cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
+    cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
+    for (uint64_t t = t0; t < n_tiles; t += 2u * wstep) {
+        cs_trip<LNT, 0>(a, t, wstep, n_tiles, lane, tile, r, off, s_t, s_reta, s_bins, s_sf, count);
+        if (t + wstep < n_tiles)
+            cs_trip<LNT, 1>(a, t + wstep, wstep, n_tiles, lane, tile, r, off, s_t, s_reta, s_bins, s_sf, count);
     }
     if (count || a.spec_flags)
         __syncthreads();
@@ -2478,6 +2789,8 @@ struct cndp_gpu_ctx {
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
     uint32_t *sp_small;   // [0] last_type, [1..65] class meta, [66..129] signature flags
+    uint32_t *cs_wl;      // k_cnet_stream worklist ([0] = count, then frame indices)
+    uint64_t cs_wl_cap;
     uint8_t *sp_class;    // class id per signature (2048)
     uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U; // sp_pt: the u16 types (speculation model)
     uint64_t sp_n_cap, sp_b_cap;
@@ -2623,6 +2936,8 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         hipFree(c->d_reta);
     if (c->d_part)
         hipFree(c->d_part);
+    if (c->cs_wl)
+        hipFree(c->cs_wl);
     free(c);
 }
 
@@ -3087,7 +3402,30 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             a.spec_flags = c->sp_small + 66;
             HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
         }
-        if (c->tune_cnet_tile || B) {
+        if (c->tune_cnet_tile == 2) {
+            // fast kernel, then the general parse of the frames it left
+            if ((uint64_t)b->n + 1 > c->cs_wl_cap) {
+                if (c->cs_wl)
+                    HIP_TRY(hipFree(c->cs_wl));
+                c->cs_wl = nullptr;
+                c->cs_wl_cap = 0;
+                const uint64_t wcap = (uint64_t)b->n + (b->n >> 3) + 1024;
+                HIP_TRY(hipMalloc((void **)&c->cs_wl, wcap * 4));
+                c->cs_wl_cap = wcap;
+            }
+            a.wl_n = c->cs_wl;
+            a.wl = c->cs_wl + 1;
+            HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
+            const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
+            uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
+            if (gt > cap)
+                gt = cap;
+            if (c->tune_lnt)
+                hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+            else
+                hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+            hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
+        } else if (c->tune_cnet_tile || B) {
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
             uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
             if (gt > cap)
@@ -3097,7 +3435,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             else
                 hipLaunchKernelGGL(k_classify_cnet_tile<false>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
         } else {
-            hipLaunchKernelGGL(k_classify_cnet, dim3(g), dim3(CNET_THREADS), 0, s, a);
+            hipLaunchKernelGGL(k_classify_cnet<false>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         }
         if (B) {
             const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
@@ -3886,7 +4224,9 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_dir16 = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_CNET_TILE:
-        c->tune_cnet_tile = value ? 1 : 0;
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_cnet_tile = value;
         return 0;
     case CNDP_TUNE_LOAD_NT:
         c->tune_lnt = value ? 1 : 0;
