@@ -299,6 +299,39 @@ def e2e_host(st, reps: int = 5):
     return res
 
 
+def imix_line(dev, rank: int, world: int, steps: int, warmup: int, parity: bool):
+    """Secondary line for the IMIX half of the metric (config C4, cnet chain),
+    measured the same way as the headline: ring of batches, one event pair
+    around `steps` back-to-back launches, max over ranks."""
+    from cndp_amd import dist as D
+    st = build_state("c4", dev, rank, None)
+    stream = torch.cuda.current_stream(dev)
+    for k in range(warmup):
+        run_step(st, stream, k)
+    torch.cuda.synchronize()
+    ok = parity_sample(st) if parity and rank == 0 else None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(steps):
+        run_step(st, stream, k)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], dev)
+    n = st["n"]
+    achieved = st["algo"] * n / (kern_ms * 1e-3) / 1e9
+    res = {"config": "c4", "workload": st["desc"], "value": round(n * world * steps / elapsed / 1e6, 2),
+           "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "kernel_ms": round(kern_ms, 5),
+           "achieved_GBs": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_pkt": st["algo"], "ring_batches": len(st["ring"]),
+           "parity_sample_vs_oracle": ok}
+    del st
+    torch.cuda.empty_cache()
+    return res
+
+
 def load_traffic(cfg: str):
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
@@ -322,6 +355,7 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) rates")
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr + gpurun_out)")
+    ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C4) line")
     ap.add_argument("--in-route-frac", type=float, default=0.9,
                     help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
     ap.add_argument("--ring", type=int, default=0,
@@ -387,17 +421,31 @@ def main():
     value = total_pkts / elapsed / 1e6
     achieved = st["algo"] * n / (kern_ms * 1e-3) / 1e9
     bins = out["bins"].cpu().numpy()
+    layout = ("packed 64-B slots" if fr.offsets is None and fr.stride == 64
+              else ("IMIX packed at roundup(len,64)" if fr.offsets is not None else f"{fr.stride}-B slots"))
+    ring_len = len(st["ring"])
+    cpu = e2e = None
     if rank == 0:
-        cpu = None
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
             cpu = cpu_baseline(st, args.cpu_budget)
-        e2e = None
         if world == 1 and not args.no_e2e and args.config != "c3rw":
             try:
                 e2e = e2e_host(st)
                 log(f"[bench] host-memory rates: {e2e}")
             except Exception as ex:  # reported, never fatal for the headline line
                 e2e = {"error": repr(ex)}
+    imix = None
+    if args.config in ("c2", "c3") and not args.no_imix:  # every rank (max over ranks inside)
+        del st["ring"], fr, out
+        st.pop("frames", None)
+        torch.cuda.empty_cache()
+        try:
+            imix = imix_line(dev, rank, world, max(5, args.steps // 2), args.warmup, not args.no_parity)
+            if rank == 0:
+                log(f"[bench] IMIX (C4) line: {imix}")
+        except Exception as ex:  # reported, never fatal for the headline line
+            imix = {"error": repr(ex)}
+    if rank == 0:
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -412,10 +460,8 @@ def main():
             "dtype": "u32",
             "data": "synthetic (seeded counter-hash frames generated in HBM)",
             "config": {"workload": st["desc"], "config": args.config, "packets_per_gpu": n,
-                       "frame_layout": "packed 64-B slots" if fr.offsets is None and fr.stride == 64
-                       else ("IMIX packed at roundup(len,64)" if fr.offsets is not None
-                             else f"{fr.stride}-B slots"),
-                       "ring_batches": len(st["ring"]),
+                       "frame_layout": layout,
+                       "ring_batches": ring_len,
                        "routes": len(st["routes"]), "parallelism": f"dp{world} (replicated FIB, sharded batches)",
                        "parity_sample_vs_oracle": parity,
                        "bins_total": int(bins.sum())},
@@ -426,6 +472,7 @@ def main():
                          "algorithmic_bytes_per_pkt": st["algo"]},
             "cpu_baseline": cpu,
             "host_memory_e2e": e2e,
+            "imix": imix,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

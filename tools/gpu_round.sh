@@ -30,7 +30,7 @@ if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
     step pytest_gpu 1200 python3 -m pytest tests -m gpu -q -p no:cacheprovider -x
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = sweep ]; then
-    step sweep_$CFG 600 python3 bench.py --config $CFG --sweep --steps 5 --warmup 2 --no-cpu-baseline --no-parity --no-e2e
+    step sweep_$CFG 600 python3 bench.py --config $CFG --sweep --steps 5 --warmup 2 --no-cpu-baseline --no-parity --no-e2e --no-imix
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
     step bench 600 python3 bench.py --config $CFG --steps 50 --warmup 5
@@ -38,10 +38,10 @@ if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
     step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_stats -o run \
-        -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-e2e
+        -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-e2e --no-imix
     step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run \
-        -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-parity --no-e2e
+        -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-parity --no-e2e --no-imix
     step prof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run \
-        -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-parity --no-e2e
+        -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-parity --no-e2e --no-imix
 fi
 echo done
