@@ -83,6 +83,20 @@ __device__ __forceinline__ uint32_t lpm4d(const uint32_t *__restrict__ d16,
     return e >> 1;
 }
 
+// Toeplitz nibble table access: 4 stream bytes b..b+3 held little-endian in x,
+// N[q][u] at tabn[q * 16 + u]; 16-entry rows make every wave lookup
+// bank-conflict free (lanes on one row hit <= 16 distinct banks)
+__device__ __forceinline__ uint32_t tz4n(const uint32_t *tabn, uint32_t b, uint32_t x)
+{
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t v = (x >> (8 * k)) & 0xffu;
+        h ^= tabn[(2 * (b + k)) * 16 + (v >> 4)] ^ tabn[(2 * (b + k) + 1) * 16 + (v & 15u)];
+    }
+    return h;
+}
+
 // Toeplitz byte table access: T[b][v] at tab[b * 256 + v]
 __device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_t x)
 {
@@ -147,6 +161,8 @@ struct KArgs {
 __device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
 #define TAB_POS 36  /* ... for the IPv6 L4 tuple */
+#define TABN_OFF (TAB_POS * 256) /* nibble tables N[q][u] (72 x 16) follow the byte tables */
+#define TAB_WORDS (TABN_OFF + 2 * TAB_POS * 16)
 
 // Bins (identical to oracle.c classify_one)
 template <int MODE>
@@ -1882,9 +1898,9 @@ __device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wst
     uint32_t h = 0;
     for (uint32_t k = 0; k < 8; k++)
         if (k < nw)
-            h ^= tz4(s_t, 4 * k, hw[k]);
+            h ^= tz4n(s_t, 4 * k, hw[k]);
     if (nw && hl4 != 0u)
-        h ^= tz4(s_t, 4 * nw, hl4);
+        h ^= tz4n(s_t, 4 * nw, hl4);
     uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
     if ((do4 || do6) && (pe == 3u || pe == 4u)) {
         nh = e >> 1;
@@ -1919,11 +1935,15 @@ __device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wst
     off.o2 = off.o3;
 }
 
+#define CS_THREADS 256
+#define CS_WAVES (CS_THREADS / 64)
 template <bool LNT>
-__global__ __launch_bounds__(CT_THREADS) void k_cnet_stream(KArgs a, uint64_t n_tiles)
+__global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_cnet_stream(KArgs a, uint64_t n_tiles)
 {
-    __shared__ uint32_t s_t[TAB_POS * 256];
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
+    // nibble Toeplitz tables (4.5 KiB) instead of the 36 KiB byte tables: ~21
+    // KiB of LDS per 4-wave block, so LDS no longer caps the waves per CU
+    __shared__ uint32_t s_t[2 * TAB_POS * 16];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CS_WAVES][256];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
     __shared__ uint32_t s_sf[64];
@@ -1931,20 +1951,20 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_stream(KArgs a, uint64_t n_
     const uint32_t tid = threadIdx.x;
     if (tid < 64)
         s_sf[tid] = 0;
-    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
-        s_t[k] = a.ttab[k];
-    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
+    for (uint32_t k = tid; k < 2 * TAB_POS * 16; k += CS_THREADS)
+        s_t[k] = a.ttab[TABN_OFF + k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += CS_THREADS)
         s_reta[k] = a.reta[k];
     const bool count = a.bins != nullptr;
     if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CS_THREADS)
             s_bins[k] = 0;
     __syncthreads();
 
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     u32x4 *tile = s_tile[wv];
-    const uint64_t wstep = (uint64_t)gridDim.x * CT_WAVES;
-    const uint64_t t0 = (uint64_t)blockIdx.x * CT_WAVES + wv;
+    const uint64_t wstep = (uint64_t)gridDim.x * CS_WAVES;
+    const uint64_t t0 = (uint64_t)blockIdx.x * CS_WAVES + wv;
     CsOff off{0, 0, 0, 0};
     if (a.offsets) {
 #pragma unroll
@@ -1970,7 +1990,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_stream(KArgs a, uint64_t n_
     if (count || a.spec_flags)
         __syncthreads();
     if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CS_THREADS)
             if (s_bins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
     if (a.spec_flags && tid < 64 && s_sf[tid])
@@ -2846,6 +2866,16 @@ static void build_ttab(const uint8_t *key, uint32_t *tab)
             tab[b * 256 + v] = h;
         }
     }
+    // N[q][u]: the 4 stream bits of nibble q (q = 2b high, 2b + 1 low nibble of
+    // byte b), so T[b][v] = N[2b][v >> 4] ^ N[2b + 1][v & 15]
+    for (uint32_t q = 0; q < 2 * TAB_POS; q++)
+        for (uint32_t u = 0; u < 16; u++) {
+            uint32_t h = 0;
+            for (uint32_t k = 0; k < 4; k++)
+                if (u & (0x8u >> k))
+                    h ^= key_window(key, 4 * q + k);
+            tab[TABN_OFF + q * 16 + u] = h;
+        }
 }
 
 static int set_device(int dev)
@@ -2888,7 +2918,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
         c->num_cu = prop.multiProcessorCount;
     if (c->num_cu <= 0)
         c->num_cu = 256;
-    if (hipMalloc((void **)&c->d_ttab, TAB_POS * 256 * 4) != hipSuccess ||
+    if (hipMalloc((void **)&c->d_ttab, TAB_WORDS * 4) != hipSuccess ||
         hipMalloc((void **)&c->d_reta, CNDP_RETA_MAX * 2) != hipSuccess) {
         cndp_gpu_fini(c);
         return -ENOMEM;
@@ -2963,12 +2993,12 @@ extern "C" int cndp_gpu_set_rss(cndp_gpu_ctx_t *c, const uint8_t *key, uint32_t 
             rt[i] = (uint16_t)(i % nb_queues);
     }
     memcpy(c->key, key ? key : ms_default_key, CNDP_RSS_KEY_LEN);
-    uint32_t *tab = (uint32_t *)malloc(TAB_POS * 256 * 4);
+    uint32_t *tab = (uint32_t *)malloc(TAB_WORDS * 4);
     if (!tab)
         return -ENOMEM;
     build_ttab(c->key, tab);
     int r = set_device(c->dev);
-    if (!r && (hipMemcpy(c->d_ttab, tab, TAB_POS * 256 * 4, hipMemcpyHostToDevice) != hipSuccess ||
+    if (!r && (hipMemcpy(c->d_ttab, tab, TAB_WORDS * 4, hipMemcpyHostToDevice) != hipSuccess ||
                hipMemcpy(c->d_reta, rt, reta_size * 2, hipMemcpyHostToDevice) != hipSuccess))
         r = -EIO;
     free(tab);
@@ -3417,13 +3447,14 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             a.wl = c->cs_wl + 1;
             HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
-            uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
-            if (gt > cap)
-                gt = cap;
+            uint64_t gt = (n_tiles + CS_WAVES - 1) / CS_WAVES;
+            const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 5u;
+            if (gt > (uint64_t)c->num_cu * bpc)
+                gt = (uint64_t)c->num_cu * bpc;
             if (c->tune_lnt)
-                hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+                hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a, n_tiles);
             else
-                hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
+                hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a, n_tiles);
             hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         } else if (c->tune_cnet_tile || B) {
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;

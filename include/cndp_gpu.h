@@ -202,7 +202,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           rewrite touches of rewritten frames, 1 = whole rewritten
  *                           frames, 2 = whole tiles holding a rewrite (default: full
  *                           coalesced lines beat partial-line writes on HBM)
- *   CNDP_TUNE_LOAD_NT       wave-tile kernels (tile 4): 1 = frame tiles loaded with the
+ *   CNDP_TUNE_LOAD_NT       wave-tile kernels (tile 4 / 5, cnet tile): 1 = frame tiles loaded with the
  *                           non-temporal hint, so the once-read stream neither allocates
  *                           in L2 / the Infinity Cache nor evicts the FIB directory from
  *                           them (default 1) */
