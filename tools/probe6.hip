@@ -63,7 +63,7 @@ struct Out {
     uint32_t *sink;
 };
 
-template <int POL, int LPOL, int STG, int PF>
+template <int POL, int LPOL, int STG, int PF, int ORD = 0>
 __global__ __launch_bounds__(256) void k_v(const uint8_t *slab, uint64_t n_tiles, Out o)
 {
     __shared__ __attribute__((aligned(16))) u32x4 s_tile[4][256];
@@ -73,9 +73,21 @@ __global__ __launch_bounds__(256) void k_v(const uint8_t *slab, uint64_t n_tiles
     u32x4 *tile = s_tile[wv];
     const uint32_t S = STG ? STG : 1;
     // wave's unit = S consecutive tiles; the block's 4 waves take 4 consecutive units
-    const uint64_t n_units = n_tiles / S;
-    const uint64_t ustep = (uint64_t)gridDim.x * 4;
+    uint64_t ustep = (uint64_t)gridDim.x * 4;
     uint64_t u = (uint64_t)blockIdx.x * 4 + wv;
+    uint64_t uend = n_tiles / (STG ? STG : 1);
+    if (ORD == 1) { // contiguous range per wave
+        const uint64_t nw = (uint64_t)gridDim.x * 4, per = (uend + nw - 1) / nw;
+        u = ((uint64_t)blockIdx.x * 4 + wv) * per;
+        uend = u + per < uend ? u + per : uend;
+        ustep = 1;
+    } else if (ORD == 2) { // contiguous range per block, its 4 waves interleaved
+        const uint64_t per = (uend + gridDim.x - 1) / gridDim.x;
+        u = (uint64_t)blockIdx.x * per + wv;
+        uend = (uint64_t)blockIdx.x * per + per < uend ? (uint64_t)blockIdx.x * per + per : uend;
+        ustep = 4;
+    }
+    const uint64_t n_units = uend;
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
     u32x4 r[PF][4];
     auto issue = [&](int slot, uint64_t tt) {
@@ -211,15 +223,12 @@ int main(int argc, char **argv)
         fflush(stdout);
     };
     char nm[96];
-#define RUN(POL, LPOL, STG, PF, BPC)                                                                   \
-    snprintf(nm, sizeof nm, "pol%d lpol%d stg%d pf%d bpc%d", POL, LPOL, STG, PF, BPC);                  \
-    for (int rot : {1, R}) for (int fl : {0, 1})                                                      \
-    timeit([&](int s) { hipLaunchKernelGGL((k_v<POL, LPOL, STG, PF>), dim3(cus * BPC), dim3(256), 0, 0, slab[s], tiles, o[s]); }, nm, rot, fl);
-    for (int rot : {1, R}) for (int fl : {0, 1})
-        timeit([&](int s) { hipLaunchKernelGGL(k_read, dim3(cus * 2), dim3(256), 0, 0, slab[s], tiles, o[s]); }, "read bpc2", rot, fl);
-    RUN(1, 0, 0, 1, 2) RUN(1, 0, 0, 1, 4)
-    RUN(0, 1, 0, 1, 2) RUN(0, 1, 0, 1, 4)
-    RUN(1, 1, 0, 1, 2) RUN(1, 1, 0, 1, 4)
-    RUN(1, 1, 8, 1, 2)
+#define RUN(POL, LPOL, STG, PF, BPC, ORD)                                                              \
+    snprintf(nm, sizeof nm, "pol%d lpol%d stg%d pf%d bpc%d ord%d", POL, LPOL, STG, PF, BPC, ORD);       \
+    timeit([&](int s) { hipLaunchKernelGGL((k_v<POL, LPOL, STG, PF, ORD>), dim3(cus * BPC), dim3(256), 0, 0, slab[s], tiles, o[s]); }, nm, R, 0);
+    RUN(1, 1, 0, 1, 2, 0) RUN(1, 1, 0, 1, 2, 1) RUN(1, 1, 0, 1, 2, 2)
+    RUN(1, 1, 0, 1, 3, 0) RUN(1, 1, 0, 1, 3, 1) RUN(1, 1, 0, 1, 3, 2)
+    RUN(1, 1, 0, 2, 2, 0) RUN(1, 1, 0, 2, 2, 1) RUN(1, 1, 0, 2, 1, 1)
+    RUN(1, 1, 8, 1, 2, 0) RUN(1, 1, 8, 1, 2, 1)
     return 0;
 }
