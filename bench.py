@@ -361,6 +361,8 @@ def main():
     ap.add_argument("--ring", type=int, default=0,
                     help="batches in the ring (0 = auto: >= 4 GiB of frames + results, at most 4)")
     ap.add_argument("--load-nt", type=int, default=None)
+    ap.add_argument("--cnet-tile", type=int, default=None)
+    ap.add_argument("--cnet-spec", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--dir16", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
@@ -379,7 +381,7 @@ def main():
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     stream = torch.cuda.current_stream(dev)
     cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16,
-                  load_nt=args.load_nt)
+                  load_nt=args.load_nt, cnet_tile=args.cnet_tile, cnet_spec=args.cnet_spec)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 
