@@ -13,7 +13,8 @@ from ctypes import (POINTER, Structure, Union, c_char_p, c_int, c_uint8, c_uint1
                     c_uint32, c_uint64, c_void_p)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libcndp_gpu.so")
+# CNDP_GPU_LIB: an alternative build of the same library (A/B timing experiments)
+LIB_PATH = os.environ.get("CNDP_GPU_LIB") or os.path.join(HERE, "lib", "libcndp_gpu.so")
 
 # cne_fib.h:34-38, :53-58, :60, :63-73 (+ CNE_FIB_LOOKUP_GPU)
 CNE_FIB_DUMMY, CNE_FIB_DIR24_8, CNE_FIB_TRIE = 0, 1, 2
