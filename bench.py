@@ -222,7 +222,8 @@ def sweep(st, stream, cfg):
         variants = [dict(cnet_tile=ct, dir16=d, cnet_spec=sp, load_nt=l) for sp in (256, 0) for ct in (2, 1, 0)
                     for d in (1, 0) for l in (1, 0) if (sp == 256 or d == 1) and (ct >= 1 or l == 1)]
     if "tx" in st:
-        variants = [dict(rw_wb=w, nt=nt, tile=4) for w in (0, 1, 2) for nt in (1, 0)] + [dict(tile=1, rw_wb=0)]
+        variants = [dict(rw_wb=w, nt=nt, tile=4, load_nt=l, blocks_per_cu=b) for w in (0, 1, 2) for nt in (1, 0)
+                    for l in (1, 0) for b in (2, 4)] + [dict(tile=1, rw_wb=0)]
     for v in variants:
         cl.set_tuning(**v)
         for k in range(3):

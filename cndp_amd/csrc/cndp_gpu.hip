@@ -3509,7 +3509,9 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         }
     } else {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
-        const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : c->tune_tile == 5 ? 2u : 4u;
+        // auto: 2 blocks per CU for the streamed kernel, 4 for the others
+        // (the fused rewrite runs the split-gather tile kernel)
+        const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : c->tune_tile == 5 && !rw_tx ? 2u : 4u;
         const uint32_t cap = (uint32_t)c->num_cu * bpc;
         if (g > cap)
             g = cap;
@@ -3561,8 +3563,12 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             const int mi = b->mode == CNDP_MODE_L3FWD ? 0 : 1, nti = c->tune_nt ? 1 : 0;
             tile_fn fn = sched == 2 && c->tune_lnt ? fns_lnt[mi][nti] : fns[mi][sched][nti];
             if (rw_tx && b->mode == CNDP_MODE_L3FWD && sched == 2 && b->n % 256u == 0 && c->d_rw_tbl) {
-                fn = c->tune_nt ? k_classify_tile<CNDP_MODE_L3FWD, 2, true, true>
-                                : k_classify_tile<CNDP_MODE_L3FWD, 2, false, true>;
+                static const tile_fn rfns[2][2] = {
+                    {k_classify_tile<CNDP_MODE_L3FWD, 2, false, true, false>,
+                     k_classify_tile<CNDP_MODE_L3FWD, 2, false, true, true>},
+                    {k_classify_tile<CNDP_MODE_L3FWD, 2, true, true, false>,
+                     k_classify_tile<CNDP_MODE_L3FWD, 2, true, true, true>}};
+                fn = rfns[c->tune_nt ? 1 : 0][c->tune_lnt ? 1 : 0];
                 a.rw_tbl = c->d_rw_tbl;
                 a.tx_edge = rw_tx;
                 a.rw_parts = c->tune_rw_wb == 1 ? 4u : c->tune_rw_wb == 2 ? 5u : c->rw_parts;
