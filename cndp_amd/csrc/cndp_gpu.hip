@@ -1390,7 +1390,12 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 // Frames that are not 16-B aligned or have < 64 bytes before the slab end
 // are staged with bounded byte loads (zero past the end), like Win.
 // ---------------------------------------------------------------------------
+#ifndef CT_THREADS // build-time overrides for A/B builds (tools/abbuild.sh)
 #define CT_THREADS 512
+#endif
+#ifndef CT_WPE
+#define CT_WPE 4 // waves per SIMD the cnet tile kernel is compiled for
+#endif
 #define CT_WAVES (CT_THREADS / 64)
 
 // frame base (bytes from slab) of packet i, or ~0 when i >= n
@@ -1408,7 +1413,7 @@ __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
 }
 
 template <bool LNT>
-__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_classify_cnet_tile(KArgs a, uint64_t n_tiles)
+__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(CT_WPE, CT_WPE))) void k_classify_cnet_tile(KArgs a, uint64_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
     __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];

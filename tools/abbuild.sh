@@ -1,0 +1,16 @@
+#!/bin/bash
+# A/B builds (diagnostic): tools/abbuild.sh <name> [-DMACRO=...]...
+# builds cndp_amd/lib/libcndp_gpu_<name>.so from the same sources with extra
+# defines; select it at run time with CNDP_GPU_LIB=<path>.
+set -e
+cd "$(dirname "$0")/.."
+name=$1
+shift
+obj=cndp_amd/build/ab_$name
+mkdir -p "$obj"
+gcc -O3 -fPIC -std=gnu11 -c cndp_amd/csrc/rib.c -o "$obj/rib.o"
+gcc -O3 -fPIC -std=gnu11 -c cndp_amd/csrc/fib.c -o "$obj/fib.o"
+/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -w "$@" -c cndp_amd/csrc/cndp_gpu.hip -o "$obj/cndp_gpu.o"
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--version-script=cndp_amd/csrc/exports.map \
+    -o "cndp_amd/lib/libcndp_gpu_$name.so" "$obj/rib.o" "$obj/fib.o" "$obj/cndp_gpu.o"
+echo "built cndp_amd/lib/libcndp_gpu_$name.so"
