@@ -1199,6 +1199,14 @@ __device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
 
 __device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) << 3) | cnet_edge(l); }
 
+// low bytes shared by types of different p_nxt (the others all go to pkt_drop)
+#define SPEC_LOWS 7
+__device__ __forceinline__ uint32_t spec_lowslot(uint32_t low)
+{
+    return low == 0x03u ? 0u : low == 0x11u ? 1u : low == 0x31u ? 2u : low == 0x91u ? 3u
+         : low == 0x41u ? 4u : low == 0xc1u ? 5u : low == 0xe1u ? 6u : SPEC_LOWS;
+}
+
 // Burst / chunk maps store their target states tagged with the target's
 // signature class (state | class << 16; SPEC_UNCH = keep the state), so map
 // composition never recomputes a signature.
@@ -2453,10 +2461,19 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
 // st + (j - c0) * spec_bstride(B) (16-B aligned groups for any B)
 __device__ __forceinline__ uint32_t spec_bstride(uint32_t B) { return (B + 3u) & ~3u; }
 
-template <int CH>
-__device__ __forceinline__ void spec_stage_chunk(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                 uint64_t c0, uint64_t c1, uint32_t lane, uint32_t *st)
+// em: bit 6 * spec_lowslot(low) + edge for every staged type (slots < SPEC_LOWS)
+__device__ __forceinline__ unsigned long long spec_em(uint32_t l, uint32_t e)
 {
+    const uint32_t q = spec_lowslot(l & 0xffu);
+    return q < SPEC_LOWS ? 1ull << (6 * q + e) : 0ull;
+}
+
+template <int CH>
+__device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *__restrict__ pt, uint32_t n,
+                                                               uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
+                                                               uint32_t *st)
+{
+    unsigned long long em = 0;
     const uint32_t bs = spec_bstride(B);
     if ((B & 7u) == 0) {
         // bursts are contiguous in LDS too (bs == B): 16-B loads of 8 types,
@@ -2482,17 +2499,16 @@ __device__ __forceinline__ void spec_stage_chunk(const uint16_t *__restrict__ pt
                     const uint32_t hi = idx + 2 * q + 1 < m ? pt[p0 + idx + 2 * q + 1] : 0u;
                     w[q] = lo | (hi << 16);
                 }
-            u32x4 o0, o1;
-            o0.x = (w[0] & 0xffffu) | (cnet_edge(w[0]) << 16);
-            o0.y = (w[0] >> 16) | (cnet_edge(w[0] >> 16) << 16);
-            o0.z = (w[1] & 0xffffu) | (cnet_edge(w[1]) << 16);
-            o0.w = (w[1] >> 16) | (cnet_edge(w[1] >> 16) << 16);
-            o1.x = (w[2] & 0xffffu) | (cnet_edge(w[2]) << 16);
-            o1.y = (w[2] >> 16) | (cnet_edge(w[2] >> 16) << 16);
-            o1.z = (w[3] & 0xffffu) | (cnet_edge(w[3]) << 16);
-            o1.w = (w[3] >> 16) | (cnet_edge(w[3] >> 16) << 16);
-            *(u32x4 *)(st + idx) = o0;
-            *(u32x4 *)(st + idx + 4) = o1;
+            uint32_t o[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t l = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu, e = cnet_edge(l);
+                o[q] = l | (e << 16);
+                if (idx + q < m)
+                    em |= spec_em(l, e);
+            }
+            *(u32x4 *)(st + idx) = (u32x4){o[0], o[1], o[2], o[3]};
+            *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
         }
     } else {
         for (uint64_t j = c0; j < c1; j++) {
@@ -2500,12 +2516,14 @@ __device__ __forceinline__ void spec_stage_chunk(const uint16_t *__restrict__ pt
             const uint32_t cnt = (uint32_t)((uint64_t)n - p0 < B ? (uint64_t)n - p0 : B);
             uint32_t *d = st + (j - c0) * bs;
             for (uint32_t k = lane; k < cnt; k += 64) {
-                const uint32_t l = pt[p0 + k];
-                d[k] = l | (cnet_edge(l) << 16);
+                const uint32_t l = pt[p0 + k], e = cnet_edge(l);
+                d[k] = l | (e << 16);
+                em |= spec_em(l, e);
             }
         }
     }
     __builtin_amdgcn_wave_barrier();
+    return em;
 }
 
 template <int CH>
@@ -2521,7 +2539,7 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-    spec_stage_chunk<CH>(pt, n, B, c0, c1, lane, st);
+    unsigned long long em = spec_stage_chunk<CH>(pt, n, B, c0, c1, lane, st);
     const uint32_t sig = lane < K ? meta[1 + lane] : 0u;
     uint32_t cm = SPEC_UNCH;
     for (uint64_t bb = c0; bb < c1; bb++) {
@@ -2549,12 +2567,31 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
     }
     if (lane < K)
         T[c * SPEC_KMAX + lane] = cm;
+    // edge-consistency summary for k_spec_cemit.  Only the low bytes in
+    // spec_lowslot() carry types of different p_nxt (ptype.c:32-46; every
+    // other type goes to pkt_drop), so per slot the chunk records which
+    // edges its frames have.  A chunk where each slot has at most one edge
+    // cannot re-route a frame unless the entering state disagrees with it.
+    for (int o = 32; o > 0; o >>= 1)
+        em |= __shfl_xor(em, o);
+    uint32_t sm = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < SPEC_LOWS; r++) {
+        const uint32_t v = (uint32_t)(em >> (6 * r)) & 0x3fu;
+        // slot r: bit 3 = present, bits 0..2 = its edge; bit 31 = two edges
+        if (v & (v - 1u))
+            sm |= 1u << 31;
+        else if (v)
+            sm |= (8u | (31u - (uint32_t)__clz(v))) << (4 * r);
+    }
+    if (lane == 0)
+        T[nch * SPEC_KMAX + c] = sm;
 }
 
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_t nb, uint64_t nch,
                                                     const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
-                                                    const uint32_t *Sblk, const uint32_t *S)
+                                                    const uint32_t *Sblk, const uint32_t *S, const uint32_t *T)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -2569,6 +2606,12 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
     } else { // chunk start state: the block's start, then the block's earlier chunks
         const uint64_t blk = c / SPEC_BLK;
         s0 = c % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (c - 1) * SPEC_KFAST, class_id, Sblk[blk]);
+    }
+    if (meta[0] <= SPEC_KMAX) { // k_spec_ctables wrote the chunk's summary
+        const uint32_t sm = T[nch * SPEC_KMAX + c], q0 = spec_lowslot(s0 & 0xffu);
+        const uint32_t slot = q0 < SPEC_LOWS ? (sm >> (4 * q0)) & 0xfu : 0u;
+        if (!(sm >> 31) && (!(slot & 8u) || (slot & 7u) == cnet_edge(s0)))
+            return; // no frame of this chunk can leave by another edge
     }
     spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st);
     for (uint64_t bb = c0; bb < c1; bb++) {
@@ -3495,7 +3538,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                    (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S);
                 hipLaunchKernelGGL(ce, dim3(gc), dim3(256), 0, s, a, B, nb, nch, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
-                                   (const uint32_t *)c->sp_S);
+                                   (const uint32_t *)c->sp_S, (const uint32_t *)c->sp_T);
             } else {
                 hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
