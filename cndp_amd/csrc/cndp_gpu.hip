@@ -1473,6 +1473,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(CT_W
             r[k] = t < n_tiles ? ldg4<LNT>(src) : (u32x4){0, 0, 0, 0};
         }
     }
+    uint32_t last_sig = 0xFFFFFFFFu; // this lane's last signature marked in s_sf
     for (; t < n_tiles; t += wstep) {
         const uint64_t i = t * 64u + lane;
         // (1) stage the tile: fast frames from the loads, others bounded
@@ -1695,7 +1696,10 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(CT_W
                 a.spec_nh[i] = e >> 1;
             if (live)
                 a.spec_t16[i] = (uint16_t)pt;
-            spec_mark(s_sf, live, spec_sig(pt & 0xffffu));
+            // the block's bitmap only grows: a lane re-marks only a new signature
+            const uint32_t sg = spec_sig(pt & 0xffffu);
+            spec_mark(s_sf, live && sg != last_sig, sg);
+            last_sig = live ? sg : last_sig;
         }
         __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
         if (live) {
