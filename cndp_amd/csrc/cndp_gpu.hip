@@ -156,7 +156,9 @@ struct KArgs {
     uint32_t rw_parts; // 16-B parts of each rewritten frame written back
 };
 
+#ifndef FAST_THREADS // build-time override for A/B builds (tools/abbuild.sh)
 #define FAST_THREADS 256
+#endif
 // a packet ip4_lookup hands to ip4_rewrite (edge 0, ip4_lookup.c:150)
 __device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
