@@ -2017,6 +2017,274 @@ __global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5
 }
 
 // ---------------------------------------------------------------------------
+// Deferred-chain cnet kernel (CNDP_TUNE_CNET_TILE 3, the default): k_cnet_stream's fast
+// path (worklist for the rest) in two stages one loop trip apart.
+//   A  tile c    stage, parse, Toeplitz, first FIB gather
+//   B  tile c-1  the rest of its FIB chain, then its results
+// A trip issues B's chain -> A's first gather -> offsets of c+3 -> windows of
+// c+2 -> B's stores.  B's chain waits only behind loads issued a trip
+// earlier, never behind the window loads of the same trip.
+// ---------------------------------------------------------------------------
+struct CdLane {
+    uint32_t ptf;  // pt (16) | do4 << 16 | do6 << 17 | fast << 18
+    uint32_t h, e, rx;
+    uint32_t d0, d1, d2, d3; // v6 destination words, or dip in d0 (v4)
+};
+
+template <bool LNT, int P>
+__device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t wstep, uint64_t n_tiles,
+                                        uint64_t nt_w, uint64_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
+                                        CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
+                                        uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig)
+{
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    const uint64_t t = t0 + jt * wstep;
+    // B: tile c-1 -- the rest of its chain (v4: page / tbl8, v6: tbl8 levels, trie.h:127-134)
+    const bool bv = jt >= 1 && jt - 1 < nt_w;
+    const uint64_t ib = (t - wstep) * 64u + lane;
+    uint32_t eb = sb.e;
+    {
+        const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
+        uint32_t j = d6 ? 3u : (a.dir16 ? 1u : 2u);
+        bool more = bv && (d4 || d6) && (eb & 1u);
+        while (__any(more)) {
+            if (more) {
+                uint32_t byte;
+                const uint32_t *tb;
+                if (d6) {
+                    const uint32_t wd = j < 4 ? sb.d0 : j < 8 ? sb.d1 : j < 12 ? sb.d2 : sb.d3;
+                    byte = (wd >> ((j & 3u) * 8)) & 0xffu;
+                    tb = a.tbl8_6;
+                } else {
+                    byte = j == 1 ? (sb.d0 >> 8) & 0xffu : sb.d0 & 0xffu;
+                    tb = j == 1 ? a.pages : a.tbl8;
+                }
+                eb = tb[(eb >> 1) * 256u + byte];
+                j++;
+                more = (eb & 1u) && (d6 ? j < 16 : j <= 2);
+            }
+        }
+    }
+    // A: tile c
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t f = 16u * k + fr_in_k;
+        tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t i = t * 64u + lane;
+    const bool live = jt < nt_w && i < a.n;
+    const uint64_t base = live ? ct_base(a, i, off.o0) : ~0ull;
+    const uint32_t sw = (lane >> 2) & 3u;
+    uint32_t W[16];
+    {
+        const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
+        W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
+        W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
+        W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
+        W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t et = W[3] & 0xffffu;
+    const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
+    const bool l4p4 = p4 == 6u || p4 == 17u || p4 == 132u, l4p6 = p6 == 6u || p6 == 17u || p6 == 132u;
+    const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
+                    ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
+    const bool f6 = et == BE16C(0x86DDu) && l4p6;
+    const bool fast = live && ct_fast(a, base) && (f4 || f6);
+    {
+        const bool slow = live && !fast;
+        const unsigned long long m = __ballot(slow);
+        if (m) {
+            uint32_t w0 = 0;
+            if (lane == (uint32_t)(__ffsll(m) - 1))
+                w0 = atomicAdd(a.wl_n, (uint32_t)__popcll(m));
+            w0 = __shfl(w0, __ffsll(m) - 1);
+            if (slow)
+                a.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+        }
+    }
+    CdLane na;
+    na.ptf = 0;
+    na.h = 0;
+    na.rx = 0;
+    na.d0 = na.d1 = na.d2 = na.d3 = 0;
+    uint32_t idx0 = 0;
+    const uint32_t *tb0 = a.tbl24_6;
+    if (fast) {
+        const uint32_t proto = f4 ? p4 : p6;
+        uint32_t pt = (f4 ? 0x11u : 0x41u) | pt_l4(proto);
+        if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
+            const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
+            pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
+        }
+        const uint32_t pe = cnet_edge(pt);
+        const bool l4ok = proto == 6u || proto == 17u;
+        Lens lens{14u, f4 ? 20u : 40u, 0u};
+        if (a.rxmeta) { // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
+            lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
+                    : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
+                         : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
+            na.rx = rx_meta(lens, W[0], W[1], et);
+        }
+        uint32_t flags = 0;
+        if (f4) {
+            const uint32_t dst = alignb(W[8], W[7], 2);
+            na.h = tz4(s_t, 0, alignb(W[7], W[6], 2)) ^ tz4(s_t, 4, dst);
+            if (l4ok)
+                na.h ^= tz4(s_t, 8, alignb(W[9], W[8], 2));
+            if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
+                uint32_t sum = 0;
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
+                    sum += (x & 0xffffu) + (x >> 16);
+                }
+                sum = (sum >> 16) + (sum & 0xffffu);
+                sum = (sum >> 16) + (sum & 0xffffu);
+                const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
+                na.d0 = ok ? bswap32(dst) : 0u;
+                flags = 1u << 16;
+                tb0 = a.dir16 ? a.dir16 : a.tbl24;
+                idx0 = a.dir16 ? na.d0 >> 16 : na.d0 >> 8;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                na.h ^= tz4(s_t, 4 * k, alignb(W[6 + k], W[5 + k], 2));
+            if (l4ok)
+                na.h ^= tz4(s_t, 32, alignb(W[14], W[13], 2));
+            if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
+                if (bswap16(W[4] >> 16) < a.buf_len) {
+                    na.d0 = alignb(W[10], W[9], 2);
+                    na.d1 = alignb(W[11], W[10], 2);
+                    na.d2 = alignb(W[12], W[11], 2);
+                    na.d3 = alignb(W[13], W[12], 2);
+                }
+                flags = 1u << 17;
+                idx0 = ((na.d0 & 0xffu) << 16) | (na.d0 & 0xff00u) | ((na.d0 >> 16) & 0xffu); // trie.h:126
+            }
+        }
+        na.ptf = pt | flags | (1u << 18);
+    }
+    na.e = tb0[idx0]; // first gather, unconditional
+    // offsets one tile further, then the windows of tile c+2
+    {
+        const uint64_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
+        off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
+        cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
+    }
+    // B's results
+    {
+        const uint32_t pt = sb.ptf & 0xffffu, pe = cnet_edge(pt);
+        const bool bf = bv && (sb.ptf & (1u << 18));
+        const bool din = (sb.ptf & (3u << 16)) != 0u;
+        uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
+        if (din && (pe == 3u || pe == 4u)) {
+            nh = eb >> 1;
+            edge = nh >> 24;
+        }
+        if (a.spec_nh) {
+            if (bf && din && (!a.nh || (pe != 3u && pe != 4u)))
+                a.spec_nh[ib] = eb >> 1;
+            if (bf)
+                a.spec_t16[ib] = (uint16_t)pt;
+            const uint32_t sg = spec_sig(pt);
+            spec_mark(s_sf, bf && sg != last_sig, sg);
+            last_sig = bf ? sg : last_sig;
+        }
+        if (bf) {
+            const uint32_t q = s_reta[sb.h & a.reta_mask];
+            if (a.ptype)
+                a.ptype[ib] = pt;
+            if (a.rxmeta)
+                a.rxmeta[ib] = sb.rx;
+            if (a.nh)
+                a.nh[ib] = nh;
+            if (a.hash)
+                a.hash[ib] = sb.h;
+            if (a.queue)
+                a.queue[ib] = (uint16_t)q;
+            if (a.edge)
+                a.edge[ib] = (uint8_t)edge;
+            if (count)
+                atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
+        }
+    }
+    sb = na;
+    off.o0 = off.o1;
+    off.o1 = off.o2;
+    off.o2 = off.o3;
+}
+
+template <bool LNT>
+__global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint64_t n_tiles)
+{
+    __shared__ uint32_t s_t[TAB_POS * 256];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ uint32_t s_sf[64];
+
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64)
+        s_sf[tid] = 0;
+    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
+
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint64_t wstep = (uint64_t)gridDim.x * CT_WAVES;
+    const uint64_t t0 = (uint64_t)blockIdx.x * CT_WAVES + wv;
+    const uint64_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
+    CsOff off{0, 0, 0, 0};
+    if (a.offsets) {
+#pragma unroll
+        for (uint32_t s = 0; s < 3; s++) {
+            const uint64_t ts = t0 + s * wstep, is = ts * 64u + lane;
+            const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
+            if (s == 0)
+                off.o0 = o;
+            else if (s == 1)
+                off.o1 = o;
+            else
+                off.o2 = o;
+        }
+    }
+    u32x4 r[2][4];
+    cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
+    cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
+    CdLane sb;
+    sb.ptf = sb.h = sb.e = sb.rx = 0;
+    sb.d0 = sb.d1 = sb.d2 = sb.d3 = 0;
+    uint32_t last_sig = 0xFFFFFFFFu;
+    const uint64_t trips = nt_w ? nt_w + 1 : 0;
+    for (uint64_t jt = 0; jt < trips; jt += 2) {
+        cd_trip<LNT, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
+                        last_sig);
+        if (jt + 1 < trips)
+            cd_trip<LNT, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
+                            count, last_sig);
+    }
+    if (count || a.spec_flags)
+        __syncthreads();
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    if (a.spec_flags && tid < 64 && s_sf[tid])
+        atomicOr(&a.spec_flags[tid], s_sf[tid]);
+}
+
+// ---------------------------------------------------------------------------
 // cnet ptype-node speculation (ptype.c:48-210) as a post-pass over the
 // per-packet ptypes the classify kernel wrote.  In each graph burst of B
 // packets the node walks 4-packet groups against its state last_type: a
@@ -2962,7 +3230,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_bpc = 0; // auto: 2 for the streamed tile kernel, 4 otherwise
     c->tune_tile = 5;
     c->tune_dir16 = 1;
-    c->tune_cnet_tile = 1;
+    c->tune_cnet_tile = 3;
     c->tune_lnt = 1;
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
@@ -3486,7 +3754,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             a.spec_flags = c->sp_small + 66;
             HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
         }
-        if (c->tune_cnet_tile == 2) {
+        if (c->tune_cnet_tile == 2 || c->tune_cnet_tile == 3) {
             // fast kernel, then the general parse of the frames it left
             if ((uint64_t)b->n + 1 > c->cs_wl_cap) {
                 if (c->cs_wl)
@@ -3501,14 +3769,26 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             a.wl = c->cs_wl + 1;
             HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
-            uint64_t gt = (n_tiles + CS_WAVES - 1) / CS_WAVES;
-            const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 5u;
-            if (gt > (uint64_t)c->num_cu * bpc)
-                gt = (uint64_t)c->num_cu * bpc;
-            if (c->tune_lnt)
-                hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a, n_tiles);
-            else
-                hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a, n_tiles);
+            if (c->tune_cnet_tile == 3) {
+                uint64_t gd = (n_tiles + CT_WAVES - 1) / CT_WAVES;
+                const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 2u;
+                if (gd > (uint64_t)c->num_cu * bpc)
+                    gd = (uint64_t)c->num_cu * bpc;
+                if (c->tune_lnt)
+                    hipLaunchKernelGGL(k_cnet_defer<true>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, n_tiles);
+                else
+                    hipLaunchKernelGGL(k_cnet_defer<false>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, n_tiles);
+            } else {
+                uint64_t gt = (n_tiles + CS_WAVES - 1) / CS_WAVES;
+                const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 5u;
+                if (gt > (uint64_t)c->num_cu * bpc)
+                    gt = (uint64_t)c->num_cu * bpc;
+                if (c->tune_lnt)
+                    hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a, n_tiles);
+                else
+                    hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a,
+                                       n_tiles);
+            }
             hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         } else if (c->tune_cnet_tile || B) {
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
@@ -4315,7 +4595,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_dir16 = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_CNET_TILE:
-        if (value < 0 || value > 2)
+        if (value < 0 || value > 3)
             return -EINVAL;
         c->tune_cnet_tile = value;
         return 0;

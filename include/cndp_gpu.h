@@ -186,11 +186,12 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           loop trip apart (default 5)
  *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
  *                           kept in front of tbl24 (default 1)
- *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = wave-tile staging with the next tile's
- *                           loads overlapping the FIB gathers (default), 2 = streamed
- *                           wave-tile fast path (two window tiles in flight) + general
- *                           per-lane parse of the frames it leaves (8-9% slower on C4),
- *                           0 = per-lane rows
+ *   CNDP_TUNE_CNET_TILE     cnet kernel: 3 = deferred-chain wave tile (fast path, the FIB
+ *                           chain of each tile finished one loop trip later, two window
+ *                           tiles in flight) + general per-lane parse of the frames it
+ *                           leaves (default), 2 = streamed fast path + the same general
+ *                           parse, 1 = wave-tile staging with the next tile's loads
+ *                           overlapping the FIB gathers, full parse inline, 0 = per-lane rows
  *   CNDP_TUNE_HOST_CHUNK    packets per pipelined chunk of cndp_gpu_classify_host
  *                           (>= 1024, default 1M)
  *   CNDP_TUNE_CNET_SPEC     cnet: graph burst size B of the ptype node's speculative

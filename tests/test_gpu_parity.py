@@ -17,7 +17,7 @@ from helpers import (CNET_DEF, L3FWD_DEF, assert_same, cnet_fibs, l3fwd_fib, l3f
                      oracle_classify)
 
 pytestmark = pytest.mark.gpu
-CNET_KERNELS = (0, 2, 1)  # per-lane rows, streamed fast path + worklist, wave tile (default, set last)
+CNET_KERNELS = (0, 1, 2, 3)  # per-lane rows, wave tile, streamed + worklist, deferred chain + worklist (default, set last)
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
@@ -145,7 +145,7 @@ def test_cnet_fuzz_parity(cnet, gpu):
         for ct in CNET_KERNELS:
             cl.set_tuning(cnet_tile=ct)
             assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
-    cl.set_tuning(cnet_tile=1)
+    cl.set_tuning(cnet_tile=3)
 
 
 def test_cnet_c5_checksum_verify(cnet, gpu):
@@ -574,7 +574,7 @@ def test_cnet_ptype_and_rxmeta(cnet, l3, gpu):
             ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
             torch.cuda.synchronize()
             assert_same(out, ref, keys=keys)
-    ccl.set_tuning(cnet_tile=1)
+    ccl.set_tuning(cnet_tile=3)
     fr = pktgen.fuzz_frames(64 * 300, seed=13, slot=64, device=gpu)
     ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
     for tile in (0, 3, 4, 5):
