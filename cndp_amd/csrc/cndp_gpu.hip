@@ -2467,11 +2467,17 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint16_t *__restrict_
         T[b * SPEC_KMAX + lane] = spec_tag(c, class_id);
 }
 
-// Burst maps are composed with a two-level LDS scan when at most
-// SPEC_KFAST signatures occur (a map is then SPEC_KFAST registers); the
-// composition "E then L" sends a class k through E, then through L.
+// Burst maps are composed with a two-level LDS scan, a map being
+// SPEC_KFAST registers when at most that many signatures occur and
+// SPEC_KMAX otherwise; the composition "E then L" sends a class k through E,
+// then through L.
 #define SPEC_KFAST 8
 #define SPEC_BLK 256
+
+// the map width of the scans for K signature classes (kfast = SPEC_KFAST, or
+// 0 to force the wide maps; kmax = SPEC_KMAX, or 0 to force the sequential
+// walk -- CNDP_TUNE_SPEC_SCAN)
+__device__ __forceinline__ uint32_t spec_kf(uint32_t K, uint32_t kfast) { return K <= kfast ? SPEC_KFAST : SPEC_KMAX; }
 
 // the 2 KiB class table into LDS with one 16-B load per thread (threads >= 128 idle)
 __device__ __forceinline__ void spec_cls_stage(uint8_t *s_cls, const uint8_t *class_id, uint32_t tid, uint32_t nthr)
@@ -2495,121 +2501,151 @@ __device__ __forceinline__ uint32_t spec_apply_t(const uint32_t *m, uint32_t st)
 }
 
 // per block of SPEC_BLK bursts or chunks: inclusive scan of their maps (P),
-// and the block's total map (Bt)
-__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint32_t *T,
-                                                        uint32_t *P, uint32_t *Bt)
+// and the block's total map (Bt).  KF = the map width: SPEC_KFAST when at
+// most that many signatures occur, else SPEC_KMAX (P and Bt rows are KF
+// words; s_m rows KF + 1, so a row store by 64 lanes hits 64 banks).
+template <uint32_t KF>
+__device__ __forceinline__ void spec_scan_a_body(uint32_t *s_m, uint64_t nb, uint32_t K, const uint32_t *T,
+                                                 uint32_t *P, uint32_t *Bt)
 {
-    __shared__ uint32_t s_m[SPEC_BLK][SPEC_KFAST + 1];
-    const uint32_t K = meta[0];
-    if (K > SPEC_KFAST)
-        return;
-    const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + threadIdx.x;
-    uint32_t m[SPEC_KFAST];
+    const uint32_t t = threadIdx.x;
+    const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + t;
+    uint32_t *row = s_m + t * (KF + 1);
+    uint32_t m[KF];
 #pragma unroll
-    for (uint32_t k = 0; k < SPEC_KFAST; k++)
+    for (uint32_t k = 0; k < KF; k++)
         m[k] = b < nb && k < K ? T[b * SPEC_KMAX + k] : SPEC_UNCH;
     for (uint32_t d = 1; d < SPEC_BLK; d <<= 1) {
 #pragma unroll
-        for (uint32_t k = 0; k < SPEC_KFAST; k++)
-            s_m[threadIdx.x][k] = m[k];
+        for (uint32_t k = 0; k < KF; k++)
+            row[k] = m[k];
         __syncthreads();
-        if (threadIdx.x >= d) {
-            const uint32_t *e = s_m[threadIdx.x - d]; // earlier map, then ours
-            const uint32_t *l = s_m[threadIdx.x];
+        if (t >= d) {
+            const uint32_t *e = row - d * (KF + 1); // earlier map, then ours
 #pragma unroll
-            for (uint32_t k = 0; k < SPEC_KFAST; k++) {
+            for (uint32_t k = 0; k < KF; k++) {
                 const uint32_t ek = e[k];
-                m[k] = k >= K ? SPEC_UNCH : ek == SPEC_UNCH ? l[k] : spec_apply_t(l, ek);
+                m[k] = k >= K ? SPEC_UNCH : ek == SPEC_UNCH ? row[k] : spec_apply_t(row, ek);
             }
         }
         __syncthreads();
     }
-    if (b < nb)
-        for (uint32_t k = 0; k < K; k++)
-            P[b * SPEC_KFAST + k] = m[k];
-    if (threadIdx.x == SPEC_BLK - 1)
-        for (uint32_t k = 0; k < K; k++)
-            Bt[(uint64_t)blockIdx.x * SPEC_KFAST + k] = m[k];
+#pragma unroll
+    for (uint32_t k = 0; k < KF; k++) { // unrolled: m stays in registers
+        if (b < nb && k < K)
+            P[b * KF + k] = m[k];
+        if (t == SPEC_BLK - 1 && k < K)
+            Bt[(uint64_t)blockIdx.x * KF + k] = m[k];
+    }
 }
 
-// block start states: Hillis-Steele over the block totals, 1024 at a time
-// with the composed map of the earlier windows carried along, and the final
-// state.  With more than SPEC_KFAST signatures: one thread walks the bursts
-// sequentially instead (S = the state entering every burst).
-__global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
-                                                     const uint32_t *Bt, uint32_t *Sblk, uint32_t *state,
-                                                     const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, uint32_t *S)
+__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint32_t *T,
+                                                        uint32_t *P, uint32_t *Bt, uint32_t kfast)
 {
-    __shared__ uint32_t s_m[1024][SPEC_KFAST + 1];
-    __shared__ uint32_t s_carry[SPEC_KFAST];
-    const uint32_t K = meta[0], t = threadIdx.x;
-    if (K > SPEC_KFAST) {
-        if (t == 0) {
-            uint32_t st = *state & 0xffffu;
-            for (uint64_t b = 0; b < nb; b++) {
-                S[b] = st;
-                const uint64_t b0 = b * B;
-                const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
-                const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
-                if (c != SPEC_UNCH)
-                    st = c;
-            }
-            *state = st;
-        }
-        return;
-    }
-    if (t < SPEC_KFAST)
+    __shared__ uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
+    const uint32_t K = meta[0];
+    if (K <= kfast)
+        spec_scan_a_body<SPEC_KFAST>(s_m, nb, K, T, P, Bt);
+    else if (K <= SPEC_KMAX)
+        spec_scan_a_body<SPEC_KMAX>(s_m, nb, K, T, P, Bt);
+}
+
+// block start states: Hillis-Steele over the block totals, W at a time with
+// the composed map of the earlier windows carried along, and the final
+// state (threads >= W only keep the barriers)
+template <uint32_t KF, uint32_t W>
+__device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carry, uint64_t nblk, uint32_t K,
+                                                 const uint8_t *class_id, const uint32_t *Bt, uint32_t *Sblk,
+                                                 uint32_t *state)
+{
+    const uint32_t t = threadIdx.x;
+    const bool act = t < W;
+    uint32_t *row = s_m + t * (KF + 1);
+    if (t < KF)
         s_carry[t] = SPEC_UNCH;
     const uint32_t s0 = spec_tag(*state & 0xffffu, class_id);
     __syncthreads();
-    for (uint64_t w0 = 0; w0 < nblk; w0 += 1024) {
+    for (uint64_t w0 = 0; w0 < nblk; w0 += W) {
         const uint64_t k0 = w0 + t;
-        uint32_t m[SPEC_KFAST];
+        uint32_t m[KF];
 #pragma unroll
-        for (uint32_t k = 0; k < SPEC_KFAST; k++)
-            m[k] = k0 < nblk && k < K ? Bt[k0 * SPEC_KFAST + k] : SPEC_UNCH;
-        const uint32_t dmax = nblk - w0 < 1024 ? (uint32_t)(nblk - w0) : 1024u;
+        for (uint32_t k = 0; k < KF; k++)
+            m[k] = act && k0 < nblk && k < K ? Bt[k0 * KF + k] : SPEC_UNCH;
+        const uint32_t dmax = nblk - w0 < W ? (uint32_t)(nblk - w0) : W;
         for (uint32_t d = 1; d < dmax; d <<= 1) {
+            if (act)
 #pragma unroll
-            for (uint32_t k = 0; k < SPEC_KFAST; k++)
-                s_m[t][k] = m[k];
+                for (uint32_t k = 0; k < KF; k++)
+                    row[k] = m[k];
             __syncthreads();
-            if (t >= d) {
-                const uint32_t *e = s_m[t - d], *l = s_m[t];
+            if (act && t >= d) {
+                const uint32_t *e = row - d * (KF + 1);
 #pragma unroll
-                for (uint32_t k = 0; k < SPEC_KFAST; k++) {
+                for (uint32_t k = 0; k < KF; k++) {
                     const uint32_t ek = e[k];
-                    m[k] = k >= K ? SPEC_UNCH : ek == SPEC_UNCH ? l[k] : spec_apply_t(l, ek);
+                    m[k] = k >= K ? SPEC_UNCH : ek == SPEC_UNCH ? row[k] : spec_apply_t(row, ek);
                 }
             }
             __syncthreads();
         }
+        if (act)
 #pragma unroll
-        for (uint32_t k = 0; k < SPEC_KFAST; k++)
-            s_m[t][k] = m[k];
+            for (uint32_t k = 0; k < KF; k++)
+                row[k] = m[k];
         __syncthreads();
         // state entering block k0: the carry, then this window's blocks before k0
-        uint32_t st = spec_apply_t(s_carry, s0);
-        if (t > 0)
-            st = spec_apply_t(s_m[t - 1], st);
-        if (k0 < nblk)
-            Sblk[k0] = st & 0xffffu;
+        if (act) {
+            uint32_t st = spec_apply_t(s_carry, s0);
+            if (t > 0)
+                st = spec_apply_t(row - (KF + 1), st);
+            if (k0 < nblk)
+                Sblk[k0] = st & 0xffffu;
+        }
         __syncthreads();
         if (t == 0) { // carry = carry then this window's total
-            const uint32_t *tot = s_m[dmax - 1];
-            uint32_t nc[SPEC_KFAST];
-            for (uint32_t k = 0; k < SPEC_KFAST; k++) {
+            const uint32_t *tot = s_m + (dmax - 1) * (KF + 1);
+            uint32_t nc[KF];
+            for (uint32_t k = 0; k < KF; k++) {
                 const uint32_t ck = s_carry[k];
                 nc[k] = k >= K ? SPEC_UNCH : ck == SPEC_UNCH ? tot[k] : spec_apply_t(tot, ck);
             }
-            for (uint32_t k = 0; k < SPEC_KFAST; k++)
+            for (uint32_t k = 0; k < KF; k++)
                 s_carry[k] = nc[k];
         }
         __syncthreads();
     }
     if (t == 0)
         *state = spec_apply_t(s_carry, s0) & 0xffffu;
+}
+
+// With more than SPEC_KMAX signatures (the parser's ptypes give fewer; a
+// guard, not a path): one thread walks the bursts sequentially instead
+// (S = the state entering every burst).
+__global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
+                                                     const uint32_t *Bt, uint32_t *Sblk, uint32_t *state,
+                                                     const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                     uint64_t nb, uint32_t *S, uint32_t kfast, uint32_t kmax)
+{
+    __shared__ uint32_t s_m[1024 * (SPEC_KFAST + 1) > 256 * (SPEC_KMAX + 1) ? 1024 * (SPEC_KFAST + 1)
+                                                                             : 256 * (SPEC_KMAX + 1)];
+    __shared__ uint32_t s_carry[SPEC_KMAX];
+    const uint32_t K = meta[0];
+    if (K <= kfast) {
+        spec_scan_c_body<SPEC_KFAST, 1024>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+    } else if (K <= kmax) {
+        spec_scan_c_body<SPEC_KMAX, 256>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+    } else if (threadIdx.x == 0) {
+        uint32_t st = *state & 0xffffu;
+        for (uint64_t b = 0; b < nb; b++) {
+            S[b] = st;
+            const uint64_t b0 = b * B;
+            const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B);
+            const uint32_t c = spec_burst_map(pt, b0, cnt, spec_sig(st), false);
+            if (c != SPEC_UNCH)
+                st = c;
+        }
+        *state = st;
+    }
 }
 
 __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
@@ -2633,7 +2669,7 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
 // one wave per burst: start state from the scan, types staged through LDS;
 // every lane walks the groups (uniform, broadcast LDS reads) and remembers
 // the state at the groups it owns (g % 64 == lane), then fixes those groups
-__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, uint32_t kseq,
+__global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t nb, uint32_t kfast, uint32_t kmax,
                                                    const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
                                                    const uint32_t *Sblk, const uint32_t *S)
 {
@@ -2647,11 +2683,11 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
     const uint64_t b0 = b * B;
     const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
     uint32_t s0;
-    if (meta[0] > kseq) {
+    if (meta[0] > kmax) {
         s0 = S[b];
     } else { // block start state through the block's earlier bursts (exclusive prefix)
         const uint64_t blk = b / SPEC_BLK;
-        s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * SPEC_KFAST, class_id, Sblk[blk]);
+        s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * spec_kf(meta[0], kfast), class_id, Sblk[blk]);
     }
     uint32_t low = s0 & 0xffu, E = cnet_edge(s0);
     uint8_t *sq = s_q[wv];
@@ -2865,7 +2901,8 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_t nb, uint64_t nch,
                                                     const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
-                                                    const uint32_t *Sblk, const uint32_t *S, const uint32_t *T)
+                                                    const uint32_t *Sblk, const uint32_t *S, const uint32_t *T,
+                                                    uint32_t kfast, uint32_t kmax)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -2875,11 +2912,11 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
     uint32_t *st = s_pt[wv];
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
     uint32_t s0;
-    if (meta[0] > SPEC_KFAST) {
+    if (meta[0] > kmax) {
         s0 = S[c0];
     } else { // chunk start state: the block's start, then the block's earlier chunks
         const uint64_t blk = c / SPEC_BLK;
-        s0 = c % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (c - 1) * SPEC_KFAST, class_id, Sblk[blk]);
+        s0 = c % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (c - 1) * spec_kf(meta[0], kfast), class_id, Sblk[blk]);
     }
     if (meta[0] <= SPEC_KMAX) { // k_spec_ctables wrote the chunk's summary
         const uint32_t sm = T[nch * SPEC_KMAX + c], q0 = spec_lowslot(s0 & 0xffu);
@@ -3127,6 +3164,7 @@ struct cndp_gpu_ctx {
     int tune_dir16;       // CNDP_TUNE_DIR16
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
     int tune_lnt;         // CNDP_TUNE_LOAD_NT
+    int tune_spec_scan;   // CNDP_TUNE_SPEC_SCAN
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
@@ -3684,7 +3722,7 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
         HIP_TRY(hipMalloc((void **)&c->sp_S, cap * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
         // inclusive burst prefixes + block totals + block start states
-        HIP_TRY(hipMalloc((void **)&c->sp_U, (cap * SPEC_KFAST + (cap / SPEC_BLK + 2) * (SPEC_KFAST + 1)) * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_U, (cap * SPEC_KMAX + (cap / SPEC_BLK + 2) * (SPEC_KMAX + 1)) * 4));
         c->sp_b_cap = cap;
     }
     return 0;
@@ -3807,6 +3845,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
             hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta);
             const uint32_t gw = (uint32_t)((nb + 3) / 4); // one wave per burst
+            const uint32_t kfast = c->tune_spec_scan == 0 ? SPEC_KFAST : 0u;
+            const uint32_t kmax = c->tune_spec_scan == 2 ? 0u : SPEC_KMAX;
             if (B <= 256) { // chunked passes (SPEC_CH bursts per wave)
                 const uint64_t nch = (nb + SPEC_CH - 1) / SPEC_CH;
                 const uint32_t gc = (uint32_t)((nch + 3) / 4);
@@ -3815,28 +3855,26 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                 hipLaunchKernelGGL(ct, dim3(gc), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B, nb, nch,
                                    (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
                 const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
-                uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
+                uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
                 hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nch,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P,
-                                   Bt);
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast);
                 hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
-                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S);
+                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax);
                 hipLaunchKernelGGL(ce, dim3(gc), dim3(256), 0, s, a, B, nb, nch, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
-                                   (const uint32_t *)c->sp_S, (const uint32_t *)c->sp_T);
+                                   (const uint32_t *)c->sp_S, (const uint32_t *)c->sp_T, kfast, kmax);
             } else {
                 hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
                 const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
-                uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KFAST, *Sblk = Bt + nblk * SPEC_KFAST;
+                uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
                 hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P,
-                                   Bt);
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast);
                 hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
-                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S);
-                hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, (uint32_t)SPEC_KFAST,
+                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax);
+                hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, kfast, kmax,
                                    (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
                                    (const uint32_t *)Sblk, (const uint32_t *)c->sp_S);
             }
@@ -4601,6 +4639,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return 0;
     case CNDP_TUNE_LOAD_NT:
         c->tune_lnt = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_SPEC_SCAN:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_spec_scan = value;
         return 0;
     case CNDP_TUNE_RW_WB:
         if (value < 0 || value > 2)

@@ -39,6 +39,7 @@ CNDP_TUNE_HOST_CHUNK = 7
 CNDP_TUNE_RW_WB = 8
 CNDP_TUNE_CNET_SPEC = 9
 CNDP_TUNE_LOAD_NT = 10
+CNDP_TUNE_SPEC_SCAN = 11
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF
 
 # l3fwd edges (node_ip4_api.h:28-34) and cnet edges (ip4_input_priv.h:26-31)

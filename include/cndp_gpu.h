@@ -206,7 +206,11 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_LOAD_NT       wave-tile kernels (tile 4 / 5, cnet tile): 1 = frame tiles loaded with the
  *                           non-temporal hint, so the once-read stream neither allocates
  *                           in L2 / the Infinity Cache nor evicts the FIB directory from
- *                           them (default 1) */
+ *                           them (default 1)
+ *   CNDP_TUNE_SPEC_SCAN     cnet speculation: how burst maps are composed. 0 = auto (maps
+ *                           of 8 entries when <= 8 ptype signatures occur, 64 up to 64,
+ *                           a sequential walk beyond), 1 = 64-entry maps, 2 = the
+ *                           sequential walk (default 0; 1 and 2 exist for tests) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -217,6 +221,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_RW_WB 8
 #define CNDP_TUNE_CNET_SPEC 9
 #define CNDP_TUNE_LOAD_NT 10
+#define CNDP_TUNE_SPEC_SCAN 11
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

@@ -608,7 +608,7 @@ def _gtp_mix(n, routes, v6, gpu, seed):
     return pktgen.Frames(fr.slab.to(gpu), n, offsets=fr.offsets.to(gpu))
 
 
-@pytest.mark.parametrize("burst", [256, 7, 64])
+@pytest.mark.parametrize("burst", [256, 7, 64, 1000])
 def test_cnet_ptype_speculation(cnet, gpu, burst):
     """ptype.c:48-210 speculation incl. the uint8_t fix_spec quirk: GPU ==
     the restated node loop, across bursts and across calls (state kept)."""
@@ -617,11 +617,15 @@ def test_cnet_ptype_speculation(cnet, gpu, burst):
     plain = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)
     ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=burst)
     assert (plain["edge"] != ref["edge"]).sum() > 0, "input does not exercise the quirk"
-    ccl.set_tuning(cnet_spec=burst)
-    out = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
-    ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
-    torch.cuda.synchronize()
-    assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    try:
+        for scan in (0, 1, 2):  # auto (8-entry maps here), 64-entry maps, sequential walk
+            ccl.set_tuning(cnet_spec=burst, spec_scan=scan)
+            out = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+            ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
+            torch.cuda.synchronize()
+            assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(spec_scan=0)
     # two calls over halves (cut on a burst boundary) == one call: the node state persists
     cut = (fr.n // 2) // burst * burst
     st = np.zeros(1, np.uint16)
@@ -637,9 +641,32 @@ def test_cnet_ptype_speculation(cnet, gpu, burst):
 
 
 def test_cnet_speculation_many_signatures(cnet, gpu):
-    """More distinct ptype signatures than the scan handles (fuzz): the
-    sequential fallback gives the same answer as the node loop."""
+    """Fuzz frames give ~21 distinct ptype signatures: more than the 8-entry
+    maps hold, so the scans run 64-entry maps; the forced sequential walk
+    (CNDP_TUNE_SPEC_SCAN 2) gives the same answer as the node loop too."""
     ccl, routes, v6, ct4, ct6 = cnet
-    for seed in (5, 6):
-        fr = pktgen.fuzz_frames(30000, seed=seed, slot=128, device=gpu)
-        assert_same(run_gpu(ccl, fr, N.CNDP_MODE_CNET), oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6))
+    try:
+        for seed in (5, 6):
+            fr = pktgen.fuzz_frames(30000, seed=seed, slot=128, device=gpu)
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
+            sigs = {((int(p) & 0xFF) << 3) | _cnet_edge(int(p)) for p in ref["ptype"]}
+            assert len(sigs) > 8, "fuzz input no longer exceeds the 8-entry maps"
+            for scan in (0, 2):
+                ccl.set_tuning(spec_scan=scan)
+                assert_same(run_gpu(ccl, fr, N.CNDP_MODE_CNET), ref)
+    finally:
+        ccl.set_tuning(spec_scan=0)
+
+
+def _cnet_edge(pt):
+    """ptype.c:32-46 p_nxt of a packet type (the signature's edge part)."""
+    pt &= 0xFFFF
+    if pt == 0x0003:
+        return 2
+    if pt in (0x0211, 0x0111, 0x0231, 0x0291):
+        return 3
+    if pt in (0x0241, 0x0141, 0x02C1, 0x02E1):
+        return 4
+    if pt in (0x8211, 0x8241):
+        return 5
+    return 0
