@@ -966,7 +966,8 @@ __device__ __forceinline__ uint32_t pt_l3_ip(uint32_t vihl)
 }
 __device__ __forceinline__ uint32_t pt_l4(uint32_t p)
 {
-    return p == 17u ? 0x200u : p == 6u ? 0x100u : p == 132u ? 0x400u : 0u;
+    // independent selects ORed (a ternary chain compiles to a branch tree)
+    return (p == 17u ? 0x200u : 0u) | (p == 6u ? 0x100u : 0u) | (p == 132u ? 0x400u : 0u);
 }
 __device__ __forceinline__ bool v6_ext(uint32_t p)
 {
@@ -1418,8 +1419,9 @@ __device__ __forceinline__ uint64_t ct_base(const KArgs &a, uint64_t i, uint64_t
 
 __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
 {
-    return base != ~0ull && base < a.slab_len && a.slab_len - base >= 64 &&
-           (((uintptr_t)a.slab + base) & 15u) == 0;
+    // base + 64 <= slab_len (base = ~0 fails it) and 16-B aligned; bitwise
+    // ANDs so the test stays straight-line
+    return (a.slab_len >= 64) & (base <= a.slab_len - 64) & ((((uintptr_t)a.slab + base) & 15u) == 0);
 }
 
 template <bool LNT>
@@ -1517,10 +1519,11 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(CT_W
         }
         const uint32_t et = W[3] & 0xffffu;         // raw bytes 12..13
         const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-        const bool l4p4 = p4 == 6u || p4 == 17u || p4 == 132u, l4p6 = p6 == 6u || p6 == 17u || p6 == 132u;
-        const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
-                        ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
-        const bool f6 = et == BE16C(0x86DDu) && l4p6;
+        // straight-line tests (bitwise &, not &&: no branch tree)
+        const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
+        const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
+                        (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
+        const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
         uint32_t pt = 0, pe = 0;
         Lens lens{14u, 0u, 0u};
         uint32_t hw[9];      // Toeplitz input words, nw of them + the L4 word
@@ -1532,7 +1535,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(CT_W
             hw[k] = 0;
         if (live && (f4 || f6)) {
             const uint32_t proto = f4 ? p4 : p6;
-            pt = (f4 ? 0x11u : 0x41u) | pt_l4(proto);
+            pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
             if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
                 const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
                 pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
@@ -1748,7 +1751,7 @@ struct CsOff { // this lane's frame offsets for tiles t, t+1, t+2 and the load f
 };
 
 template <bool LNT>
-__device__ __forceinline__ void cs_issue(const KArgs &a, uint64_t tt, uint64_t n_tiles, uint64_t off,
+__device__ __forceinline__ void cs_issue(const KArgs &a, uint32_t tt, uint32_t n_tiles, uint64_t off,
                                          uint32_t lane, u32x4 (&r)[4])
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
@@ -1765,13 +1768,13 @@ __device__ __forceinline__ void cs_issue(const KArgs &a, uint64_t tt, uint64_t n
 }
 
 template <bool LNT, int P>
-__device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wstep, uint64_t n_tiles, uint32_t lane,
+__device__ __forceinline__ void cs_trip(const KArgs &a, uint32_t t, uint32_t wstep, uint32_t n_tiles, uint32_t lane,
                                         u32x4 *tile, u32x4 (&r)[2][4], CsOff &off,
                                         const uint32_t *s_t, const uint16_t *s_reta, uint32_t *s_bins,
                                         uint32_t *s_sf, bool count)
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const uint64_t i = t * 64u + lane;
+    const uint32_t i = t * 64u + lane;
     // (1) stage the tile (chunks of non-fast frames are never read)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1796,11 +1799,12 @@ __device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wst
     // to the worklist
     const uint32_t et = W[3] & 0xffffu; // raw bytes 12..13
     const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-    const bool l4p4 = p4 == 6u || p4 == 17u || p4 == 132u, l4p6 = p6 == 6u || p6 == 17u || p6 == 132u;
-    const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
-                    ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
-    const bool f6 = et == BE16C(0x86DDu) && l4p6;
-    const bool fast = live && ct_fast(a, base) && (f4 || f6);
+    // straight-line tests (bitwise &, not &&: no branch tree)
+    const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
+    const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
+                    (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
+    const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
+    const bool fast = live & ct_fast(a, base) & (f4 | f6);
     {
         const bool slow = live && !fast;
         const unsigned long long m = __ballot(slow);
@@ -1824,7 +1828,7 @@ __device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wst
         hw[k] = 0;
     if (fast) {
         const uint32_t proto = f4 ? p4 : p6;
-        pt = (f4 ? 0x11u : 0x41u) | pt_l4(proto);
+        pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
         if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
             const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
             pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
@@ -1909,7 +1913,7 @@ __device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wst
     }
     // (4) the offsets one tile further, then the windows of tile t+2
     {
-        const uint64_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
+        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
         cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
     }
@@ -1957,7 +1961,7 @@ __device__ __forceinline__ void cs_trip(const KArgs &a, uint64_t t, uint64_t wst
 #define CS_THREADS 256
 #define CS_WAVES (CS_THREADS / 64)
 template <bool LNT>
-__global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_cnet_stream(KArgs a, uint64_t n_tiles)
+__global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_cnet_stream(KArgs a, uint32_t n_tiles)
 {
     // nibble Toeplitz tables (4.5 KiB) instead of the 36 KiB byte tables: ~21
     // KiB of LDS per 4-wave block, so LDS no longer caps the waves per CU
@@ -1982,13 +1986,13 @@ __global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5
 
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     u32x4 *tile = s_tile[wv];
-    const uint64_t wstep = (uint64_t)gridDim.x * CS_WAVES;
-    const uint64_t t0 = (uint64_t)blockIdx.x * CS_WAVES + wv;
+    const uint32_t wstep = gridDim.x * CS_WAVES;
+    const uint32_t t0 = blockIdx.x * CS_WAVES + wv;
     CsOff off{0, 0, 0, 0};
     if (a.offsets) {
 #pragma unroll
         for (uint32_t s = 0; s < 3; s++) {
-            const uint64_t ts = t0 + s * wstep, is = ts * 64u + lane;
+            const uint32_t ts = t0 + s * wstep, is = ts * 64u + lane;
             const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
             if (s == 0)
                 off.o0 = o;
@@ -2001,7 +2005,7 @@ __global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5
     u32x4 r[2][4];
     cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
     cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
-    for (uint64_t t = t0; t < n_tiles; t += 2u * wstep) {
+    for (uint32_t t = t0; t < n_tiles; t += 2u * wstep) {
         cs_trip<LNT, 0>(a, t, wstep, n_tiles, lane, tile, r, off, s_t, s_reta, s_bins, s_sf, count);
         if (t + wstep < n_tiles)
             cs_trip<LNT, 1>(a, t + wstep, wstep, n_tiles, lane, tile, r, off, s_t, s_reta, s_bins, s_sf, count);
@@ -2032,16 +2036,16 @@ struct CdLane {
 };
 
 template <bool LNT, int P>
-__device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t wstep, uint64_t n_tiles,
-                                        uint64_t nt_w, uint64_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
+__device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
+                                        uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
                                         CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
                                         uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig)
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const uint64_t t = t0 + jt * wstep;
+    const uint32_t t = t0 + jt * wstep;
     // B: tile c-1 -- the rest of its chain (v4: page / tbl8, v6: tbl8 levels, trie.h:127-134)
     const bool bv = jt >= 1 && jt - 1 < nt_w;
-    const uint64_t ib = (t - wstep) * 64u + lane;
+    const uint32_t ib = (t - wstep) * 64u + lane;
     uint32_t eb = sb.e;
     {
         const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
@@ -2072,7 +2076,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t ws
         tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
     }
     __builtin_amdgcn_wave_barrier();
-    const uint64_t i = t * 64u + lane;
+    const uint32_t i = t * 64u + lane;
     const bool live = jt < nt_w && i < a.n;
     const uint64_t base = live ? ct_base(a, i, off.o0) : ~0ull;
     const uint32_t sw = (lane >> 2) & 3u;
@@ -2088,11 +2092,12 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t ws
     __builtin_amdgcn_wave_barrier();
     const uint32_t et = W[3] & 0xffffu;
     const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-    const bool l4p4 = p4 == 6u || p4 == 17u || p4 == 132u, l4p6 = p6 == 6u || p6 == 17u || p6 == 132u;
-    const bool f4 = et == BE16C(0x0800u) && ((W[3] >> 16) & 0xffu) == 0x45u &&
-                    ((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u && l4p4;
-    const bool f6 = et == BE16C(0x86DDu) && l4p6;
-    const bool fast = live && ct_fast(a, base) && (f4 || f6);
+    // straight-line tests (bitwise &, not &&: no branch tree)
+    const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
+    const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
+                    (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
+    const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
+    const bool fast = live & ct_fast(a, base) & (f4 | f6);
     {
         const bool slow = live && !fast;
         const unsigned long long m = __ballot(slow);
@@ -2114,7 +2119,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t ws
     const uint32_t *tb0 = a.tbl24_6;
     if (fast) {
         const uint32_t proto = f4 ? p4 : p6;
-        uint32_t pt = (f4 ? 0x11u : 0x41u) | pt_l4(proto);
+        uint32_t pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
         if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
             const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
             pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
@@ -2171,7 +2176,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t ws
     na.e = tb0[idx0]; // first gather, unconditional
     // offsets one tile further, then the windows of tile c+2
     {
-        const uint64_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
+        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
         cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
     }
@@ -2219,7 +2224,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint64_t t0, uint64_t ws
 }
 
 template <bool LNT>
-__global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint64_t n_tiles)
+__global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
     __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
@@ -2242,14 +2247,14 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint64_t n_t
 
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     u32x4 *tile = s_tile[wv];
-    const uint64_t wstep = (uint64_t)gridDim.x * CT_WAVES;
-    const uint64_t t0 = (uint64_t)blockIdx.x * CT_WAVES + wv;
-    const uint64_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
+    const uint32_t wstep = gridDim.x * CT_WAVES;
+    const uint32_t t0 = blockIdx.x * CT_WAVES + wv;
+    const uint32_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
     CsOff off{0, 0, 0, 0};
     if (a.offsets) {
 #pragma unroll
         for (uint32_t s = 0; s < 3; s++) {
-            const uint64_t ts = t0 + s * wstep, is = ts * 64u + lane;
+            const uint32_t ts = t0 + s * wstep, is = ts * 64u + lane;
             const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
             if (s == 0)
                 off.o0 = o;
@@ -2266,8 +2271,8 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint64_t n_t
     sb.ptf = sb.h = sb.e = sb.rx = 0;
     sb.d0 = sb.d1 = sb.d2 = sb.d3 = 0;
     uint32_t last_sig = 0xFFFFFFFFu;
-    const uint64_t trips = nt_w ? nt_w + 1 : 0;
-    for (uint64_t jt = 0; jt < trips; jt += 2) {
+    const uint32_t trips = nt_w ? nt_w + 1 : 0;
+    for (uint32_t jt = 0; jt < trips; jt += 2) {
         cd_trip<LNT, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
                         last_sig);
         if (jt + 1 < trips)
@@ -3792,7 +3797,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             a.spec_flags = c->sp_small + 66;
             HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
         }
-        if (c->tune_cnet_tile == 2 || c->tune_cnet_tile == 3) {
+        // the streamed kernels index frames in 32 bits (t * 64 + lane < 2^32)
+        if ((c->tune_cnet_tile == 2 || c->tune_cnet_tile == 3) && b->n <= 0xFFFFFF00u) {
             // fast kernel, then the general parse of the frames it left
             if ((uint64_t)b->n + 1 > c->cs_wl_cap) {
                 if (c->cs_wl)
@@ -3813,19 +3819,22 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                 if (gd > (uint64_t)c->num_cu * bpc)
                     gd = (uint64_t)c->num_cu * bpc;
                 if (c->tune_lnt)
-                    hipLaunchKernelGGL(k_cnet_defer<true>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, n_tiles);
+                    hipLaunchKernelGGL(k_cnet_defer<true>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a,
+                                       (uint32_t)n_tiles);
                 else
-                    hipLaunchKernelGGL(k_cnet_defer<false>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, n_tiles);
+                    hipLaunchKernelGGL(k_cnet_defer<false>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a,
+                                       (uint32_t)n_tiles);
             } else {
                 uint64_t gt = (n_tiles + CS_WAVES - 1) / CS_WAVES;
                 const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 5u;
                 if (gt > (uint64_t)c->num_cu * bpc)
                     gt = (uint64_t)c->num_cu * bpc;
                 if (c->tune_lnt)
-                    hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a, n_tiles);
+                    hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a,
+                                       (uint32_t)n_tiles);
                 else
                     hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a,
-                                       n_tiles);
+                                       (uint32_t)n_tiles);
             }
             hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         } else if (c->tune_cnet_tile || B) {
