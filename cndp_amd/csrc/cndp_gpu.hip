@@ -2134,11 +2134,26 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             na.rx = rx_meta(lens, W[0], W[1], et);
         }
         uint32_t flags = 0;
+        // Toeplitz, one instruction stream for both families: the v6 words
+        // are V[0..7] + L4 V[8], the v4 ones V[1..2] + L4 V[3] (a zero word
+        // adds nothing); positions past the v4 tuple only when the wave has v6
+        {
+            uint32_t V[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++)
+                V[k] = alignb(W[6 + k], W[5 + k], 2);
+            const bool any6 = __any(f6);
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                if (k >= 3 && !any6)
+                    break;
+                uint32_t u = k < 2 ? (f4 ? V[k + 1] : V[k]) : k == 2 ? (f4 ? (l4ok ? V[3] : 0u) : V[2])
+                           : k < 8 ? (f4 ? 0u : V[k]) : (f4 || !l4ok ? 0u : V[8]);
+                na.h ^= tz4(s_t, 4 * k, u);
+            }
+        }
         if (f4) {
             const uint32_t dst = alignb(W[8], W[7], 2);
-            na.h = tz4(s_t, 0, alignb(W[7], W[6], 2)) ^ tz4(s_t, 4, dst);
-            if (l4ok)
-                na.h ^= tz4(s_t, 8, alignb(W[9], W[8], 2));
             if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
                 uint32_t sum = 0;
 #pragma unroll
@@ -2155,11 +2170,6 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 idx0 = a.dir16 ? na.d0 >> 16 : na.d0 >> 8;
             }
         } else {
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                na.h ^= tz4(s_t, 4 * k, alignb(W[6 + k], W[5 + k], 2));
-            if (l4ok)
-                na.h ^= tz4(s_t, 32, alignb(W[14], W[13], 2));
             if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
                 if (bswap16(W[4] >> 16) < a.buf_len) {
                     na.d0 = alignb(W[10], W[9], 2);
