@@ -1210,6 +1210,27 @@ __device__ __forceinline__ uint32_t spec_lowslot(uint32_t low)
          : low == 0x41u ? 4u : low == 0xc1u ? 5u : low == 0xe1u ? 6u : SPEC_LOWS;
 }
 
+// cnet_edge / spec_lowslot by low byte, an LDS table of 256 words filled by
+// the kernel: bits 3h..3h+2 = p_nxt of type H[h] << 8 | low for H = {0x00,
+// 0x01, 0x02, 0x82} (every other high byte goes to pkt_drop), bits 12..14 =
+// spec_lowslot(low).  One LDS read + ~8 ops instead of the compare chains.
+__device__ __forceinline__ void cnet_lut_fill(uint32_t *lut, uint32_t tid, uint32_t nthr)
+{
+    for (uint32_t k = tid; k < 256; k += nthr)
+        lut[k] = cnet_edge(k) | (cnet_edge(0x100u | k) << 3) | (cnet_edge(0x200u | k) << 6) |
+                 (cnet_edge(0x8200u | k) << 9) | (spec_lowslot(k) << 12);
+}
+__device__ __forceinline__ uint32_t cnet_edge_v(uint32_t v, uint32_t l) // v = lut[l & 0xff]
+{
+    const uint32_t h = (l >> 8) & 0xffu;
+    const uint32_t hi = h < 3u ? h : h == 0x82u ? 3u : 4u; // 4: bits 12.. masked off
+    return ((v & 0xfffu) >> (3u * hi)) & 7u;
+}
+__device__ __forceinline__ uint32_t cnet_edge_l(const uint32_t *lut, uint32_t l)
+{
+    return cnet_edge_v(lut[l & 0xffu], l);
+}
+
 // Burst / chunk maps store their target states tagged with the target's
 // signature class (state | class << 16; SPEC_UNCH = keep the state), so map
 // composition never recomputes a signature.
@@ -2030,7 +2051,7 @@ __global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5
 // earlier, never behind the window loads of the same trip.
 // ---------------------------------------------------------------------------
 struct CdLane {
-    uint32_t ptf;  // pt (16) | do4 << 16 | do6 << 17 | fast << 18
+    uint32_t ptf;  // pt (16) | do4 << 16 | do6 << 17 | fast << 18 | p_nxt edge << 19
     uint32_t h, e, rx;
     uint32_t d0, d1, d2, d3; // v6 destination words, or dip in d0 (v4)
 };
@@ -2120,11 +2141,13 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     if (fast) {
         const uint32_t proto = f4 ? p4 : p6;
         uint32_t pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
-        if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
-            const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
-            pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
-        }
-        const uint32_t pe = cnet_edge(pt);
+        // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
+        const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
+        const bool udp = proto == 17u, gtpu = udp & (dport == BE16C(2152u)), gtpc = udp & (dport == BE16C(2123u));
+        pt |= gtpu ? 0x8000u : gtpc ? 0x7000u : 0u;
+        // cnet_edge(pt) for these shapes (ptype.c:32-46): TCP / UDP go to the
+        // family's input node, GTP-U to gtpu_input, GTP-C and SCTP to pkt_drop
+        const uint32_t pe = (proto == 6u) | (udp & !gtpc) ? (gtpu ? 5u : f4 ? 3u : 4u) : 0u;
         const bool l4ok = proto == 6u || proto == 17u;
         Lens lens{14u, f4 ? 20u : 40u, 0u};
         if (a.rxmeta) { // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
@@ -2181,7 +2204,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 idx0 = ((na.d0 & 0xffu) << 16) | (na.d0 & 0xff00u) | ((na.d0 >> 16) & 0xffu); // trie.h:126
             }
         }
-        na.ptf = pt | flags | (1u << 18);
+        na.ptf = pt | flags | (1u << 18) | (pe << 19);
     }
     na.e = tb0[idx0]; // first gather, unconditional
     // offsets one tile further, then the windows of tile c+2
@@ -2192,7 +2215,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     }
     // B's results
     {
-        const uint32_t pt = sb.ptf & 0xffffu, pe = cnet_edge(pt);
+        const uint32_t pt = sb.ptf & 0xffffu, pe = sb.ptf >> 19;
         const bool bf = bv && (sb.ptf & (1u << 18));
         const bool din = (sb.ptf & (3u << 16)) != 0u;
         uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
@@ -2205,7 +2228,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 a.spec_nh[ib] = eb >> 1;
             if (bf)
                 a.spec_t16[ib] = (uint16_t)pt;
-            const uint32_t sg = spec_sig(pt);
+            const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
         }
@@ -2319,8 +2342,31 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 #define SPEC_UNCH 0xFFFFFFFFu
 
 // meta[0] = K, meta[1 + k] = signature of class k; class_id[sig] = k or 0xFF
-// (64 threads: thread t owns flag word t, classes numbered in signature order)
-__global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta)
+// (64 threads: thread t owns flag word t, classes numbered in signature order).
+//
+// Batch-level shortcut, meta[SPEC_SKIP]: when no low byte among the
+// signatures present (the entering state's included) carries two p_nxt
+// edges, a quiet group's speculated edge p_nxt[last_type] is every one of
+// its frames' own edge, so the node routes exactly like the per-frame result
+// already written -- only the final last_type is left to find.  A
+// "universal" group (low bytes not all equal, 3rd type == 4th) sets the state
+// to its 4th type whatever it was, so the final state is the walk from the
+// batch's last universal group to its end.  The wave looks for one in the
+// last SPEC_TAIL bursts; found, it stores the final state and sets
+// meta[SPEC_SKIP], and the table / scan / replay passes return at once.
+#define SPEC_SKIP 129
+#define SPEC_TAIL 16
+__device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t &cur)
+{
+    const uint32_t low = cur & 0xffu;
+    const bool quiet = (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low && (l3 & 0xffu) == low;
+    if (!quiet && (l2 == l3 || cnet_edge(cur) == cnet_edge(l3)))
+        cur = l3;
+}
+
+__global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta,
+                                                     const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                     uint64_t nb, uint32_t allow_skip)
 {
     const uint32_t t = threadIdx.x;
     const uint32_t g0 = spec_sig(meta[-1] & 0xffffu); // the node state entering the batch
@@ -2345,6 +2391,53 @@ __global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint
     }
     if (t == 63)
         meta[0] = pre;
+    // flag word t holds the 8 edge bits of low bytes 4t..4t+3: one edge each?
+    bool one = true;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t e8 = (w >> (8 * q)) & 0xffu;
+        one = one && (e8 & (e8 - 1u)) == 0u;
+    }
+    uint32_t skip = 0;
+    if (allow_skip && __ballot(!one) == 0ull) {
+        int64_t ub = -1; // the last universal group: burst ub, group ug
+        uint32_t ug = 0;
+        for (uint64_t q = 0; q < SPEC_TAIL && q < nb && ub < 0; q++) {
+            const uint64_t b = nb - 1 - q, b0 = b * B;
+            const uint32_t ng = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B) >> 2;
+            int best = -1;
+            for (uint32_t j = t; j < ng; j += 64) {
+                const uint32_t l0 = pt[b0 + 4 * j], l1 = pt[b0 + 4 * j + 1];
+                const uint32_t l2 = pt[b0 + 4 * j + 2], l3 = pt[b0 + 4 * j + 3];
+                const uint32_t v = l0 & 0xffu;
+                const bool allq = (l1 & 0xffu) == v && (l2 & 0xffu) == v && (l3 & 0xffu) == v;
+                if (!allq && l2 == l3)
+                    best = (int)j;
+            }
+            for (int o = 32; o > 0; o >>= 1)
+                best = max(best, __shfl_xor(best, o));
+            if (best >= 0) {
+                ub = (int64_t)b;
+                ug = (uint32_t)best;
+            }
+        }
+        if (ub >= 0) {
+            skip = 1;
+            if (t == 0) { // walk from it to the batch end
+                uint32_t cur = pt[(uint64_t)ub * B + 4 * ug + 3];
+                uint32_t j = ug + 1;
+                for (uint64_t b = (uint64_t)ub; b < nb; b++, j = 0) {
+                    const uint64_t b0 = b * B;
+                    const uint32_t ng = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B) >> 2;
+                    for (; j < ng; j++)
+                        spec_step(pt[b0 + 4 * j], pt[b0 + 4 * j + 1], pt[b0 + 4 * j + 2], pt[b0 + 4 * j + 3], cur);
+                }
+                meta[-1] = cur;
+            }
+        }
+    }
+    if (t == 0)
+        meta[SPEC_SKIP] = skip;
 }
 
 // the 4 types of the group at packet j (16-B load when the burst size keeps
@@ -2444,7 +2537,7 @@ __global__ __launch_bounds__(256) void k_spec_tables(const uint16_t *__restrict_
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t b = (uint64_t)blockIdx.x * 4 + wv;
     const uint32_t K = meta[0];
-    if (b >= nb || K > SPEC_KMAX)
+    if (b >= nb || K > SPEC_KMAX || meta[SPEC_SKIP])
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t b0 = b * B;
@@ -2559,6 +2652,8 @@ __global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uin
 {
     __shared__ uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
     const uint32_t K = meta[0];
+    if (meta[SPEC_SKIP])
+        return;
     if (K <= kfast)
         spec_scan_a_body<SPEC_KFAST>(s_m, nb, K, T, P, Bt);
     else if (K <= SPEC_KMAX)
@@ -2645,6 +2740,8 @@ __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint3
                                                                              : 256 * (SPEC_KMAX + 1)];
     __shared__ uint32_t s_carry[SPEC_KMAX];
     const uint32_t K = meta[0];
+    if (meta[SPEC_SKIP])
+        return;
     if (K <= kfast) {
         spec_scan_c_body<SPEC_KFAST, 1024>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
     } else if (K <= kmax) {
@@ -2692,7 +2789,7 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
     __shared__ uint8_t s_q[4][SPEC_STAGE / 4];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t b = (uint64_t)blockIdx.x * 4 + wv;
-    if (b >= nb)
+    if (b >= nb || meta[SPEC_SKIP])
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t b0 = b * B;
@@ -2793,10 +2890,17 @@ __device__ __forceinline__ unsigned long long spec_em(uint32_t l, uint32_t e)
     return q < SPEC_LOWS ? 1ull << (6 * q + e) : 0ull;
 }
 
+// em bit of a type from its LUT word v and edge e
+__device__ __forceinline__ unsigned long long spec_em_v(uint32_t v, uint32_t e)
+{
+    const uint32_t q = (v >> 12) & 7u;
+    return q < SPEC_LOWS ? 1ull << (6 * q + e) : 0ull;
+}
+
 template <int CH>
 __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *__restrict__ pt, uint32_t n,
                                                                uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
-                                                               uint32_t *st)
+                                                               uint32_t *st, const uint32_t *lut)
 {
     unsigned long long em = 0;
     const uint32_t bs = spec_bstride(B);
@@ -2827,10 +2931,11 @@ __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *_
             uint32_t o[8];
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++) {
-                const uint32_t l = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu, e = cnet_edge(l);
+                const uint32_t l = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu, v = lut[l & 0xffu];
+                const uint32_t e = cnet_edge_v(v, l);
                 o[q] = l | (e << 16);
                 if (idx + q < m)
-                    em |= spec_em(l, e);
+                    em |= spec_em_v(v, e);
             }
             *(u32x4 *)(st + idx) = (u32x4){o[0], o[1], o[2], o[3]};
             *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
@@ -2841,9 +2946,9 @@ __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *_
             const uint32_t cnt = (uint32_t)((uint64_t)n - p0 < B ? (uint64_t)n - p0 : B);
             uint32_t *d = st + (j - c0) * bs;
             for (uint32_t k = lane; k < cnt; k += 64) {
-                const uint32_t l = pt[p0 + k], e = cnet_edge(l);
+                const uint32_t l = pt[p0 + k], v = lut[l & 0xffu], e = cnet_edge_v(v, l);
                 d[k] = l | (e << 16);
-                em |= spec_em(l, e);
+                em |= spec_em_v(v, e);
             }
         }
     }
@@ -2857,14 +2962,19 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
                                                       const uint8_t *class_id, uint32_t *T)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
+    __shared__ uint32_t s_lut[256];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     const uint32_t K = meta[0];
-    if (c >= nch || K > SPEC_KMAX)
+    if (K > SPEC_KMAX || meta[SPEC_SKIP]) // block-uniform: before the barrier
+        return;
+    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    __syncthreads();
+    if (c >= nch)
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-    unsigned long long em = spec_stage_chunk<CH>(pt, n, B, c0, c1, lane, st);
+    unsigned long long em = spec_stage_chunk<CH>(pt, n, B, c0, c1, lane, st, s_lut);
     const uint32_t sig = lane < K ? meta[1 + lane] : 0u;
     uint32_t cm = SPEC_UNCH;
     for (uint64_t bb = c0; bb < c1; bb++) {
@@ -2920,8 +3030,13 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
                                                     uint32_t kfast, uint32_t kmax)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
+    __shared__ uint32_t s_lut[256];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if (meta[SPEC_SKIP]) // block-uniform: before the barrier
+        return;
+    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    __syncthreads();
     if (c >= nch)
         return;
     uint32_t *st = s_pt[wv];
@@ -2939,7 +3054,7 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
         if (!(sm >> 31) && (!(slot & 8u) || (slot & 7u) == cnet_edge(s0)))
             return; // no frame of this chunk can leave by another edge
     }
-    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st);
+    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
     for (uint64_t bb = c0; bb < c1; bb++) {
         const uint32_t *sb = st + (bb - c0) * spec_bstride(B);
         const uint64_t b0 = bb * B;
@@ -3862,7 +3977,8 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         if (B) {
             const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
             uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
-            hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta);
+            hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta,
+                               (const uint16_t *)a.spec_t16, b->n, B, nb, (uint32_t)(c->tune_spec_scan == 0));
             const uint32_t gw = (uint32_t)((nb + 3) / 4); // one wave per burst
             const uint32_t kfast = c->tune_spec_scan == 0 ? SPEC_KFAST : 0u;
             const uint32_t kmax = c->tune_spec_scan == 2 ? 0u : SPEC_KMAX;

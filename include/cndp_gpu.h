@@ -207,10 +207,12 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           non-temporal hint, so the once-read stream neither allocates
  *                           in L2 / the Infinity Cache nor evicts the FIB directory from
  *                           them (default 1)
- *   CNDP_TUNE_SPEC_SCAN     cnet speculation: how burst maps are composed. 0 = auto (maps
- *                           of 8 entries when <= 8 ptype signatures occur, 64 up to 64,
- *                           a sequential walk beyond), 1 = 64-entry maps, 2 = the
- *                           sequential walk (default 0; 1 and 2 exist for tests) */
+ *   CNDP_TUNE_SPEC_SCAN     cnet speculation: how burst maps are composed. 0 = auto (none
+ *                           when no low byte of the batch's ptypes carries two p_nxt
+ *                           edges -- only the final node state is walked -- else maps of
+ *                           8 entries when <= 8 ptype signatures occur, 64 up to 64, a
+ *                           sequential walk beyond), 1 = always 64-entry maps, 2 = always
+ *                           the sequential walk (default 0; 1 and 2 exist for tests) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3

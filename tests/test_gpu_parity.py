@@ -640,6 +640,44 @@ def test_cnet_ptype_speculation(cnet, gpu, burst):
     ccl.set_tuning(cnet_spec=256)
 
 
+@pytest.mark.parametrize("burst", [256, 7, 1000])
+def test_cnet_speculation_batch_shortcut(cnet, gpu, burst):
+    """Batches whose low ptype bytes each carry one p_nxt edge (plain IMIX:
+    v4 UDP 0x0211 / v6 UDP 0x0241) skip the map passes and only walk the
+    final node state from the last universal group; pure single-type traffic
+    has no universal group and takes the full passes.  Both == the node loop,
+    across chained calls (the state carried), and == the forced full scans."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    # seeds whose random UDP ports miss the GTP ports (GTP-U 0x8211 would share
+    # low byte 0x11 with 0x0211 under another edge: no shortcut)
+    mixed = pktgen.imix(20000, v4routes=routes, v6routes=v6, device=gpu, seed=1001 if burst == 1000 else burst)
+    pure = pktgen.packed_ipv4(20000, routes=routes, device=gpu, seed=burst)
+    pure.slab.view(pure.n, pure.stride)[:, 36] = 0x12  # UDP dport off the GTP ports: one type
+    try:
+        for fr in (mixed, pure):
+            types = set((oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)["ptype"] & 0xFFFF).tolist())
+            assert types <= {0x0211, 0x0241}, "input no longer one edge per low byte"
+
+            cuts = (0, (fr.n // 3) // burst * burst, fr.n)
+            for scan in (0, 1, 2):
+                ccl.set_tuning(cnet_spec=burst, spec_scan=scan)  # also resets the node state
+                st = np.zeros(1, np.uint16)
+                for lo, hi in zip(cuts[:-1], cuts[1:]):
+                    if fr.offsets is not None:
+                        part = pktgen.Frames(fr.slab, hi - lo, offsets=fr.offsets[lo:hi].contiguous())
+                    else:
+                        part = pktgen.Frames(fr.slab[lo * fr.stride:hi * fr.stride], hi - lo, stride=fr.stride,
+                                             data_off=fr.data_off)
+                    ref = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=burst,
+                                          spec_state=st)
+                    o = ccl.alloc_outputs(part.n, 64, device=gpu, meta=True)
+                    ccl.classify(part, N.CNDP_MODE_CNET, out=o)
+                    torch.cuda.synchronize()
+                    assert_same(o, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_scan=0)
+
+
 def test_cnet_speculation_many_signatures(cnet, gpu):
     """Fuzz frames give ~21 distinct ptype signatures: more than the 8-entry
     maps hold, so the scans run 64-entry maps; the forced sequential walk
