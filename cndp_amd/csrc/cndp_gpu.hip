@@ -1188,7 +1188,7 @@ __device__ __forceinline__ uint32_t rx_meta(const Lens &ln, uint32_t w0, uint32_
 }
 
 // lib/cnet/ptype/ptype.c:32-46 (indexed by ptype & 0xffff)
-__device__ __forceinline__ uint32_t cnet_edge(uint32_t pt)
+__host__ __device__ __forceinline__ constexpr uint32_t cnet_edge(uint32_t pt)
 {
     // branch-free: bitwise ORs of the compares, selects (it runs in the
     // speculation walks once per group)
@@ -1204,21 +1204,35 @@ __device__ __forceinline__ uint32_t spec_sig(uint32_t l) { return ((l & 0xffu) <
 
 // low bytes shared by types of different p_nxt (the others all go to pkt_drop)
 #define SPEC_LOWS 7
-__device__ __forceinline__ uint32_t spec_lowslot(uint32_t low)
+__host__ __device__ __forceinline__ constexpr uint32_t spec_lowslot(uint32_t low)
 {
     return low == 0x03u ? 0u : low == 0x11u ? 1u : low == 0x31u ? 2u : low == 0x91u ? 3u
          : low == 0x41u ? 4u : low == 0xc1u ? 5u : low == 0xe1u ? 6u : SPEC_LOWS;
 }
 
-// cnet_edge / spec_lowslot by low byte, an LDS table of 256 words filled by
-// the kernel: bits 3h..3h+2 = p_nxt of type H[h] << 8 | low for H = {0x00,
-// 0x01, 0x02, 0x82} (every other high byte goes to pkt_drop), bits 12..14 =
-// spec_lowslot(low).  One LDS read + ~8 ops instead of the compare chains.
+// cnet_edge / spec_lowslot by low byte, a table of 256 words (built at
+// compile time, copied to LDS by the kernels that use it): bits 3h..3h+2 =
+// p_nxt of type H[h] << 8 | low for H = {0x00, 0x01, 0x02, 0x82} (every other
+// high byte goes to pkt_drop), bits 12..14 = spec_lowslot(low).  One LDS read
+// + ~8 ops instead of the compare chains.
+struct CnetLut {
+    uint32_t v[256];
+};
+constexpr CnetLut make_cnet_lut()
+{
+    CnetLut t{};
+    for (uint32_t k = 0; k < 256; k++)
+        t.v[k] = cnet_edge(k) | (cnet_edge(0x100u | k) << 3) | (cnet_edge(0x200u | k) << 6) |
+                 (cnet_edge(0x8200u | k) << 9) | (spec_lowslot(k) << 12);
+    return t;
+}
+__constant__ CnetLut g_cnet_lut = make_cnet_lut();
+static_assert(make_cnet_lut().v[0x11] == (0u | 3u << 3 | 3u << 6 | 5u << 9 | 1u << 12), "cnet LUT");
+static_assert(make_cnet_lut().v[0x03] == (2u | 0u << 12), "cnet LUT");
 __device__ __forceinline__ void cnet_lut_fill(uint32_t *lut, uint32_t tid, uint32_t nthr)
 {
     for (uint32_t k = tid; k < 256; k += nthr)
-        lut[k] = cnet_edge(k) | (cnet_edge(0x100u | k) << 3) | (cnet_edge(0x200u | k) << 6) |
-                 (cnet_edge(0x8200u | k) << 9) | (spec_lowslot(k) << 12);
+        lut[k] = g_cnet_lut.v[k];
 }
 __device__ __forceinline__ uint32_t cnet_edge_v(uint32_t v, uint32_t l) // v = lut[l & 0xff]
 {
@@ -2709,7 +2723,7 @@ __device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carr
             if (t > 0)
                 st = spec_apply_t(row - (KF + 1), st);
             if (k0 < nblk)
-                Sblk[k0] = st & 0xffffu;
+                Sblk[k0] = st; // tagged: the consumers index P rows with it
         }
         __syncthreads();
         if (t == 0) { // carry = carry then this window's total
@@ -2760,6 +2774,17 @@ __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint3
     }
 }
 
+// the plain state entering burst / chunk j of a scan block: the block's
+// tagged start state sb, then the block's earlier items (inclusive prefix of
+// item j - 1, kf-word rows of P)
+__device__ __forceinline__ uint32_t spec_enter(const uint32_t *P, uint64_t j, uint32_t kf, uint32_t sb)
+{
+    if (j % SPEC_BLK == 0)
+        return sb & 0xffffu;
+    const uint32_t nx = P[(j - 1) * kf + (sb >> 16)];
+    return (nx == SPEC_UNCH ? sb : nx) & 0xffffu;
+}
+
 __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
 {
     const uint32_t own = cnet_edge(own_l);
@@ -2799,7 +2824,7 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
         s0 = S[b];
     } else { // block start state through the block's earlier bursts (exclusive prefix)
         const uint64_t blk = b / SPEC_BLK;
-        s0 = b % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (b - 1) * spec_kf(meta[0], kfast), class_id, Sblk[blk]);
+        s0 = spec_enter(P, b, spec_kf(meta[0], kfast), Sblk[blk]);
     }
     uint32_t low = s0 & 0xffu, E = cnet_edge(s0);
     uint8_t *sq = s_q[wv];
@@ -3030,14 +3055,10 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
                                                     uint32_t kfast, uint32_t kmax)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
-    __shared__ uint32_t s_lut[256];
+    __shared__ uint32_t s_lut[4][256]; // per wave: filled only by the waves that replay
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    if (meta[SPEC_SKIP]) // block-uniform: before the barrier
-        return;
-    cnet_lut_fill(s_lut, threadIdx.x, 256);
-    __syncthreads();
-    if (c >= nch)
+    if (c >= nch || meta[SPEC_SKIP])
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
@@ -3046,7 +3067,7 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
         s0 = S[c0];
     } else { // chunk start state: the block's start, then the block's earlier chunks
         const uint64_t blk = c / SPEC_BLK;
-        s0 = c % SPEC_BLK == 0 ? Sblk[blk] : spec_apply(P + (c - 1) * spec_kf(meta[0], kfast), class_id, Sblk[blk]);
+        s0 = spec_enter(P, c, spec_kf(meta[0], kfast), Sblk[blk]);
     }
     if (meta[0] <= SPEC_KMAX) { // k_spec_ctables wrote the chunk's summary
         const uint32_t sm = T[nch * SPEC_KMAX + c], q0 = spec_lowslot(s0 & 0xffu);
@@ -3054,7 +3075,9 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
         if (!(sm >> 31) && (!(slot & 8u) || (slot & 7u) == cnet_edge(s0)))
             return; // no frame of this chunk can leave by another edge
     }
-    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
+    cnet_lut_fill(s_lut[wv], lane, 64);
+    __builtin_amdgcn_wave_barrier();
+    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut[wv]);
     for (uint64_t bb = c0; bb < c1; bb++) {
         const uint32_t *sb = st + (bb - c0) * spec_bstride(B);
         const uint64_t b0 = bb * B;
