@@ -2988,12 +2988,14 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
     __shared__ uint32_t s_lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     const uint32_t K = meta[0];
     if (K > SPEC_KMAX || meta[SPEC_SKIP]) // block-uniform: before the barrier
         return;
     cnet_lut_fill(s_lut, threadIdx.x, 256);
+    spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
     __syncthreads();
     if (c >= nch)
         return;
@@ -3021,7 +3023,9 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
             spec_walk(sb, 0, ng, low, E, mp);
         }
         // cm = this burst after the chunk so far (tagged states)
-        mp = lane < K ? spec_tag(mp, class_id) : SPEC_UNCH;
+        // tag with the class (LDS tables, not two dependent global loads)
+        mp = lane < K && mp != SPEC_UNCH ? mp | ((uint32_t)s_cls[((mp & 0xffu) << 3) | cnet_edge_l(s_lut, mp)] << 16)
+                                          : SPEC_UNCH;
         const uint32_t nx = __shfl(mp, (int)(cm == SPEC_UNCH ? 0u : cm >> 16));
         cm = cm == SPEC_UNCH ? mp : nx == SPEC_UNCH ? cm : nx;
     }

@@ -43,5 +43,7 @@ if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
         -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-parity --no-e2e --no-imix
     step prof_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run \
         -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-parity --no-e2e --no-imix
+    # keep only this library's kernels (gpurun returns at most 64 MiB)
+    python3 tools/pmc_filter.py $(find $OUT/prof_fetch $OUT/prof_write -name '*counter_collection.csv')
 fi
 echo done
