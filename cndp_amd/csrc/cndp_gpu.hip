@@ -2070,7 +2070,7 @@ struct CdLane {
     uint32_t d0, d1, d2, d3; // v6 destination words, or dip in d0 (v4)
 };
 
-template <bool LNT, int P>
+template <bool LNT, bool META, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
                                         CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
@@ -2164,7 +2164,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const uint32_t pe = (proto == 6u) | (udp & !gtpc) ? (gtpu ? 5u : f4 ? 3u : 4u) : 0u;
         const bool l4ok = proto == 6u || proto == 17u;
         Lens lens{14u, f4 ? 20u : 40u, 0u};
-        if (a.rxmeta) { // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
+        if (META && a.rxmeta) { // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
             lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
                     : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
                          : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
@@ -2248,9 +2248,9 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         }
         if (bf) {
             const uint32_t q = s_reta[sb.h & a.reta_mask];
-            if (a.ptype)
+            if (META && a.ptype)
                 a.ptype[ib] = pt;
-            if (a.rxmeta)
+            if (META && a.rxmeta)
                 a.rxmeta[ib] = sb.rx;
             if (a.nh)
                 a.nh[ib] = nh;
@@ -2270,7 +2270,9 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     off.o2 = off.o3;
 }
 
-template <bool LNT>
+// META: ptype / rxmeta outputs requested (without them the kernel keeps
+// 14 VGPRs and 18 spilled SGPRs fewer)
+template <bool LNT, bool META>
 __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
@@ -2320,10 +2322,10 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     uint32_t last_sig = 0xFFFFFFFFu;
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {
-        cd_trip<LNT, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
+        cd_trip<LNT, META, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
                         last_sig);
         if (jt + 1 < trips)
-            cd_trip<LNT, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
+            cd_trip<LNT, META, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
                             count, last_sig);
     }
     if (count || a.spec_flags)
@@ -3970,12 +3972,13 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                 const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 2u;
                 if (gd > (uint64_t)c->num_cu * bpc)
                     gd = (uint64_t)c->num_cu * bpc;
-                if (c->tune_lnt)
-                    hipLaunchKernelGGL(k_cnet_defer<true>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a,
-                                       (uint32_t)n_tiles);
-                else
-                    hipLaunchKernelGGL(k_cnet_defer<false>, dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a,
-                                       (uint32_t)n_tiles);
+                static void (*const dfns[2][2])(KArgs, uint32_t) = {{k_cnet_defer<false, false>,
+                                                                     k_cnet_defer<false, true>},
+                                                                    {k_cnet_defer<true, false>,
+                                                                     k_cnet_defer<true, true>}};
+                const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
+                hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
+                                   0, s, a, (uint32_t)n_tiles);
             } else {
                 uint64_t gt = (n_tiles + CS_WAVES - 1) / CS_WAVES;
                 const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 5u;
