@@ -2371,6 +2371,8 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 // last SPEC_TAIL bursts; found, it stores the final state and sets
 // meta[SPEC_SKIP], and the table / scan / replay passes return at once.
 #define SPEC_SKIP 129
+#define SPEC_FULL 130 // k_spec_local left a chunk unresolved: run the full passes
+#define SPEC_IN 131   // the node state entering this batch (meta[-1] becomes the final one)
 #define SPEC_TAIL 16
 __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t &cur)
 {
@@ -2385,7 +2387,11 @@ __global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint
                                                      uint64_t nb, uint32_t allow_skip)
 {
     const uint32_t t = threadIdx.x;
-    const uint32_t g0 = spec_sig(meta[-1] & 0xffffu); // the node state entering the batch
+    const uint32_t s_in = meta[-1] & 0xffffu, g0 = spec_sig(s_in); // the node state entering the batch
+    if (t == 0) {
+        meta[SPEC_IN] = s_in;
+        meta[SPEC_FULL] = 0;
+    }
     const uint32_t w = flags[t] | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
     uint32_t pre = cnt; // inclusive wave prefix
     for (int o = 1; o < 64; o <<= 1) {
@@ -2664,11 +2670,11 @@ __device__ __forceinline__ void spec_scan_a_body(uint32_t *s_m, uint64_t nb, uin
 }
 
 __global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint32_t *T,
-                                                        uint32_t *P, uint32_t *Bt, uint32_t kfast)
+                                                        uint32_t *P, uint32_t *Bt, uint32_t kfast, uint32_t gated)
 {
     __shared__ uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
     const uint32_t K = meta[0];
-    if (meta[SPEC_SKIP])
+    if (meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL]))
         return;
     if (K <= kfast)
         spec_scan_a_body<SPEC_KFAST>(s_m, nb, K, T, P, Bt);
@@ -2689,7 +2695,7 @@ __device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carr
     uint32_t *row = s_m + t * (KF + 1);
     if (t < KF)
         s_carry[t] = SPEC_UNCH;
-    const uint32_t s0 = spec_tag(*state & 0xffffu, class_id);
+    const uint32_t s0 = spec_tag(state[SPEC_IN + 1] & 0xffffu, class_id); // state = meta - 1
     __syncthreads();
     for (uint64_t w0 = 0; w0 < nblk; w0 += W) {
         const uint64_t k0 = w0 + t;
@@ -2750,20 +2756,21 @@ __device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carr
 __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
                                                      const uint32_t *Bt, uint32_t *Sblk, uint32_t *state,
                                                      const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, uint32_t *S, uint32_t kfast, uint32_t kmax)
+                                                     uint64_t nb, uint32_t *S, uint32_t kfast, uint32_t kmax,
+                                                     uint32_t gated)
 {
     __shared__ uint32_t s_m[1024 * (SPEC_KFAST + 1) > 256 * (SPEC_KMAX + 1) ? 1024 * (SPEC_KFAST + 1)
                                                                              : 256 * (SPEC_KMAX + 1)];
     __shared__ uint32_t s_carry[SPEC_KMAX];
     const uint32_t K = meta[0];
-    if (meta[SPEC_SKIP])
+    if (meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL]))
         return;
     if (K <= kfast) {
         spec_scan_c_body<SPEC_KFAST, 1024>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
     } else if (K <= kmax) {
         spec_scan_c_body<SPEC_KMAX, 256>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
     } else if (threadIdx.x == 0) {
-        uint32_t st = *state & 0xffffu;
+        uint32_t st = meta[SPEC_IN] & 0xffffu;
         for (uint64_t b = 0; b < nb; b++) {
             S[b] = st;
             const uint64_t b0 = b * B;
@@ -2983,10 +2990,42 @@ __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *_
     return em;
 }
 
+// Edge-consistency summary of a chunk (em OR-reduced over the wave).  Only
+// the low bytes in spec_lowslot() carry types of different p_nxt
+// (ptype.c:32-46; every other type goes to pkt_drop), so per slot the chunk
+// records which edges its frames have: slot r = bit 3 present, bits 0..2 its
+// edge; bit 31 = a slot with two edges.  A chunk where each slot has at most
+// one edge cannot re-route a frame unless the entering state disagrees.
+__device__ __forceinline__ uint32_t spec_summary(unsigned long long em)
+{
+    for (int o = 32; o > 0; o >>= 1)
+        em |= __shfl_xor(em, o);
+    uint32_t sm = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < SPEC_LOWS; r++) {
+        const uint32_t v = (uint32_t)(em >> (6 * r)) & 0x3fu;
+        if (v & (v - 1u))
+            sm |= 1u << 31;
+        else if (v)
+            sm |= (8u | (31u - (uint32_t)__clz(v))) << (4 * r);
+    }
+    return sm;
+}
+
+// true when no frame of a chunk with summary sm can leave by another edge
+// from the entering state s0
+__device__ __forceinline__ bool spec_chunk_quiet(uint32_t sm, uint32_t s0)
+{
+    const uint32_t q0 = spec_lowslot(s0 & 0xffu);
+    const uint32_t slot = q0 < SPEC_LOWS ? (sm >> (4 * q0)) & 0xfu : 0u;
+    return !(sm >> 31) && (!(slot & 8u) || (slot & 7u) == cnet_edge(s0));
+}
+
+// gated: run only when k_spec_local left a chunk unresolved (meta[SPEC_FULL])
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
                                                       uint64_t nb, uint64_t nch, const uint32_t *meta,
-                                                      const uint8_t *class_id, uint32_t *T)
+                                                      const uint8_t *class_id, uint32_t *T, uint32_t gated)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
     __shared__ uint32_t s_lut[256];
@@ -2994,7 +3033,7 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     const uint32_t K = meta[0];
-    if (K > SPEC_KMAX || meta[SPEC_SKIP]) // block-uniform: before the barrier
+    if (K > SPEC_KMAX || meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL])) // block-uniform: before the barrier
         return;
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
@@ -3033,38 +3072,27 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
     }
     if (lane < K)
         T[c * SPEC_KMAX + lane] = cm;
-    // edge-consistency summary for k_spec_cemit.  Only the low bytes in
-    // spec_lowslot() carry types of different p_nxt (ptype.c:32-46; every
-    // other type goes to pkt_drop), so per slot the chunk records which
-    // edges its frames have.  A chunk where each slot has at most one edge
-    // cannot re-route a frame unless the entering state disagrees with it.
-    for (int o = 32; o > 0; o >>= 1)
-        em |= __shfl_xor(em, o);
-    uint32_t sm = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < SPEC_LOWS; r++) {
-        const uint32_t v = (uint32_t)(em >> (6 * r)) & 0x3fu;
-        // slot r: bit 3 = present, bits 0..2 = its edge; bit 31 = two edges
-        if (v & (v - 1u))
-            sm |= 1u << 31;
-        else if (v)
-            sm |= (8u | (31u - (uint32_t)__clz(v))) << (4 * r);
-    }
+    const uint32_t sm = spec_summary(em);
     if (lane == 0)
         T[nch * SPEC_KMAX + c] = sm;
 }
 
 template <int CH>
+__device__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
+                            const uint32_t *st);
+
+template <int CH>
 __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_t nb, uint64_t nch,
                                                     const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
                                                     const uint32_t *Sblk, const uint32_t *S, const uint32_t *T,
-                                                    uint32_t kfast, uint32_t kmax)
+                                                    uint32_t kfast, uint32_t kmax, const uint8_t *done)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
     __shared__ uint32_t s_lut[4][256]; // per wave: filled only by the waves that replay
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    if (c >= nch || meta[SPEC_SKIP])
+    // done != nullptr: k_spec_local ran first; only the chunks it left unresolved
+    if (c >= nch || meta[SPEC_SKIP] || (done && (!meta[SPEC_FULL] || done[c])))
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
@@ -3075,15 +3103,22 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
         const uint64_t blk = c / SPEC_BLK;
         s0 = spec_enter(P, c, spec_kf(meta[0], kfast), Sblk[blk]);
     }
-    if (meta[0] <= SPEC_KMAX) { // k_spec_ctables wrote the chunk's summary
-        const uint32_t sm = T[nch * SPEC_KMAX + c], q0 = spec_lowslot(s0 & 0xffu);
-        const uint32_t slot = q0 < SPEC_LOWS ? (sm >> (4 * q0)) & 0xfu : 0u;
-        if (!(sm >> 31) && (!(slot & 8u) || (slot & 7u) == cnet_edge(s0)))
-            return; // no frame of this chunk can leave by another edge
-    }
+    // k_spec_ctables wrote the chunk's summary
+    if (meta[0] <= SPEC_KMAX && spec_chunk_quiet(T[nch * SPEC_KMAX + c], s0))
+        return; // no frame of this chunk can leave by another edge
     cnet_lut_fill(s_lut[wv], lane, 64);
     __builtin_amdgcn_wave_barrier();
     spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut[wv]);
+    spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+}
+
+// replay the staged chunk [c0, c1) from its entering state s0: lane g finds
+// the state entering group g, fixes the group's frames if it is quiet under
+// that state, and lane ng-1 hands the burst's exit state to the next burst
+template <int CH>
+__device__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
+                            const uint32_t *st)
+{
     for (uint64_t bb = c0; bb < c1; bb++) {
         const uint32_t *sb = st + (bb - c0) * spec_bstride(B);
         const uint64_t b0 = bb * B;
@@ -3126,6 +3161,119 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
         }
         s0 = ng ? __shfl(nxt, (int)ng - 1) : s0;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Local resolution (bursts <= 256, the default): the state entering chunk c
+// is the walk from the last universal group before it, and for IMIX-like
+// traffic one sits in the previous chunk's last burst.  k_spec_local finds it
+// there, stages chunk c and replays it when its summary says a frame could
+// leave by another edge; the last chunk's wave also walks the final state.  A
+// chunk whose previous chunk holds no universal group (long single-type runs)
+// is left to the table / scan / replay passes, which run only then
+// (meta[SPEC_FULL]) and replay only the chunks left (done[c] == 0).
+// ---------------------------------------------------------------------------
+// group `lane` of the burst at packet b0 (cnt packets) as two words
+__device__ __forceinline__ void spec_group_regs(const uint16_t *__restrict__ pt, uint64_t b0, uint32_t cnt,
+                                                uint32_t lane, uint32_t &q0, uint32_t &q1)
+{
+    q0 = q1 = 0;
+    if (4 * lane + 4 <= cnt) {
+        if ((b0 & 3u) == 0) {
+            const u32x2 v = *(const u32x2 *)(pt + b0 + 4 * lane);
+            q0 = v.x;
+            q1 = v.y;
+        } else {
+            const uint16_t *g = pt + b0 + 4 * lane;
+            q0 = (uint32_t)g[0] | ((uint32_t)g[1] << 16);
+            q1 = (uint32_t)g[2] | ((uint32_t)g[3] << 16);
+        }
+    }
+}
+
+// walk groups [g0, ng) of a burst held one group per lane (ptype.c:95-130)
+__device__ __forceinline__ void spec_walk_regs(uint32_t q0, uint32_t q1, uint32_t g0, uint32_t ng,
+                                               const uint32_t *lut, uint32_t &cur)
+{
+    for (uint32_t g = g0; g < ng; g++) {
+        const uint32_t a0 = __shfl(q0, (int)g), a1 = __shfl(q1, (int)g);
+        const uint32_t l0 = a0 & 0xffffu, l1 = a0 >> 16, l2 = a1 & 0xffffu, l3 = a1 >> 16;
+        const uint32_t low = cur & 0xffu;
+        const bool quiet =
+            (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low && (l3 & 0xffu) == low;
+        if (!quiet && (l2 == l3 || cnet_edge_l(lut, cur) == cnet_edge_l(lut, l3)))
+            cur = l3;
+    }
+}
+
+// the node state after bursts [b_lo, b_hi): the walk from the last universal
+// group in them to their end; false when they hold none
+__device__ bool spec_lookback(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t b_lo, uint64_t b_hi,
+                              uint32_t lane, const uint32_t *lut, uint32_t &s_out)
+{
+    for (uint64_t j = b_hi; j-- > b_lo;) {
+        const uint64_t b0 = j * B;
+        const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B), ng = cnt >> 2;
+        uint32_t q0, q1;
+        spec_group_regs(pt, b0, cnt, lane, q0, q1);
+        const uint32_t v = q0 & 0xffu;
+        const bool allq = ((q0 >> 16) & 0xffu) == v && (q1 & 0xffu) == v && ((q1 >> 16) & 0xffu) == v;
+        const unsigned long long U = __ballot(lane < ng && !allq && (q1 & 0xffffu) == (q1 >> 16));
+        if (U) {
+            const uint32_t u = 63u - (uint32_t)__clzll(U);
+            uint32_t cur = __shfl(q1, (int)u) >> 16;
+            spec_walk_regs(q0, q1, u + 1, ng, lut, cur);
+            for (uint64_t k = j + 1; k < b_hi; k++) {
+                const uint64_t k0 = k * B;
+                const uint32_t kc = (uint32_t)((uint64_t)n - k0 < B ? (uint64_t)n - k0 : B);
+                spec_group_regs(pt, k0, kc, lane, q0, q1);
+                spec_walk_regs(q0, q1, 0, kc >> 2, lut, cur);
+            }
+            s_out = cur;
+            return true;
+        }
+    }
+    return false;
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+                                                    uint8_t *done)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
+    __shared__ uint32_t s_lut[256];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if (meta[SPEC_SKIP]) // block-uniform: before the barrier
+        return;
+    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    __syncthreads();
+    if (c >= nch)
+        return;
+    const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+    if (c == nch - 1) { // the final node state (meta[-1]; the entering one is meta[SPEC_IN])
+        uint32_t sf = 0;
+        if (spec_lookback(a.spec_t16, a.n, B, c0, c1, lane, s_lut, sf)) {
+            if (lane == 0)
+                meta[-1] = sf;
+        } else if (lane == 0) {
+            atomicOr(&meta[SPEC_FULL], 1u);
+        }
+    }
+    uint32_t s0 = meta[SPEC_IN] & 0xffffu;
+    if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0)) {
+        if (lane == 0) {
+            done[c] = 0;
+            atomicOr(&meta[SPEC_FULL], 1u);
+        }
+        return;
+    }
+    uint32_t *st = s_pt[wv];
+    const unsigned long long em = spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
+    if (!spec_chunk_quiet(spec_summary(em), s0))
+        spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+    if (lane == 0)
+        done[c] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -3332,6 +3480,7 @@ struct cndp_gpu_ctx {
     uint64_t cs_wl_cap;
     uint8_t *sp_class;    // class id per signature (2048)
     uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U; // sp_pt: the u16 types (speculation model)
+    uint8_t *sp_done;     // per chunk: resolved by k_spec_local
     uint64_t sp_n_cap, sp_b_cap;
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
     hipStream_t hs[3];    // copy-in, classify, copy-out
@@ -3475,7 +3624,7 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         hipFree(c->m_dres);
     if (c->d_rw_tbl)
         hipFree(c->d_rw_tbl);
-    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt, c->sp_nh, c->sp_S, c->sp_T, c->sp_U};
+    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt, c->sp_nh, c->sp_S, c->sp_T, c->sp_U, c->sp_done};
     for (void *q : sp)
         if (q)
             hipFree(q);
@@ -3875,10 +4024,14 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
             HIP_TRY(hipFree(c->sp_T));
         if (c->sp_U)
             HIP_TRY(hipFree(c->sp_U));
+        if (c->sp_done)
+            HIP_TRY(hipFree(c->sp_done));
         c->sp_S = c->sp_T = c->sp_U = nullptr;
+        c->sp_done = nullptr;
         c->sp_b_cap = 0;
         const uint64_t cap = nb + (nb >> 3) + 64;
         HIP_TRY(hipMalloc((void **)&c->sp_S, cap * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_done, cap));
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
         // inclusive burst prefixes + block totals + block start states
         HIP_TRY(hipMalloc((void **)&c->sp_U, (cap * SPEC_KMAX + (cap / SPEC_BLK + 2) * (SPEC_KMAX + 1)) * 4));
@@ -4017,28 +4170,35 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                 const uint32_t gc = (uint32_t)((nch + 3) / 4);
                 auto ct = k_spec_ctables<SPEC_CH>;
                 auto ce = k_spec_cemit<SPEC_CH>;
+                // auto mode: the local pass first, the full passes only for what it leaves
+                const uint32_t gated = c->tune_spec_scan == 0 ? 1u : 0u;
+                if (gated) {
+                    auto lo = k_spec_local<SPEC_CH>;
+                    hipLaunchKernelGGL(lo, dim3(gc), dim3(256), 0, s, a, B, nb, nch, meta, c->sp_done);
+                }
                 hipLaunchKernelGGL(ct, dim3(gc), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B, nb, nch,
-                                   (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
+                                   (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T, gated);
                 const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
                 uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
                 hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nch,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast);
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast, gated);
                 hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
-                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax);
+                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax, gated);
                 hipLaunchKernelGGL(ce, dim3(gc), dim3(256), 0, s, a, B, nb, nch, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
-                                   (const uint32_t *)c->sp_S, (const uint32_t *)c->sp_T, kfast, kmax);
+                                   (const uint32_t *)c->sp_S, (const uint32_t *)c->sp_T, kfast, kmax,
+                                   gated ? (const uint8_t *)c->sp_done : (const uint8_t *)nullptr);
             } else {
                 hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
                 const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
                 uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
                 hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast);
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast, 0u);
                 hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
-                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax);
+                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax, 0u);
                 hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, kfast, kmax,
                                    (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
                                    (const uint32_t *)Sblk, (const uint32_t *)c->sp_S);

@@ -678,6 +678,32 @@ def test_cnet_speculation_batch_shortcut(cnet, gpu, burst):
         ccl.set_tuning(cnet_spec=256, spec_scan=0)
 
 
+def test_cnet_speculation_local_and_full(cnet, gpu):
+    """The local pass resolves a chunk from the last universal group of the
+    chunk before it; chunks behind single-type runs (no universal group) are
+    left to the table / scan / replay passes.  A GTP mix with two such runs
+    (frames aliased to one plain IPv4 UDP frame) takes both in one call."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = _gtp_mix(40000, routes, v6, gpu, seed=31)
+    plain = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)
+    pick = int(np.flatnonzero(plain["ptype"] == 0x0211)[0])
+    off = fr.offsets.clone()
+    for lo, hi in ((8192, 8192 + 3 * 1024), (20480, 20480 + 2 * 1024 + 100)):
+        off[lo:hi] = off[pick]
+    fr = pktgen.Frames(fr.slab, fr.n, offsets=off)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=256)
+    assert (plain["edge"] != ref["edge"]).sum() > 0, "input does not exercise the quirk"
+    try:
+        for scan in (0, 1):
+            ccl.set_tuning(cnet_spec=256, spec_scan=scan)
+            out = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+            ccl.classify(fr, N.CNDP_MODE_CNET, out=out)
+            torch.cuda.synchronize()
+            assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_scan=0)
+
+
 def test_cnet_speculation_many_signatures(cnet, gpu):
     """Fuzz frames give ~21 distinct ptype signatures: more than the 8-entry
     maps hold, so the scans run 64-entry maps; the forced sequential walk
