@@ -2911,7 +2911,9 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
 //                   the group is quiet under it, and lane ng-1 hands the
 //                   burst's exit state to the next burst.
 // ---------------------------------------------------------------------------
+#ifndef SPEC_CH // build-time override for A/B builds
 #define SPEC_CH 4 // measured: 4 beats 1 and 16 (occupancy vs per-wave latency)
+#endif
 
 // stage the types of bursts [c0, c1) as type | p_nxt << 16, burst j at
 // st + (j - c0) * spec_bstride(B) (16-B aligned groups for any B)
