@@ -326,6 +326,46 @@ def test_full_size_c3_16M(l3, gpu):
     assert int(ref["bins"].sum()) == 1 << 24
 
 
+@pytest.mark.slow
+def test_full_size_c4_16M(cnet, gpu):
+    """BASELINE C4 per-GPU batch at full size (16M IMIX frames, ~6 GB of
+    slots), default cnet path with the speculation model, bit-exact against
+    the C oracle's node loop."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = pktgen.imix(1 << 24, v4routes=routes, v6routes=v6, device=gpu)
+    got = run_gpu(ccl, fr, N.CNDP_MODE_CNET)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6)
+    assert_same(got, ref)
+    assert int(ref["bins"].sum()) == 1 << 24
+
+
+@pytest.mark.slow
+def test_full_size_c5_sampled(cnet, gpu):
+    """BASELINE C5 per-GPU shard at full size: 32M x 1536-B frames (48 GiB
+    in HBM), 1/1024 with a corrupted IPv4 checksum.  Per-frame routing
+    (speculation model off): every 97th frame is checked bit-exact against
+    the oracle run over a gathered copy of those frames, and the whole batch
+    through its counts (every frame in exactly one bin)."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    n = 1 << 25
+    fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, device=gpu)
+    bad = pktgen.corrupt_cksum(fr, 1024)
+    assert bad > n // 2048
+    try:
+        ccl.set_tuning(cnet_spec=0)
+        out = ccl.classify(fr, N.CNDP_MODE_CNET, n_bins=64)
+        torch.cuda.synchronize()
+        assert int(out["bins"].sum()) == n
+        idx = torch.arange(0, n, 97, device=gpu)
+        sample = fr.slab.view(n, 1536)[idx].reshape(-1).contiguous()
+        sfr = pktgen.Frames(sample, idx.numel(), stride=1536)
+        ref = oracle_classify(O.MODE_CNET, sfr, tables4=ct4, tables6=ct6, spec_burst=0)
+        sub = {k: (v[idx] if torch.is_tensor(v) and v.dim() == 1 and v.numel() == n else v) for k, v in out.items()}
+        assert_same(sub, ref, keys=("nh", "hash", "queue", "edge"))
+    finally:
+        ccl.set_tuning(cnet_spec=256)
+
+
 @pytest.mark.parametrize("mode", [N.CNDP_MODE_L3FWD, N.CNDP_MODE_HASH])
 def test_tuning_variants_identical(l3, gpu, mode):
     """Every kernel variant (nt / unroll / grid) produces the same bits."""
