@@ -1210,40 +1210,45 @@ __host__ __device__ __forceinline__ constexpr uint32_t spec_lowslot(uint32_t low
          : low == 0x41u ? 4u : low == 0xc1u ? 5u : low == 0xe1u ? 6u : SPEC_LOWS;
 }
 
-// cnet_edge / spec_lowslot by low byte, a table of 256 words (built at
-// compile time, copied to LDS by the kernels that use it): bits 3h..3h+2 =
-// p_nxt of type H[h] << 8 | low for H = {0x00, 0x01, 0x02, 0x82} (every other
-// high byte goes to pkt_drop), bits 12..14 = spec_lowslot(low).  One LDS read
-// + ~8 ops instead of the compare chains.
-struct CnetLut {
-    uint32_t v[256];
+// cnet_edge and the speculation summary bit of a type, by (high-byte class
+// hi, low byte): a 5 x 256 table of u16 built at compile time and copied to
+// LDS by the kernels that use it.  hi = 0..3 for high bytes 0x00, 0x01,
+// 0x02, 0x82 (the only ones any p_nxt entry other than pkt_drop has,
+// ptype.c:32-46), 4 for every other.  Entry = p_nxt << 6 | em bit, the em
+// bit being 6 * spec_lowslot(low) + p_nxt, or 63 (masked off) outside the
+// slots.  One LDS read + ~6 ops instead of the compare chains.
+#define CNET_LUT_N (5 * 256)
+struct alignas(16) CnetLut {
+    uint16_t v[CNET_LUT_N];
 };
 constexpr CnetLut make_cnet_lut()
 {
     CnetLut t{};
-    for (uint32_t k = 0; k < 256; k++)
-        t.v[k] = cnet_edge(k) | (cnet_edge(0x100u | k) << 3) | (cnet_edge(0x200u | k) << 6) |
-                 (cnet_edge(0x8200u | k) << 9) | (spec_lowslot(k) << 12);
+    for (uint32_t hi = 0; hi < 5; hi++)
+        for (uint32_t k = 0; k < 256; k++) {
+            const uint32_t hb = hi == 0 ? 0x00u : hi == 1 ? 0x01u : hi == 2 ? 0x02u : 0x82u;
+            const uint32_t e = hi < 4 ? cnet_edge((hb << 8) | k) : 0u, q = spec_lowslot(k);
+            t.v[hi * 256 + k] = (uint16_t)((e << 6) | (q < SPEC_LOWS ? 6 * q + e : 63u));
+        }
     return t;
 }
 __constant__ CnetLut g_cnet_lut = make_cnet_lut();
-static_assert(make_cnet_lut().v[0x11] == (0u | 3u << 3 | 3u << 6 | 5u << 9 | 1u << 12), "cnet LUT");
-static_assert(make_cnet_lut().v[0x03] == (2u | 0u << 12), "cnet LUT");
-__device__ __forceinline__ void cnet_lut_fill(uint32_t *lut, uint32_t tid, uint32_t nthr)
+static_assert(make_cnet_lut().v[2 * 256 + 0x11] == (3u << 6 | 9u), "cnet LUT");
+static_assert(make_cnet_lut().v[3 * 256 + 0x41] == (5u << 6 | 29u), "cnet LUT");
+static_assert(make_cnet_lut().v[0 * 256 + 0x03] == (2u << 6 | 2u), "cnet LUT");
+static_assert(make_cnet_lut().v[4 * 256 + 0x55] == 63u, "cnet LUT");
+__device__ __forceinline__ void cnet_lut_fill(uint16_t *lut, uint32_t tid, uint32_t nthr)
 {
-    for (uint32_t k = tid; k < 256; k += nthr)
-        lut[k] = g_cnet_lut.v[k];
+    for (uint32_t k = tid; k < CNET_LUT_N / 2; k += nthr) // two entries per 4-B copy
+        ((uint32_t *)lut)[k] = ((const uint32_t *)g_cnet_lut.v)[k];
 }
-__device__ __forceinline__ uint32_t cnet_edge_v(uint32_t v, uint32_t l) // v = lut[l & 0xff]
+__device__ __forceinline__ uint32_t cnet_lut_x(const uint16_t *lut, uint32_t l)
 {
     const uint32_t h = (l >> 8) & 0xffu;
-    const uint32_t hi = h < 3u ? h : h == 0x82u ? 3u : 4u; // 4: bits 12.. masked off
-    return ((v & 0xfffu) >> (3u * hi)) & 7u;
+    const uint32_t hi = h < 3u ? h : h == 0x82u ? 3u : 4u;
+    return lut[hi * 256u + (l & 0xffu)];
 }
-__device__ __forceinline__ uint32_t cnet_edge_l(const uint32_t *lut, uint32_t l)
-{
-    return cnet_edge_v(lut[l & 0xffu], l);
-}
+__device__ __forceinline__ uint32_t cnet_edge_l(const uint16_t *lut, uint32_t l) { return cnet_lut_x(lut, l) >> 6; }
 
 // Burst / chunk maps store their target states tagged with the target's
 // signature class (state | class << 16; SPEC_UNCH = keep the state), so map
@@ -2926,17 +2931,10 @@ __device__ __forceinline__ unsigned long long spec_em(uint32_t l, uint32_t e)
     return q < SPEC_LOWS ? 1ull << (6 * q + e) : 0ull;
 }
 
-// em bit of a type from its LUT word v and edge e
-__device__ __forceinline__ unsigned long long spec_em_v(uint32_t v, uint32_t e)
-{
-    const uint32_t q = (v >> 12) & 7u;
-    return q < SPEC_LOWS ? 1ull << (6 * q + e) : 0ull;
-}
-
 template <int CH>
 __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *__restrict__ pt, uint32_t n,
                                                                uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
-                                                               uint32_t *st, const uint32_t *lut)
+                                                               uint32_t *st, const uint16_t *lut)
 {
     unsigned long long em = 0;
     const uint32_t bs = spec_bstride(B);
@@ -2967,11 +2965,10 @@ __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *_
             uint32_t o[8];
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++) {
-                const uint32_t l = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu, v = lut[l & 0xffu];
-                const uint32_t e = cnet_edge_v(v, l);
-                o[q] = l | (e << 16);
+                const uint32_t l = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu, x = cnet_lut_x(lut, l);
+                o[q] = l | ((x >> 6) << 16);
                 if (idx + q < m)
-                    em |= spec_em_v(v, e);
+                    em |= 1ull << (x & 63u);
             }
             *(u32x4 *)(st + idx) = (u32x4){o[0], o[1], o[2], o[3]};
             *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
@@ -2982,14 +2979,14 @@ __device__ __forceinline__ unsigned long long spec_stage_chunk(const uint16_t *_
             const uint32_t cnt = (uint32_t)((uint64_t)n - p0 < B ? (uint64_t)n - p0 : B);
             uint32_t *d = st + (j - c0) * bs;
             for (uint32_t k = lane; k < cnt; k += 64) {
-                const uint32_t l = pt[p0 + k], v = lut[l & 0xffu], e = cnet_edge_v(v, l);
-                d[k] = l | (e << 16);
-                em |= spec_em_v(v, e);
+                const uint32_t l = pt[p0 + k], x = cnet_lut_x(lut, l);
+                d[k] = l | ((x >> 6) << 16);
+                em |= 1ull << (x & 63u);
             }
         }
     }
     __builtin_amdgcn_wave_barrier();
-    return em;
+    return em & ~(1ull << 63); // bit 63: types outside the slots
 }
 
 // Edge-consistency summary of a chunk (em OR-reduced over the wave).  Only
@@ -3030,7 +3027,7 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
                                                       const uint8_t *class_id, uint32_t *T, uint32_t gated)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
-    __shared__ uint32_t s_lut[256];
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
@@ -3090,7 +3087,7 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
                                                     uint32_t kfast, uint32_t kmax, const uint8_t *done)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
-    __shared__ uint32_t s_lut[4][256]; // per wave: filled only by the waves that replay
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[4][CNET_LUT_N]; // per wave: filled only by the waves that replay
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     // done != nullptr: k_spec_local ran first; only the chunks it left unresolved
@@ -3195,7 +3192,7 @@ __device__ __forceinline__ void spec_group_regs(const uint16_t *__restrict__ pt,
 
 // walk groups [g0, ng) of a burst held one group per lane (ptype.c:95-130)
 __device__ __forceinline__ void spec_walk_regs(uint32_t q0, uint32_t q1, uint32_t g0, uint32_t ng,
-                                               const uint32_t *lut, uint32_t &cur)
+                                               const uint16_t *lut, uint32_t &cur)
 {
     for (uint32_t g = g0; g < ng; g++) {
         const uint32_t a0 = __shfl(q0, (int)g), a1 = __shfl(q1, (int)g);
@@ -3211,7 +3208,7 @@ __device__ __forceinline__ void spec_walk_regs(uint32_t q0, uint32_t q1, uint32_
 // the node state after bursts [b_lo, b_hi): the walk from the last universal
 // group in them to their end; false when they hold none
 __device__ bool spec_lookback(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t b_lo, uint64_t b_hi,
-                              uint32_t lane, const uint32_t *lut, uint32_t &s_out)
+                              uint32_t lane, const uint16_t *lut, uint32_t &s_out)
 {
     for (uint64_t j = b_hi; j-- > b_lo;) {
         const uint64_t b0 = j * B;
@@ -3243,7 +3240,7 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
                                                     uint8_t *done)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
-    __shared__ uint32_t s_lut[256];
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (meta[SPEC_SKIP]) // block-uniform: before the barrier
