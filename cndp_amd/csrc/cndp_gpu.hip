@@ -3245,11 +3245,23 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (meta[SPEC_SKIP]) // block-uniform: before the barrier
         return;
+    const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+    // the chunk's types (16-B loads of 8) are issued first, so that they
+    // overlap the table fill and the look-back
+    constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+    const bool pre = (B & 7u) == 0 && c < nch;
+    const uint64_t p0 = c0 * B, p1 = c1 * B < a.n ? c1 * B : a.n;
+    const uint32_t m = pre ? (uint32_t)(p1 - p0) : 0u;
+    u32x4 v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+        const uint32_t idx = (r * 64u + lane) * 8u;
+        v[r] = idx + 8u <= m ? *(const u32x4 *)(a.spec_t16 + p0 + idx) : (u32x4){0, 0, 0, 0};
+    }
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     __syncthreads();
     if (c >= nch)
         return;
-    const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
     if (c == nch - 1) { // the final node state (meta[-1]; the entering one is meta[SPEC_IN])
         uint32_t sf = 0;
         if (spec_lookback(a.spec_t16, a.n, B, c0, c1, lane, s_lut, sf)) {
@@ -3268,9 +3280,34 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
         return;
     }
     uint32_t *st = s_pt[wv];
-    const unsigned long long em = spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
-    if (!spec_chunk_quiet(spec_summary(em), s0))
-        spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+    if (pre) { // summary from the registers; stage in LDS only to replay
+        unsigned long long em = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) {
+            const uint32_t idx = (r * 64u + lane) * 8u;
+            if (idx >= m)
+                continue;
+            uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            if (idx + 8u > m) // the batch's last partial vector
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint32_t lo = idx + 2 * q < m ? a.spec_t16[p0 + idx + 2 * q] : 0u;
+                    const uint32_t hi = idx + 2 * q + 1 < m ? a.spec_t16[p0 + idx + 2 * q + 1] : 0u;
+                    w[q] = lo | (hi << 16);
+                }
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                if (idx + q < m)
+                    em |= 1ull << (cnet_lut_x(s_lut, (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu) & 63u);
+        }
+        if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0)) {
+            spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
+            spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+        }
+    } else {
+        const unsigned long long em = spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
+        if (!spec_chunk_quiet(spec_summary(em), s0))
+            spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+    }
     if (lane == 0)
         done[c] = 1;
 }
