@@ -2387,9 +2387,12 @@ __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2,
         cur = l3;
 }
 
-__global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint8_t *class_id, uint32_t *meta,
+// It also clears the signature flags and the worklist count for the next
+// call (both were read before: the flags here, the count by the general
+// kernel), which saves the two per-call memsets.
+__global__ __launch_bounds__(64) void k_spec_classes(uint32_t *flags, uint8_t *class_id, uint32_t *meta,
                                                      const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, uint32_t allow_skip)
+                                                     uint64_t nb, uint32_t allow_skip, uint32_t *wl_n)
 {
     const uint32_t t = threadIdx.x;
     const uint32_t s_in = meta[-1] & 0xffffu, g0 = spec_sig(s_in); // the node state entering the batch
@@ -2398,6 +2401,9 @@ __global__ __launch_bounds__(64) void k_spec_classes(const uint32_t *flags, uint
         meta[SPEC_FULL] = 0;
     }
     const uint32_t w = flags[t] | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
+    flags[t] = 0;
+    if (wl_n && t == 0)
+        *wl_n = 0;
     uint32_t pre = cnt; // inclusive wave prefix
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t v = __shfl_up(pre, o);
@@ -3508,6 +3514,7 @@ struct cndp_gpu_ctx {
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
     int tune_lnt;         // CNDP_TUNE_LOAD_NT
     int tune_spec_scan;   // CNDP_TUNE_SPEC_SCAN
+    int sf_clean, wl_clean; // signature flags / worklist count known zero (no memset needed)
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
@@ -4138,7 +4145,9 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
             a.spec_t16 = (uint16_t *)c->sp_pt;
             a.spec_nh = c->sp_nh;
             a.spec_flags = c->sp_small + 66;
-            HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
+            if (!c->sf_clean) // k_spec_classes of the previous call clears them
+                HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
+            c->sf_clean = 0;
         }
         // the streamed kernels index frames in 32 bits (t * 64 + lane < 2^32)
         if ((c->tune_cnet_tile == 2 || c->tune_cnet_tile == 3) && b->n <= 0xFFFFFF00u) {
@@ -4151,10 +4160,13 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                 const uint64_t wcap = (uint64_t)b->n + (b->n >> 3) + 1024;
                 HIP_TRY(hipMalloc((void **)&c->cs_wl, wcap * 4));
                 c->cs_wl_cap = wcap;
+                c->wl_clean = 0;
             }
             a.wl_n = c->cs_wl;
             a.wl = c->cs_wl + 1;
-            HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
+            if (!c->wl_clean) // else k_spec_classes of the previous call cleared it
+                HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
+            c->wl_clean = 0;
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
             if (c->tune_cnet_tile == 3) {
                 uint64_t gd = (n_tiles + CT_WAVES - 1) / CT_WAVES;
@@ -4196,8 +4208,11 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         if (B) {
             const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
             uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
-            hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, (const uint32_t *)flags, c->sp_class, meta,
-                               (const uint16_t *)a.spec_t16, b->n, B, nb, (uint32_t)(c->tune_spec_scan == 0));
+            hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, flags, c->sp_class, meta,
+                               (const uint16_t *)a.spec_t16, b->n, B, nb, (uint32_t)(c->tune_spec_scan == 0),
+                               a.wl_n);
+            c->sf_clean = 1;
+            c->wl_clean = a.wl_n != nullptr;
             const uint32_t gw = (uint32_t)((nb + 3) / 4); // one wave per burst
             const uint32_t kfast = c->tune_spec_scan == 0 ? SPEC_KFAST : 0u;
             const uint32_t kmax = c->tune_spec_scan == 2 ? 0u : SPEC_KMAX;
