@@ -3906,8 +3906,11 @@ extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
         HIP_TRY(hipMemcpyAsync((uint8_t *)t->dev_tbl8 + t->d8_lo * esz, t->tbl8 + t->d8_lo * esz,
                                (t->d8_hi - t->d8_lo) * esz, hipMemcpyHostToDevice, s));
     }
-    const bool dirty = t->d24_hi > t->d24_lo || t->d8_hi > t->d8_lo || !t->dev_dir16;
-    if (!t->is_trie && t->nh_sz == 2) {
+    // (the /16 directory exists for 4-B DIR-24-8 tables only: a trie table
+    // without one is not dirty -- that test made every cnet call wait here)
+    const bool has_dir16 = !t->is_trie && t->nh_sz == 2;
+    const bool dirty = t->d24_hi > t->d24_lo || t->d8_hi > t->d8_lo || (has_dir16 && !t->dev_dir16);
+    if (has_dir16) {
         int r = dir16_sync(t, s, t->d24_lo, t->d24_hi);
         if (r)
             return r;
