@@ -2676,21 +2676,9 @@ __device__ __forceinline__ void spec_scan_a_body(uint32_t *s_m, uint64_t nb, uin
         if (b < nb && k < K)
             P[b * KF + k] = m[k];
         if (t == SPEC_BLK - 1 && k < K)
-            Bt[(uint64_t)blockIdx.x * KF + k] = m[k];
+            __hip_atomic_store(&Bt[(uint64_t)blockIdx.x * KF + k], m[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT); // sc1: read by the last block to arrive
     }
-}
-
-__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan_a(uint64_t nb, const uint32_t *meta, const uint32_t *T,
-                                                        uint32_t *P, uint32_t *Bt, uint32_t kfast, uint32_t gated)
-{
-    __shared__ uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
-    const uint32_t K = meta[0];
-    if (meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL]))
-        return;
-    if (K <= kfast)
-        spec_scan_a_body<SPEC_KFAST>(s_m, nb, K, T, P, Bt);
-    else if (K <= SPEC_KMAX)
-        spec_scan_a_body<SPEC_KMAX>(s_m, nb, K, T, P, Bt);
 }
 
 // block start states: Hillis-Steele over the block totals, W at a time with
@@ -2713,7 +2701,9 @@ __device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carr
         uint32_t m[KF];
 #pragma unroll
         for (uint32_t k = 0; k < KF; k++)
-            m[k] = act && k0 < nblk && k < K ? Bt[k0 * KF + k] : SPEC_UNCH;
+            m[k] = act && k0 < nblk && k < K ? __hip_atomic_load((uint32_t *)&Bt[k0 * KF + k], __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT)
+                                             : SPEC_UNCH;
         const uint32_t dmax = nblk - w0 < W ? (uint32_t)(nblk - w0) : W;
         for (uint32_t d = 1; d < dmax; d <<= 1) {
             if (act)
@@ -2761,25 +2751,50 @@ __device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carr
         *state = spec_apply_t(s_carry, s0) & 0xffffu;
 }
 
-// With more than SPEC_KMAX signatures (the parser's ptypes give fewer; a
-// guard, not a path): one thread walks the bursts sequentially instead
-// (S = the state entering every burst).
-__global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint32_t *meta, const uint8_t *class_id,
-                                                     const uint32_t *Bt, uint32_t *Sblk, uint32_t *state,
-                                                     const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, uint32_t *S, uint32_t kfast, uint32_t kmax,
-                                                     uint32_t gated)
+// Both scan levels in one launch: every block scans its SPEC_BLK items
+// (bursts or chunks) into P and writes its total to Bt with write-through
+// (sc1) stores; after every wave's vmcnt(0) and a block barrier one lane adds
+// to an arrival ticket (agent scope), and the block that draws the last
+// ticket (acquire fence, sc1 loads of Bt) composes the totals into the block
+// start states Sblk and the final state -- MI355X_MICROARCH.md hand-off row 1,
+// no release fence (which writes back the XCD's dirty L2) on any block.  With
+// more than SPEC_KMAX signatures (the parser's ptypes give fewer; a guard, not
+// a path) that block's thread 0 walks the bursts sequentially instead
+// (S = the state entering every burst).  gated: only when k_spec_local left
+// a chunk unresolved (meta[SPEC_FULL]).
+__global__ __launch_bounds__(SPEC_BLK) void k_spec_scan(uint64_t nitems, const uint32_t *meta, const uint32_t *T,
+                                                      uint32_t *P, uint32_t *Bt, const uint8_t *class_id,
+                                                      uint32_t *Sblk, uint32_t *state, uint32_t *ticket,
+                                                      const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
+                                                      uint64_t nb, uint32_t *S, uint32_t kfast, uint32_t kmax,
+                                                      uint32_t gated)
 {
-    __shared__ uint32_t s_m[1024 * (SPEC_KFAST + 1) > 256 * (SPEC_KMAX + 1) ? 1024 * (SPEC_KFAST + 1)
-                                                                             : 256 * (SPEC_KMAX + 1)];
+    __shared__ uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
     __shared__ uint32_t s_carry[SPEC_KMAX];
+    __shared__ uint32_t s_last;
     const uint32_t K = meta[0];
     if (meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL]))
         return;
+    if (K <= kfast)
+        spec_scan_a_body<SPEC_KFAST>(s_m, nitems, K, T, P, Bt);
+    else if (K <= kmax)
+        spec_scan_a_body<SPEC_KMAX>(s_m, nitems, K, T, P, Bt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+    __syncthreads();
+    if (!s_last)
+        return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
     if (K <= kfast) {
-        spec_scan_c_body<SPEC_KFAST, 1024>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+        spec_scan_c_body<SPEC_KFAST, SPEC_BLK>(s_m, s_carry, gridDim.x, K, class_id, Bt, Sblk, state);
     } else if (K <= kmax) {
-        spec_scan_c_body<SPEC_KMAX, 256>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+        spec_scan_c_body<SPEC_KMAX, SPEC_BLK>(s_m, s_carry, gridDim.x, K, class_id, Bt, Sblk, state);
     } else if (threadIdx.x == 0) {
         uint32_t st = meta[SPEC_IN] & 0xffffu;
         for (uint64_t b = 0; b < nb; b++) {
@@ -2792,6 +2807,8 @@ __global__ __launch_bounds__(1024) void k_spec_scan_c(uint64_t nblk, const uint3
         }
         *state = st;
     }
+    if (threadIdx.x == 0)
+        *ticket = 0; // for the next launch (kernel boundary)
 }
 
 // the plain state entering burst / chunk j of a scan block: the block's
@@ -4211,6 +4228,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         if (B) {
             const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
             uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
+            uint32_t *ticket = c->sp_small + 140; // k_spec_scan's arrival count (0 between launches)
             hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, flags, c->sp_class, meta,
                                (const uint16_t *)a.spec_t16, b->n, B, nb, (uint32_t)(c->tune_spec_scan == 0),
                                a.wl_n);
@@ -4234,10 +4252,9 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                    (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T, gated);
                 const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
                 uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
-                hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nch,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast, gated);
-                hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
-                                   (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
+                hipLaunchKernelGGL(k_spec_scan, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nch,
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt,
+                                   (const uint8_t *)c->sp_class, Sblk, state, ticket,
                                    (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax, gated);
                 hipLaunchKernelGGL(ce, dim3(gc), dim3(256), 0, s, a, B, nb, nch, (const uint32_t *)meta,
                                    (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
@@ -4248,10 +4265,9 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
                 const uint64_t nblk = (nb + SPEC_BLK - 1) / SPEC_BLK;
                 uint32_t *P = c->sp_U, *Bt = c->sp_U + nb * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
-                hipLaunchKernelGGL(k_spec_scan_a, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt, kfast, 0u);
-                hipLaunchKernelGGL(k_spec_scan_c, dim3(1), dim3(1024), 0, s, nblk, (const uint32_t *)meta,
-                                   (const uint8_t *)c->sp_class, (const uint32_t *)Bt, Sblk, state,
+                hipLaunchKernelGGL(k_spec_scan, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nb,
+                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt,
+                                   (const uint8_t *)c->sp_class, Sblk, state, ticket,
                                    (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax, 0u);
                 hipLaunchKernelGGL(k_spec_emit, dim3(gw), dim3(256), 0, s, a, B, nb, kfast, kmax,
                                    (const uint32_t *)meta, (const uint8_t *)c->sp_class, (const uint32_t *)P,
