@@ -2378,6 +2378,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 #define SPEC_SKIP 129
 #define SPEC_FULL 130 // k_spec_local left a chunk unresolved: run the full passes
 #define SPEC_IN 131   // the node state entering this batch (meta[-1] becomes the final one)
+#define SPEC_NOLOCAL 132 // one low byte only: no universal group exists, k_spec_local is skipped
 #define SPEC_TAIL 16
 __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t &cur)
 {
@@ -2432,6 +2433,20 @@ __global__ __launch_bounds__(64) void k_spec_classes(uint32_t *flags, uint8_t *c
         one = one && (e8 & (e8 - 1u)) == 0u;
     }
     uint32_t skip = 0;
+    // every type with one low byte (e.g. all IPv4 + L2 ether): no group can
+    // be universal, so k_spec_local would resolve nothing -- go straight to
+    // the full passes
+    uint32_t lows = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++)
+        lows += ((w >> (8 * q)) & 0xffu) != 0u;
+    for (int o = 32; o > 0; o >>= 1)
+        lows += __shfl_xor(lows, o);
+    if (t == 0) {
+        meta[SPEC_NOLOCAL] = lows <= 1u;
+        if (lows <= 1u)
+            meta[SPEC_FULL] = 1;
+    }
     if (allow_skip && __ballot(!one) == 0ull) {
         int64_t ub = -1; // the last universal group: burst ub, group ug
         uint32_t ug = 0;
@@ -3114,7 +3129,7 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     // done != nullptr: k_spec_local ran first; only the chunks it left unresolved
-    if (c >= nch || meta[SPEC_SKIP] || (done && (!meta[SPEC_FULL] || done[c])))
+    if (c >= nch || meta[SPEC_SKIP] || (done && (!meta[SPEC_FULL] || (!meta[SPEC_NOLOCAL] && done[c]))))
         return;
     uint32_t *st = s_pt[wv];
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
@@ -3258,6 +3273,15 @@ __device__ bool spec_lookback(const uint16_t *__restrict__ pt, uint32_t n, uint3
     return false;
 }
 
+// raise meta[SPEC_FULL]: read first, so that a batch where every chunk is
+// unresolved (single-type traffic, C5) does not serialize one atomic per wave
+// on one word (that cost C5 0.4 ms)
+__device__ __forceinline__ void spec_flag_full(uint32_t *meta)
+{
+    if (!__hip_atomic_load(&meta[SPEC_FULL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(&meta[SPEC_FULL], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
                                                     uint8_t *done)
@@ -3266,7 +3290,7 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    if (meta[SPEC_SKIP]) // block-uniform: before the barrier
+    if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL]) // block-uniform: before the barrier
         return;
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
     // the chunk's types (16-B loads of 8) are issued first, so that they
@@ -3291,14 +3315,14 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
             if (lane == 0)
                 meta[-1] = sf;
         } else if (lane == 0) {
-            atomicOr(&meta[SPEC_FULL], 1u);
+            spec_flag_full(meta);
         }
     }
     uint32_t s0 = meta[SPEC_IN] & 0xffffu;
     if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0)) {
         if (lane == 0) {
             done[c] = 0;
-            atomicOr(&meta[SPEC_FULL], 1u);
+            spec_flag_full(meta);
         }
         return;
     }
