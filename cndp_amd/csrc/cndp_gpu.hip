@@ -2072,7 +2072,10 @@ __global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5
 struct CdLane {
     uint32_t ptf;  // pt (16) | do4 << 16 | do6 << 17 | fast << 18 | p_nxt edge << 19
     uint32_t h, e, rx;
-    uint32_t d0, d1, d2, d3; // v6 destination words, or dip in d0 (v4)
+    // the chain's key bytes after the first gather, next byte lowest: v6
+    // address bytes 3..15 (trie.h:127-134); v4 dip bits 15:8 then 7:0 with
+    // the /16 directory, bits 7:0 without (dir24_8.h:135-140)
+    uint32_t q0, q1, q2, q3;
 };
 
 template <bool LNT, bool META, int P>
@@ -2088,25 +2091,25 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     const uint32_t ib = (t - wstep) * 64u + lane;
     uint32_t eb = sb.e;
     {
+        // one branch-free body for both families: the key bytes stream out of
+        // q0..q3, the level count and the table pair are fixed per lane
         const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
-        uint32_t j = d6 ? 3u : (a.dir16 ? 1u : 2u);
-        bool more = bv && (d4 || d6) && (eb & 1u);
+        uint32_t rem = d6 ? 13u : (a.dir16 ? 2u : 1u);
+        const uint32_t *tb = d6 ? a.tbl8_6 : (a.dir16 ? a.pages : a.tbl8);
+        const uint32_t *const tb2 = d6 ? a.tbl8_6 : a.tbl8;
+        uint32_t q0 = sb.q0, q1 = sb.q1, q2 = sb.q2, q3 = sb.q3;
+        bool more = bv & (d4 | d6) & ((eb & 1u) != 0u);
         while (__any(more)) {
-            if (more) {
-                uint32_t byte;
-                const uint32_t *tb;
-                if (d6) {
-                    const uint32_t wd = j < 4 ? sb.d0 : j < 8 ? sb.d1 : j < 12 ? sb.d2 : sb.d3;
-                    byte = (wd >> ((j & 3u) * 8)) & 0xffu;
-                    tb = a.tbl8_6;
-                } else {
-                    byte = j == 1 ? (sb.d0 >> 8) & 0xffu : sb.d0 & 0xffu;
-                    tb = j == 1 ? a.pages : a.tbl8;
-                }
-                eb = tb[(eb >> 1) * 256u + byte];
-                j++;
-                more = (eb & 1u) && (d6 ? j < 16 : j <= 2);
-            }
+            const uint32_t idx = ((eb >> 1) << 8) | (q0 & 0xffu);
+            if (more)
+                eb = tb[idx];
+            tb = tb2;
+            q0 = alignb(q1, q0, 1);
+            q1 = alignb(q2, q1, 1);
+            q2 = alignb(q3, q2, 1);
+            q3 >>= 8;
+            rem--;
+            more = more & ((eb & 1u) != 0u) & (rem != 0u);
         }
     }
     // A: tile c
@@ -2154,7 +2157,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     na.ptf = 0;
     na.h = 0;
     na.rx = 0;
-    na.d0 = na.d1 = na.d2 = na.d3 = 0;
+    na.q0 = na.q1 = na.q2 = na.q3 = 0;
     uint32_t idx0 = 0;
     const uint32_t *tb0 = a.tbl24_6;
     if (fast) {
@@ -2206,21 +2209,27 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 sum = (sum >> 16) + (sum & 0xffffu);
                 sum = (sum >> 16) + (sum & 0xffffu);
                 const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
-                na.d0 = ok ? bswap32(dst) : 0u;
+                const uint32_t d0 = ok ? bswap32(dst) : 0u;
+                na.q0 = ok ? dst >> (a.dir16 ? 16 : 24) : 0u; // network bytes 2, 3
                 flags = 1u << 16;
                 tb0 = a.dir16 ? a.dir16 : a.tbl24;
-                idx0 = a.dir16 ? na.d0 >> 16 : na.d0 >> 8;
+                idx0 = a.dir16 ? d0 >> 16 : d0 >> 8;
             }
         } else {
             if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
+                uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
                 if (bswap16(W[4] >> 16) < a.buf_len) {
-                    na.d0 = alignb(W[10], W[9], 2);
-                    na.d1 = alignb(W[11], W[10], 2);
-                    na.d2 = alignb(W[12], W[11], 2);
-                    na.d3 = alignb(W[13], W[12], 2);
+                    d0 = alignb(W[10], W[9], 2);
+                    d1 = alignb(W[11], W[10], 2);
+                    d2 = alignb(W[12], W[11], 2);
+                    d3 = alignb(W[13], W[12], 2);
                 }
+                na.q0 = alignb(d1, d0, 3);
+                na.q1 = alignb(d2, d1, 3);
+                na.q2 = alignb(d3, d2, 3);
+                na.q3 = d3 >> 24;
                 flags = 1u << 17;
-                idx0 = ((na.d0 & 0xffu) << 16) | (na.d0 & 0xff00u) | ((na.d0 >> 16) & 0xffu); // trie.h:126
+                idx0 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu); // trie.h:126
             }
         }
         na.ptf = pt | flags | (1u << 18) | (pe << 19);
@@ -2323,7 +2332,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
     CdLane sb;
     sb.ptf = sb.h = sb.e = sb.rx = 0;
-    sb.d0 = sb.d1 = sb.d2 = sb.d3 = 0;
+    sb.q0 = sb.q1 = sb.q2 = sb.q3 = 0;
     uint32_t last_sig = 0xFFFFFFFFu;
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {

@@ -128,6 +128,46 @@ def test_cnet_imix_c4_parity(cnet, gpu):
     assert (ref["edge"] == 1).mean() > 0.5
 
 
+def test_cnet_deep_v6_chains(gpu):
+    """cnet trie chains through every tbl8 level: the lpm6_1000 rule set
+    (/1../128, fib6_test.c / lpm6_data_test.h) behind ip6_input's edge values,
+    destinations from its golden lookups, IPv4 and IPv6 frames mixed in each
+    wave (the deferred kernel runs both families' chains in one loop)."""
+    from cndp_amd.classify import Classifier
+    from cndp_amd.fib import Fib6, node_ip6_add_input
+    from helpers import CNET_DEF
+    g = np.load(os.path.join(GOLD, "lpm6_1000.npz"))
+    fib, _, routes, v6, v4vals, _ = cnet_fibs()
+    fib6 = Fib6("deep6", N.CNE_FIB_TRIE, default_nh=CNET_DEF, max_routes=2000,
+                nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15)
+    v6vals = []
+    for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
+        assert node_ip6_add_input(fib6, bytes(ip), int(d), int(nh)) == 0
+        v6vals.append((bytes(ip), int(d), int(nh) | ((2 if d == 32 else 1) << 24)))
+    cl = Classifier(0)
+    cl.set_fib(fib, fib6)
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    n = g["ip"].shape[0]
+    fr = pktgen.imix(n, v4routes=routes, v6routes=v6, device=gpu, v6_frac=0.7)
+    base = fr.offsets + fr.data_off
+    is6 = (fr.slab[base + 12] == 0x86) & (fr.slab[base + 13] == 0xDD)
+    dst = torch.as_tensor(g["ip"], device=gpu)
+    pos = (base[is6, None] + 38 + torch.arange(16, device=gpu)).reshape(-1)
+    fr.slab[pos] = dst[is6].reshape(-1)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+    for ct in CNET_KERNELS:
+        cl.set_tuning(cnet_tile=ct)
+        assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
+    # pinned by the reference's own golden lookups where a rule matched (frames
+    # that reached ip6_input: a random UDP port may be GTP-C -> pkt_drop)
+    nh = ref["nh"][is6.cpu().numpy()]
+    gold = g["nh"][is6.cpu().numpy()].astype(np.uint32)
+    hit = ((nh & 0xFFFFFF) != CNET_DEF) & (nh != 0xFFFFFFFF)
+    assert hit.mean() > 0.5
+    assert np.array_equal(nh[hit] & 0xFFFF, gold[hit])
+
+
 def test_cnet_fuzz_parity(cnet, gpu):
     """cne_get_ptype over random structures (parity vs the unpinned restatement)."""
     cl, routes, v6, t4, t6 = cnet
