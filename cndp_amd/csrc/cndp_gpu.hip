@@ -2388,6 +2388,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 #define SPEC_FULL 130 // k_spec_local left a chunk unresolved: run the full passes
 #define SPEC_IN 131   // the node state entering this batch (meta[-1] becomes the final one)
 #define SPEC_NOLOCAL 132 // one low byte only: no universal group exists, k_spec_local is skipped
+#define SPEC_UNIF 133 // every type has the entering state's low byte: k_spec_local's uniform pass only
 #define SPEC_TAIL 16
 __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t &cur)
 {
@@ -2451,12 +2452,26 @@ __global__ __launch_bounds__(64) void k_spec_classes(uint32_t *flags, uint8_t *c
         lows += ((w >> (8 * q)) & 0xffu) != 0u;
     for (int o = 32; o > 0; o >>= 1)
         lows += __shfl_xor(lows, o);
+    // Uniform batch (auto mode, bursts <= 256): lows <= 1 counts the entering
+    // state's low byte too, so every type shares it.  Each full group is then
+    // quiet (ptype.c:109-110), goes whole to p_nxt[last_type] and never moves
+    // the state (the per-packet tail, :171-187, does not either): the final
+    // state is the entering one, and only frames of full groups whose own
+    // edge differs get re-routed -- by k_spec_local's uniform pass, or by
+    // nobody when no other signature is present.
+    const bool unif = allow_skip && lows <= 1u && B <= 256u;
     if (t == 0) {
         meta[SPEC_NOLOCAL] = lows <= 1u;
-        if (lows <= 1u)
+        meta[SPEC_UNIF] = 0;
+        if (lows <= 1u && !unif)
             meta[SPEC_FULL] = 1;
     }
-    if (allow_skip && __ballot(!one) == 0ull) {
+    if (unif) {
+        const uint32_t own = t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u;
+        skip = __ballot((w & ~own) != 0u) == 0ull;
+        if (t == 0)
+            meta[SPEC_UNIF] = !skip;
+    } else if (allow_skip && __ballot(!one) == 0ull) {
         int64_t ub = -1; // the last universal group: burst ub, group ug
         uint32_t ug = 0;
         for (uint64_t q = 0; q < SPEC_TAIL && q < nb && ub < 0; q++) {
@@ -3291,6 +3306,38 @@ __device__ __forceinline__ void spec_flag_full(uint32_t *meta)
         __hip_atomic_store(&meta[SPEC_FULL], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// uniform batch (k_spec_classes): every frame of a full group of bursts
+// [c0, c1) leaves by edge E, the entering state's p_nxt; fix those whose own
+// edge differs.  Tail frames (a burst's last cnt % 4) keep their own edge.
+__device__ void spec_uniform_chunk(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane, uint32_t E)
+{
+    const uint32_t p0 = (uint32_t)(c0 * B), p1 = (uint32_t)(c1 * B < a.n ? c1 * B : a.n);
+    const bool vec = (B & 7u) == 0;
+    for (uint32_t i0 = p0 + lane * 8u; i0 < p1; i0 += 512u) {
+        uint32_t l[8];
+        if (vec && i0 + 8u <= p1) {
+            const u32x4 v = *(const u32x4 *)(a.spec_t16 + i0);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                l[q] = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu;
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                l[q] = i0 + q < p1 ? a.spec_t16[i0 + q] : 0u;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t i = i0 + q;
+            if (i >= p1 || cnet_edge(l[q]) == E)
+                continue;
+            const uint32_t b0 = i / B * B, bend = b0 + B < a.n ? b0 + B : a.n;
+            if (b0 + ((i - b0) & ~3u) + 4u <= bend) // a full group
+                spec_fix(a, i, l[q], E);
+        }
+    }
+}
+
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
                                                     uint8_t *done)
@@ -3299,6 +3346,12 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if (meta[SPEC_UNIF]) { // block-uniform
+        if (c < nch)
+            spec_uniform_chunk(a, B, c * CH, (c * CH + CH < nb ? c * CH + CH : nb), lane,
+                               cnet_edge(meta[SPEC_IN] & 0xffffu));
+        return;
+    }
     if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL]) // block-uniform: before the barrier
         return;
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;

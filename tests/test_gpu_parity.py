@@ -758,6 +758,47 @@ def test_cnet_speculation_batch_shortcut(cnet, gpu, burst):
         ccl.set_tuning(cnet_spec=256, spec_scan=0)
 
 
+@pytest.mark.parametrize("burst", [256, 7, 64, 1000])
+def test_cnet_speculation_uniform(cnet, gpu, burst):
+    """One low ptype byte in the whole batch (IPv4/UDP with some GTP-U and
+    GTP-C ports: three types sharing low byte 0x11 under three edges, the C5
+    shape).  Once the node state has that low byte every full group is quiet
+    and the state never moves, so each call after the first takes
+    k_spec_local's uniform pass.  Chained calls == the node loop, and == the
+    forced full scans."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = pktgen.packed_ipv4(30000, routes=routes, device=gpu, seed=burst + 7)
+    rows = fr.slab.view(fr.n, fr.stride)
+    idx = torch.arange(fr.n, device=gpu)
+    rows[:, 36] = 0x12                      # UDP dport 0x12xx: plain UDP
+    for every, first, lo in ((997, 5, 0x68), (1499, 11, 0x4B)):  # 2152 GTP-U, 2123 GTP-C
+        sel = (idx % every) == first
+        rows[sel, 36] = 0x08
+        rows[sel, 37] = lo
+    pt = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)["ptype"] & 0xFFFF
+    assert len({int(p) & 0xFF for p in pt}) == 1 and len({_cnet_edge(int(p)) for p in pt}) == 3
+    cuts = (0, (fr.n // 3) // burst * burst, (2 * fr.n // 3) // burst * burst, fr.n)
+    try:
+        for scan in (0, 1):
+            ccl.set_tuning(cnet_spec=burst, spec_scan=scan)  # also resets the node state
+            st = np.zeros(1, np.uint16)
+            moved = 0
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                part = pktgen.Frames(fr.slab[lo * fr.stride:hi * fr.stride], hi - lo, stride=fr.stride,
+                                     data_off=fr.data_off)
+                plain = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=0)
+                ref = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=burst,
+                                      spec_state=st)
+                moved += int((plain["edge"] != ref["edge"]).sum())
+                o = ccl.alloc_outputs(part.n, 64, device=gpu, meta=True)
+                ccl.classify(part, N.CNDP_MODE_CNET, out=o)
+                torch.cuda.synchronize()
+                assert_same(o, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+            assert moved > 0, "input does not exercise the quirk"
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_scan=0)
+
+
 def test_cnet_speculation_local_and_full(cnet, gpu):
     """The local pass resolves a chunk from the last universal group of the
     chunk before it; chunks behind single-type runs (no universal group) are
