@@ -3139,7 +3139,7 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
 }
 
 template <int CH>
-__device__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
+__device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
                             const uint32_t *st);
 
 template <int CH>
@@ -3177,7 +3177,7 @@ __global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_
 // the state entering group g, fixes the group's frames if it is quiet under
 // that state, and lane ng-1 hands the burst's exit state to the next burst
 template <int CH>
-__device__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
+__device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
                             const uint32_t *st)
 {
     for (uint64_t bb = c0; bb < c1; bb++) {
@@ -3269,7 +3269,7 @@ __device__ __forceinline__ void spec_walk_regs(uint32_t q0, uint32_t q1, uint32_
 
 // the node state after bursts [b_lo, b_hi): the walk from the last universal
 // group in them to their end; false when they hold none
-__device__ bool spec_lookback(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t b_lo, uint64_t b_hi,
+__device__ __forceinline__ bool spec_lookback(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t b_lo, uint64_t b_hi,
                               uint32_t lane, const uint16_t *lut, uint32_t &s_out)
 {
     for (uint64_t j = b_hi; j-- > b_lo;) {
@@ -3309,15 +3309,34 @@ __device__ __forceinline__ void spec_flag_full(uint32_t *meta)
 // uniform batch (k_spec_classes): every frame of a full group of bursts
 // [c0, c1) leaves by edge E, the entering state's p_nxt; fix those whose own
 // edge differs.  Tail frames (a burst's last cnt % 4) keep their own edge.
-__device__ void spec_uniform_chunk(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane, uint32_t E)
+// A wave takes SPEC_UNIF_W chunks and issues all its type loads (16 B = 8
+// types each) before the first is used (measured on C5: 4 chunks per wave,
+// a quarter of the waves with 8 loads each, is slower than 1)
+#ifndef SPEC_UNIF_W
+#define SPEC_UNIF_W 1
+#endif
+template <int CH>
+__device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane, uint32_t E)
 {
+    constexpr uint32_t U = CH * SPEC_UNIF_W * 256 / 512 > 0 ? CH * SPEC_UNIF_W * 256 / 512 : 1;
     const uint32_t p0 = (uint32_t)(c0 * B), p1 = (uint32_t)(c1 * B < a.n ? c1 * B : a.n);
     const bool vec = (B & 7u) == 0;
-    for (uint32_t i0 = p0 + lane * 8u; i0 < p1; i0 += 512u) {
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t r = 0; r < U; r++) {
+        const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
+        v[r] = vec && i0 + 8u <= p1 ? *(const u32x4 *)(a.spec_t16 + i0) : (u32x4){0, 0, 0, 0};
+    }
+    // B <= 256 here (k_spec_classes), so a wave's range is <= U * 512 types
+#pragma unroll
+    for (uint32_t r = 0; r < U; r++) {
+        const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
+        if (i0 >= p1)
+            continue;
         uint32_t l[8];
         if (vec && i0 + 8u <= p1) {
-            const u32x4 v = *(const u32x4 *)(a.spec_t16 + i0);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const u32x4 x = v[r];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
                 l[q] = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu;
@@ -3346,10 +3365,10 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    if (meta[SPEC_UNIF]) { // block-uniform
-        if (c < nch)
-            spec_uniform_chunk(a, B, c * CH, (c * CH + CH < nb ? c * CH + CH : nb), lane,
-                               cnet_edge(meta[SPEC_IN] & 0xffffu));
+    if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
+        const uint64_t u0 = c * SPEC_UNIF_W * CH, u1 = u0 + SPEC_UNIF_W * CH;
+        if (u0 < nb)
+            spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, cnet_edge(meta[SPEC_IN] & 0xffffu));
         return;
     }
     if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL]) // block-uniform: before the barrier
