@@ -3316,8 +3316,11 @@ __device__ __forceinline__ void spec_flag_full(uint32_t *meta)
 #define SPEC_UNIF_W 1
 #endif
 template <int CH>
-__device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane, uint32_t E)
+__device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
+                                                   uint32_t T)
 {
+    // T: the node state; 8 types all equal to it need no cnet_edge (4 compares)
+    const uint32_t E = cnet_edge(T), TT = T | (T << 16);
     constexpr uint32_t U = CH * SPEC_UNIF_W * 256 / 512 > 0 ? CH * SPEC_UNIF_W * 256 / 512 : 1;
     const uint32_t p0 = (uint32_t)(c0 * B), p1 = (uint32_t)(c1 * B < a.n ? c1 * B : a.n);
     const bool vec = (B & 7u) == 0;
@@ -3336,6 +3339,8 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
         uint32_t l[8];
         if (vec && i0 + 8u <= p1) {
             const u32x4 x = v[r];
+            if ((x.x == TT) & (x.y == TT) & (x.z == TT) & (x.w == TT))
+                continue;
             const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
@@ -3368,7 +3373,7 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
         const uint64_t u0 = c * SPEC_UNIF_W * CH, u1 = u0 + SPEC_UNIF_W * CH;
         if (u0 < nb)
-            spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, cnet_edge(meta[SPEC_IN] & 0xffffu));
+            spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, meta[SPEC_IN] & 0xffffu);
         return;
     }
     if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL]) // block-uniform: before the barrier
