@@ -3372,6 +3372,9 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
         const uint64_t u0 = c * SPEC_UNIF_W * CH, u1 = u0 + SPEC_UNIF_W * CH;
+#ifdef UNIF_DIAG // timing-only builds: the pass's fixed cost
+        return;
+#endif
         if (u0 < nb)
             spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, meta[SPEC_IN] & 0xffffu);
         return;
