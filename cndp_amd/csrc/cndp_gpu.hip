@@ -3334,13 +3334,15 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
 #pragma unroll
     for (uint32_t r = 0; r < U; r++) {
         const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
-        if (i0 >= p1)
-            continue;
         uint32_t l[8];
-        if (vec && i0 + 8u <= p1) {
-            const u32x4 x = v[r];
-            if ((x.x == TT) & (x.y == TT) & (x.z == TT) & (x.w == TT))
-                continue;
+        const bool full8 = vec && i0 + 8u <= p1;
+        const u32x4 x = v[r];
+        const bool same = (i0 >= p1) | (full8 & (x.x == TT) & (x.y == TT) & (x.z == TT) & (x.w == TT));
+        if (__all(same)) // wave-uniform skip: no divergent per-type code at all
+            continue;
+        if (same)
+            continue;
+        if (full8) {
             const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
@@ -3356,8 +3358,10 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
             if (i >= p1 || cnet_edge(l[q]) == E)
                 continue;
             const uint32_t b0 = i / B * B, bend = b0 + B < a.n ? b0 + B : a.n;
+#ifndef UNIF_NOFIX
             if (b0 + ((i - b0) & ~3u) + 4u <= bend) // a full group
                 spec_fix(a, i, l[q], E);
+#endif
         }
     }
 }
@@ -3372,7 +3376,24 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
         const uint64_t u0 = c * SPEC_UNIF_W * CH, u1 = u0 + SPEC_UNIF_W * CH;
-#ifdef UNIF_DIAG // timing-only builds: the pass's fixed cost
+#ifdef UNIF_DIAG // timing-only builds: 1 the pass's fixed cost, 2 / 3 its loads alone (plain / nt)
+        if (UNIF_DIAG == 1 || u0 >= nb)
+            return;
+        {
+            const uint32_t p0 = (uint32_t)(u0 * B), p1 = (uint32_t)((u1 < nb ? u1 : nb) * B < a.n ? (u1 < nb ? u1 : nb) * B : a.n);
+            uint32_t acc = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < SPEC_UNIF_W * CH * 256 / 512; r++) {
+                const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
+                if (i0 + 8u <= p1) {
+                    const u32x4 *q = (const u32x4 *)(a.spec_t16 + i0);
+                    const u32x4 x = UNIF_DIAG == 3 ? __builtin_nontemporal_load(q) : *q;
+                    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+                }
+            }
+            if (acc == 0x9E3779B9u)
+                meta[200] = acc;
+        }
         return;
 #endif
         if (u0 < nb)
