@@ -3334,33 +3334,38 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
 #pragma unroll
     for (uint32_t r = 0; r < U; r++) {
         const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
-        uint32_t l[8];
         const bool full8 = vec && i0 + 8u <= p1;
-        const u32x4 x = v[r];
+        u32x4 x = v[r];
         const bool same = (i0 >= p1) | (full8 & (x.x == TT) & (x.y == TT) & (x.z == TT) & (x.w == TT));
-        if (__all(same)) // wave-uniform skip: no divergent per-type code at all
+        if (__all(same)) // wave-uniform skip
             continue;
-        if (same)
-            continue;
-        if (full8) {
+        if (!same && !full8) { // ragged end, or bursts not a multiple of 8
+            uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+                w[q >> 1] |= (i0 + q < p1 ? (uint32_t)a.spec_t16[i0 + q] : 0u) << (16 * (q & 1u));
+            x = (u32x4){w[0], w[1], w[2], w[3]};
+        }
+        // frames of this vector whose own edge differs, then one fix site
+        uint32_t m = 0;
+        if (!same) {
             const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (uint32_t q = 0; q < 8; q++)
-                l[q] = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu;
-        } else {
-#pragma unroll
-            for (uint32_t q = 0; q < 8; q++)
-                l[q] = i0 + q < p1 ? a.spec_t16[i0 + q] : 0u;
+                m |= (uint32_t)((i0 + q < p1) & (cnet_edge((w[q >> 1] >> (16 * (q & 1u))) & 0xffffu) != E)) << q;
         }
-#pragma unroll
-        for (uint32_t q = 0; q < 8; q++) {
-            const uint32_t i = i0 + q;
-            if (i >= p1 || cnet_edge(l[q]) == E)
-                continue;
+        const uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
+        while (m) {
+            const uint32_t q = (uint32_t)__ffs(m) - 1u;
+            m &= m - 1u;
+            const uint32_t i = i0 + q, l = (uint32_t)((q < 4 ? lo : hi) >> (16 * (q & 3u))) & 0xffffu;
             const uint32_t b0 = i / B * B, bend = b0 + B < a.n ? b0 + B : a.n;
 #ifndef UNIF_NOFIX
             if (b0 + ((i - b0) & ~3u) + 4u <= bend) // a full group
-                spec_fix(a, i, l[q], E);
+                spec_fix(a, i, l, E);
+#else
+            if (b0 + ((i - b0) & ~3u) + 4u <= bend)
+                a.edge[i] = (uint8_t)E;
 #endif
         }
     }
