@@ -2861,7 +2861,10 @@ __device__ __forceinline__ uint32_t spec_enter(const uint32_t *P, uint64_t j, ui
     return (nx == SPEC_UNCH ? sb : nx) & 0xffffu;
 }
 
-__device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
+// lbins != nullptr: the bin moves go to a block's LDS counters (flushed by
+// the caller) -- the uniform pass moves every frame from the same few bins,
+// and same-address global atomics serialize
+__device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst, int *lbins = nullptr)
 {
     const uint32_t own = cnet_edge(own_l);
     const bool own_in = own == 3u || own == 4u;
@@ -2873,7 +2876,10 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
         a.nh[i] = nh;
     if (a.edge)
         a.edge[i] = (uint8_t)edge;
-    if (a.bins) {
+    if (a.bins && lbins) {
+        atomicAdd(&lbins[bin_of<CNDP_MODE_CNET>(old_nh, old_edge, 0, a.n_bins)], -1);
+        atomicAdd(&lbins[bin_of<CNDP_MODE_CNET>(nh, edge, 0, a.n_bins)], 1);
+    } else if (a.bins) {
         atomicAdd(&a.bins[bin_of<CNDP_MODE_CNET>(old_nh, old_edge, 0, a.n_bins)], ~0ull); // -1
         atomicAdd(&a.bins[bin_of<CNDP_MODE_CNET>(nh, edge, 0, a.n_bins)], 1ull);
     }
@@ -3317,7 +3323,7 @@ __device__ __forceinline__ void spec_flag_full(uint32_t *meta)
 #endif
 template <int CH>
 __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
-                                                   uint32_t T)
+                                                   uint32_t T, int *lbins)
 {
     // T: the node state; 8 types all equal to it need no cnet_edge (4 compares)
     const uint32_t E = cnet_edge(T), TT = T | (T << 16);
@@ -3362,7 +3368,7 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
             const uint32_t b0 = i / B * B, bend = b0 + B < a.n ? b0 + B : a.n;
 #ifndef UNIF_NOFIX
             if (b0 + ((i - b0) & ~3u) + 4u <= bend) // a full group
-                spec_fix(a, i, l, E);
+                spec_fix(a, i, l, E, lbins);
 #else
             if (b0 + ((i - b0) & ~3u) + 4u <= bend)
                 a.edge[i] = (uint8_t)E;
@@ -3381,6 +3387,12 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
         const uint64_t u0 = c * SPEC_UNIF_W * CH, u1 = u0 + SPEC_UNIF_W * CH;
+        static_assert(4 * CH * 256 >= CNDP_BINS_MAX + 2, "bin counters must fit the staging tile");
+        int *lbins = (int *)&s_pt[0][0]; // n_bins + 2 <= CNDP_BINS_MAX + 2 ints fit the staging tile
+        const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            lbins[k] = 0;
+        __syncthreads();
 #ifdef UNIF_DIAG // timing-only builds: 1 the pass's fixed cost, 2 / 3 its loads alone (plain / nt)
         if (UNIF_DIAG == 1 || u0 >= nb)
             return;
@@ -3402,7 +3414,11 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
         return;
 #endif
         if (u0 < nb)
-            spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, meta[SPEC_IN] & 0xffffu);
+            spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, meta[SPEC_IN] & 0xffffu, lbins);
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            if (lbins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)(long long)lbins[k]);
         return;
     }
     if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL]) // block-uniform: before the barrier
