@@ -402,6 +402,21 @@ def test_full_size_c5_sampled(cnet, gpu):
         ref = oracle_classify(O.MODE_CNET, sfr, tables4=ct4, tables6=ct6, spec_burst=0)
         sub = {k: (v[idx] if torch.is_tensor(v) and v.dim() == 1 and v.numel() == n else v) for k, v in out.items()}
         assert_same(sub, ref, keys=("nh", "hash", "queue", "edge"))
+        # speculation on, second call: the node state carries the batch's one
+        # low byte (0x11), so the uniform pass runs at full size.  Every frame
+        # sits in a full group: those whose own edge is the state's (plain
+        # UDP -> ip4_input) keep the per-frame result, the GTP-U / GTP-C
+        # frames are re-routed to ip4_input (ptype.c:109-110)
+        ccl.set_tuning(cnet_spec=256)
+        for _ in range(2):
+            spec = ccl.classify(fr, N.CNDP_MODE_CNET, n_bins=64)
+            torch.cuda.synchronize()
+            assert int(spec["bins"].sum()) == n
+        own_in = out["edge"] < 0x80
+        assert int((~own_in).sum()) > 0, "no GTP frames: the uniform pass moves nothing"
+        assert torch.equal(spec["edge"][own_in], out["edge"][own_in])
+        assert torch.equal(spec["nh"][own_in], out["nh"][own_in])
+        assert bool((spec["edge"][~own_in] < 0x80).all())
     finally:
         ccl.set_tuning(cnet_spec=256)
 
