@@ -3275,14 +3275,22 @@ __device__ __forceinline__ void spec_walk_regs(uint32_t q0, uint32_t q1, uint32_
 
 // the node state after bursts [b_lo, b_hi): the walk from the last universal
 // group in them to their end; false when they hold none
+// pre: the groups of burst b_hi - 1 are already in (pq0, pq1) (loaded by
+// the caller ahead of its barrier)
 __device__ __forceinline__ bool spec_lookback(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t b_lo, uint64_t b_hi,
-                              uint32_t lane, const uint16_t *lut, uint32_t &s_out)
+                              uint32_t lane, const uint16_t *lut, uint32_t &s_out, bool pre = false,
+                              uint32_t pq0 = 0, uint32_t pq1 = 0)
 {
     for (uint64_t j = b_hi; j-- > b_lo;) {
         const uint64_t b0 = j * B;
         const uint32_t cnt = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B), ng = cnt >> 2;
         uint32_t q0, q1;
-        spec_group_regs(pt, b0, cnt, lane, q0, q1);
+        if (pre && j + 1 == b_hi) {
+            q0 = pq0;
+            q1 = pq1;
+        } else {
+            spec_group_regs(pt, b0, cnt, lane, q0, q1);
+        }
         const uint32_t v = q0 & 0xffu;
         const bool allq = ((q0 >> 16) & 0xffu) == v && (q1 & 0xffu) == v && ((q1 >> 16) & 0xffu) == v;
         const unsigned long long U = __ballot(lane < ng && !allq && (q1 & 0xffffu) == (q1 >> 16));
@@ -3436,6 +3444,13 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
         const uint32_t idx = (r * 64u + lane) * 8u;
         v[r] = idx + 8u <= m ? *(const u32x4 *)(a.spec_t16 + p0 + idx) : (u32x4){0, 0, 0, 0};
     }
+    // and the previous chunk's last burst, where the look-back starts
+    uint32_t pq0 = 0, pq1 = 0;
+    const bool prev = c > 0 && c < nch;
+    if (prev) {
+        const uint64_t b0 = (c0 - 1) * B; // a full burst: only the batch's last burst is short
+        spec_group_regs(a.spec_t16, b0, B, lane, pq0, pq1);
+    }
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     __syncthreads();
     if (c >= nch)
@@ -3450,7 +3465,7 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
         }
     }
     uint32_t s0 = meta[SPEC_IN] & 0xffffu;
-    if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0)) {
+    if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, pq0, pq1)) {
         if (lane == 0) {
             done[c] = 0;
             spec_flag_full(meta);
