@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include "fib_internal.h"
+#include "node_internal.h"
 #include "../../include/cndp_gpu.h"
 
 #define CNDP_VERSION "cndp_amd 0.1 (gfx950)"
@@ -105,17 +106,10 @@ __device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_
            tab[(b + 2) * 256 + ((x >> 16) & 0xffu)] ^ tab[(b + 3) * 256 + (x >> 24)];
 }
 
-#define CNDP_RW_MAX_NH 64     // CNE_GRAPH_IP4_REWRITE_MAX_NH
-#define CNDP_RW_MAX_LEN 56    // CNE_GRAPH_IP4_REWRITE_MAX_LEN
-#define CNDP_RW_MAX_PORTS 32  // CNE_MAX_ETHPORTS
-// struct ip4_rewrite_nh_header (ip4_rewrite_priv.h:24-38)
-struct cndp_rw_nh {
-    uint16_t rewrite_len;
-    uint16_t tx_node;
-    uint16_t enabled;
-    uint16_t rsvd;
-    uint8_t rewrite_data[CNDP_RW_MAX_LEN];
-};
+#define CNDP_RW_MAX_NH CNDP_IP4_REWRITE_MAX_NH       // CNE_GRAPH_IP4_REWRITE_MAX_NH
+#define CNDP_RW_MAX_LEN CNDP_IP4_REWRITE_MAX_LEN     // CNE_GRAPH_IP4_REWRITE_MAX_LEN
+#define CNDP_RW_MAX_PORTS CNDP_IP4_REWRITE_MAX_PORTS // CNE_MAX_ETHPORTS
+// struct cndp_rw_nh = struct ip4_rewrite_nh_header (node_internal.h)
 
 struct KArgs {
     const uint8_t *slab;
@@ -3729,6 +3723,8 @@ struct cndp_gpu_ctx {
     uint16_t rw_next[CNDP_RW_MAX_PORTS];
     struct cndp_rw_nh *d_rw_tbl;
     int rw_dirty;
+    int rw_local;         // the ctx-level rewrite API was used: do not follow the node table
+    uint64_t rw_gen_seen; // generation of the process-global table (node.c) last copied
     uint32_t rw_parts;    // 16-B parts a rewrite touches: ceil(max(26, longest rewrite) / 16)
 };
 
@@ -4960,6 +4956,11 @@ extern "C" int cndp_gpu_ip4_rewrite_set_next(cndp_gpu_ctx_t *c, uint16_t port_id
 {
     if (!c || port_id >= CNDP_RW_MAX_PORTS)
         return -EINVAL;
+    if (!c->rw_local) { // from now on this context keeps a table of its own
+        memset(c->rw_tbl, 0, sizeof(c->rw_tbl));
+        c->rw_local = 1;
+        c->rw_dirty = 1;
+    }
     c->rw_next[port_id] = next_index;
     return 0;
 }
@@ -4990,6 +4991,12 @@ extern "C" int cndp_gpu_ip4_rewrite_add(cndp_gpu_ctx_t *c, uint16_t next_hop, co
 
 static int rw_sync(cndp_gpu_ctx_t *c, hipStream_t s)
 {
+    // a context without a table of its own follows the node table that
+    // cne_node_ip4_rewrite_add fills (node.c), like the reference node does
+    if (!c->rw_local && cndp_node_rw_gen() != c->rw_gen_seen) {
+        c->rw_gen_seen = cndp_node_rw_snapshot(c->rw_tbl);
+        c->rw_dirty = 1;
+    }
     if (!c->d_rw_tbl) {
         HIP_TRY(hipMalloc((void **)&c->d_rw_tbl, sizeof(c->rw_tbl)));
         c->rw_dirty = 1;

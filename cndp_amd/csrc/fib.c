@@ -843,6 +843,12 @@ int cne_fib6_lookup_bulk(struct cne_fib6 *fib, uint8_t ips[][IPV6_ADDR_LEN], uin
 
 void *cne_fib6_get_dp(struct cne_fib6 *fib) { return fib ? &fib->t : NULL; }
 
+/* cne_fib6.c:202-205: the build's RIB (path-compressed trie over 128-bit keys) */
+struct cne_rib6 *cne_fib6_get_rib(struct cne_fib6 *fib)
+{
+    return fib ? (struct cne_rib6 *)&fib->rib : NULL;
+}
+
 int cne_fib6_select_lookup(struct cne_fib6 *fib, enum cne_fib_lookup_type type)
 {
     if (!fib || fib->type != CNE_FIB_TRIE)

@@ -174,22 +174,49 @@ class Fib6:
         return {"routes": r.value, "tbl8_used": u.value, "rsvd_tbl8s": s.value}
 
 
+class NodeFib(Fib):
+    """The l3fwd node FIB libcndp_gpu owns (ip4_lookup_nm, ip4_lookup.c:31-42),
+    created by cndp_node_ip4_lookup_init (setup_fib, :292-311).  Routes go in
+    through cne_node_ip4_route_add; this handle does not own the table."""
+
+    def __init__(self):  # noqa: super().__init__ would create a second FIB
+        self._L = N.lib()
+        N.check(self._L.cndp_node_ip4_lookup_init(), "cndp_node_ip4_lookup_init")
+        self.h = self._L.cndp_node_ip4_lookup_fib()
+        self.type = N.CNE_FIB_DIR24_8
+        self.default_nh = N.IP4_LOOKUP_NEXT_PKT_DROP << 16
+
+    def close(self):
+        self.h = None  # the library keeps the table (cndp_node_ip4_lookup_fini frees it)
+
+    @staticmethod
+    def fini():
+        N.lib().cndp_node_ip4_lookup_fini()
+
+    def route_add(self, ip: int, depth: int, next_hop: int, next_node: int) -> int:
+        return N.lib().cne_node_ip4_route_add(ip & 0xFFFFFFFF, depth, next_hop, next_node)
+
+
+def cne_node_ip4_route_add(ip: int, depth: int, next_hop: int, next_node: int) -> int:
+    """The exported cne_node_ip4_route_add (ip4_lookup.c:259-289) on the node FIB."""
+    return N.lib().cne_node_ip4_route_add(ip & 0xFFFFFFFF, depth, next_hop, next_node)
+
+
 def node_ip4_route_add(fib: Fib, ip: int, depth: int, next_hop: int, next_node: int) -> int:
-    """cne_node_ip4_route_add (lib/usr/clib/nodes/ip4_lookup.c:259-289):
-    the FIB value embeds the next node id, val = (next_node << 16 | nh) & 0xFFFFFF."""
+    """cne_node_ip4_route_add's arithmetic (ip4_lookup.c:272) applied to any FIB
+    handle: val = (next_node << 16 | nh) & 0xFFFFFF.  For the node FIB itself use
+    cne_node_ip4_route_add (the C export)."""
     val = ((next_node << 16) | next_hop) & ((1 << 24) - 1)
     return fib.add(ip, depth, val)
 
 
 def node_ip4_add_input(fib: Fib, ip: int, depth: int, hop: int) -> int:
-    """cne_node_ip4_add_input (lib/cnet/ipv4/ip4_input.c:263-272):
+    """cne_node_ip4_add_input (lib/cnet/ipv4/ip4_input.c:263-272), the C export:
     nh = hop | (depth == 32 ? PROTO : FORWARD) << 24."""
-    edge = N.IP4_INPUT_NEXT_PROTO if depth == 32 else N.IP4_INPUT_NEXT_FORWARD
-    return fib.add(ip, depth, hop | (edge << 24))
+    return N.lib().cne_node_ip4_add_input(fib.h, ip & 0xFFFFFFFF, depth, hop)
 
 
 def node_ip6_add_input(fib6: Fib6, ip, depth: int, hop: int) -> int:
-    """cne_node_ip6_add_input (lib/cnet/ipv6/ip6_input.c:263-274), including
-    its `depth == 32` test (not 128) for the PROTO edge."""
-    edge = N.IP4_INPUT_NEXT_PROTO if depth == 32 else N.IP4_INPUT_NEXT_FORWARD
-    return fib6.add(ip, depth, hop | (edge << 24))
+    """cne_node_ip6_add_input (lib/cnet/ipv6/ip6_input.c:263-274), the C export,
+    including its `depth == 32` test (not 128) for the PROTO edge."""
+    return N.lib().cne_node_ip6_add_input(fib6.h, Fib6._ip(ip), depth, hop)

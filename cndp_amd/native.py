@@ -1,5 +1,5 @@
-"""ctypes binding of libcndp_gpu.so (the C-ABI declared in include/cndp_fib.h
-and include/cndp_gpu.h).
+"""ctypes binding of libcndp_gpu.so (the C-ABI declared in include/cndp_fib.h,
+include/cndp_node.h and include/cndp_gpu.h).
 
 The library is built in-tree (cndp_amd/lib/libcndp_gpu.so, see build.py).
 There is no fallback: if the shared object is missing, importing the
@@ -111,6 +111,7 @@ def lib():
         "cne_fib6_delete": (c_int, [c_void_p, c_void_p, c_uint8]),
         "cne_fib6_lookup_bulk": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
         "cne_fib6_get_dp": (c_void_p, [c_void_p]),
+        "cne_fib6_get_rib": (c_void_p, [c_void_p]),
         "cne_fib6_select_lookup": (c_int, [c_void_p, c_int]),
         "cndp_fib_image": (c_int, [c_void_p, POINTER(FibImage)]),
         "cndp_fib6_image": (c_int, [c_void_p, POINTER(FibImage)]),
@@ -120,6 +121,18 @@ def lib():
         "cndp_fib6_lookup_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
         "cndp_fib_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
         "cndp_fib6_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+        # cndp_node.h
+        "cne_node_ip4_route_add": (c_int, [c_uint32, c_uint8, c_uint16, c_int]),
+        "cne_node_ip4_rewrite_add": (c_int, [c_uint16, c_void_p, c_uint8, c_uint16]),
+        "ip4_rewrite_set_next": (c_int, [c_uint16, c_uint16]),
+        "cne_node_ip4_add_input": (c_int, [c_void_p, c_uint32, c_uint8, c_uint32]),
+        "cne_node_ip6_add_input": (c_int, [c_void_p, c_void_p, c_uint8, c_uint32]),
+        "cndp_node_ip4_lookup_init": (c_int, []),
+        "cndp_node_ip4_lookup_fib": (c_void_p, []),
+        "cndp_node_ip4_lookup_fini": (None, []),
+        "cndp_node_ip4_rewrite_get": (c_int, [c_uint16, c_void_p, POINTER(c_uint16), POINTER(c_uint16),
+                                              POINTER(c_uint16)]),
+        "cndp_node_ip4_rewrite_reset": (None, []),
         # cndp_gpu.h
         "cndp_gpu_init": (c_int, [c_int, POINTER(c_void_p)]),
         "cndp_gpu_fini": (None, [c_void_p]),
@@ -156,10 +169,10 @@ def exported_symbols():
     import re
     names = []
     inc = os.path.join(os.path.dirname(HERE), "include")
-    for h in ("cndp_fib.h", "cndp_gpu.h"):
+    for h in ("cndp_fib.h", "cndp_node.h", "cndp_gpu.h"):
         with open(os.path.join(inc, h)) as f:
             txt = f.read()
-        names += re.findall(r"^[A-Za-z_][\w \*]*?\b((?:cne|cndp)_\w+)\s*\(", txt, re.M)
+        names += re.findall(r"^[A-Za-z_][\w \*]*?\b((?:cne|cndp|ip4)_\w+)\s*\(", txt, re.M)
     return sorted(set(n for n in names if not n.endswith("_fn_t")))
 
 

@@ -18,7 +18,15 @@
  *   cne_fib.h:173   cne_fib_get_dp               same (host table image)
  *   cne_fib.h:183   cne_fib_get_rib              returns the build's RIB
  *   cne_fib.h:197   cne_fib_select_lookup        same (+ CNE_FIB_LOOKUP_GPU)
- *   cne_fib6.h:41-138  cne_fib6_*                same set for IPv6
+ *   cne_fib6.h:41-138  cne_fib6_*                same set for IPv6, including
+ *                                                cne_fib6_get_rib (cne_fib6.h:124)
+ *
+ * The type definitions below (enums, struct cne_fib_conf, the function
+ * typedefs) are token-compatible with the reference's and sit behind the
+ * reference's own include guards (_CNE_FIB_H_ / _CNE_FIB6_H_): a translation
+ * unit that already included CNDP's cne_fib.h / cne_fib6.h skips them, and the
+ * prototypes that follow are then checked by the compiler against the
+ * reference declarations (tests/test_abi.py::test_prototypes_match_reference).
  * Extensions (device-resident batches, no reference counterpart):
  *   cndp_fib_lookup_dev / cndp_fib6_lookup_dev, cndp_fib_sync / cndp_fib6_sync.
  */
@@ -31,13 +39,19 @@
 extern "C" {
 #endif
 
-#define CNE_FIB_MAXDEPTH 32   /* cne_fib.h:31 */
-#define CNE_FIB6_MAXDEPTH 128 /* private_fib6.h:28 */
-#define IPV6_ADDR_LEN 16
-
 struct cne_fib;
 struct cne_fib6;
 struct cne_rib;
+struct cne_rib6;
+
+#ifndef CNE_FIB6_MAXDEPTH
+#define CNE_FIB6_MAXDEPTH 128 /* private_fib6.h:28 */
+#endif
+
+#ifndef _CNE_FIB_H_
+#define _CNE_FIB_H_
+#define CNE_FIB_MAXDEPTH 32 /* cne_fib.h:31 */
+#define IPV6_ADDR_LEN 16    /* cne_inet.h:33 (an enum constant there) */
 
 /* cne_fib.h:34-38 */
 enum cne_fib_type {
@@ -98,6 +112,12 @@ struct cne_fib_conf {
         } trie;
     };
 };
+#endif /* _CNE_FIB_H_ */
+#ifndef _CNE_FIB6_H_
+#define _CNE_FIB6_H_
+#endif
+/* the GPU selector's value, also when CNDP's own cne_fib.h defined the enum */
+#define CNDP_FIB_LOOKUP_GPU 7
 
 /* ---- IPv4 (lib/usr/clib/fib/cne_fib.h) ---------------------------------- */
 struct cne_fib *cne_fib_create(const char *name, struct cne_fib_conf *conf);
@@ -118,6 +138,7 @@ int cne_fib6_delete(struct cne_fib6 *fib, const uint8_t ip[IPV6_ADDR_LEN], uint8
 int cne_fib6_lookup_bulk(struct cne_fib6 *fib, uint8_t ips[][IPV6_ADDR_LEN], uint64_t *next_hops,
                          int n);
 void *cne_fib6_get_dp(struct cne_fib6 *fib);
+struct cne_rib6 *cne_fib6_get_rib(struct cne_fib6 *fib);
 int cne_fib6_select_lookup(struct cne_fib6 *fib, enum cne_fib_lookup_type type);
 
 /* ---- build extensions ---------------------------------------------------
