@@ -3699,6 +3699,14 @@ struct cndp_gpu_ctx {
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
+    int spec_reset;       // the node state (last_type) restarts at 0 on the next cnet call
+    // Stream order of the context's scratch (speculation state, worklist,
+    // partition scratch): every call that uses it records ev_scratch on its
+    // stream, and a call on another stream first waits for that event, so
+    // calls on different streams never overlap on the shared scratch.
+    hipEvent_t ev_scratch;
+    hipStream_t scratch_stream;
+    int scratch_used;
     uint32_t *sp_small;   // [0] last_type, [1..65] class meta, [66..129] signature flags
     uint32_t *cs_wl;      // k_cnet_stream worklist ([0] = count, then frame indices)
     uint64_t cs_wl_cap;
@@ -3778,6 +3786,21 @@ static int set_device(int dev)
     return 0;
 }
 
+// order this call after the previous scratch user if it ran on another stream
+static int scratch_acquire(cndp_gpu_ctx_t *c, hipStream_t s)
+{
+    if (c->scratch_used && s != c->scratch_stream)
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_scratch, 0));
+    return 0;
+}
+static int scratch_release(cndp_gpu_ctx_t *c, hipStream_t s)
+{
+    HIP_TRY(hipEventRecord(c->ev_scratch, s));
+    c->scratch_stream = s;
+    c->scratch_used = 1;
+    return 0;
+}
+
 extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
 {
     if (!out)
@@ -3813,7 +3836,8 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     if (c->num_cu <= 0)
         c->num_cu = 256;
     if (hipMalloc((void **)&c->d_ttab, TAB_WORDS * 4) != hipSuccess ||
-        hipMalloc((void **)&c->d_reta, CNDP_RETA_MAX * 2) != hipSuccess) {
+        hipMalloc((void **)&c->d_reta, CNDP_RETA_MAX * 2) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_scratch, hipEventDisableTiming) != hipSuccess) {
         cndp_gpu_fini(c);
         return -ENOMEM;
     }
@@ -3831,6 +3855,9 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
     if (!c)
         return;
     hipSetDevice(c->dev);
+    hipDeviceSynchronize(); // nothing in flight may still use the scratch below
+    if (c->ev_scratch)
+        hipEventDestroy(c->ev_scratch);
     for (int k = 0; k < 3; k++)
         if (c->hs[k])
             hipStreamDestroy(c->hs[k]);
@@ -3930,6 +3957,15 @@ extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
         hipFree(t->dev_dir16);
     if (t->dev_pages)
         hipFree(t->dev_pages);
+    if (t->lk_stream)
+        hipStreamDestroy((hipStream_t)t->lk_stream);
+    if (t->lk_host)
+        hipHostFree(t->lk_host);
+    if (t->lk_dbuf)
+        hipFree(t->lk_dbuf);
+    t->lk_stream = nullptr;
+    t->lk_host = t->lk_hdev = t->lk_dbuf = nullptr;
+    t->lk_cap = 0;
     hipSetDevice(cur);
     t->dev_dir16 = t->dev_pages = nullptr;
     t->dev_cap_pages = 0;
@@ -4051,7 +4087,8 @@ static int dir16_sync(struct cndp_tbl *t, hipStream_t s, uint64_t d24_lo, uint64
     return 0;
 }
 
-extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
+// caller holds t->dev_lock
+static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
 {
     if (!t || !t->tbl24)
         return -EINVAL;
@@ -4106,10 +4143,23 @@ extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
     return 0;
 }
 
+extern "C" int cndp_tbl_dev_sync(struct cndp_tbl *t, void *stream)
+{
+    if (!t || !t->tbl24)
+        return -EINVAL;
+    pthread_mutex_lock(&t->dev_lock);
+    const int r = tbl_dev_sync_locked(t, stream);
+    pthread_mutex_unlock(&t->dev_lock);
+    return r;
+}
+
 static inline uint32_t blocks_for(uint64_t n, uint32_t threads)
 {
     return (uint32_t)((n + threads - 1) / threads);
 }
+
+static int tbl_lookup4_launch(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s);
+static int tbl_lookup6_launch(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n, hipStream_t s);
 
 extern "C" int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh,
                                     uint32_t n, void *stream)
@@ -4117,9 +4167,22 @@ extern "C" int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uin
     int r = cndp_tbl_dev_sync(t, stream);
     if (r)
         return r;
+    return tbl_lookup4_launch(t, ips, nh, n, (hipStream_t)stream);
+}
+
+extern "C" int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n,
+                                    void *stream)
+{
+    int r = cndp_tbl_dev_sync(t, stream);
+    if (r)
+        return r;
+    return tbl_lookup6_launch(t, ips, nh, n, (hipStream_t)stream);
+}
+
+static int tbl_lookup4_launch(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s)
+{
     if (n == 0)
         return 0;
-    hipStream_t s = (hipStream_t)stream;
     const uint32_t g = blocks_for(n, 256);
     switch (t->nh_sz) {
     case 0:
@@ -4143,15 +4206,10 @@ extern "C" int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uin
     return 0;
 }
 
-extern "C" int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n,
-                                    void *stream)
+static int tbl_lookup6_launch(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n, hipStream_t s)
 {
-    int r = cndp_tbl_dev_sync(t, stream);
-    if (r)
-        return r;
     if (n == 0)
         return 0;
-    hipStream_t s = (hipStream_t)stream;
     const uint32_t g = blocks_for(n, 256);
     switch (t->nh_sz) {
     case 1:
@@ -4171,41 +4229,103 @@ extern "C" int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips, uint
     return 0;
 }
 
-// host-array lookups: stage through device scratch on the current device
-static int lookup_host_common(struct cndp_tbl *t, const void *ips, size_t ip_bytes, uint64_t *nh,
+// Host-array lookups (cne_fib_lookup_bulk / cne_fib6_lookup_bulk).  The
+// reference lookup reads the table in place and cannot fail
+// (cne_fib.c:111-116); callers like examples/cndpfwd/l3-fwd.c:85 call it per
+// burst from every forwarding thread on one FIB and ignore the return code.
+// So: one lock per table (device mirror + staging), the mirror's own device
+// (not the caller's current one), staging allocated once per table, and on
+// any failure every next hop is set to the FIB default before the negative
+// errno is returned.  Small calls (the per-burst case) stage keys and next
+// hops in pinned, mapped host memory that the kernel reads and writes in
+// place: one launch and one stream wait, no DMA set-up.  Larger calls move
+// the keys and next hops by DMA through device scratch.
+#define LK_MAPPED_MAX 16384u   // lookups per round through mapped staging
+#define LK_DMA_CHUNK (1u << 20) // lookups per round through device scratch
+
+static int lookup_host_locked(struct cndp_tbl *t, const uint8_t *ips, uint32_t key_sz, uint64_t *nh,
                               uint32_t n, int v6)
 {
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-        return -ENODEV;
-    void *d_ip = nullptr;
-    uint64_t *d_nh = nullptr;
-    HIP_TRY(hipMalloc(&d_ip, ip_bytes));
-    if (hipMalloc((void **)&d_nh, (size_t)n * 8) != hipSuccess) {
-        hipFree(d_ip);
-        return -ENOMEM;
+    if (!t->lk_stream) {
+        hipStream_t st = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        t->lk_stream = st;
     }
-    int r = 0;
-    if (hipMemcpy(d_ip, ips, ip_bytes, hipMemcpyHostToDevice) != hipSuccess)
-        r = -EIO;
-    if (!r)
-        r = v6 ? cndp_tbl_lookup6_dev(t, (const uint8_t *)d_ip, d_nh, n, nullptr)
-               : cndp_tbl_lookup4_dev(t, (const uint32_t *)d_ip, d_nh, n, nullptr);
-    if (!r && hipMemcpy(nh, d_nh, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
-        r = -EIO;
-    hipFree(d_ip);
-    hipFree(d_nh);
+    hipStream_t s = (hipStream_t)t->lk_stream;
+    if (!t->lk_host) {
+        void *h = nullptr, *d = nullptr;
+        HIP_TRY(hipHostMalloc(&h, (size_t)LK_MAPPED_MAX * (16 + 8), hipHostMallocMapped));
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            hipHostFree(h);
+            return -EIO;
+        }
+        t->lk_host = (uint8_t *)h;
+        t->lk_hdev = (uint8_t *)d;
+        t->lk_cap = LK_MAPPED_MAX;
+    }
+    int r = tbl_dev_sync_locked(t, s);
+    if (r)
+        return r;
+    if (n <= LK_MAPPED_MAX) {
+        uint8_t *hk = t->lk_host, *hn = t->lk_host + (size_t)LK_MAPPED_MAX * key_sz;
+        memcpy(hk, ips, (size_t)n * key_sz);
+        const uint8_t *dk = t->lk_hdev;
+        uint64_t *dn = (uint64_t *)(t->lk_hdev + (size_t)LK_MAPPED_MAX * key_sz);
+        r = v6 ? tbl_lookup6_launch(t, dk, dn, n, s) : tbl_lookup4_launch(t, (const uint32_t *)dk, dn, n, s);
+        if (r)
+            return r;
+        HIP_TRY(hipStreamSynchronize(s));
+        memcpy(nh, hn, (size_t)n * 8);
+        return 0;
+    }
+    if (!t->lk_dbuf)
+        HIP_TRY(hipMalloc((void **)&t->lk_dbuf, (size_t)LK_DMA_CHUNK * (16 + 8)));
+    for (uint32_t i0 = 0; i0 < n; i0 += LK_DMA_CHUNK) {
+        const uint32_t c = n - i0 < LK_DMA_CHUNK ? n - i0 : LK_DMA_CHUNK;
+        uint8_t *dk = t->lk_dbuf;
+        uint64_t *dn = (uint64_t *)(t->lk_dbuf + (size_t)LK_DMA_CHUNK * key_sz);
+        HIP_TRY(hipMemcpyAsync(dk, ips + (size_t)i0 * key_sz, (size_t)c * key_sz, hipMemcpyHostToDevice, s));
+        r = v6 ? tbl_lookup6_launch(t, dk, dn, c, s) : tbl_lookup4_launch(t, (const uint32_t *)dk, dn, c, s);
+        if (r)
+            return r;
+        HIP_TRY(hipMemcpyAsync(nh + i0, dn, (size_t)c * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
+static int lookup_host_common(struct cndp_tbl *t, const void *ips, size_t key_sz, uint64_t *nh, uint32_t n,
+                              int v6)
+{
+    int r = 0, ndev = 0, cur = -1;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        r = -ENODEV;
+    } else {
+        hipGetDevice(&cur);
+        pthread_mutex_lock(&t->dev_lock);
+        const int dev = t->dev_id >= 0 ? t->dev_id : (cur >= 0 ? cur : 0);
+        if (dev != cur && hipSetDevice(dev) != hipSuccess)
+            r = -ENODEV;
+        if (!r)
+            r = lookup_host_locked(t, (const uint8_t *)ips, (uint32_t)key_sz, nh, n, v6);
+        pthread_mutex_unlock(&t->dev_lock);
+        if (cur >= 0 && dev != cur)
+            hipSetDevice(cur);
+    }
+    if (r) // the caller may ignore the code: leave it the default next hop
+        for (uint32_t i = 0; i < n; i++)
+            nh[i] = t->def_nh;
     return r;
 }
 
 extern "C" int cndp_tbl_lookup4_host(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n)
 {
-    return lookup_host_common(t, ips, (size_t)n * 4, nh, n, 0);
+    return lookup_host_common(t, ips, 4, nh, n, 0);
 }
 
 extern "C" int cndp_tbl_lookup6_host(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n)
 {
-    return lookup_host_common(t, ips, (size_t)n * 16, nh, n, 1);
+    return lookup_host_common(t, ips, 16, nh, n, 1);
 }
 
 // ---- classify ---------------------------------------------------------------
@@ -4269,6 +4389,10 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
     return 0;
 }
 
+static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, hipStream_t s);
+static int classify_l3(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, hipStream_t s, uint16_t *rw_tx,
+                       bool *fused);
+
 // rw_tx != nullptr asks for ip4_rewrite fused into the wave-tile kernel
 // (256-packet bursts); *fused says whether that kernel ran
 static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream, uint16_t *rw_tx,
@@ -4320,6 +4444,19 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
     a.rxmeta = b->mode == CNDP_MODE_CNET ? b->rxmeta : nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (b->mode == CNDP_MODE_CNET) {
+        if ((r = scratch_acquire(c, s)))
+            return r;
+        r = classify_cnet(c, b, a, s);
+        const int r2 = scratch_release(c, s);
+        return r ? r : r2;
+    }
+    return classify_l3(c, b, a, s, rw_tx, fused);
+}
+
+static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, hipStream_t s)
+{
+    int r;
+    {
         uint32_t g = blocks_for(b->n, CNET_THREADS);
         const uint32_t cap = (uint32_t)c->num_cu * 2u;
         if (g > cap)
@@ -4327,6 +4464,10 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
         const uint32_t B = c->spec_burst;
         if (B && (r = spec_scratch(c, b->n, ((uint64_t)b->n + B - 1) / B)))
             return r;
+        if (c->spec_reset && c->sp_small) { // CNDP_TUNE_CNET_SPEC was set: a new graph
+            HIP_TRY(hipMemsetAsync(c->sp_small, 0, 4, s));
+            c->spec_reset = 0;
+        }
         if (B) {
             a.spec_t16 = (uint16_t *)c->sp_pt;
             a.spec_nh = c->sp_nh;
@@ -4440,7 +4581,15 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
                                    (const uint32_t *)Sblk, (const uint32_t *)c->sp_S);
             }
         }
-    } else {
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+static int classify_l3(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, hipStream_t s, uint16_t *rw_tx,
+                       bool *fused)
+{
+    {
         uint32_t g = blocks_for(b->n, FAST_THREADS);
         // auto: 2 blocks per CU for the streamed kernel, 4 for the others
         // (the fused rewrite runs the split-gather tile kernel)
@@ -5168,6 +5317,8 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
         HIP_TRY(hipMemsetAsync(bin_start, 0, (size_t)(nbt + 1) * 4, s));
         return 0;
     }
+    if ((r = scratch_acquire(c, s)))
+        return r;
     hipLaunchKernelGGL(k_part_hist, dim3(tiles), dim3(PART_THREADS), 0, s, bin_of, n, nbt, tiles,
                        c->d_part);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, c->d_part, (uint32_t)need, tiles, nbt,
@@ -5175,7 +5326,7 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
     hipLaunchKernelGGL(k_part_scatter, dim3(tiles), dim3(PART_THREADS), 0, s, bin_of, n, nbt, tiles,
                        c->d_part, order);
     HIP_TRY(hipGetLastError());
-    return 0;
+    return scratch_release(c, s);
 }
 
 extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
@@ -5226,8 +5377,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0)
             return -EINVAL;
         c->spec_burst = (uint32_t)value;
-        if (c->sp_small) // a new graph: ctx->last_type starts at 0 again
-            HIP_TRY(hipMemset(c->sp_small, 0, 4));
+        c->spec_reset = 1; // a new graph: ctx->last_type starts at 0 again (stream-ordered, next call)
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

@@ -95,6 +95,8 @@ static int tbl_init(struct cndp_tbl *t, uint32_t nh_sz, uint32_t is_trie, uint32
                     uint64_t def_nh)
 {
     memset(t, 0, sizeof(*t));
+    pthread_mutex_init(&t->dev_lock, NULL);
+    t->def_nh = def_nh;
     t->nh_sz = nh_sz;
     t->is_trie = is_trie;
     t->num_tbl8 = num_tbl8;
@@ -108,6 +110,7 @@ static int tbl_init(struct cndp_tbl *t, uint32_t nh_sz, uint32_t is_trie, uint32
         free(t->tbl24);
         free(t->tbl8);
         free(t->used);
+        pthread_mutex_destroy(&t->dev_lock);
         return -ENOMEM;
     }
     uint64_t v = def_nh << 1;
@@ -130,6 +133,7 @@ static void tbl_fini(struct cndp_tbl *t)
     free(t->page_of);
     free(t->pages);
     free(t->page_free);
+    pthread_mutex_destroy(&t->dev_lock);
     memset(t, 0, sizeof(*t));
 }
 

@@ -12,6 +12,7 @@
 #ifndef CNDP_FIB_INTERNAL_H
 #define CNDP_FIB_INTERNAL_H
 
+#include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -56,6 +57,16 @@ struct cndp_tbl {
     void *dev_dir16;
     void *dev_pages;
     uint32_t dev_cap_pages;
+    /* host-array lookups (cne_fib_lookup_bulk): callers are many forwarding
+     * threads on one FIB (examples/cndpfwd/l3-fwd.c:85), so the device mirror
+     * state and the staging below are guarded by dev_lock */
+    uint64_t def_nh;        /* written to every next hop of a lookup that cannot run */
+    pthread_mutex_t dev_lock;
+    void *lk_stream;        /* hipStream_t (non-blocking) of host-array lookups */
+    uint8_t *lk_host;       /* pinned + mapped staging: keys, then 8-B next hops */
+    uint8_t *lk_hdev;       /* device address of lk_host */
+    uint8_t *lk_dbuf;       /* device scratch for large lookups (DMA path) */
+    uint64_t lk_cap;        /* lookups one staging round holds */
 };
 
 struct cne_fib {

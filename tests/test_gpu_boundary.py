@@ -1,0 +1,181 @@
+"""GPU tests of the drop-in boundary: the node control API driving the GPU
+paths, the host-array FIB lookups (per-burst callers, many threads), and the
+stream order of a context's scratch.  Everything goes through the C-ABI."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from cndp_amd import native as N
+from cndp_amd import pktgen
+from oracle import oracle as O
+
+from helpers import CNET_DEF, assert_same, cnet_fibs, l3fwd_fib, l3fwd_oracle_tables, oracle_classify
+
+pytestmark = pytest.mark.gpu
+
+
+def test_node_fib_ladder_gpu(gpu):
+    """fib_test.c:239-288 check_fib through the exported cne_node_ip4_route_add
+    on the library-owned node FIB, looked up by the GPU cne_fib_lookup_bulk."""
+    from test_oracle_golden import _ladder4
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    NodeFib.fini()
+    nf = NodeFib()
+    try:
+        _ladder4(nf.lookup_bulk, lambda ip, d, nh: cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE),
+                 nf.delete, def_nh=N.IP4_LOOKUP_NEXT_PKT_DROP << 16)
+    finally:
+        NodeFib.fini()
+
+
+def _routes_fib(seed, nh_sz=N.CNE_FIB_DIR24_8_4B):
+    from cndp_amd.fib import Fib
+    rng = np.random.default_rng(seed)
+    f = Fib(f"t{seed}", N.CNE_FIB_DIR24_8, default_nh=9, max_routes=4096, nh_sz=nh_sz, num_tbl8=512)
+    routes = {}
+    for _ in range(500):
+        d = int(rng.integers(8, 33))
+        ip = (0x0A000000 | int(rng.integers(0, 1 << 24))) & (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+        nh = int(rng.integers(0, 1 << 20))
+        if f.add(ip, d, nh) == 0:
+            routes[(ip, d)] = nh
+    return f, [(ip, d, nh) for (ip, d), nh in routes.items()]
+
+
+def test_fib_lookup_bulk_many_threads(gpu):
+    """examples/cndpfwd/l3-fwd.c:85 calls cne_fib_lookup_bulk per burst from
+    every forwarding thread on one FIB.  Eight threads start on a FIB that has
+    no device mirror yet (the first lookups race to create it) and issue
+    4-, 256- and 5000-key calls; every answer equals brute-force LPM."""
+    f, routes = _routes_fib(21)
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, 2**32, size=1 << 16, dtype=np.uint64).astype(np.uint32)
+    keys[::2] = 0x0A000000 | (keys[::2] & 0x00FFFFFF)
+    want = O.lpm4_bruteforce(routes, 9, keys)
+    errors = []
+
+    def worker(t):
+        try:
+            r = np.random.default_rng(100 + t)
+            for it in range(60):
+                n = (4, 256, 5000)[it % 3]
+                lo = int(r.integers(0, keys.size - n))
+                ips = keys[lo:lo + n].copy()
+                out = np.zeros(n, np.uint64)
+                rc = f._L.cne_fib_lookup_bulk(f.h, ips.ctypes.data, out.ctypes.data, n)
+                if rc != 0 or not np.array_equal(out, want[lo:lo + n]):
+                    errors.append((t, it, rc))
+                    return
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:4]
+
+
+def test_fib_lookup_bulk_large_and_v6(gpu):
+    """Calls above the mapped-staging size (DMA path, chunked) and IPv6."""
+    f, routes = _routes_fib(22)
+    rng = np.random.default_rng(6)
+    ips = rng.integers(0, 2**32, size=(1 << 20) + 12345, dtype=np.uint64).astype(np.uint32)
+    ips[::2] = 0x0A000000 | (ips[::2] & 0x00FFFFFF)
+    got = f.lookup_bulk(ips)
+    sel = slice(0, None, 97)
+    assert np.array_equal(got[sel], O.lpm4_bruteforce(routes, 9, ips[sel]))
+    t24, t8 = f.image()
+    assert np.array_equal(got, O.dir24_8_lookup(t24, t8, ips))
+    import os
+    from cndp_amd.fib import Fib6
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "lpm6_1000.npz"))
+    f6 = Fib6("l6b", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 14)
+    for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
+        assert f6.add(bytes(ip), int(d), int(nh)) == 0
+    for n in (1, 4, 256, 20000):
+        assert np.array_equal(f6.lookup_bulk(g["ip"][:n]), g["nh"][:n].astype(np.uint64))
+
+
+def test_node_rewrite_table_drives_gpu_rewrite(gpu):
+    """A context without a table of its own rewrites with the table filled
+    through the exported ip4_rewrite_set_next / cne_node_ip4_rewrite_add
+    (ip4_rewrite.c:266-312), and follows later changes to it."""
+    from cndp_amd.classify import Classifier
+    L = N.lib()
+    L.cndp_node_ip4_rewrite_reset()
+    fib, vals = l3fwd_fib()
+    t4 = l3fwd_oracle_tables(vals)
+    cl = Classifier(0)
+    cl.set_fib(fib)
+    tbl = np.zeros(64, O.REWRITE_NH)
+    for p in range(4):
+        assert L.ip4_rewrite_set_next(p, p + 1) == 0
+    rng = np.random.default_rng(8)
+    for nh in range(40):
+        data = rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        buf = ctypes.create_string_buffer(data, 12)
+        assert L.cne_node_ip4_rewrite_add(nh, buf, 12, nh % 4) == 0
+        tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = 12, nh % 4 + 1, 1
+        tbl[nh]["rewrite_data"][:12] = np.frombuffer(data, np.uint8)
+    for step in range(2):
+        fr = pktgen.packed_ipv4(30000, routes=pktgen.l3fwd_routes(), seed=40 + step)
+        ref = oracle_classify(O.MODE_L3FWD, fr, tables4=t4)
+        host = fr.slab.numpy().copy()
+        ref_tx = O.ip4_rewrite(host, fr.n, ref["nh"], tbl, burst=256)
+        dfr = pktgen.Frames(fr.slab.to(gpu), fr.n, stride=64)
+        out = cl.classify(dfr, N.CNDP_MODE_L3FWD)
+        tx = cl.ip4_rewrite(dfr, out["nh"], burst=256)
+        torch.cuda.synchronize()
+        assert np.array_equal(tx.cpu().numpy().view(np.uint16), ref_tx)
+        assert np.array_equal(dfr.slab.cpu().numpy(), host)
+        # change next hop 3 (new data, port 2) between the two batches
+        data = bytes(range(100, 112))
+        assert L.cne_node_ip4_rewrite_add(3, ctypes.create_string_buffer(data, 12), 12, 2) == 0
+        tbl[3]["tx_node"] = 3
+        tbl[3]["rewrite_data"][:12] = np.frombuffer(data, np.uint8)
+    cl.close()
+    L.cndp_node_ip4_rewrite_reset()
+
+
+def test_scratch_stream_order(gpu):
+    """One context, cnet calls alternating between two streams and the host
+    path with no synchronisation in between: the speculation state carries
+    from call to call exactly as if the calls ran one after another."""
+    from cndp_amd.classify import Classifier
+    from test_gpu_parity import _gtp_mix
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    cl = Classifier(0)
+    cl.set_fib(fib, fib6)
+    cl.set_tuning(cnet_spec=256)
+    fr = _gtp_mix(256 * 200, routes, v6, gpu, seed=3)
+    parts = 6
+    cut = [k * (fr.n // parts) // 256 * 256 for k in range(parts)] + [fr.n]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs, refs = [], []
+    st = np.zeros(1, np.uint16)
+    host_slab = fr.slab.cpu().numpy()
+    host_off = fr.offsets.cpu().numpy().astype(np.uint64)
+    prts = [pktgen.Frames(fr.slab, cut[k + 1] - cut[k], offsets=fr.offsets[cut[k]:cut[k + 1]].contiguous())
+            for k in range(parts)]
+    outb = [cl.alloc_outputs(p.n, 64, device=gpu) for p in prts]
+    torch.cuda.synchronize()
+    for k in range(parts):
+        lo, hi = cut[k], cut[k + 1]
+        refs.append(oracle_classify(O.MODE_CNET, prts[k], tables4=t4, tables6=t6, spec_burst=256, spec_state=st))
+        if k % 3 == 2:   # the host path (its own streams) in the middle of the chain
+            o = cl.classify_host(host_slab, hi - lo, N.CNDP_MODE_CNET, offsets=host_off[lo:hi].copy())
+        else:
+            s = s1 if k % 3 == 0 else s2
+            o = cl.classify(prts[k], N.CNDP_MODE_CNET, out=outb[k], stream=s.cuda_stream)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert_same(o, r)
+    cl.close()
