@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "fib_internal.h"
 #include "node_internal.h"
@@ -3676,6 +3677,7 @@ __global__ __launch_bounds__(PART_THREADS) void k_part_scatter(const uint16_t *_
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+#define CNDP_MAX_REGIONS 16
 struct cndp_gpu_ctx {
     int dev;
     uint8_t key[CNDP_RSS_KEY_LEN];
@@ -3700,6 +3702,7 @@ struct cndp_gpu_ctx {
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
     uint32_t spec_burst;  // CNDP_TUNE_CNET_SPEC: ptype-node speculation burst (0 = off)
     int spec_reset;       // the node state (last_type) restarts at 0 on the next cnet call
+    int mbuf_hash;        // CNDP_TUNE_MBUF_HASH: cndp_gpu_l3fwd_mbufs also writes m->hash
     // Stream order of the context's scratch (speculation state, worklist,
     // partition scratch): every call that uses it records ev_scratch on its
     // stream, and a call on another stream first waits for that event, so
@@ -3707,6 +3710,12 @@ struct cndp_gpu_ctx {
     hipEvent_t ev_scratch;
     hipStream_t scratch_stream;
     int scratch_used;
+    // host regions registered with cndp_gpu_host_register (zero-copy mbuf queues)
+    struct {
+        uint8_t *host, *dev;
+        uint64_t len;
+    } reg[CNDP_MAX_REGIONS];
+    int n_reg;
     uint32_t *sp_small;   // [0] last_type, [1..65] class meta, [66..129] signature flags
     uint32_t *cs_wl;      // k_cnet_stream worklist ([0] = count, then frame indices)
     uint64_t cs_wl_cap;
@@ -5086,7 +5095,8 @@ extern "C" int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *c, void *const *mbufs, uint3
         const uint32_t et = ((uint32_t)w[12] << 8) | w[13];
         // pktdev_rx.c:24-34 l3_ptype
         *(uint32_t *)(m + MB_PTYPE) = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
-        *(uint32_t *)(m + MB_HASH) = c->m_hres[c->m_cap + i];
+        if (c->mbuf_hash) // no reference node writes m->hash: opt-in (CNDP_TUNE_MBUF_HASH)
+            *(uint32_t *)(m + MB_HASH) = c->m_hres[c->m_cap + i];
         const uint32_t val = c->m_hres[i];
         if (val == CNDP_NH_INVALID) { // pkt_cls.c: not IPv4 -> pkt_drop
             edges[i] = CNDP_MBUF_EDGE_CLS_DROP;
@@ -5250,13 +5260,18 @@ extern "C" int cndp_gpu_host_register(cndp_gpu_ctx_t *c, void *ptr, uint64_t len
         fprintf(stderr, "cndp_gpu: hipHostRegister failed: %s\n", hipGetErrorString(e));
         return -ENOMEM;
     }
-    if (dev_ptr) {
-        void *d = nullptr;
-        if (hipHostGetDevicePointer(&d, ptr, 0) != hipSuccess) {
-            hipHostUnregister(ptr);
-            return -EIO;
-        }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, ptr, 0) != hipSuccess) {
+        hipHostUnregister(ptr);
+        return -EIO;
+    }
+    if (dev_ptr)
         *dev_ptr = d;
+    if (c->n_reg < CNDP_MAX_REGIONS) { // remembered for zero-copy mbuf queues
+        c->reg[c->n_reg].host = (uint8_t *)ptr;
+        c->reg[c->n_reg].dev = (uint8_t *)d;
+        c->reg[c->n_reg].len = len;
+        c->n_reg++;
     }
     return 0;
 }
@@ -5268,6 +5283,11 @@ extern "C" int cndp_gpu_host_unregister(cndp_gpu_ctx_t *c, void *ptr)
     int r = set_device(c->dev);
     if (r)
         return r;
+    for (int k = 0; k < c->n_reg; k++)
+        if (c->reg[k].host == ptr) {
+            c->reg[k] = c->reg[--c->n_reg];
+            break;
+        }
     return hipHostUnregister(ptr) == hipSuccess ? 0 : -ENOENT;
 }
 
@@ -5329,6 +5349,583 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
     return scratch_release(c, s);
 }
 
+// ---------------------------------------------------------------------------
+// Asynchronous node path over pktmbuf_t bursts (cndp_gpu_mq_*, cndp_gpu.h).
+// Bursts fill the open batch slot on the host (frame offsets, or staged frame
+// bytes); a full slot -- or, at poll time, a partly filled one when nothing
+// is in flight or it is older than max_delay_us -- is launched on the
+// queue's stream: H2D of the slot's offsets / staging, the kernels, one D2H
+// of compact per-packet records, an event.  poll checks the oldest slot's
+// event without waiting and writes the records back into the mbufs.
+// ---------------------------------------------------------------------------
+#define MQ_FREE 0
+#define MQ_OPEN 1
+#define MQ_FLIGHT 2
+#define MQ_DONE 3
+#define MQ_BURST 256u       // CNE_GRAPH_BURST_SIZE (cne_graph.h:30)
+#define MQ_WIN4 64u         // ip4_lookup staged bytes (it reads bytes 22..33)
+#define MQ_RUNS_MAX 512u    // cnet: runs of equal-size bursts per batch
+
+// ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
+// mtod + 14 + 16, priv1 = {nh = val & 0xffff, ttl, hdr_checksum}, edge = val >> 16
+__global__ __launch_bounds__(256) void k_mq_ip4_lookup(const uint8_t *__restrict__ slab, uint64_t slab_len,
+                                                       const uint64_t *__restrict__ off, uint32_t n,
+                                                       const uint32_t *__restrict__ t24,
+                                                       const uint32_t *__restrict__ t8,
+                                                       const uint32_t *__restrict__ d16,
+                                                       const uint32_t *__restrict__ pages, uint64_t *priv1,
+                                                       uint16_t *edge)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint64_t base = off[i];
+        const uint8_t *p = slab + base;
+        const uint64_t avail = base < slab_len ? slab_len - base : 0;
+        uint32_t ttl, ck, dip;
+        if (avail >= 36 && (base & 15u) == 0) { // two loads (one PCIe read each when zero-copy)
+            const u32x4 q = *(const u32x4 *)(p + 16); // bytes 16..31
+            const uint32_t w8 = *(const uint32_t *)(p + 32);
+            ttl = (q.y >> 16) & 0xffu;
+            ck = q.z & 0xffffu;
+            dip = bswap32(alignb(w8, q.w, 2));
+        } else {
+            ttl = gbyte(p, avail, 22);
+            ck = gbyte(p, avail, 24) | (gbyte(p, avail, 25) << 8);
+            dip = (gbyte(p, avail, 30) << 24) | (gbyte(p, avail, 31) << 16) | (gbyte(p, avail, 32) << 8) |
+                  gbyte(p, avail, 33);
+        }
+        const uint32_t val = d16 ? lpm4d(d16, pages, t8, dip) : lpm4(t24, t8, dip);
+        priv1[i] = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
+        edge[i] = (uint16_t)(val >> 16);
+    }
+}
+
+// cnet records: {packet_type, rxmeta, data_len | edge << 16 | node << 24, hash}.
+// Frames an input node took get data_len = total_length (ip4_input.c:121-124)
+// or payload_len (ip6_input.c:121-124), read at mtod after eth_rx's
+// pktmbuf_adj_offset(l2_len) (eth_rx.c:62, pktmbuf.h:955-984: skipped when
+// l2_len exceeds data_len or the buffer).  Which input node: ip4_input for
+// the low ptype bytes of its p_nxt entries (0x11, 0x31, 0x91), ip6_input for
+// 0x41, 0xc1, 0xe1 -- the ptype node's speculation only ever sends a frame
+// to the edge of a type with the same low byte (ptype.c:109-110).
+// A frame shorter than its L2 header (l2_len > data_len) keeps its data_off,
+// so the input node takes the bytes at the frame start for its IP header:
+// its length/checksum test and lookup are redone here from there
+// (ip4_input.c:121-150, ip6_input.c:121-150, trie.h:126-134).
+struct MqTables {
+    const uint32_t *t24, *t8, *d16, *pages, *t24_6, *t8_6;
+    uint32_t buf_len;
+};
+
+__device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t o, bool v6, const MqTables &t)
+{
+    if (!v6) {
+        const uint32_t x0 = gld32(slab, slab_len, o);
+        const uint32_t hl = x0 & 0xfu;
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < hl; k++) {
+            const uint32_t x = k == 0 ? x0 : gld32(slab, slab_len, o + 4 * k);
+            sum += (x & 0xffffu) + (x >> 16);
+        }
+        sum = (sum >> 16) + (sum & 0xffffu);
+        sum = (sum >> 16) + (sum & 0xffffu);
+        const bool ok = bswap16(x0 >> 16) < t.buf_len && ((~sum) & 0xffffu) == 0u;
+        const uint32_t dip = ok ? bswap32(gld32(slab, slab_len, o + 16)) : 0u;
+        return t.d16 ? lpm4d(t.d16, t.pages, t.t8, dip) : lpm4(t.t24, t.t8, dip);
+    }
+    const bool ok = ((gbyte(slab, slab_len, o + 4) << 8) | gbyte(slab, slab_len, o + 5)) < t.buf_len;
+    uint32_t e = t.t24_6[ok ? (gbyte(slab, slab_len, o + 24) << 16) | (gbyte(slab, slab_len, o + 25) << 8) |
+                                  gbyte(slab, slab_len, o + 26)
+                            : 0u];
+    for (uint32_t j = 3; (e & 1u) && j < 16; j++)
+        e = t.t8_6[(e >> 1) * 256u + (ok ? gbyte(slab, slab_len, o + 24 + j) : 0u)];
+    return e >> 1;
+}
+
+__global__ __launch_bounds__(256) void k_mq_cnet_post(const uint8_t *__restrict__ slab, uint64_t slab_len,
+                                                      const uint64_t *__restrict__ off,
+                                                      const uint32_t *__restrict__ lens, uint32_t n,
+                                                      const uint32_t *__restrict__ ptype,
+                                                      const uint32_t *__restrict__ rxmeta,
+                                                      const uint8_t *__restrict__ edge,
+                                                      const uint32_t *__restrict__ hash, u32x4 *rec, MqTables tb)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t pt = ptype[i], rm = rxmeta[i], e8 = edge[i];
+        uint32_t node, e, dlen = 0;
+        if (e8 & 0x80u) {
+            node = CNDP_MQ_NODE_PTYPE;
+            e = e8 & 0x7fu;
+        } else {
+            const uint32_t low = pt & 0xffu;
+            const bool v6 = low == 0x41u || low == 0xc1u || low == 0xe1u;
+            node = v6 ? CNDP_MQ_NODE_IP6 : CNDP_MQ_NODE_IP4;
+            e = e8;
+            const uint32_t l2 = rm & 0x7fu, dl = lens[i] & 0xffffu, room = lens[i] >> 16;
+            const bool adj = l2 <= dl && l2 <= room;
+            const uint64_t o = off[i] + (adj ? l2 : 0u) + (v6 ? 4u : 2u);
+            dlen = (gbyte(slab, slab_len, o) << 8) | gbyte(slab, slab_len, o + 1);
+            if (!adj)
+                e = mq_input_at(slab, slab_len, off[i], v6, tb) >> 24;
+        }
+        u32x4 r;
+        r.x = pt;
+        r.y = rm;
+        r.z = dlen | (e << 16) | (node << 24);
+        r.w = hash ? hash[i] : 0u;
+        rec[i] = r;
+    }
+}
+
+struct MqSlot {
+    int state;
+    uint32_t n, polled, buf_len;
+    uint64_t t_open_ns;    // when the first mbuf went in
+    uint64_t stage_used;   // staged bytes
+    uint32_t nrun;         // cnet: runs of equal-size bursts (each ends with at most one short burst)
+    uint32_t run_B[MQ_RUNS_MAX], run_n[MQ_RUNS_MAX];
+    uint8_t run_closed;
+    void **mb;             // host
+    uint8_t *h;            // pinned: offsets | lens | staging | records
+    uint8_t *d;            // device: offsets | lens | staging | outputs | records
+    hipEvent_t ev;
+};
+
+struct cndp_gpu_mq {
+    cndp_gpu_ctx_t *c;
+    struct cndp_mq_conf conf;
+    hipStream_t s;
+    const uint8_t *r_host, *r_dev; // zero-copy region (NULL: staged)
+    uint64_t r_len;
+    uint32_t stage;                // staged bytes reserved per frame
+    // byte offsets inside each slot's host (H) and device (D) blocks
+    uint64_t h_off, h_len, h_stage, h_rec, h_bytes;
+    uint64_t d_off, d_len, d_stage, d_nh, d_edge, d_pt, d_rm, d_hash, d_rec, d_bytes;
+    uint32_t head, open, in_flight; // head: oldest slot not fully polled
+    uint32_t pending;
+    MqSlot slot[CNDP_MQ_DEPTH_MAX];
+};
+
+static uint64_t now_ns()
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+static inline uint64_t al64(uint64_t x) { return (x + 63u) & ~63ull; }
+
+extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *conf, cndp_gpu_mq_t **out)
+{
+    if (!c || !conf || !out)
+        return -EINVAL;
+    *out = nullptr;
+    struct cndp_mq_conf k = *conf;
+    if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET)
+        return -EINVAL;
+    if (k.flags & ~CNDP_MQ_F_HASH)
+        return -EINVAL;
+    k.batch = k.batch ? k.batch : 8192u;
+    k.depth = k.depth ? k.depth : 4u;
+    k.max_delay_us = k.max_delay_us ? k.max_delay_us : 50u;
+    k.stage_max = k.stage_max ? k.stage_max : 2048u;
+    if (k.batch < MQ_BURST || k.batch > (1u << 24) || k.depth < 2 || k.depth > CNDP_MQ_DEPTH_MAX ||
+        k.stage_max < 64 || k.stage_max > 65535)
+        return -EINVAL;
+    if (k.mode == CNDP_MQ_IP4_LOOKUP ? !c->fib4 : (!c->fib4 || !c->fib6))
+        return -EINVAL;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    cndp_gpu_mq_t *q = (cndp_gpu_mq_t *)calloc(1, sizeof(*q));
+    if (!q)
+        return -ENOMEM;
+    q->c = c;
+    q->conf = k;
+    if (k.umem) {
+        for (int j = 0; j < c->n_reg; j++)
+            if (c->reg[j].host == (uint8_t *)k.umem) {
+                q->r_host = c->reg[j].host;
+                q->r_dev = c->reg[j].dev;
+                q->r_len = c->reg[j].len;
+            }
+        if (!q->r_host) {
+            free(q);
+            return -EINVAL; // not registered with cndp_gpu_host_register
+        }
+    }
+    const uint64_t B = k.batch;
+    const bool cnet = k.mode == CNDP_MQ_CNET;
+    q->stage = q->r_host ? 0u : cnet ? (uint32_t)al64(k.stage_max) : MQ_WIN4;
+    q->h_off = 0;
+    q->h_len = al64(B * 8);
+    q->h_stage = q->h_len + (cnet ? al64(B * 4) : 0);
+    q->h_rec = q->h_stage + B * q->stage;
+    q->h_bytes = q->h_rec + (cnet ? B * 16 : al64(B * 8) + B * 2);
+    q->d_off = 0;
+    q->d_len = al64(B * 8);
+    q->d_stage = q->d_len + (cnet ? al64(B * 4) : 0);
+    q->d_nh = q->d_stage + B * q->stage;
+    q->d_edge = q->d_nh + al64(B * 4);
+    q->d_pt = q->d_edge + al64(B * 2);
+    q->d_rm = q->d_pt + al64(B * 4);
+    q->d_hash = q->d_rm + al64(B * 4);
+    q->d_rec = q->d_hash + al64(B * 4);
+    q->d_bytes = q->d_rec + (cnet ? B * 16 : al64(B * 8) + B * 2);
+    r = -ENOMEM;
+    if (hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) != hipSuccess)
+        goto fail;
+    for (uint32_t j = 0; j < k.depth; j++) {
+        MqSlot *sl = &q->slot[j];
+        sl->mb = (void **)malloc(B * sizeof(void *));
+        if (!sl->mb || hipHostMalloc((void **)&sl->h, q->h_bytes, 0) != hipSuccess ||
+            hipMalloc((void **)&sl->d, q->d_bytes) != hipSuccess ||
+            hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess)
+            goto fail;
+    }
+    *out = q;
+    return 0;
+fail:
+    cndp_gpu_mq_free(q);
+    return r;
+}
+
+extern "C" void cndp_gpu_mq_free(cndp_gpu_mq_t *q)
+{
+    if (!q)
+        return;
+    hipSetDevice(q->c->dev);
+    if (q->s)
+        hipStreamSynchronize(q->s);
+    for (uint32_t j = 0; j < CNDP_MQ_DEPTH_MAX; j++) {
+        MqSlot *sl = &q->slot[j];
+        free(sl->mb);
+        if (sl->h)
+            hipHostFree(sl->h);
+        if (sl->d)
+            hipFree(sl->d);
+        if (sl->ev)
+            hipEventDestroy(sl->ev);
+    }
+    if (q->s)
+        hipStreamDestroy(q->s);
+    free(q);
+}
+
+extern "C" uint32_t cndp_gpu_mq_pending(const cndp_gpu_mq_t *q) { return q ? q->pending : 0u; }
+
+// the slot being filled, opened on demand (nullptr: every slot is busy)
+static MqSlot *mq_open_slot(cndp_gpu_mq_t *q)
+{
+    MqSlot *sl = &q->slot[q->open];
+    if (sl->state == MQ_OPEN)
+        return sl;
+    if (sl->state != MQ_FREE)
+        return nullptr;
+    sl->state = MQ_OPEN;
+    sl->n = sl->polled = 0;
+    sl->nrun = 0;
+    sl->run_closed = 0;
+    sl->stage_used = 0;
+    sl->buf_len = 0;
+    return sl;
+}
+
+static MqTables mq_tables(cndp_gpu_ctx_t *c, uint32_t buf_len)
+{
+    MqTables t;
+    memset(&t, 0, sizeof(t));
+    struct cndp_tbl *t4 = &c->fib4->t, *t6 = &c->fib6->t;
+    t.t24 = (const uint32_t *)t4->dev_tbl24;
+    t.t8 = (const uint32_t *)t4->dev_tbl8;
+    if (c->tune_dir16 && t4->dev_dir16 && t4->dev_pages) {
+        t.d16 = (const uint32_t *)t4->dev_dir16;
+        t.pages = (const uint32_t *)t4->dev_pages;
+    }
+    t.t24_6 = (const uint32_t *)t6->dev_tbl24;
+    t.t8_6 = (const uint32_t *)t6->dev_tbl8;
+    t.buf_len = buf_len;
+    return t;
+}
+
+static int mq_launch(cndp_gpu_mq_t *q)
+{
+    MqSlot *sl = &q->slot[q->open];
+    if (sl->state != MQ_OPEN || sl->n == 0)
+        return 0;
+    cndp_gpu_ctx_t *c = q->c;
+    int r = set_device(c->dev);
+    if (r)
+        return r;
+    hipStream_t s = q->s;
+    const uint32_t n = sl->n;
+    const bool cnet = q->conf.mode == CNDP_MQ_CNET;
+    uint8_t *H = sl->h, *D = sl->d;
+    HIP_TRY(hipMemcpyAsync(D + q->d_off, H + q->h_off, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (cnet)
+        HIP_TRY(hipMemcpyAsync(D + q->d_len, H + q->h_len, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    if (sl->stage_used)
+        HIP_TRY(hipMemcpyAsync(D + q->d_stage, H + q->h_stage, sl->stage_used, hipMemcpyHostToDevice, s));
+    const uint8_t *slab = q->r_host ? q->r_dev : D + q->d_stage;
+    const uint64_t slab_len = q->r_host ? q->r_len : (sl->stage_used ? sl->stage_used : 64);
+    const uint64_t *off = (const uint64_t *)(D + q->d_off);
+    const uint32_t g = blocks_for(n, 256);
+    if (!cnet) {
+        struct cndp_tbl *t = &c->fib4->t;
+        if ((r = cndp_tbl_dev_sync(t, s)))
+            return r;
+        const bool d16 = c->tune_dir16 && t->dev_dir16 && t->dev_pages;
+        hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(256), 0, s, slab, slab_len, off, n,
+                           (const uint32_t *)t->dev_tbl24, (const uint32_t *)t->dev_tbl8,
+                           d16 ? (const uint32_t *)t->dev_dir16 : nullptr,
+                           d16 ? (const uint32_t *)t->dev_pages : nullptr, (uint64_t *)(D + q->d_rec),
+                           (uint16_t *)(D + q->d_rec + al64((uint64_t)q->conf.batch * 8)));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(H + q->h_rec, D + q->d_rec, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(H + q->h_rec + al64((uint64_t)q->conf.batch * 8),
+                               D + q->d_rec + al64((uint64_t)q->conf.batch * 8), (size_t)n * 2,
+                               hipMemcpyDeviceToHost, s));
+    } else {
+        // one classify per run of equal-size graph bursts, the ptype node's
+        // speculation run with that burst size, its state carried in the
+        // context from run to run and batch to batch
+        const uint32_t saved_B = c->spec_burst;
+        uint32_t i0 = 0;
+        for (uint32_t k = 0; k < sl->nrun && !r; k++) {
+            struct cndp_batch b;
+            memset(&b, 0, sizeof(b));
+            b.mode = CNDP_MODE_CNET;
+            b.n = sl->run_n[k];
+            b.slab = slab;
+            b.slab_len = slab_len;
+            b.offsets = off + i0;
+            b.buf_len = sl->buf_len;
+            b.nh = (uint32_t *)(D + q->d_nh) + i0;
+            b.edge = D + q->d_edge + i0;
+            b.ptype = (uint32_t *)(D + q->d_pt) + i0;
+            b.rxmeta = (uint32_t *)(D + q->d_rm) + i0;
+            b.hash = (q->conf.flags & CNDP_MQ_F_HASH) ? (uint32_t *)(D + q->d_hash) + i0 : nullptr;
+            c->spec_burst = saved_B ? sl->run_B[k] : 0u;
+            r = cndp_gpu_classify(c, &b, s);
+            i0 += sl->run_n[k];
+        }
+        c->spec_burst = saved_B;
+        if (r)
+            return r;
+        hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(256), 0, s, slab, slab_len, off,
+                           (const uint32_t *)(D + q->d_len), n, (const uint32_t *)(D + q->d_pt),
+                           (const uint32_t *)(D + q->d_rm), (const uint8_t *)(D + q->d_edge),
+                           (q->conf.flags & CNDP_MQ_F_HASH) ? (const uint32_t *)(D + q->d_hash) : nullptr,
+                           (u32x4 *)(D + q->d_rec), mq_tables(c, sl->buf_len));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(H + q->h_rec, D + q->d_rec, (size_t)n * 16, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipEventRecord(sl->ev, s));
+    sl->state = MQ_FLIGHT;
+    q->in_flight++;
+    q->open = (q->open + 1) % q->conf.depth;
+    return 0;
+}
+
+extern "C" int cndp_gpu_mq_flush(cndp_gpu_mq_t *q)
+{
+    if (!q)
+        return -EINVAL;
+    return mq_launch(q);
+}
+
+// pktmbuf_t fields (pktmbuf.h:102-204)
+#define MB_LPORT 26
+#define MB_DATA_LEN 30
+#define MB_TX_OFFLOAD 40
+#define MB_OL_FLAGS 48
+
+extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t n)
+{
+    if (!q || (n && !mbufs))
+        return -EINVAL;
+    const bool cnet = q->conf.mode == CNDP_MQ_CNET;
+    if (q->r_host) // zero-copy: every buffer must lie in the registered region
+        for (uint32_t i = 0; i < n; i++) {
+            const uint8_t *m = (const uint8_t *)mbufs[i];
+            const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
+            const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
+            if (buf + doff < q->r_host || buf + doff >= q->r_host + q->r_len)
+                return -EINVAL;
+        }
+    uint32_t done = 0;
+    while (done < n) {
+        MqSlot *sl = mq_open_slot(q);
+        if (!sl)
+            break;
+        // one graph burst (<= 256 mbufs) at a time, never split across batches
+        const uint32_t k = n - done < MQ_BURST ? n - done : MQ_BURST;
+        bool full = sl->n + k > q->conf.batch;
+        if (cnet && !full) {
+            const uint16_t bl = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
+            for (uint32_t i = 0; i < k && !full; i++) // one buf_len per batch (the input nodes' length check)
+                full = *(const uint16_t *)((const uint8_t *)mbufs[done + i] + MB_BUF_LEN) != (sl->n ? sl->buf_len : bl);
+            if (!full && sl->nrun == MQ_RUNS_MAX && !(sl->run_closed == 0 && k <= sl->run_B[sl->nrun - 1]))
+                full = true;
+        }
+        if (full) {
+            if (sl->n == 0)
+                return -EINVAL; // a single burst with mixed buf_len
+            int r = mq_launch(q);
+            if (r)
+                return r;
+            continue;
+        }
+        if (sl->n == 0)
+            sl->t_open_ns = now_ns();
+        uint64_t *ho = (uint64_t *)(sl->h + q->h_off);
+        uint32_t *hl = (uint32_t *)(sl->h + q->h_len);
+        for (uint32_t i = 0; i < k; i++) {
+            uint8_t *m = (uint8_t *)mbufs[done + i];
+            const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
+            const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
+            const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+            const uint16_t dlen = *(const uint16_t *)(m + MB_DATA_LEN);
+            const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
+            const uint32_t j = sl->n + i;
+            sl->mb[j] = m;
+            if (cnet)
+                hl[j] = (uint32_t)dlen | (room << 16);
+            if (q->r_host) {
+                ho[j] = (uint64_t)(buf + doff - q->r_host);
+            } else {
+                // staged copy of the bytes the nodes can read (bounded by the buffer)
+                const uint32_t want = cnet ? (room < q->conf.stage_max ? room : q->conf.stage_max) : MQ_WIN4;
+                const uint32_t cp = room < want ? room : want;
+                uint8_t *dst = sl->h + q->h_stage + sl->stage_used;
+                memcpy(dst, buf + doff, cp);
+                const uint64_t span = al64(want ? want : 1);
+                memset(dst + cp, 0, span - cp);
+                ho[j] = sl->stage_used;
+                sl->stage_used += span;
+            }
+        }
+        if (cnet) { // runs of equal-size bursts, each closed by a shorter one
+            if (sl->nrun && !sl->run_closed && k == sl->run_B[sl->nrun - 1]) {
+                sl->run_n[sl->nrun - 1] += k;
+            } else if (sl->nrun && !sl->run_closed && k < sl->run_B[sl->nrun - 1]) {
+                sl->run_n[sl->nrun - 1] += k;
+                sl->run_closed = 1;
+            } else {
+                sl->run_B[sl->nrun] = k;
+                sl->run_n[sl->nrun] = k;
+                sl->nrun++;
+                sl->run_closed = 0;
+            }
+            sl->buf_len = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
+        }
+        sl->n += k;
+        done += k;
+        q->pending += k;
+        if (sl->n + MQ_BURST > q->conf.batch) { // no room for another full burst
+            int r = mq_launch(q);
+            if (r)
+                return r;
+        }
+    }
+    return (int)done;
+}
+
+// write one finished slot's records back into its mbufs
+static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1, void **out, uint16_t *edges)
+{
+    const uint8_t *R = sl->h + q->h_rec;
+    if (q->conf.mode == CNDP_MQ_IP4_LOOKUP) {
+        const uint64_t *priv1 = (const uint64_t *)R;
+        const uint16_t *e = (const uint16_t *)(R + al64((uint64_t)q->conf.batch * 8));
+        for (uint32_t i = i0; i < i1; i++) {
+            uint8_t *m = (uint8_t *)sl->mb[i];
+            *(uint64_t *)(m + MB_UDATA64) = priv1[i]; // node_mbuf_priv1 (ip4_lookup.c:144-154)
+            out[i - i0] = m;
+            edges[i - i0] = e[i];
+        }
+        return;
+    }
+    const uint32_t *rec = (const uint32_t *)R;
+    const bool wh = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
+    const uint16_t lport = q->conf.lport;
+    for (uint32_t i = i0; i < i1; i++) {
+        uint8_t *m = (uint8_t *)sl->mb[i];
+        const uint32_t pt = rec[4 * i], rm = rec[4 * i + 1], w2 = rec[4 * i + 2];
+        // eth_rx mbuf_update (eth_rx.c:35-63)
+        *(uint32_t *)(m + MB_PTYPE) = pt;
+        *(uint64_t *)(m + MB_OL_FLAGS) = (uint64_t)(rm >> 29) << 61;
+        *(uint64_t *)(m + MB_TX_OFFLOAD) = (uint64_t)(rm & 0xffffffu);
+        *(uint16_t *)(m + MB_LPORT) = lport;
+        const uint16_t l2 = (uint16_t)(rm & 0x7fu);
+        uint16_t doff = *(uint16_t *)(m + MB_DATA_OFF), dlen = *(uint16_t *)(m + MB_DATA_LEN);
+        const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+        if (l2 <= dlen && (uint32_t)l2 + doff <= blen) { // pktmbuf_adj_offset
+            doff = (uint16_t)(doff + l2);
+            dlen = (uint16_t)(dlen - l2);
+        }
+        const uint32_t node = w2 >> 24;
+        if (node != CNDP_MQ_NODE_PTYPE) // ip4_input / ip6_input: data_len from the IP header
+            dlen = (uint16_t)(w2 & 0xffffu);
+        *(uint16_t *)(m + MB_DATA_OFF) = doff;
+        *(uint16_t *)(m + MB_DATA_LEN) = dlen;
+        if (wh)
+            *(uint32_t *)(m + MB_HASH) = rec[4 * i + 3];
+        out[i - i0] = m;
+        edges[i - i0] = (uint16_t)(w2 >> 16);
+    }
+}
+
+extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges, uint32_t max)
+{
+    if (!q || (max && (!mbufs || !edges)))
+        return -EINVAL;
+    // adaptive batching: a partly filled batch goes out when the GPU is idle
+    // or the batch has waited max_delay_us
+    MqSlot *op = &q->slot[q->open];
+    if (op->state == MQ_OPEN && op->n &&
+        (q->in_flight == 0 || now_ns() - op->t_open_ns >= (uint64_t)q->conf.max_delay_us * 1000u)) {
+        int r = mq_launch(q);
+        if (r)
+            return r;
+    }
+    uint32_t got = 0;
+    while (got < max) {
+        MqSlot *sl = &q->slot[q->head];
+        if (sl->state == MQ_FLIGHT) {
+            const hipError_t e = hipEventQuery(sl->ev);
+            if (e == hipErrorNotReady)
+                break;
+            if (e != hipSuccess)
+                return -EIO;
+            sl->state = MQ_DONE;
+            q->in_flight--;
+        }
+        if (sl->state != MQ_DONE)
+            break;
+        const uint32_t take = sl->n - sl->polled < max - got ? sl->n - sl->polled : max - got;
+        mq_writeback(q, sl, sl->polled, sl->polled + take, mbufs + got, edges + got);
+        sl->polled += take;
+        got += take;
+        q->pending -= take;
+        if (sl->polled == sl->n) {
+            sl->state = MQ_FREE;
+            q->head = (q->head + 1) % q->conf.depth;
+        }
+    }
+    return (int)got;
+}
+
+extern "C" int cndp_gpu_mq_wait(cndp_gpu_mq_t *q)
+{
+    if (!q)
+        return -EINVAL;
+    MqSlot *sl = &q->slot[q->head];
+    if (sl->state != MQ_FLIGHT)
+        return 0;
+    HIP_TRY(hipEventSynchronize(sl->ev));
+    return 0;
+}
+
 extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
 {
     if (!c)
@@ -5378,6 +5975,9 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
             return -EINVAL;
         c->spec_burst = (uint32_t)value;
         c->spec_reset = 1; // a new graph: ctx->last_type starts at 0 again (stream-ordered, next call)
+        return 0;
+    case CNDP_TUNE_MBUF_HASH:
+        c->mbuf_hash = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

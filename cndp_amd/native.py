@@ -40,6 +40,10 @@ CNDP_TUNE_RW_WB = 8
 CNDP_TUNE_CNET_SPEC = 9
 CNDP_TUNE_LOAD_NT = 10
 CNDP_TUNE_SPEC_SCAN = 11
+CNDP_TUNE_MBUF_HASH = 12
+CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET = 0, 1
+CNDP_MQ_F_HASH = 1
+CNDP_MQ_NODE_PTYPE, CNDP_MQ_NODE_IP4, CNDP_MQ_NODE_IP6 = 0, 1, 2
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF
 
 # l3fwd edges (node_ip4_api.h:28-34) and cnet edges (ip4_input_priv.h:26-31)
@@ -76,6 +80,13 @@ class Batch(Structure):
                 ("buf_len", c_uint32), ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p),
                 ("edge", c_void_p), ("bins", c_void_p), ("n_bins", c_uint32), ("ptype", c_void_p),
                 ("rxmeta", c_void_p)]
+
+
+class MqConf(Structure):
+    """struct cndp_mq_conf (cndp_gpu.h)."""
+    _fields_ = [("mode", c_uint32), ("flags", c_uint32), ("batch", c_uint32), ("depth", c_uint32),
+                ("max_delay_us", c_uint32), ("stage_max", c_uint32), ("umem", c_void_p),
+                ("lport", c_uint16), ("rsvd", c_uint16 * 3)]
 
 
 class NativeLibraryMissing(RuntimeError):
@@ -154,6 +165,13 @@ def lib():
         "cndp_gpu_bin_ids": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32,
                                      c_uint32, c_void_p, c_void_p]),
         "cndp_gpu_set_tuning": (c_int, [c_void_p, c_int, c_int]),
+        "cndp_gpu_mq_create": (c_int, [c_void_p, POINTER(MqConf), POINTER(c_void_p)]),
+        "cndp_gpu_mq_free": (None, [c_void_p]),
+        "cndp_gpu_mq_submit": (c_int, [c_void_p, c_void_p, c_uint32]),
+        "cndp_gpu_mq_flush": (c_int, [c_void_p]),
+        "cndp_gpu_mq_poll": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
+        "cndp_gpu_mq_wait": (c_int, [c_void_p]),
+        "cndp_gpu_mq_pending": (c_uint32, [c_void_p]),
         "cndp_gpu_version": (c_char_p, []),
     }
     for name, (res, args) in sig.items():

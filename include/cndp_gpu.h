@@ -118,7 +118,8 @@ int cndp_gpu_classify_host(cndp_gpu_ctx_t *ctx, const struct cndp_batch *host_ba
  * parse (pktdev_rx.c:24-34), pkt_cls (pkt_cls.c:19-31) and ip4_lookup
  * (ip4_lookup.c:48-256) on the GPU and writes back what those nodes write:
  * m->packet_type, m->udata64 = node_mbuf_priv1 {nh, ttl, cksum}
- * (node_private.h:24-35), plus m->hash (the flow hash, build-defined).
+ * (node_private.h:24-35), plus m->hash (the flow hash, build-defined) when
+ * CNDP_TUNE_MBUF_HASH is set.
  * edges[i] = the ip4_lookup next edge (val >> 16: 0 rewrite, 1 drop), or
  * CNDP_MBUF_EDGE_CLS_DROP when pkt_cls sends the frame to pkt_drop.  Header
  * windows are gathered into pinned staging, classified, and the call waits
@@ -126,6 +127,87 @@ int cndp_gpu_classify_host(cndp_gpu_ctx_t *ctx, const struct cndp_batch *host_ba
 #define CNDP_MBUF_EDGE_CLS_DROP 0xFFFFu
 int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, uint16_t *edges,
                          void *stream);
+
+/* ---- asynchronous node path over pktmbuf_t bursts (cndp_gpu_mq_*) -------
+ * The graph-node boundary without a PCIe round trip per burst: a node's
+ * process() callback hands each burst of pktmbuf_t pointers to
+ * cndp_gpu_mq_submit, which never waits; bursts collect into a batch, whole
+ * batches run on the GPU on the queue's own stream (up to `depth` in flight,
+ * double-buffered pinned staging), and cndp_gpu_mq_poll returns finished
+ * mbufs -- with every field the replaced nodes write already written back --
+ * plus the next edge of each, in submission order.  A graph's source node
+ * (node/ip4_lookup_gpu.c) polls once per walk, which also launches a partly
+ * filled batch when the GPU has nothing in flight or the batch is older
+ * than max_delay_us.
+ *
+ * Frame bytes: when conf.umem names a region registered with
+ * cndp_gpu_host_register (the AF_XDP UMEM / pktmbuf pool, cne_lport.h:91),
+ * the kernels read each frame where it lies (zero-copy: only the 8-B frame
+ * offsets cross PCIe); every mbuf's buffer must lie in that region.  With
+ * conf.umem NULL, the host copies each frame into pinned staging (ip4_lookup:
+ * 64 B, enough for every byte the node reads; cnet: the buffer from data_off
+ * to buf_len, at most conf.stage_max bytes).
+ *
+ * Modes and what is written back (pktmbuf_t layout, pktmbuf.h:102-204):
+ *   CNDP_MQ_IP4_LOOKUP  the ip4_lookup node (ip4_lookup.c:48-256): udata64 =
+ *                       node_mbuf_priv1 {nh, ttl, cksum} (node_private.h:24-35);
+ *                       edge = FIB value >> 16 (0 ip4_rewrite, 1 pkt_drop).
+ *                       The FIB is the context's fib4 (normally
+ *                       cndp_node_ip4_lookup_fib()).
+ *   CNDP_MQ_CNET        eth_rx (eth_rx.c:35-63) + ptype (ptype.c:48-210, its
+ *                       4-wide speculation with the uint8_t fix_spec quirk over
+ *                       the submitted bursts, node state kept in the context)
+ *                       + ip4_input / ip6_input (length + checksum, FIB):
+ *                       packet_type, ol_flags, tx_offload l2/l3/l4_len, lport,
+ *                       data_off/data_len as pktmbuf_adj_offset(l2_len), then
+ *                       data_len = total_length / payload_len for frames an
+ *                       input node took.  edge = CNDP_MQ_EDGE(node, e): node
+ *                       CNDP_MQ_NODE_PTYPE with e = the ptype edge (pkt_drop 0,
+ *                       punt 2, gtpu 5), or CNDP_MQ_NODE_IP4 / _IP6 with e =
+ *                       the input node's edge (drop 0, forward 1, proto 2).
+ *                       Each submit call is one graph burst (<= 256 mbufs;
+ *                       larger calls are cut into 256s).
+ *   flag CNDP_MQ_F_HASH also store the Toeplitz flow hash in m->hash (no
+ *                       reference node writes it, so it is off by default).
+ */
+typedef struct cndp_gpu_mq cndp_gpu_mq_t;
+
+#define CNDP_MQ_IP4_LOOKUP 0u
+#define CNDP_MQ_CNET 1u
+#define CNDP_MQ_F_HASH (1u << 0)
+#define CNDP_MQ_NODE_PTYPE 0u
+#define CNDP_MQ_NODE_IP4 1u
+#define CNDP_MQ_NODE_IP6 2u
+#define CNDP_MQ_EDGE(node, e) ((uint16_t)(((node) << 8) | (e)))
+#define CNDP_MQ_DEPTH_MAX 16u
+
+struct cndp_mq_conf {
+    uint32_t mode;         /* CNDP_MQ_* */
+    uint32_t flags;        /* CNDP_MQ_F_* */
+    uint32_t batch;        /* mbufs per GPU launch, >= 256 (0 = 8192) */
+    uint32_t depth;        /* batches in flight, 2..16 (0 = 4) */
+    uint32_t max_delay_us; /* a partly filled batch launches at this age (0 = 50 us) */
+    uint32_t stage_max;    /* cnet staged mode: bytes copied per frame (0 = 2048) */
+    void *umem;            /* registered region the mbufs live in, or NULL */
+    uint16_t lport;        /* cnet: m->lport (eth_rx.c:59) */
+    uint16_t rsvd[3];
+};
+
+int cndp_gpu_mq_create(cndp_gpu_ctx_t *ctx, const struct cndp_mq_conf *conf, cndp_gpu_mq_t **out);
+/* Waits for batches in flight; mbufs not yet polled are simply forgotten. */
+void cndp_gpu_mq_free(cndp_gpu_mq_t *q);
+/* Accepts up to n mbufs (a graph burst), returns how many (0 when every
+ * batch slot is in flight or waiting to be polled), or a negative errno
+ * (-EINVAL: an mbuf outside conf.umem, -EIO: a failed launch). */
+int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t n);
+/* Launch the partly filled batch now (no-op when empty). */
+int cndp_gpu_mq_flush(cndp_gpu_mq_t *q);
+/* Never waits: up to max finished mbufs and their edges, oldest first. */
+int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges, uint32_t max);
+/* Block until the oldest batch in flight has finished (0 if none). */
+int cndp_gpu_mq_wait(cndp_gpu_mq_t *q);
+/* mbufs accepted and not yet returned by poll. */
+uint32_t cndp_gpu_mq_pending(const cndp_gpu_mq_t *q);
 
 /* ip4_rewrite node on the device (ip4_rewrite.c).  Control plane mirrors
  * ip4_rewrite_set_next (:252-263) and cne_node_ip4_rewrite_add (:265-295):
@@ -207,6 +289,8 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           non-temporal hint, so the once-read stream neither allocates
  *                           in L2 / the Infinity Cache nor evicts the FIB directory from
  *                           them (default 1)
+ *   CNDP_TUNE_MBUF_HASH     1 = cndp_gpu_l3fwd_mbufs also stores the flow hash in m->hash
+ *                           (no reference node writes it; default 0)
  *   CNDP_TUNE_SPEC_SCAN     cnet speculation: how burst maps are composed. 0 = auto (none
  *                           when no low byte of the batch's ptypes carries two p_nxt
  *                           edges -- only the final node state is walked -- else maps of
@@ -224,6 +308,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_CNET_SPEC 9
 #define CNDP_TUNE_LOAD_NT 10
 #define CNDP_TUNE_SPEC_SCAN 11
+#define CNDP_TUNE_MBUF_HASH 12
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Version / build info string. */

@@ -1,0 +1,268 @@
+"""The asynchronous node path over pktmbuf_t bursts (cndp_gpu_mq_*) against the
+oracle, on mbuf pools laid out like CNDP's (pktmbuf.h:102-204, pktmbuf.c:60-80).
+
+  ip4_lookup node   lib/usr/clib/nodes/ip4_lookup.c:48-256 (priv1 in udata64, edge)
+  cnet input chain  lib/cnet/eth/eth_rx.c:35-63 (packet_type, ol_flags,
+                    tx_offload, lport, pktmbuf_adj_offset), lib/cnet/ptype/ptype.c:48-210
+                    (4-wide speculation over the submitted bursts), ip4_input.c /
+                    ip6_input.c:50-260 (data_len, edges)
+
+Both frame paths run: zero-copy (the pool registered with
+cndp_gpu_host_register, kernels read the frames in host memory) and staged
+(frames copied into pinned staging).  Bursts are fed as a graph node would,
+draining the queue whenever it is full."""
+import numpy as np
+import pytest
+import torch
+
+from cndp_amd import native as N
+from cndp_amd import pktgen
+from cndp_amd.mbuf import HDR, MbufPool, MbufQueue
+from oracle import oracle as O
+
+from helpers import CNET_DEF, cnet_fibs, l3fwd_fib, l3fwd_oracle_tables
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def l3(gpu):
+    from cndp_amd.classify import Classifier
+    fib, vals = l3fwd_fib()
+    cl = Classifier(0)
+    cl.set_fib(fib)
+    return cl, fib, l3fwd_oracle_tables(vals)
+
+
+@pytest.fixture(scope="module")
+def cn(gpu):
+    from cndp_amd.classify import Classifier
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    cl = Classifier(0)
+    cl.set_fib(fib, fib6)
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    return cl, routes, v6, t4, t6
+
+
+def _bursts(n, seed, kind):
+    rng = np.random.default_rng(seed)
+    if kind == "full":
+        return [256] * (n // 256) + ([n % 256] if n % 256 else [])
+    out, left = [], n
+    while left:
+        b = int(rng.choice([256, 256, 256, 100, 64, 64, 7, 3, 1, 255]))
+        b = min(b, left)
+        out.append(b)
+        left -= b
+    return out
+
+
+def _mixed_l3_frames(n, seed):
+    """Routed IPv4 frames with fuzz frames mixed in (non-IPv4, odd IHL...)."""
+    a = pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=seed)
+    f = pktgen.fuzz_frames(n, seed=seed, slot=64)
+    slab = a.slab.view(n, 64).clone()
+    fz = torch.zeros(n * 64, dtype=torch.uint8)
+    fz[: f.slab.numel()] = f.slab
+    pick = torch.arange(n) % 5 == 3
+    slab[pick] = fz.view(n, 64)[pick]
+    return pktgen.Frames(slab.reshape(-1), n, stride=64)
+
+
+@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("kind", ["full", "ragged"])
+def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
+    cl, fib, t4 = l3
+    n = 20000
+    pool = MbufPool(n)
+    fr = _mixed_l3_frames(n, seed=3 if kind == "full" else 4)
+    pool.fill(fr)
+    pool.hdr["udata64"] = 0xABABABABABABABAB
+    umem = None
+    if zero_copy:
+        cl.host_register(pool.mem)
+        umem = pool.base
+    try:
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, batch=4096, depth=3, umem=umem)
+        order = np.random.default_rng(9).permutation(n)  # mbufs come in any order
+        addrs, edges = q.run(pool, order, _bursts(n, 5, kind))
+        q.close()
+    finally:
+        if zero_copy:
+            cl.host_unregister(pool.mem)
+    idx = pool.index_of(addrs)
+    assert np.array_equal(idx, order), "completions out of submission order"
+    d = pool.data_pos()
+    b = pool.mem
+    ttl = b[(d + 22).astype(np.int64)].astype(np.uint64)
+    ck = b[(d + 24).astype(np.int64)].astype(np.uint64) | (b[(d + 25).astype(np.int64)].astype(np.uint64) << 8)
+    dip = np.zeros(n, np.uint32)
+    for k in range(4):
+        dip = (dip << 8) | b[(d + 30 + k).astype(np.int64)].astype(np.uint32)
+    val = O.dir24_8_lookup(t4[0], t4[1], dip).astype(np.uint64)
+    want = (val & 0xFFFF) | (ttl << 16) | (ck << 32)
+    assert np.array_equal(pool.hdr["udata64"], want)
+    assert np.array_equal(edges, (val[idx] >> 16).astype(np.uint16))
+    assert (edges == 1).sum() > 0 and (edges == 0).sum() > 0
+
+
+def _cnet_expect(pool, order, bursts, t4, t6, hash_flag, lport):
+    """Oracle results for the mbufs in submission order: one oracle call per
+    run of equal-size bursts (closed by one shorter burst), the ptype node
+    state carried from run to run."""
+    n = len(order)
+    d = pool.data_pos()[order]
+    st = np.zeros(1, np.uint16)
+    outs = []
+    runs = []
+    for b in bursts:
+        if runs and not runs[-1][2] and b == runs[-1][0]:
+            runs[-1][1] += b
+        elif runs and not runs[-1][2] and b < runs[-1][0]:
+            runs[-1][1] += b
+            runs[-1][2] = True
+        else:
+            runs.append([b, b, False])
+    pos = 0
+    for B, cnt, _ in runs:
+        outs.append(O.classify(O.MODE_CNET, pool.mem, cnt, offsets=d[pos:pos + cnt], buf_len=1984,
+                               tables4=t4, tables6=t6, spec_burst=B, spec_state=st))
+        pos += cnt
+    ref = {k: np.concatenate([o[k] for o in outs]) for k in ("nh", "hash", "edge", "ptype", "rxmeta")}
+    assert pos == n
+    return ref
+
+
+@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("kind", ["full", "ragged"])
+def test_mq_cnet(cn, gpu, zero_copy, kind):
+    cl, routes, v6, t4, t6 = cn
+    n = 24000
+    pool = MbufPool(n)
+    imx = pktgen.imix(n, v4routes=routes, v6routes=v6, seed=11, v6_frac=0.4)
+    fz = pktgen.fuzz_frames(n, seed=12, slot=128)
+    from test_gpu_parity import _gtp_mix
+    gt = _gtp_mix(n, routes, v6, "cpu", seed=14)
+    pool.fill(imx)
+    # every 3rd mbuf: a fuzz frame (VLAN, QinQ, ext headers, tunnels, bad IHL ...)
+    # every 7th: a GTP-U / GTP-C / TCP frame in a UDP run (the fix_spec quirk)
+    pf = MbufPool(n)
+    pf.fill(fz)
+    pg = MbufPool(n)
+    pg.fill(gt)
+    for i in range(0, n, 3):
+        pool.mem[i * 2048:(i + 1) * 2048] = pf.mem[i * 2048:(i + 1) * 2048]
+    for i in range(1, n, 7):
+        pool.mem[i * 2048:(i + 1) * 2048] = pg.mem[i * 2048:(i + 1) * 2048]
+    pool.hdr["buf_addr"] = pool.base + np.arange(n, dtype=np.uint64) * 2048 + HDR
+    pool.hdr["data_len"][::5] = 10      # runts: pktmbuf_adj_offset(l2_len) is skipped
+    orig = pool.hdr.copy()
+    umem = None
+    flags = N.CNDP_MQ_F_HASH if kind == "ragged" else 0
+    if zero_copy:
+        cl.host_register(pool.mem)
+        umem = pool.base
+    bursts = _bursts(n, 21, kind)
+    order = np.arange(n)
+    try:
+        cl.set_tuning(cnet_spec=256)   # fresh ptype node state
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=flags, batch=4096, depth=3, umem=umem, lport=7)
+        ref = _cnet_expect(pool, order, bursts, t4, t6, flags, 7)
+        addrs, edges = q.run(pool, order, bursts)
+        q.close()
+    finally:
+        if zero_copy:
+            cl.host_unregister(pool.mem)
+    assert np.array_equal(pool.index_of(addrs), order)
+    h = pool.hdr
+    assert np.array_equal(h["packet_type"], ref["ptype"])
+    assert np.array_equal(h["ol_flags"], (ref["rxmeta"] >> 29).astype(np.uint64) << np.uint64(61))
+    assert np.array_equal(h["tx_offload"], (ref["rxmeta"] & 0xFFFFFF).astype(np.uint64))
+    assert np.all(h["lport"] == 7)
+    l2 = (ref["rxmeta"] & 0x7F).astype(np.int64)
+    dl0 = orig["data_len"].astype(np.int64)
+    doff0 = orig["data_off"].astype(np.int64)
+    adj = (l2 <= dl0) & (l2 + doff0 <= orig["buf_len"].astype(np.int64))
+    doff = np.where(adj, doff0 + l2, doff0)
+    dlen = np.where(adj, dl0 - l2, dl0)
+    e8 = ref["edge"].astype(np.int64)
+    at_input = e8 < 0x80
+    low = ref["ptype"] & 0xFF
+    v6 = (low == 0x41) | (low == 0xC1) | (low == 0xE1)
+    mt = np.arange(n, dtype=np.int64) * 2048 + HDR + doff
+    ipl = np.where(v6, mt + 4, mt + 2)
+    hdrlen = (pool.mem[ipl].astype(np.int64) << 8) | pool.mem[ipl + 1]
+    dlen = np.where(at_input, hdrlen, dlen)
+    assert np.array_equal(h["data_off"], doff.astype(np.uint16))
+    assert np.array_equal(h["data_len"], dlen.astype(np.uint16))
+    # frames shorter than their L2 header keep data_off, so the input node reads
+    # its IP header at the frame start (ip4_input.c:121-150 / ip6_input.c:121-150)
+    e_in = e8.copy()
+    for i in np.nonzero(at_input & ~adj)[0]:
+        o = int(mt[i])
+        hdr = bytes(pool.mem[o:o + 64])
+        if v6[i]:
+            ok = int.from_bytes(hdr[4:6], "big") < 1984
+            dip = np.frombuffer(hdr[24:40] if ok else bytes(16), np.uint8)
+            nh = int(O.trie_lookup(t6[0], t6[1], dip)[0])
+        else:
+            ok = int.from_bytes(hdr[2:4], "big") < 1984 and O.ipv4_cksum(hdr) == 0
+            dip = np.array([int.from_bytes(hdr[16:20], "big") if ok else 0], np.uint32)
+            nh = int(O.dir24_8_lookup(t4[0], t4[1], dip)[0])
+        e_in[i] = nh >> 24
+    assert (at_input & ~adj).sum() > 0
+    node = np.where(at_input, np.where(v6, N.CNDP_MQ_NODE_IP6, N.CNDP_MQ_NODE_IP4), N.CNDP_MQ_NODE_PTYPE)
+    want_e = (node << 8) | np.where(at_input, e_in, e8 & 0x7F)
+    assert np.array_equal(edges.astype(np.int64), want_e)
+    if flags & N.CNDP_MQ_F_HASH:
+        assert np.array_equal(h["hash"], ref["hash"])
+    else:
+        assert np.all(h["hash"] == 0)
+    # every node and edge kind shows up
+    assert {0, 1, 2} <= set(np.unique(node).tolist())
+    assert (want_e == ((N.CNDP_MQ_NODE_PTYPE << 8) | 5)).sum() > 0   # gtpu
+
+
+def test_mq_backpressure_and_errors(l3, gpu):
+    cl, fib, t4 = l3
+    n = 256 * 8
+    pool = MbufPool(n)
+    pool.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=7))
+    q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, batch=256, depth=2, max_delay_us=1000000)
+    # two slots of one burst each: the third burst is refused until a poll
+    assert q.submit(pool.ptrs(range(0, 256))) == 256
+    assert q.submit(pool.ptrs(range(256, 512))) == 256
+    assert q.submit(pool.ptrs(range(512, 768))) == 0
+    assert q.pending == 512
+    q.wait()
+    q.wait()
+    import time
+    t0 = time.time()
+    got = 0
+    while got < 512 and time.time() - t0 < 10:
+        a, e = q.poll()
+        got += a.size
+        q.wait()
+    assert got == 512 and q.pending == 0
+    assert q.submit(pool.ptrs(range(512, 768))) == 256
+    q.close()
+    # an mbuf outside the registered region is refused
+    cl.host_register(pool.mem)
+    try:
+        q2 = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, umem=pool.base)
+        other = MbufPool(4)
+        assert cl._L.cndp_gpu_mq_submit(q2.h, other.ptrs(range(4)), 4) == -22
+        q2.close()
+    finally:
+        cl.host_unregister(pool.mem)
+    # bad configurations
+    import ctypes
+    c = N.MqConf()
+    c.mode = 7
+    h = ctypes.c_void_p()
+    assert cl._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)) == -22
+    c.mode, c.batch = N.CNDP_MQ_IP4_LOOKUP, 100
+    assert cl._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)) == -22
+    c.batch, c.umem = 0, 12345
+    assert cl._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)) == -22
