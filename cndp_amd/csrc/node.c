@@ -202,3 +202,51 @@ int cne_node_ip6_add_input(struct cne_fib6 *fib, const uint8_t ip[IPV6_ADDR_LEN]
           << CNDP_RT_NEXT_INDEX_SHIFT;
     return cne_fib6_add(fib, ip, depth, nh);
 }
+
+/* ---- regions the GPU nodes may read in place ----------------------------- */
+#define UMEM_MAX 16
+static struct {
+    void *addr;
+    uint64_t len;
+} umems[UMEM_MAX];
+static uint32_t n_umems;
+
+int cndp_node_gpu_umem_add(void *addr, uint64_t len)
+{
+    if (!addr || !len)
+        return -EINVAL;
+    int r = 0;
+    pthread_mutex_lock(&node_lock);
+    if (n_umems == UMEM_MAX) {
+        r = -ENOSPC;
+    } else {
+        umems[n_umems].addr = addr;
+        umems[n_umems].len = len;
+        n_umems++;
+    }
+    pthread_mutex_unlock(&node_lock);
+    return r;
+}
+
+int cndp_node_gpu_umem_get(uint32_t i, void **addr, uint64_t *len)
+{
+    int r = 0;
+    pthread_mutex_lock(&node_lock);
+    if (i >= n_umems) {
+        r = -ENOENT;
+    } else {
+        if (addr)
+            *addr = umems[i].addr;
+        if (len)
+            *len = umems[i].len;
+    }
+    pthread_mutex_unlock(&node_lock);
+    return r;
+}
+
+void cndp_node_gpu_umem_reset(void)
+{
+    pthread_mutex_lock(&node_lock);
+    n_umems = 0;
+    pthread_mutex_unlock(&node_lock);
+}

@@ -144,6 +144,9 @@ def lib():
         "cndp_node_ip4_rewrite_get": (c_int, [c_uint16, c_void_p, POINTER(c_uint16), POINTER(c_uint16),
                                               POINTER(c_uint16)]),
         "cndp_node_ip4_rewrite_reset": (None, []),
+        "cndp_node_gpu_umem_add": (c_int, [c_void_p, c_uint64]),
+        "cndp_node_gpu_umem_get": (c_int, [c_uint32, POINTER(c_void_p), POINTER(c_uint64)]),
+        "cndp_node_gpu_umem_reset": (None, []),
         # cndp_gpu.h
         "cndp_gpu_init": (c_int, [c_int, POINTER(c_void_p)]),
         "cndp_gpu_fini": (None, [c_void_p]),

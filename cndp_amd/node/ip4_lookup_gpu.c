@@ -1,0 +1,252 @@
+/*
+ * ip4_lookup_gpu.c -- the l3fwd-graph "ip4_lookup" node with its arithmetic on
+ * the MI355X (libcndp_gpu.so).
+ *
+ * Built in a CNDP tree in place of lib/usr/clib/nodes/ip4_lookup.c (see
+ * INTEGRATION.md): it registers a node under the same name and edges
+ * (ip4_lookup.c:345-359), owns the lookup FIB the same way (ip4_lookup_nm,
+ * :31-42; here libcndp_gpu holds it and exports cne_node_ip4_route_add), and
+ * writes the same per-mbuf result: node_mbuf_priv1 {nh, ttl, cksum} in
+ * udata64 and the next edge = FIB value >> 16 (:108-154).  So
+ * examples/l3fwd-graph links and runs unchanged: its "ip4*" graph pattern
+ * (fwd.c:128) picks up both nodes below.
+ *
+ * What differs is time, not results: process() never waits for the GPU.
+ * Each burst is handed to an asynchronous queue (cndp_gpu_mq_submit) that
+ * batches bursts and runs whole batches on the device; finished mbufs come
+ * back from cndp_gpu_mq_poll in arrival order and are enqueued to
+ * ip4_rewrite / pkt_drop.  Completions are collected
+ *   - by process() itself after each submit, and
+ *   - by "ip4_lookup_gpu_drain", a source node (CNE_NODE_SOURCE_F) with the
+ *     same two edges that every cne_graph_walk calls; its poll also launches
+ *     a partly filled batch when the GPU is idle or the batch is older than
+ *     CNDP_GPU_DELAY_US, which is the flush timer an idle port needs.
+ * When every batch slot is in flight, process() drains and then waits for the
+ * oldest batch (back-pressure instead of dropping).
+ *
+ * Tuning from the environment (the application stays unchanged):
+ *   CNDP_GPU_DEVICE (0), CNDP_GPU_BATCH (8192), CNDP_GPU_DEPTH (4),
+ *   CNDP_GPU_DELAY_US (50).  Frames are read in place when the application
+ *   registered its UMEM with cndp_node_gpu_umem_add(), else staged.
+ *
+ * One GPU context and queue per graph (graphs are per lcore, cne_graph_worker.h
+ * notes a graph is not shared between threads); contexts share the node FIB,
+ * whose device mirror libcndp_gpu keeps on one device per process.
+ */
+#include <errno.h>
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <cne_graph.h>
+#include <cne_graph_worker.h>
+#include <pktmbuf.h>
+
+#include "cndp_gpu.h"
+#include "cndp_node.h"
+
+#define GPU_POLL_MAX 256
+#define GPU_GRAPHS_MAX 256 /* graph ids this module tracks */
+#define DRAIN_NODE_NAME "ip4_lookup_gpu_drain"
+
+/* ip4_lookup.c:38: the rewrite node reads priv1 at this offset */
+int node_mbuf_priv1_dynfield_offset = -1;
+
+struct gpu_graph_state {
+    int refs; /* the two nodes of one graph */
+    cndp_gpu_ctx_t *gpu;
+    cndp_gpu_mq_t *q;
+    void *done[GPU_POLL_MAX];
+    uint16_t edge[GPU_POLL_MAX];
+};
+
+static pthread_mutex_t gs_lock = PTHREAD_MUTEX_INITIALIZER;
+static struct gpu_graph_state *gs_by_graph[GPU_GRAPHS_MAX];
+
+struct gpu_node_ctx { /* node->ctx is CNE_NODE_CTX_SZ (16) bytes */
+    struct gpu_graph_state *st;
+};
+#define GPU_NODE_STATE(node) (((struct gpu_node_ctx *)(node)->ctx)->st)
+
+static uint32_t env_u32(const char *name, uint32_t dflt)
+{
+    const char *v = getenv(name);
+    return v && *v ? (uint32_t)strtoul(v, NULL, 0) : dflt;
+}
+
+static void state_put(struct gpu_graph_state *st)
+{
+    if (st && --st->refs == 0) {
+        cndp_gpu_mq_free(st->q);
+        cndp_gpu_fini(st->gpu);
+        free(st);
+    }
+}
+
+/* the state of this graph, created by whichever of the two nodes starts first */
+static struct gpu_graph_state *state_get(const struct cne_graph *graph)
+{
+    const unsigned gid = graph->id;
+    if (gid >= GPU_GRAPHS_MAX)
+        return NULL;
+    pthread_mutex_lock(&gs_lock);
+    struct gpu_graph_state *st = gs_by_graph[gid];
+    if (st) {
+        st->refs++;
+        pthread_mutex_unlock(&gs_lock);
+        return st;
+    }
+    st = calloc(1, sizeof(*st));
+    if (!st)
+        goto fail;
+    st->refs = 1;
+    if (cndp_node_ip4_lookup_init() < 0 || cndp_gpu_init((int)env_u32("CNDP_GPU_DEVICE", 0), &st->gpu) < 0)
+        goto fail;
+    if (cndp_gpu_set_fib(st->gpu, cndp_node_ip4_lookup_fib(), NULL) < 0)
+        goto fail;
+    struct cndp_mq_conf conf = {0};
+    conf.mode = CNDP_MQ_IP4_LOOKUP;
+    conf.batch = env_u32("CNDP_GPU_BATCH", 8192);
+    conf.depth = env_u32("CNDP_GPU_DEPTH", 4);
+    conf.max_delay_us = env_u32("CNDP_GPU_DELAY_US", 50);
+    void *umem = NULL;
+    uint64_t ulen = 0;
+    if (cndp_node_gpu_umem_get(0, &umem, &ulen) == 0) {
+        int r = cndp_gpu_host_register(st->gpu, umem, ulen, NULL);
+        if (r == 0 || r == -EEXIST)
+            conf.umem = umem; /* zero-copy: the kernels read the frames in the UMEM */
+    }
+    if (cndp_gpu_mq_create(st->gpu, &conf, &st->q) < 0)
+        goto fail;
+    gs_by_graph[gid] = st;
+    pthread_mutex_unlock(&gs_lock);
+    return st;
+fail:
+    if (st) {
+        if (st->gpu)
+            cndp_gpu_fini(st->gpu);
+        free(st);
+    }
+    pthread_mutex_unlock(&gs_lock);
+    return NULL;
+}
+
+static void state_release(const struct cne_graph *graph, struct gpu_graph_state *st)
+{
+    pthread_mutex_lock(&gs_lock);
+    if (st && st->refs == 1 && graph->id < GPU_GRAPHS_MAX && gs_by_graph[graph->id] == st)
+        gs_by_graph[graph->id] = NULL;
+    state_put(st);
+    pthread_mutex_unlock(&gs_lock);
+}
+
+/* hand every finished mbuf on to its edge, runs of one edge at a time */
+static uint16_t gpu_drain(struct cne_graph *graph, struct cne_node *node, struct gpu_graph_state *st)
+{
+    uint16_t total = 0;
+    for (;;) {
+        const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, GPU_POLL_MAX);
+        if (k <= 0)
+            break;
+        int i = 0;
+        while (i < k) {
+            int j = i + 1;
+            while (j < k && st->edge[j] == st->edge[i])
+                j++;
+            cne_node_enqueue(graph, node, (cne_edge_t)st->edge[i], &st->done[i], (uint16_t)(j - i));
+            i = j;
+        }
+        total = (uint16_t)(total + k);
+        if (k < GPU_POLL_MAX)
+            break;
+    }
+    return total;
+}
+
+static uint16_t ip4_lookup_gpu_process(struct cne_graph *graph, struct cne_node *node, void **objs,
+                                       uint16_t nb_objs)
+{
+    struct gpu_graph_state *st = GPU_NODE_STATE(node);
+    uint16_t done = 0;
+    while (done < nb_objs) {
+        const int k = cndp_gpu_mq_submit(st->q, objs + done, (uint32_t)(nb_objs - done));
+        if (k < 0) { /* the device failed: the objects still have to go somewhere */
+            cne_node_enqueue(graph, node, CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP, objs + done,
+                             (uint16_t)(nb_objs - done));
+            break;
+        }
+        done = (uint16_t)(done + k);
+        if (done < nb_objs && gpu_drain(graph, node, st) == 0 && cndp_gpu_mq_wait(st->q) < 0) {
+            cne_node_enqueue(graph, node, CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP, objs + done,
+                             (uint16_t)(nb_objs - done));
+            break;
+        }
+    }
+    gpu_drain(graph, node, st);
+    return nb_objs;
+}
+
+static int ip4_lookup_gpu_init(const struct cne_graph *graph, struct cne_node *node)
+{
+    node_mbuf_priv1_dynfield_offset = offsetof(pktmbuf_t, udata64); /* ip4_lookup.c:322 */
+    struct gpu_graph_state *st = state_get(graph);
+    if (!st)
+        return -ENODEV; /* no CPU path behind this node: fail loudly at graph create */
+    GPU_NODE_STATE(node) = st;
+    return 0;
+}
+
+static void ip4_lookup_gpu_fini(const struct cne_graph *graph, struct cne_node *node)
+{
+    state_release(graph, GPU_NODE_STATE(node));
+    GPU_NODE_STATE(node) = NULL;
+}
+
+static struct cne_node_register ip4_lookup_node = {
+    .process = ip4_lookup_gpu_process,
+    .name = "ip4_lookup",
+    .init = ip4_lookup_gpu_init,
+    .fini = ip4_lookup_gpu_fini,
+    .nb_edges = CNE_NODE_IP4_LOOKUP_NEXT_MAX,
+    .next_nodes =
+        {
+            [CNE_NODE_IP4_LOOKUP_NEXT_REWRITE] = "ip4_rewrite",
+            [CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP] = "pkt_drop",
+        },
+};
+CNE_NODE_REGISTER(ip4_lookup_node);
+
+/* the source node: called once per cne_graph_walk, polls (and so flushes) */
+static uint16_t ip4_lookup_gpu_drain_process(struct cne_graph *graph, struct cne_node *node, void **objs,
+                                             uint16_t nb_objs)
+{
+    (void)objs;
+    (void)nb_objs;
+    struct gpu_graph_state *st = GPU_NODE_STATE(node);
+    return st ? gpu_drain(graph, node, st) : 0;
+}
+
+static int ip4_lookup_gpu_drain_init(const struct cne_graph *graph, struct cne_node *node)
+{
+    struct gpu_graph_state *st = state_get(graph);
+    if (!st)
+        return -ENODEV;
+    GPU_NODE_STATE(node) = st;
+    return 0;
+}
+
+static struct cne_node_register ip4_lookup_gpu_drain_node = {
+    .process = ip4_lookup_gpu_drain_process,
+    .flags = CNE_NODE_SOURCE_F,
+    .name = DRAIN_NODE_NAME,
+    .init = ip4_lookup_gpu_drain_init,
+    .fini = ip4_lookup_gpu_fini,
+    .nb_edges = CNE_NODE_IP4_LOOKUP_NEXT_MAX,
+    .next_nodes =
+        {
+            [CNE_NODE_IP4_LOOKUP_NEXT_REWRITE] = "ip4_rewrite",
+            [CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP] = "pkt_drop",
+        },
+};
+CNE_NODE_REGISTER(ip4_lookup_gpu_drain_node);

@@ -97,6 +97,16 @@ int cndp_node_ip4_rewrite_get(uint16_t next_hop, uint8_t *rewrite_data, uint16_t
                               uint16_t *tx_node, uint16_t *enabled);
 void cndp_node_ip4_rewrite_reset(void);
 
+/* Host regions (AF_XDP UMEMs, the pktmbuf pool: lport_cfg_t.umem_addr /
+ * umem_size, cne_lport.h:91) the GPU nodes may read frames from in place.
+ * An application that calls this once per UMEM gets zero-copy nodes; without
+ * it the nodes stage frame bytes through pinned memory.  Up to 16 regions;
+ * -ENOSPC beyond, -EINVAL for a NULL / empty region.
+ * cndp_node_gpu_umem_get: region i (-ENOENT past the last). */
+int cndp_node_gpu_umem_add(void *addr, uint64_t len);
+int cndp_node_gpu_umem_get(uint32_t i, void **addr, uint64_t *len);
+void cndp_node_gpu_umem_reset(void);
+
 #ifdef __cplusplus
 }
 #endif

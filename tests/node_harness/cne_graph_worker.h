@@ -1,0 +1,27 @@
+/*
+ * Test-only stand-in for cne_graph_worker.h (see cne_graph.h here): the graph
+ * and node objects a node's callbacks see, and cne_node_enqueue (same
+ * signature as cne_graph_worker.h:310-311), which the harness records per edge.
+ */
+#ifndef NODE_HARNESS_CNE_GRAPH_WORKER_H
+#define NODE_HARNESS_CNE_GRAPH_WORKER_H
+#include "cne_graph.h"
+
+struct cne_graph {
+    cne_graph_t id;
+};
+
+struct cne_node {
+    uint8_t ctx[CNE_NODE_CTX_SZ];
+    const struct cne_node_register *reg;
+};
+
+void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16_t nb_objs);
+
+static inline void cne_node_enqueue(struct cne_graph *graph, struct cne_node *node, cne_edge_t next,
+                                    void **objs, uint16_t nb_objs)
+{
+    (void)graph;
+    harness_enqueue(node, next, objs, nb_objs);
+}
+#endif

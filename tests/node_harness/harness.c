@@ -1,0 +1,123 @@
+/*
+ * Test-only driver for cndp_amd/node/ip4_lookup_gpu.c: collects the nodes the
+ * source registers (CNE_NODE_REGISTER), instantiates them for one graph, calls
+ * their process callbacks as cne_graph_walk would (the source node once per
+ * walk, ip4_lookup once per burst it is given) and records, per edge name,
+ * the objects each node enqueues -- the way graph_test.c (test/testcne) drives
+ * fake nodes without a NIC.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "cne_graph_worker.h"
+
+#define MAX_REG 8
+#define MAX_OUT (1u << 22)
+
+static const struct cne_node_register *regs[MAX_REG];
+static int n_regs;
+
+cne_node_t __cne_node_register(const struct cne_node_register *node)
+{
+    if (n_regs == MAX_REG)
+        return CNE_NODE_ID_INVALID;
+    regs[n_regs] = node;
+    return (cne_node_t)n_regs++;
+}
+
+static struct cne_graph g;
+static struct cne_node nodes[MAX_REG];
+static int inited[MAX_REG];
+/* objects enqueued per edge name: 0 = "ip4_rewrite", 1 = "pkt_drop", 2 = other */
+static void **out[3];
+static uint32_t n_out[3];
+static uint64_t enqueue_calls;
+
+static int find(const char *name)
+{
+    for (int i = 0; i < n_regs; i++)
+        if (strcmp(regs[i]->name, name) == 0)
+            return i;
+    return -1;
+}
+
+void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16_t nb_objs)
+{
+    const char *to = next < node->reg->nb_edges ? node->reg->next_nodes[next] : "";
+    const int k = strcmp(to, "ip4_rewrite") == 0 ? 0 : strcmp(to, "pkt_drop") == 0 ? 1 : 2;
+    for (uint16_t i = 0; i < nb_objs && n_out[k] < MAX_OUT; i++)
+        out[k][n_out[k]++] = objs[i];
+    enqueue_calls++;
+}
+
+/* node names and flags as registered, for the test to check */
+int harness_node_info(int i, char *name, uint64_t *flags, int *nb_edges, const char **e0, const char **e1)
+{
+    if (i < 0 || i >= n_regs)
+        return -1;
+    strcpy(name, regs[i]->name);
+    *flags = regs[i]->flags;
+    *nb_edges = regs[i]->nb_edges;
+    *e0 = regs[i]->nb_edges > 0 ? regs[i]->next_nodes[0] : NULL;
+    *e1 = regs[i]->nb_edges > 1 ? regs[i]->next_nodes[1] : NULL;
+    return n_regs;
+}
+
+/* graph create: init every registered node (graph id gid) */
+int harness_graph_create(int gid)
+{
+    g.id = (cne_graph_t)gid;
+    for (int k = 0; k < 3; k++) {
+        if (!out[k] && !(out[k] = malloc(sizeof(void *) * MAX_OUT)))
+            return -12;
+        n_out[k] = 0;
+    }
+    for (int i = 0; i < n_regs; i++) {
+        memset(&nodes[i], 0, sizeof(nodes[i]));
+        nodes[i].reg = regs[i];
+        int r = regs[i]->init ? regs[i]->init(&g, &nodes[i]) : 0;
+        if (r)
+            return r;
+        inited[i] = 1;
+    }
+    return 0;
+}
+
+void harness_graph_destroy(void)
+{
+    for (int i = 0; i < n_regs; i++)
+        if (inited[i] && regs[i]->fini)
+            regs[i]->fini(&g, &nodes[i]);
+    memset(inited, 0, sizeof(inited));
+}
+
+/* one burst into the named node's process() */
+int harness_process(const char *name, void **objs, uint16_t n)
+{
+    const int i = find(name);
+    if (i < 0)
+        return -1;
+    return regs[i]->process(&g, &nodes[i], objs, n);
+}
+
+/* the source nodes' turn of one cne_graph_walk */
+int harness_walk_sources(void)
+{
+    int total = 0;
+    for (int i = 0; i < n_regs; i++)
+        if (regs[i]->flags & CNE_NODE_SOURCE_F)
+            total += regs[i]->process(&g, &nodes[i], NULL, 0);
+    return total;
+}
+
+uint32_t harness_take(int k, void **dst, uint32_t max)
+{
+    const uint32_t n = n_out[k] < max ? n_out[k] : max;
+    memcpy(dst, out[k], n * sizeof(void *));
+    return n;
+}
+
+uint32_t harness_count(int k) { return n_out[k]; }
+uint64_t harness_enqueue_calls(void) { return enqueue_calls; }
+extern int node_mbuf_priv1_dynfield_offset;
+int harness_priv1_offset(void) { return node_mbuf_priv1_dynfield_offset; }

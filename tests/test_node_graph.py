@@ -1,0 +1,137 @@
+"""The GPU ip4_lookup graph node (cndp_amd/node/ip4_lookup_gpu.c), compiled
+against the test-only graph stand-in (tests/node_harness) and driven the way
+cne_graph_walk drives a node: bursts into process(), the source node once per
+walk.  Checks the node registry (names, edges, source flag), the loud failure
+without a GPU, and -- on the GPU -- that every mbuf leaves by the edge and with
+the node_mbuf_priv1 the reference ip4_lookup gives it (ip4_lookup.c:48-256),
+routes added through the exported cne_node_ip4_route_add."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from cndp_amd import native as N
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HARNESS = os.path.join(HERE, "node_harness", "libnode_harness.so")
+
+
+def _harness():
+    if not os.path.exists(HARNESS):
+        pytest.skip("node harness not built (build() makes it)")
+    N.lib()  # the same libcndp_gpu.so instance the harness links
+    H = ctypes.CDLL(HARNESS)
+    H.harness_node_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(ctypes.c_char_p)]
+    H.harness_process.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint16]
+    H.harness_take.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32]
+    H.harness_take.restype = ctypes.c_uint32
+    H.harness_count.restype = ctypes.c_uint32
+    H.harness_enqueue_calls.restype = ctypes.c_uint64
+    return H
+
+
+def test_node_registry():
+    """Same node name and edges as ip4_lookup.c:345-359, plus the drain source
+    node the "ip4*" pattern of l3fwd-graph (fwd.c:128) also picks up."""
+    H = _harness()
+    info = {}
+    name = ctypes.create_string_buffer(64)
+    fl, ne = ctypes.c_uint64(), ctypes.c_int()
+    e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
+    n = H.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+    for i in range(n):
+        H.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+        info[name.value.decode()] = (fl.value, ne.value, e0.value, e1.value)
+    assert info["ip4_lookup"] == (0, 2, b"ip4_rewrite", b"pkt_drop")
+    assert info["ip4_lookup_gpu_drain"] == (1, 2, b"ip4_rewrite", b"pkt_drop")
+    assert all(k.startswith("ip4") for k in info)
+
+
+def test_node_init_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    H = _harness()
+    assert H.harness_graph_create(0) == -19   # -ENODEV: there is no CPU path behind the node
+    assert H.harness_priv1_offset() == 56      # offsetof(pktmbuf_t, udata64), set as ip4_lookup_node_init does
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_node_graph_walk(gpu, zero_copy):
+    from cndp_amd import pktgen
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    from cndp_amd.mbuf import MbufPool
+    from oracle import oracle as O
+    import torch
+    H = _harness()
+    L = N.lib()
+    NodeFib.fini()
+    L.cndp_node_gpu_umem_reset()
+    n = 30000
+    pool = MbufPool(n)
+    a = pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=77)
+    f = pktgen.fuzz_frames(n, seed=78, slot=64)
+    slab = a.slab.view(n, 64).clone()
+    fz = torch.zeros(n * 64, dtype=torch.uint8)
+    fz[: f.slab.numel()] = f.slab
+    slab[torch.arange(n) % 6 == 1] = fz.view(n, 64)[torch.arange(n) % 6 == 1]
+    pool.fill(pktgen.Frames(slab.reshape(-1), n, stride=64))
+    if zero_copy:
+        assert L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes) == 0
+    os.environ["CNDP_GPU_BATCH"] = "2048"
+    os.environ["CNDP_GPU_DEPTH"] = "3"
+    try:
+        assert H.harness_graph_create(3) == 0
+        # routes after graph create, as l3fwd-graph does (fwd.c:160-201)
+        routes = pktgen.l3fwd_routes()
+        for ip, d, nh in routes:
+            assert cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
+        rng = np.random.default_rng(1)
+        order = rng.permutation(n)
+        pos = 0
+        while pos < n:
+            b = int(min(n - pos, rng.choice([256, 256, 200, 31, 1])))
+            ptrs = pool.ptrs(order[pos:pos + b])
+            assert H.harness_process(b"ip4_lookup", ptrs, b) == b
+            H.harness_walk_sources()
+            pos += b
+        for _ in range(100000):   # later walks drain the rest (flush on idle)
+            if H.harness_count(0) + H.harness_count(1) == n:
+                break
+            H.harness_walk_sources()
+        got = []
+        for k in (0, 1):
+            cnt = H.harness_count(k)
+            buf = (ctypes.c_void_p * max(cnt, 1))()
+            H.harness_take(k, buf, cnt)
+            got.append(pool.index_of([x for x in buf[:cnt]]))
+        assert H.harness_count(2) == 0
+        assert len(got[0]) + len(got[1]) == n
+    finally:
+        H.harness_graph_destroy()
+        os.environ.pop("CNDP_GPU_BATCH", None)
+        os.environ.pop("CNDP_GPU_DEPTH", None)
+        L.cndp_node_gpu_umem_reset()
+    vals = [(ip, d, nh) for ip, d, nh in routes]
+    t24, t8 = O.dir24_8_build(vals, N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
+    d = pool.data_pos().astype(np.int64)
+    bb = pool.mem
+    dip = np.zeros(n, np.uint32)
+    for k in range(4):
+        dip = (dip << 8) | bb[d + 30 + k].astype(np.uint32)
+    val = O.dir24_8_lookup(t24, t8, dip).astype(np.uint64)
+    ttl = bb[d + 22].astype(np.uint64)
+    ck = bb[d + 24].astype(np.uint64) | (bb[d + 25].astype(np.uint64) << 8)
+    assert np.array_equal(pool.hdr["udata64"], (val & 0xFFFF) | (ttl << 16) | (ck << 32))
+    for k in (0, 1):
+        assert np.all((val[got[k]] >> 16) == k)
+        # each edge's stream keeps the arrival order (a subsequence of it)
+        rank = np.empty(n, np.int64)
+        rank[order] = np.arange(n)
+        assert np.all(np.diff(rank[got[k]]) > 0)
+    assert len(got[0]) > 0 and len(got[1]) > 0
+    NodeFib.fini()

@@ -1,0 +1,60 @@
+"""Per-call latency of the host-array FIB lookups (cne_fib_lookup_bulk /
+cne_fib6_lookup_bulk) on the GPU: n = 4 (ip4_lookup's 4-wide call), 256 (a
+graph burst, examples/cndpfwd/l3-fwd.c:85), 64K; median / p99 over many calls.
+usage: python tools/fib_latency.py [--json out.json]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cndp_amd import native as N  # noqa: E402
+from cndp_amd import pktgen  # noqa: E402
+from cndp_amd.fib import Fib, Fib6, node_ip4_route_add  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json")
+    ap.add_argument("--calls", type=int, default=2000)
+    args = ap.parse_args()
+    f = Fib("lat", N.CNE_FIB_DIR24_8, default_nh=1 << 16, max_routes=1024, nh_sz=N.CNE_FIB_DIR24_8_4B,
+            num_tbl8=256)
+    for ip, d, nh in pktgen.l3fwd_routes():
+        node_ip4_route_add(f, ip, d, nh, 0)
+    f6 = Fib6("lat6", N.CNE_FIB_TRIE, default_nh=0, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15)
+    for ip, d, i in pktgen.v6_routes():
+        f6.add(ip, d, i)
+    rng = np.random.default_rng(0)
+    res = {}
+    L = N.lib()
+    for n in (4, 256, 65536):
+        ips = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        ips[::2] = (10 << 24) | (ips[::2] & 0x0003FFFF)
+        out = np.zeros(n, np.uint64)
+        ips6 = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+        ips6[:, :4] = [0x20, 0x01, 0x0d, 0xb8]
+        calls = args.calls if n <= 256 else max(50, args.calls // 20)
+        for tag, fn, arg in (("v4", L.cne_fib_lookup_bulk, (f.h, ips.ctypes.data, out.ctypes.data, n)),
+                             ("v6", L.cne_fib6_lookup_bulk, (f6.h, ips6.ctypes.data, out.ctypes.data, n))):
+            for _ in range(20):
+                assert fn(*arg) == 0
+            t = np.empty(calls)
+            for k in range(calls):
+                t0 = time.perf_counter_ns()
+                fn(*arg)
+                t[k] = time.perf_counter_ns() - t0
+            res[f"{tag}_n{n}"] = {"median_us": round(float(np.median(t)) / 1e3, 2),
+                                 "p99_us": round(float(np.percentile(t, 99)) / 1e3, 2),
+                                 "Mlookups_per_s": round(n / (float(np.median(t)) / 1e3), 2)}
+    print(json.dumps(res, indent=1))
+    if args.json:
+        with open(args.json, "w") as fo:
+            json.dump(res, fo, indent=1)
+
+
+if __name__ == "__main__":
+    main()
