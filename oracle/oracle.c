@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /*
  * oracle.c -- CPU restatement of CNDP's parse / Toeplitz / LPM hot path.
  *
@@ -243,6 +244,32 @@ void orc_dir24_8_lookup(const uint32_t *tbl24, const uint32_t *tbl8, const uint3
                         uint32_t n, uint64_t *nh)
 {
     for (uint32_t i = 0; i < n; i++) {
+        uint32_t e = tbl24[ips[i] >> 8];
+        if (e & 1u)
+            e = tbl8[(uint8_t)ips[i] + (e >> 1) * 256u];
+        nh[i] = e >> 1;
+    }
+}
+
+/* dir24_8.h:118-148 LOOKUP_FUNC(4b, uint32_t, 15, 2), the lookup the
+ * reference's cne_fib_lookup_bulk runs by default: prefetch the
+ * tbl24 entries of the first min(15, n) keys, then look up key i while
+ * prefetching key i + 15.  Same results as orc_dir24_8_lookup. */
+void orc_dir24_8_lookup_bulk_pf(const uint32_t *tbl24, const uint32_t *tbl8, const uint32_t *ips, uint32_t n,
+                                uint64_t *nh)
+{
+    const uint32_t pf = n < 15u ? n : 15u;
+    uint32_t i;
+    for (i = 0; i < pf; i++)
+        __builtin_prefetch(&tbl24[ips[i] >> 8], 0, 3);
+    for (i = 0; i < n - pf; i++) {
+        __builtin_prefetch(&tbl24[ips[i + pf] >> 8], 0, 3);
+        uint32_t e = tbl24[ips[i] >> 8];
+        if (e & 1u)
+            e = tbl8[(uint8_t)ips[i] + (e >> 1) * 256u];
+        nh[i] = e >> 1;
+    }
+    for (; i < n; i++) {
         uint32_t e = tbl24[ips[i] >> 8];
         if (e & 1u)
             e = tbl8[(uint8_t)ips[i] + (e >> 1) * 256u];
@@ -952,12 +979,24 @@ struct bench_shard {
     const struct orc_classify_args *a;
     uint32_t lo, hi;
     int iters;
+    int cpu; /* pinned to this CPU (-1: not pinned) */
     uint64_t sink;
 };
+
+static void bench_pin(int cpu)
+{
+    if (cpu < 0)
+        return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
 
 static void *bench_worker(void *arg)
 {
     struct bench_shard *s = arg;
+    bench_pin(s->cpu);
     const struct orc_classify_args *a = s->a;
     const uint8_t *ptrs[256];
     uint32_t ptype[256];
@@ -980,7 +1019,7 @@ static void *bench_worker(void *arg)
                 uint32_t m = cnt - k < 4 ? cnt - k : 4;
                 for (uint32_t q = 0; q < m; q++)
                     dip[q] = ptype[k + q] == 0x90u ? rd_be32(ptrs[k + q] + 30) : 0;
-                orc_dir24_8_lookup(a->tbl24, a->tbl8, dip, m, dst);
+                orc_dir24_8_lookup_bulk_pf(a->tbl24, a->tbl8, dip, m, dst);
                 for (uint32_t q = 0; q < m; q++) {
                     const uint8_t *ip = ptrs[k + q] + 14;
                     uint32_t h = 0;
@@ -1001,6 +1040,80 @@ static void *bench_worker(void *arg)
     return NULL;
 }
 
+/* cnet chain per 256-packet burst (eth_rx.c:65-109 parse into the mbuf
+ * fields, ptype.c:48-210 speculation over the burst, ip4_input / ip6_input
+ * length + checksum + 4-wide lookups), plus the build's flow hash: each
+ * thread runs classify_one over its bursts and then walks the burst's types
+ * as the ptype node does. */
+static void *cnet_bench_worker(void *arg)
+{
+    struct bench_shard *s = arg;
+    bench_pin(s->cpu);
+    struct orc_classify_args b = *s->a;
+    b.bins = NULL;
+    uint64_t sink = 0;
+    uint16_t last_type = 0;
+    for (int it = 0; it < s->iters; it++) {
+        for (uint32_t b0 = s->lo; b0 < s->hi; b0 += 256) {
+            const uint32_t cnt = s->hi - b0 < 256 ? s->hi - b0 : 256;
+            for (uint32_t k = 0; k < cnt; k++)
+                classify_one(&b, b0 + k);
+            uint16_t next_index = cnet_ptype_edge(last_type);
+            uint32_t k = 0;
+            for (; k + 4 <= cnt; k += 4) {
+                const uint16_t g0 = (uint16_t)b.ptype[b0 + k], g1 = (uint16_t)b.ptype[b0 + k + 1],
+                               g2 = (uint16_t)b.ptype[b0 + k + 2], g3 = (uint16_t)b.ptype[b0 + k + 3];
+                const uint8_t fix = (uint8_t)((last_type ^ g0) | (last_type ^ g1) | (last_type ^ g2) |
+                                              (last_type ^ g3));
+                if (fix) {
+                    if (last_type != g3 && g2 == g3 && next_index != cnet_ptype_edge(g3)) {
+                        next_index = cnet_ptype_edge(g3);
+                        last_type = g3;
+                    } else if (next_index == cnet_ptype_edge(g3)) {
+                        last_type = g3;
+                    }
+                }
+                sink += next_index;
+            }
+            for (; k < cnt; k++)
+                sink += b.nh[b0 + k] ^ b.hash[b0 + k];
+        }
+    }
+    s->sink = sink;
+    return NULL;
+}
+
+/* Per-burst CPU baseline on nthreads threads, thread t pinned to cpus[t]
+ * when cpus is given: the l3fwd node loop (MODE_L3FWD / MODE_HASH) or the
+ * cnet chain (MODE_CNET, needs a->ptype).  Returns seconds. */
+double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iters, const int *cpus)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 512)
+        nthreads = 512;
+    if (a->mode == MODE_CNET && !a->ptype)
+        return -1.0;
+    static struct bench_shard sh[512];
+    static pthread_t th[512];
+    uint32_t per = (a->n + nthreads - 1) / nthreads;
+    per = (per + 255) & ~255u;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < nthreads; t++) {
+        sh[t].a = a;
+        sh[t].lo = (uint32_t)t * per < a->n ? (uint32_t)t * per : a->n;
+        sh[t].hi = sh[t].lo + per < a->n ? sh[t].lo + per : a->n;
+        sh[t].iters = iters;
+        sh[t].cpu = cpus ? cpus[t] : -1;
+        pthread_create(&th[t], NULL, a->mode == MODE_CNET ? cnet_bench_worker : bench_worker, &sh[t]);
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, int iters)
 {
     if (nthreads < 1)
@@ -1018,6 +1131,7 @@ double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, in
         sh[t].lo = (uint32_t)t * per < a->n ? (uint32_t)t * per : a->n;
         sh[t].hi = sh[t].lo + per < a->n ? sh[t].lo + per : a->n;
         sh[t].iters = iters;
+        sh[t].cpu = -1;
         pthread_create(&th[t], NULL, bench_worker, &sh[t]);
     }
     for (int t = 0; t < nthreads; t++)

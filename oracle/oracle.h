@@ -127,6 +127,9 @@ int orc_classify(const struct orc_classify_args *a);
  * arrays (256-pkt bursts, ip4_lookup.c:83-241), used as the CPU baseline.
  * Multi-threaded over nthreads contiguous shards; returns elapsed seconds. */
 double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, int iters);
+double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iters, const int *cpus);
+void orc_dir24_8_lookup_bulk_pf(const uint32_t *tbl24, const uint32_t *tbl8, const uint32_t *ips, uint32_t n,
+                                uint64_t *nh);
 
 /* ip4_rewrite node (ip4_rewrite.c:40-247) over a batch cut into graph
  * bursts of `burst` packets.  nh[i] is the l3fwd classify output (edge << 16

@@ -74,6 +74,9 @@ def lib():
         L.orc_classify.argtypes = [POINTER(ClassifyArgs)]
         L.orc_l3fwd_burst_bench.restype = c_double
         L.orc_l3fwd_burst_bench.argtypes = [POINTER(ClassifyArgs), c_int, c_int]
+        L.orc_burst_bench.restype = c_double
+        L.orc_burst_bench.argtypes = [POINTER(ClassifyArgs), c_int, c_int, c_void_p]
+        L.orc_dir24_8_lookup_bulk_pf.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
         L.orc_ip4_rewrite.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32, c_void_p,
                                       c_uint32, c_void_p, c_void_p]
         L.orc_mac_swap.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]
@@ -215,6 +218,23 @@ def classify(mode, slab, n, **kw) -> dict:
     if rc < 0:
         raise OSError(-rc, "orc_classify")
     del keep
+    return out
+
+
+def burst_bench(mode, slab, n, nthreads=1, iters=1, cpus=None, **kw) -> float:
+    """Seconds for `iters` passes of the per-burst CPU chain over n packets on
+    nthreads threads (thread t pinned to cpus[t] when given)."""
+    a, out, keep = make_args(mode, slab, n, **kw)
+    cp = np.ascontiguousarray(cpus, dtype=np.int32) if cpus is not None else None
+    t = lib().orc_burst_bench(ctypes.byref(a), nthreads, iters, _p(cp))
+    del keep, cp
+    return t
+
+
+def dir24_8_lookup_bulk_pf(t24, t8, ips) -> np.ndarray:
+    ips = np.ascontiguousarray(ips, dtype=np.uint32)
+    out = np.zeros(len(ips), np.uint64)
+    lib().orc_dir24_8_lookup_bulk_pf(_p(t24), _p(t8), _p(ips), len(ips), _p(out))
     return out
 
 

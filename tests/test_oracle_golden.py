@@ -235,3 +235,35 @@ def test_oracle_rxmeta_known_answers():
     assert list(l4) == [32, 8, 0, 32]
     assert [(x >> 29) & 7 for x in m] == [0, 4, 2, 1]      # IPv6, BCAST, MCAST bits
     assert list(r["ptype"][:3]) == [0x111, 0x241, 0x3]
+
+
+def test_prefetching_bulk_lookup_matches():
+    """dir24_8.h:118-148 restated with its prefetch schedule (the CPU
+    baseline's lookup) == the plain lookup, for every n around the 15-ahead
+    prefetch distance."""
+    from cndp_amd import pktgen
+    vals = [(ip, d, nh) for ip, d, nh in pktgen.l3fwd_routes()]
+    t24, t8 = O.dir24_8_build(vals, 1 << 16, 256)
+    rng = np.random.default_rng(4)
+    for n in (0, 1, 4, 14, 15, 16, 31, 1000):
+        ips = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        ips[::2] = (10 << 24) | (ips[::2] & 0x0004FFFF)
+        assert np.array_equal(O.dir24_8_lookup_bulk_pf(t24, t8, ips), O.dir24_8_lookup(t24, t8, ips))
+
+
+def test_burst_bench_runs_both_chains():
+    """The CPU baselines (l3fwd node loop, cnet chain) run pinned on 2 threads."""
+    from cndp_amd import pktgen
+    import os as _os
+    vals = [(ip, d, nh) for ip, d, nh in pktgen.l3fwd_routes()]
+    t4 = O.dir24_8_build(vals, 1 << 16, 256)
+    fr = pktgen.packed_ipv4(4096, routes=pktgen.l3fwd_routes())
+    slab = fr.slab.numpy()
+    cpus = sorted(_os.sched_getaffinity(0))[:2]
+    assert O.burst_bench(O.MODE_L3FWD, slab, 4096, nthreads=len(cpus), cpus=cpus, stride=64, tables4=t4) > 0
+    v6 = pktgen.v6_routes()
+    t6 = O.trie_build([(ip, d, i | (1 << 24)) for ip, d, i in v6], 1025, 1 << 15)
+    im = pktgen.imix(4096, v4routes=pktgen.l3fwd_routes(), v6routes=v6)
+    t = O.burst_bench(O.MODE_CNET, im.slab.numpy(), 4096, nthreads=len(cpus), cpus=cpus,
+                      offsets=im.offsets.numpy().astype(np.uint64), tables4=t4, tables6=t6)
+    assert t > 0
