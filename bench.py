@@ -10,6 +10,15 @@ N > 1 (torchrun) every rank classifies its own batch (weak scaling, no data
 collective); after the K timed steps the per-bin counters are all-reduced
 once over RCCL (the "final per-output-port count reduce").  Rank 0 prints one
 JSON line.  Inputs are generated in HBM (synthetic, seeded) before timing.
+
+The same line carries, besides the headline:
+  configs        every other BASELINE config measured the same way (C2, C4,
+                 C5), each with its roofline object and its CPU baseline;
+  node_boundary  the graph-node boundary over pktmbuf_t bursts of 256 (the
+                 GPU ip4_lookup node, the cnet queue) next to one CPU core
+                 running the same nodes;
+  host_memory_e2e  frames starting and ending in host memory (packed slab and
+                 the AF_XDP UMEM layout), never `value`.
 """
 from __future__ import annotations
 
@@ -182,25 +191,65 @@ def parity_sample(state, k: int = 1 << 16) -> bool:
     return ok
 
 
+def host_cpus():
+    """CPUs this process may run on, the CPU model, and the cgroup CPU quota."""
+    cpus = sorted(os.sched_getaffinity(0))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return cpus, model, quota
+
+
 def cpu_baseline(state, budget_s: float = 10.0):
-    """The oracle's per-burst l3fwd loop on this host's cores (rank 0, N=1)."""
+    """The oracle's per-burst chain on this host's cores (rank 0, N=1): the
+    l3fwd node loop (C2 / C3) or the cnet chain (C4 / C5), per 256-packet
+    burst, one pinned thread per CPU of the process's affinity set, and 1
+    thread.  Bounded sample of the same frames, repeated to ~budget_s."""
+    from cndp_amd import native as N
     from oracle import oracle as O
-    fr = state["frames"]
-    n = min(fr.n, 1 << 22)
-    slab = np.concatenate([fr.slab[: n * fr.stride].cpu().numpy(), np.zeros(256, np.uint8)])
-    t24, t8 = (x.copy() for x in state["fib"].image())
-    threads = max(1, min(16, os.cpu_count() or 1))
-    t1 = O.l3fwd_burst_bench(slab, n, fr.stride, (t24, t8), nthreads=1, iters=1)
+    fr, mode = state["frames"], state["mode"]
+    cnet = mode == N.CNDP_MODE_CNET
+    n = min(fr.n, (1 << 20) if cnet else (1 << 22))
+    kw = {"tables4": tuple(x.copy() for x in state["fib"].image())}
+    if cnet:
+        kw["tables6"] = tuple(x.copy() for x in state["fib6"].image())
+    if fr.offsets is not None:
+        offs = fr.offsets[:n].cpu().numpy().astype(np.uint64)
+        slab = fr.slab[: int(offs[-1]) + 2048].cpu().numpy()
+        kw["offsets"] = offs
+    else:
+        slab = np.concatenate([fr.slab[: n * fr.stride].cpu().numpy(), np.zeros(2048, np.uint8)])
+        kw.update(stride=fr.stride, data_off=fr.data_off)
+    cpus, model, quota = host_cpus()
+    t1 = O.burst_bench(mode, slab, n, nthreads=1, iters=1, cpus=cpus[:1], **kw)
     single = n / t1 / 1e6
-    tt = O.l3fwd_burst_bench(slab, n, fr.stride, (t24, t8), nthreads=threads, iters=1)
+    tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=1, cpus=cpus, **kw)
     iters = max(1, int(budget_s / max(tt, 1e-6)))
-    tt = O.l3fwd_burst_bench(slab, n, fr.stride, (t24, t8), nthreads=threads, iters=iters)
+    tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=iters, cpus=cpus, **kw)
     multi = n * iters / tt / 1e6
-    return {"value": round(multi, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-            "sample": (f"oracle/oracle.c per-256-burst l3fwd loop (ethertype parse, 4-wide DIR-24-8 "
-                       f"lookup, cne_softrss restatement, RETA) over {n} of the same 64-B frames x "
-                       f"{iters} passes on {threads} host threads ({tt:.1f} s); 1 thread: "
-                       f"{single:.1f} Mpps")}
+    chain = ("cnet chain per 256-burst (cne_get_ptype restatement, eth_rx fields, ptype-node speculation, "
+             "ip4/ip6_input length + checksum + DIR-24-8 / trie lookups, cne_softrss)" if cnet else
+             "l3fwd node loop per 256-burst (ethertype parse, pkt_cls, ip4_lookup's 4-wide "
+             "cne_fib_lookup_bulk with dir24_8.h's prefetching lookup" +
+             (", skipped in C2" if mode == N.CNDP_MODE_HASH else "") + ", cne_softrss restatement, RETA)")
+    return {"value": round(multi, 2), "unit": "Mpps", "cores": len(cpus), "kind": "port",
+            "cpu_model": model, "cgroup_cpu_quota": quota, "single_core_Mpps": round(single, 2),
+            "sample": (f"oracle/oracle.c {chain} over {n} of the same frames x {iters} passes on "
+                       f"{len(cpus)} pinned threads ({tt:.1f} s); 1 thread: {single:.2f} Mpps")}
 
 
 def sweep(st, stream, cfg):
@@ -245,7 +294,7 @@ def sweep(st, stream, cfg):
                   load_nt=1)
 
 
-def e2e_host(st, reps: int = 5):
+def e2e_host(st, reps: int = 5, frames=None):
     """Host-memory rates (rank 0, N=1): the frames start in host memory and
     the results end there (SURVEY §8(d) 'End to end').  Two paths, same
     kernel, same batch:
@@ -256,7 +305,8 @@ def e2e_host(st, reps: int = 5):
                       as an AF_XDP UMEM would be) and read by the kernel over
                       PCIe; results to HBM."""
     import mmap
-    fr, cl, mode, n = st["frames"], st["cl"], st["mode"], st["n"]
+    fr, cl, mode = frames or st["frames"], st["cl"], st["mode"]
+    n = fr.n
     res = {}
     host = fr.slab.cpu().pin_memory()
     offs = fr.offsets.cpu().pin_memory() if fr.offsets is not None else None
@@ -300,18 +350,24 @@ def e2e_host(st, reps: int = 5):
     return res
 
 
-def imix_line(dev, rank: int, world: int, steps: int, warmup: int, parity: bool):
-    """Secondary line for the IMIX half of the metric (config C4, cnet chain),
-    measured the same way as the headline: ring of batches, one event pair
-    around `steps` back-to-back launches, max over ranks."""
+def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, parity: bool,
+                cpu: bool, cpu_budget: float):
+    """One more BASELINE config measured like the headline: ring of batches,
+    one event pair around `steps` back-to-back launches, max over ranks, with
+    its roofline object (traffic from profiles/pmc_<cfg>.json) and, on rank 0
+    at N=1, its CPU baseline."""
     from cndp_amd import dist as D
-    st = build_state("c4", dev, rank, None)
+    st = build_state(cfg, dev, rank, None)
     stream = torch.cuda.current_stream(dev)
     for k in range(warmup):
         run_step(st, stream, k)
     torch.cuda.synchronize()
     ok = parity_sample(st) if parity and rank == 0 else None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
     for k in range(steps):
@@ -323,13 +379,120 @@ def imix_line(dev, rank: int, world: int, steps: int, warmup: int, parity: bool)
     elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], dev)
     n = st["n"]
     achieved = st["algo"] * n / (kern_ms * 1e-3) / 1e9
-    res = {"config": "c4", "workload": st["desc"], "value": round(n * world * steps / elapsed / 1e6, 2),
-           "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "kernel_ms": round(kern_ms, 5),
-           "achieved_GBs": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-           "algorithmic_bytes_per_pkt": st["algo"], "ring_batches": len(st["ring"]),
-           "parity_sample_vs_oracle": ok}
+    value = n * world * steps / elapsed / 1e6
+    res = {"config": cfg, "workload": st["desc"], "value": round(value, 2),
+           "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "packets_per_gpu": n,
+           "ring_batches": len(st["ring"]), "parity_sample_vs_oracle": ok,
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(cfg),
+                        "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_pkt": st["algo"]}}
+    if cfg == "c5":  # the 1500-B point also as wire-equivalent bandwidth
+        pps = value * 1e6
+        res["wire_Gbps"] = {"l2_1500B": round(pps * 1500 * 8 / 1e9, 1),
+                            "line_1500B_plus_20B_preamble_ifg": round(pps * 1520 * 8 / 1e9, 1)}
+    if cpu and rank == 0 and world == 1:
+        try:
+            res["cpu_baseline"] = cpu_baseline(st, cpu_budget)
+        except Exception as ex:  # reported, never fatal
+            res["cpu_baseline"] = {"error": repr(ex)}
     del st
     torch.cuda.empty_cache()
+    return res
+
+
+def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
+    """The graph-node boundary over pktmbuf_t bursts (rank 0, N=1).  One host
+    thread drives, as one lcore's graph walk would:
+      l3fwd : the GPU ip4_lookup node (cndp_amd/node/ip4_lookup_gpu.c, through
+              the test-only graph stand-in) -- process() per burst, the drain
+              source node per walk -- mbufs in a UMEM-layout pool, read in
+              place (zero-copy) or staged; beside it the ip4_lookup node's CPU
+              loop over the same mbufs on one core;
+      cnet  : the cnet queue (eth_rx + ptype + ip4/ip6_input) driven per burst
+              from C, zero-copy and staged; beside it the cnet chain on one core.
+    Rates are mbufs in -> mbufs out with every field written back."""
+    import ctypes
+    from cndp_amd import native as N
+    from cndp_amd import pktgen
+    from cndp_amd.classify import Classifier
+    from cndp_amd.fib import Fib, Fib6, NodeFib, cne_node_ip4_route_add, node_ip4_add_input, node_ip6_add_input
+    from cndp_amd.mbuf import MbufPool, MbufQueue
+    from oracle import oracle as O
+    hp = os.path.join(ROOT, "tests", "node_harness", "libnode_harness.so")
+    L = N.lib()
+    H = ctypes.CDLL(hp)
+    H.harness_drive.restype = ctypes.c_double
+    H.harness_drive.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int]
+    H.harness_mq_drive.restype = ctypes.c_double
+    H.harness_mq_drive.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int]
+    res = {"burst": burst, "mbufs": n, "host_threads": 1, "batch": 8192, "depth": 4,
+           "pool": "2 KiB frames, pktmbuf_t at +0, data at +256 (pktmbuf.c:60-80)"}
+    routes = pktgen.l3fwd_routes()
+    # ---- l3fwd: the ip4_lookup node
+    pool = MbufPool(n)
+    pool.fill(pktgen.packed_ipv4(n, routes=routes, seed=99))
+    ptrs = pool.ptrs(np.arange(n))
+    l3 = {}
+    NodeFib.fini()
+    for zc in (True, False):
+        L.cndp_node_gpu_umem_reset()
+        if zc:
+            L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
+        assert H.harness_graph_create(10 + int(zc)) == 0
+        for ip, d, nh in routes:
+            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+        H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
+        t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
+        H.harness_graph_destroy()
+        l3["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+    L.cndp_node_gpu_umem_reset()
+    fib = NodeFib()
+    t24, t8 = (x.copy() for x in fib.image())
+    O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, 1)
+    t = O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
+    l3["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+    l3["cpu_chain"] = "the ip4_lookup node loop over the same mbufs (oracle/oracle.c orc_ip4_lookup_mbufs)"
+    NodeFib.fini()
+    res["l3fwd_ip4_lookup"] = l3
+    del ptrs, pool
+    # ---- cnet: eth_rx + ptype + ip4_input / ip6_input
+    nc = n // 4
+    v6 = pktgen.v6_routes()
+    cl = Classifier(dev.index)
+    f4 = Fib("nb4", N.CNE_FIB_DIR24_8, default_nh=1025, max_routes=1024, nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=256)
+    for i, (ip, d, _) in enumerate(routes):
+        node_ip4_add_input(f4, ip, d, i)
+    f6 = Fib6("nb6", N.CNE_FIB_TRIE, default_nh=1025, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15)
+    for ip, d, i in v6:
+        node_ip6_add_input(f6, ip, d, i)
+    cl.set_fib(f4, f6)
+    pool = MbufPool(nc)
+    pool.fill(pktgen.imix(nc, v4routes=routes, v6routes=v6, seed=98))
+    ptrs = pool.ptrs(np.arange(nc))
+    cn = {}
+    for zc in (True, False):
+        umem = None
+        if zc:
+            cl.host_register(pool.mem)
+            umem = pool.base
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=8192, depth=4, umem=umem)
+        H.harness_mq_drive(q.h, ptrs, nc, burst, 1)
+        t = H.harness_mq_drive(q.h, ptrs, nc, burst, passes)
+        q.close()
+        if zc:
+            cl.host_unregister(pool.mem)
+        cn["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(nc * passes / t / 1e6, 2) if t > 0 else None
+    # the cnet chain on one core over the same frames (the pool as the slab)
+    kw = {"tables4": tuple(x.copy() for x in f4.image()), "tables6": tuple(x.copy() for x in f6.image()),
+          "offsets": pool.data_pos().astype(np.uint64)}
+    cpus, _, _ = host_cpus()
+    O.burst_bench(N.CNDP_MODE_CNET, pool.mem, nc, nthreads=1, iters=1, cpus=cpus[:1], **kw)
+    t = O.burst_bench(N.CNDP_MODE_CNET, pool.mem, nc, nthreads=1, iters=passes, cpus=cpus[:1], **kw)
+    cn["cpu_1core_Mpps"] = round(nc * passes / t / 1e6, 2)
+    cn["mbufs"] = nc
+    cn["frames"] = "IMIX 64/570/1500 7:4:1, IPv4+IPv6"
+    res["cnet"] = cn
+    cl.close()
     return res
 
 
@@ -356,7 +519,10 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe) rates")
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant (stderr + gpurun_out)")
-    ap.add_argument("--no-imix", action="store_true", help="skip the secondary IMIX (C4) line")
+    ap.add_argument("--extra", default="c2,c4,c5",
+                    help="other configs measured after the headline (comma list, '' = none)")
+    ap.add_argument("--no-imix", action="store_true", help="same as --extra ''")
+    ap.add_argument("--no-node", action="store_true", help="skip the pktmbuf node-boundary rates")
     ap.add_argument("--in-route-frac", type=float, default=0.9,
                     help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
     ap.add_argument("--ring", type=int, default=0,
@@ -371,6 +537,8 @@ def main():
     ap.add_argument("--unroll", type=int, default=None)
     ap.add_argument("--bpc", type=int, default=None)
     args = ap.parse_args()
+    if args.no_imix:
+        args.extra = ""
 
     from cndp_amd import dist as D
     world, rank, local = setup_dist()
@@ -429,27 +597,44 @@ def main():
     layout = ("packed 64-B slots" if fr.offsets is None and fr.stride == 64
               else ("IMIX packed at roundup(len,64)" if fr.offsets is not None else f"{fr.stride}-B slots"))
     ring_len = len(st["ring"])
-    cpu = e2e = None
-    if rank == 0:
-        if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
+    cpu = e2e = nb = None
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline and args.config != "c3rw":
             cpu = cpu_baseline(st, args.cpu_budget)
-        if world == 1 and not args.no_e2e and args.config != "c3rw":
+        if not args.no_e2e and args.config != "c3rw":
             try:
-                e2e = e2e_host(st)
+                e2e = {"packed_slab": e2e_host(st)}
+                if args.config in ("c2", "c3"):
+                    # the AF_XDP UMEM layout: 2 KiB frames, data at +256 (pktmbuf.c:60-80)
+                    from cndp_amd import pktgen
+                    um = pktgen.umem_ipv4(1 << 22, routes=st["routes"], seed=5, device=dev)
+                    e2e["umem_2KiB_frames"] = e2e_host(st, frames=um)
+                    e2e["umem_2KiB_frames"]["packets"] = um.n
+                    del um
                 log(f"[bench] host-memory rates: {e2e}")
             except Exception as ex:  # reported, never fatal for the headline line
                 e2e = {"error": repr(ex)}
-    imix = None
-    if args.config in ("c2", "c3") and not args.no_imix:  # every rank (max over ranks inside)
+    extra = {}
+    todo = [c for c in args.extra.split(",") if c and c != args.config] if args.config in ("c2", "c3") else []
+    if todo:  # every rank (max over ranks inside)
         del st["ring"], fr, out
         st.pop("frames", None)
         torch.cuda.empty_cache()
+    for c in todo:
         try:
-            imix = imix_line(dev, rank, world, max(5, args.steps // 2), args.warmup, not args.no_parity)
+            extra[c] = config_line(c, dev, rank, world, max(5, args.steps // 2), args.warmup, not args.no_parity,
+                                   not args.no_cpu_baseline, min(args.cpu_budget, 5.0))
             if rank == 0:
-                log(f"[bench] IMIX (C4) line: {imix}")
+                log(f"[bench] {c} line: {extra[c]}")
         except Exception as ex:  # reported, never fatal for the headline line
-            imix = {"error": repr(ex)}
+            extra[c] = {"error": repr(ex)}
+        torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_node:
+        try:
+            nb = node_boundary(dev)
+            log(f"[bench] node boundary: {nb}")
+        except Exception as ex:  # reported, never fatal for the headline line
+            nb = {"error": repr(ex)}
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -476,8 +661,9 @@ def main():
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_pkt": st["algo"]},
             "cpu_baseline": cpu,
+            "configs": extra,
+            "node_boundary": nb,
             "host_memory_e2e": e2e,
-            "imix": imix,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -3865,6 +3865,8 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         return;
     hipSetDevice(c->dev);
     hipDeviceSynchronize(); // nothing in flight may still use the scratch below
+    for (int k = 0; k < c->n_reg; k++) // regions registered through this context
+        hipHostUnregister(c->reg[k].host);
     if (c->ev_scratch)
         hipEventDestroy(c->ev_scratch);
     for (int k = 0; k < 3; k++)

@@ -71,6 +71,13 @@ class MbufPool:
             else:
                 lengths = np.full(n, frames.stride, np.int64)
         dpos = self.data_pos()
+        if frames.offsets is None and frames.lengths is None and slab.size >= n * frames.stride \
+                and np.all(self.hdr["data_off"][:n] == HEADROOM):
+            ln = int(min(frames.stride, max_bytes))   # fixed-stride slab: one strided copy
+            rows = self.mem.reshape(self.n, FRAME)[:n, HDR + HEADROOM:HDR + HEADROOM + ln]
+            rows[:] = slab[:n * frames.stride].reshape(n, frames.stride)[:, frames.data_off:frames.data_off + ln]
+            self.hdr["data_len"][:n] = lengths
+            return
         for i in range(n):
             o = int(offs[i])
             ln = int(min(lengths[i], max_bytes, max(0, slab.size - o)))

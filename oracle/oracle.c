@@ -1019,7 +1019,10 @@ static void *bench_worker(void *arg)
                 uint32_t m = cnt - k < 4 ? cnt - k : 4;
                 for (uint32_t q = 0; q < m; q++)
                     dip[q] = ptype[k + q] == 0x90u ? rd_be32(ptrs[k + q] + 30) : 0;
-                orc_dir24_8_lookup_bulk_pf(a->tbl24, a->tbl8, dip, m, dst);
+                if (a->mode == MODE_HASH) /* C2: parse + hash + queue only */
+                    memset(dst, 0, sizeof(dst));
+                else
+                    orc_dir24_8_lookup_bulk_pf(a->tbl24, a->tbl8, dip, m, dst);
                 for (uint32_t q = 0; q < m; q++) {
                     const uint8_t *ip = ptrs[k + q] + 14;
                     uint32_t h = 0;
@@ -1111,6 +1114,49 @@ double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iter
     for (int t = 0; t < nthreads; t++)
         pthread_join(th[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* The ip4_lookup node's CPU work over pktmbuf_t pointer arrays, one thread
+ * (ip4_lookup.c:48-256): per graph burst, mtod + 14 of every mbuf, dip /
+ * ttl / checksum into node_mbuf_priv1 (udata64, @56), 4-wide
+ * cne_fib_lookup_bulk with the default prefetching lookup, edge = val >> 16.
+ * pktmbuf_t offsets: buf_addr @8, data_off @24 (pktmbuf.h:102-204).
+ * Returns seconds for `iters` passes; writes udata64 like the node. */
+double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                            const uint32_t *tbl8, int iters)
+{
+    struct timespec t0, t1;
+    uint64_t sink = 0;
+    if (burst == 0)
+        burst = 256;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int it = 0; it < iters; it++) {
+        for (uint32_t b = 0; b < n; b += burst) {
+            const uint32_t cnt = n - b < burst ? n - b : burst;
+            for (uint32_t k = 0; k < cnt; k += 4) {
+                const uint32_t m = cnt - k < 4 ? cnt - k : 4;
+                uint32_t dip[4];
+                uint64_t dst[4];
+                uint8_t *mb[4];
+                const uint8_t *ip[4];
+                for (uint32_t q = 0; q < m; q++) {
+                    mb[q] = (uint8_t *)mbufs[b + k + q];
+                    const uint8_t *buf = *(uint8_t *const *)(mb[q] + 8);
+                    ip[q] = buf + *(const uint16_t *)(mb[q] + 24) + 14;
+                    dip[q] = rd_be32(ip[q] + 16);
+                }
+                orc_dir24_8_lookup_bulk_pf(tbl24, tbl8, dip, m, dst);
+                for (uint32_t q = 0; q < m; q++) {
+                    const uint64_t ck = (uint64_t)ip[q][10] | ((uint64_t)ip[q][11] << 8);
+                    *(uint64_t *)(mb[q] + 56) = (dst[q] & 0xffffu) | ((uint64_t)ip[q][8] << 16) | (ck << 32);
+                    sink += dst[q] >> 16;
+                }
+            }
+        }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    (void)sink;
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 

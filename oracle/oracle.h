@@ -128,6 +128,8 @@ int orc_classify(const struct orc_classify_args *a);
  * Multi-threaded over nthreads contiguous shards; returns elapsed seconds. */
 double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, int iters);
 double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iters, const int *cpus);
+double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                            const uint32_t *tbl8, int iters);
 void orc_dir24_8_lookup_bulk_pf(const uint32_t *tbl24, const uint32_t *tbl8, const uint32_t *ips, uint32_t n,
                                 uint64_t *nh);
 

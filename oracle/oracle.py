@@ -77,6 +77,8 @@ def lib():
         L.orc_burst_bench.restype = c_double
         L.orc_burst_bench.argtypes = [POINTER(ClassifyArgs), c_int, c_int, c_void_p]
         L.orc_dir24_8_lookup_bulk_pf.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
+        L.orc_ip4_lookup_mbufs.restype = c_double
+        L.orc_ip4_lookup_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_int]
         L.orc_ip4_rewrite.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32, c_void_p,
                                       c_uint32, c_void_p, c_void_p]
         L.orc_mac_swap.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]
@@ -236,6 +238,11 @@ def dir24_8_lookup_bulk_pf(t24, t8, ips) -> np.ndarray:
     out = np.zeros(len(ips), np.uint64)
     lib().orc_dir24_8_lookup_bulk_pf(_p(t24), _p(t8), _p(ips), len(ips), _p(out))
     return out
+
+
+def ip4_lookup_mbufs(ptrs, n, tables4, burst=256, iters=1) -> float:
+    """The ip4_lookup node's CPU loop over pktmbuf_t pointers (one thread): seconds."""
+    return lib().orc_ip4_lookup_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), iters)
 
 
 def l3fwd_burst_bench(slab, n, stride, tables4, nthreads=1, iters=1, **kw) -> float:

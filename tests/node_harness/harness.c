@@ -121,3 +121,75 @@ uint32_t harness_count(int k) { return n_out[k]; }
 uint64_t harness_enqueue_calls(void) { return enqueue_calls; }
 extern int node_mbuf_priv1_dynfield_offset;
 int harness_priv1_offset(void) { return node_mbuf_priv1_dynfield_offset; }
+
+/* ---- measurement drivers (bench.py's node-boundary leg) ------------------
+ * harness_drive: graph walks over the named node, as cne_graph_walk would
+ * run them on one lcore: per walk, the source nodes, then one burst of
+ * `burst` mbufs into `name`'s process(); after the last burst, walks until
+ * every mbuf has been enqueued.  `passes` times over objs[0..n).  Returns
+ * seconds (CLOCK_MONOTONIC), or -1 if mbufs went missing. */
+#include <time.h>
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, int passes)
+{
+    const int i = find(name);
+    if (i < 0 || burst == 0)
+        return -1.0;
+    const double t0 = now_s();
+    for (int p = 0; p < passes; p++) {
+        for (int k = 0; k < 3; k++)
+            n_out[k] = 0;
+        for (uint32_t b = 0; b < n; b += burst) {
+            harness_walk_sources();
+            const uint16_t c = (uint16_t)(n - b < burst ? n - b : burst);
+            regs[i]->process(&g, &nodes[i], objs + b, c);
+        }
+        for (long spin = 0; n_out[0] + n_out[1] + n_out[2] < n; spin++) {
+            if (spin > 100000000L)
+                return -1.0;
+            harness_walk_sources();
+        }
+    }
+    return now_s() - t0;
+}
+
+/* The asynchronous queue alone, driven by one thread the way a node does:
+ * submit a burst, poll what finished, wait when every slot is busy. */
+#include "cndp_gpu.h"
+double harness_mq_drive(cndp_gpu_mq_t *q, void **objs, uint32_t n, uint16_t burst, int passes)
+{
+    void *done[1024];
+    uint16_t edges[1024];
+    const double t0 = now_s();
+    for (int p = 0; p < passes; p++) {
+        uint32_t got = 0;
+        for (uint32_t b = 0; b < n;) {
+            const uint32_t c = n - b < burst ? n - b : burst;
+            const int k = cndp_gpu_mq_submit(q, objs + b, c);
+            if (k < 0)
+                return -1.0;
+            b += (uint32_t)k;
+            int r = cndp_gpu_mq_poll(q, done, edges, 1024);
+            if (r < 0)
+                return -1.0;
+            got += (uint32_t)r;
+            if (k == 0 && r == 0 && cndp_gpu_mq_wait(q) < 0)
+                return -1.0;
+        }
+        for (long spin = 0; got < n; spin++) {
+            if (spin > 100000000L)
+                return -1.0;
+            const int r = cndp_gpu_mq_poll(q, done, edges, 1024);
+            if (r < 0)
+                return -1.0;
+            got += (uint32_t)r;
+        }
+    }
+    return now_s() - t0;
+}
