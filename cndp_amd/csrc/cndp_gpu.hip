@@ -5353,12 +5353,23 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 
 // ---------------------------------------------------------------------------
 // Asynchronous node path over pktmbuf_t bursts (cndp_gpu_mq_*, cndp_gpu.h).
-// Bursts fill the open batch slot on the host (frame offsets, or staged frame
-// bytes); a full slot -- or, at poll time, a partly filled one when nothing
-// is in flight or it is older than max_delay_us -- is launched on the
-// queue's stream: H2D of the slot's offsets / staging, the kernels, one D2H
-// of compact per-packet records, an event.  poll checks the oldest slot's
-// event without waiting and writes the records back into the mbufs.
+//
+// Bursts fill the open batch slot on the host; a full slot -- or, at poll
+// time, a partly filled one when nothing is in flight or it has waited
+// max_delay_us -- is launched on the queue's stream.  Every host buffer a
+// slot uses is pinned and mapped, so the kernels read their inputs and write
+// their outputs in host memory directly: no DMA calls per batch.
+//   zero-copy (conf.umem): the host only copies the burst's mbuf pointers.
+//     The kernels read each mbuf's header (buf_addr, data_off, ...) and its
+//     frame in the registered region over PCIe, and write the fields the
+//     replaced nodes write straight into the mbuf.
+//   staged: the host gathers each frame's bytes (and header fields) into the
+//     slot's pinned staging; the kernels read that and return compact
+//     records, which poll writes into the mbufs.
+// The batch's last kernel ends with a completion flag: each block makes its
+// host writes visible system-wide (__threadfence_system), the last block to
+// arrive (device ticket) stores the batch sequence number into the slot's
+// pinned flag.  poll is a plain acquire load of that flag -- no HIP call.
 // ---------------------------------------------------------------------------
 #define MQ_FREE 0
 #define MQ_OPEN 1
@@ -5367,24 +5378,88 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 #define MQ_BURST 256u       // CNE_GRAPH_BURST_SIZE (cne_graph.h:30)
 #define MQ_WIN4 64u         // ip4_lookup staged bytes (it reads bytes 22..33)
 #define MQ_RUNS_MAX 512u    // cnet: runs of equal-size bursts per batch
+#define MQ_EDGE_NONE 0xFFFFu // zero-copy: an mbuf whose buffer is outside the region
+
+// pktmbuf_t fields (pktmbuf.h:102-204)
+#define MB_LPORT 26
+#define MB_DATA_LEN 30
+#define MB_TX_OFFLOAD 40
+#define MB_OL_FLAGS 48
+
+struct MqTables {
+    const uint32_t *t24, *t8, *d16, *pages, *t24_6, *t8_6;
+    uint32_t buf_len;
+};
+
+struct MqArgs {
+    uint32_t n;
+    uint32_t zc;            // zero-copy: mbuf pointers in, fields written into the mbufs
+    const uint64_t *ptrs;   // zc: host addresses of the mbufs (read in place)
+    int64_t delta;          // zc: device address - host address inside the region
+    const uint8_t *slab;    // frames: the region (zc) or the staging (device view)
+    uint64_t slab_len;
+    const uint64_t *off;    // frame offsets in slab (staged: host-filled; zc cnet: from k_mq_cnet_pre)
+    u32x2 *lens;            // cnet: {data_len | room << 16, buf_len | data_off << 16}
+    uint16_t *edges;        // out: next edge per mbuf (pinned host)
+    uint64_t *priv1;        // out (staged ip4_lookup): node_mbuf_priv1
+    u32x4 *rec;             // out (staged cnet): {ptype, rxmeta, data_len | edge << 16 | node << 24, hash}
+    // cnet classify outputs (device)
+    const uint32_t *ptype, *rxmeta, *hash;
+    const uint8_t *edge8;
+    uint32_t lport, want_hash;
+    MqTables tb;
+    uint32_t *ticket;       // device arrival counter of this slot
+    uint32_t *flag;         // device view of the slot's pinned completion flag
+    uint32_t seq;           // value the flag takes when the batch is done
+};
+
+// every block: its host writes visible, then the last block raises the flag
+__device__ __forceinline__ void mq_complete(const MqArgs &a)
+{
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = atomicAdd(a.ticket, 1u);
+        if (t == gridDim.x - 1) {
+            *a.ticket = 0u; // ready for the slot's next batch (stream order)
+            __threadfence_system();
+            __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// the mbuf header fields the nodes read, at the device view of host mbuf m
+__device__ __forceinline__ void mq_hdr(const MqArgs &a, uint64_t m, uint64_t &fo, uint32_t &doff, uint32_t &blen,
+                                       uint32_t &dlen, bool &ok)
+{
+    const uint8_t *dm = (const uint8_t *)(m + a.delta);
+    const uint64_t buf = *(const uint64_t *)(dm + MB_BUF_ADDR);
+    const uint64_t w = *(const uint64_t *)(dm + MB_DATA_OFF); // data_off, lport, buf_len, data_len
+    doff = (uint32_t)(w & 0xffffu);
+    blen = (uint32_t)((w >> 32) & 0xffffu);
+    dlen = (uint32_t)(w >> 48);
+    fo = (uint64_t)((int64_t)(buf + doff) + a.delta - (int64_t)(uintptr_t)a.slab);
+    ok = fo < a.slab_len;
+}
 
 // ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
 // mtod + 14 + 16, priv1 = {nh = val & 0xffff, ttl, hdr_checksum}, edge = val >> 16
-__global__ __launch_bounds__(256) void k_mq_ip4_lookup(const uint8_t *__restrict__ slab, uint64_t slab_len,
-                                                       const uint64_t *__restrict__ off, uint32_t n,
-                                                       const uint32_t *__restrict__ t24,
-                                                       const uint32_t *__restrict__ t8,
-                                                       const uint32_t *__restrict__ d16,
-                                                       const uint32_t *__restrict__ pages, uint64_t *priv1,
-                                                       uint16_t *edge)
+__global__ __launch_bounds__(256) void k_mq_ip4_lookup(MqArgs a)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint64_t base = off[i];
-        const uint8_t *p = slab + base;
-        const uint64_t avail = base < slab_len ? slab_len - base : 0;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+        uint64_t base;
+        bool ok = true;
+        if (a.zc) {
+            uint32_t doff, blen, dlen;
+            mq_hdr(a, a.ptrs[i], base, doff, blen, dlen, ok);
+        } else {
+            base = a.off[i];
+        }
+        const uint8_t *p = a.slab + base;
+        const uint64_t avail = ok && base < a.slab_len ? a.slab_len - base : 0;
         uint32_t ttl, ck, dip;
-        if (avail >= 36 && (base & 15u) == 0) { // two loads (one PCIe read each when zero-copy)
-            const u32x4 q = *(const u32x4 *)(p + 16); // bytes 16..31
+        if (avail >= 36 && (((uintptr_t)p) & 15u) == 0) { // two loads (one PCIe read each in place)
+            const u32x4 q = *(const u32x4 *)(p + 16);      // bytes 16..31
             const uint32_t w8 = *(const uint32_t *)(p + 32);
             ttl = (q.y >> 16) & 0xffu;
             ck = q.z & 0xffffu;
@@ -5395,30 +5470,43 @@ __global__ __launch_bounds__(256) void k_mq_ip4_lookup(const uint8_t *__restrict
             dip = (gbyte(p, avail, 30) << 24) | (gbyte(p, avail, 31) << 16) | (gbyte(p, avail, 32) << 8) |
                   gbyte(p, avail, 33);
         }
-        const uint32_t val = d16 ? lpm4d(d16, pages, t8, dip) : lpm4(t24, t8, dip);
-        priv1[i] = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
-        edge[i] = (uint16_t)(val >> 16);
+        const uint32_t val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
+        const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
+        if (a.zc) {
+            if (ok)
+                *(uint64_t *)(a.ptrs[i] + a.delta + MB_UDATA64) = priv1;
+            a.edges[i] = ok ? (uint16_t)(val >> 16) : (uint16_t)MQ_EDGE_NONE;
+        } else {
+            a.priv1[i] = priv1;
+            a.edges[i] = (uint16_t)(val >> 16);
+        }
+    }
+    mq_complete(a);
+}
+
+// zero-copy cnet: frame offsets and length fields from the mbuf headers
+__global__ __launch_bounds__(256) void k_mq_cnet_pre(MqArgs a, uint64_t *off)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+        uint64_t fo;
+        uint32_t doff, blen, dlen;
+        bool ok;
+        mq_hdr(a, a.ptrs[i], fo, doff, blen, dlen, ok);
+        off[i] = ok ? fo : a.slab_len; // outside the region: reads as zero bytes
+        u32x2 l;
+        l.x = dlen | ((blen > doff ? blen - doff : 0u) << 16);
+        l.y = blen | (doff << 16);
+        a.lens[i] = l;
     }
 }
 
-// cnet records: {packet_type, rxmeta, data_len | edge << 16 | node << 24, hash}.
-// Frames an input node took get data_len = total_length (ip4_input.c:121-124)
-// or payload_len (ip6_input.c:121-124), read at mtod after eth_rx's
-// pktmbuf_adj_offset(l2_len) (eth_rx.c:62, pktmbuf.h:955-984: skipped when
-// l2_len exceeds data_len or the buffer).  Which input node: ip4_input for
-// the low ptype bytes of its p_nxt entries (0x11, 0x31, 0x91), ip6_input for
-// 0x41, 0xc1, 0xe1 -- the ptype node's speculation only ever sends a frame
-// to the edge of a type with the same low byte (ptype.c:109-110).
-// A frame shorter than its L2 header (l2_len > data_len) keeps its data_off,
-// so the input node takes the bytes at the frame start for its IP header:
-// its length/checksum test and lookup are redone here from there
-// (ip4_input.c:121-150, ip6_input.c:121-150, trie.h:126-134).
-struct MqTables {
-    const uint32_t *t24, *t8, *d16, *pages, *t24_6, *t8_6;
-    uint32_t buf_len;
-};
-
-__device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t o, bool v6, const MqTables &t)
+// A frame an input node takes is re-evaluated here when the batch-wide
+// classify could not see its case: eth_rx's pktmbuf_adj_offset(l2_len) was
+// skipped (l2_len > data_len: the node then reads its IP header at the frame
+// start, pktmbuf.h:955-984) or its buf_len differs from the batch's (the
+// length test, ip4_input.c:121-140 / ip6_input.c:121-135).
+__device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t o, bool v6, const MqTables &t,
+                                uint32_t buf_len)
 {
     if (!v6) {
         const uint32_t x0 = gld32(slab, slab_len, o);
@@ -5430,11 +5518,11 @@ __device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t
         }
         sum = (sum >> 16) + (sum & 0xffffu);
         sum = (sum >> 16) + (sum & 0xffffu);
-        const bool ok = bswap16(x0 >> 16) < t.buf_len && ((~sum) & 0xffffu) == 0u;
+        const bool ok = bswap16(x0 >> 16) < buf_len && ((~sum) & 0xffffu) == 0u;
         const uint32_t dip = ok ? bswap32(gld32(slab, slab_len, o + 16)) : 0u;
         return t.d16 ? lpm4d(t.d16, t.pages, t.t8, dip) : lpm4(t.t24, t.t8, dip);
     }
-    const bool ok = ((gbyte(slab, slab_len, o + 4) << 8) | gbyte(slab, slab_len, o + 5)) < t.buf_len;
+    const bool ok = ((gbyte(slab, slab_len, o + 4) << 8) | gbyte(slab, slab_len, o + 5)) < buf_len;
     uint32_t e = t.t24_6[ok ? (gbyte(slab, slab_len, o + 24) << 16) | (gbyte(slab, slab_len, o + 25) << 8) |
                                   gbyte(slab, slab_len, o + 26)
                             : 0u];
@@ -5443,17 +5531,23 @@ __device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t
     return e >> 1;
 }
 
-__global__ __launch_bounds__(256) void k_mq_cnet_post(const uint8_t *__restrict__ slab, uint64_t slab_len,
-                                                      const uint64_t *__restrict__ off,
-                                                      const uint32_t *__restrict__ lens, uint32_t n,
-                                                      const uint32_t *__restrict__ ptype,
-                                                      const uint32_t *__restrict__ rxmeta,
-                                                      const uint8_t *__restrict__ edge,
-                                                      const uint32_t *__restrict__ hash, u32x4 *rec, MqTables tb)
+// cnet results per mbuf.  Frames an input node took get data_len =
+// total_length (ip4_input.c:121-124) or payload_len (ip6_input.c:121-124),
+// read at mtod after eth_rx's pktmbuf_adj_offset(l2_len) (eth_rx.c:62).
+// Which input node: ip4_input for the low ptype bytes of its p_nxt entries
+// (0x11, 0x31, 0x91), ip6_input for 0x41, 0xc1, 0xe1 -- the ptype node's
+// speculation only sends a frame to the edge of a type with the same low
+// byte (ptype.c:109-110).  Zero-copy: the eth_rx fields (eth_rx.c:35-63) and
+// data_len go straight into the mbuf; staged: into records for poll.
+__global__ __launch_bounds__(256) void k_mq_cnet_post(MqArgs a)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t pt = ptype[i], rm = rxmeta[i], e8 = edge[i];
-        uint32_t node, e, dlen = 0;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+        const uint32_t pt = a.ptype[i], rm = a.rxmeta[i], e8 = a.edge8[i];
+        const u32x2 ln = a.lens[i];
+        const uint32_t dl = ln.x & 0xffffu, room = ln.x >> 16, blen = ln.y & 0xffffu, doff = ln.y >> 16;
+        const uint32_t l2 = rm & 0x7fu;
+        const bool adj = l2 <= dl && l2 <= room;
+        uint32_t node, e, dlen = adj ? dl - l2 : dl;
         if (e8 & 0x80u) {
             node = CNDP_MQ_NODE_PTYPE;
             e = e8 & 0x7fu;
@@ -5462,33 +5556,56 @@ __global__ __launch_bounds__(256) void k_mq_cnet_post(const uint8_t *__restrict_
             const bool v6 = low == 0x41u || low == 0xc1u || low == 0xe1u;
             node = v6 ? CNDP_MQ_NODE_IP6 : CNDP_MQ_NODE_IP4;
             e = e8;
-            const uint32_t l2 = rm & 0x7fu, dl = lens[i] & 0xffffu, room = lens[i] >> 16;
-            const bool adj = l2 <= dl && l2 <= room;
-            const uint64_t o = off[i] + (adj ? l2 : 0u) + (v6 ? 4u : 2u);
-            dlen = (gbyte(slab, slab_len, o) << 8) | gbyte(slab, slab_len, o + 1);
-            if (!adj)
-                e = mq_input_at(slab, slab_len, off[i], v6, tb) >> 24;
+            const uint64_t o = a.off[i] + (adj ? l2 : 0u);
+            dlen = (gbyte(a.slab, a.slab_len, o + (v6 ? 4u : 2u)) << 8) | gbyte(a.slab, a.slab_len, o + (v6 ? 5u : 3u));
+            if (!adj || blen != a.tb.buf_len)
+                e = mq_input_at(a.slab, a.slab_len, o, v6, a.tb, blen) >> 24;
         }
-        u32x4 r;
-        r.x = pt;
-        r.y = rm;
-        r.z = dlen | (e << 16) | (node << 24);
-        r.w = hash ? hash[i] : 0u;
-        rec[i] = r;
+        const uint32_t h = a.want_hash ? a.hash[i] : 0u;
+        if (a.zc) {
+            const uint64_t m = a.ptrs[i] + a.delta;
+            if (a.off[i] < a.slab_len) {
+                // data_off, lport, buf_len, data_len in one 8-B store
+                *(uint64_t *)(m + MB_DATA_OFF) = (uint64_t)(adj ? doff + l2 : doff) |
+                                                 ((uint64_t)a.lport << 16) | ((uint64_t)blen << 32) |
+                                                 ((uint64_t)(dlen & 0xffffu) << 48);
+                *(uint32_t *)(m + MB_PTYPE) = pt;
+                u32x4 tol; // tx_offload = l2 | l3 << 7 | l4 << 16, ol_flags = MCAST/BCAST/IPv6 bits 61..63
+                tol.x = rm & 0xffffffu;
+                tol.y = 0u;
+                tol.z = 0u;
+                tol.w = (rm >> 29) << 29;
+                *(u32x4 *)(m + MB_TX_OFFLOAD) = tol;
+                if (a.want_hash)
+                    *(uint32_t *)(m + MB_HASH) = h;
+                a.edges[i] = (uint16_t)((node << 8) | e);
+            } else {
+                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
+            }
+        } else {
+            u32x4 r;
+            r.x = pt;
+            r.y = rm;
+            r.z = dlen | (e << 16) | (node << 24);
+            r.w = h;
+            a.rec[i] = r;
+            a.edges[i] = (uint16_t)((node << 8) | e);
+        }
     }
+    mq_complete(a);
 }
 
 struct MqSlot {
     int state;
-    uint32_t n, polled, buf_len;
+    uint32_t n, polled, buf_len, seq;
     uint64_t t_open_ns;    // when the first mbuf went in
     uint64_t stage_used;   // staged bytes
     uint32_t nrun;         // cnet: runs of equal-size bursts (each ends with at most one short burst)
     uint32_t run_B[MQ_RUNS_MAX], run_n[MQ_RUNS_MAX];
     uint8_t run_closed;
     void **mb;             // host
-    uint8_t *h;            // pinned: offsets | lens | staging | records
-    uint8_t *d;            // device: offsets | lens | staging | outputs | records
+    uint8_t *h, *hd;       // pinned + mapped block (host view, device view)
+    uint8_t *d;            // device block (cnet classify outputs, zero-copy offsets)
     hipEvent_t ev;
 };
 
@@ -5499,10 +5616,12 @@ struct cndp_gpu_mq {
     const uint8_t *r_host, *r_dev; // zero-copy region (NULL: staged)
     uint64_t r_len;
     uint32_t stage;                // staged bytes reserved per frame
-    // byte offsets inside each slot's host (H) and device (D) blocks
-    uint64_t h_off, h_len, h_stage, h_rec, h_bytes;
-    uint64_t d_off, d_len, d_stage, d_nh, d_edge, d_pt, d_rm, d_hash, d_rec, d_bytes;
-    uint32_t head, open, in_flight; // head: oldest slot not fully polled
+    uint32_t *flags, *flags_d;     // pinned completion flags (host / device view)
+    uint32_t *tickets;             // device, one per slot
+    // byte offsets inside each slot's pinned block (H) and device block (D)
+    uint64_t h_ptr, h_len, h_edge, h_rec, h_stage, h_bytes;
+    uint64_t d_off, d_len, d_nh, d_edge, d_pt, d_rm, d_hash, d_bytes;
+    uint32_t head, open, in_flight, seq; // head: oldest slot not fully polled
     uint32_t pending;
     MqSlot slot[CNDP_MQ_DEPTH_MAX];
 };
@@ -5557,29 +5676,36 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     }
     const uint64_t B = k.batch;
     const bool cnet = k.mode == CNDP_MQ_CNET;
-    q->stage = q->r_host ? 0u : cnet ? (uint32_t)al64(k.stage_max) : MQ_WIN4;
-    q->h_off = 0;
-    q->h_len = al64(B * 8);
-    q->h_stage = q->h_len + (cnet ? al64(B * 4) : 0);
-    q->h_rec = q->h_stage + B * q->stage;
-    q->h_bytes = q->h_rec + (cnet ? B * 16 : al64(B * 8) + B * 2);
-    q->d_off = 0;
+    const bool zc = q->r_host != nullptr;
+    q->stage = zc ? 0u : cnet ? (uint32_t)al64(k.stage_max) : MQ_WIN4;
+    q->h_ptr = 0;                                       // zc: mbuf pointers; staged: frame offsets
+    q->h_len = al64(B * 8);                             // staged cnet: length fields
+    q->h_edge = q->h_len + (cnet && !zc ? al64(B * 8) : 0);
+    q->h_rec = q->h_edge + al64(B * 2);                 // staged: records
+    q->h_stage = q->h_rec + (zc ? 0 : al64(B * (cnet ? 16 : 8)));
+    q->h_bytes = q->h_stage + B * q->stage;
+    q->d_off = 0;                                       // zc cnet: offsets / lengths from the headers
     q->d_len = al64(B * 8);
-    q->d_stage = q->d_len + (cnet ? al64(B * 4) : 0);
-    q->d_nh = q->d_stage + B * q->stage;
+    q->d_nh = q->d_len + al64(B * 8);
     q->d_edge = q->d_nh + al64(B * 4);
-    q->d_pt = q->d_edge + al64(B * 2);
+    q->d_pt = q->d_edge + al64(B);
     q->d_rm = q->d_pt + al64(B * 4);
     q->d_hash = q->d_rm + al64(B * 4);
-    q->d_rec = q->d_hash + al64(B * 4);
-    q->d_bytes = q->d_rec + (cnet ? B * 16 : al64(B * 8) + B * 2);
+    q->d_bytes = cnet ? q->d_hash + al64(B * 4) : 64;
     r = -ENOMEM;
     if (hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) != hipSuccess)
         goto fail;
+    if (hipHostMalloc((void **)&q->flags, CNDP_MQ_DEPTH_MAX * 64, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&q->flags_d, q->flags, 0) != hipSuccess ||
+        hipMalloc((void **)&q->tickets, CNDP_MQ_DEPTH_MAX * 4) != hipSuccess ||
+        hipMemset(q->tickets, 0, CNDP_MQ_DEPTH_MAX * 4) != hipSuccess)
+        goto fail;
+    memset(q->flags, 0, CNDP_MQ_DEPTH_MAX * 64);
     for (uint32_t j = 0; j < k.depth; j++) {
         MqSlot *sl = &q->slot[j];
         sl->mb = (void **)malloc(B * sizeof(void *));
-        if (!sl->mb || hipHostMalloc((void **)&sl->h, q->h_bytes, 0) != hipSuccess ||
+        if (!sl->mb || hipHostMalloc((void **)&sl->h, q->h_bytes, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&sl->hd, sl->h, 0) != hipSuccess ||
             hipMalloc((void **)&sl->d, q->d_bytes) != hipSuccess ||
             hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess)
             goto fail;
@@ -5608,6 +5734,10 @@ extern "C" void cndp_gpu_mq_free(cndp_gpu_mq_t *q)
         if (sl->ev)
             hipEventDestroy(sl->ev);
     }
+    if (q->flags)
+        hipHostFree(q->flags);
+    if (q->tickets)
+        hipFree(q->tickets);
     if (q->s)
         hipStreamDestroy(q->s);
     free(q);
@@ -5636,22 +5766,25 @@ static MqTables mq_tables(cndp_gpu_ctx_t *c, uint32_t buf_len)
 {
     MqTables t;
     memset(&t, 0, sizeof(t));
-    struct cndp_tbl *t4 = &c->fib4->t, *t6 = &c->fib6->t;
+    struct cndp_tbl *t4 = &c->fib4->t;
     t.t24 = (const uint32_t *)t4->dev_tbl24;
     t.t8 = (const uint32_t *)t4->dev_tbl8;
     if (c->tune_dir16 && t4->dev_dir16 && t4->dev_pages) {
         t.d16 = (const uint32_t *)t4->dev_dir16;
         t.pages = (const uint32_t *)t4->dev_pages;
     }
-    t.t24_6 = (const uint32_t *)t6->dev_tbl24;
-    t.t8_6 = (const uint32_t *)t6->dev_tbl8;
+    if (c->fib6) {
+        t.t24_6 = (const uint32_t *)c->fib6->t.dev_tbl24;
+        t.t8_6 = (const uint32_t *)c->fib6->t.dev_tbl8;
+    }
     t.buf_len = buf_len;
     return t;
 }
 
 static int mq_launch(cndp_gpu_mq_t *q)
 {
-    MqSlot *sl = &q->slot[q->open];
+    const uint32_t slot_i = q->open;
+    MqSlot *sl = &q->slot[slot_i];
     if (sl->state != MQ_OPEN || sl->n == 0)
         return 0;
     cndp_gpu_ctx_t *c = q->c;
@@ -5660,33 +5793,39 @@ static int mq_launch(cndp_gpu_mq_t *q)
         return r;
     hipStream_t s = q->s;
     const uint32_t n = sl->n;
-    const bool cnet = q->conf.mode == CNDP_MQ_CNET;
-    uint8_t *H = sl->h, *D = sl->d;
-    HIP_TRY(hipMemcpyAsync(D + q->d_off, H + q->h_off, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    if (cnet)
-        HIP_TRY(hipMemcpyAsync(D + q->d_len, H + q->h_len, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    if (sl->stage_used)
-        HIP_TRY(hipMemcpyAsync(D + q->d_stage, H + q->h_stage, sl->stage_used, hipMemcpyHostToDevice, s));
-    const uint8_t *slab = q->r_host ? q->r_dev : D + q->d_stage;
-    const uint64_t slab_len = q->r_host ? q->r_len : (sl->stage_used ? sl->stage_used : 64);
-    const uint64_t *off = (const uint64_t *)(D + q->d_off);
+    const bool cnet = q->conf.mode == CNDP_MQ_CNET, zc = q->r_host != nullptr;
+    uint8_t *HD = sl->hd, *D = sl->d;
+    MqArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.zc = zc;
+    a.ptrs = (const uint64_t *)(HD + q->h_ptr);
+    a.delta = zc ? (int64_t)((intptr_t)q->r_dev - (intptr_t)q->r_host) : 0;
+    a.slab = zc ? q->r_dev : HD + q->h_stage;
+    a.slab_len = zc ? q->r_len : (sl->stage_used ? sl->stage_used : 64);
+    a.off = zc ? (const uint64_t *)(D + q->d_off) : (const uint64_t *)(HD + q->h_ptr);
+    a.lens = zc ? (u32x2 *)(D + q->d_len) : (u32x2 *)(HD + q->h_len);
+    a.edges = (uint16_t *)(HD + q->h_edge);
+    a.priv1 = (uint64_t *)(HD + q->h_rec);
+    a.rec = (u32x4 *)(HD + q->h_rec);
+    a.lport = q->conf.lport;
+    a.want_hash = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
+    a.ticket = q->tickets + slot_i;
+    a.flag = q->flags_d + slot_i * 16u;
+    sl->seq = ++q->seq;
+    a.seq = sl->seq;
     const uint32_t g = blocks_for(n, 256);
     if (!cnet) {
-        struct cndp_tbl *t = &c->fib4->t;
-        if ((r = cndp_tbl_dev_sync(t, s)))
+        if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
-        const bool d16 = c->tune_dir16 && t->dev_dir16 && t->dev_pages;
-        hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(256), 0, s, slab, slab_len, off, n,
-                           (const uint32_t *)t->dev_tbl24, (const uint32_t *)t->dev_tbl8,
-                           d16 ? (const uint32_t *)t->dev_dir16 : nullptr,
-                           d16 ? (const uint32_t *)t->dev_pages : nullptr, (uint64_t *)(D + q->d_rec),
-                           (uint16_t *)(D + q->d_rec + al64((uint64_t)q->conf.batch * 8)));
+        a.tb = mq_tables(c, 0);
+        hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(256), 0, s, a);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(H + q->h_rec, D + q->d_rec, (size_t)n * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(H + q->h_rec + al64((uint64_t)q->conf.batch * 8),
-                               D + q->d_rec + al64((uint64_t)q->conf.batch * 8), (size_t)n * 2,
-                               hipMemcpyDeviceToHost, s));
     } else {
+        if (zc) {
+            hipLaunchKernelGGL(k_mq_cnet_pre, dim3(g), dim3(256), 0, s, a, (uint64_t *)(D + q->d_off));
+            HIP_TRY(hipGetLastError());
+        }
         // one classify per run of equal-size graph bursts, the ptype node's
         // speculation run with that burst size, its state carried in the
         // context from run to run and batch to batch
@@ -5697,15 +5836,15 @@ static int mq_launch(cndp_gpu_mq_t *q)
             memset(&b, 0, sizeof(b));
             b.mode = CNDP_MODE_CNET;
             b.n = sl->run_n[k];
-            b.slab = slab;
-            b.slab_len = slab_len;
-            b.offsets = off + i0;
+            b.slab = a.slab;
+            b.slab_len = a.slab_len;
+            b.offsets = a.off + i0;
             b.buf_len = sl->buf_len;
             b.nh = (uint32_t *)(D + q->d_nh) + i0;
             b.edge = D + q->d_edge + i0;
             b.ptype = (uint32_t *)(D + q->d_pt) + i0;
             b.rxmeta = (uint32_t *)(D + q->d_rm) + i0;
-            b.hash = (q->conf.flags & CNDP_MQ_F_HASH) ? (uint32_t *)(D + q->d_hash) + i0 : nullptr;
+            b.hash = a.want_hash ? (uint32_t *)(D + q->d_hash) + i0 : nullptr;
             c->spec_burst = saved_B ? sl->run_B[k] : 0u;
             r = cndp_gpu_classify(c, &b, s);
             i0 += sl->run_n[k];
@@ -5713,13 +5852,13 @@ static int mq_launch(cndp_gpu_mq_t *q)
         c->spec_burst = saved_B;
         if (r)
             return r;
-        hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(256), 0, s, slab, slab_len, off,
-                           (const uint32_t *)(D + q->d_len), n, (const uint32_t *)(D + q->d_pt),
-                           (const uint32_t *)(D + q->d_rm), (const uint8_t *)(D + q->d_edge),
-                           (q->conf.flags & CNDP_MQ_F_HASH) ? (const uint32_t *)(D + q->d_hash) : nullptr,
-                           (u32x4 *)(D + q->d_rec), mq_tables(c, sl->buf_len));
+        a.ptype = (const uint32_t *)(D + q->d_pt);
+        a.rxmeta = (const uint32_t *)(D + q->d_rm);
+        a.hash = (const uint32_t *)(D + q->d_hash);
+        a.edge8 = D + q->d_edge;
+        a.tb = mq_tables(c, sl->buf_len);
+        hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(256), 0, s, a);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(H + q->h_rec, D + q->d_rec, (size_t)n * 16, hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipEventRecord(sl->ev, s));
     sl->state = MQ_FLIGHT;
@@ -5735,23 +5874,15 @@ extern "C" int cndp_gpu_mq_flush(cndp_gpu_mq_t *q)
     return mq_launch(q);
 }
 
-// pktmbuf_t fields (pktmbuf.h:102-204)
-#define MB_LPORT 26
-#define MB_DATA_LEN 30
-#define MB_TX_OFFLOAD 40
-#define MB_OL_FLAGS 48
-
 extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t n)
 {
     if (!q || (n && !mbufs))
         return -EINVAL;
-    const bool cnet = q->conf.mode == CNDP_MQ_CNET;
-    if (q->r_host) // zero-copy: every buffer must lie in the registered region
+    const bool cnet = q->conf.mode == CNDP_MQ_CNET, zc = q->r_host != nullptr;
+    if (zc) // zero-copy: the mbufs themselves must lie in the registered region
         for (uint32_t i = 0; i < n; i++) {
             const uint8_t *m = (const uint8_t *)mbufs[i];
-            const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
-            const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
-            if (buf + doff < q->r_host || buf + doff >= q->r_host + q->r_len)
+            if (m < q->r_host || m + 64 > q->r_host + q->r_len)
                 return -EINVAL;
         }
     uint32_t done = 0;
@@ -5762,43 +5893,47 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
         // one graph burst (<= 256 mbufs) at a time, never split across batches
         const uint32_t k = n - done < MQ_BURST ? n - done : MQ_BURST;
         bool full = sl->n + k > q->conf.batch;
-        if (cnet && !full) {
-            const uint16_t bl = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
-            for (uint32_t i = 0; i < k && !full; i++) // one buf_len per batch (the input nodes' length check)
-                full = *(const uint16_t *)((const uint8_t *)mbufs[done + i] + MB_BUF_LEN) != (sl->n ? sl->buf_len : bl);
-            if (!full && sl->nrun == MQ_RUNS_MAX && !(sl->run_closed == 0 && k <= sl->run_B[sl->nrun - 1]))
-                full = true;
-        }
+        if (cnet && !full && sl->nrun == MQ_RUNS_MAX && !(sl->run_closed == 0 && k <= sl->run_B[sl->nrun - 1]))
+            full = true;
         if (full) {
-            if (sl->n == 0)
-                return -EINVAL; // a single burst with mixed buf_len
             int r = mq_launch(q);
             if (r)
                 return r;
             continue;
         }
-        if (sl->n == 0)
+        if (sl->n == 0) {
             sl->t_open_ns = now_ns();
-        uint64_t *ho = (uint64_t *)(sl->h + q->h_off);
-        uint32_t *hl = (uint32_t *)(sl->h + q->h_len);
-        for (uint32_t i = 0; i < k; i++) {
-            uint8_t *m = (uint8_t *)mbufs[done + i];
-            const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
-            const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
-            const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
-            const uint16_t dlen = *(const uint16_t *)(m + MB_DATA_LEN);
-            const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
-            const uint32_t j = sl->n + i;
-            sl->mb[j] = m;
+            // the batch's buf_len for the input nodes' length test; frames with
+            // another one are re-evaluated by k_mq_cnet_post
             if (cnet)
-                hl[j] = (uint32_t)dlen | (room << 16);
-            if (q->r_host) {
-                ho[j] = (uint64_t)(buf + doff - q->r_host);
-            } else {
+                sl->buf_len = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
+        }
+        uint8_t *H = sl->h;
+        if (zc) {
+            memcpy(H + q->h_ptr + (size_t)sl->n * 8, mbufs + done, (size_t)k * 8);
+            memcpy(sl->mb + sl->n, mbufs + done, (size_t)k * sizeof(void *));
+        } else {
+            uint64_t *ho = (uint64_t *)(H + q->h_ptr);
+            u32x2 *hl = (u32x2 *)(H + q->h_len);
+            for (uint32_t i = 0; i < k; i++) {
+                uint8_t *m = (uint8_t *)mbufs[done + i];
+                const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
+                const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
+                const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+                const uint16_t dlen = *(const uint16_t *)(m + MB_DATA_LEN);
+                const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
+                const uint32_t j = sl->n + i;
+                sl->mb[j] = m;
+                if (cnet) {
+                    u32x2 l;
+                    l.x = (uint32_t)dlen | (room << 16);
+                    l.y = (uint32_t)blen | ((uint32_t)doff << 16);
+                    hl[j] = l;
+                }
                 // staged copy of the bytes the nodes can read (bounded by the buffer)
                 const uint32_t want = cnet ? (room < q->conf.stage_max ? room : q->conf.stage_max) : MQ_WIN4;
                 const uint32_t cp = room < want ? room : want;
-                uint8_t *dst = sl->h + q->h_stage + sl->stage_used;
+                uint8_t *dst = H + q->h_stage + sl->stage_used;
                 memcpy(dst, buf + doff, cp);
                 const uint64_t span = al64(want ? want : 1);
                 memset(dst + cp, 0, span - cp);
@@ -5818,7 +5953,6 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
                 sl->nrun++;
                 sl->run_closed = 0;
             }
-            sl->buf_len = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
         }
         sl->n += k;
         done += k;
@@ -5832,19 +5966,14 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
     return (int)done;
 }
 
-// write one finished slot's records back into its mbufs
-static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1, void **out, uint16_t *edges)
+// staged: write one finished slot's records back into its mbufs
+static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
 {
     const uint8_t *R = sl->h + q->h_rec;
     if (q->conf.mode == CNDP_MQ_IP4_LOOKUP) {
         const uint64_t *priv1 = (const uint64_t *)R;
-        const uint16_t *e = (const uint16_t *)(R + al64((uint64_t)q->conf.batch * 8));
-        for (uint32_t i = i0; i < i1; i++) {
-            uint8_t *m = (uint8_t *)sl->mb[i];
-            *(uint64_t *)(m + MB_UDATA64) = priv1[i]; // node_mbuf_priv1 (ip4_lookup.c:144-154)
-            out[i - i0] = m;
-            edges[i - i0] = e[i];
-        }
+        for (uint32_t i = i0; i < i1; i++) // node_mbuf_priv1 (ip4_lookup.c:144-154)
+            *(uint64_t *)((uint8_t *)sl->mb[i] + MB_UDATA64) = priv1[i];
         return;
     }
     const uint32_t *rec = (const uint32_t *)R;
@@ -5859,21 +5988,15 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1,
         *(uint64_t *)(m + MB_TX_OFFLOAD) = (uint64_t)(rm & 0xffffffu);
         *(uint16_t *)(m + MB_LPORT) = lport;
         const uint16_t l2 = (uint16_t)(rm & 0x7fu);
-        uint16_t doff = *(uint16_t *)(m + MB_DATA_OFF), dlen = *(uint16_t *)(m + MB_DATA_LEN);
+        uint16_t doff = *(uint16_t *)(m + MB_DATA_OFF);
+        const uint16_t dlen0 = *(uint16_t *)(m + MB_DATA_LEN);
         const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
-        if (l2 <= dlen && (uint32_t)l2 + doff <= blen) { // pktmbuf_adj_offset
+        if (l2 <= dlen0 && (uint32_t)l2 + doff <= blen) // pktmbuf_adj_offset
             doff = (uint16_t)(doff + l2);
-            dlen = (uint16_t)(dlen - l2);
-        }
-        const uint32_t node = w2 >> 24;
-        if (node != CNDP_MQ_NODE_PTYPE) // ip4_input / ip6_input: data_len from the IP header
-            dlen = (uint16_t)(w2 & 0xffffu);
         *(uint16_t *)(m + MB_DATA_OFF) = doff;
-        *(uint16_t *)(m + MB_DATA_LEN) = dlen;
+        *(uint16_t *)(m + MB_DATA_LEN) = (uint16_t)(w2 & 0xffffu); // adjusted, or the IP header's
         if (wh)
             *(uint32_t *)(m + MB_HASH) = rec[4 * i + 3];
-        out[i - i0] = m;
-        edges[i - i0] = (uint16_t)(w2 >> 16);
     }
 }
 
@@ -5892,20 +6015,21 @@ extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges,
     }
     uint32_t got = 0;
     while (got < max) {
-        MqSlot *sl = &q->slot[q->head];
+        const uint32_t hi = q->head;
+        MqSlot *sl = &q->slot[hi];
         if (sl->state == MQ_FLIGHT) {
-            const hipError_t e = hipEventQuery(sl->ev);
-            if (e == hipErrorNotReady)
+            if (__atomic_load_n(&q->flags[hi * 16u], __ATOMIC_ACQUIRE) != sl->seq)
                 break;
-            if (e != hipSuccess)
-                return -EIO;
             sl->state = MQ_DONE;
             q->in_flight--;
         }
         if (sl->state != MQ_DONE)
             break;
         const uint32_t take = sl->n - sl->polled < max - got ? sl->n - sl->polled : max - got;
-        mq_writeback(q, sl, sl->polled, sl->polled + take, mbufs + got, edges + got);
+        if (q->r_host == nullptr)
+            mq_writeback(q, sl, sl->polled, sl->polled + take);
+        memcpy(mbufs + got, sl->mb + sl->polled, (size_t)take * sizeof(void *));
+        memcpy(edges + got, (const uint16_t *)(sl->h + q->h_edge) + sl->polled, (size_t)take * 2);
         sl->polled += take;
         got += take;
         q->pending -= take;

@@ -142,11 +142,16 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  *
  * Frame bytes: when conf.umem names a region registered with
  * cndp_gpu_host_register (the AF_XDP UMEM / pktmbuf pool, cne_lport.h:91),
- * the kernels read each frame where it lies (zero-copy: only the 8-B frame
- * offsets cross PCIe); every mbuf's buffer must lie in that region.  With
- * conf.umem NULL, the host copies each frame into pinned staging (ip4_lookup:
- * 64 B, enough for every byte the node reads; cnet: the buffer from data_off
- * to buf_len, at most conf.stage_max bytes).
+ * the mbufs and their buffers must lie in it, and the host does no per-mbuf
+ * work at all: the kernels read each mbuf header and frame where they lie and
+ * write the results straight into the mbuf (zero-copy; submit refuses mbufs
+ * outside the region with -EINVAL; an mbuf whose buffer points outside it
+ * comes back untouched with edge CNDP_MQ_EDGE_NONE).  With conf.umem NULL,
+ * the host copies each frame into pinned staging (ip4_lookup: 64 B, enough for
+ * every byte the node reads; cnet: the buffer from data_off to buf_len, at
+ * most conf.stage_max bytes) and poll writes the results back.
+ * Completion is a flag the batch's last kernel raises in pinned memory, so
+ * poll costs a load, not a HIP call.
  *
  * Modes and what is written back (pktmbuf_t layout, pktmbuf.h:102-204):
  *   CNDP_MQ_IP4_LOOKUP  the ip4_lookup node (ip4_lookup.c:48-256): udata64 =
@@ -179,6 +184,7 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
 #define CNDP_MQ_NODE_IP4 1u
 #define CNDP_MQ_NODE_IP6 2u
 #define CNDP_MQ_EDGE(node, e) ((uint16_t)(((node) << 8) | (e)))
+#define CNDP_MQ_EDGE_NONE 0xFFFFu
 #define CNDP_MQ_DEPTH_MAX 16u
 
 struct cndp_mq_conf {
