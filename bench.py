@@ -235,6 +235,9 @@ def cpu_baseline(state, budget_s: float = 10.0):
         slab = np.concatenate([fr.slab[: n * fr.stride].cpu().numpy(), np.zeros(2048, np.uint8)])
         kw.update(stride=fr.stride, data_off=fr.data_off)
     cpus, model, quota = host_cpus()
+    aff = len(cpus)
+    if quota:  # a CPU quota below the affinity set: one pinned thread per CPU of the quota
+        cpus = cpus[:max(1, int(-(-quota // 1)))]
     t1 = O.burst_bench(mode, slab, n, nthreads=1, iters=1, cpus=cpus[:1], **kw)
     single = n / t1 / 1e6
     tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=1, cpus=cpus, **kw)
@@ -247,7 +250,8 @@ def cpu_baseline(state, budget_s: float = 10.0):
              "cne_fib_lookup_bulk with dir24_8.h's prefetching lookup" +
              (", skipped in C2" if mode == N.CNDP_MODE_HASH else "") + ", cne_softrss restatement, RETA)")
     return {"value": round(multi, 2), "unit": "Mpps", "cores": len(cpus), "kind": "port",
-            "cpu_model": model, "cgroup_cpu_quota": quota, "single_core_Mpps": round(single, 2),
+            "cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "single_core_Mpps": round(single, 2),
             "sample": (f"oracle/oracle.c {chain} over {n} of the same frames x {iters} passes on "
                        f"{len(cpus)} pinned threads ({tt:.1f} s); 1 thread: {single:.2f} Mpps")}
 
