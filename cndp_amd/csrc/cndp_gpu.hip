@@ -5484,6 +5484,43 @@ __global__ __launch_bounds__(256) void k_mq_ip4_lookup(MqArgs a)
     mq_complete(a);
 }
 
+// cndpfwd _loopback_test (examples/cndpfwd/main.c:317-339): MAC_SWAP =
+// swap_mac_addresses (main.h:303-315) at pktmbuf_mtod of every mbuf, then tx.
+// Zero-copy: in the frame where it lies; staged: in the staged window, which
+// poll copies back.  Every mbuf leaves by edge 0 (tx).
+__global__ __launch_bounds__(256) void k_mq_mac_swap(MqArgs a)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+        uint64_t base;
+        bool ok = true;
+        if (a.zc) {
+            uint32_t doff, blen, dlen;
+            mq_hdr(a, a.ptrs[i], base, doff, blen, dlen, ok);
+        } else {
+            base = a.off[i];
+        }
+        ok = ok && base + 12 <= a.slab_len;
+        if (ok) {
+            uint8_t *p = (uint8_t *)a.slab + base;
+            if ((((uintptr_t)p) & 3u) == 0) {
+                uint32_t *d = (uint32_t *)p;
+                const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+                d[0] = alignb(d2, d1, 2);       // bytes 6..9
+                d[1] = (d2 >> 16) | (d0 << 16); // bytes 10, 11, 0, 1
+                d[2] = alignb(d1, d0, 2);       // bytes 2..5
+            } else {
+                for (int k = 0; k < 6; k++) {
+                    const uint8_t t = p[k];
+                    p[k] = p[6 + k];
+                    p[6 + k] = t;
+                }
+            }
+        }
+        a.edges[i] = ok || !a.zc ? (uint16_t)0 : (uint16_t)MQ_EDGE_NONE;
+    }
+    mq_complete(a);
+}
+
 // zero-copy cnet: frame offsets and length fields from the mbuf headers
 __global__ __launch_bounds__(256) void k_mq_cnet_pre(MqArgs a, uint64_t *off)
 {
@@ -5641,7 +5678,7 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
         return -EINVAL;
     *out = nullptr;
     struct cndp_mq_conf k = *conf;
-    if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET)
+    if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP)
         return -EINVAL;
     if (k.flags & ~CNDP_MQ_F_HASH)
         return -EINVAL;
@@ -5652,7 +5689,7 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.batch < MQ_BURST || k.batch > (1u << 24) || k.depth < 2 || k.depth > CNDP_MQ_DEPTH_MAX ||
         k.stage_max < 64 || k.stage_max > 65535)
         return -EINVAL;
-    if (k.mode == CNDP_MQ_IP4_LOOKUP ? !c->fib4 : (!c->fib4 || !c->fib6))
+    if (k.mode == CNDP_MQ_IP4_LOOKUP ? !c->fib4 : k.mode == CNDP_MQ_CNET ? (!c->fib4 || !c->fib6) : false)
         return -EINVAL;
     int r = set_device(c->dev);
     if (r)
@@ -5815,7 +5852,10 @@ static int mq_launch(cndp_gpu_mq_t *q)
     sl->seq = ++q->seq;
     a.seq = sl->seq;
     const uint32_t g = blocks_for(n, 256);
-    if (!cnet) {
+    if (q->conf.mode == CNDP_MQ_MAC_SWAP) {
+        hipLaunchKernelGGL(k_mq_mac_swap, dim3(g), dim3(256), 0, s, a);
+        HIP_TRY(hipGetLastError());
+    } else if (!cnet) {
         if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
         a.tb = mq_tables(c, 0);
@@ -5970,6 +6010,18 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
 static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
 {
     const uint8_t *R = sl->h + q->h_rec;
+    if (q->conf.mode == CNDP_MQ_MAC_SWAP) { // the swapped addresses back into the frame
+        const uint64_t *ho = (const uint64_t *)(sl->h + q->h_ptr);
+        for (uint32_t i = i0; i < i1; i++) {
+            uint8_t *m = (uint8_t *)sl->mb[i];
+            uint8_t *buf = *(uint8_t **)(m + MB_BUF_ADDR);
+            const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
+            const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+            const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
+            memcpy(buf + doff, sl->h + q->h_stage + ho[i], room < 12 ? room : 12);
+        }
+        return;
+    }
     if (q->conf.mode == CNDP_MQ_IP4_LOOKUP) {
         const uint64_t *priv1 = (const uint64_t *)R;
         for (uint32_t i = i0; i < i1; i++) // node_mbuf_priv1 (ip4_lookup.c:144-154)

@@ -41,7 +41,7 @@ CNDP_TUNE_CNET_SPEC = 9
 CNDP_TUNE_LOAD_NT = 10
 CNDP_TUNE_SPEC_SCAN = 11
 CNDP_TUNE_MBUF_HASH = 12
-CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET = 0, 1
+CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP = 0, 1, 2
 CNDP_MQ_F_HASH = 1
 CNDP_MQ_NODE_PTYPE, CNDP_MQ_NODE_IP4, CNDP_MQ_NODE_IP6 = 0, 1, 2
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF

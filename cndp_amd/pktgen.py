@@ -335,3 +335,39 @@ def fuzz_frames(n: int, seed: int = 1, slot: int = 128, device="cpu") -> Frames:
         raw[okm] = rows
     slab = raw.reshape(-1)[: n * slot - 37].contiguous()  # ragged tail
     return Frames(slab.to(device), n, stride=slot)
+
+
+def cndpfwd_udp(n: int, pkt_len: int = 60, src_mac: bytes = bytes.fromhex("020000000001")) -> Frames:
+    """C1: the frame examples/cndpfwd builds (setup_pkt_udp_ip_headers,
+    main.c:53-97): dst MAC ff:ff:ff:ff:ff:ff, the port's MAC as source (a
+    synthetic locally administered one here), IPv4 IHL 5, TTL 64, UDP,
+    198.18.0.1 -> 198.18.0.2, ports 9 -> 9, IPv4 and UDP checksums set,
+    pkt_len bytes (60: a 64-B frame with its FCS).  Packed 64-B slots."""
+    import struct
+    f = bytearray(64)
+    f[0:6] = b"\xff" * 6
+    f[6:12] = src_mac
+    f[12:14] = b"\x08\x00"
+    ip_len = pkt_len - 14
+    ip = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0, ip_len, 0, 0, 64, 17, 0,
+                               bytes([198, 18, 0, 1]), bytes([198, 18, 0, 2])))
+    s = sum(struct.unpack(">10H", bytes(ip)))
+    s = (s >> 16) + (s & 0xFFFF)
+    s = (s >> 16) + (s & 0xFFFF)
+    ip[10:12] = struct.pack(">H", (~s) & 0xFFFF)
+    udp_len = pkt_len - 14 - 20
+    udp = bytearray(struct.pack(">HHHH", 9, 9, udp_len, 0)) + bytes(udp_len - 8)
+    # cne_ipv4_udptcp_cksum (cne_ip.h:311-325): pseudo header + UDP, 0 -> 0xffff
+    ph = bytes([198, 18, 0, 1, 198, 18, 0, 2, 0, 17]) + struct.pack(">H", udp_len)
+    data = ph + bytes(udp)
+    if len(data) & 1:
+        data += b"\x00"
+    c = sum(struct.unpack(f">{len(data) // 2}H", data))
+    while c >> 16:
+        c = (c >> 16) + (c & 0xFFFF)
+    c = (~c) & 0xFFFF
+    udp[6:8] = struct.pack(">H", c or 0xFFFF)
+    f[14:34] = ip
+    f[34:34 + len(udp)] = udp[: 64 - 34]
+    slab = torch.tensor(list(bytes(f)) * n, dtype=torch.uint8)
+    return Frames(slab, n, stride=64, lengths=torch.full((n,), pkt_len, dtype=torch.int64))

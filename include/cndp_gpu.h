@@ -172,6 +172,10 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  *                       the input node's edge (drop 0, forward 1, proto 2).
  *                       Each submit call is one graph burst (<= 256 mbufs;
  *                       larger calls are cut into 256s).
+ *   CNDP_MQ_MAC_SWAP    cndpfwd's loopback mode (examples/cndpfwd/main.c:317-339):
+ *                       destination and source MAC swapped in the frame
+ *                       (swap_mac_addresses, main.h:303-315); edge 0 (tx).
+ *                       Needs no FIB.
  *   flag CNDP_MQ_F_HASH also store the Toeplitz flow hash in m->hash (no
  *                       reference node writes it, so it is off by default).
  */
@@ -179,6 +183,7 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
 
 #define CNDP_MQ_IP4_LOOKUP 0u
 #define CNDP_MQ_CNET 1u
+#define CNDP_MQ_MAC_SWAP 2u
 #define CNDP_MQ_F_HASH (1u << 0)
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u

@@ -193,3 +193,41 @@ double harness_mq_drive(cndp_gpu_mq_t *q, void **objs, uint32_t n, uint16_t burs
     }
     return now_s() - t0;
 }
+
+/* Latency of one request of n mbufs through the queue, as cndpfwd's
+ * loopback takes it: bursts of `burst` submitted back to back, then polled
+ * until all n are back; us[r] = microseconds of repetition r. */
+int harness_mq_latency(cndp_gpu_mq_t *q, void **objs, uint32_t n, uint16_t burst, int reps, double *us)
+{
+    void *done[1024];
+    uint16_t edges[1024];
+    for (int r = 0; r < reps; r++) {
+        const double t0 = now_s();
+        uint32_t got = 0;
+        for (uint32_t b = 0; b < n;) {
+            const uint32_t c = n - b < burst ? n - b : burst;
+            const int k = cndp_gpu_mq_submit(q, objs + b, c);
+            if (k < 0)
+                return -1;
+            b += (uint32_t)k;
+            if (k == 0) {
+                const int p = cndp_gpu_mq_poll(q, done, edges, 1024);
+                if (p < 0)
+                    return -1;
+                got += (uint32_t)p;
+            }
+        }
+        if (cndp_gpu_mq_flush(q) < 0)
+            return -1;
+        for (long spin = 0; got < n; spin++) {
+            if (spin > 100000000L)
+                return -1;
+            const int p = cndp_gpu_mq_poll(q, done, edges, 1024);
+            if (p < 0)
+                return -1;
+            got += (uint32_t)p;
+        }
+        us[r] = (now_s() - t0) * 1e6;
+    }
+    return 0;
+}

@@ -266,3 +266,37 @@ def test_mq_backpressure_and_errors(l3, gpu):
     assert cl._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)) == -22
     c.batch, c.umem = 0, 12345
     assert cl._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)) == -22
+
+
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_c1_cndpfwd_loopback(l3, gpu, zero_copy):
+    """C1 (BASELINE configs[0]): cndpfwd loopback mode over one 512-packet
+    request, clamped to two 256-bursts (parse-args.c:394-397, main.h:48-49)
+    as _loopback_test (main.c:317-339) takes them from the ring: every frame
+    comes back in order with its MAC addresses swapped (main.h:303-315)."""
+    cl, fib, t4 = l3
+    n = 512
+    burst = 512
+    burst = burst if 0 < burst <= 256 else 256   # the -b clamp
+    pool = MbufPool(n)
+    fr = pktgen.cndpfwd_udp(n)
+    pool.fill(fr)
+    before = pool.mem.copy()
+    umem = None
+    if zero_copy:
+        cl.host_register(pool.mem)
+        umem = pool.base
+    try:
+        q = MbufQueue(cl, N.CNDP_MQ_MAC_SWAP, batch=256, depth=2, umem=umem)
+        addrs, edges = q.run(pool, np.arange(n), [burst, burst])
+        q.close()
+    finally:
+        if zero_copy:
+            cl.host_unregister(pool.mem)
+    assert np.array_equal(pool.index_of(addrs), np.arange(n))
+    assert np.all(edges == 0)
+    want = before.copy()
+    O.mac_swap(want, n, stride=2048, data_off=256)
+    assert np.array_equal(pool.mem, want)
+    d = pool.data_pos().astype(np.int64)
+    assert np.all(pool.mem[d[:, None] + np.arange(6, 12)] == 0xFF)   # broadcast now the source
