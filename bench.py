@@ -261,22 +261,15 @@ def sweep(st, stream, cfg):
     from cndp_amd import native as N
     cl, fr, out, mode = st["cl"], st["frames"], st["out"], st["mode"]
     rows = []
-    variants = [dict(tile=0, nt=0, unroll=1, blocks_per_cu=4), dict(tile=0, nt=1, unroll=1, blocks_per_cu=4),
-                dict(tile=0, nt=0, unroll=2, blocks_per_cu=4)]
-    variants += [dict(tile=t, nt=nt, unroll=1, blocks_per_cu=b) for t in (1, 4) for nt in (0, 1) for b in (2, 4, 8)]
-    variants += [dict(tile=2, nt=1, unroll=1, blocks_per_cu=4), dict(tile=3, nt=0, unroll=1, blocks_per_cu=4)]
-    variants = [dict(v, dir16=1, load_nt=0) for v in variants] + [dict(tile=4, nt=1, unroll=1, blocks_per_cu=4,
-                                                                      dir16=0, load_nt=0)]
-    variants += [dict(tile=4, nt=nt, unroll=1, blocks_per_cu=b, dir16=1, load_nt=1) for nt in (1, 0)
-                 for b in (2, 3, 4, 6)]
-    variants += [dict(tile=5, nt=1, unroll=1, blocks_per_cu=b, dir16=d, load_nt=l) for l in (1, 0)
+    variants = [dict(tile=0, nt=nt, blocks_per_cu=b) for nt in (0, 1) for b in (2, 4)]
+    variants += [dict(tile=1, nt=nt, blocks_per_cu=b, dir16=d, load_nt=l) for nt in (1, 0) for l in (1, 0)
                  for b in (1, 2, 3, 4) for d in (1, 0)]
     if mode == N.CNDP_MODE_CNET:
-        variants = [dict(cnet_tile=ct, dir16=d, cnet_spec=sp, load_nt=l) for sp in (256, 0) for ct in (3, 2, 1, 0)
+        variants = [dict(cnet_tile=ct, dir16=d, cnet_spec=sp, load_nt=l) for sp in (256, 0) for ct in (1, 0)
                     for d in (1, 0) for l in (1, 0) if (sp == 256 or d == 1) and (ct >= 1 or l == 1)]
     if "tx" in st:
-        variants = [dict(rw_wb=w, nt=nt, tile=4, load_nt=l, blocks_per_cu=b) for w in (0, 1, 2) for nt in (1, 0)
-                    for l in (1, 0) for b in (2, 4)] + [dict(tile=1, rw_wb=0)]
+        variants = [dict(rw_wb=w, nt=nt, load_nt=l, blocks_per_cu=b) for w in (0, 1, 2) for nt in (1, 0)
+                    for l in (1, 0) for b in (2, 4)]
     for v in variants:
         cl.set_tuning(**v)
         for k in range(3):
@@ -294,7 +287,7 @@ def sweep(st, stream, cfg):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"sweep_{cfg}.json"), "w") as f:
         json.dump(rows, f, indent=1)
-    cl.set_tuning(tile=5, nt=1, unroll=1, blocks_per_cu=0, dir16=1, cnet_tile=3, rw_wb=2, cnet_spec=256,
+    cl.set_tuning(tile=1, nt=1, unroll=1, blocks_per_cu=0, dir16=1, cnet_tile=1, rw_wb=2, cnet_spec=256,
                   load_nt=1)
 
 

@@ -85,20 +85,6 @@ __device__ __forceinline__ uint32_t lpm4d(const uint32_t *__restrict__ d16,
     return e >> 1;
 }
 
-// Toeplitz nibble table access: 4 stream bytes b..b+3 held little-endian in x,
-// N[q][u] at tabn[q * 16 + u]; 16-entry rows make every wave lookup
-// bank-conflict free (lanes on one row hit <= 16 distinct banks)
-__device__ __forceinline__ uint32_t tz4n(const uint32_t *tabn, uint32_t b, uint32_t x)
-{
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t v = (x >> (8 * k)) & 0xffu;
-        h ^= tabn[(2 * (b + k)) * 16 + (v >> 4)] ^ tabn[(2 * (b + k) + 1) * 16 + (v & 15u)];
-    }
-    return h;
-}
-
 // Toeplitz byte table access: T[b][v] at tab[b * 256 + v]
 __device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_t x)
 {
@@ -151,9 +137,7 @@ struct KArgs {
     uint32_t rw_parts; // 16-B parts of each rewritten frame written back
 };
 
-#ifndef FAST_THREADS // build-time override for A/B builds (tools/abbuild.sh)
 #define FAST_THREADS 256
-#endif
 // a packet ip4_lookup hands to ip4_rewrite (edge 0, ip4_lookup.c:150)
 __device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
@@ -802,126 +786,6 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_stream(KArgs a, uint6
 
 
 // ---------------------------------------------------------------------------
-// Software-pipelined per-lane variant (any layout).  vmcnt retires loads in
-// issue order, so in every loop trip the loads go out oldest-dependency
-// first:  tbl8 of packet k-1 (its tbl24 entry arrived last trip), tbl24 of
-// packet k (its frame arrived last trip), then the frame of packet k+1.
-// Each wait therefore leaves the younger loads in flight: the frame stream
-// never stops while the FIB gathers resolve.  The tbl8 / tbl24 loads are
-// issued unconditionally (index 0 when unused) so no branch splits the
-// counter bookkeeping.
-// ---------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(FAST_THREADS) void k_classify_pipe(KArgs a)
-{
-    __shared__ uint32_t s_t[TAB4_POS * 256];
-    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
-    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
-
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < TAB4_POS * 256; k += FAST_THREADS)
-        s_t[k] = a.ttab[k];
-    for (uint32_t k = tid; k <= a.reta_mask; k += FAST_THREADS)
-        s_reta[k] = a.reta[k];
-    const bool count = a.bins != nullptr;
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
-            s_bins[k] = 0;
-    __syncthreads();
-
-    const uint64_t step = (uint64_t)gridDim.x * FAST_THREADS;
-    uint64_t i = (uint64_t)blockIdx.x * FAST_THREADS + tid;
-    bool have_cur = i < a.n, have_prev = false;
-    FastHdr cur;
-    if (have_cur)
-        fast_load<false>(a, i, cur);
-    uint64_t ip = 0;
-    uint32_t e_prev = 0, lo_prev = 0, q_prev = 0;
-    bool is4_prev = false;
-    while (have_cur || have_prev) {
-        // (1) tbl8 of the previous packet (dir24_8.h:132-134)
-        uint32_t e8 = 0;
-        if (MODE == CNDP_MODE_L3FWD && have_prev)
-            e8 = a.tbl8[(e_prev & 1u) ? (e_prev >> 1) * 256u + lo_prev : 0u];
-        // (2) tbl24 of the current packet (dir24_8.h:131)
-        uint32_t e24 = 0, dip = 0;
-        bool is4 = false;
-        if (have_cur) {
-            is4 = bswap16(cur.w3 & 0xffffu) == 0x0800u;
-            dip = bswap32(alignb(cur.w8, cur.w7, 2));
-            if (MODE == CNDP_MODE_L3FWD)
-                e24 = a.tbl24[is4 ? dip >> 8 : 0u];
-        }
-        // (3) frame of the next packet
-        const uint64_t in = i + step;
-        const bool have_nxt = have_cur && in < a.n;
-        FastHdr nxt;
-        if (have_nxt)
-            fast_load<false>(a, in, nxt);
-        // (4) flow hash + RSS queue of the current packet
-        uint32_t q = 0;
-        if (have_cur) {
-            const uint32_t et = bswap16(cur.w3 & 0xffffu);
-            uint32_t hs = 0;
-            if (et == 0x0800u) {
-                const uint32_t ihl = (cur.w3 >> 16) & 0xfu;
-                const uint32_t proto = cur.w5 >> 24;
-                const uint32_t frag = bswap16(cur.w5 & 0xffffu) & 0x3fffu;
-                hs = tz4(s_t, 0, alignb(cur.w7, cur.w6, 2)) ^ tz4(s_t, 4, alignb(cur.w8, cur.w7, 2));
-                if (ihl >= 5 && (proto == 6u || proto == 17u) && frag == 0) {
-                    const uint32_t ports =
-                        ihl == 5 ? alignb(cur.w9, cur.w8, 2) : gld32(cur.p, cur.avail, 14 + 4 * ihl);
-                    hs ^= tz4(s_t, 8, ports);
-                }
-            } else if (et == 0x86DDu) {
-                const uint32_t nx = cur.w5 & 0xffu;
-                hs = hash_v6_global(cur.p, cur.avail, 14, nx == 6u || nx == 17u, a.ttab);
-            }
-            q = s_reta[hs & a.reta_mask];
-            if (a.hash)
-                a.hash[i] = hs;
-            if (a.queue)
-                a.queue[i] = (uint16_t)q;
-            if (a.ptype) // pktdev_rx.c:24-34 l3_ptype
-                a.ptype[i] = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
-        }
-        // (5) next hop, edge and bin of the previous packet
-        if (have_prev) {
-            uint32_t nh = CNDP_NH_INVALID, edge;
-            if (MODE == CNDP_MODE_L3FWD) {
-                if (is4_prev)
-                    nh = ((e_prev & 1u) ? e8 : e_prev) >> 1;
-                edge = is4_prev ? ((nh >> 16) & 0xffu) : 0xFFu;
-            } else {
-                edge = 0;
-            }
-            if (a.nh)
-                a.nh[ip] = nh;
-            if (a.edge)
-                a.edge[ip] = (uint8_t)edge;
-            if (count)
-                atomicAdd(&s_bins[bin_of<MODE>(nh, edge, q_prev, a.n_bins)], 1u);
-        }
-        // (6) shift the pipeline
-        have_prev = have_cur;
-        ip = i;
-        e_prev = e24;
-        lo_prev = dip & 0xffu;
-        is4_prev = is4;
-        q_prev = q;
-        have_cur = have_nxt;
-        cur = nxt;
-        i = in;
-    }
-    if (count) {
-        __syncthreads();
-        for (uint32_t k = tid; k < a.n_bins + 2; k += FAST_THREADS)
-            if (s_bins[k])
-                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // cnet classify: eth_rx (cne_get_ptype) -> ptype -> ip4_input / ip6_input.
 // ---------------------------------------------------------------------------
 #define CNET_THREADS 512
@@ -969,37 +833,6 @@ __device__ __forceinline__ bool v6_ext(uint32_t p)
     return p == 0u || p == 43u || p == 44u || p == 50u || p == 51u || p == 60u;
 }
 
-// The same 64-byte window held in a wave's swizzled LDS frame tile (the
-// layout k_classify_tile uses): dword d of frame slot f sits at
-// tile[(f*4 + ((d>>2) ^ ((f>>2)&3)))*4 + (d&3)].
-struct TWin {
-    const uint32_t *t; // wave tile, as dwords
-    uint32_t f4, sw;   // f*4, swizzle of frame slot f
-    const uint8_t *g;
-    uint64_t avail;
-    __device__ __forceinline__ uint32_t dw(uint32_t d) const
-    {
-        return t[((f4 + ((d >> 2) ^ sw)) << 2) | (d & 3u)];
-    }
-    __device__ __forceinline__ uint32_t ld32(uint32_t o) const
-    {
-        if (o + 4 <= 64) {
-            const uint32_t d = o >> 2;
-            const uint32_t lo = dw(d);
-            if ((o & 3u) == 0)
-                return lo;
-            return alignb(dw(d + 1), lo, o & 3u);
-        }
-        return gld32(g, avail, o);
-    }
-    __device__ __forceinline__ uint32_t b8(uint32_t o) const
-    {
-        return o < 64 ? (dw(o >> 2) >> ((o & 3u) * 8)) & 0xffu : gbyte(g, avail, o);
-    }
-    __device__ __forceinline__ uint32_t raw16(uint32_t o) const { return ld32(o) & 0xffffu; }
-    __device__ __forceinline__ uint32_t be16(uint32_t o) const { return bswap16(ld32(o) & 0xffffu); }
-    __device__ __forceinline__ uint32_t be32(uint32_t o) const { return bswap32(ld32(o)); }
-};
 
 // pktmbuf_ptype.c:426-468 (skip_ip6_ext); returns -1 past 5 headers
 template <class W>
@@ -1436,12 +1269,7 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 // Frames that are not 16-B aligned or have < 64 bytes before the slab end
 // are staged with bounded byte loads (zero past the end), like Win.
 // ---------------------------------------------------------------------------
-#ifndef CT_THREADS // build-time overrides for A/B builds (tools/abbuild.sh)
 #define CT_THREADS 512
-#endif
-#ifndef CT_WPE
-#define CT_WPE 4 // waves per SIMD the cnet tile kernel is compiled for
-#endif
 #define CT_WAVES (CT_THREADS / 64)
 
 // frame base (bytes from slab) of packet i, or ~0 when i >= n
@@ -1457,317 +1285,6 @@ __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
     // base + 64 <= slab_len (base = ~0 fails it) and 16-B aligned; bitwise
     // ANDs so the test stays straight-line
     return (a.slab_len >= 64) & (base <= a.slab_len - 64) & ((((uintptr_t)a.slab + base) & 15u) == 0);
-}
-
-template <bool LNT>
-__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(CT_WPE, CT_WPE))) void k_classify_cnet_tile(KArgs a, uint64_t n_tiles)
-{
-    __shared__ uint32_t s_t[TAB_POS * 256];
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
-    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
-    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
-    __shared__ uint32_t s_sf[64]; // type signatures seen (speculation model)
-
-    const uint32_t tid = threadIdx.x;
-    if (tid < 64)
-        s_sf[tid] = 0;
-    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
-        s_t[k] = a.ttab[k];
-    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
-        s_reta[k] = a.reta[k];
-    const bool count = a.bins != nullptr;
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
-            s_bins[k] = 0;
-    __syncthreads();
-
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
-    u32x4 *tile = s_tile[wv];
-    const uint32_t *tdw = (const uint32_t *)tile;
-    const uint64_t wstep = (uint64_t)gridDim.x * CT_WAVES;
-    // quad lane geometry: in load k, this lane fetches part (lane&3) of frame
-    // slot 16k + lane/4, written to slot*4 + (part ^ swizzle(slot))
-    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-
-    uint64_t t = (uint64_t)blockIdx.x * CT_WAVES + wv;
-    // this lane's own frame offset, one tile ahead of the loads
-    uint64_t off_cur = 0, off_nxt = 0;
-    if (a.offsets) {
-        const uint64_t i0 = t * 64u + lane, i1 = (t + wstep) * 64u + lane;
-        off_cur = t < n_tiles && i0 < a.n ? a.offsets[i0] : 0;
-        off_nxt = t + wstep < n_tiles && i1 < a.n ? a.offsets[i1] : 0;
-    }
-    // frame bases of the 4 frames this lane loads parts of, and the loads
-    uint64_t qb[4];
-    u32x4 r[4];
-    {
-        const uint64_t my_base = ct_base(a, t * 64u + lane, off_cur);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            qb[k] = __shfl(my_base, 16 * k + (int)fr_in_k);
-            // frames off the fast path load a dummy chunk of the (aligned,
-            // 36 KiB) Toeplitz table instead, so every load is unconditional
-            const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u
-                                                   : (const uint8_t *)a.ttab + part * 16u;
-            r[k] = t < n_tiles ? ldg4<LNT>(src) : (u32x4){0, 0, 0, 0};
-        }
-    }
-    uint32_t last_sig = 0xFFFFFFFFu; // this lane's last signature marked in s_sf
-    for (; t < n_tiles; t += wstep) {
-        const uint64_t i = t * 64u + lane;
-        // (1) stage the tile: fast frames from the loads, others bounded
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t f = 16u * k + fr_in_k;
-            u32x4 v = r[k];
-            if (!ct_fast(a, qb[k])) {
-                v = (u32x4){0, 0, 0, 0};
-                if (qb[k] != ~0ull) {
-                    const uint8_t *p = a.slab + qb[k];
-                    const uint64_t avail = qb[k] < a.slab_len ? a.slab_len - qb[k] : 0;
-                    v.x = gld32(p, avail, part * 16u + 0);
-                    v.y = gld32(p, avail, part * 16u + 4);
-                    v.z = gld32(p, avail, part * 16u + 8);
-                    v.w = gld32(p, avail, part * 16u + 12);
-                }
-            }
-            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v;
-        }
-        __builtin_amdgcn_wave_barrier();
-
-        // (2) parse this lane's frame.  Fast path from 16 registers for the
-        // common shapes -- Ethernet + IPv4 IHL 5 unfragmented or IPv6 without
-        // extension headers, carrying TCP / UDP / SCTP -- where every field
-        // sits at a fixed offset inside the window; everything else runs the
-        // general cne_get_ptype restatement against the LDS window.
-        const bool live = i < a.n;
-        const uint64_t base = ct_base(a, i, off_cur);
-        const uint32_t sw = (lane >> 2) & 3u;
-        uint32_t W[16];
-        {
-            const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
-            const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
-            W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
-            W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
-            W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
-            W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
-        }
-        const uint32_t et = W[3] & 0xffffu;         // raw bytes 12..13
-        const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-        // straight-line tests (bitwise &, not &&: no branch tree)
-        const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
-        const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
-                        (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
-        const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
-        uint32_t pt = 0, pe = 0;
-        Lens lens{14u, 0u, 0u};
-        uint32_t hw[9];      // Toeplitz input words, nw of them + the L4 word
-        uint32_t nw = 0, hl4 = 0;
-        uint32_t dip = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-        bool do4 = false, do6 = false;
-#pragma unroll
-        for (int k = 0; k < 9; k++)
-            hw[k] = 0;
-        if (live && (f4 || f6)) {
-            const uint32_t proto = f4 ? p4 : p6;
-            pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
-            if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
-                const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
-                pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
-            }
-            pe = cnet_edge(pt);
-            const bool l4ok = proto == 6u || proto == 17u;
-            lens.l3 = f4 ? 20u : 40u;
-            if (a.rxmeta) // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
-                lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
-                        : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
-                             : (gbyte(a.slab + base, base < a.slab_len ? a.slab_len - base : 0, 66) & 0xf0u) >> 2;
-            if (f4) {
-                nw = 2;
-                hw[0] = alignb(W[7], W[6], 2);
-                hw[1] = alignb(W[8], W[7], 2);
-                hl4 = l4ok ? alignb(W[9], W[8], 2) : 0u;
-                if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
-                    uint32_t sum = 0;
-#pragma unroll
-                    for (int k = 0; k < 5; k++) {
-                        const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
-                        sum += (x & 0xffffu) + (x >> 16);
-                    }
-                    sum = (sum >> 16) + (sum & 0xffffu);
-                    sum = (sum >> 16) + (sum & 0xffffu);
-                    const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
-                    dip = ok ? bswap32(hw[1]) : 0u;
-                    do4 = true;
-                }
-            } else {
-                nw = 8;
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    hw[k] = alignb(W[6 + k], W[5 + k], 2);
-                hl4 = l4ok ? alignb(W[14], W[13], 2) : 0u;
-                if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
-                    if (bswap16(W[4] >> 16) < a.buf_len) {
-                        d0 = hw[4];
-                        d1 = hw[5];
-                        d2 = hw[6];
-                        d3 = hw[7];
-                    }
-                    do6 = true;
-                }
-            }
-            if (!l4ok)
-                hl4 = 0;
-        } else if (live) {
-            const TWin w{tdw, lane * 4u, sw, a.slab + base, base < a.slab_len ? a.slab_len - base : 0};
-            Lens ln{14u, 0u, 0u};
-            pt = get_ptype(w, ln);
-            lens = ln;
-            const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
-            const uint32_t ip = ln.l2;
-            const bool l4ok = l4t == 0x100u || l4t == 0x200u;
-            pe = cnet_edge(pt);
-            if (l3 != 0u && !(l3 & 0x40u)) {
-                nw = 2;
-                hw[0] = w.ld32(ip + 12);
-                hw[1] = w.ld32(ip + 16);
-            } else if (l3 & 0x40u) {
-                nw = 8;
-                for (uint32_t k = 0; k < 8; k++)
-                    hw[k] = w.ld32(ip + 8 + 4 * k);
-            }
-            hl4 = nw && l4ok ? w.ld32(ip + ln.l3) : 0u;
-            // with the speculation model, frames of the types a quiet 4-group can
-            // carry into ip4/ip6_input (L2 ether + IPv4 / IPv6 variants) get the
-            // input node's result computed as well
-            const uint32_t lb = pt & 0xffu;
-            const bool alt4 = a.spec_nh && (lb == 0x11u || lb == 0x31u || lb == 0x91u);
-            const bool alt6 = a.spec_nh && (lb == 0x41u || lb == 0xc1u || lb == 0xe1u);
-            if (pe == 3u || alt4) {
-                const uint32_t x0 = w.ld32(ip);
-                const uint32_t hl = x0 & 0xfu;
-                uint32_t sum = 0;
-                for (uint32_t k = 0; k < hl; k++) {
-                    const uint32_t x = k == 0 ? x0 : w.ld32(ip + 4 * k);
-                    sum += (x & 0xffffu) + (x >> 16);
-                }
-                sum = (sum >> 16) + (sum & 0xffffu);
-                sum = (sum >> 16) + (sum & 0xffffu);
-                const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
-                dip = ok ? w.be32(ip + 16) : 0u;
-                do4 = true;
-            } else if (pe == 4u || alt6) {
-                if (w.be16(ip + 4) < a.buf_len) {
-                    d0 = w.ld32(ip + 24);
-                    d1 = w.ld32(ip + 28);
-                    d2 = w.ld32(ip + 32);
-                    d3 = w.ld32(ip + 36);
-                }
-                do6 = true;
-            }
-        }
-        // (3) first FIB gather, unconditional (every lane indexes in bounds)
-        const uint32_t *tb0;
-        uint32_t idx0;
-        if (!do4) {
-            tb0 = a.tbl24_6;
-            idx0 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu); // trie.h:126
-        } else if (a.dir16) {
-            tb0 = a.dir16;
-            idx0 = dip >> 16;
-        } else {
-            tb0 = a.tbl24;
-            idx0 = dip >> 8;
-        }
-        uint32_t e = tb0[idx0];
-        // (4) next tile's window loads (and the offsets one tile further)
-        const uint64_t tn = t + wstep;
-        {
-            const uint64_t nb = ct_base(a, tn * 64u + lane, off_nxt);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                qb[k] = __shfl(nb, 16 * k + (int)fr_in_k);
-                const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u
-                                                       : (const uint8_t *)a.ttab + part * 16u;
-                r[k] = ldg4<LNT>(src);
-            }
-            off_cur = off_nxt;
-            if (a.offsets) {
-                const uint64_t i2 = (tn + wstep) * 64u + lane;
-                off_nxt = tn + wstep < n_tiles && i2 < a.n ? a.offsets[i2] : 0;
-            }
-        }
-        // (5) Toeplitz over the nw address words, then the L4 word
-        uint32_t h = 0;
-        for (uint32_t k = 0; k < 8; k++)
-            if (k < nw)
-                h ^= tz4(s_t, 4 * k, hw[k]);
-        if (nw && hl4 != 0u)
-            h ^= tz4(s_t, 4 * nw, hl4);
-        // (6) rest of the chain: v4 page / tbl8, v6 tbl8 levels (trie.h:127-134)
-        uint32_t j = do6 ? 3u : (a.dir16 ? 1u : 2u);
-        bool more = (do4 || do6) && (e & 1u);
-        while (__any(more)) {
-            if (more) {
-                uint32_t byte;
-                const uint32_t *tb;
-                if (do6) {
-                    const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
-                    byte = (wd >> ((j & 3u) * 8)) & 0xffu;
-                    tb = a.tbl8_6;
-                } else {
-                    byte = j == 1 ? (dip >> 8) & 0xffu : dip & 0xffu;
-                    tb = j == 1 ? a.pages : a.tbl8;
-                }
-                e = tb[(e >> 1) * 256u + byte];
-                j++;
-                more = (e & 1u) && (do6 ? j < 16 : j <= 2);
-            }
-        }
-        uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
-        if ((do4 || do6) && (pe == 3u || pe == 4u)) {
-            nh = e >> 1;
-            edge = nh >> 24;
-        }
-        if (a.spec_nh) {
-            // the input-node result is kept for the frames whose own edge does
-            // not carry it in nh already (spec_fix reads nh for the others)
-            if (live && (do4 || do6) && (!a.nh || (pe != 3u && pe != 4u)))
-                a.spec_nh[i] = e >> 1;
-            if (live)
-                a.spec_t16[i] = (uint16_t)pt;
-            // the block's bitmap only grows: a lane re-marks only a new signature
-            const uint32_t sg = spec_sig(pt & 0xffffu);
-            spec_mark(s_sf, live && sg != last_sig, sg);
-            last_sig = live ? sg : last_sig;
-        }
-        __builtin_amdgcn_wave_barrier(); // tile reads done before the next stage
-        if (live) {
-            const uint32_t q = s_reta[h & a.reta_mask];
-            if (a.ptype)
-                a.ptype[i] = pt;
-            if (a.rxmeta)
-                a.rxmeta[i] = rx_meta(lens, W[0], W[1], et);
-            if (a.nh)
-                a.nh[i] = nh;
-            if (a.hash)
-                a.hash[i] = h;
-            if (a.queue)
-                a.queue[i] = (uint16_t)q;
-            if (a.edge)
-                a.edge[i] = (uint8_t)edge;
-            if (count)
-                atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
-        }
-    }
-    if (count || a.spec_flags)
-        __syncthreads();
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
-            if (s_bins[k])
-                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    if (a.spec_flags && tid < 64 && s_sf[tid])
-        atomicOr(&a.spec_flags[tid], s_sf[tid]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1800,259 +1317,6 @@ __device__ __forceinline__ void cs_issue(const KArgs &a, uint32_t tt, uint32_t n
         const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u : (const uint8_t *)a.ttab + part * 16u;
         r[k] = ldg4<LNT>(src);
     }
-}
-
-template <bool LNT, int P>
-__device__ __forceinline__ void cs_trip(const KArgs &a, uint32_t t, uint32_t wstep, uint32_t n_tiles, uint32_t lane,
-                                        u32x4 *tile, u32x4 (&r)[2][4], CsOff &off,
-                                        const uint32_t *s_t, const uint16_t *s_reta, uint32_t *s_bins,
-                                        uint32_t *s_sf, bool count)
-{
-    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const uint32_t i = t * 64u + lane;
-    // (1) stage the tile (chunks of non-fast frames are never read)
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t f = 16u * k + fr_in_k;
-        tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
-    }
-    __builtin_amdgcn_wave_barrier();
-    const bool live = i < a.n;
-    const uint64_t base = ct_base(a, i, off.o0);
-    const uint32_t sw = (lane >> 2) & 3u;
-    uint32_t W[16];
-    {
-        const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
-        const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
-        W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
-        W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
-        W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
-        W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
-    }
-    __builtin_amdgcn_wave_barrier();
-    // (2) fast-path shape test (pktmbuf_ptype.c for these shapes); the rest go
-    // to the worklist
-    const uint32_t et = W[3] & 0xffffu; // raw bytes 12..13
-    const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-    // straight-line tests (bitwise &, not &&: no branch tree)
-    const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
-    const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
-                    (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
-    const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
-    const bool fast = live & ct_fast(a, base) & (f4 | f6);
-    {
-        const bool slow = live && !fast;
-        const unsigned long long m = __ballot(slow);
-        if (m) {
-            uint32_t w0 = 0;
-            if (lane == (uint32_t)(__ffsll(m) - 1))
-                w0 = atomicAdd(a.wl_n, (uint32_t)__popcll(m));
-            w0 = __shfl(w0, __ffsll(m) - 1);
-            if (slow)
-                a.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
-        }
-    }
-    uint32_t pt = 0, pe = 0;
-    Lens lens{14u, 0u, 0u};
-    uint32_t hw[9];
-    uint32_t nw = 0, hl4 = 0;
-    uint32_t dip = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-    bool do4 = false, do6 = false;
-#pragma unroll
-    for (int k = 0; k < 9; k++)
-        hw[k] = 0;
-    if (fast) {
-        const uint32_t proto = f4 ? p4 : p6;
-        pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
-        if (proto == 17u) { // pktmbuf_ptype.c: UDP dport 2152 / 2123 (GTP)
-            const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
-            pt |= dport == BE16C(2152u) ? 0x8000u : dport == BE16C(2123u) ? 0x7000u : 0u;
-        }
-        pe = cnet_edge(pt);
-        const bool l4ok = proto == 6u || proto == 17u;
-        lens.l3 = f4 ? 20u : 40u;
-        if (a.rxmeta) // l4_len: UDP 8, SCTP 12, TCP data offset (pktmbuf_ptype.c:596-615)
-            lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
-                    : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
-                         : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
-        if (f4) {
-            nw = 2;
-            hw[0] = alignb(W[7], W[6], 2);
-            hw[1] = alignb(W[8], W[7], 2);
-            hl4 = l4ok ? alignb(W[9], W[8], 2) : 0u;
-            if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
-                uint32_t sum = 0;
-#pragma unroll
-                for (int k = 0; k < 5; k++) {
-                    const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
-                    sum += (x & 0xffffu) + (x >> 16);
-                }
-                sum = (sum >> 16) + (sum & 0xffffu);
-                sum = (sum >> 16) + (sum & 0xffffu);
-                const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
-                dip = ok ? bswap32(hw[1]) : 0u;
-                do4 = true;
-            }
-        } else {
-            nw = 8;
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                hw[k] = alignb(W[6 + k], W[5 + k], 2);
-            hl4 = l4ok ? alignb(W[14], W[13], 2) : 0u;
-            if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
-                if (bswap16(W[4] >> 16) < a.buf_len) {
-                    d0 = hw[4];
-                    d1 = hw[5];
-                    d2 = hw[6];
-                    d3 = hw[7];
-                }
-                do6 = true;
-            }
-        }
-    }
-    // (3) the whole FIB gather chain of this tile (v4: directory or tbl24,
-    // page, tbl8; v6: tbl24 then tbl8 levels, trie.h:126-134)
-    const uint32_t *tb0;
-    uint32_t idx0;
-    if (!do4) {
-        tb0 = a.tbl24_6;
-        idx0 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu);
-    } else if (a.dir16) {
-        tb0 = a.dir16;
-        idx0 = dip >> 16;
-    } else {
-        tb0 = a.tbl24;
-        idx0 = dip >> 8;
-    }
-    uint32_t e = tb0[idx0];
-    {
-        uint32_t j = do6 ? 3u : (a.dir16 ? 1u : 2u);
-        bool more = (do4 || do6) && (e & 1u);
-        while (__any(more)) {
-            if (more) {
-                uint32_t byte;
-                const uint32_t *tb;
-                if (do6) {
-                    const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
-                    byte = (wd >> ((j & 3u) * 8)) & 0xffu;
-                    tb = a.tbl8_6;
-                } else {
-                    byte = j == 1 ? (dip >> 8) & 0xffu : dip & 0xffu;
-                    tb = j == 1 ? a.pages : a.tbl8;
-                }
-                e = tb[(e >> 1) * 256u + byte];
-                j++;
-                more = (e & 1u) && (do6 ? j < 16 : j <= 2);
-            }
-        }
-    }
-    // (4) the offsets one tile further, then the windows of tile t+2
-    {
-        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
-        off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
-        cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
-    }
-    // (5) Toeplitz, results
-    uint32_t h = 0;
-    for (uint32_t k = 0; k < 8; k++)
-        if (k < nw)
-            h ^= tz4n(s_t, 4 * k, hw[k]);
-    if (nw && hl4 != 0u)
-        h ^= tz4n(s_t, 4 * nw, hl4);
-    uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
-    if ((do4 || do6) && (pe == 3u || pe == 4u)) {
-        nh = e >> 1;
-        edge = nh >> 24;
-    }
-    if (a.spec_nh) {
-        if (fast && (do4 || do6) && (!a.nh || (pe != 3u && pe != 4u)))
-            a.spec_nh[i] = e >> 1;
-        if (fast)
-            a.spec_t16[i] = (uint16_t)pt;
-        spec_mark(s_sf, fast, spec_sig(pt & 0xffffu));
-    }
-    if (fast) {
-        const uint32_t q = s_reta[h & a.reta_mask];
-        if (a.ptype)
-            a.ptype[i] = pt;
-        if (a.rxmeta)
-            a.rxmeta[i] = rx_meta(lens, W[0], W[1], et);
-        if (a.nh)
-            a.nh[i] = nh;
-        if (a.hash)
-            a.hash[i] = h;
-        if (a.queue)
-            a.queue[i] = (uint16_t)q;
-        if (a.edge)
-            a.edge[i] = (uint8_t)edge;
-        if (count)
-            atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
-    }
-    off.o0 = off.o1;
-    off.o1 = off.o2;
-    off.o2 = off.o3;
-}
-
-#define CS_THREADS 256
-#define CS_WAVES (CS_THREADS / 64)
-template <bool LNT>
-__global__ __launch_bounds__(CS_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_cnet_stream(KArgs a, uint32_t n_tiles)
-{
-    // nibble Toeplitz tables (4.5 KiB) instead of the 36 KiB byte tables: ~21
-    // KiB of LDS per 4-wave block, so LDS no longer caps the waves per CU
-    __shared__ uint32_t s_t[2 * TAB_POS * 16];
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CS_WAVES][256];
-    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
-    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
-    __shared__ uint32_t s_sf[64];
-
-    const uint32_t tid = threadIdx.x;
-    if (tid < 64)
-        s_sf[tid] = 0;
-    for (uint32_t k = tid; k < 2 * TAB_POS * 16; k += CS_THREADS)
-        s_t[k] = a.ttab[TABN_OFF + k];
-    for (uint32_t k = tid; k <= a.reta_mask; k += CS_THREADS)
-        s_reta[k] = a.reta[k];
-    const bool count = a.bins != nullptr;
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CS_THREADS)
-            s_bins[k] = 0;
-    __syncthreads();
-
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
-    u32x4 *tile = s_tile[wv];
-    const uint32_t wstep = gridDim.x * CS_WAVES;
-    const uint32_t t0 = blockIdx.x * CS_WAVES + wv;
-    CsOff off{0, 0, 0, 0};
-    if (a.offsets) {
-#pragma unroll
-        for (uint32_t s = 0; s < 3; s++) {
-            const uint32_t ts = t0 + s * wstep, is = ts * 64u + lane;
-            const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
-            if (s == 0)
-                off.o0 = o;
-            else if (s == 1)
-                off.o1 = o;
-            else
-                off.o2 = o;
-        }
-    }
-    u32x4 r[2][4];
-    cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
-    cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
-    for (uint32_t t = t0; t < n_tiles; t += 2u * wstep) {
-        cs_trip<LNT, 0>(a, t, wstep, n_tiles, lane, tile, r, off, s_t, s_reta, s_bins, s_sf, count);
-        if (t + wstep < n_tiles)
-            cs_trip<LNT, 1>(a, t + wstep, wstep, n_tiles, lane, tile, r, off, s_t, s_reta, s_bins, s_sf, count);
-    }
-    if (count || a.spec_flags)
-        __syncthreads();
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CS_THREADS)
-            if (s_bins[k])
-                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    if (a.spec_flags && tid < 64 && s_sf[tid])
-        atomicOr(&a.spec_flags[tid], s_sf[tid]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2979,9 +2243,7 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
 //                   the group is quiet under it, and lane ng-1 hands the
 //                   burst's exit state to the next burst.
 // ---------------------------------------------------------------------------
-#ifndef SPEC_CH // build-time override for A/B builds
 #define SPEC_CH 4 // measured: 4 beats 1 and 16 (occupancy vs per-wave latency)
-#endif
 
 // stage the types of bursts [c0, c1) as type | p_nxt << 16, burst j at
 // st + (j - c0) * spec_bstride(B) (16-B aligned groups for any B)
@@ -3318,19 +2580,15 @@ __device__ __forceinline__ void spec_flag_full(uint32_t *meta)
 // uniform batch (k_spec_classes): every frame of a full group of bursts
 // [c0, c1) leaves by edge E, the entering state's p_nxt; fix those whose own
 // edge differs.  Tail frames (a burst's last cnt % 4) keep their own edge.
-// A wave takes SPEC_UNIF_W chunks and issues all its type loads (16 B = 8
-// types each) before the first is used (measured on C5: 4 chunks per wave,
-// a quarter of the waves with 8 loads each, is slower than 1)
-#ifndef SPEC_UNIF_W
-#define SPEC_UNIF_W 1
-#endif
+// A wave takes one chunk and issues all its type loads (16 B = 8 types
+// each) before the first is used (4 chunks per wave measured slower on C5)
 template <int CH>
 __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
                                                    uint32_t T, int *lbins)
 {
     // T: the node state; 8 types all equal to it need no cnet_edge (4 compares)
     const uint32_t E = cnet_edge(T), TT = T | (T << 16);
-    constexpr uint32_t U = CH * SPEC_UNIF_W * 256 / 512 > 0 ? CH * SPEC_UNIF_W * 256 / 512 : 1;
+    constexpr uint32_t U = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
     const uint32_t p0 = (uint32_t)(c0 * B), p1 = (uint32_t)(c1 * B < a.n ? c1 * B : a.n);
     const bool vec = (B & 7u) == 0;
     u32x4 v[U];
@@ -3369,13 +2627,8 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
             m &= m - 1u;
             const uint32_t i = i0 + q, l = (uint32_t)((q < 4 ? lo : hi) >> (16 * (q & 3u))) & 0xffffu;
             const uint32_t b0 = i / B * B, bend = b0 + B < a.n ? b0 + B : a.n;
-#ifndef UNIF_NOFIX
             if (b0 + ((i - b0) & ~3u) + 4u <= bend) // a full group
                 spec_fix(a, i, l, E, lbins);
-#else
-            if (b0 + ((i - b0) & ~3u) + 4u <= bend)
-                a.edge[i] = (uint8_t)E;
-#endif
         }
     }
 }
@@ -3389,33 +2642,13 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
-        const uint64_t u0 = c * SPEC_UNIF_W * CH, u1 = u0 + SPEC_UNIF_W * CH;
+        const uint64_t u0 = c * CH, u1 = u0 + CH;
         static_assert(4 * CH * 256 >= CNDP_BINS_MAX + 2, "bin counters must fit the staging tile");
         int *lbins = (int *)&s_pt[0][0]; // n_bins + 2 <= CNDP_BINS_MAX + 2 ints fit the staging tile
         const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
         for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
             lbins[k] = 0;
         __syncthreads();
-#ifdef UNIF_DIAG // timing-only builds: 1 the pass's fixed cost, 2 / 3 its loads alone (plain / nt)
-        if (UNIF_DIAG == 1 || u0 >= nb)
-            return;
-        {
-            const uint32_t p0 = (uint32_t)(u0 * B), p1 = (uint32_t)((u1 < nb ? u1 : nb) * B < a.n ? (u1 < nb ? u1 : nb) * B : a.n);
-            uint32_t acc = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < SPEC_UNIF_W * CH * 256 / 512; r++) {
-                const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
-                if (i0 + 8u <= p1) {
-                    const u32x4 *q = (const u32x4 *)(a.spec_t16 + i0);
-                    const u32x4 x = UNIF_DIAG == 3 ? __builtin_nontemporal_load(q) : *q;
-                    acc ^= x.x ^ x.y ^ x.z ^ x.w;
-                }
-            }
-            if (acc == 0x9E3779B9u)
-                meta[200] = acc;
-        }
-        return;
-#endif
         if (u0 < nb)
             spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, meta[SPEC_IN] & 0xffffu, lbins);
         __syncthreads();
@@ -3832,9 +3065,9 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_nt = 1;
     c->tune_unroll = 1;
     c->tune_bpc = 0; // auto: 2 for the streamed tile kernel, 4 otherwise
-    c->tune_tile = 5;
+    c->tune_tile = 1;
     c->tune_dir16 = 1;
-    c->tune_cnet_tile = 3;
+    c->tune_cnet_tile = 1;
     c->tune_lnt = 1;
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
@@ -4487,8 +3720,8 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
             c->sf_clean = 0;
         }
-        // the streamed kernels index frames in 32 bits (t * 64 + lane < 2^32)
-        if ((c->tune_cnet_tile == 2 || c->tune_cnet_tile == 3) && b->n <= 0xFFFFFF00u) {
+        // the deferred kernel indexes frames in 32 bits (t * 64 + lane < 2^32)
+        if (c->tune_cnet_tile && b->n <= 0xFFFFFF00u) {
             // fast kernel, then the general parse of the frames it left
             if ((uint64_t)b->n + 1 > c->cs_wl_cap) {
                 if (c->cs_wl)
@@ -4506,40 +3739,18 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
             c->wl_clean = 0;
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
-            if (c->tune_cnet_tile == 3) {
-                uint64_t gd = (n_tiles + CT_WAVES - 1) / CT_WAVES;
-                const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 2u;
-                if (gd > (uint64_t)c->num_cu * bpc)
-                    gd = (uint64_t)c->num_cu * bpc;
-                static void (*const dfns[2][2])(KArgs, uint32_t) = {{k_cnet_defer<false, false>,
-                                                                     k_cnet_defer<false, true>},
-                                                                    {k_cnet_defer<true, false>,
-                                                                     k_cnet_defer<true, true>}};
-                const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
-                hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
-                                   0, s, a, (uint32_t)n_tiles);
-            } else {
-                uint64_t gt = (n_tiles + CS_WAVES - 1) / CS_WAVES;
-                const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 5u;
-                if (gt > (uint64_t)c->num_cu * bpc)
-                    gt = (uint64_t)c->num_cu * bpc;
-                if (c->tune_lnt)
-                    hipLaunchKernelGGL(k_cnet_stream<true>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a,
-                                       (uint32_t)n_tiles);
-                else
-                    hipLaunchKernelGGL(k_cnet_stream<false>, dim3((uint32_t)gt), dim3(CS_THREADS), 0, s, a,
-                                       (uint32_t)n_tiles);
-            }
+            uint64_t gd = (n_tiles + CT_WAVES - 1) / CT_WAVES;
+            const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 2u;
+            if (gd > (uint64_t)c->num_cu * bpc)
+                gd = (uint64_t)c->num_cu * bpc;
+            static void (*const dfns[2][2])(KArgs, uint32_t) = {{k_cnet_defer<false, false>,
+                                                                 k_cnet_defer<false, true>},
+                                                                {k_cnet_defer<true, false>,
+                                                                 k_cnet_defer<true, true>}};
+            const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
+            hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
+                               0, s, a, (uint32_t)n_tiles);
             hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
-        } else if (c->tune_cnet_tile || B) {
-            const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
-            uint64_t gt = (n_tiles + CT_WAVES - 1) / CT_WAVES;
-            if (gt > cap)
-                gt = cap;
-            if (c->tune_lnt)
-                hipLaunchKernelGGL(k_classify_cnet_tile<true>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
-            else
-                hipLaunchKernelGGL(k_classify_cnet_tile<false>, dim3((uint32_t)gt), dim3(CT_THREADS), 0, s, a, n_tiles);
         } else {
             hipLaunchKernelGGL(k_classify_cnet<false>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         }
@@ -4604,87 +3815,51 @@ static int classify_l3(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, 
         uint32_t g = blocks_for(b->n, FAST_THREADS);
         // auto: 2 blocks per CU for the streamed kernel, 4 for the others
         // (the fused rewrite runs the split-gather tile kernel)
-        const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : c->tune_tile == 5 && !rw_tx ? 2u : 4u;
+        const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : !rw_tx ? 2u : 4u;
         const uint32_t cap = (uint32_t)c->num_cu * bpc;
         if (g > cap)
             g = cap;
-        if (c->tune_tile == 3) {
-            if (b->mode == CNDP_MODE_L3FWD)
-                hipLaunchKernelGGL(k_classify_pipe<CNDP_MODE_L3FWD>, dim3(g), dim3(FAST_THREADS), 0, s, a);
-            else
-                hipLaunchKernelGGL(k_classify_pipe<CNDP_MODE_HASH>, dim3(g), dim3(FAST_THREADS), 0, s, a);
-            HIP_TRY(hipGetLastError());
-            return 0;
-        }
         // wave-tile path: packed 64-B slots, 16-B aligned, whole tiles in bounds
         const uint64_t n_tiles = b->n / 64u;
         const bool tile_ok = c->tune_tile && !b->offsets && b->stride == 64 &&
                              (((uintptr_t)b->slab + b->data_off) & 15u) == 0 && n_tiles > 0 &&
                              b->data_off + n_tiles * 4096u <= b->slab_len;
+        const int mi = b->mode == CNDP_MODE_L3FWD ? 0 : 1, nti = c->tune_nt ? 1 : 0, li = c->tune_lnt ? 1 : 0;
         if (tile_ok) {
             uint32_t gt = (uint32_t)((n_tiles + TILE_WAVES - 1) / TILE_WAVES);
             if (gt > cap)
                 gt = cap;
-            if (c->tune_tile == 5 && !rw_tx) {
-                typedef void (*stream_fn)(KArgs, uint64_t);
-                static const stream_fn sfns[2][2][2] = {
-                    {{k_classify_stream<CNDP_MODE_L3FWD, false, false>, k_classify_stream<CNDP_MODE_L3FWD, false, true>},
-                     {k_classify_stream<CNDP_MODE_L3FWD, true, false>, k_classify_stream<CNDP_MODE_L3FWD, true, true>}},
-                    {{k_classify_stream<CNDP_MODE_HASH, false, false>, k_classify_stream<CNDP_MODE_HASH, false, true>},
-                     {k_classify_stream<CNDP_MODE_HASH, true, false>, k_classify_stream<CNDP_MODE_HASH, true, true>}}};
-                hipLaunchKernelGGL(sfns[b->mode == CNDP_MODE_L3FWD ? 0 : 1][c->tune_nt ? 1 : 0][c->tune_lnt ? 1 : 0],
-                                   dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
-                HIP_TRY(hipGetLastError());
-                return 0;
-            }
-            // tile 1: gathers then prefetch; 2: prefetch then gathers; 4: split
-            const int sched = c->tune_tile == 2 ? 0 : (c->tune_tile == 4 || c->tune_tile == 5) ? 2 : 1;
             typedef void (*tile_fn)(KArgs, uint64_t);
-            static const tile_fn fns[2][3][2] = {
-                {{k_classify_tile<CNDP_MODE_L3FWD, 0, false>, k_classify_tile<CNDP_MODE_L3FWD, 0, true>},
-                 {k_classify_tile<CNDP_MODE_L3FWD, 1, false>, k_classify_tile<CNDP_MODE_L3FWD, 1, true>},
-                 {k_classify_tile<CNDP_MODE_L3FWD, 2, false>, k_classify_tile<CNDP_MODE_L3FWD, 2, true>}},
-                {{k_classify_tile<CNDP_MODE_HASH, 0, false>, k_classify_tile<CNDP_MODE_HASH, 0, true>},
-                 {k_classify_tile<CNDP_MODE_HASH, 1, false>, k_classify_tile<CNDP_MODE_HASH, 1, true>},
-                 {k_classify_tile<CNDP_MODE_HASH, 2, false>, k_classify_tile<CNDP_MODE_HASH, 2, true>}}};
-            // split schedule with non-temporal frame loads (CNDP_TUNE_LOAD_NT)
-            static const tile_fn fns_lnt[2][2] = {
-                {k_classify_tile<CNDP_MODE_L3FWD, 2, false, false, true>,
-                 k_classify_tile<CNDP_MODE_L3FWD, 2, true, false, true>},
-                {k_classify_tile<CNDP_MODE_HASH, 2, false, false, true>,
-                 k_classify_tile<CNDP_MODE_HASH, 2, true, false, true>}};
-            const int mi = b->mode == CNDP_MODE_L3FWD ? 0 : 1, nti = c->tune_nt ? 1 : 0;
-            tile_fn fn = sched == 2 && c->tune_lnt ? fns_lnt[mi][nti] : fns[mi][sched][nti];
-            if (rw_tx && b->mode == CNDP_MODE_L3FWD && sched == 2 && b->n % 256u == 0 && c->d_rw_tbl) {
+            if (rw_tx && b->mode == CNDP_MODE_L3FWD && b->n % 256u == 0 && c->d_rw_tbl) {
+                // ip4_rewrite fused into the split-gather tile kernel (the rewrite is
+                // applied to the frame tile already in LDS)
                 static const tile_fn rfns[2][2] = {
                     {k_classify_tile<CNDP_MODE_L3FWD, 2, false, true, false>,
                      k_classify_tile<CNDP_MODE_L3FWD, 2, false, true, true>},
                     {k_classify_tile<CNDP_MODE_L3FWD, 2, true, true, false>,
                      k_classify_tile<CNDP_MODE_L3FWD, 2, true, true, true>}};
-                fn = rfns[c->tune_nt ? 1 : 0][c->tune_lnt ? 1 : 0];
                 a.rw_tbl = c->d_rw_tbl;
                 a.tx_edge = rw_tx;
                 a.rw_parts = c->tune_rw_wb == 1 ? 4u : c->tune_rw_wb == 2 ? 5u : c->rw_parts;
                 *fused = true;
+                hipLaunchKernelGGL(rfns[nti][li], dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
+                HIP_TRY(hipGetLastError());
+                return 0;
             }
-            hipLaunchKernelGGL(fn, dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
+            static const tile_fn sfns[2][2][2] = {
+                {{k_classify_stream<CNDP_MODE_L3FWD, false, false>, k_classify_stream<CNDP_MODE_L3FWD, false, true>},
+                 {k_classify_stream<CNDP_MODE_L3FWD, true, false>, k_classify_stream<CNDP_MODE_L3FWD, true, true>}},
+                {{k_classify_stream<CNDP_MODE_HASH, false, false>, k_classify_stream<CNDP_MODE_HASH, false, true>},
+                 {k_classify_stream<CNDP_MODE_HASH, true, false>, k_classify_stream<CNDP_MODE_HASH, true, true>}}};
+            hipLaunchKernelGGL(sfns[mi][nti][li], dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
             HIP_TRY(hipGetLastError());
             return 0;
         }
-#define LAUNCH_FAST(M, NTV, UV) \
-    hipLaunchKernelGGL((k_classify_fast<M, NTV, UV>), dim3(g), dim3(FAST_THREADS), 0, s, a)
-        const int v = (b->mode == CNDP_MODE_L3FWD ? 0 : 4) | (c->tune_nt ? 2 : 0) | (c->tune_unroll == 2 ? 1 : 0);
-        switch (v) {
-        case 0: LAUNCH_FAST(CNDP_MODE_L3FWD, false, 1); break;
-        case 1: LAUNCH_FAST(CNDP_MODE_L3FWD, false, 2); break;
-        case 2: LAUNCH_FAST(CNDP_MODE_L3FWD, true, 1); break;
-        case 3: LAUNCH_FAST(CNDP_MODE_L3FWD, true, 2); break;
-        case 4: LAUNCH_FAST(CNDP_MODE_HASH, false, 1); break;
-        case 5: LAUNCH_FAST(CNDP_MODE_HASH, false, 2); break;
-        case 6: LAUNCH_FAST(CNDP_MODE_HASH, true, 1); break;
-        default: LAUNCH_FAST(CNDP_MODE_HASH, true, 2); break;
-        }
-#undef LAUNCH_FAST
+        // any layout (strided UMEM frames, IMIX offsets, unaligned slabs): per lane
+        typedef void (*fast_fn)(KArgs);
+        static const fast_fn ffns[2][2] = {{k_classify_fast<CNDP_MODE_L3FWD, false, 1>, k_classify_fast<CNDP_MODE_L3FWD, true, 1>},
+                                           {k_classify_fast<CNDP_MODE_HASH, false, 1>, k_classify_fast<CNDP_MODE_HASH, true, 1>}};
+        hipLaunchKernelGGL(ffns[mi][nti], dim3(g), dim3(FAST_THREADS), 0, s, a);
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -6113,7 +5288,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_nt = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_UNROLL:
-        if (value != 1 && value != 2)
+        if (value != 1)
             return -EINVAL;
         c->tune_unroll = value;
         return 0;
@@ -6123,7 +5298,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_bpc = value;
         return 0;
     case CNDP_TUNE_TILE:
-        if (value < 0 || value > 5)
+        if (value < 0 || value > 1)
             return -EINVAL;
         c->tune_tile = value;
         return 0;
@@ -6131,7 +5306,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_dir16 = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_CNET_TILE:
-        if (value < 0 || value > 3)
+        if (value < 0 || value > 1)
             return -EINVAL;
         c->tune_cnet_tile = value;
         return 0;

@@ -266,37 +266,33 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 
 /* Kernel variant knobs (performance only; results never change):
  *   CNDP_TUNE_NT            1 = non-temporal hint on the once-touched streams: frame loads
- *                           and output stores (per-lane kernels), output stores only
+ *                           and output stores (per-lane kernel), output stores only
  *                           (wave-tile kernels) (default 1)
- *   CNDP_TUNE_UNROLL        packets per lane per loop trip, 1 or 2 (default 1)
+ *   CNDP_TUNE_UNROLL        packets per lane per loop trip: 1 (the only value kept)
  *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 0 = auto:
  *                           2 for the streamed wave-tile kernel, 4 for the others)
- *   CNDP_TUNE_TILE          l3fwd/hash kernel: 0 per-lane, 1 / 2 wave-tile LDS staging
- *                           (packed 64-B slots; prefetch before / after the FIB gathers),
- *                           3 software-pipelined per-lane, 4 wave-tile with the next
- *                           tile's loads issued between the two FIB gathers, 5 streamed
- *                           wave-tile: frames two tiles ahead, each FIB gather level one
- *                           loop trip apart (default 5)
+ *   CNDP_TUNE_TILE          l3fwd/hash kernel for packed 64-B slots: 1 = streamed wave tile
+ *                           (frames two tiles ahead, each FIB gather level one loop trip
+ *                           apart; default), 0 = the per-lane kernel every other layout
+ *                           (strided UMEM frames, IMIX offsets) uses
  *   CNDP_TUNE_DIR16         1 = resolve IPv4 lookups through the L2-resident /16 directory
  *                           kept in front of tbl24 (default 1)
- *   CNDP_TUNE_CNET_TILE     cnet kernel: 3 = deferred-chain wave tile (fast path, the FIB
+ *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = deferred-chain wave tile (fast path, the FIB
  *                           chain of each tile finished one loop trip later, two window
- *                           tiles in flight) + general per-lane parse of the frames it
- *                           leaves (default), 2 = streamed fast path + the same general
- *                           parse, 1 = wave-tile staging with the next tile's loads
- *                           overlapping the FIB gathers, full parse inline, 0 = per-lane rows
+ *                           tiles in flight) + the general per-lane parse of the frames it
+ *                           leaves (default), 0 = the general per-lane parse for every frame
  *   CNDP_TUNE_HOST_CHUNK    packets per pipelined chunk of cndp_gpu_classify_host
  *                           (>= 1024, default 1M)
  *   CNDP_TUNE_CNET_SPEC     cnet: graph burst size B of the ptype node's speculative
  *                           4-wide loop (ptype.c:48-210, uint8_t fix_spec quirk
  *                           included); the node state (last_type) persists across calls
- *                           and is reset to 0 by setting this key.  0 = route every
- *                           frame by p_nxt[its type] instead (default 256)
+ *                           and restarts at 0 on the next call after this key is set.
+ *                           0 = route every frame by p_nxt[its type] instead (default 256)
  *   CNDP_TUNE_RW_WB         fused classify+rewrite write-back: 0 = the 16-B parts the
  *                           rewrite touches of rewritten frames, 1 = whole rewritten
  *                           frames, 2 = whole tiles holding a rewrite (default: full
  *                           coalesced lines beat partial-line writes on HBM)
- *   CNDP_TUNE_LOAD_NT       wave-tile kernels (tile 4 / 5, cnet tile): 1 = frame tiles loaded with the
+ *   CNDP_TUNE_LOAD_NT       wave-tile kernels: 1 = frame tiles loaded with the
  *                           non-temporal hint, so the once-read stream neither allocates
  *                           in L2 / the Infinity Cache nor evicts the FIB directory from
  *                           them (default 1)

@@ -10,7 +10,8 @@ obj=cndp_amd/build/ab_$name
 mkdir -p "$obj"
 gcc -O3 -fPIC -std=gnu11 -c cndp_amd/csrc/rib.c -o "$obj/rib.o"
 gcc -O3 -fPIC -std=gnu11 -c cndp_amd/csrc/fib.c -o "$obj/fib.o"
+gcc -O3 -fPIC -std=gnu11 -c cndp_amd/csrc/node.c -o "$obj/node.o"
 /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -w "$@" -c cndp_amd/csrc/cndp_gpu.hip -o "$obj/cndp_gpu.o"
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--version-script=cndp_amd/csrc/exports.map \
-    -o "cndp_amd/lib/libcndp_gpu_$name.so" "$obj/rib.o" "$obj/fib.o" "$obj/cndp_gpu.o"
+    -o "cndp_amd/lib/libcndp_gpu_$name.so" "$obj/rib.o" "$obj/fib.o" "$obj/node.o" "$obj/cndp_gpu.o" -lpthread
 echo "built cndp_amd/lib/libcndp_gpu_$name.so"
