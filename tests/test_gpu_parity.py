@@ -533,7 +533,14 @@ def test_l3fwd_mbuf_shim(l3, gpu):
         h[56:64] = 0xAB                                                # udata64 sentinel
     ptrs = (ctypes.c_void_p * n)(*[hdrs.ctypes.data + 64 * i for i in range(n)])
     edges = np.zeros(n, np.uint16)
+    # by default m->hash is left alone (no reference node writes it) ...
     N.check(cl._L.cndp_gpu_l3fwd_mbufs(cl.h, ptrs, n, edges.ctypes.data, None), "l3fwd_mbufs")
+    assert np.all(hdrs[:, 16:20] == 0)
+    # ... and written on request (CNDP_TUNE_MBUF_HASH)
+    cl.set_tuning(mbuf_hash=1)
+    hdrs[:, 56:64] = 0xAB
+    N.check(cl._L.cndp_gpu_l3fwd_mbufs(cl.h, ptrs, n, edges.ctypes.data, None), "l3fwd_mbufs")
+    cl.set_tuning(mbuf_hash=0)
     et = (win[:, 12].astype(np.uint32) << 8) | win[:, 13]
     ptype = hdrs[:, 32:36].copy().view(np.uint32).ravel()
     assert np.array_equal(ptype, np.where(et == 0x0800, 0x90, np.where(et == 0x86DD, 0xE0, 0)))
