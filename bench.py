@@ -59,9 +59,15 @@ def log(*a):
 
 
 def setup_dist():
+    """One process per GPU (torchrun), RCCL ("nccl") for the one collective.
+    CNDP_DIST_BACKEND=gloo rehearses the same multi-rank path on a box with
+    fewer GPUs than ranks (ranks then share devices: local_rank % devices)."""
     from cndp_amd import dist as D
-    world, rank, local = D.init_from_env("nccl")
+    backend = os.environ.get("CNDP_DIST_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
     torch.cuda.set_device(local)
+    world, rank, _ = D.init_from_env(backend)
     return world, rank, local
 
 
