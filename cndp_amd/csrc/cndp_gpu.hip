@@ -131,6 +131,16 @@ struct KArgs {
     // fast kernel leaves to the general parse, and their count
     uint32_t *wl;
     uint32_t *wl_n;
+    // speculation bookkeeping, folded into k_classify_cnet's last block to
+    // finish (spec_classes): nullptr spec_meta = no speculation model
+    uint32_t *spec_meta;   // sp_small + 1 (meta[-1] = the node state)
+    uint8_t *spec_cls;     // class id per signature (2048)
+    uint32_t *spec_ticket; // k_classify_cnet's block arrivals, 9 words 32 apart (0 between launches)
+    uint32_t *spec_bar;    // k_spec_fallback's barrier words, reset by spec_classes
+    uint8_t *spec_tile;    // per 64-frame tile: 0x80 | edge when every frame has that edge, else 0
+    uint32_t *spec_hint;   // pinned host words (device view): the last call's worklist size class, uniform flag
+    uint32_t spec_B;       // graph burst size
+    uint32_t spec_allow;   // batch shortcuts allowed (CNDP_TUNE_SPEC_SCAN auto)
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -138,6 +148,7 @@ struct KArgs {
 };
 
 #define FAST_THREADS 256
+#define SPEC_CH_K 4 // graph bursts per speculation chunk (SPEC_CH)
 // a packet ip4_lookup hands to ip4_rewrite (edge 0, ip4_lookup.c:150)
 __device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
@@ -1038,6 +1049,11 @@ __host__ __device__ __forceinline__ constexpr uint32_t spec_lowslot(uint32_t low
          : low == 0x41u ? 4u : low == 0xc1u ? 5u : low == 0xe1u ? 6u : SPEC_LOWS;
 }
 
+// The edge every frame of a canonical tile (k_cnet_defer's tile words) has
+// for its low byte: 0x11 (IPv4) -> ip4_input, 0x41 (IPv6) -> ip6_input; a
+// canonical tile holds no other low byte.  0xFF: none.
+__device__ __forceinline__ uint32_t spec_canon(uint32_t low) { return low == 0x11u ? 3u : low == 0x41u ? 4u : 0xFFu; }
+
 // cnet_edge and the speculation summary bit of a type, by (high-byte class
 // hi, low byte): a 5 x 256 table of u16 built at compile time and copied to
 // LDS by the kernels that use it.  hi = 0..3 for high bytes 0x00, 0x01,
@@ -1106,6 +1122,49 @@ __device__ __forceinline__ void spec_mark(uint32_t *s_f, bool on, uint32_t g)
 }
 
 
+__device__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uint32_t *meta,
+                             const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t nb,
+                             uint32_t allow_skip, uint32_t *wl_n, uint32_t *bar, uint32_t *hint);
+
+// The speculation classes pass, folded into k_classify_cnet (no launch of its
+// own): every block takes an arrival ticket once its flag ORs (device
+// atomics) and, if it parsed frames, its type stores have left -- each wave's
+// vmcnt(0), a block barrier, then a release fence by a block that stored --
+// and the block that draws the last ticket acquires and runs spec_classes
+// with its wave 0.  The ticket is two-level (MI355X_MICROARCH.md fanin: one
+// word takes ~88 returning atomics per µs, 512 blocks would queue ~6 µs on
+// it): block b counts on word b % 8, the last of each group on word 8
+// (words 128 B apart).
+__device__ __forceinline__ void cnet_spec_tail(const KArgs &a, bool stored)
+{
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (stored)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t G = gridDim.x, g = blockIdx.x & 7u, ng = G < 8u ? G : 8u;
+        const uint32_t in_g = (G - g + 7u) / 8u; // blocks of group g
+        bool last = __hip_atomic_fetch_add(&a.spec_ticket[32u * g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    in_g - 1u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent"); // pass the group's releases on
+            last = __hip_atomic_fetch_add(&a.spec_ticket[32u * 8u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   ng - 1u;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x >= 64)
+        return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (threadIdx.x < 9)
+        a.spec_ticket[32u * threadIdx.x] = 0; // for the next launch (kernel boundary)
+    const uint64_t nb = ((uint64_t)a.n + a.spec_B - 1) / a.spec_B;
+    spec_classes(threadIdx.x, a.spec_flags, a.spec_cls, a.spec_meta, a.spec_t16, a.n, a.spec_B, nb, a.spec_allow,
+                 a.wl_n, a.spec_bar, a.spec_hint);
+}
+
 template <bool WL>
 __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 {
@@ -1116,8 +1175,12 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
     __shared__ uint32_t s_sf[64]; // type signatures seen (speculation model)
 
     const uint32_t tid = threadIdx.x;
-    if (WL && (uint64_t)blockIdx.x * CNET_THREADS >= *a.wl_n)
-        return; // nothing left for this block
+    // WL: nothing left for this block -- it only takes its arrival ticket
+    if (WL && (uint64_t)blockIdx.x * CNET_THREADS >= *a.wl_n) {
+        if (a.spec_meta)
+            cnet_spec_tail(a, false);
+        return;
+    }
     if (tid < 64)
         s_sf[tid] = 0;
     for (uint32_t k = tid; k < TAB_POS * 256; k += CNET_THREADS)
@@ -1252,6 +1315,8 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
     if (a.spec_flags && tid < 64 && s_sf[tid])
         atomicOr(&a.spec_flags[tid], s_sf[tid]);
+    if (a.spec_meta)
+        cnet_spec_tail(a, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -1518,6 +1583,16 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
+            if (a.spec_tile && bv) {
+                // the tile's word for the speculation passes (spec_canon): 1 when
+                // every frame has its low byte's common edge -- parsed here (low
+                // byte 0x11 / 0x41) and bound for ip4_input / ip6_input, not GTP
+                // or pkt_drop, nor left to the general parse
+                const bool odd = ib < a.n && !(bf && (pe == 3u || pe == 4u));
+                const bool canon = __ballot(odd) == 0ull;
+                if (lane == 0)
+                    a.spec_tile[t - wstep] = (uint8_t)canon;
+            }
         }
         if (bf) {
             const uint32_t q = s_reta[sb.h & a.reta_mask];
@@ -1648,6 +1723,13 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 #define SPEC_IN 131   // the node state entering this batch (meta[-1] becomes the final one)
 #define SPEC_NOLOCAL 132 // one low byte only: no universal group exists, k_spec_local is skipped
 #define SPEC_UNIF 133 // every type has the entering state's low byte: k_spec_local's uniform pass only
+#define SPEC_ERR 134  // a k_spec_fallback barrier poll expired (diagnostic; sticky)
+// chunks k_spec_local_t leaves to k_spec_fallback (entering state known, types
+// needed): 8 lists, one per block % 8 (the arrivals spread over 8 words, each
+// 128 B from the others and from the meta words every wave reads), list x's
+// count at meta[SPEC_RCNT + 32 x], its entries (chunk, state) at R + x * 2 * nch
+#define SPEC_RCNT 640
+#define SPEC_HINT 900 // the hint words last written to host memory
 #define SPEC_TAIL 16
 __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t &cur)
 {
@@ -1657,20 +1739,27 @@ __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2,
         cur = l3;
 }
 
-// It also clears the signature flags and the worklist count for the next
-// call (both were read before: the flags here, the count by the general
-// kernel), which saves the two per-call memsets.
-__global__ __launch_bounds__(64) void k_spec_classes(uint32_t *flags, uint8_t *class_id, uint32_t *meta,
-                                                     const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                     uint64_t nb, uint32_t allow_skip, uint32_t *wl_n)
+// Run by wave 0 of the last block of k_classify_cnet to finish (after every
+// block's flag ORs and type stores, see there).  It also clears the signature
+// flags, the worklist count and k_spec_fallback's barrier words for the next
+// call (the flags and the count were read before), which saves per-call
+// memsets.
+__device__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uint32_t *meta,
+                             const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t nb,
+                             uint32_t allow_skip, uint32_t *wl_n, uint32_t *bar, uint32_t *hint)
 {
-    const uint32_t t = threadIdx.x;
+    const uint32_t wl_cnt = wl_n ? *wl_n : 0u; // for the hint, before the reset below
+    if (t < 8)
+        meta[SPEC_RCNT + 32 * t] = 0;
     const uint32_t s_in = meta[-1] & 0xffffu, g0 = spec_sig(s_in); // the node state entering the batch
     if (t == 0) {
         meta[SPEC_IN] = s_in;
         meta[SPEC_FULL] = 0;
+        bar[0] = 0;
+        bar[1] = 0;
     }
-    const uint32_t w = flags[t] | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
+    const uint32_t f = __hip_atomic_load(&flags[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t w = f | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
     flags[t] = 0;
     if (wl_n && t == 0)
         *wl_n = 0;
@@ -1767,8 +1856,21 @@ __global__ __launch_bounds__(64) void k_spec_classes(uint32_t *flags, uint8_t *c
             }
         }
     }
-    if (t == 0)
+    if (t == 0) {
         meta[SPEC_SKIP] = skip;
+        if (hint) {
+            // host-visible launch-size hint for the next call (pinned, mapped):
+            // the worklist size class and the uniform flag, written only when
+            // they change (a write to host memory delays the kernel's end)
+            const uint32_t h0 = wl_cnt ? 32u - (uint32_t)__clz(wl_cnt) : 0u, h1 = meta[SPEC_UNIF];
+            if (meta[SPEC_HINT] != h0 || meta[SPEC_HINT + 1] != h1) {
+                meta[SPEC_HINT] = h0;
+                meta[SPEC_HINT + 1] = h1;
+                __hip_atomic_store(&hint[0], h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&hint[1], h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 // the 4 types of the group at packet j (16-B load when the burst size keeps
@@ -1945,10 +2047,10 @@ __device__ __forceinline__ uint32_t spec_apply_t(const uint32_t *m, uint32_t st)
 // words; s_m rows KF + 1, so a row store by 64 lanes hits 64 banks).
 template <uint32_t KF>
 __device__ __forceinline__ void spec_scan_a_body(uint32_t *s_m, uint64_t nb, uint32_t K, const uint32_t *T,
-                                                 uint32_t *P, uint32_t *Bt)
+                                                 uint32_t *P, uint32_t *Bt, uint64_t vb)
 {
     const uint32_t t = threadIdx.x;
-    const uint64_t b = (uint64_t)blockIdx.x * SPEC_BLK + t;
+    const uint64_t b = vb * SPEC_BLK + t;
     uint32_t *row = s_m + t * (KF + 1);
     uint32_t m[KF];
 #pragma unroll
@@ -1974,7 +2076,7 @@ __device__ __forceinline__ void spec_scan_a_body(uint32_t *s_m, uint64_t nb, uin
         if (b < nb && k < K)
             P[b * KF + k] = m[k];
         if (t == SPEC_BLK - 1 && k < K)
-            __hip_atomic_store(&Bt[(uint64_t)blockIdx.x * KF + k], m[k], __ATOMIC_RELAXED,
+            __hip_atomic_store(&Bt[vb * KF + k], m[k], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT); // sc1: read by the last block to arrive
     }
 }
@@ -2033,15 +2135,10 @@ __device__ __forceinline__ void spec_scan_c_body(uint32_t *s_m, uint32_t *s_carr
                 Sblk[k0] = st; // tagged: the consumers index P rows with it
         }
         __syncthreads();
-        if (t == 0) { // carry = carry then this window's total
+        if (t < KF) { // carry = carry then this window's total (entry t reads only entry t)
             const uint32_t *tot = s_m + (dmax - 1) * (KF + 1);
-            uint32_t nc[KF];
-            for (uint32_t k = 0; k < KF; k++) {
-                const uint32_t ck = s_carry[k];
-                nc[k] = k >= K ? SPEC_UNCH : ck == SPEC_UNCH ? tot[k] : spec_apply_t(tot, ck);
-            }
-            for (uint32_t k = 0; k < KF; k++)
-                s_carry[k] = nc[k];
+            const uint32_t ck = s_carry[t];
+            s_carry[t] = t >= K ? SPEC_UNCH : ck == SPEC_UNCH ? tot[t] : spec_apply_t(tot, ck);
         }
         __syncthreads();
     }
@@ -2074,9 +2171,9 @@ __global__ __launch_bounds__(SPEC_BLK) void k_spec_scan(uint64_t nitems, const u
     if (meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL]))
         return;
     if (K <= kfast)
-        spec_scan_a_body<SPEC_KFAST>(s_m, nitems, K, T, P, Bt);
+        spec_scan_a_body<SPEC_KFAST>(s_m, nitems, K, T, P, Bt, blockIdx.x);
     else if (K <= kmax)
-        spec_scan_a_body<SPEC_KMAX>(s_m, nitems, K, T, P, Bt);
+        spec_scan_a_body<SPEC_KMAX>(s_m, nitems, K, T, P, Bt, blockIdx.x);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
@@ -2123,13 +2220,24 @@ __device__ __forceinline__ uint32_t spec_enter(const uint32_t *P, uint64_t j, ui
 // lbins != nullptr: the bin moves go to a block's LDS counters (flushed by
 // the caller) -- the uniform pass moves every frame from the same few bins,
 // and same-address global atomics serialize
-__device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst, int *lbins = nullptr)
+// The one word a fix reads: the frame's own input-node result when its own
+// edge is ip4/ip6_input (nh, or spec_nh without an nh output), else the
+// speculated destination's when that is an input node (spec_nh), else none.
+__device__ __forceinline__ uint32_t spec_fix_load(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst)
+{
+    const uint32_t own = cnet_edge(own_l);
+    if (own == 3u || own == 4u)
+        return a.nh ? a.nh[i] : a.spec_nh[i];
+    return dst == 3u || dst == 4u ? a.spec_nh[i] : 0u;
+}
+
+__device__ void spec_fix_v(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst, uint32_t v, int *lbins)
 {
     const uint32_t own = cnet_edge(own_l);
     const bool own_in = own == 3u || own == 4u;
-    const uint32_t old_nh = own_in ? (a.nh ? a.nh[i] : a.spec_nh[i]) : CNDP_NH_INVALID;
+    const uint32_t old_nh = own_in ? v : CNDP_NH_INVALID;
     const uint32_t old_edge = own_in ? old_nh >> 24 : 0x80u | own;
-    const uint32_t nh = dst == 3u || dst == 4u ? (own_in ? old_nh : a.spec_nh[i]) : CNDP_NH_INVALID;
+    const uint32_t nh = dst == 3u || dst == 4u ? v : CNDP_NH_INVALID;
     const uint32_t edge = dst == 3u || dst == 4u ? nh >> 24 : 0x80u | dst;
     if (a.nh)
         a.nh[i] = nh;
@@ -2142,6 +2250,12 @@ __device__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t ds
         atomicAdd(&a.bins[bin_of<CNDP_MODE_CNET>(old_nh, old_edge, 0, a.n_bins)], ~0ull); // -1
         atomicAdd(&a.bins[bin_of<CNDP_MODE_CNET>(nh, edge, 0, a.n_bins)], 1ull);
     }
+}
+
+__device__ __forceinline__ void spec_fix(const KArgs &a, uint64_t i, uint32_t own_l, uint32_t dst,
+                                         int *lbins = nullptr)
+{
+    spec_fix_v(a, i, own_l, dst, spec_fix_load(a, i, own_l, dst), lbins);
 }
 
 // one wave per burst: start state from the scan, types staged through LDS;
@@ -2236,14 +2350,20 @@ __global__ __launch_bounds__(256) void k_spec_emit(KArgs a, uint32_t B, uint64_t
 // Chunked speculation passes for graph bursts of B <= 256 packets (<= 64
 // groups, one group per lane): one wave per chunk of SPEC_CH bursts, the
 // chunk's types staged in LDS by one batch of loads.
-//   k_spec_ctables  the chunk's map (its bursts' maps composed), lane k =
+//   spec_ctable_chunk  the chunk's map (its bursts' maps composed), lane k =
 //                   signature class k -- the scans then run over chunks;
-//   k_spec_cemit    from the chunk's entering state, burst after burst: lane
+//   spec_cemit_chunk   from the chunk's entering state, burst after burst: lane
 //                   g finds the state entering group g, fixes its frames if
 //                   the group is quiet under it, and lane ng-1 hands the
 //                   burst's exit state to the next burst.
 // ---------------------------------------------------------------------------
-#define SPEC_CH 4 // measured: 4 beats 1 and 16 (occupancy vs per-wave latency)
+#define SPEC_CH SPEC_CH_K // measured: 4 beats 1 and 16 (occupancy vs per-wave latency)
+#ifndef SPEC_LQ
+#define SPEC_LQ 4 // chunks per wave of k_spec_local_t (grid-stride, next chunk prefetched; 4 beats 1, 2, 8)
+#endif
+#ifndef SPEC_WPB
+#define SPEC_WPB 4 // waves (chunks) per block of k_spec_local (measured: 4 beats 8 and 16)
+#endif
 
 // stage the types of bursts [c0, c1) as type | p_nxt << 16, burst j at
 // st + (j - c0) * spec_bstride(B) (16-B aligned groups for any B)
@@ -2345,26 +2465,13 @@ __device__ __forceinline__ bool spec_chunk_quiet(uint32_t sm, uint32_t s0)
     return !(sm >> 31) && (!(slot & 8u) || (slot & 7u) == cnet_edge(s0));
 }
 
-// gated: run only when k_spec_local left a chunk unresolved (meta[SPEC_FULL])
+// chunk c's map (lane k = signature class k) and its edge summary into T
 template <int CH>
-__global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B,
-                                                      uint64_t nb, uint64_t nch, const uint32_t *meta,
-                                                      const uint8_t *class_id, uint32_t *T, uint32_t gated)
+__device__ __forceinline__ void spec_ctable_chunk(const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t nb, uint64_t nch,
+                                  uint64_t c, uint32_t K, const uint32_t *meta, uint32_t *T, uint32_t *st,
+                                  const uint16_t *s_lut, const uint8_t *s_cls)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
-    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
-    __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    const uint32_t K = meta[0];
-    if (K > SPEC_KMAX || meta[SPEC_SKIP] || (gated && !meta[SPEC_FULL])) // block-uniform: before the barrier
-        return;
-    cnet_lut_fill(s_lut, threadIdx.x, 256);
-    spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
-    __syncthreads();
-    if (c >= nch)
-        return;
-    uint32_t *st = s_pt[wv];
+    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
     unsigned long long em = spec_stage_chunk<CH>(pt, n, B, c0, c1, lane, st, s_lut);
     const uint32_t sig = lane < K ? meta[1 + lane] : 0u;
@@ -2404,35 +2511,34 @@ __global__ __launch_bounds__(256) void k_spec_ctables(const uint16_t *__restrict
 template <int CH>
 __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
                             const uint32_t *st);
-
 template <int CH>
-__global__ __launch_bounds__(256) void k_spec_cemit(KArgs a, uint32_t B, uint64_t nb, uint64_t nch,
-                                                    const uint32_t *meta, const uint8_t *class_id, const uint32_t *P,
-                                                    const uint32_t *Sblk, const uint32_t *S, const uint32_t *T,
-                                                    uint32_t kfast, uint32_t kmax, const uint8_t *done)
+__device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
+                                                 uint32_t lane, const uint32_t *st, uint32_t &fm, uint32_t &fe);
+template <int CH>
+__device__ __forceinline__ void spec_replay_fix(const KArgs &a, uint32_t B, uint64_t c0, uint32_t lane,
+                                                const uint32_t *st, uint32_t fm, uint32_t fe);
+
+// replay chunk c from its entering state (the scan's block start, then the
+// block's earlier chunks) unless its summary says no frame can move
+template <int CH>
+__device__ __forceinline__ void spec_cemit_chunk(const KArgs &a, uint32_t B, uint64_t nb, uint64_t nch, uint64_t c,
+                                 const uint32_t *meta, const uint32_t *P, const uint32_t *Sblk, const uint32_t *S,
+                                 const uint32_t *T, uint32_t kfast, uint32_t kmax, uint32_t *st,
+                                 const uint16_t *s_lut)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
-    __shared__ __attribute__((aligned(16))) uint16_t s_lut[4][CNET_LUT_N]; // per wave: filled only by the waves that replay
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    // done != nullptr: k_spec_local ran first; only the chunks it left unresolved
-    if (c >= nch || meta[SPEC_SKIP] || (done && (!meta[SPEC_FULL] || (!meta[SPEC_NOLOCAL] && done[c]))))
-        return;
-    uint32_t *st = s_pt[wv];
+    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
     uint32_t s0;
     if (meta[0] > kmax) {
         s0 = S[c0];
-    } else { // chunk start state: the block's start, then the block's earlier chunks
+    } else {
         const uint64_t blk = c / SPEC_BLK;
         s0 = spec_enter(P, c, spec_kf(meta[0], kfast), Sblk[blk]);
     }
-    // k_spec_ctables wrote the chunk's summary
+    // spec_ctable_chunk wrote the chunk's summary
     if (meta[0] <= SPEC_KMAX && spec_chunk_quiet(T[nch * SPEC_KMAX + c], s0))
         return; // no frame of this chunk can leave by another edge
-    cnet_lut_fill(s_lut[wv], lane, 64);
-    __builtin_amdgcn_wave_barrier();
-    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut[wv]);
+    spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
     spec_replay<CH>(a, B, c0, c1, s0, lane, st);
 }
 
@@ -2443,6 +2549,19 @@ template <int CH>
 __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
                             const uint32_t *st)
 {
+    uint32_t fm, fe;
+    spec_replay_walk<CH>(a, B, c0, c1, s0, lane, st, fm, fe);
+    spec_replay_fix<CH>(a, B, c0, lane, st, fm, fe);
+}
+
+// the walk: fm = frames to fix (bit 4 * burst + j), fe = each burst's edge (3 bits)
+template <int CH>
+__device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
+                                                 uint32_t lane, const uint32_t *st, uint32_t &fm, uint32_t &fe)
+{
+    static_assert(CH <= 8, "fix masks: 4 frames and 3 edge bits per burst");
+    fm = 0;
+    fe = 0;
     for (uint64_t bb = c0; bb < c1; bb++) {
         const uint32_t *sb = st + (bb - c0) * spec_bstride(B);
         const uint64_t b0 = bb * B;
@@ -2475,15 +2594,39 @@ __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t
             nxt = cur;
             if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || e == (x.w >> 16)))
                 nxt = x.w & 0xffffu;
-            if (quiet) { // the group goes whole to p_nxt[state]
+            if (quiet) { // the group goes whole to p_nxt[state]: mark the frames that move
                 const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++)
-                    if ((xs[j] >> 16) != e)
-                        spec_fix(a, b0 + lane * 4u + j, xs[j] & 0xffffu, e);
+                    fm |= (uint32_t)((xs[j] >> 16) != e) << (4u * (uint32_t)(bb - c0) + j);
+                fe |= e << (3u * (uint32_t)(bb - c0));
             }
         }
         s0 = ng ? __shfl(nxt, (int)ng - 1) : s0;
+    }
+}
+
+// the fixes after the walk, a burst at a time: its reads first, then its
+// writes (bursts without a fix cost nothing)
+template <int CH>
+__device__ __forceinline__ void spec_replay_fix(const KArgs &a, uint32_t B, uint64_t c0, uint32_t lane,
+                                                const uint32_t *st, uint32_t fm, uint32_t fe)
+{
+#pragma unroll 1
+    for (uint32_t bq = 0; bq < (uint32_t)CH; bq++) {
+        const uint32_t m4 = (fm >> (4u * bq)) & 0xfu, dst = (fe >> (3u * bq)) & 7u;
+        if (__ballot(m4 != 0u) == 0ull)
+            continue;
+        const uint32_t *sg = st + bq * spec_bstride(B) + lane * 4u;
+        const uint64_t i0 = (c0 + bq) * B + lane * 4u;
+        uint32_t v[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            v[j] = (m4 >> j) & 1u ? spec_fix_load(a, i0 + j, sg[j] & 0xffffu, dst) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            if ((m4 >> j) & 1u)
+                spec_fix_v(a, i0 + j, sg[j] & 0xffffu, dst, v[j], nullptr);
     }
 }
 
@@ -2577,7 +2720,7 @@ __device__ __forceinline__ void spec_flag_full(uint32_t *meta)
         __hip_atomic_store(&meta[SPEC_FULL], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// uniform batch (k_spec_classes): every frame of a full group of bursts
+// uniform batch (spec_classes): every frame of a full group of bursts
 // [c0, c1) leaves by edge E, the entering state's p_nxt; fix those whose own
 // edge differs.  Tail frames (a burst's last cnt % 4) keep their own edge.
 // A wave takes one chunk and issues all its type loads (16 B = 8 types
@@ -2597,7 +2740,7 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
         const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
         v[r] = vec && i0 + 8u <= p1 ? *(const u32x4 *)(a.spec_t16 + i0) : (u32x4){0, 0, 0, 0};
     }
-    // B <= 256 here (k_spec_classes), so a wave's range is <= U * 512 types
+    // B <= 256 here (spec_classes), so a wave's range is <= U * 512 types
 #pragma unroll
     for (uint32_t r = 0; r < U; r++) {
         const uint32_t i0 = p0 + (r * 64u + lane) * 8u;
@@ -2633,26 +2776,72 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
     }
 }
 
+// a chunk whose entering state s0 is known, from its types: the edge
+// summary from registers (16-B loads of 8 when the bursts allow), then --
+// when a frame could leave by another edge -- staged in LDS and replayed
 template <int CH>
-__global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+__device__ __forceinline__ void spec_chunk_types(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
+                                                 uint32_t lane, uint32_t *st, const uint16_t *s_lut)
+{
+    if ((B & 7u) != 0) {
+        const unsigned long long em = spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
+        if (!spec_chunk_quiet(spec_summary(em), s0))
+            spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+        return;
+    }
+    constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+    const uint64_t p0 = c0 * B, p1 = c1 * B < a.n ? c1 * B : a.n;
+    const uint32_t m = (uint32_t)(p1 - p0);
+    u32x4 v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+        const uint32_t idx = (r * 64u + lane) * 8u;
+        v[r] = idx + 8u <= m ? *(const u32x4 *)(a.spec_t16 + p0 + idx) : (u32x4){0, 0, 0, 0};
+    }
+    unsigned long long em = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < R; r++) {
+        const uint32_t idx = (r * 64u + lane) * 8u;
+        if (idx >= m)
+            continue;
+        uint32_t w[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+        if (idx + 8u > m) // the batch's last partial vector
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t lo = idx + 2 * q < m ? a.spec_t16[p0 + idx + 2 * q] : 0u;
+                const uint32_t hi = idx + 2 * q + 1 < m ? a.spec_t16[p0 + idx + 2 * q + 1] : 0u;
+                w[q] = lo | (hi << 16);
+            }
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++)
+            if (idx + q < m)
+                em |= 1ull << (cnet_lut_x(s_lut, (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu) & 63u);
+    }
+    if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0)) {
+        spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
+        spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+    }
+}
+
+template <int CH, int WPB>
+__global__ __launch_bounds__(WPB * 64) void k_spec_local(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
                                                     uint8_t *done)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_pt[4][CH * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pt[WPB][CH * 256];
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    const uint64_t c = (uint64_t)blockIdx.x * WPB + wv;
     if (meta[SPEC_UNIF]) { // block-uniform; wave c takes chunks [c*W, c*W + W), the rest return
         const uint64_t u0 = c * CH, u1 = u0 + CH;
-        static_assert(4 * CH * 256 >= CNDP_BINS_MAX + 2, "bin counters must fit the staging tile");
+        static_assert(WPB * CH * 256 >= CNDP_BINS_MAX + 2, "bin counters must fit the staging tile");
         int *lbins = (int *)&s_pt[0][0]; // n_bins + 2 <= CNDP_BINS_MAX + 2 ints fit the staging tile
         const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
-        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+        for (uint32_t k = threadIdx.x; k < nb2; k += WPB * 64u)
             lbins[k] = 0;
         __syncthreads();
         if (u0 < nb)
             spec_uniform_range<CH>(a, B, u0, u1 < nb ? u1 : nb, lane, meta[SPEC_IN] & 0xffffu, lbins);
         __syncthreads();
-        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+        for (uint32_t k = threadIdx.x; k < nb2; k += WPB * 64u)
             if (lbins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)(long long)lbins[k]);
         return;
@@ -2679,7 +2868,7 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
         const uint64_t b0 = (c0 - 1) * B; // a full burst: only the batch's last burst is short
         spec_group_regs(a.spec_t16, b0, B, lane, pq0, pq1);
     }
-    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    cnet_lut_fill(s_lut, threadIdx.x, WPB * 64);
     __syncthreads();
     if (c >= nch)
         return;
@@ -2731,6 +2920,262 @@ __global__ __launch_bounds__(256) void k_spec_local(KArgs a, uint32_t B, uint64_
     }
     if (lane == 0)
         done[c] = 1;
+}
+
+// k_spec_local over the main kernel's tile words (k_cnet_defer wrote one per
+// 64 frames; spec_canon).  The pass is latency-bound -- a few dependent loads
+// per wave, next to no traffic -- and the types of a chunk are read only when
+// its tiles cannot rule out a re-routed frame:
+//   uniform batch  the wave's share of tiles: a canonical tile's frames all
+//                  have spec_canon(T), so when that is E only the other tiles
+//                  are looked at (frame by frame); otherwise every chunk goes
+//                  through spec_uniform_range as without tile words;
+//   otherwise      per chunk: the entering state from the look-back, then
+//                  quiet when every tile is canonical and the state agrees
+//                  with its low byte's common edge (or has another low byte).
+// Any grid is correct (chunks and tiles are strided over the waves): the host
+// sizes it from the previous call's hint -- one chunk per wave, or a small
+// grid when that call was a uniform batch.
+
+// chunk c's tile words (lane < tiles covering it: <= 17 for B <= 256) and
+// the burst before it (its groups, one per lane)
+__device__ __forceinline__ void spec_chunk_pre(const KArgs &a, uint32_t B, uint64_t nch, uint64_t c, uint32_t lane,
+                                               uint32_t &tw, uint32_t &pq0, uint32_t &pq1)
+{
+    tw = 1u;
+    pq0 = pq1 = 0u;
+    if (c < nch) {
+        const uint64_t p0 = c * SPEC_CH * B, e1 = (c + 1) * SPEC_CH * B, p1 = e1 < a.n ? e1 : a.n;
+        const uint64_t tl0 = p0 >> 6, ntl = ((p1 - 1) >> 6) - tl0 + 1;
+        if (lane < ntl)
+            tw = a.spec_tile[tl0 + lane];
+        if (c > 0) // a full burst: only the batch's last burst is short
+            spec_group_regs(a.spec_t16, (c * SPEC_CH - 1) * B, B, lane, pq0, pq1);
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+                                                      uint8_t *done, uint32_t *R)
+{
+    static_assert(CH == SPEC_CH, "spec_chunk_pre");
+    __shared__ int s_bins[CNDP_BINS_MAX + 2]; // the uniform pass's bin moves
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    // wave-uniform in SGPRs (the chunk index and all that derives from it)
+    const uint64_t wid = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wv), W = (uint64_t)gridDim.x * 4;
+    const uint32_t unif = meta[SPEC_UNIF], s_in = meta[SPEC_IN] & 0xffffu;
+    if (unif) { // block-uniform
+        const uint32_t T = s_in, E = cnet_edge(T);
+        const bool tcan = spec_canon(T & 0xffu) == E;
+        const uint64_t n_tiles = ((uint64_t)a.n + 63u) >> 6, tpw = (n_tiles + W - 1) / W;
+        const uint64_t t_lo = wid * tpw, t_hi = t_lo + tpw < n_tiles ? t_lo + tpw : n_tiles;
+        // the tile words of the wave's first 64 tiles, before the barrier
+        uint32_t tw = tcan && t_lo + lane < t_hi ? a.spec_tile[t_lo + lane] : 0u;
+        int *lbins = s_bins;
+        const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            lbins[k] = 0;
+        __syncthreads();
+        if (tcan) {
+            for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
+                if (t0 != t_lo)
+                    tw = t0 + lane < t_hi ? a.spec_tile[t0 + lane] : 1u;
+                unsigned long long m = __ballot(t0 + lane < t_hi && tw == 0u);
+                while (m) { // the few other tiles: the wave takes their frames one per lane
+                    const uint32_t k = (uint32_t)__ffsll(m) - 1u;
+                    m &= m - 1ull;
+                    const uint64_t i = (t0 + k) * 64u + lane;
+                    if (i < a.n) {
+                        const uint32_t l = a.spec_t16[i];
+                        const uint64_t b0 = i / B * B, bend = b0 + B < a.n ? b0 + B : a.n;
+                        if (cnet_edge(l) != E && b0 + ((i - b0) & ~3ull) + 4u <= bend) // a full group
+                            spec_fix(a, i, l, E, lbins);
+                    }
+                }
+            }
+        } else {
+            for (uint64_t c = wid; c < nch; c += W) {
+                const uint64_t u0 = c * CH, u1 = u0 + CH < nb ? u0 + CH : nb;
+                spec_uniform_range<CH>(a, B, u0, u1, lane, T, lbins);
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            if (lbins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)(long long)lbins[k]);
+        return;
+    }
+    uint32_t tw, pq0, pq1;
+    spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
+    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    __syncthreads();
+    if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL])
+        return;
+    for (uint64_t c = wid; c < nch; c += W) {
+        const uint32_t ctw = tw, cq0 = pq0, cq1 = pq1;
+        spec_chunk_pre(a, B, nch, c + W, lane, tw, pq0, pq1); // the next chunk's loads, in flight meanwhile
+        const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+        if (c == nch - 1) { // the final node state (meta[-1]; the entering one is meta[SPEC_IN])
+            uint32_t sf = 0;
+            if (spec_lookback(a.spec_t16, a.n, B, c0, c1, lane, s_lut, sf)) {
+                if (lane == 0)
+                    meta[-1] = sf;
+            } else if (lane == 0) {
+                spec_flag_full(meta);
+            }
+        }
+        const bool odd = __ballot(ctw == 0u) != 0ull; // a non-canonical tile
+        uint32_t s0 = s_in;
+        if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, cq0, cq1)) {
+            if (lane == 0) {
+                done[c] = 0;
+                spec_flag_full(meta);
+            }
+            continue;
+        }
+        const uint32_t cn = spec_canon(s0 & 0xffu);
+        if (odd || (cn != 0xFFu && cn != cnet_edge_l(s_lut, s0))) {
+            // its types decide: k_spec_fallback reads them (and replays) from
+            // the list, so this kernel carries no replay code (occupancy)
+            if (lane == 0) {
+                const uint32_t x = blockIdx.x & 7u, k = atomicAdd(&meta[SPEC_RCNT + 32 * x], 1u);
+                R[x * 2 * nch + 2 * k] = (uint32_t)c;
+                R[x * 2 * nch + 2 * k + 1] = s0;
+            }
+        }
+        if (lane == 0)
+            done[c] = 1;
+    }
+}
+
+// Grid barrier of k_spec_fallback: bar[0] counts arrivals (monotonic within a
+// launch), bar[1] is the generation the last arriver publishes; spec_classes
+// zeroes both every call.  Each wave's stores are drained, then lane 0
+// releases, arrives, polls (relaxed sc1 loads + s_sleep) and acquires
+// (MI355X_MICROARCH.md barrier-counter).  The grid is one block per CU, so
+// every block is resident; the poll is bounded all the same (meta[SPEC_ERR]
+// records an expiry: a wrong result, not a hung GPU).
+#define SPEC_ERR 134
+__device__ __forceinline__ void spec_grid_sync(uint32_t *bar, uint32_t gen, uint32_t *meta)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t old = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gen * gridDim.x - 1u) {
+            __hip_atomic_store(&bar[1], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (uint32_t it = 0; __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen; it++) {
+                if (it == (1u << 22)) { // ~0.2 s
+                    __hip_atomic_store(&meta[SPEC_ERR], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
+// The general resolution, for what k_spec_local leaves (meta[SPEC_FULL]) or
+// for everything (gated == 0, CNDP_TUNE_SPEC_SCAN forced): one persistent
+// launch, one block of 4 waves per CU, three phases split by grid barriers --
+//   tables  every chunk's map over the signature classes and its summary,
+//   scan    the chunk maps composed (blocks of SPEC_BLK chunks, then block 0
+//           composes the block totals into block start states and the final
+//           node state; more than SPEC_KMAX classes: block 0's thread 0
+//           walks the bursts in order instead),
+//   replay  each chunk k_spec_local did not resolve, from its entering state.
+// With nothing left to resolve it returns at once (one launch of ~256 empty
+// blocks instead of three gated launches).
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+                                                       const uint8_t *class_id, uint32_t *T, uint32_t *P,
+                                                       uint32_t *Bt, uint32_t *Sblk, uint32_t *S, const uint8_t *done,
+                                                       uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated,
+                                                       const uint32_t *R)
+{
+    // the scan's rows; the tables / replay staging reuse the same bytes
+    __shared__ __attribute__((aligned(16))) uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
+    __shared__ uint32_t s_carry[SPEC_KMAX];
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
+    static_assert(SPEC_BLK * (SPEC_KMAX + 1) >= 4 * CH * 256, "staging fits the scan rows");
+    uint32_t rc[8], nrep = 0; // the 8 replay lists (k_spec_local_t)
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        rc[x] = gated ? meta[SPEC_RCNT + 32 * x] : 0u;
+        nrep += rc[x];
+    }
+    const bool full = !gated || meta[SPEC_FULL];
+    if (meta[SPEC_SKIP] || (!full && nrep == 0)) // grid-uniform
+        return;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t K = meta[0];
+    uint32_t *st = s_m + wv * (CH * 256);
+    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
+    __syncthreads();
+    const uint64_t W = (uint64_t)gridDim.x * 4, wid = (uint64_t)blockIdx.x * 4 + wv;
+    // the chunks k_spec_local_t listed (their entering states known): types,
+    // then a replay where a frame can move -- before the full passes, which
+    // leave these chunks alone (done[c] = 1)
+    for (uint64_t k = wid; k < nrep; k += W) {
+        uint32_t x = 0, j = (uint32_t)k; // entry j of list x
+        while (j >= rc[x]) // uniform
+            j -= rc[x++];
+        const uint32_t *e = R + x * 2 * nch + 2 * j;
+        const uint64_t c = e[0], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+        spec_chunk_types<CH>(a, B, c0, c1, e[1], lane, st, s_lut);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (!full)
+        return;
+    __syncthreads(); // the staging rows become the scan's
+    if (K <= SPEC_KMAX)
+        for (uint64_t c = (uint64_t)blockIdx.x * 4 + wv; c < nch; c += W) {
+            spec_ctable_chunk<CH>(a.spec_t16, a.n, B, nb, nch, c, K, meta, T, st, s_lut, s_cls);
+            __builtin_amdgcn_wave_barrier();
+        }
+    spec_grid_sync(bar, 1, meta);
+    const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
+    for (uint64_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+        if (K <= kfast)
+            spec_scan_a_body<SPEC_KFAST>(s_m, nch, K, T, P, Bt, vb);
+        else if (K <= kmax)
+            spec_scan_a_body<SPEC_KMAX>(s_m, nch, K, T, P, Bt, vb);
+        __syncthreads();
+    }
+    spec_grid_sync(bar, 2, meta);
+    if (blockIdx.x == 0) {
+        uint32_t *state = meta - 1;
+        if (K <= kfast) {
+            spec_scan_c_body<SPEC_KFAST, SPEC_BLK>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+        } else if (K <= kmax) {
+            spec_scan_c_body<SPEC_KMAX, SPEC_BLK>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+        } else if (threadIdx.x == 0) {
+            uint32_t s = meta[SPEC_IN] & 0xffffu;
+            for (uint64_t b = 0; b < nb; b++) {
+                S[b] = s;
+                const uint64_t b0 = b * B;
+                const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
+                const uint32_t m = spec_burst_map(a.spec_t16, b0, cnt, spec_sig(s), false);
+                if (m != SPEC_UNCH)
+                    s = m;
+            }
+            *state = s;
+        }
+    }
+    spec_grid_sync(bar, 3, meta);
+    const bool all = !gated || meta[SPEC_NOLOCAL];
+    for (uint64_t c = (uint64_t)blockIdx.x * 4 + wv; c < nch; c += W) {
+        if (all || !done[c])
+            spec_cemit_chunk<CH>(a, B, nb, nch, c, meta, P, Sblk, S, T, kfast, kmax, st, s_lut);
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2955,6 +3400,9 @@ struct cndp_gpu_ctx {
     uint8_t *sp_class;    // class id per signature (2048)
     uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U; // sp_pt: the u16 types (speculation model)
     uint8_t *sp_done;     // per chunk: resolved by k_spec_local
+    uint32_t *sp_R;       // chunks k_spec_local_t leaves to k_spec_fallback: (chunk, entering state)
+    uint8_t *sp_tile;     // per 64-frame tile: the main kernel's canonical-tile word
+    uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch uniform
     uint64_t sp_n_cap, sp_b_cap;
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
     hipStream_t hs[3];    // copy-in, classify, copy-out
@@ -3121,10 +3569,12 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         hipFree(c->m_dres);
     if (c->d_rw_tbl)
         hipFree(c->d_rw_tbl);
-    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt, c->sp_nh, c->sp_S, c->sp_T, c->sp_U, c->sp_done};
+    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt, c->sp_nh, c->sp_S, c->sp_T, c->sp_U, c->sp_done, c->sp_tile, c->sp_R};
     for (void *q : sp)
         if (q)
             hipFree(q);
+    if (c->sp_hint)
+        hipHostFree(c->sp_hint);
     if (c->d_ttab)
         hipFree(c->d_ttab);
     if (c->d_reta)
@@ -3594,20 +4044,27 @@ static int validate_batch(const cndp_gpu_ctx_t *c, const struct cndp_batch *b)
 static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
 {
     if (!c->sp_small) {
-        HIP_TRY(hipMalloc((void **)&c->sp_small, 256 * 4));
-        HIP_TRY(hipMemset(c->sp_small, 0, 256 * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_small, 1024 * 4));
+        HIP_TRY(hipMemset(c->sp_small, 0, 1024 * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_class, 2048));
+        HIP_TRY(hipHostMalloc((void **)&c->sp_hint, 64, hipHostMallocMapped));
+        memset(c->sp_hint, 0, 64);
+        HIP_TRY(hipHostGetDevicePointer((void **)&c->sp_hint_d, c->sp_hint, 0));
     }
     if (n > c->sp_n_cap) {
         if (c->sp_pt)
             HIP_TRY(hipFree(c->sp_pt));
         if (c->sp_nh)
             HIP_TRY(hipFree(c->sp_nh));
+        if (c->sp_tile)
+            HIP_TRY(hipFree(c->sp_tile));
         c->sp_pt = c->sp_nh = nullptr;
+        c->sp_tile = nullptr;
         c->sp_n_cap = 0;
         const uint64_t cap = n + (n >> 3) + 1024;
         HIP_TRY(hipMalloc((void **)&c->sp_pt, cap * 2));
         HIP_TRY(hipMalloc((void **)&c->sp_nh, cap * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_tile, cap / 64 + 1));
         c->sp_n_cap = cap;
     }
     if (nb > c->sp_b_cap) {
@@ -3619,12 +4076,15 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
             HIP_TRY(hipFree(c->sp_U));
         if (c->sp_done)
             HIP_TRY(hipFree(c->sp_done));
-        c->sp_S = c->sp_T = c->sp_U = nullptr;
+        if (c->sp_R)
+            HIP_TRY(hipFree(c->sp_R));
+        c->sp_S = c->sp_T = c->sp_U = c->sp_R = nullptr;
         c->sp_done = nullptr;
         c->sp_b_cap = 0;
         const uint64_t cap = nb + (nb >> 3) + 64;
         HIP_TRY(hipMalloc((void **)&c->sp_S, cap * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_done, cap));
+        HIP_TRY(hipMalloc((void **)&c->sp_R, cap * 16 * 4)); // 8 lists of (chunk, state), chunks <= cap
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
         // inclusive burst prefixes + block totals + block start states
         HIP_TRY(hipMalloc((void **)&c->sp_U, (cap * SPEC_KMAX + (cap / SPEC_BLK + 2) * (SPEC_KMAX + 1)) * 4));
@@ -3716,9 +4176,18 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             a.spec_t16 = (uint16_t *)c->sp_pt;
             a.spec_nh = c->sp_nh;
             a.spec_flags = c->sp_small + 66;
-            if (!c->sf_clean) // k_spec_classes of the previous call clears them
+            if (!c->sf_clean) // spec_classes of the previous call clears them
                 HIP_TRY(hipMemsetAsync(a.spec_flags, 0, 64 * 4, s));
             c->sf_clean = 0;
+            // sp_small: [0] node state, [1..] meta, [66..129] flags, [140] k_spec_scan's
+            // ticket, [142..143] k_spec_fallback's barrier, [512 + 32 g] k_classify_cnet's tickets
+            a.spec_meta = c->sp_small + 1;
+            a.spec_cls = c->sp_class;
+            a.spec_ticket = c->sp_small + 512;
+            a.spec_bar = c->sp_small + 142;
+            a.spec_B = B;
+            a.spec_allow = c->tune_spec_scan == 0 ? 1u : 0u;
+            a.spec_hint = c->sp_hint_d;
         }
         // the deferred kernel indexes frames in 32 bits (t * 64 + lane < 2^32)
         if (c->tune_cnet_tile && b->n <= 0xFFFFFF00u) {
@@ -3735,7 +4204,7 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             }
             a.wl_n = c->cs_wl;
             a.wl = c->cs_wl + 1;
-            if (!c->wl_clean) // else k_spec_classes of the previous call cleared it
+            if (!c->wl_clean) // else spec_classes of the previous call cleared it
                 HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
             c->wl_clean = 0;
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
@@ -3748,6 +4217,7 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                                                                 {k_cnet_defer<true, false>,
                                                                  k_cnet_defer<true, true>}};
             const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
+            a.spec_tile = B ? c->sp_tile : nullptr; // written by this kernel only
             hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
                                0, s, a, (uint32_t)n_tiles);
             hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
@@ -3756,39 +4226,36 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
         }
         if (B) {
             const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
-            uint32_t *state = c->sp_small, *meta = c->sp_small + 1, *flags = c->sp_small + 66;
+            uint32_t *state = c->sp_small, *meta = c->sp_small + 1;
             uint32_t *ticket = c->sp_small + 140; // k_spec_scan's arrival count (0 between launches)
-            hipLaunchKernelGGL(k_spec_classes, dim3(1), dim3(64), 0, s, flags, c->sp_class, meta,
-                               (const uint16_t *)a.spec_t16, b->n, B, nb, (uint32_t)(c->tune_spec_scan == 0),
-                               a.wl_n);
-            c->sf_clean = 1;
+            c->sf_clean = 1; // spec_classes (k_classify_cnet's last block) clears them
             c->wl_clean = a.wl_n != nullptr;
             const uint32_t gw = (uint32_t)((nb + 3) / 4); // one wave per burst
             const uint32_t kfast = c->tune_spec_scan == 0 ? SPEC_KFAST : 0u;
             const uint32_t kmax = c->tune_spec_scan == 2 ? 0u : SPEC_KMAX;
             if (B <= 256) { // chunked passes (SPEC_CH bursts per wave)
                 const uint64_t nch = (nb + SPEC_CH - 1) / SPEC_CH;
-                const uint32_t gc = (uint32_t)((nch + 3) / 4);
-                auto ct = k_spec_ctables<SPEC_CH>;
-                auto ce = k_spec_cemit<SPEC_CH>;
-                // auto mode: the local pass first, the full passes only for what it leaves
+                // auto mode: the local pass first, the general one only for what it leaves
                 const uint32_t gated = c->tune_spec_scan == 0 ? 1u : 0u;
-                if (gated) {
-                    auto lo = k_spec_local<SPEC_CH>;
-                    hipLaunchKernelGGL(lo, dim3(gc), dim3(256), 0, s, a, B, nb, nch, meta, c->sp_done);
+                if (gated && a.spec_tile) { // the main kernel wrote tile words
+                    auto lo = k_spec_local_t<SPEC_CH>;
+                    uint32_t gl = (uint32_t)((nch + 4 * SPEC_LQ - 1) / (4 * SPEC_LQ)); // SPEC_LQ chunks per wave
+                    // the previous call was a uniform batch: a wave per 64+ tiles
+                    if (c->sp_hint && ((volatile uint32_t *)c->sp_hint)[1] && gl > (uint32_t)c->num_cu * 4u)
+                        gl = (uint32_t)c->num_cu * 4u;
+                    hipLaunchKernelGGL(lo, dim3(gl), dim3(256), 0, s, a, B, nb, nch, meta, c->sp_done, c->sp_R);
+                } else if (gated) {
+                    auto lo = k_spec_local<SPEC_CH, SPEC_WPB>;
+                    const uint32_t gl = (uint32_t)((nch + SPEC_WPB - 1) / SPEC_WPB);
+                    hipLaunchKernelGGL(lo, dim3(gl), dim3(SPEC_WPB * 64), 0, s, a, B, nb, nch, meta, c->sp_done);
                 }
-                hipLaunchKernelGGL(ct, dim3(gc), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B, nb, nch,
-                                   (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T, gated);
                 const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
                 uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
-                hipLaunchKernelGGL(k_spec_scan, dim3((uint32_t)nblk), dim3(SPEC_BLK), 0, s, nch,
-                                   (const uint32_t *)meta, (const uint32_t *)c->sp_T, P, Bt,
-                                   (const uint8_t *)c->sp_class, Sblk, state, ticket,
-                                   (const uint16_t *)a.spec_t16, b->n, B, nb, c->sp_S, kfast, kmax, gated);
-                hipLaunchKernelGGL(ce, dim3(gc), dim3(256), 0, s, a, B, nb, nch, (const uint32_t *)meta,
-                                   (const uint8_t *)c->sp_class, (const uint32_t *)P, (const uint32_t *)Sblk,
-                                   (const uint32_t *)c->sp_S, (const uint32_t *)c->sp_T, kfast, kmax,
-                                   gated ? (const uint8_t *)c->sp_done : (const uint8_t *)nullptr);
+                auto fb = k_spec_fallback<SPEC_CH>;
+                hipLaunchKernelGGL(fb, dim3((uint32_t)c->num_cu), dim3(256), 0, s, a, B, nb, nch, meta,
+                                   (const uint8_t *)c->sp_class, c->sp_T, P, Bt, Sblk, c->sp_S,
+                                   (const uint8_t *)c->sp_done, a.spec_bar, kfast, kmax, gated,
+                                   (const uint32_t *)c->sp_R);
             } else {
                 hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);

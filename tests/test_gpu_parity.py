@@ -847,6 +847,39 @@ def test_cnet_speculation_local_and_full(cnet, gpu):
         ccl.set_tuning(cnet_spec=256, spec_scan=0)
 
 
+def test_cnet_speculation_fallback_grid(cnet, gpu):
+    """The general resolution (k_spec_fallback) over a batch big enough that
+    every block of its persistent grid takes several chunks and the scan
+    runs over several blocks of chunks: 2M frames, single-type runs every
+    ~64K frames leave chunks to it.  Auto and forced-full == the node loop;
+    chained calls too (the final state it walks)."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    n = 1 << 21
+    fr = _gtp_mix(n, routes, v6, gpu, seed=77)
+    plain = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)
+    pick = int(np.flatnonzero(plain["ptype"] == 0x0211)[0])
+    off = fr.offsets.clone()
+    for lo in range(5000, n - 4096, 65536):
+        off[lo:lo + 2048 + (lo % 977)] = off[pick]
+    off[n - 3000:] = off[pick]  # the batch ends inside a run: the final state from the scan
+    fr = pktgen.Frames(fr.slab, n, offsets=off)
+    try:
+        for scan in (0, 1):
+            ccl.set_tuning(cnet_spec=256, spec_scan=scan)  # also resets the node state
+            st = np.zeros(1, np.uint16)
+            cut = (n // 2) // 256 * 256
+            for lo, hi in ((0, cut), (cut, n)):
+                part = pktgen.Frames(fr.slab, hi - lo, offsets=fr.offsets[lo:hi].contiguous())
+                ref = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=256,
+                                      spec_state=st)
+                o = ccl.alloc_outputs(part.n, 64, device=gpu, meta=True)
+                ccl.classify(part, N.CNDP_MODE_CNET, out=o)
+                torch.cuda.synchronize()
+                assert_same(o, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_scan=0)
+
+
 def test_cnet_speculation_many_signatures(cnet, gpu):
     """Fuzz frames give ~21 distinct ptype signatures: more than the 8-entry
     maps hold, so the scans run 64-entry maps; the forced sequential walk

@@ -1,8 +1,10 @@
-"""Print our kernels' rocprofv3 --stats rows (diagnostic): python tools/kstats.py <run_kernel_stats.csv>"""
+"""Print this library's kernels from rocprofv3 --stats csv files (avg / min / max µs)."""
 import csv
 import sys
 
-for r in csv.DictReader(open(sys.argv[1])):
-    n = r["Name"]
-    if n.startswith("k_") or n.startswith("void k_"):
-        print(f"{n[:60]:60s} calls {r['Calls']:>5s} avg {float(r['AverageNs']) / 1e3:9.2f} us")
+for p in sys.argv[1:]:
+    print("==", p)
+    for r in csv.DictReader(open(p)):
+        if " k_" in " " + r["Name"].replace("void ", " "):
+            print(f"  {r['Name'][:60]:60s} calls={r['Calls']:>4s} avg={float(r['AverageNs']) / 1e3:8.2f} "
+                  f"min={float(r['MinNs']) / 1e3:8.2f} max={float(r['MaxNs']) / 1e3:8.2f}")
