@@ -880,6 +880,32 @@ def test_cnet_speculation_fallback_grid(cnet, gpu):
         ccl.set_tuning(cnet_spec=256, spec_scan=0)
 
 
+def test_cnet_speculation_launch_hint(cnet, gpu):
+    """The local pass's grid is sized from the previous call's hint (a
+    uniform batch shrinks it); a mixed batch right after uniform ones then
+    runs on the small grid, every wave striding over several chunks.  Each
+    call == the node loop from the state the previous call left."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    n = 1 << 20
+    uni = pktgen.packed_ipv4(n, routes=routes, device=gpu, seed=3)
+    rows = uni.slab.view(uni.n, uni.stride)
+    rows[:, 36] = 0x12
+    sel = (torch.arange(uni.n, device=gpu) % 4099) == 17
+    rows[sel, 36], rows[sel, 37] = 0x08, 0x68  # GTP-U: same low byte, another edge
+    mixed = _gtp_mix(n, routes, v6, gpu, seed=5)
+    try:
+        ccl.set_tuning(cnet_spec=256)  # resets the node state
+        st = np.zeros(1, np.uint16)
+        for fr in (uni, uni, uni, mixed, uni, mixed):
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=256, spec_state=st)
+            o = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+            ccl.classify(fr, N.CNDP_MODE_CNET, out=o)
+            torch.cuda.synchronize()
+            assert_same(o, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_scan=0)
+
+
 def test_cnet_speculation_many_signatures(cnet, gpu):
     """Fuzz frames give ~21 distinct ptype signatures: more than the 8-entry
     maps hold, so the scans run 64-entry maps; the forced sequential walk
