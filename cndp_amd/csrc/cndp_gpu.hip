@@ -1363,6 +1363,18 @@ __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
 // the window loads of the tile two ahead, so the in-order vmcnt waits of the
 // chain only ever include loads issued a trip earlier.
 // ---------------------------------------------------------------------------
+// element i of a per-frame output through a 32-bit byte offset (a scalar base
+// + zero-extended VGPR offset: one store, no 64-bit address per lane); the
+// deferred kernel runs only for n < 2^30, so i * 4 fits
+__device__ __forceinline__ uint32_t &at32(uint32_t *p, uint32_t i)
+{
+    return *(uint32_t *)((char *)p + (uint32_t)(i << 2));
+}
+__device__ __forceinline__ uint16_t &at16(uint16_t *p, uint32_t i)
+{
+    return *(uint16_t *)((char *)p + (uint32_t)(i << 1));
+}
+
 struct CsOff { // this lane's frame offsets for tiles t, t+1, t+2 and the load for t+3
     uint64_t o0, o1, o2, o3;
 };
@@ -1521,41 +1533,36 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 na.h ^= tz4(s_t, 4 * k, u);
             }
         }
-        if (f4) {
-            const uint32_t dst = alignb(W[8], W[7], 2);
-            if (pe == 3u || a.spec_nh) { // ip4_input.c:121-140
-                uint32_t sum = 0;
+        // both families' input-node pieces, straight-line, then selects: the
+        // waves of an IMIX batch hold both families, and a branch per family
+        // ran both bodies anyway (plus the exec-mask saves and zero fills)
+        const bool do4 = f4 & ((pe == 3u) | (a.spec_nh != nullptr)); // ip4_input.c:121-140
+        const bool do6 = !f4 & ((pe == 4u) | (a.spec_nh != nullptr)); // ip6_input.c:115-135
+        const uint32_t dst = alignb(W[8], W[7], 2);
+        uint32_t sum = 0;
 #pragma unroll
-                for (int k = 0; k < 5; k++) {
-                    const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
-                    sum += (x & 0xffffu) + (x >> 16);
-                }
-                sum = (sum >> 16) + (sum & 0xffffu);
-                sum = (sum >> 16) + (sum & 0xffffu);
-                const bool ok = bswap16(W[4] & 0xffffu) < a.buf_len && ((~sum) & 0xffffu) == 0u;
-                const uint32_t d0 = ok ? bswap32(dst) : 0u;
-                na.q0 = ok ? dst >> (a.dir16 ? 16 : 24) : 0u; // network bytes 2, 3
-                flags = 1u << 16;
-                tb0 = a.dir16 ? a.dir16 : a.tbl24;
-                idx0 = a.dir16 ? d0 >> 16 : d0 >> 8;
-            }
-        } else {
-            if (pe == 4u || a.spec_nh) { // ip6_input.c:115-135
-                uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-                if (bswap16(W[4] >> 16) < a.buf_len) {
-                    d0 = alignb(W[10], W[9], 2);
-                    d1 = alignb(W[11], W[10], 2);
-                    d2 = alignb(W[12], W[11], 2);
-                    d3 = alignb(W[13], W[12], 2);
-                }
-                na.q0 = alignb(d1, d0, 3);
-                na.q1 = alignb(d2, d1, 3);
-                na.q2 = alignb(d3, d2, 3);
-                na.q3 = d3 >> 24;
-                flags = 1u << 17;
-                idx0 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu); // trie.h:126
-            }
+        for (int k = 0; k < 5; k++) {
+            const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
+            sum += (x & 0xffffu) + (x >> 16);
         }
+        sum = (sum >> 16) + (sum & 0xffffu);
+        sum = (sum >> 16) + (sum & 0xffffu);
+        const bool ok4 = (bswap16(W[4] & 0xffffu) < a.buf_len) & (((~sum) & 0xffffu) == 0u);
+        const uint32_t d4 = ok4 ? bswap32(dst) : 0u;
+        const bool ok6 = bswap16(W[4] >> 16) < a.buf_len;
+        const uint32_t d0 = ok6 ? alignb(W[10], W[9], 2) : 0u, d1 = ok6 ? alignb(W[11], W[10], 2) : 0u;
+        const uint32_t d2 = ok6 ? alignb(W[12], W[11], 2) : 0u, d3 = ok6 ? alignb(W[13], W[12], 2) : 0u;
+        const uint32_t q04 = ok4 ? dst >> (a.dir16 ? 16 : 24) : 0u; // network bytes 2, 3
+        na.q0 = do4 ? q04 : do6 ? alignb(d1, d0, 3) : 0u;
+        na.q1 = do6 ? alignb(d2, d1, 3) : 0u;
+        na.q2 = do6 ? alignb(d3, d2, 3) : 0u;
+        na.q3 = do6 ? d3 >> 24 : 0u;
+        flags = do4 ? 1u << 16 : do6 ? 1u << 17 : 0u;
+        const uint32_t i4 = a.dir16 ? d4 >> 16 : d4 >> 8;
+        const uint32_t i6 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu); // trie.h:126
+        idx0 = do4 ? i4 : do6 ? i6 : 0u;
+        if (do4)
+            tb0 = a.dir16 ? a.dir16 : a.tbl24;
         na.ptf = pt | flags | (1u << 18) | (pe << 19);
     }
     na.e = tb0[idx0]; // first gather, unconditional
@@ -1577,9 +1584,9 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         }
         if (a.spec_nh) {
             if (bf && din && (!a.nh || (pe != 3u && pe != 4u)))
-                a.spec_nh[ib] = eb >> 1;
+                at32(a.spec_nh, ib) = eb >> 1;
             if (bf)
-                a.spec_t16[ib] = (uint16_t)pt;
+                at16(a.spec_t16, ib) = (uint16_t)pt;
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
@@ -1597,15 +1604,15 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         if (bf) {
             const uint32_t q = s_reta[sb.h & a.reta_mask];
             if (META && a.ptype)
-                a.ptype[ib] = pt;
+                at32(a.ptype, ib) = pt;
             if (META && a.rxmeta)
-                a.rxmeta[ib] = sb.rx;
+                at32(a.rxmeta, ib) = sb.rx;
             if (a.nh)
-                a.nh[ib] = nh;
+                at32(a.nh, ib) = nh;
             if (a.hash)
-                a.hash[ib] = sb.h;
+                at32(a.hash, ib) = sb.h;
             if (a.queue)
-                a.queue[ib] = (uint16_t)q;
+                at16(a.queue, ib) = (uint16_t)q;
             if (a.edge)
                 a.edge[ib] = (uint8_t)edge;
             if (count)
@@ -4189,8 +4196,9 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             a.spec_allow = c->tune_spec_scan == 0 ? 1u : 0u;
             a.spec_hint = c->sp_hint_d;
         }
-        // the deferred kernel indexes frames in 32 bits (t * 64 + lane < 2^32)
-        if (c->tune_cnet_tile && b->n <= 0xFFFFFF00u) {
+        // the deferred kernel indexes frames in 32 bits and its outputs by 32-bit
+        // byte offsets (at32: n < 2^30)
+        if (c->tune_cnet_tile && b->n < (1u << 30)) {
             // fast kernel, then the general parse of the frames it left
             if ((uint64_t)b->n + 1 > c->cs_wl_cap) {
                 if (c->cs_wl)
