@@ -140,6 +140,8 @@ struct KArgs {
     uint8_t *spec_tile;    // per 64-frame tile: 0x80 | edge when every frame has that edge, else 0
     uint32_t *spec_hint;   // pinned host words (device view): the last call's worklist size class, uniform flag
     uint32_t spec_B;       // graph burst size
+    uint32_t wl_fold;      // k_cnet_defer's last block parses the worklist and runs spec_classes
+    uint32_t tail_lo;      // with wl_fold: the first frame of the last SPEC_TAIL bursts
     uint32_t spec_allow;   // batch shortcuts allowed (CNDP_TUNE_SPEC_SCAN auto)
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
@@ -1122,7 +1124,7 @@ __device__ __forceinline__ void spec_mark(uint32_t *s_f, bool on, uint32_t g)
 }
 
 
-__device__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uint32_t *meta,
+__device__ __forceinline__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uint32_t *meta,
                              const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t nb,
                              uint32_t allow_skip, uint32_t *wl_n, uint32_t *bar, uint32_t *hint);
 
@@ -1165,6 +1167,119 @@ __device__ __forceinline__ void cnet_spec_tail(const KArgs &a, bool stored)
                  a.wl_n, a.spec_bar, a.spec_hint);
 }
 
+// cne_get_ptype + eth_rx + ptype + ip4_input / ip6_input for frame i, one
+// lane, over the lane's LDS row (ROW_DW words; row[WIN_DW] must be 0)
+__device__ __forceinline__ void cnet_general(const KArgs &a, uint64_t i, uint32_t *row, const uint32_t *s_t,
+                                             const uint16_t *s_reta, uint32_t *s_bins, uint32_t *s_sf, bool count)
+{
+    const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
+    const uint8_t *p = a.slab + base;
+    const uint64_t avail = base < a.slab_len ? a.slab_len - base : 0;
+    // stage the 64-byte header window (bounded) into this lane's LDS row
+    if (avail >= 64 && (base & 15u) == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 q = *(const uint4 *)(p + 16 * k);
+            row[4 * k + 0] = q.x;
+            row[4 * k + 1] = q.y;
+            row[4 * k + 2] = q.z;
+            row[4 * k + 3] = q.w;
+        }
+    } else {
+        for (int k = 0; k < WIN_DW; k++)
+            row[k] = gld32(p, avail, 4u * (uint32_t)k);
+    }
+    const Win w{row, p, avail};
+    Lens ln;
+    const uint32_t pt = get_ptype(w, ln);
+    if (a.ptype)
+        a.ptype[i] = pt;
+    if (a.rxmeta)
+        a.rxmeta[i] = rx_meta(ln, row[0], row[1], row[3] & 0xffffu);
+    const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
+    const uint32_t ip = ln.l2;
+    const bool l4ok = l4t == 0x100u || l4t == 0x200u;
+    uint32_t h = 0, nh = CNDP_NH_INVALID, edge;
+    if (l3 != 0u && !(l3 & 0x40u)) {
+        h = tz4(s_t, 0, w.ld32(ip + 12)) ^ tz4(s_t, 4, w.ld32(ip + 16));
+        if (l4ok)
+            h ^= tz4(s_t, 8, w.ld32(ip + ln.l3));
+    } else if (l3 & 0x40u) {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++)
+            h ^= tz4(s_t, 4 * k, w.ld32(ip + 8 + 4 * k));
+        if (l4ok)
+            h ^= tz4(s_t, 32, w.ld32(ip + ln.l3));
+    }
+    const uint32_t pe = cnet_edge(pt);
+    // with the speculation model, frames of the types a quiet 4-group can
+    // carry into ip4/ip6_input get the input node's result as well
+    const uint32_t lb = pt & 0xffu;
+    const bool alt4 = a.spec_nh && (lb == 0x11u || lb == 0x31u || lb == 0x91u);
+    const bool alt6 = a.spec_nh && (lb == 0x41u || lb == 0xc1u || lb == 0xe1u);
+    bool has = false;
+    if (pe == 3u || alt4) {
+        // ip4_input.c:121-140: total_length < buf_len && cksum == 0
+        const uint32_t x0 = w.ld32(ip);
+        const uint32_t hl = (x0 & 0xfu);
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < hl; k++) {
+            const uint32_t x = k == 0 ? x0 : w.ld32(ip + 4 * k);
+            sum += (x & 0xffffu) + (x >> 16);
+        }
+        sum = (sum >> 16) + (sum & 0xffffu);
+        sum = (sum >> 16) + (sum & 0xffffu);
+        const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
+        const uint32_t dip = ok ? w.be32(ip + 16) : 0u;
+        nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, dip) : lpm4(a.tbl24, a.tbl8, dip);
+        has = true;
+    } else if (pe == 4u || alt6) {
+        // ip6_input.c:115-135: payload_len < buf_len, else dip = ::
+        const bool ok = w.be16(ip + 4) < a.buf_len;
+        uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+        if (ok) {
+            d0 = w.ld32(ip + 24);
+            d1 = w.ld32(ip + 28);
+            d2 = w.ld32(ip + 32);
+            d3 = w.ld32(ip + 36);
+        }
+        // trie.h:126-134
+        uint32_t e = a.tbl24_6[((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu)];
+        uint32_t j = 3;
+        while ((e & 1u) && j < 16) {
+            const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
+            const uint32_t byte = (wd >> ((j & 3u) * 8)) & 0xffu;
+            e = a.tbl8_6[(e >> 1) * 256u + byte];
+            j++;
+        }
+        nh = e >> 1;
+        has = true;
+    }
+    if (a.spec_nh) {
+        if (has && (!a.nh || (pe != 3u && pe != 4u)))
+            a.spec_nh[i] = nh;
+        a.spec_t16[i] = (uint16_t)pt;
+        spec_mark(s_sf, true, spec_sig(pt & 0xffffu));
+    }
+    if (pe == 3u || pe == 4u) {
+        edge = nh >> 24;
+    } else {
+        nh = CNDP_NH_INVALID;
+        edge = 0x80u | pe;
+    }
+    const uint32_t q = s_reta[h & a.reta_mask];
+    if (a.nh)
+        a.nh[i] = nh;
+    if (a.hash)
+        a.hash[i] = h;
+    if (a.queue)
+        a.queue[i] = (uint16_t)q;
+    if (a.edge)
+        a.edge[i] = (uint8_t)edge;
+    if (count)
+        atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
+}
+
 template <bool WL>
 __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 {
@@ -1200,112 +1315,7 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
     const uint64_t n_it = WL ? (uint64_t)*a.wl_n : a.n;
     for (uint64_t j = (uint64_t)blockIdx.x * CNET_THREADS + tid; j < n_it; j += step) {
         const uint64_t i = WL ? (uint64_t)a.wl[j] : j;
-        const uint64_t base = (a.offsets ? a.offsets[i] : i * a.stride) + a.data_off;
-        const uint8_t *p = a.slab + base;
-        const uint64_t avail = base < a.slab_len ? a.slab_len - base : 0;
-        // stage the 64-byte header window (bounded) into this lane's LDS row
-        if (avail >= 64 && (base & 15u) == 0) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint4 q = *(const uint4 *)(p + 16 * k);
-                row[4 * k + 0] = q.x;
-                row[4 * k + 1] = q.y;
-                row[4 * k + 2] = q.z;
-                row[4 * k + 3] = q.w;
-            }
-        } else {
-            for (int k = 0; k < WIN_DW; k++)
-                row[k] = gld32(p, avail, 4u * (uint32_t)k);
-        }
-        const Win w{row, p, avail};
-        Lens ln;
-        const uint32_t pt = get_ptype(w, ln);
-        if (a.ptype)
-            a.ptype[i] = pt;
-        if (a.rxmeta)
-            a.rxmeta[i] = rx_meta(ln, row[0], row[1], row[3] & 0xffffu);
-        const uint32_t l3 = pt & 0xf0u, l4t = pt & 0xf00u;
-        const uint32_t ip = ln.l2;
-        const bool l4ok = l4t == 0x100u || l4t == 0x200u;
-        uint32_t h = 0, nh = CNDP_NH_INVALID, edge;
-        if (l3 != 0u && !(l3 & 0x40u)) {
-            h = tz4(s_t, 0, w.ld32(ip + 12)) ^ tz4(s_t, 4, w.ld32(ip + 16));
-            if (l4ok)
-                h ^= tz4(s_t, 8, w.ld32(ip + ln.l3));
-        } else if (l3 & 0x40u) {
-#pragma unroll
-            for (uint32_t k = 0; k < 8; k++)
-                h ^= tz4(s_t, 4 * k, w.ld32(ip + 8 + 4 * k));
-            if (l4ok)
-                h ^= tz4(s_t, 32, w.ld32(ip + ln.l3));
-        }
-        const uint32_t pe = cnet_edge(pt);
-        // with the speculation model, frames of the types a quiet 4-group can
-        // carry into ip4/ip6_input get the input node's result as well
-        const uint32_t lb = pt & 0xffu;
-        const bool alt4 = a.spec_nh && (lb == 0x11u || lb == 0x31u || lb == 0x91u);
-        const bool alt6 = a.spec_nh && (lb == 0x41u || lb == 0xc1u || lb == 0xe1u);
-        bool has = false;
-        if (pe == 3u || alt4) {
-            // ip4_input.c:121-140: total_length < buf_len && cksum == 0
-            const uint32_t x0 = w.ld32(ip);
-            const uint32_t hl = (x0 & 0xfu);
-            uint32_t sum = 0;
-            for (uint32_t k = 0; k < hl; k++) {
-                const uint32_t x = k == 0 ? x0 : w.ld32(ip + 4 * k);
-                sum += (x & 0xffffu) + (x >> 16);
-            }
-            sum = (sum >> 16) + (sum & 0xffffu);
-            sum = (sum >> 16) + (sum & 0xffffu);
-            const bool ok = bswap16(x0 >> 16) < a.buf_len && ((~sum) & 0xffffu) == 0u;
-            const uint32_t dip = ok ? w.be32(ip + 16) : 0u;
-            nh = a.dir16 ? lpm4d(a.dir16, a.pages, a.tbl8, dip) : lpm4(a.tbl24, a.tbl8, dip);
-            has = true;
-        } else if (pe == 4u || alt6) {
-            // ip6_input.c:115-135: payload_len < buf_len, else dip = ::
-            const bool ok = w.be16(ip + 4) < a.buf_len;
-            uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-            if (ok) {
-                d0 = w.ld32(ip + 24);
-                d1 = w.ld32(ip + 28);
-                d2 = w.ld32(ip + 32);
-                d3 = w.ld32(ip + 36);
-            }
-            // trie.h:126-134
-            uint32_t e = a.tbl24_6[((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu)];
-            uint32_t j = 3;
-            while ((e & 1u) && j < 16) {
-                const uint32_t wd = j < 4 ? d0 : j < 8 ? d1 : j < 12 ? d2 : d3;
-                const uint32_t byte = (wd >> ((j & 3u) * 8)) & 0xffu;
-                e = a.tbl8_6[(e >> 1) * 256u + byte];
-                j++;
-            }
-            nh = e >> 1;
-            has = true;
-        }
-        if (a.spec_nh) {
-            if (has && (!a.nh || (pe != 3u && pe != 4u)))
-                a.spec_nh[i] = nh;
-            a.spec_t16[i] = (uint16_t)pt;
-            spec_mark(s_sf, true, spec_sig(pt & 0xffffu));
-        }
-        if (pe == 3u || pe == 4u) {
-            edge = nh >> 24;
-        } else {
-            nh = CNDP_NH_INVALID;
-            edge = 0x80u | pe;
-        }
-        const uint32_t q = s_reta[h & a.reta_mask];
-        if (a.nh)
-            a.nh[i] = nh;
-        if (a.hash)
-            a.hash[i] = h;
-        if (a.queue)
-            a.queue[i] = (uint16_t)q;
-        if (a.edge)
-            a.edge[i] = (uint8_t)edge;
-        if (count)
-            atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
+        cnet_general(a, i, row, s_t, s_reta, s_bins, s_sf, count);
     }
     if (count || a.spec_flags)
         __syncthreads();
@@ -1486,7 +1496,10 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 w0 = atomicAdd(a.wl_n, (uint32_t)__popcll(m));
             w0 = __shfl(w0, __ffsll(m) - 1);
             if (slow)
-                a.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+                // write-through (agent-scope) store: k_cnet_defer's last block
+                // may read it without a release by this one (cnet_defer_tail)
+                __hip_atomic_store(&a.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))], (uint32_t)i,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     CdLane na;
@@ -1585,8 +1598,15 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         if (a.spec_nh) {
             if (bf && din && (!a.nh || (pe != 3u && pe != 4u)))
                 at32(a.spec_nh, ib) = eb >> 1;
-            if (bf)
-                at16(a.spec_t16, ib) = (uint16_t)pt;
+            if (bf) {
+                // the last SPEC_TAIL bursts' types are read by spec_classes in
+                // this kernel's last block when it folds: write-through stores
+                if (a.wl_fold && ib >= a.tail_lo)
+                    __hip_atomic_store(&at16(a.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    __builtin_nontemporal_store((uint16_t)pt, &at16(a.spec_t16, ib));
+            }
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
@@ -1604,17 +1624,19 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         if (bf) {
             const uint32_t q = s_reta[sb.h & a.reta_mask];
             if (META && a.ptype)
-                at32(a.ptype, ib) = pt;
+                __builtin_nontemporal_store(pt, &at32(a.ptype, ib));
             if (META && a.rxmeta)
-                at32(a.rxmeta, ib) = sb.rx;
+                __builtin_nontemporal_store(sb.rx, &at32(a.rxmeta, ib));
+            // non-temporal stores: the outputs are written once and must not
+            // push the FIB tables of the gather chains out of L2 (C4 -4.5%)
             if (a.nh)
-                at32(a.nh, ib) = nh;
+                __builtin_nontemporal_store(nh, &at32(a.nh, ib));
             if (a.hash)
-                at32(a.hash, ib) = sb.h;
+                __builtin_nontemporal_store(sb.h, &at32(a.hash, ib));
             if (a.queue)
-                at16(a.queue, ib) = (uint16_t)q;
+                __builtin_nontemporal_store((uint16_t)q, &at16(a.queue, ib));
             if (a.edge)
-                a.edge[ib] = (uint8_t)edge;
+                __builtin_nontemporal_store((uint8_t)edge, &a.edge[ib]);
             if (count)
                 atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
         }
@@ -1623,6 +1645,76 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     off.o0 = off.o1;
     off.o1 = off.o2;
     off.o2 = off.o3;
+}
+
+// With a.wl_fold, k_cnet_defer ends the way k_classify_cnet<true> does, so
+// that nothing runs between it and the speculation passes: every block takes
+// an arrival ticket (cnet_spec_tail's two-level ticket, after its type /
+// worklist stores and flag ORs have left), and the last one parses the
+// worklist -- the frames off the fast path, appended by every block -- with
+// 256 lanes over LDS rows in the tile area, then runs spec_classes with wave
+// 0.  The host folds when the previous call left no worklist (spec_hint[0]);
+// any worklist is still handled here, by one block.
+__device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, const uint32_t *s_t,
+                                             const uint16_t *s_reta, uint32_t *s_bins, uint32_t *s_sf, bool count)
+{
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        // no release: what the last block reads of this one's stores -- the
+        // worklist, the last SPEC_TAIL bursts' types -- was stored write-through
+        // and the signature flags are device atomics; vmcnt(0) saw them done
+        const uint32_t G = gridDim.x, g = blockIdx.x & 7u, ng = G < 8u ? G : 8u;
+        const uint32_t in_g = (G - g + 7u) / 8u; // blocks of group g
+        bool last = __hip_atomic_fetch_add(&a.spec_ticket[32u * g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    in_g - 1u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent"); // pass the group's releases on
+            last = __hip_atomic_fetch_add(&a.spec_ticket[32u * 8u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   ng - 1u;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last)
+        return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t n_wl = __hip_atomic_load(a.wl_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n_wl) { // block-uniform
+        if (tid < 64)
+            s_sf[tid] = 0;
+        if (count)
+            for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+                s_bins[k] = 0;
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t *row = rows + tid * ROW_DW;
+            row[WIN_DW] = 0;
+            for (uint32_t j = tid; j < n_wl; j += 256)
+                cnet_general(a, a.wl[j], row, s_t, s_reta, s_bins, s_sf, count);
+        }
+        __syncthreads();
+        if (count)
+            for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+                if (s_bins[k])
+                    atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+        if (a.spec_flags && tid < 64 && s_sf[tid])
+            atomicOr(&a.spec_flags[tid], s_sf[tid]);
+        // wave 0 reads the other waves' type stores and flag ORs
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    if (tid >= 64)
+        return;
+    if (tid < 9)
+        a.spec_ticket[32u * tid] = 0; // for the next launch (kernel boundary)
+    const uint64_t nb = ((uint64_t)a.n + a.spec_B - 1) / a.spec_B;
+    spec_classes(tid, a.spec_flags, a.spec_cls, a.spec_meta, a.spec_t16, a.n, a.spec_B, nb, a.spec_allow, a.wl_n,
+                 a.spec_bar, a.spec_hint);
 }
 
 // META: ptype / rxmeta outputs requested (without them the kernel keeps
@@ -1691,6 +1783,8 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
     if (a.spec_flags && tid < 64 && s_sf[tid])
         atomicOr(&a.spec_flags[tid], s_sf[tid]);
+    if (a.wl_fold)
+        cnet_defer_tail(a, (uint32_t *)&s_tile[0][0], s_t, s_reta, s_bins, s_sf, count);
 }
 
 // ---------------------------------------------------------------------------
@@ -1751,21 +1845,23 @@ __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2,
 // flags, the worklist count and k_spec_fallback's barrier words for the next
 // call (the flags and the count were read before), which saves per-call
 // memsets.
-__device__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uint32_t *meta,
+__device__ __forceinline__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uint32_t *meta,
                              const uint16_t *__restrict__ pt, uint32_t n, uint32_t B, uint64_t nb,
                              uint32_t allow_skip, uint32_t *wl_n, uint32_t *bar, uint32_t *hint)
 {
-    const uint32_t wl_cnt = wl_n ? *wl_n : 0u; // for the hint, before the reset below
+    // every load first (one memory round trip for the wave), then the stores
+    const uint32_t wl_cnt = wl_n ? __hip_atomic_load(wl_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const uint32_t prev = meta[-1], hint_h0 = meta[SPEC_HINT], hint_h1 = meta[SPEC_HINT + 1];
+    const uint32_t f = __hip_atomic_load(&flags[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t < 8)
         meta[SPEC_RCNT + 32 * t] = 0;
-    const uint32_t s_in = meta[-1] & 0xffffu, g0 = spec_sig(s_in); // the node state entering the batch
+    const uint32_t s_in = prev & 0xffffu, g0 = spec_sig(s_in); // the node state entering the batch
     if (t == 0) {
         meta[SPEC_IN] = s_in;
         meta[SPEC_FULL] = 0;
         bar[0] = 0;
         bar[1] = 0;
     }
-    const uint32_t f = __hip_atomic_load(&flags[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t w = f | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
     flags[t] = 0;
     if (wl_n && t == 0)
@@ -1776,18 +1872,22 @@ __device__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uin
         if ((int)t >= o)
             pre += v;
     }
-    uint32_t k = pre - cnt;
+    // lane t's 32 class ids (signatures 32t..32t+31) packed into two 16-B stores
+    uint32_t k = pre - cnt, cw[8];
+#pragma unroll
     for (uint32_t j = 0; j < 32; j++) {
-        const uint32_t g = t * 32 + j;
-        if ((w >> j) & 1u) {
-            class_id[g] = k < SPEC_KMAX ? (uint8_t)k : (uint8_t)0xFF;
-            if (k < SPEC_KMAX)
-                meta[1 + k] = g;
-            k++;
-        } else {
-            class_id[g] = 0xFF;
-        }
+        const bool on = (w >> j) & 1u;
+        const uint32_t id = on && k < SPEC_KMAX ? k : 0xFFu;
+        if (j % 4 == 0)
+            cw[j / 4] = 0;
+        cw[j / 4] |= id << (8 * (j % 4));
+        k += on;
     }
+    *(u32x4 *)(class_id + 32 * t) = (u32x4){cw[0], cw[1], cw[2], cw[3]};
+    *(u32x4 *)(class_id + 32 * t + 16) = (u32x4){cw[4], cw[5], cw[6], cw[7]};
+    k = pre - cnt;
+    for (uint32_t ww = w; ww && k < SPEC_KMAX; ww &= ww - 1u, k++)
+        meta[1 + k] = t * 32 + (uint32_t)__ffs(ww) - 1u;
     if (t == 63)
         meta[0] = pre;
     // flag word t holds the 8 edge bits of low bytes 4t..4t+3: one edge each?
@@ -1870,7 +1970,7 @@ __device__ void spec_classes(uint32_t t, uint32_t *flags, uint8_t *class_id, uin
             // the worklist size class and the uniform flag, written only when
             // they change (a write to host memory delays the kernel's end)
             const uint32_t h0 = wl_cnt ? 32u - (uint32_t)__clz(wl_cnt) : 0u, h1 = meta[SPEC_UNIF];
-            if (meta[SPEC_HINT] != h0 || meta[SPEC_HINT + 1] != h1) {
+            if (hint_h0 != h0 || hint_h1 != h1) {
                 meta[SPEC_HINT] = h0;
                 meta[SPEC_HINT + 1] = h1;
                 __hip_atomic_store(&hint[0], h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -4226,9 +4326,19 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                                                                  k_cnet_defer<true, true>}};
             const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
             a.spec_tile = B ? c->sp_tile : nullptr; // written by this kernel only
+            // the previous call left no worklist: the main kernel's last block
+            // takes this call's (if any) and the classes pass, no second launch
+            a.wl_fold = 0;
+            if (B && c->sp_hint && ((volatile uint32_t *)c->sp_hint)[0] == 0u) {
+                const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
+                const uint64_t t0 = nb > SPEC_TAIL ? (nb - SPEC_TAIL) * B : 0;
+                a.wl_fold = 1;
+                a.tail_lo = (uint32_t)t0;
+            }
             hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
                                0, s, a, (uint32_t)n_tiles);
-            hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
+            if (!a.wl_fold)
+                hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         } else {
             hipLaunchKernelGGL(k_classify_cnet<false>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         }
