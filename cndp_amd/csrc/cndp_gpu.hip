@@ -2617,13 +2617,13 @@ __device__ __forceinline__ void spec_ctable_chunk(const uint16_t *__restrict__ p
 
 template <int CH>
 __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
-                            const uint32_t *st);
+                            const uint32_t *st, int *lbins = nullptr);
 template <int CH>
 __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
                                                  uint32_t lane, const uint32_t *st, uint32_t &fm, uint32_t &fe);
 template <int CH>
 __device__ __forceinline__ void spec_replay_fix(const KArgs &a, uint32_t B, uint64_t c0, uint32_t lane,
-                                                const uint32_t *st, uint32_t fm, uint32_t fe);
+                                                const uint32_t *st, uint32_t fm, uint32_t fe, int *lbins = nullptr);
 
 // replay chunk c from its entering state (the scan's block start, then the
 // block's earlier chunks) unless its summary says no frame can move
@@ -2654,11 +2654,11 @@ __device__ __forceinline__ void spec_cemit_chunk(const KArgs &a, uint32_t B, uin
 // that state, and lane ng-1 hands the burst's exit state to the next burst
 template <int CH>
 __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0, uint32_t lane,
-                            const uint32_t *st)
+                            const uint32_t *st, int *lbins)
 {
     uint32_t fm, fe;
     spec_replay_walk<CH>(a, B, c0, c1, s0, lane, st, fm, fe);
-    spec_replay_fix<CH>(a, B, c0, lane, st, fm, fe);
+    spec_replay_fix<CH>(a, B, c0, lane, st, fm, fe, lbins);
 }
 
 // the walk: fm = frames to fix (bit 4 * burst + j), fe = each burst's edge (3 bits)
@@ -2717,7 +2717,7 @@ __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uin
 // writes (bursts without a fix cost nothing)
 template <int CH>
 __device__ __forceinline__ void spec_replay_fix(const KArgs &a, uint32_t B, uint64_t c0, uint32_t lane,
-                                                const uint32_t *st, uint32_t fm, uint32_t fe)
+                                                const uint32_t *st, uint32_t fm, uint32_t fe, int *lbins)
 {
 #pragma unroll 1
     for (uint32_t bq = 0; bq < (uint32_t)CH; bq++) {
@@ -2733,7 +2733,7 @@ __device__ __forceinline__ void spec_replay_fix(const KArgs &a, uint32_t B, uint
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++)
             if ((m4 >> j) & 1u)
-                spec_fix_v(a, i0 + j, sg[j] & 0xffffu, dst, v[j], nullptr);
+                spec_fix_v(a, i0 + j, sg[j] & 0xffffu, dst, v[j], lbins);
     }
 }
 
@@ -2888,12 +2888,12 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
 // when a frame could leave by another edge -- staged in LDS and replayed
 template <int CH>
 __device__ __forceinline__ void spec_chunk_types(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
-                                                 uint32_t lane, uint32_t *st, const uint16_t *s_lut)
+                                                 uint32_t lane, uint32_t *st, const uint16_t *s_lut, int *lbins)
 {
     if ((B & 7u) != 0) {
         const unsigned long long em = spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
         if (!spec_chunk_quiet(spec_summary(em), s0))
-            spec_replay<CH>(a, B, c0, c1, s0, lane, st);
+            spec_replay<CH>(a, B, c0, c1, s0, lane, st, lbins);
         return;
     }
     constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
@@ -2905,6 +2905,8 @@ __device__ __forceinline__ void spec_chunk_types(const KArgs &a, uint32_t B, uin
         const uint32_t idx = (r * 64u + lane) * 8u;
         v[r] = idx + 8u <= m ? *(const u32x4 *)(a.spec_t16 + p0 + idx) : (u32x4){0, 0, 0, 0};
     }
+    // the summary and the LDS staging (spec_stage_chunk's layout) from the
+    // same registers: a replay does not load the types a second time
     unsigned long long em = 0;
 #pragma unroll
     for (uint32_t r = 0; r < R; r++) {
@@ -2918,15 +2920,20 @@ __device__ __forceinline__ void spec_chunk_types(const KArgs &a, uint32_t B, uin
                 const uint32_t hi = idx + 2 * q + 1 < m ? a.spec_t16[p0 + idx + 2 * q + 1] : 0u;
                 w[q] = lo | (hi << 16);
             }
+        uint32_t o[8];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; q++)
+        for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t l = (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu, x = cnet_lut_x(s_lut, l);
+            o[q] = l | ((x >> 6) << 16);
             if (idx + q < m)
-                em |= 1ull << (cnet_lut_x(s_lut, (w[q >> 1] >> (16 * (q & 1u))) & 0xffffu) & 63u);
+                em |= 1ull << (x & 63u);
+        }
+        *(u32x4 *)(st + idx) = (u32x4){o[0], o[1], o[2], o[3]};
+        *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
     }
-    if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0)) {
-        spec_stage_chunk<CH>(a.spec_t16, a.n, B, c0, c1, lane, st, s_lut);
-        spec_replay<CH>(a, B, c0, c1, s0, lane, st);
-    }
+    __builtin_amdgcn_wave_barrier();
+    if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0))
+        spec_replay<CH>(a, B, c0, c1, s0, lane, st, lbins);
 }
 
 template <int CH, int WPB>
@@ -3210,6 +3217,10 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
     __shared__ uint32_t s_carry[SPEC_KMAX];
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
+    // the replays' bin moves, one global atomic per bin and block at the end
+    // (the moves of re-routed frames mostly leave one bin: same-address
+    // device atomics serialize, ~1 µs per hundred)
+    __shared__ int s_lb[CNDP_BINS_MAX + 2];
     static_assert(SPEC_BLK * (SPEC_KMAX + 1) >= 4 * CH * 256, "staging fits the scan rows");
     uint32_t rc[8], nrep = 0; // the 8 replay lists (k_spec_local_t)
 #pragma unroll
@@ -3225,6 +3236,9 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
     uint32_t *st = s_m + wv * (CH * 256);
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
+    const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
+    for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+        s_lb[k] = 0;
     __syncthreads();
     const uint64_t W = (uint64_t)gridDim.x * 4, wid = (uint64_t)blockIdx.x * 4 + wv;
     // the chunks k_spec_local_t listed (their entering states known): types,
@@ -3236,8 +3250,14 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
             j -= rc[x++];
         const uint32_t *e = R + x * 2 * nch + 2 * j;
         const uint64_t c = e[0], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-        spec_chunk_types<CH>(a, B, c0, c1, e[1], lane, st, s_lut);
+        spec_chunk_types<CH>(a, B, c0, c1, e[1], lane, st, s_lut, a.bins ? s_lb : nullptr);
         __builtin_amdgcn_wave_barrier();
+    }
+    if (nrep) { // block-uniform
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            if (s_lb[k])
+                atomicAdd(&a.bins[k], (unsigned long long)(long long)s_lb[k]);
     }
     if (!full)
         return;
