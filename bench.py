@@ -481,6 +481,7 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     pool = MbufPool(nc)
     pool.fill(pktgen.imix(nc, v4routes=routes, v6routes=v6, seed=98))
     ptrs = pool.ptrs(np.arange(nc))
+    hdr0 = pool.hdr.copy()
     cn = {}
     for zc in (True, False):
         umem = None
@@ -488,13 +489,22 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
             cl.host_register(pool.mem)
             umem = pool.base
         q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=8192, depth=4, umem=umem)
-        H.harness_mq_drive(q.h, ptrs, nc, burst, 1)
-        t = H.harness_mq_drive(q.h, ptrs, nc, burst, passes)
+        # eth_rx advances data_off by l2_len in every mbuf it returns: each pass
+        # starts from the received mbufs again (headers restored outside the clock)
+        t = 0.0
+        for p in range(passes + 1):  # pass 0 warms up
+            pool.hdr[:] = hdr0
+            dt = H.harness_mq_drive(q.h, ptrs, nc, burst, 1)
+            if dt < 0:
+                t = -1.0
+                break
+            t += dt if p else 0.0
         q.close()
         if zc:
             cl.host_unregister(pool.mem)
         cn["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(nc * passes / t / 1e6, 2) if t > 0 else None
     # the cnet chain on one core over the same frames (the pool as the slab)
+    pool.hdr[:] = hdr0
     kw = {"tables4": tuple(x.copy() for x in f4.image()), "tables6": tuple(x.copy() for x in f6.image()),
           "offsets": pool.data_pos().astype(np.uint64)}
     cpus, _, _ = host_cpus()

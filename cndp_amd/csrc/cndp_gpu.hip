@@ -5159,6 +5159,44 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 #define MQ_WIN4 64u         // ip4_lookup staged bytes (it reads bytes 22..33)
 #define MQ_RUNS_MAX 512u    // cnet: runs of equal-size bursts per batch
 #define MQ_EDGE_NONE 0xFFFFu // zero-copy: an mbuf whose buffer is outside the region
+#define MQ_SHORT 128u       // cnet staged bytes of a frame whose parse stays in its first 128
+#define MQ_PF 8u            // staged: mbufs prefetched ahead in the host loops
+
+// Staged cnet: whether a frame's bytes past its first MQ_SHORT can matter.
+// cne_get_ptype (pktmbuf_ptype.c:472-615) stops early for ARP and MPLS, and
+// after Ethernet (at most one VLAN / QinQ tag), IPv4 (any IHL; a fragment
+// stops there) or IPv6 without extension headers, and TCP / UDP / SCTP: it
+// reads below l2 (<= 22) + l3 (<= 60) + 13 < 128, and so do the input nodes
+// (ip4_input.c / ip6_input.c: the IP header) and the flow hash (the tuple).
+// Every other frame -- extension headers, tunnels, and the protocols the
+// inner-header walk picks up by their raw value -- gets the whole buffer (up
+// to stage_max), so the staged bytes never change a result.
+static inline bool mq_short_reach(const uint8_t *f, uint32_t room)
+{
+    if (room <= MQ_SHORT)
+        return true; // the whole buffer fits anyway
+    uint32_t et = ((uint32_t)f[12] << 8) | f[13], l2 = 14;
+    if (et == 0x0806u || et == 0x8847u || et == 0x8848u) // ARP, MPLS
+        return true;
+    if (et == 0x8100u) {
+        et = ((uint32_t)f[16] << 8) | f[17];
+        l2 = 18;
+    } else if (et == 0x88A8u) {
+        et = ((uint32_t)f[20] << 8) | f[21];
+        l2 = 22;
+    }
+    uint32_t proto;
+    if (et == 0x0800u) {
+        if (((((uint32_t)f[l2 + 6] << 8) | f[l2 + 7]) & 0x3fffu) != 0)
+            return true; // a fragment: no L4 read
+        proto = f[l2 + 9];
+    } else if (et == 0x86DDu) {
+        proto = f[l2 + 6];
+    } else {
+        return false;
+    }
+    return proto == 6u || proto == 17u || proto == 132u;
+}
 
 // pktmbuf_t fields (pktmbuf.h:102-204)
 #define MB_LPORT 26
@@ -5736,6 +5774,15 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
             uint64_t *ho = (uint64_t *)(H + q->h_ptr);
             u32x2 *hl = (u32x2 *)(H + q->h_len);
             for (uint32_t i = 0; i < k; i++) {
+                // the mbuf headers MQ_PF ahead, the frames of the ones half as far
+                // (their buf_addr already in cache): a pool larger than the caches
+                // costs two misses per mbuf otherwise, one after the other
+                if (i + MQ_PF < k)
+                    __builtin_prefetch((const uint8_t *)mbufs[done + i + MQ_PF], 1);
+                if (i + MQ_PF / 2 < k) {
+                    const uint8_t *pm = (const uint8_t *)mbufs[done + i + MQ_PF / 2];
+                    __builtin_prefetch(*(uint8_t *const *)(pm + MB_BUF_ADDR) + *(const uint16_t *)(pm + MB_DATA_OFF));
+                }
                 uint8_t *m = (uint8_t *)mbufs[done + i];
                 const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
                 const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
@@ -5751,7 +5798,9 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
                     hl[j] = l;
                 }
                 // staged copy of the bytes the nodes can read (bounded by the buffer)
-                const uint32_t want = cnet ? (room < q->conf.stage_max ? room : q->conf.stage_max) : MQ_WIN4;
+                const uint32_t cap = cnet && q->conf.stage_max > MQ_SHORT && mq_short_reach(buf + doff, room)
+                                         ? MQ_SHORT : q->conf.stage_max;
+                const uint32_t want = cnet ? (room < cap ? room : cap) : MQ_WIN4;
                 const uint32_t cp = room < want ? room : want;
                 uint8_t *dst = H + q->h_stage + sl->stage_used;
                 memcpy(dst, buf + doff, cp);
@@ -5804,14 +5853,19 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
     }
     if (q->conf.mode == CNDP_MQ_IP4_LOOKUP) {
         const uint64_t *priv1 = (const uint64_t *)R;
-        for (uint32_t i = i0; i < i1; i++) // node_mbuf_priv1 (ip4_lookup.c:144-154)
+        for (uint32_t i = i0; i < i1; i++) { // node_mbuf_priv1 (ip4_lookup.c:144-154)
+            if (i + MQ_PF < i1)
+                __builtin_prefetch((uint8_t *)sl->mb[i + MQ_PF] + MB_UDATA64, 1);
             *(uint64_t *)((uint8_t *)sl->mb[i] + MB_UDATA64) = priv1[i];
+        }
         return;
     }
     const uint32_t *rec = (const uint32_t *)R;
     const bool wh = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
     const uint16_t lport = q->conf.lport;
     for (uint32_t i = i0; i < i1; i++) {
+        if (i + MQ_PF < i1)
+            __builtin_prefetch(sl->mb[i + MQ_PF], 1);
         uint8_t *m = (uint8_t *)sl->mb[i];
         const uint32_t pt = rec[4 * i], rm = rec[4 * i + 1], w2 = rec[4 * i + 2];
         // eth_rx mbuf_update (eth_rx.c:35-63)
@@ -5882,6 +5936,15 @@ extern "C" int cndp_gpu_mq_wait(cndp_gpu_mq_t *q)
         return 0;
     HIP_TRY(hipEventSynchronize(sl->ev));
     return 0;
+}
+
+extern "C" int64_t cndp_gpu_get_stat(cndp_gpu_ctx_t *c, int key)
+{
+    if (!c || (key != CNDP_STAT_CNET_WORKLIST && key != CNDP_STAT_CNET_UNIFORM))
+        return -EINVAL;
+    if (!c->sp_hint)
+        return 0;
+    return ((volatile uint32_t *)c->sp_hint)[key == CNDP_STAT_CNET_WORKLIST ? 0 : 1];
 }
 
 extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)

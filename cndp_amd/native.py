@@ -40,6 +40,7 @@ CNDP_TUNE_RW_WB = 8
 CNDP_TUNE_CNET_SPEC = 9
 CNDP_TUNE_LOAD_NT = 10
 CNDP_TUNE_SPEC_SCAN = 11
+CNDP_STAT_CNET_WORKLIST, CNDP_STAT_CNET_UNIFORM = 1, 2
 CNDP_TUNE_MBUF_HASH = 12
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP = 0, 1, 2
 CNDP_MQ_F_HASH = 1
@@ -175,6 +176,7 @@ def lib():
         "cndp_gpu_mq_poll": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
         "cndp_gpu_mq_wait": (c_int, [c_void_p]),
         "cndp_gpu_mq_pending": (c_uint32, [c_void_p]),
+        "cndp_gpu_get_stat": (ctypes.c_int64, [c_void_p, c_int]),
         "cndp_gpu_version": (c_char_p, []),
     }
     for name, (res, args) in sig.items():

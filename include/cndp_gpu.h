@@ -318,6 +318,17 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_MBUF_HASH 12
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
+/* Observability: the last cnet classify's shape, read from pinned host words
+ * the kernels update (no HIP call).  Returns -EINVAL for an unknown key.
+ *   CNDP_STAT_CNET_WORKLIST  bit length of the number of frames the last call
+ *                            left to the general parse (0: every frame took
+ *                            the fast path)
+ *   CNDP_STAT_CNET_UNIFORM   1 when the last call's ptypes all had the entering
+ *                            node state's low byte (the uniform speculation pass) */
+#define CNDP_STAT_CNET_WORKLIST 1
+#define CNDP_STAT_CNET_UNIFORM 2
+int64_t cndp_gpu_get_stat(cndp_gpu_ctx_t *ctx, int key);
+
 /* Version / build info string. */
 const char *cndp_gpu_version(void);
 

@@ -26,6 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert L.cndp_gpu_version().startswith(b"cndp_amd")
+    assert L.cndp_gpu_get_stat(None, N.CNDP_STAT_CNET_WORKLIST) == -22  # -EINVAL, no context
 
 
 def test_no_oracle_in_product():
