@@ -503,6 +503,36 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         if zc:
             cl.host_unregister(pool.mem)
         cn["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(nc * passes / t / 1e6, 2) if t > 0 else None
+    # the same through the GPU eth_rx graph node (cndp_amd/node/eth_rx_gpu.c):
+    # graph walks pull 256-mbuf bursts from the port, finished mbufs leave on
+    # the ptype / ip4_input / ip6_input edges
+    HC = ctypes.CDLL(os.path.join(ROOT, "tests", "node_harness", "libcnet_harness.so"))
+    HC.harness_rx_load.argtypes = [ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint32]
+    HC.harness_cnet_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    HC.harness_eth_rx_port.argtypes = [ctypes.c_uint32, ctypes.c_uint16]
+    HC.harness_walk_until.argtypes = [ctypes.c_uint64]
+    HC.harness_walk_until.restype = ctypes.c_double
+    HC.harness_cnet_set(f4.h, f6.h)
+    HC.harness_eth_rx_port(0, 0)
+    for zc in (True, False):
+        L.cndp_node_gpu_umem_reset()
+        if zc:
+            L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
+        assert HC.harness_graph_create(20 + int(zc)) == 0
+        t = 0.0
+        for p in range(passes + 1):  # pass 0 warms up
+            pool.hdr[:] = hdr0
+            HC.harness_rx_load(0, ptrs, nc)
+            HC.harness_reset_counts()
+            dt = HC.harness_walk_until(nc)
+            if dt < 0:
+                t = -1.0
+                break
+            t += dt if p else 0.0
+        HC.harness_graph_destroy()
+        cn["eth_rx_node_zero_copy_Mpps" if zc else "eth_rx_node_staged_Mpps"] = \
+            round(nc * passes / t / 1e6, 2) if t > 0 else None
+    L.cndp_node_gpu_umem_reset()
     # the cnet chain on one core over the same frames (the pool as the slab)
     pool.hdr[:] = hdr0
     kw = {"tables4": tuple(x.copy() for x in f4.image()), "tables6": tuple(x.copy() for x in f6.image()),

@@ -1,0 +1,268 @@
+/*
+ * eth_rx_gpu.c -- the cnet receive path (eth_rx -> ptype -> ip4_input /
+ * ip6_input) as one graph source node with its arithmetic on the MI355X
+ * (libcndp_gpu.so).
+ *
+ * Built in a CNDP tree in place of lib/cnet/eth/eth_rx.c.
+ * It keeps that file's interface to the rest of cnet:
+ *   - the node "eth_rx", a source node (CNE_NODE_SOURCE_F, eth_rx.c:171-190)
+ *     that pkt_ctrl.c:55-72 clones per port ("eth_rx-<port>") through
+ *     eth_rx_node_get() and registers in eth_rx_get_node_data_get()'s list
+ *     ({port_id, nid} elements, eth_rx_priv.h), which node init looks up;
+ *   - per call, one pktdev_rx_burst of up to CNE_GRAPH_BURST_SIZE mbufs from
+ *     the node's port (eth_rx.c:112-130).
+ * What the next nodes receive is what the reference chain hands them: the
+ * mbuf fields eth_rx's mbuf_update writes (packet_type, l2/l3/l4 lengths,
+ * ol_flags, lport, data_off / data_len after pktmbuf_adj_offset,
+ * eth_rx.c:35-63), ptype's 4-wide speculative routing with its node state
+ * (ptype.c:48-210), ip4_input / ip6_input's data_len, checksum / length test
+ * and FIB lookup in this_cnet->rt4_finfo / rt6_finfo (ip4_input.c:50-260,
+ * ip6_input.c:50-260).  So the mbufs leave this node on the edges the
+ * reference's ptype and input nodes would have used:
+ *   ptype's pkt_drop / punt_kernel / punt_l2_kernel / gtpu_input,
+ *   ip4_input's ip4_forward / ip4_proto, ip6_input's ip6_forward / ip6_proto.
+ * The node also keeps an edge to "ptype" (never used), so the graph still
+ * reaches ptype, ip4_input and ip6_input, which stay registered and idle.
+ *
+ * Each burst is handed to an asynchronous queue (cndp_gpu_mq_submit, mode
+ * CNDP_MQ_CNET) that batches bursts and runs whole batches on the device;
+ * finished mbufs come back in receive order from cndp_gpu_mq_poll, which is
+ * called on every graph walk (this is a source node, so that is also the flush
+ * of a partly filled batch on an idle port).  When every batch slot is in
+ * flight the node drains and then waits for the oldest batch.
+ *
+ * Tuning from the environment: CNDP_GPU_DEVICE (0), CNDP_GPU_BATCH (8192),
+ * CNDP_GPU_DEPTH (4), CNDP_GPU_DELAY_US (50).  Frames are read in place when
+ * the application registered its UMEM with cndp_node_gpu_umem_add(), else
+ * staged.  One GPU context and queue per cloned node (per port and graph).
+ */
+#include <errno.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <cne_graph.h>
+#include <cne_graph_worker.h>
+#include <pktdev.h>
+#include <pktmbuf.h>
+#include <cnet.h>
+#include <cnet_fib_info.h>
+
+#include "eth_rx_priv.h"
+
+#include "cndp_gpu.h"
+#include "cndp_node.h"
+
+#define RX_BURST 256 /* CNE_GRAPH_BURST_SIZE (cne_graph.h:30) */
+
+/* this node's edges: the next nodes of ptype, ip4_input and ip6_input */
+enum eth_rx_gpu_next {
+    ETH_RX_GPU_NEXT_PKT_DROP,    /* ptype / ip4_input / ip6_input ..._PKT_DROP */
+    ETH_RX_GPU_NEXT_PKT_PUNT,    /* PTYPE_NEXT_PKT_PUNT */
+    ETH_RX_GPU_NEXT_FRAME_PUNT,  /* PTYPE_NEXT_FRAME_PUNT */
+    ETH_RX_GPU_NEXT_GTPU_INPUT,  /* PTYPE_NEXT_GTPU_INPUT */
+    ETH_RX_GPU_NEXT_IP4_FORWARD, /* CNE_NODE_IP4_INPUT_NEXT_FORWARD */
+    ETH_RX_GPU_NEXT_IP4_PROTO,   /* CNE_NODE_IP4_INPUT_NEXT_PROTO */
+    ETH_RX_GPU_NEXT_IP6_FORWARD, /* CNE_NODE_IP6_INPUT_NEXT_FORWARD */
+    ETH_RX_GPU_NEXT_IP6_PROTO,   /* CNE_NODE_IP6_INPUT_NEXT_PROTO */
+    ETH_RX_GPU_NEXT_PTYPE,       /* keeps ptype (and behind it the input nodes) in the graph */
+    ETH_RX_GPU_NEXT_MAX,
+};
+
+/* ptype_priv.h:19-29 with CNET_ENABLE_IP6: the ptype edge ids the queue returns */
+#define PT_NEXT_PKT_PUNT 1
+#define PT_NEXT_FRAME_PUNT 2
+#define PT_NEXT_GTPU_INPUT 5
+
+static struct eth_rx_node_main eth_rx_main;
+
+struct gpu_rx_state {
+    cndp_gpu_ctx_t *gpu;
+    cndp_gpu_mq_t *q;
+    void *rx[RX_BURST];
+    void *done[RX_BURST];
+    uint16_t edge[RX_BURST];
+};
+
+struct gpu_rx_ctx { /* node->ctx is CNE_NODE_CTX_SZ (16) bytes */
+    uint16_t port_id; /* eth_rx_node_ctx_t's one field, where the reference keeps it */
+    struct gpu_rx_state *st;
+};
+_Static_assert(sizeof(struct gpu_rx_ctx) <= CNE_NODE_CTX_SZ, "node context");
+#define GPU_RX_CTX(node) ((struct gpu_rx_ctx *)(node)->ctx)
+
+static uint32_t env_u32(const char *name, uint32_t dflt)
+{
+    const char *v = getenv(name);
+    return v && *v ? (uint32_t)strtoul(v, NULL, 0) : dflt;
+}
+
+/* the queue's (node << 8 | node edge) as one of this node's edges; a FIB value
+ * whose next index names no input edge, and an mbuf the zero-copy queue could
+ * not read (outside the registered UMEM), leave by pkt_drop */
+static inline cne_edge_t rx_edge(uint16_t e)
+{
+    const unsigned node = e >> 8, x = e & 0xffu;
+    if (e == CNDP_MQ_EDGE_NONE)
+        return ETH_RX_GPU_NEXT_PKT_DROP;
+    if (node == CNDP_MQ_NODE_IP4)
+        return x == CNDP_INPUT_NEXT_FORWARD ? ETH_RX_GPU_NEXT_IP4_FORWARD
+             : x == CNDP_INPUT_NEXT_PROTO   ? ETH_RX_GPU_NEXT_IP4_PROTO
+                                            : ETH_RX_GPU_NEXT_PKT_DROP;
+    if (node == CNDP_MQ_NODE_IP6)
+        return x == CNDP_INPUT_NEXT_FORWARD ? ETH_RX_GPU_NEXT_IP6_FORWARD
+             : x == CNDP_INPUT_NEXT_PROTO   ? ETH_RX_GPU_NEXT_IP6_PROTO
+                                            : ETH_RX_GPU_NEXT_PKT_DROP;
+    return x == PT_NEXT_PKT_PUNT     ? ETH_RX_GPU_NEXT_PKT_PUNT
+         : x == PT_NEXT_FRAME_PUNT   ? ETH_RX_GPU_NEXT_FRAME_PUNT
+         : x == PT_NEXT_GTPU_INPUT   ? ETH_RX_GPU_NEXT_GTPU_INPUT
+                                     : ETH_RX_GPU_NEXT_PKT_DROP;
+}
+
+/* hand every finished mbuf on to its edge, runs of one edge at a time */
+static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct gpu_rx_state *st)
+{
+    uint16_t total = 0;
+    for (;;) {
+        const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, RX_BURST);
+        if (k <= 0)
+            break;
+        int i = 0;
+        while (i < k) {
+            const cne_edge_t e = rx_edge(st->edge[i]);
+            int j = i + 1;
+            while (j < k && rx_edge(st->edge[j]) == e)
+                j++;
+            cne_node_enqueue(graph, node, e, &st->done[i], (uint16_t)(j - i));
+            i = j;
+        }
+        total = (uint16_t)(total + k);
+        if (k < RX_BURST)
+            break;
+    }
+    return total;
+}
+
+static uint16_t eth_rx_gpu_process(struct cne_graph *graph, struct cne_node *node, void **objs, uint16_t cnt)
+{
+    (void)objs;
+    (void)cnt;
+    struct gpu_rx_ctx *ctx = GPU_RX_CTX(node);
+    struct gpu_rx_state *st = ctx->st;
+    rx_drain(graph, node, st); /* free slots first */
+    const uint16_t count = pktdev_rx_burst(ctx->port_id, (pktmbuf_t **)st->rx, RX_BURST);
+    if (count == PKTDEV_ADMIN_STATE_DOWN)
+        return count;
+    uint16_t done = 0;
+    while (done < count) {
+        const int k = cndp_gpu_mq_submit(st->q, st->rx + done, (uint32_t)(count - done));
+        if (k < 0) { /* the device failed: the mbufs still have to go somewhere */
+            cne_node_enqueue(graph, node, ETH_RX_GPU_NEXT_PKT_DROP, st->rx + done, (uint16_t)(count - done));
+            break;
+        }
+        done = (uint16_t)(done + k);
+        if (done < count && rx_drain(graph, node, st) == 0 && cndp_gpu_mq_wait(st->q) < 0) {
+            cne_node_enqueue(graph, node, ETH_RX_GPU_NEXT_PKT_DROP, st->rx + done, (uint16_t)(count - done));
+            break;
+        }
+    }
+    rx_drain(graph, node, st);
+    return count;
+}
+
+static void rx_state_free(struct gpu_rx_state *st)
+{
+    if (!st)
+        return;
+    cndp_gpu_mq_free(st->q);
+    cndp_gpu_fini(st->gpu);
+    free(st);
+}
+
+static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
+{
+    (void)graph;
+    struct gpu_rx_ctx *ctx = GPU_RX_CTX(node);
+    memset(ctx, 0, sizeof(*ctx));
+    for (eth_rx_node_elem_t *elem = eth_rx_main.head; elem; elem = elem->next)
+        if (elem->nid == node->id) { /* eth_rx.c:146-158 */
+            ctx->port_id = elem->ctx.port_id;
+            break;
+        }
+    struct cnet *cnet = this_cnet;
+    if (!cnet || !cnet->rt4_finfo || !cnet->rt6_finfo)
+        return -EINVAL;
+    struct gpu_rx_state *st = calloc(1, sizeof(*st));
+    if (!st)
+        return -ENOMEM;
+    int r = cndp_gpu_init((int)env_u32("CNDP_GPU_DEVICE", 0), &st->gpu);
+    if (r < 0) {
+        free(st);
+        return -ENODEV; /* no CPU path behind this node: fail loudly at graph create */
+    }
+    if ((r = cndp_gpu_set_fib(st->gpu, cnet->rt4_finfo->fib, cnet->rt6_finfo->fib6)) < 0)
+        goto fail;
+    struct cndp_mq_conf conf;
+    memset(&conf, 0, sizeof(conf));
+    conf.mode = CNDP_MQ_CNET;
+    conf.lport = ctx->port_id;
+    conf.batch = env_u32("CNDP_GPU_BATCH", 8192);
+    conf.depth = env_u32("CNDP_GPU_DEPTH", 4);
+    conf.max_delay_us = env_u32("CNDP_GPU_DELAY_US", 50);
+    void *umem = NULL;
+    uint64_t ulen = 0;
+    if (cndp_node_gpu_umem_get(0, &umem, &ulen) == 0) {
+        const int rr = cndp_gpu_host_register(st->gpu, umem, ulen, NULL);
+        if (rr == 0 || rr == -EEXIST)
+            conf.umem = umem; /* zero-copy: the kernels read the frames in the UMEM */
+    }
+    if ((r = cndp_gpu_mq_create(st->gpu, &conf, &st->q)) < 0)
+        goto fail;
+    ctx->st = st;
+    return 0;
+fail:
+    rx_state_free(st);
+    return r;
+}
+
+static void eth_rx_gpu_fini(const struct cne_graph *graph, struct cne_node *node)
+{
+    (void)graph;
+    struct gpu_rx_ctx *ctx = GPU_RX_CTX(node);
+    rx_state_free(ctx->st);
+    ctx->st = NULL;
+}
+
+static struct cne_node_register eth_rx_node_base = {
+    .process = eth_rx_gpu_process,
+    .flags = CNE_NODE_SOURCE_F,
+    .name = "eth_rx",
+    .init = eth_rx_gpu_init,
+    .fini = eth_rx_gpu_fini,
+    .nb_edges = ETH_RX_GPU_NEXT_MAX,
+    .next_nodes =
+        {
+            [ETH_RX_GPU_NEXT_PKT_DROP] = "pkt_drop",
+            [ETH_RX_GPU_NEXT_PKT_PUNT] = "punt_kernel",
+            [ETH_RX_GPU_NEXT_FRAME_PUNT] = "punt_l2_kernel",
+            [ETH_RX_GPU_NEXT_GTPU_INPUT] = "gtpu_input",
+            [ETH_RX_GPU_NEXT_IP4_FORWARD] = "ip4_forward",
+            [ETH_RX_GPU_NEXT_IP4_PROTO] = "ip4_proto",
+            [ETH_RX_GPU_NEXT_IP6_FORWARD] = "ip6_forward",
+            [ETH_RX_GPU_NEXT_IP6_PROTO] = "ip6_proto",
+            [ETH_RX_GPU_NEXT_PTYPE] = "ptype",
+        },
+};
+CNE_NODE_REGISTER(eth_rx_node_base);
+
+/* eth_rx_priv.h: what pkt_ctrl.c uses to clone the node per port */
+struct eth_rx_node_main *eth_rx_get_node_data_get(void)
+{
+    return &eth_rx_main;
+}
+
+struct cne_node_register *eth_rx_node_get(void)
+{
+    return &eth_rx_node_base;
+}

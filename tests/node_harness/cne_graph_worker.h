@@ -1,6 +1,6 @@
 /*
  * Test-only stand-in for cne_graph_worker.h (see cne_graph.h here): the graph
- * and node objects a node's callbacks see, and cne_node_enqueue (same
+ * and node objects a node's callbacks see (the reference's field names), and cne_node_enqueue (same
  * signature as cne_graph_worker.h:310-311), which the harness records per edge.
  */
 #ifndef NODE_HARNESS_CNE_GRAPH_WORKER_H
@@ -13,6 +13,7 @@ struct cne_graph {
 
 struct cne_node {
     uint8_t ctx[CNE_NODE_CTX_SZ];
+    cne_node_t id;
     const struct cne_node_register *reg;
 };
 

@@ -1,5 +1,6 @@
 /*
- * Test-only driver for cndp_amd/node/ip4_lookup_gpu.c: collects the nodes the
+ * Test-only driver for the GPU graph node sources (cndp_amd/node/ip4_lookup_gpu.c,
+ * and eth_rx_gpu.c with cnet_stubs.c): collects the nodes the
  * source registers (CNE_NODE_REGISTER), instantiates them for one graph, calls
  * their process callbacks as cne_graph_walk would (the source node once per
  * walk, ip4_lookup once per burst it is given) and records, per edge name,
@@ -32,6 +33,24 @@ static int inited[MAX_REG];
 static void **out[3];
 static uint32_t n_out[3];
 static uint64_t enqueue_calls;
+/* and per edge name (any node's edges) */
+#define MAX_NAMES 16
+static char e_name[MAX_NAMES][CNE_NODE_NAMESIZE];
+static void **e_out[MAX_NAMES];
+static uint32_t e_n[MAX_NAMES], n_names;
+static uint64_t n_total;
+
+static int name_slot(const char *to)
+{
+    for (uint32_t k = 0; k < n_names; k++)
+        if (strcmp(e_name[k], to) == 0)
+            return (int)k;
+    if (n_names == MAX_NAMES || !(e_out[n_names] = malloc(sizeof(void *) * MAX_OUT)))
+        return -1;
+    strncpy(e_name[n_names], to, CNE_NODE_NAMESIZE - 1);
+    e_n[n_names] = 0;
+    return (int)n_names++;
+}
 
 static int find(const char *name)
 {
@@ -47,6 +66,10 @@ void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16
     const int k = strcmp(to, "ip4_rewrite") == 0 ? 0 : strcmp(to, "pkt_drop") == 0 ? 1 : 2;
     for (uint16_t i = 0; i < nb_objs && n_out[k] < MAX_OUT; i++)
         out[k][n_out[k]++] = objs[i];
+    const int s = name_slot(to);
+    for (uint16_t i = 0; s >= 0 && i < nb_objs && e_n[s] < MAX_OUT; i++)
+        e_out[s][e_n[s]++] = objs[i];
+    n_total += nb_objs;
     enqueue_calls++;
 }
 
@@ -72,8 +95,12 @@ int harness_graph_create(int gid)
             return -12;
         n_out[k] = 0;
     }
+    for (uint32_t k = 0; k < n_names; k++)
+        e_n[k] = 0;
+    n_total = 0;
     for (int i = 0; i < n_regs; i++) {
         memset(&nodes[i], 0, sizeof(nodes[i]));
+        nodes[i].id = regs[i]->id;
         nodes[i].reg = regs[i];
         int r = regs[i]->init ? regs[i]->init(&g, &nodes[i]) : 0;
         if (r)
@@ -119,8 +146,34 @@ uint32_t harness_take(int k, void **dst, uint32_t max)
 
 uint32_t harness_count(int k) { return n_out[k]; }
 uint64_t harness_enqueue_calls(void) { return enqueue_calls; }
+uint64_t harness_total(void) { return n_total; }
+#ifndef HARNESS_CNET
 extern int node_mbuf_priv1_dynfield_offset;
 int harness_priv1_offset(void) { return node_mbuf_priv1_dynfield_offset; }
+#endif
+
+/* the objects enqueued to the edge named `to`, in enqueue order */
+uint32_t harness_take_edge(const char *to, void **dst, uint32_t max)
+{
+    for (uint32_t k = 0; k < n_names; k++)
+        if (strcmp(e_name[k], to) == 0) {
+            const uint32_t n = e_n[k] < max ? e_n[k] : max;
+            memcpy(dst, e_out[k], n * sizeof(void *));
+            return n;
+        }
+    return 0;
+}
+
+/* the edge names of registered node i (up to max), for registry checks */
+int harness_node_edges(int i, const char **names, int max)
+{
+    if (i < 0 || i >= n_regs)
+        return -1;
+    int k = 0;
+    for (; k < regs[i]->nb_edges && k < max; k++)
+        names[k] = regs[i]->next_nodes[k];
+    return k;
+}
 
 /* ---- measurement drivers (bench.py's node-boundary leg) ------------------
  * harness_drive: graph walks over the named node, as cne_graph_walk would
@@ -157,6 +210,30 @@ double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, 
         }
     }
     return now_s() - t0;
+}
+
+/* Graph walks (source nodes only) until `want` objects have been enqueued in
+ * all since graph create / the last reset: the cnet receive node pulls its
+ * bursts from the harness receive queue itself.  Returns seconds, -1 on a
+ * stall (the spin bound). */
+double harness_walk_until(uint64_t want)
+{
+    const double t0 = now_s();
+    for (long spin = 0; n_total < want; spin++) {
+        if (spin > 100000000L)
+            return -1.0;
+        harness_walk_sources();
+    }
+    return now_s() - t0;
+}
+
+void harness_reset_counts(void)
+{
+    for (int k = 0; k < 3; k++)
+        n_out[k] = 0;
+    for (uint32_t k = 0; k < n_names; k++)
+        e_n[k] = 0;
+    n_total = 0;
 }
 
 /* The asynchronous queue alone, driven by one thread the way a node does:

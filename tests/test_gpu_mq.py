@@ -159,19 +159,17 @@ def _no_reach_past_buffer(pool, idx, donor):
     return n_rep
 
 
-@pytest.mark.parametrize("zero_copy", [True, False])
-@pytest.mark.parametrize("kind", ["full", "ragged"])
-def test_mq_cnet(cn, gpu, zero_copy, kind):
-    cl, routes, v6, t4, t6 = cn
-    n = 24000
+def cnet_pool(n, routes, v6, zero_copy):
+    """IMIX mbufs, every 3rd a fuzz frame (VLAN, QinQ, ext headers, tunnels,
+    bad IHL ...), every 7th a GTP-U / GTP-C / TCP frame in a UDP run (the
+    fix_spec quirk), every 5th a runt (data_len 10: pktmbuf_adj_offset(l2_len)
+    is skipped).  Returns the pool and a copy of its headers."""
     pool = MbufPool(n)
     imx = pktgen.imix(n, v4routes=routes, v6routes=v6, seed=11, v6_frac=0.4)
     fz = pktgen.fuzz_frames(n, seed=12, slot=128)
     from test_gpu_parity import _gtp_mix
     gt = _gtp_mix(n, routes, v6, "cpu", seed=14)
     pool.fill(imx)
-    # every 3rd mbuf: a fuzz frame (VLAN, QinQ, ext headers, tunnels, bad IHL ...)
-    # every 7th: a GTP-U / GTP-C / TCP frame in a UDP run (the fix_spec quirk)
     pf = MbufPool(n)
     pf.fill(fz)
     pg = MbufPool(n)
@@ -183,25 +181,15 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
     pool.hdr["buf_addr"] = pool.base + np.arange(n, dtype=np.uint64) * 2048 + HDR
     if not zero_copy:
         _no_reach_past_buffer(pool, range(0, n, 3), donor=2)
-    pool.hdr["data_len"][::5] = 10      # runts: pktmbuf_adj_offset(l2_len) is skipped
-    orig = pool.hdr.copy()
-    umem = None
-    flags = N.CNDP_MQ_F_HASH if kind == "ragged" else 0
-    if zero_copy:
-        cl.host_register(pool.mem)
-        umem = pool.base
-    bursts = _bursts(n, 21, kind)
-    order = np.arange(n)
-    try:
-        cl.set_tuning(cnet_spec=256)   # fresh ptype node state
-        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=flags, batch=4096, depth=3, umem=umem, lport=7)
-        ref = _cnet_expect(pool, order, bursts, t4, t6, flags, 7)
-        addrs, edges = q.run(pool, order, bursts)
-        q.close()
-    finally:
-        if zero_copy:
-            cl.host_unregister(pool.mem)
-    assert np.array_equal(pool.index_of(addrs), order)
+    pool.hdr["data_len"][::5] = 10
+    return pool, pool.hdr.copy()
+
+
+def cnet_check(pool, orig, ref, t4, t6, lport):
+    """The mbuf fields eth_rx / the input nodes write, against the oracle
+    (ref: _cnet_expect); returns each mbuf's expected queue edge
+    (CNDP_MQ_EDGE(node, e))."""
+    n = pool.n
     h = pool.hdr
     bad = np.nonzero(h["packet_type"] != ref["ptype"])[0]
     for i in bad[:4]:
@@ -211,7 +199,7 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
     assert bad.size == 0, f"{bad.size} packet types differ"
     assert np.array_equal(h["ol_flags"], (ref["rxmeta"] >> 29).astype(np.uint64) << np.uint64(61))
     assert np.array_equal(h["tx_offload"], (ref["rxmeta"] & 0xFFFFFF).astype(np.uint64))
-    assert np.all(h["lport"] == 7)
+    assert np.all(h["lport"] == lport)
     l2 = (ref["rxmeta"] & 0x7F).astype(np.int64)
     dl0 = orig["data_len"].astype(np.int64)
     doff0 = orig["data_off"].astype(np.int64)
@@ -245,8 +233,36 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
         e_in[i] = nh >> 24
     assert (at_input & ~adj).sum() > 0
     node = np.where(at_input, np.where(v6, N.CNDP_MQ_NODE_IP6, N.CNDP_MQ_NODE_IP4), N.CNDP_MQ_NODE_PTYPE)
-    want_e = (node << 8) | np.where(at_input, e_in, e8 & 0x7F)
+    return (node << 8) | np.where(at_input, e_in, e8 & 0x7F)
+
+
+@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("kind", ["full", "ragged"])
+def test_mq_cnet(cn, gpu, zero_copy, kind):
+    cl, routes, v6, t4, t6 = cn
+    n = 24000
+    pool, orig = cnet_pool(n, routes, v6, zero_copy)
+    umem = None
+    flags = N.CNDP_MQ_F_HASH if kind == "ragged" else 0
+    if zero_copy:
+        cl.host_register(pool.mem)
+        umem = pool.base
+    bursts = _bursts(n, 21, kind)
+    order = np.arange(n)
+    try:
+        cl.set_tuning(cnet_spec=256)   # fresh ptype node state
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=flags, batch=4096, depth=3, umem=umem, lport=7)
+        ref = _cnet_expect(pool, order, bursts, t4, t6, flags, 7)
+        addrs, edges = q.run(pool, order, bursts)
+        q.close()
+    finally:
+        if zero_copy:
+            cl.host_unregister(pool.mem)
+    assert np.array_equal(pool.index_of(addrs), order)
+    want_e = cnet_check(pool, orig, ref, t4, t6, 7)
+    node = want_e >> 8
     assert np.array_equal(edges.astype(np.int64), want_e)
+    h = pool.hdr
     if flags & N.CNDP_MQ_F_HASH:
         assert np.array_equal(h["hash"], ref["hash"])
     else:

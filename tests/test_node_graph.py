@@ -135,3 +135,115 @@ def test_node_graph_walk(gpu, zero_copy):
         assert np.all(np.diff(rank[got[k]]) > 0)
     assert len(got[0]) > 0 and len(got[1]) > 0
     NodeFib.fini()
+
+
+# ---- the cnet receive node (cndp_amd/node/eth_rx_gpu.c) -------------------
+CNET_HARNESS = os.path.join(HERE, "node_harness", "libcnet_harness.so")
+ETH_RX_EDGES = [b"pkt_drop", b"punt_kernel", b"punt_l2_kernel", b"gtpu_input", b"ip4_forward", b"ip4_proto",
+                b"ip6_forward", b"ip6_proto", b"ptype"]
+
+
+def _cnet_harness():
+    if not os.path.exists(CNET_HARNESS):
+        pytest.skip("cnet node harness not built (build() makes it)")
+    N.lib()
+    H = ctypes.CDLL(CNET_HARNESS)
+    H.harness_node_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(ctypes.c_char_p)]
+    H.harness_node_edges.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    H.harness_take_edge.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32]
+    H.harness_take_edge.restype = ctypes.c_uint32
+    H.harness_rx_load.argtypes = [ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint32]
+    H.harness_rx_left.restype = ctypes.c_uint32
+    H.harness_cnet_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    H.harness_eth_rx_port.argtypes = [ctypes.c_uint32, ctypes.c_uint16]
+    H.harness_walk_until.argtypes = [ctypes.c_uint64]
+    H.harness_walk_until.restype = ctypes.c_double
+    H.harness_total.restype = ctypes.c_uint64
+    return H
+
+
+def test_cnet_node_registry():
+    """The node replacing lib/cnet/eth/eth_rx.c: registered as "eth_rx", a
+    source node (eth_rx.c:171-190) that pkt_ctrl.c clones per port; its edges
+    are the next nodes of ptype (ptype.c:213-230), ip4_input (ip4_input.c:274-287)
+    and ip6_input (ip6_input.c:275-288), plus ptype itself, which keeps the
+    replaced nodes reachable in the graph."""
+    H = _cnet_harness()
+    name = ctypes.create_string_buffer(64)
+    fl, ne = ctypes.c_uint64(), ctypes.c_int()
+    e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
+    assert H.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1)) == 1
+    assert name.value == b"eth_rx" and fl.value == 1 and ne.value == len(ETH_RX_EDGES)
+    names = (ctypes.c_char_p * 16)()
+    k = H.harness_node_edges(0, names, 16)
+    assert list(names[:k]) == ETH_RX_EDGES
+
+
+def test_cnet_node_init_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from helpers import cnet_fibs
+    H = _cnet_harness()
+    assert H.harness_graph_create(0) == -22      # no cnet instance: -EINVAL
+    fib, fib6 = cnet_fibs()[:2]
+    H.harness_cnet_set(fib.h, fib6.h)
+    assert H.harness_graph_create(0) == -19      # -ENODEV: no CPU path behind the node
+    H.harness_graph_destroy()
+
+
+def _edge_of_queue_code(e):
+    """eth_rx_gpu.c rx_edge: the queue's CNDP_MQ_EDGE(node, e) -> this node's edge."""
+    node, x = e >> 8, e & 0xFF
+    if node == N.CNDP_MQ_NODE_IP4:
+        return {1: 4, 2: 5}.get(x, 0)
+    if node == N.CNDP_MQ_NODE_IP6:
+        return {1: 6, 2: 7}.get(x, 0)
+    return {1: 1, 2: 2, 5: 3}.get(x, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_cnet_node_graph_walk(gpu, zero_copy):
+    """Graph walks over the GPU eth_rx node: it pulls 256-mbuf bursts from its
+    port, and every mbuf leaves by the edge the reference's ptype /
+    ip4_input / ip6_input would have sent it to, with the fields eth_rx and the
+    input nodes write (the oracle over the same bursts, node state from 0)."""
+    from helpers import CNET_DEF, cnet_fibs
+    from oracle import oracle as O
+    from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
+    H = _cnet_harness()
+    L = N.lib()
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    n, port = 24000, 3
+    pool, orig = cnet_pool(n, routes, v6, zero_copy)
+    ref = _cnet_expect(pool, np.arange(n), _bursts(n, 0, "full"), t4, t6, 0, port)
+    L.cndp_node_gpu_umem_reset()
+    if zero_copy:
+        L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
+    H.harness_cnet_set(fib.h, fib6.h)
+    assert H.harness_eth_rx_port(0, port) == 0
+    ptrs = pool.ptrs(np.arange(n))
+    assert H.harness_rx_load(port, ptrs, n) == 0
+    try:
+        assert H.harness_graph_create(5) == 0
+        assert H.harness_walk_until(n) >= 0
+        assert H.harness_rx_left(port) == 0 and H.harness_total() == n
+        got = np.full(n, -1, np.int64)
+        buf = (ctypes.c_void_p * n)()
+        for k, name in enumerate(ETH_RX_EDGES):
+            m = H.harness_take_edge(name, buf, n)
+            idx = pool.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))
+            assert np.all(np.diff(idx) > 0), f"{name}: out of receive order"
+            got[idx] = k
+    finally:
+        H.harness_graph_destroy()
+        L.cndp_node_gpu_umem_reset()
+    want_e = cnet_check(pool, orig, ref, t4, t6, port)
+    want = np.array([_edge_of_queue_code(int(e)) for e in want_e])
+    assert np.array_equal(got, want)
+    assert set(np.unique(got).tolist()) >= {0, 3, 4, 6}   # drop, gtpu_input, ip4_forward, ip6_forward
