@@ -319,7 +319,9 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words
- * the kernels update (no HIP call).  Returns -EINVAL for an unknown key.
+ * the kernels update (no HIP call) -- with the ptype-node speculation model on
+ * (CNDP_TUNE_CNET_SPEC, the default); with it off they are not updated.
+ * Returns -EINVAL for an unknown key or a NULL context.
  *   CNDP_STAT_CNET_WORKLIST  bit length of the number of frames the last call
  *                            left to the general parse (0: every frame took
  *                            the fast path)
