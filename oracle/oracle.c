@@ -683,6 +683,9 @@ static uint8_t cnet_ptype_edge(uint32_t pt)
     }
 }
 
+/* exported for tests/test_oracle_golden.py (the p_nxt fixture check) */
+uint32_t orc_cnet_ptype_edge(uint32_t pt) { return cnet_ptype_edge(pt); }
+
 static inline uint32_t lookup4(const uint32_t *t24, const uint32_t *t8, uint32_t ip)
 {
     uint32_t e = t24[ip >> 8];

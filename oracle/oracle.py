@@ -68,6 +68,8 @@ def lib():
         L.orc_trie_build.restype = c_int
         L.orc_trie_build.argtypes = [c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p]
         L.orc_trie_lookup.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
+        L.orc_cnet_ptype_edge.restype = c_uint32
+        L.orc_cnet_ptype_edge.argtypes = [c_uint32]
         L.orc_get_ptype.restype = c_uint32
         L.orc_get_ptype.argtypes = [c_void_p, c_uint64, POINTER(HdrLens), c_uint32]
         L.orc_classify.restype = c_int
@@ -177,6 +179,11 @@ def trie_lookup(t24, t8, ips) -> np.ndarray:
     out = np.zeros(len(ips), np.uint64)
     lib().orc_trie_lookup(_p(t24), _p(t8), _p(ips), len(ips), _p(out))
     return out
+
+
+def cnet_ptype_edge(pt: int) -> int:
+    """The ptype node's p_nxt[pt & _PTYPE_MASK] (ptype.c:32-46)."""
+    return int(lib().orc_cnet_ptype_edge(ctypes.c_uint32(pt & 0xFFFFFFFF)))
 
 
 def get_ptype(pkt: bytes):

@@ -936,3 +936,34 @@ def _cnet_edge(pt):
     if pt in (0x8211, 0x8241):
         return 5
     return 0
+
+
+def test_cnet_ptype_reference_tables(cnet, gpu):
+    """The GPU's packet types checked straight against the reference's own
+    tables (tests/golden/ptype_ref.json, evaluated from pktmbuf_ptype.c / .h and
+    ptype.c): one frame per IPv4 IHL byte, L4 protocol, IPv6 next header and
+    GRE flag value, plus the L2 and GTP encodings -- no restatement in
+    between -- and every frame's ptype-node edge against p_nxt."""
+    from helpers import ptype_kat, ptype_ref
+    cl = cnet[0]
+    kat = ptype_kat(slot=128)
+    n = len(kat)
+    slab = torch.tensor(np.frombuffer(b"".join(k[0] for k in kat), np.uint8).copy(), device=gpu)
+    fr = pktgen.Frames(slab, n, stride=128)
+    pnxt = {int(k, 16): v for k, v in ptype_ref()["pnxt"].items()}
+    for ct in CNET_KERNELS:
+        cl.set_tuning(cnet_tile=ct, cnet_spec=0)   # per-frame edges (no burst speculation)
+        out = cl.classify(fr, N.CNDP_MODE_CNET, out=cl.alloc_outputs(n, meta=True, device=gpu))
+        torch.cuda.synchronize()
+        pt = out["ptype"].cpu().numpy().astype(np.uint32)
+        edge = out["edge"].cpu().numpy()
+        bad = [(what, hex(int(p)), hex(want)) for (_, mask, want, what), p in zip(kat, pt) if (int(p) & mask) != want]
+        assert not bad, (ct, bad[:8])
+        for p, e in zip(pt.tolist(), edge.tolist()):
+            pe = pnxt.get(p & 0xFFFF, 0)
+            # frames the ptype node sends to an input node carry that node's edge
+            if pe in (3, 4):
+                assert e < 0x80
+            else:
+                assert e == 0x80 | pe, (hex(p), e)
+    cl.set_tuning(cnet_tile=1, cnet_spec=256)

@@ -267,3 +267,32 @@ def test_burst_bench_runs_both_chains():
     t = O.burst_bench(O.MODE_CNET, im.slab.numpy(), 4096, nthreads=len(cpus), cpus=cpus,
                       offsets=im.offsets.numpy().astype(np.uint64), tables4=t4, tables6=t6)
     assert t > 0
+
+
+def test_ptype_node_table_matches_reference():
+    """The oracle's ptype-node edge, p_nxt[ptype & _PTYPE_MASK], against the
+    table evaluated from lib/cnet/ptype/ptype.c:20-46 (tests/golden/ptype_ref.json)."""
+    from helpers import ptype_ref
+    ref = ptype_ref()
+    assert ref["pnxt_mask"] == 0xFFFF
+    want = {int(k, 16): v for k, v in ref["pnxt"].items()}
+    rng = np.random.default_rng(3)
+    high = rng.integers(0, 1 << 16, 64, dtype=np.uint64) << np.uint64(16)
+    for pt in range(1 << 16):
+        assert O.cnet_ptype_edge(pt) == want.get(pt, 0), hex(pt)
+    for h in high.tolist():  # bits above the mask do not matter
+        for pt in want:
+            assert O.cnet_ptype_edge(pt | int(h)) == want[pt]
+
+
+def test_get_ptype_tables_match_reference():
+    """cne_get_ptype's lookup tables (IPv4 IHL, L4 protocol, IPv6 extension
+    headers, GRE option lengths) and the L2 / GTP encodings, one frame per
+    table input, against the values evaluated from pktmbuf_ptype.c / .h."""
+    from helpers import ptype_kat
+    bad = []
+    for frame, mask, want, what in ptype_kat():
+        pt, _ = O.get_ptype(frame)
+        if (pt & mask) != want:
+            bad.append((what, hex(pt), hex(want)))
+    assert not bad, bad[:8]
