@@ -296,3 +296,45 @@ def test_get_ptype_tables_match_reference():
         if (pt & mask) != want:
             bad.append((what, hex(pt), hex(want)))
     assert not bad, bad[:8]
+
+
+def test_eth_rx_fields_match_reference_layout():
+    """What eth_rx's mbuf_update writes (eth_rx.c:35-63), as the mbuf shim and
+    the node queue store it (tx_offload = rxmeta & 0xFFFFFF, ol_flags = rxmeta
+    >> 29 << 61): decoded with the reference's tx_offload bit-field layout and
+    CNE_MBUF_TYPE_* bits (tests/golden/ptype_ref.json from pktmbuf_offload.h),
+    the l2/l3/l4 lengths are cne_get_ptype's and the type bits follow the
+    destination MAC and ethertype."""
+    from helpers import CNET_DEF, cnet_fibs, ptype_kat, ptype_ref
+    ref = ptype_ref()
+    L, F = ref["tx_offload_layout"], ref["ol_flags_type"]
+    frames = [k[0] for k in ptype_kat()]
+    # destination MACs: unicast, broadcast, multicast, on IPv4 and IPv6 frames
+    extra = []
+    for f in frames[:3] + frames[512 + 4:512 + 7]:
+        for dst in (bytes([0, 1, 2, 3, 4, 5]), b"\xff" * 6, bytes([1, 0, 0x5e, 0, 0, 1])):
+            extra.append(dst + f[6:])
+    frames = frames + extra
+    n = len(frames)
+    slab = np.frombuffer(b"".join(frames), np.uint8).copy()
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    out = O.classify(O.MODE_CNET, slab, n, stride=128, tables4=t4, tables6=t6, spec_burst=0)
+    rm = out["rxmeta"].astype(np.uint64)
+    txo = rm & np.uint64(0xFFFFFF)
+    olf = (rm >> np.uint64(29)) << np.uint64(61)
+
+    def field(v, name):
+        return (int(v) >> L[f"CNE_MBUF_{name}_LEN_OFS"]) & ((1 << L[f"CNE_MBUF_{name}_LEN_BITS"]) - 1)
+
+    for i, f in enumerate(frames):
+        _, hl = O.get_ptype(f)
+        assert (field(txo[i], "L2"), field(txo[i], "L3"), field(txo[i], "L4")) == \
+            (hl.l2_len & 0x7F, hl.l3_len & 0x1FF, hl.l4_len & 0xFF), i
+        want = F["CNE_MBUF_TYPE_IPv6"] if f[12:14] == b"\x86\xdd" else 0
+        if f[:6] == b"\xff" * 6:
+            want |= F["CNE_MBUF_TYPE_BCAST"]
+        elif f[0] & 1:
+            want |= F["CNE_MBUF_TYPE_MCAST"]
+        assert int(olf[i]) == want, (i, hex(int(olf[i])), hex(want))

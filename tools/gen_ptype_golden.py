@@ -10,7 +10,10 @@
   * cne_get_ptype's lookup tables (lib/core/pktmbuf/pktmbuf_ptype.c:279-321,
     :372-380): IPv4 version/IHL byte -> L3 type, IPv6 next header -> the
     IPv6 / IPv6-with-extensions offset, protocol -> L4 type, GRE flags ->
-    option length.  IPPROTO_* are the C library's (netinet/in.h) numbers.
+    option length.  IPPROTO_* are the C library's (netinet/in.h) numbers,
+  * what eth_rx's mbuf_update writes them into (lib/cnet/eth/eth_rx.c:35-63):
+    the tx_offload bit-field layout (the CNE_MBUF_*_BITS / _OFS enum of
+    lib/core/pktmbuf/pktmbuf_offload.h) and the CNE_MBUF_TYPE_* ol_flags bits.
 
 pktmbuf_ptype.c / ptype.c cannot be compiled here (pktmbuf.h needs
 <bsd/string.h>), so the table is taken from the text the compiler would
@@ -92,12 +95,26 @@ def main():
 
     tables = {"l3_ip_by_ihl": arr("ptype_l3_ip_proto_map"), "l4_by_proto": arr("ptype_l4_proto"),
               "ip6_ext_by_proto": arr("ip6_ext_proto_map"), "gre_opt_len": arr("opt_len")}
+    off = open(os.path.join(REF, "lib/core/pktmbuf/pktmbuf_offload.h")).read()
+    oenum = re.search(r"enum\s*\{([^}]*CNE_MBUF_L2_LEN_BITS[^}]*)\}", off, re.S).group(1)
+    layout = {}
+    for m in re.finditer(r"(CNE_MBUF_\w+)\s*=\s*([^,]+),", oenum):
+        if "sizeof" in m.group(2):
+            continue
+        expr = m.group(2)
+        for k, v in layout.items():
+            expr = re.sub(r"\b" + k + r"\b", str(v), expr)
+        assert re.fullmatch(r"[\d\s+()-]+", expr), expr
+        layout[m.group(1)] = int(eval(expr, {"__builtins__": {}}, {}))
+    olf = {m.group(1): 1 << int(m.group(2))
+           for m in re.finditer(r"#define\s+(CNE_MBUF_TYPE_\w+)\s+\(1ULL << (\d+)\)", off)}
     res = {"source": "lib/core/pktmbuf/pktmbuf_ptype.h, lib/cnet/ptype/ptype_priv.h (CNET_ENABLE_IP6=1), "
-                     "lib/cnet/ptype/ptype.c:20-46, lib/core/pktmbuf/pktmbuf_ptype.c:279-321,372-380 "
-                     "(CNDP v25.08.0)",
+                     "lib/cnet/ptype/ptype.c:20-46, lib/core/pktmbuf/pktmbuf_ptype.c:279-321,372-380, "
+                     "lib/core/pktmbuf/pktmbuf_offload.h:365-412 (CNDP v25.08.0)",
            "ptype_consts": consts, "ptype_next": edges, "pnxt_mask": mask,
            "pnxt": {f"{k:#06x}": v for k, v in sorted(table.items())},
-           "get_ptype_tables": {n: {str(k): v for k, v in sorted(t.items())} for n, t in tables.items()}}
+           "get_ptype_tables": {n: {str(k): v for k, v in sorted(t.items())} for n, t in tables.items()},
+           "tx_offload_layout": layout, "ol_flags_type": olf}
     with open(OUT, "w") as f:
         json.dump(res, f, indent=1)
     print(f"wrote {OUT}: {len(consts)} constants, {len(edges)} edges, {len(table)} table entries, mask {mask:#x}")
