@@ -247,3 +247,33 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
     want = np.array([_edge_of_queue_code(int(e)) for e in want_e])
     assert np.array_equal(got, want)
     assert set(np.unique(got).tolist()) >= {0, 3, 4, 6}   # drop, gtpu_input, ip4_forward, ip6_forward
+
+
+def test_cnet_node_edges_match_reference_names():
+    """The GPU eth_rx node's edges are exactly the reference's next nodes of
+    ptype (p_nxt edge ids -> ptype.c:213-230 names), ip4_input / ip6_input
+    (their enums, ip{4,6}_input_priv.h) plus ptype, by the names in
+    cnet_node_names.h; and cndp_node.h's input-edge ids and FIB next-index
+    shift are the reference's (tests/golden/ptype_ref.json)."""
+    import re
+    from helpers import ptype_ref
+    ref = ptype_ref()
+    nm = ref["cnet_node_names"]
+    assert ETH_RX_EDGES == [nm[k].encode() for k in (
+        "PKT_DROP_NODE_NAME", "PUNT_KERNEL_NODE_NAME", "PUNT_ETHER_NODE_NAME", "GTPU_INPUT_NODE_NAME",
+        "IP4_FORWARD_NODE_NAME", "IP4_PROTO_NODE_NAME", "IP6_FORWARD_NODE_NAME", "IP6_PROTO_NODE_NAME",
+        "PTYPE_NODE_NAME")]
+    hdr = open(os.path.join(HERE, "..", "include", "cndp_node.h")).read()
+    val = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+(CNDP_\w+)\s+(\d+)", hdr)}
+    inp = ref["input_next"]
+    for fam in ("IP4", "IP6"):
+        assert val["CNDP_INPUT_NEXT_PKT_DROP"] == inp[f"CNE_NODE_{fam}_INPUT_NEXT_PKT_DROP"]
+        assert val["CNDP_INPUT_NEXT_FORWARD"] == inp[f"CNE_NODE_{fam}_INPUT_NEXT_FORWARD"]
+        assert val["CNDP_INPUT_NEXT_PROTO"] == inp[f"CNE_NODE_{fam}_INPUT_NEXT_PROTO"]
+    assert val["CNDP_RT_NEXT_INDEX_SHIFT"] == ref["next_index_shift"]["RT4_NEXT_INDEX_SHIFT"] \
+        == ref["next_index_shift"]["RT6_NEXT_INDEX_SHIFT"]
+    # the ptype edge ids the queue reports (eth_rx_gpu.c PT_NEXT_*) are ptype_priv.h's
+    src = open(os.path.join(HERE, "..", "cndp_amd", "node", "eth_rx_gpu.c")).read()
+    pt = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+PT_NEXT_(\w+)\s+(\d+)", src)}
+    for k, v in pt.items():
+        assert ref["ptype_next"]["PTYPE_NEXT_" + k] == v, k

@@ -13,7 +13,10 @@
     option length.  IPPROTO_* are the C library's (netinet/in.h) numbers,
   * what eth_rx's mbuf_update writes them into (lib/cnet/eth/eth_rx.c:35-63):
     the tx_offload bit-field layout (the CNE_MBUF_*_BITS / _OFS enum of
-    lib/core/pktmbuf/pktmbuf_offload.h) and the CNE_MBUF_TYPE_* ol_flags bits.
+    lib/core/pktmbuf/pktmbuf_offload.h) and the CNE_MBUF_TYPE_* ol_flags bits,
+  * the cnet input nodes' edge ids (ip4_input_priv.h / ip6_input_priv.h), the
+    next-index shift of a cnet FIB value (cnet_route4.h / cnet_route6.h) and the
+    cnet node names (lib/cnet/incs/cnet_node_names.h).
 
 pktmbuf_ptype.c / ptype.c cannot be compiled here (pktmbuf.h needs
 <bsd/string.h>), so the table is taken from the text the compiler would
@@ -108,13 +111,30 @@ def main():
         layout[m.group(1)] = int(eval(expr, {"__builtins__": {}}, {}))
     olf = {m.group(1): 1 << int(m.group(2))
            for m in re.finditer(r"#define\s+(CNE_MBUF_TYPE_\w+)\s+\(1ULL << (\d+)\)", off)}
+    inp = {}
+    for f, en in (("lib/cnet/ipv4/ip4_input_priv.h", "cne_node_ip4_input_next"),
+                  ("lib/cnet/ipv6/ip6_input_priv.h", "cne_node_ip6_input_next")):
+        t = open(os.path.join(REF, f)).read()
+        body = re.search(r"enum\s+" + en + r"\s*\{(.*?)\}", t, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        for i, nm in enumerate(x.strip() for x in body.split(",") if x.strip()):
+            inp[nm] = i
+    shift = {}
+    for f, nm in (("lib/cnet/route/cnet_route4.h", "RT4_NEXT_INDEX_SHIFT"),
+                  ("lib/cnet/route/cnet_route6.h", "RT6_NEXT_INDEX_SHIFT")):
+        shift[nm] = int(re.search(r"#define\s+" + nm + r"\s+(\d+)", open(os.path.join(REF, f)).read()).group(1))
+    names = dict(re.findall(r'#define\s+(\w+_NODE_NAME)\s+"([^"]+)"',
+                            open(os.path.join(REF, "lib/cnet/incs/cnet_node_names.h")).read()))
     res = {"source": "lib/core/pktmbuf/pktmbuf_ptype.h, lib/cnet/ptype/ptype_priv.h (CNET_ENABLE_IP6=1), "
                      "lib/cnet/ptype/ptype.c:20-46, lib/core/pktmbuf/pktmbuf_ptype.c:279-321,372-380, "
-                     "lib/core/pktmbuf/pktmbuf_offload.h:365-412 (CNDP v25.08.0)",
+                     "lib/core/pktmbuf/pktmbuf_offload.h:365-412, "
+                     "lib/cnet/ipv{4,6}/ip{4,6}_input_priv.h, lib/cnet/route/cnet_route{4,6}.h:28, "
+                     "lib/cnet/incs/cnet_node_names.h (CNDP v25.08.0)",
            "ptype_consts": consts, "ptype_next": edges, "pnxt_mask": mask,
            "pnxt": {f"{k:#06x}": v for k, v in sorted(table.items())},
            "get_ptype_tables": {n: {str(k): v for k, v in sorted(t.items())} for n, t in tables.items()},
-           "tx_offload_layout": layout, "ol_flags_type": olf}
+           "tx_offload_layout": layout, "ol_flags_type": olf,
+           "input_next": inp, "next_index_shift": shift, "cnet_node_names": names}
     with open(OUT, "w") as f:
         json.dump(res, f, indent=1)
     print(f"wrote {OUT}: {len(consts)} constants, {len(edges)} edges, {len(table)} table entries, mask {mask:#x}")
