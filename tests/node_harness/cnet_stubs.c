@@ -76,6 +76,11 @@ void harness_cnet_set(struct cne_fib *fib4, struct cne_fib6 *fib6)
 /* pkt_ctrl.c:55-72: node nid receives from port port_id */
 int harness_eth_rx_port(cne_node_t nid, uint16_t port_id)
 {
+    for (eth_rx_node_elem_t *e = eth_rx_get_node_data_get()->head; e; e = e->next)
+        if (e->nid == nid) { /* re-registration (a later test): update */
+            e->ctx.port_id = port_id;
+            return 0;
+        }
     struct eth_rx_node_main *m = eth_rx_get_node_data_get();
     eth_rx_node_elem_t *e = calloc(1, sizeof(*e));
     if (!e)

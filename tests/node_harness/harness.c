@@ -7,6 +7,7 @@
  * the objects each node enqueues -- the way graph_test.c (test/testcne) drives
  * fake nodes without a NIC.
  */
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -84,6 +85,38 @@ int harness_node_info(int i, char *name, uint64_t *flags, int *nb_edges, const c
     *e0 = regs[i]->nb_edges > 0 ? regs[i]->next_nodes[0] : NULL;
     *e1 = regs[i]->nb_edges > 1 ? regs[i]->next_nodes[1] : NULL;
     return n_regs;
+}
+
+/* cne_node_clone (cne_graph.h): a node "<name>-<suffix>" with the parent's
+ * callbacks and edges and a context of its own, as pkt_ctrl.c:61 makes one
+ * eth_rx per port; returns its id */
+cne_node_t harness_clone(const char *name, const char *suffix)
+{
+    const int i = find(name);
+    if (i < 0 || n_regs == MAX_REG)
+        return CNE_NODE_ID_INVALID;
+    const size_t sz = sizeof(struct cne_node_register) + regs[i]->nb_edges * sizeof(const char *);
+    struct cne_node_register *r = malloc(sz);
+    if (!r)
+        return CNE_NODE_ID_INVALID;
+    memcpy(r, regs[i], sz);
+    char nm[2 * CNE_NODE_NAMESIZE + 2];
+    snprintf(nm, sizeof(nm), "%s-%s", regs[i]->name, suffix);
+    memcpy(r->name, nm, CNE_NODE_NAMESIZE - 1);
+    r->name[CNE_NODE_NAMESIZE - 1] = 0;
+    r->parent_id = regs[i]->id;
+    r->id = (cne_node_t)n_regs;
+    regs[n_regs] = r;
+    return (cne_node_t)n_regs++;
+}
+
+/* forget the clones (back to the registered nodes) */
+void harness_drop_clones(void)
+{
+    while (n_regs > 0 && regs[n_regs - 1]->parent_id != CNE_NODE_ID_INVALID) {
+        free((void *)regs[n_regs - 1]);
+        n_regs--;
+    }
 }
 
 /* graph create: init every registered node (graph id gid) */

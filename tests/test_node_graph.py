@@ -277,3 +277,51 @@ def test_cnet_node_edges_match_reference_names():
     pt = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+PT_NEXT_(\w+)\s+(\d+)", src)}
     for k, v in pt.items():
         assert ref["ptype_next"]["PTYPE_NEXT_" + k] == v, k
+
+
+@pytest.mark.gpu
+def test_cnet_node_clones_per_port(gpu):
+    """Two ports, one eth_rx clone each (cne_node_clone + the {port, nid}
+    list, as pkt_ctrl.c:55-72 sets them up): every mbuf leaves by its edge
+    with lport = its port, and each clone keeps its own ptype-node state
+    (the oracle runs the two ports' burst streams separately)."""
+    from helpers import CNET_DEF, cnet_fibs
+    from oracle import oracle as O
+    from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
+    H = _cnet_harness()
+    H.harness_clone.restype = ctypes.c_uint32
+    H.harness_clone.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    L = N.lib()
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    n = 16000
+    half = n // 2 + 100   # the ports' streams end on different burst boundaries
+    pool, orig = cnet_pool(n, routes, v6, zero_copy=False)
+    parts = ((3, np.arange(half)), (5, np.arange(half, n)))
+    refs = [_cnet_expect(pool, idx, _bursts(len(idx), 0, "full"), t4, t6, 0, p) for p, idx in parts]
+    ref = {k: np.concatenate([r[k] for r in refs]) for k in refs[0]}
+    L.cndp_node_gpu_umem_reset()
+    H.harness_cnet_set(fib.h, fib6.h)
+    assert H.harness_eth_rx_port(0, 7) == 0   # the parent node (also in the graph here) on an idle port
+    try:
+        for p, idx in parts:
+            nid = H.harness_clone(b"eth_rx", str(p).encode())
+            assert nid != 0xFFFFFFFF
+            assert H.harness_eth_rx_port(nid, p) == 0
+            assert H.harness_rx_load(p, pool.ptrs(idx), len(idx)) == 0
+        assert H.harness_graph_create(7) == 0
+        assert H.harness_walk_until(n) >= 0
+        assert H.harness_rx_left(3) == 0 and H.harness_rx_left(5) == 0 and H.harness_total() == n
+        got = np.full(n, -1, np.int64)
+        buf = (ctypes.c_void_p * n)()
+        for k, name in enumerate(ETH_RX_EDGES):
+            m = H.harness_take_edge(name, buf, n)
+            got[pool.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))] = k
+    finally:
+        H.harness_graph_destroy()
+        H.harness_drop_clones()
+    lport = np.concatenate([np.full(len(idx), p) for p, idx in parts])
+    want_e = cnet_check(pool, orig, ref, t4, t6, lport)
+    want = np.array([_edge_of_queue_code(int(e)) for e in want_e])
+    assert np.array_equal(got, want)
