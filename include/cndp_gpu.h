@@ -148,8 +148,13 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  * outside the region with -EINVAL; an mbuf whose buffer points outside it
  * comes back untouched with edge CNDP_MQ_EDGE_NONE).  With conf.umem NULL,
  * the host copies each frame into pinned staging (ip4_lookup: 64 B, enough for
- * every byte the node reads; cnet: the buffer from data_off to buf_len, at
- * most conf.stage_max bytes) and poll writes the results back.
+ * every byte the node reads; cnet: 128 B for a frame whose header walk stays
+ * there -- Ethernet with at most one tag, then IPv4 or IPv6 without extension
+ * headers carrying TCP / UDP / SCTP, an IPv4 fragment, ARP or MPLS -- else the
+ * buffer from data_off to buf_len, at most conf.stage_max bytes) and poll
+ * writes the results back.  Bytes past a frame's buffer, which the reference
+ * parse reads only for malformed extension-header lengths, are the next
+ * staged frame's here (undefined in the reference either way).
  * Completion is a flag the batch's last kernel raises in pinned memory, so
  * poll costs a load, not a HIP call.
  *
@@ -198,7 +203,7 @@ struct cndp_mq_conf {
     uint32_t batch;        /* mbufs per GPU launch, >= 256 (0 = 8192) */
     uint32_t depth;        /* batches in flight, 2..16 (0 = 4) */
     uint32_t max_delay_us; /* a partly filled batch launches at this age (0 = 50 us) */
-    uint32_t stage_max;    /* cnet staged mode: bytes copied per frame (0 = 2048) */
+    uint32_t stage_max;    /* cnet staged mode: most bytes copied per frame (0 = 2048) */
     void *umem;            /* registered region the mbufs live in, or NULL */
     uint16_t lport;        /* cnet: m->lport (eth_rx.c:59) */
     uint16_t rsvd[3];
