@@ -200,6 +200,7 @@ __device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip
 //       before the first dependent LPM gather: more bytes in flight).
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); // dword-aligned 16-B load
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool NT>
@@ -5260,28 +5261,34 @@ __device__ __forceinline__ void mq_hdr(const MqArgs &a, uint64_t m, uint64_t &fo
     ok = fo < a.slab_len;
 }
 
+// node-queue kernels: one wave per block, so a batch spreads over 4x the CUs
+// (in place, each mbuf costs dependent PCIe reads; more CUs keep more in flight)
+#define MQ_TPB 64u
+
 // ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
 // mtod + 14 + 16, priv1 = {nh = val & 0xffff, ttl, hdr_checksum}, edge = val >> 16
-__global__ __launch_bounds__(256) void k_mq_ip4_lookup(MqArgs a)
+__global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
-        uint64_t base;
+    for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
+        uint64_t base, m = 0;
         bool ok = true;
         if (a.zc) {
             uint32_t doff, blen, dlen;
-            mq_hdr(a, a.ptrs[i], base, doff, blen, dlen, ok);
+            m = a.ptrs[i]; // read once: the priv1 store below reuses it
+            mq_hdr(a, m, base, doff, blen, dlen, ok);
         } else {
             base = a.off[i];
         }
         const uint8_t *p = a.slab + base;
         const uint64_t avail = ok && base < a.slab_len ? a.slab_len - base : 0;
         uint32_t ttl, ck, dip;
-        if (avail >= 36 && (((uintptr_t)p) & 15u) == 0) { // two loads (one PCIe read each in place)
-            const u32x4 q = *(const u32x4 *)(p + 16);      // bytes 16..31
-            const uint32_t w8 = *(const uint32_t *)(p + 32);
-            ttl = (q.y >> 16) & 0xffu;
-            ck = q.z & 0xffffu;
-            dip = bswap32(alignb(w8, q.w, 2));
+        if (avail >= 36 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p + 20u) & 63u) <= 48u) {
+            // bytes 20..35 (ttl, checksum, dst) in one load inside one 64-B
+            // line: one PCIe read per frame when the mbuf is read in place
+            const u32x4a4 q = *(const u32x4a4 *)(p + 20);
+            ttl = (q.x >> 16) & 0xffu;
+            ck = q.y & 0xffffu;
+            dip = bswap32(alignb(q.w, q.z, 2));
         } else {
             ttl = gbyte(p, avail, 22);
             ck = gbyte(p, avail, 24) | (gbyte(p, avail, 25) << 8);
@@ -5292,7 +5299,7 @@ __global__ __launch_bounds__(256) void k_mq_ip4_lookup(MqArgs a)
         const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
         if (a.zc) {
             if (ok)
-                *(uint64_t *)(a.ptrs[i] + a.delta + MB_UDATA64) = priv1;
+                *(uint64_t *)(m + a.delta + MB_UDATA64) = priv1;
             a.edges[i] = ok ? (uint16_t)(val >> 16) : (uint16_t)MQ_EDGE_NONE;
         } else {
             a.priv1[i] = priv1;
@@ -5306,9 +5313,9 @@ __global__ __launch_bounds__(256) void k_mq_ip4_lookup(MqArgs a)
 // swap_mac_addresses (main.h:303-315) at pktmbuf_mtod of every mbuf, then tx.
 // Zero-copy: in the frame where it lies; staged: in the staged window, which
 // poll copies back.  Every mbuf leaves by edge 0 (tx).
-__global__ __launch_bounds__(256) void k_mq_mac_swap(MqArgs a)
+__global__ __launch_bounds__(MQ_TPB) void k_mq_mac_swap(MqArgs a)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+    for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
         uint64_t base;
         bool ok = true;
         if (a.zc) {
@@ -5340,9 +5347,9 @@ __global__ __launch_bounds__(256) void k_mq_mac_swap(MqArgs a)
 }
 
 // zero-copy cnet: frame offsets and length fields from the mbuf headers
-__global__ __launch_bounds__(256) void k_mq_cnet_pre(MqArgs a, uint64_t *off)
+__global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_pre(MqArgs a, uint64_t *off)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+    for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
         uint64_t fo;
         uint32_t doff, blen, dlen;
         bool ok;
@@ -5394,9 +5401,9 @@ __device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t
 // speculation only sends a frame to the edge of a type with the same low
 // byte (ptype.c:109-110).  Zero-copy: the eth_rx fields (eth_rx.c:35-63) and
 // data_len go straight into the mbuf; staged: into records for poll.
-__global__ __launch_bounds__(256) void k_mq_cnet_post(MqArgs a)
+__global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u) {
+    for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
         const uint32_t pt = a.ptype[i], rm = a.rxmeta[i], e8 = a.edge8[i];
         const u32x2 ln = a.lens[i];
         const uint32_t dl = ln.x & 0xffffu, room = ln.x >> 16, blen = ln.y & 0xffffu, doff = ln.y >> 16;
@@ -5669,19 +5676,19 @@ static int mq_launch(cndp_gpu_mq_t *q)
     a.flag = q->flags_d + slot_i * 16u;
     sl->seq = ++q->seq;
     a.seq = sl->seq;
-    const uint32_t g = blocks_for(n, 256);
+    const uint32_t g = blocks_for(n, MQ_TPB);
     if (q->conf.mode == CNDP_MQ_MAC_SWAP) {
-        hipLaunchKernelGGL(k_mq_mac_swap, dim3(g), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mq_mac_swap, dim3(g), dim3(MQ_TPB), 0, s, a);
         HIP_TRY(hipGetLastError());
     } else if (!cnet) {
         if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
         a.tb = mq_tables(c, 0);
-        hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
         HIP_TRY(hipGetLastError());
     } else {
         if (zc) {
-            hipLaunchKernelGGL(k_mq_cnet_pre, dim3(g), dim3(256), 0, s, a, (uint64_t *)(D + q->d_off));
+            hipLaunchKernelGGL(k_mq_cnet_pre, dim3(g), dim3(MQ_TPB), 0, s, a, (uint64_t *)(D + q->d_off));
             HIP_TRY(hipGetLastError());
         }
         // one classify per run of equal-size graph bursts, the ptype node's
@@ -5715,7 +5722,7 @@ static int mq_launch(cndp_gpu_mq_t *q)
         a.hash = (const uint32_t *)(D + q->d_hash);
         a.edge8 = D + q->d_edge;
         a.tb = mq_tables(c, sl->buf_len);
-        hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(MQ_TPB), 0, s, a);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(sl->ev, s));
