@@ -201,6 +201,7 @@ __device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); // dword-aligned 16-B load
+typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool NT>
@@ -5419,7 +5420,11 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
             node = v6 ? CNDP_MQ_NODE_IP6 : CNDP_MQ_NODE_IP4;
             e = e8;
             const uint64_t o = a.off[i] + (adj ? l2 : 0u);
-            dlen = (gbyte(a.slab, a.slab_len, o + (v6 ? 4u : 2u)) << 8) | gbyte(a.slab, a.slab_len, o + (v6 ? 5u : 3u));
+            const uint64_t lo = o + (v6 ? 4u : 2u);
+            if ((lo & 1u) == 0 && lo + 2 <= a.slab_len) // one read (one PCIe read in place)
+                dlen = bswap16(*(const uint16_t *)(a.slab + lo));
+            else
+                dlen = (gbyte(a.slab, a.slab_len, lo) << 8) | gbyte(a.slab, a.slab_len, lo + 1);
             if (!adj || blen != a.tb.buf_len)
                 e = mq_input_at(a.slab, a.slab_len, o, v6, a.tb, blen) >> 24;
         }
@@ -5427,11 +5432,12 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
         if (a.zc) {
             const uint64_t m = a.ptrs[i] + a.delta;
             if (a.off[i] < a.slab_len) {
-                // data_off, lport, buf_len, data_len in one 8-B store
-                *(uint64_t *)(m + MB_DATA_OFF) = (uint64_t)(adj ? doff + l2 : doff) |
-                                                 ((uint64_t)a.lport << 16) | ((uint64_t)blen << 32) |
-                                                 ((uint64_t)(dlen & 0xffffu) << 48);
-                *(uint32_t *)(m + MB_PTYPE) = pt;
+                // data_off, lport, buf_len, data_len, packet_type in one 12-B store
+                u32x3a4 w;
+                w.x = (adj ? doff + l2 : doff) | (a.lport << 16);
+                w.y = blen | ((dlen & 0xffffu) << 16);
+                w.z = pt;
+                *(u32x3a4 *)(m + MB_DATA_OFF) = w;
                 u32x4 tol; // tx_offload = l2 | l3 << 7 | l4 << 16, ol_flags = MCAST/BCAST/IPv6 bits 61..63
                 tol.x = rm & 0xffffffu;
                 tol.y = 0u;
