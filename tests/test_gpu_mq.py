@@ -71,11 +71,15 @@ def _mixed_l3_frames(n, seed):
 
 
 @pytest.mark.parametrize("zero_copy", [True, False])
-@pytest.mark.parametrize("kind", ["full", "ragged"])
+@pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
+    """"shifted": data_off = 256 + (i mod 61), so frames start at every
+    alignment and line position (the kernel's one-load and byte-wise reads)."""
     cl, fib, t4 = l3
     n = 20000
     pool = MbufPool(n)
+    if kind == "shifted":
+        pool.hdr["data_off"] = 256 + np.arange(n) % 61
     fr = _mixed_l3_frames(n, seed=3 if kind == "full" else 4)
     pool.fill(fr)
     pool.hdr["udata64"] = 0xABABABABABABABAB
@@ -159,20 +163,22 @@ def _no_reach_past_buffer(pool, idx, donor):
     return n_rep
 
 
-def cnet_pool(n, routes, v6, zero_copy):
+def cnet_pool(n, routes, v6, zero_copy, shift=False):
     """IMIX mbufs, every 3rd a fuzz frame (VLAN, QinQ, ext headers, tunnels,
     bad IHL ...), every 7th a GTP-U / GTP-C / TCP frame in a UDP run (the
     fix_spec quirk), every 5th a runt (data_len 10: pktmbuf_adj_offset(l2_len)
-    is skipped).  Returns the pool and a copy of its headers."""
-    pool = MbufPool(n)
+    is skipped); shift: data_off = 256 + (i mod 61), frames at every
+    alignment.  Returns the pool and a copy of its headers."""
+    pool, pf, pg = MbufPool(n), MbufPool(n), MbufPool(n)
+    if shift:
+        for p in (pool, pf, pg):
+            p.hdr["data_off"] = 256 + np.arange(n) % 61
     imx = pktgen.imix(n, v4routes=routes, v6routes=v6, seed=11, v6_frac=0.4)
     fz = pktgen.fuzz_frames(n, seed=12, slot=128)
     from test_gpu_parity import _gtp_mix
     gt = _gtp_mix(n, routes, v6, "cpu", seed=14)
     pool.fill(imx)
-    pf = MbufPool(n)
     pf.fill(fz)
-    pg = MbufPool(n)
     pg.fill(gt)
     for i in range(0, n, 3):
         pool.mem[i * 2048:(i + 1) * 2048] = pf.mem[i * 2048:(i + 1) * 2048]
@@ -237,11 +243,11 @@ def cnet_check(pool, orig, ref, t4, t6, lport):
 
 
 @pytest.mark.parametrize("zero_copy", [True, False])
-@pytest.mark.parametrize("kind", ["full", "ragged"])
+@pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_cnet(cn, gpu, zero_copy, kind):
     cl, routes, v6, t4, t6 = cn
     n = 24000
-    pool, orig = cnet_pool(n, routes, v6, zero_copy)
+    pool, orig = cnet_pool(n, routes, v6, zero_copy, shift=kind == "shifted")
     umem = None
     flags = N.CNDP_MQ_F_HASH if kind == "ragged" else 0
     if zero_copy:
