@@ -5162,7 +5162,7 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 #define MQ_RUNS_MAX 512u    // cnet: runs of equal-size bursts per batch
 #define MQ_EDGE_NONE 0xFFFFu // zero-copy: an mbuf whose buffer is outside the region
 #define MQ_SHORT 128u       // cnet staged bytes of a frame whose parse stays in its first 128
-#define MQ_PF 8u            // staged: mbufs prefetched ahead in the host loops
+#define MQ_PF 32u           // staged: mbufs prefetched ahead in the host loops (8 / 16 / 32 swept: tools/pf_sweep.sh)
 
 // Staged cnet: whether a frame's bytes past its first MQ_SHORT can matter.
 // cne_get_ptype (pktmbuf_ptype.c:472-615) stops early for ARP and MPLS, and
