@@ -31,12 +31,21 @@ BUF_LEN = FRAME - HDR   # 1984
 
 class MbufPool:
     """n mbufs in one page-aligned host buffer (optionally registered with a
-    Classifier for zero-copy)."""
+    Classifier for zero-copy).  hugepages: an anonymous mapping advised for
+    2 MiB transparent huge pages, 2 MiB-aligned, as a UMEM from CNDP's
+    mmap_alloc(MMAP_HUGEPAGE_2MB) would be (lib/core/mmap/cne_mmap.h:29)."""
 
-    def __init__(self, n: int):
+    def __init__(self, n: int, hugepages: bool = False):
         self.n = n
-        raw = np.zeros(n * FRAME + 4096, np.uint8)
-        a = (-raw.ctypes.data) % 4096
+        if hugepages:
+            import mmap
+            self._mm = mmap.mmap(-1, n * FRAME + (2 << 20), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+            self._mm.madvise(mmap.MADV_HUGEPAGE)
+            raw = np.frombuffer(self._mm, np.uint8)
+            a = (-raw.ctypes.data) % (2 << 20)
+        else:
+            raw = np.zeros(n * FRAME + 4096, np.uint8)
+            a = (-raw.ctypes.data) % 4096
         self._raw = raw
         self.mem = raw[a:a + n * FRAME]
         self.base = self.mem.ctypes.data

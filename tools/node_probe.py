@@ -31,12 +31,12 @@ f6 = Fib6("np6", N.CNE_FIB_TRIE, default_nh=1025, max_routes=1024, nh_sz=N.CNE_F
 for ip, d, i in v6:
     node_ip6_add_input(f6, ip, d, i)
 cl.set_fib(f4, f6)
-pool = MbufPool(nc)
+pool = MbufPool(nc, hugepages=mode.endswith("hp"))
 pool.fill(pktgen.imix(nc, v4routes=routes, v6routes=v6, seed=98))
 ptrs = pool.ptrs(np.arange(nc))
 hdr0 = pool.hdr.copy()
 umem = None
-if mode == "zc":
+if mode.startswith("zc"):
     cl.host_register(pool.mem)
     umem = pool.base
 for batch in (8192, 32768):

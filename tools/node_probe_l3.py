@@ -27,11 +27,11 @@ for ip, d, nh in routes:
     cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
 cl = Classifier(0)
 cl.set_fib(NodeFib())
-pool = MbufPool(n)
+pool = MbufPool(n, hugepages=mode.endswith("hp"))
 pool.fill(pktgen.packed_ipv4(n, routes=routes, seed=99))
 ptrs = pool.ptrs(np.arange(n))
 umem = None
-if mode == "zc":
+if mode.startswith("zc"):
     cl.host_register(pool.mem)
     umem = pool.base
 for batch in (8192, 32768):
