@@ -123,6 +123,8 @@ struct KArgs {
     uint32_t n_bins;
     uint32_t *ptype;   // optional: packet_type per frame
     uint32_t *rxmeta;  // optional (cnet): eth_rx lengths + ol_flags, packed (cndp_gpu.h)
+    uint32_t *iplen;   // node queue (cnet): 1 << 16 | IPv4 total_length / IPv6 payload_len
+                       // of the frames the fast path parsed (the rest left 0)
     uint32_t *spec_nh; // cnet speculation model: input-node result of every frame a
                        // ptype-node group could send to ip4/ip6_input (else ~0)
     uint32_t *spec_flags; // 2048-bit set of the type signatures seen (speculation model)
@@ -1420,6 +1422,7 @@ __device__ __forceinline__ void cs_issue(const KArgs &a, uint32_t tt, uint32_t n
 struct CdLane {
     uint32_t ptf;  // pt (16) | do4 << 16 | do6 << 17 | fast << 18 | p_nxt edge << 19
     uint32_t h, e, rx;
+    uint32_t ipl; // META: 1 << 16 | the IP length field (KArgs::iplen)
     // the chain's key bytes after the first gather, next byte lowest: v6
     // address bytes 3..15 (trie.h:127-134); v4 dip bits 15:8 then 7:0 with
     // the /16 directory, bits 7:0 without (dir24_8.h:135-140)
@@ -1529,6 +1532,8 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                          : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
             na.rx = rx_meta(lens, W[0], W[1], et);
         }
+        if (META && a.iplen) // at mtod + l2_len 2 / 4 (ip4_input.c:121-124, ip6_input.c:121-124)
+            na.ipl = (1u << 16) | bswap16(f4 ? (W[4] & 0xffffu) : (W[4] >> 16));
         uint32_t flags = 0;
         // Toeplitz, one instruction stream for both families: the v6 words
         // are V[0..7] + L4 V[8], the v4 ones V[1..2] + L4 V[3] (a zero word
@@ -1629,6 +1634,8 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 __builtin_nontemporal_store(pt, &at32(a.ptype, ib));
             if (META && a.rxmeta)
                 __builtin_nontemporal_store(sb.rx, &at32(a.rxmeta, ib));
+            if (META && a.iplen)
+                __builtin_nontemporal_store(sb.ipl, &at32(a.iplen, ib));
             // non-temporal stores: the outputs are written once and must not
             // push the FIB tables of the gather chains out of L2 (C4 -4.5%)
             if (a.nh)
@@ -3487,6 +3494,7 @@ __global__ __launch_bounds__(PART_THREADS) void k_part_scatter(const uint16_t *_
 #define CNDP_MAX_REGIONS 16
 struct cndp_gpu_ctx {
     int dev;
+    uint32_t *mq_iplen; // set by the node queue around its classify calls (KArgs::iplen)
     uint8_t key[CNDP_RSS_KEY_LEN];
     uint32_t *d_ttab;     // 36 x 256
     uint16_t *d_reta;
@@ -4275,6 +4283,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
     a.n_bins = b->n_bins;
     a.ptype = b->ptype;
     a.rxmeta = b->mode == CNDP_MODE_CNET ? b->rxmeta : nullptr;
+    a.iplen = b->mode == CNDP_MODE_CNET && b->rxmeta ? c->mq_iplen : nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (b->mode == CNDP_MODE_CNET) {
         if ((r = scratch_acquire(c, s)))
@@ -5226,6 +5235,7 @@ struct MqArgs {
     // cnet classify outputs (device)
     const uint32_t *ptype, *rxmeta, *hash;
     const uint8_t *edge8;
+    uint32_t *iplen;        // cnet: the IP length fields the parse read (0: read the frame); cleared here
     uint32_t lport, want_hash;
     MqTables tb;
     uint32_t *ticket;       // device arrival counter of this slot
@@ -5407,6 +5417,12 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
         const uint32_t pt = a.ptype[i], rm = a.rxmeta[i], e8 = a.edge8[i];
         const u32x2 ln = a.lens[i];
+        uint32_t ipl = 0;
+        if (a.iplen) { // consumed: the next batch's fast path writes only its own frames
+            ipl = a.iplen[i];
+            if (ipl)
+                a.iplen[i] = 0u;
+        }
         const uint32_t dl = ln.x & 0xffffu, room = ln.x >> 16, blen = ln.y & 0xffffu, doff = ln.y >> 16;
         const uint32_t l2 = rm & 0x7fu;
         const bool adj = l2 <= dl && l2 <= room;
@@ -5421,7 +5437,9 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
             e = e8;
             const uint64_t o = a.off[i] + (adj ? l2 : 0u);
             const uint64_t lo = o + (v6 ? 4u : 2u);
-            if ((lo & 1u) == 0 && lo + 2 <= a.slab_len) // one read (one PCIe read in place)
+            if (adj && ipl) // the parse's read of the same field (no second read of the frame)
+                dlen = ipl & 0xffffu;
+            else if ((lo & 1u) == 0 && lo + 2 <= a.slab_len) // one read (one PCIe read in place)
                 dlen = bswap16(*(const uint16_t *)(a.slab + lo));
             else
                 dlen = (gbyte(a.slab, a.slab_len, lo) << 8) | gbyte(a.slab, a.slab_len, lo + 1);
@@ -5488,7 +5506,7 @@ struct cndp_gpu_mq {
     uint32_t *tickets;             // device, one per slot
     // byte offsets inside each slot's pinned block (H) and device block (D)
     uint64_t h_ptr, h_len, h_edge, h_rec, h_stage, h_bytes;
-    uint64_t d_off, d_len, d_nh, d_edge, d_pt, d_rm, d_hash, d_bytes;
+    uint64_t d_off, d_len, d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_bytes;
     uint32_t head, open, in_flight, seq; // head: oldest slot not fully polled
     uint32_t pending;
     MqSlot slot[CNDP_MQ_DEPTH_MAX];
@@ -5559,7 +5577,8 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->d_pt = q->d_edge + al64(B);
     q->d_rm = q->d_pt + al64(B * 4);
     q->d_hash = q->d_rm + al64(B * 4);
-    q->d_bytes = cnet ? q->d_hash + al64(B * 4) : 64;
+    q->d_ipl = q->d_hash + al64(B * 4);
+    q->d_bytes = cnet ? q->d_ipl + al64(B * 4) : 64;
     r = -ENOMEM;
     if (hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) != hipSuccess)
         goto fail;
@@ -5575,9 +5594,13 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
         if (!sl->mb || hipHostMalloc((void **)&sl->h, q->h_bytes, hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void **)&sl->hd, sl->h, 0) != hipSuccess ||
             hipMalloc((void **)&sl->d, q->d_bytes) != hipSuccess ||
+            hipMemset(sl->d, 0, q->d_bytes) != hipSuccess || // iplen starts cleared
             hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess)
             goto fail;
     }
+    // the clears done before the queue's own (non-blocking) stream first runs
+    if (hipDeviceSynchronize() != hipSuccess)
+        goto fail;
     *out = q;
     return 0;
 fail:
@@ -5717,7 +5740,9 @@ static int mq_launch(cndp_gpu_mq_t *q)
             b.rxmeta = (uint32_t *)(D + q->d_rm) + i0;
             b.hash = a.want_hash ? (uint32_t *)(D + q->d_hash) + i0 : nullptr;
             c->spec_burst = saved_B ? sl->run_B[k] : 0u;
+            c->mq_iplen = (uint32_t *)(D + q->d_ipl) + i0;
             r = cndp_gpu_classify(c, &b, s);
+            c->mq_iplen = nullptr;
             i0 += sl->run_n[k];
         }
         c->spec_burst = saved_B;
@@ -5727,6 +5752,7 @@ static int mq_launch(cndp_gpu_mq_t *q)
         a.rxmeta = (const uint32_t *)(D + q->d_rm);
         a.hash = (const uint32_t *)(D + q->d_hash);
         a.edge8 = D + q->d_edge;
+        a.iplen = (uint32_t *)(D + q->d_ipl);
         a.tb = mq_tables(c, sl->buf_len);
         hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(MQ_TPB), 0, s, a);
         HIP_TRY(hipGetLastError());
