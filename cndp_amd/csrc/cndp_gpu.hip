@@ -98,6 +98,11 @@ __device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_
 #define CNDP_RW_MAX_PORTS CNDP_IP4_REWRITE_MAX_PORTS // CNE_MAX_ETHPORTS
 // struct cndp_rw_nh = struct ip4_rewrite_nh_header (node_internal.h)
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); // dword-aligned 16-B load
+typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 struct KArgs {
     const uint8_t *slab;
     uint64_t slab_len;
@@ -125,6 +130,8 @@ struct KArgs {
     uint32_t *rxmeta;  // optional (cnet): eth_rx lengths + ol_flags, packed (cndp_gpu.h)
     uint32_t *iplen;   // node queue (cnet): 1 << 16 | IPv4 total_length / IPv6 payload_len
                        // of the frames the fast path parsed (the rest left 0)
+    u32x4 *win;        // node queue (zero-copy cnet): each frame's first 64 bytes as parsed
+                       // (4 x 16 B per frame), the source of the cnet_metadata addresses
     uint32_t *spec_nh; // cnet speculation model: input-node result of every frame a
                        // ptype-node group could send to ip4/ip6_input (else ~0)
     uint32_t *spec_flags; // 2048-bit set of the type signatures seen (speculation model)
@@ -201,10 +208,6 @@ __device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip
 //   U   packets per lane per loop trip (U = 2 issues both frames' loads
 //       before the first dependent LPM gather: more bytes in flight).
 // ---------------------------------------------------------------------------
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); // dword-aligned 16-B load
-typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool NT>
 __device__ __forceinline__ u32x4 ldg4(const uint8_t *p)
@@ -1194,6 +1197,9 @@ __device__ __forceinline__ void cnet_general(const KArgs &a, uint64_t i, uint32_
             row[k] = gld32(p, avail, 4u * (uint32_t)k);
     }
     const Win w{row, p, avail};
+    if (a.win) // the node queue's metadata source (k_mq_cnet_post)
+        for (int k = 0; k < 4; k++)
+            a.win[4 * i + k] = (u32x4){row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]};
     Lens ln;
     const uint32_t pt = get_ptype(w, ln);
     if (a.ptype)
@@ -1534,6 +1540,12 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         }
         if (META && a.iplen) // at mtod + l2_len 2 / 4 (ip4_input.c:121-124, ip6_input.c:121-124)
             na.ipl = (1u << 16) | bswap16(f4 ? (W[4] & 0xffffu) : (W[4] >> 16));
+        if (META && a.win) { // the node queue's metadata source (k_mq_cnet_post)
+            u32x4 *dw = a.win + 4ull * i;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                dw[k] = (u32x4){W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
+        }
         uint32_t flags = 0;
         // Toeplitz, one instruction stream for both families: the v6 words
         // are V[0..7] + L4 V[8], the v4 ones V[1..2] + L4 V[3] (a zero word
@@ -3495,6 +3507,7 @@ __global__ __launch_bounds__(PART_THREADS) void k_part_scatter(const uint16_t *_
 struct cndp_gpu_ctx {
     int dev;
     uint32_t *mq_iplen; // set by the node queue around its classify calls (KArgs::iplen)
+    u32x4 *mq_win;      // ... and KArgs::win (zero-copy cnet: the windows the metadata comes from)
     uint8_t key[CNDP_RSS_KEY_LEN];
     uint32_t *d_ttab;     // 36 x 256
     uint16_t *d_reta;
@@ -3512,6 +3525,8 @@ struct cndp_gpu_ctx {
     int tune_cnet_tile;   // CNDP_TUNE_CNET_TILE
     int tune_lnt;         // CNDP_TUNE_LOAD_NT
     int tune_spec_scan;   // CNDP_TUNE_SPEC_SCAN
+    int tune_cnet_fold;   // CNDP_TUNE_CNET_FOLD: 0 hint, 1 always, 2 never
+    int tune_spec_grid;   // CNDP_TUNE_SPEC_GRID: 0 hint, 1 shrunk (2 blocks), 2 full
     int sf_clean, wl_clean; // signature flags / worklist count known zero (no memset needed)
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
@@ -3525,10 +3540,12 @@ struct cndp_gpu_ctx {
     hipEvent_t ev_scratch;
     hipStream_t scratch_stream;
     int scratch_used;
-    // host regions registered with cndp_gpu_host_register (zero-copy mbuf queues)
+    // host regions registered through this context (zero-copy mbuf queues),
+    // each holding `refs` references on the process-wide registration
     struct {
         uint8_t *host, *dev;
         uint64_t len;
+        int refs;
     } reg[CNDP_MAX_REGIONS];
     int n_reg;
     uint32_t *sp_small;   // [0] last_type, [1..65] class meta, [66..129] signature flags
@@ -3683,8 +3700,8 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         return;
     hipSetDevice(c->dev);
     hipDeviceSynchronize(); // nothing in flight may still use the scratch below
-    for (int k = 0; k < c->n_reg; k++) // regions registered through this context
-        hipHostUnregister(c->reg[k].host);
+    while (c->n_reg > 0) // references this context holds on registered regions
+        cndp_gpu_host_unregister(c, c->reg[0].host);
     if (c->ev_scratch)
         hipEventDestroy(c->ev_scratch);
     for (int k = 0; k < 3; k++)
@@ -4284,6 +4301,7 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
     a.ptype = b->ptype;
     a.rxmeta = b->mode == CNDP_MODE_CNET ? b->rxmeta : nullptr;
     a.iplen = b->mode == CNDP_MODE_CNET && b->rxmeta ? c->mq_iplen : nullptr;
+    a.win = b->mode == CNDP_MODE_CNET && b->rxmeta ? c->mq_win : nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (b->mode == CNDP_MODE_CNET) {
         if ((r = scratch_acquire(c, s)))
@@ -4358,9 +4376,14 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
             a.spec_tile = B ? c->sp_tile : nullptr; // written by this kernel only
             // the previous call left no worklist: the main kernel's last block
-            // takes this call's (if any) and the classes pass, no second launch
+            // takes this call's (if any) and the classes pass, no second launch.
+            // The hint is a pinned word an earlier call's kernel wrote, maybe
+            // not yet this call's predecessor: either branch gives the same
+            // results (CNDP_TUNE_CNET_FOLD forces one, the tests run both)
             a.wl_fold = 0;
-            if (B && c->sp_hint && ((volatile uint32_t *)c->sp_hint)[0] == 0u) {
+            const bool fold = c->tune_cnet_fold == 1 ||
+                              (c->tune_cnet_fold == 0 && c->sp_hint && ((volatile uint32_t *)c->sp_hint)[0] == 0u);
+            if (B && fold) {
                 const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
                 const uint64_t t0 = nb > SPEC_TAIL ? (nb - SPEC_TAIL) * B : 0;
                 a.wl_fold = 1;
@@ -4390,8 +4413,13 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                     auto lo = k_spec_local_t<SPEC_CH>;
                     uint32_t gl = (uint32_t)((nch + 4 * SPEC_LQ - 1) / (4 * SPEC_LQ)); // SPEC_LQ chunks per wave
                     // the previous call was a uniform batch: a wave per 64+ tiles
-                    if (c->sp_hint && ((volatile uint32_t *)c->sp_hint)[1] && gl > (uint32_t)c->num_cu * 4u)
-                        gl = (uint32_t)c->num_cu * 4u;
+                    // (any grid gives the same results; CNDP_TUNE_SPEC_GRID forces
+                    // a 2-block grid or the full one)
+                    const bool shrink = c->tune_spec_grid == 1 ||
+                                        (c->tune_spec_grid == 0 && c->sp_hint && ((volatile uint32_t *)c->sp_hint)[1]);
+                    const uint32_t cap = c->tune_spec_grid == 1 ? 2u : (uint32_t)c->num_cu * 4u;
+                    if (shrink && gl > cap)
+                        gl = cap;
                     hipLaunchKernelGGL(lo, dim3(gl), dim3(256), 0, s, a, B, nb, nch, meta, c->sp_done, c->sp_R);
                 } else if (gated) {
                     auto lo = k_spec_local<SPEC_CH, SPEC_WPB>;
@@ -5039,6 +5067,22 @@ extern "C" int cndp_gpu_mac_swap(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
 // Pin + map host memory (an AF_XDP UMEM region, a socket buffer pool) so the
 // device reads frames from it in place (zero-copy ingest) and DMA runs at
 // full rate.  *dev_ptr is the device-side address of `ptr`.
+// hipHostRegister is per process, while every graph node holds its own
+// context: the registration is shared and reference counted.  A region
+// already registered through another context (or by the application itself,
+// hipHostRegister) is recorded with its device address and never
+// unregistered by a context that did not register it; the last reference
+// registered here unregisters it.
+struct HostRegion {
+    uint8_t *host, *dev;
+    uint64_t len;
+    int refs;
+    bool owned; // registered by this library (else by the application)
+};
+static pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+static HostRegion g_reg[64];
+static int g_nreg;
+
 extern "C" int cndp_gpu_host_register(cndp_gpu_ctx_t *c, void *ptr, uint64_t len, void **dev_ptr)
 {
     if (!c || !ptr || !len)
@@ -5046,42 +5090,82 @@ extern "C" int cndp_gpu_host_register(cndp_gpu_ctx_t *c, void *ptr, uint64_t len
     int r = set_device(c->dev);
     if (r)
         return r;
-    hipError_t e = hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
-    if (e == hipErrorHostMemoryAlreadyRegistered)
-        return -EEXIST;
-    if (e != hipSuccess) {
-        fprintf(stderr, "cndp_gpu: hipHostRegister failed: %s\n", hipGetErrorString(e));
-        return -ENOMEM;
+    pthread_mutex_lock(&g_reg_lock);
+    int gi = -1, ci = -1;
+    for (int k = 0; k < g_nreg; k++)
+        if (g_reg[k].host == (uint8_t *)ptr)
+            gi = k;
+    for (int k = 0; k < c->n_reg; k++)
+        if (c->reg[k].host == (uint8_t *)ptr)
+            ci = k;
+    if (gi >= 0 && len > g_reg[gi].len) {
+        r = -EEXIST; // a different (larger) range at the same address
+    } else if (ci < 0 && c->n_reg == CNDP_MAX_REGIONS) {
+        r = -ENOSPC;
+    } else if (gi < 0) {
+        if (g_nreg == (int)(sizeof(g_reg) / sizeof(g_reg[0]))) {
+            r = -ENOSPC;
+        } else {
+            const hipError_t e = hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
+            void *d = nullptr;
+            if (e == hipSuccess || e == hipErrorHostMemoryAlreadyRegistered) {
+                if (hipHostGetDevicePointer(&d, ptr, 0) != hipSuccess) {
+                    if (e == hipSuccess)
+                        hipHostUnregister(ptr);
+                    r = e == hipSuccess ? -EIO : -EEXIST; // registered by the application, unmapped
+                }
+            } else {
+                fprintf(stderr, "cndp_gpu: hipHostRegister failed: %s\n", hipGetErrorString(e));
+                r = -ENOMEM;
+            }
+            if (!r) {
+                gi = g_nreg++;
+                g_reg[gi] = HostRegion{(uint8_t *)ptr, (uint8_t *)d, len, 0, e == hipSuccess};
+            }
+        }
     }
-    void *d = nullptr;
-    if (hipHostGetDevicePointer(&d, ptr, 0) != hipSuccess) {
-        hipHostUnregister(ptr);
-        return -EIO;
+    if (!r) {
+        g_reg[gi].refs++;
+        if (ci < 0) {
+            ci = c->n_reg++;
+            c->reg[ci].host = g_reg[gi].host;
+            c->reg[ci].dev = g_reg[gi].dev;
+            c->reg[ci].len = g_reg[gi].len;
+            c->reg[ci].refs = 0;
+        }
+        c->reg[ci].refs++;
+        if (dev_ptr)
+            *dev_ptr = g_reg[gi].dev;
     }
-    if (dev_ptr)
-        *dev_ptr = d;
-    if (c->n_reg < CNDP_MAX_REGIONS) { // remembered for zero-copy mbuf queues
-        c->reg[c->n_reg].host = (uint8_t *)ptr;
-        c->reg[c->n_reg].dev = (uint8_t *)d;
-        c->reg[c->n_reg].len = len;
-        c->n_reg++;
-    }
-    return 0;
+    pthread_mutex_unlock(&g_reg_lock);
+    return r;
 }
 
 extern "C" int cndp_gpu_host_unregister(cndp_gpu_ctx_t *c, void *ptr)
 {
     if (!c || !ptr)
         return -EINVAL;
-    int r = set_device(c->dev);
-    if (r)
-        return r;
+    pthread_mutex_lock(&g_reg_lock);
+    int ci = -1, gi = -1, r = 0;
     for (int k = 0; k < c->n_reg; k++)
-        if (c->reg[k].host == ptr) {
-            c->reg[k] = c->reg[--c->n_reg];
-            break;
+        if (c->reg[k].host == (uint8_t *)ptr)
+            ci = k;
+    for (int k = 0; k < g_nreg; k++)
+        if (g_reg[k].host == (uint8_t *)ptr)
+            gi = k;
+    if (ci < 0 || gi < 0) {
+        r = -ENOENT;
+    } else {
+        if (--c->reg[ci].refs == 0)
+            c->reg[ci] = c->reg[--c->n_reg];
+        if (--g_reg[gi].refs == 0) {
+            if (g_reg[gi].owned && hipHostUnregister(ptr) != hipSuccess)
+                r = -ENOENT;
+            g_reg[gi] = g_reg[--g_nreg];
         }
-    return hipHostUnregister(ptr) == hipSuccess ? 0 : -ENOENT;
+    }
+    pthread_mutex_unlock(&g_reg_lock);
+    return r;
 }
 
 extern "C" int cndp_gpu_bin_ids(cndp_gpu_ctx_t *c, uint32_t mode, const uint32_t *nh,
@@ -5167,11 +5251,19 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 #define MQ_FLIGHT 2
 #define MQ_DONE 3
 #define MQ_BURST 256u       // CNE_GRAPH_BURST_SIZE (cne_graph.h:30)
-#define MQ_WIN4 64u         // ip4_lookup staged bytes (it reads bytes 22..33)
+#define MQ_W4_AT 20u        // ip4_lookup reads bytes 22..33 (ttl, checksum, dst): the window 20..35
+#define MQ_W4 16u
+#define MQ_SWAP 16u         // mac swap: staged bytes (it touches 0..11)
+#define MQ_RW_STAGE 64u     // ip4_rewrite: staged bytes (rewrite data <= 56, TTL / checksum at 22..25)
 #define MQ_RUNS_MAX 512u    // cnet: runs of equal-size bursts per batch
-#define MQ_EDGE_NONE 0xFFFFu // zero-copy: an mbuf whose buffer is outside the region
+#define MQ_EDGE_NONE 0xFFFFu // zero-copy: an mbuf or frame outside every registered region
 #define MQ_SHORT 128u       // cnet staged bytes of a frame whose parse stays in its first 128
-#define MQ_PF 32u           // staged: mbufs prefetched ahead in the host loops (8 / 16 / 32 swept: tools/pf_sweep.sh)
+#define MQ_PF 32u           // mbufs prefetched ahead in the host loops (8 / 16 / 32 swept: tools/pf_sweep.sh)
+#define MQ_ADDR_MASK ((1ull << 56) - 1ull) // frame word: device address | readable bytes (<= 255) << 56
+#define MQ_RW_TAIL 1ull     // ip4_rewrite: the frame takes the tail loop's checksum rule
+#define MQ_MD_LEN 40u       // struct cnet_metadata {faddr, laddr} (cnet_meta.h:20-25, cne_inet.h:37-45)
+#define MQ_AF_INET 2u
+#define MQ_AF_INET6 10u
 
 // Staged cnet: whether a frame's bytes past its first MQ_SHORT can matter.
 // cne_get_ptype (pktmbuf_ptype.c:472-615) stops early for ARP and MPLS, and
@@ -5220,15 +5312,22 @@ struct MqTables {
     uint32_t buf_len;
 };
 
+// Per-mbuf inputs are host-filled pinned arrays (read by the kernels over
+// PCIe as coalesced runs): the host has each mbuf's header line in cache
+// anyway -- the node that hands the burst over just touched it -- so it
+// resolves the frame address there and the kernels read only frame bytes in
+// place (one PCIe read per frame instead of three dependent ones).
 struct MqArgs {
     uint32_t n;
-    uint32_t zc;            // zero-copy: mbuf pointers in, fields written into the mbufs
-    const uint64_t *ptrs;   // zc: host addresses of the mbufs (read in place)
-    int64_t delta;          // zc: device address - host address inside the region
-    const uint8_t *slab;    // frames: the region (zc) or the staging (device view)
+    uint32_t zc;            // zero-copy: frames read and fields written in the registered regions
+    const uint64_t *mb;     // zc: device address of each mbuf (0: outside every region); rewrite: MQ_RW_TAIL
+    const uint64_t *off;    // zc ip4 / swap / rewrite: frame word (device address | readable << 56, 0: none)
+                            // zc cnet: frame offset in the batch's region; staged: offset in the staging
+    const u32x2 *lens;      // cnet: {data_len | room << 16, buf_len | data_off << 16}
+    const uint64_t *priv;   // rewrite: node_mbuf_priv1 (udata64) as ip4_lookup left it
+    const uint64_t *md;     // cnet zc: device address of pktmbuf_metadata(m) (0: poll writes it)
+    const uint8_t *slab;    // cnet zc: the batch's region (device view); staged: the staging
     uint64_t slab_len;
-    const uint64_t *off;    // frame offsets in slab (staged: host-filled; zc cnet: from k_mq_cnet_pre)
-    u32x2 *lens;            // cnet: {data_len | room << 16, buf_len | data_off << 16}
     uint16_t *edges;        // out: next edge per mbuf (pinned host)
     uint64_t *priv1;        // out (staged ip4_lookup): node_mbuf_priv1
     u32x4 *rec;             // out (staged cnet): {ptype, rxmeta, data_len | edge << 16 | node << 24, hash}
@@ -5236,6 +5335,8 @@ struct MqArgs {
     const uint32_t *ptype, *rxmeta, *hash;
     const uint8_t *edge8;
     uint32_t *iplen;        // cnet: the IP length fields the parse read (0: read the frame); cleared here
+    const u32x4 *win;       // cnet: each fast-parsed or general-parsed frame's first 64 bytes
+    const struct cndp_rw_nh *rw; // rewrite: next-hop table (device)
     uint32_t lport, want_hash;
     MqTables tb;
     uint32_t *ticket;       // device arrival counter of this slot
@@ -5258,22 +5359,16 @@ __device__ __forceinline__ void mq_complete(const MqArgs &a)
     }
 }
 
-// the mbuf header fields the nodes read, at the device view of host mbuf m
-__device__ __forceinline__ void mq_hdr(const MqArgs &a, uint64_t m, uint64_t &fo, uint32_t &doff, uint32_t &blen,
-                                       uint32_t &dlen, bool &ok)
+// a zero-copy frame word: the frame's device address and how many bytes
+// from there lie inside its registered region (capped at 255)
+__device__ __forceinline__ uint8_t *mq_frame(uint64_t w, uint32_t &avail)
 {
-    const uint8_t *dm = (const uint8_t *)(m + a.delta);
-    const uint64_t buf = *(const uint64_t *)(dm + MB_BUF_ADDR);
-    const uint64_t w = *(const uint64_t *)(dm + MB_DATA_OFF); // data_off, lport, buf_len, data_len
-    doff = (uint32_t)(w & 0xffffu);
-    blen = (uint32_t)((w >> 32) & 0xffffu);
-    dlen = (uint32_t)(w >> 48);
-    fo = (uint64_t)((int64_t)(buf + doff) + a.delta - (int64_t)(uintptr_t)a.slab);
-    ok = fo < a.slab_len;
+    avail = (uint32_t)(w >> 56);
+    return (uint8_t *)(uintptr_t)(w & MQ_ADDR_MASK);
 }
 
 // node-queue kernels: one wave per block, so a batch spreads over 4x the CUs
-// (in place, each mbuf costs dependent PCIe reads; more CUs keep more in flight)
+// (in place, each mbuf costs a PCIe round trip; more CUs keep more in flight)
 #define MQ_TPB 64u
 
 // ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
@@ -5281,41 +5376,45 @@ __device__ __forceinline__ void mq_hdr(const MqArgs &a, uint64_t m, uint64_t &fo
 __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
-        uint64_t base, m = 0;
-        bool ok = true;
+        const uint64_t w = a.off[i];
+        const uint8_t *p; // bytes 20..35 of the frame
+        uint32_t avail;   // readable bytes from p
+        uint64_t m = 0;
         if (a.zc) {
-            uint32_t doff, blen, dlen;
-            m = a.ptrs[i]; // read once: the priv1 store below reuses it
-            mq_hdr(a, m, base, doff, blen, dlen, ok);
+            m = a.mb[i];
+            uint32_t fa;
+            const uint8_t *f = mq_frame(w, fa);
+            if (m == 0 || f == nullptr) {
+                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
+                continue;
+            }
+            p = f + MQ_W4_AT;
+            avail = fa > MQ_W4_AT ? fa - MQ_W4_AT : 0u;
         } else {
-            base = a.off[i];
+            p = a.slab + w;
+            avail = MQ_W4;
         }
-        const uint8_t *p = a.slab + base;
-        const uint64_t avail = ok && base < a.slab_len ? a.slab_len - base : 0;
         uint32_t ttl, ck, dip;
-        if (avail >= 36 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p + 20u) & 63u) <= 48u) {
-            // bytes 20..35 (ttl, checksum, dst) in one load inside one 64-B
-            // line: one PCIe read per frame when the mbuf is read in place
-            const u32x4a4 q = *(const u32x4a4 *)(p + 20);
+        if (avail >= 16 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p) & 63u) <= 48u) {
+            // ttl, checksum and dst in one load inside one 64-B line: the
+            // frame's only PCIe read when it is read in place
+            const u32x4a4 q = *(const u32x4a4 *)p;
             ttl = (q.x >> 16) & 0xffu;
             ck = q.y & 0xffffu;
             dip = bswap32(alignb(q.w, q.z, 2));
         } else {
-            ttl = gbyte(p, avail, 22);
-            ck = gbyte(p, avail, 24) | (gbyte(p, avail, 25) << 8);
-            dip = (gbyte(p, avail, 30) << 24) | (gbyte(p, avail, 31) << 16) | (gbyte(p, avail, 32) << 8) |
-                  gbyte(p, avail, 33);
+            ttl = gbyte(p, avail, 2);
+            ck = gbyte(p, avail, 4) | (gbyte(p, avail, 5) << 8);
+            dip = (gbyte(p, avail, 10) << 24) | (gbyte(p, avail, 11) << 16) | (gbyte(p, avail, 12) << 8) |
+                  gbyte(p, avail, 13);
         }
         const uint32_t val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
         const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
-        if (a.zc) {
-            if (ok)
-                *(uint64_t *)(m + a.delta + MB_UDATA64) = priv1;
-            a.edges[i] = ok ? (uint16_t)(val >> 16) : (uint16_t)MQ_EDGE_NONE;
-        } else {
+        if (a.zc)
+            *(uint64_t *)(m + MB_UDATA64) = priv1;
+        else
             a.priv1[i] = priv1;
-            a.edges[i] = (uint16_t)(val >> 16);
-        }
+        a.edges[i] = (uint16_t)(val >> 16);
     }
     mq_complete(a);
 }
@@ -5327,17 +5426,16 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
 __global__ __launch_bounds__(MQ_TPB) void k_mq_mac_swap(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
-        uint64_t base;
-        bool ok = true;
+        uint8_t *p;
+        uint32_t avail;
         if (a.zc) {
-            uint32_t doff, blen, dlen;
-            mq_hdr(a, a.ptrs[i], base, doff, blen, dlen, ok);
+            p = mq_frame(a.off[i], avail);
         } else {
-            base = a.off[i];
+            p = (uint8_t *)a.slab + a.off[i];
+            avail = MQ_SWAP;
         }
-        ok = ok && base + 12 <= a.slab_len;
+        const bool ok = p != nullptr && avail >= 12;
         if (ok) {
-            uint8_t *p = (uint8_t *)a.slab + base;
             if ((((uintptr_t)p) & 3u) == 0) {
                 uint32_t *d = (uint32_t *)p;
                 const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
@@ -5357,20 +5455,67 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_mac_swap(MqArgs a)
     mq_complete(a);
 }
 
-// zero-copy cnet: frame offsets and length fields from the mbuf headers
-__global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_pre(MqArgs a, uint64_t *off)
+// ip4_rewrite_node_process (ip4_rewrite.c:40-247) per packet of the node's
+// bursts: the next hop's rewrite data at mtod (:85), TTL = priv1.ttl - 1 and
+// the checksum from priv1.cksum + htons(0x0100) -- in the 4-wide loop with
+// the u32 end-around carry (:97-104, :109-110), in the tail loop as a u16
+// with `chksum += chksum >= 0xffff` (:209-216); the host marks which frames
+// of each burst the tail loop takes (the last nb_objs % 4).  edge = the next
+// hop's tx_node (ip4_rewrite_set_next / cne_node_ip4_rewrite_add); next hops
+// past the reference's 64-entry array act as unset entries (no data, edge 0).
+__global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_rewrite(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
-        uint64_t fo;
-        uint32_t doff, blen, dlen;
-        bool ok;
-        mq_hdr(a, a.ptrs[i], fo, doff, blen, dlen, ok);
-        off[i] = ok ? fo : a.slab_len; // outside the region: reads as zero bytes
-        u32x2 l;
-        l.x = dlen | ((blen > doff ? blen - doff : 0u) << 16);
-        l.y = blen | (doff << 16);
-        a.lens[i] = l;
+        const bool tail = (a.mb[i] & MQ_RW_TAIL) != 0u;
+        uint8_t *p;
+        uint32_t avail;
+        if (a.zc) {
+            p = mq_frame(a.off[i], avail);
+            if (p == nullptr) {
+                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
+                continue;
+            }
+        } else {
+            p = (uint8_t *)a.slab + a.off[i];
+            avail = MQ_RW_STAGE;
+        }
+        const uint64_t pv = a.priv[i];
+        const uint32_t nh = (uint32_t)(pv & 0xffffu), ttl = (uint32_t)(pv >> 16) & 0xffffu;
+        const uint32_t ck32 = (uint32_t)(pv >> 32);
+        const bool set = nh < CNDP_RW_MAX_NH;
+        const struct cndp_rw_nh *e = &a.rw[set ? nh : 0u];
+        const uint32_t hdr = set ? *(const uint32_t *)e : 0u; // rewrite_len | tx_node << 16
+        uint32_t len = hdr & 0xffffu;
+        len = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
+        const uint32_t *src = (const uint32_t *)e->rewrite_data;
+        if (len <= avail && (((uintptr_t)p) & 3u) == 0 && (len & 3u) == 0) {
+            for (uint32_t k = 0; k < len / 4; k++)
+                ((uint32_t *)p)[k] = src[k];
+        } else {
+            for (uint32_t k = 0; k < len && k < avail; k++)
+                p[k] = e->rewrite_data[k];
+        }
+        uint32_t nck;
+        if (!tail) {
+            const uint32_t c32 = ck32 + 1u;
+            nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
+        } else {
+            const uint32_t c16 = (ck32 + 1u) & 0xffffu;
+            nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
+        }
+        if (avail > 22)
+            p[22] = (uint8_t)(ttl - 1u);
+        if (avail > 25 && (((uintptr_t)p) & 1u) == 0) {
+            *(uint16_t *)(p + 24) = (uint16_t)nck;
+        } else {
+            if (avail > 24)
+                p[24] = (uint8_t)nck;
+            if (avail > 25)
+                p[25] = (uint8_t)(nck >> 8);
+        }
+        a.edges[i] = (uint16_t)(hdr >> 16);
     }
+    mq_complete(a);
 }
 
 // A frame an input node takes is re-evaluated here when the batch-wide
@@ -5404,14 +5549,57 @@ __device__ uint32_t mq_input_at(const uint8_t *slab, uint64_t slab_len, uint64_t
     return e >> 1;
 }
 
+// the 4 frame bytes at o (< 61) of a saved 64-B window, little-endian
+__device__ __forceinline__ uint32_t mq_win32(const u32x4 *w, uint32_t o)
+{
+    const uint32_t *d = (const uint32_t *)w;
+    const uint32_t k = o >> 2, s = o & 3u;
+    return s ? alignb(d[k + 1], d[k], s) : d[k];
+}
+
+// ipv4_save_metadata / ipv6_save_metadata (ip4_input.c:33-48, ip6_input.c:32-48)
+// for a frame whose IP header sits at byte ip of its window: faddr / laddr
+// {cin_family, cin_len, ..., address} at pktmbuf_metadata(m); cin_port and
+// the rest of the address union are left as they were, as there.
+__device__ void mq_save_md(uint8_t *d, const u32x4 *w, const uint8_t *fr, uint64_t favail, uint32_t ip, bool v6)
+{
+    const uint32_t na = v6 ? 4u : 1u, s_at = ip + (v6 ? 8u : 12u), d_at = ip + (v6 ? 24u : 16u);
+    uint32_t sa[4], da[4];
+    const bool inwin = d_at + 4u * na <= 64u;
+    for (uint32_t k = 0; k < na; k++) {
+        sa[k] = inwin ? mq_win32(w, s_at + 4 * k) : gld32(fr, favail, s_at + 4 * k);
+        da[k] = inwin ? mq_win32(w, d_at + 4 * k) : gld32(fr, favail, d_at + 4 * k);
+    }
+    const uint32_t fl = v6 ? (MQ_AF_INET6 | (16u << 8)) : (MQ_AF_INET | (4u << 8));
+    if ((((uintptr_t)d) & 3u) == 0) {
+        *(uint16_t *)d = (uint16_t)fl;
+        *(uint16_t *)(d + 20) = (uint16_t)fl;
+        if (v6) {
+            *(u32x4a4 *)(d + 4) = (u32x4a4){sa[0], sa[1], sa[2], sa[3]};
+            *(u32x4a4 *)(d + 24) = (u32x4a4){da[0], da[1], da[2], da[3]};
+        } else {
+            *(uint32_t *)(d + 4) = sa[0];
+            *(uint32_t *)(d + 24) = da[0];
+        }
+    } else {
+        d[0] = d[20] = (uint8_t)fl;
+        d[1] = d[21] = (uint8_t)(fl >> 8);
+        for (uint32_t k = 0; k < 4 * na; k++) {
+            d[4 + k] = (uint8_t)(sa[k >> 2] >> (8 * (k & 3u)));
+            d[24 + k] = (uint8_t)(da[k >> 2] >> (8 * (k & 3u)));
+        }
+    }
+}
+
 // cnet results per mbuf.  Frames an input node took get data_len =
 // total_length (ip4_input.c:121-124) or payload_len (ip6_input.c:121-124),
-// read at mtod after eth_rx's pktmbuf_adj_offset(l2_len) (eth_rx.c:62).
-// Which input node: ip4_input for the low ptype bytes of its p_nxt entries
-// (0x11, 0x31, 0x91), ip6_input for 0x41, 0xc1, 0xe1 -- the ptype node's
-// speculation only sends a frame to the edge of a type with the same low
-// byte (ptype.c:109-110).  Zero-copy: the eth_rx fields (eth_rx.c:35-63) and
-// data_len go straight into the mbuf; staged: into records for poll.
+// read at mtod after eth_rx's pktmbuf_adj_offset(l2_len) (eth_rx.c:62), and
+// their cnet_metadata addresses (ipv4/ipv6_save_metadata).  Which input node:
+// ip4_input for the low ptype bytes of its p_nxt entries (0x11, 0x31, 0x91),
+// ip6_input for 0x41, 0xc1, 0xe1 -- the ptype node's speculation only sends a
+// frame to the edge of a type with the same low byte (ptype.c:109-110).
+// Zero-copy: the eth_rx fields (eth_rx.c:35-63), data_len and the metadata go
+// straight into the mbuf; staged: into records for poll.
 __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
@@ -5426,16 +5614,18 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
         const uint32_t dl = ln.x & 0xffffu, room = ln.x >> 16, blen = ln.y & 0xffffu, doff = ln.y >> 16;
         const uint32_t l2 = rm & 0x7fu;
         const bool adj = l2 <= dl && l2 <= room;
+        const uint64_t fo = a.off[i];
         uint32_t node, e, dlen = adj ? dl - l2 : dl;
+        bool v6 = false;
         if (e8 & 0x80u) {
             node = CNDP_MQ_NODE_PTYPE;
             e = e8 & 0x7fu;
         } else {
             const uint32_t low = pt & 0xffu;
-            const bool v6 = low == 0x41u || low == 0xc1u || low == 0xe1u;
+            v6 = low == 0x41u || low == 0xc1u || low == 0xe1u;
             node = v6 ? CNDP_MQ_NODE_IP6 : CNDP_MQ_NODE_IP4;
             e = e8;
-            const uint64_t o = a.off[i] + (adj ? l2 : 0u);
+            const uint64_t o = fo + (adj ? l2 : 0u);
             const uint64_t lo = o + (v6 ? 4u : 2u);
             if (adj && ipl) // the parse's read of the same field (no second read of the frame)
                 dlen = ipl & 0xffffu;
@@ -5448,8 +5638,8 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
         }
         const uint32_t h = a.want_hash ? a.hash[i] : 0u;
         if (a.zc) {
-            const uint64_t m = a.ptrs[i] + a.delta;
-            if (a.off[i] < a.slab_len) {
+            const uint64_t m = a.mb[i];
+            if (m != 0 && fo < a.slab_len) {
                 // data_off, lport, buf_len, data_len, packet_type in one 12-B store
                 u32x3a4 w;
                 w.x = (adj ? doff + l2 : doff) | (a.lport << 16);
@@ -5464,6 +5654,9 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
                 *(u32x4 *)(m + MB_TX_OFFLOAD) = tol;
                 if (a.want_hash)
                     *(uint32_t *)(m + MB_HASH) = h;
+                if (node != CNDP_MQ_NODE_PTYPE && a.md && a.md[i])
+                    mq_save_md((uint8_t *)(uintptr_t)a.md[i], a.win + 4ull * i, a.slab + fo, a.slab_len - fo,
+                               adj ? l2 : 0u, v6);
                 a.edges[i] = (uint16_t)((node << 8) | e);
             } else {
                 a.edges[i] = (uint16_t)MQ_EDGE_NONE;
@@ -5483,7 +5676,9 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
 
 struct MqSlot {
     int state;
+    int failed;            // its launch failed: every mbuf comes back with CNDP_MQ_EDGE_NONE
     uint32_t n, polled, buf_len, seq;
+    int32_t rg;            // cnet zero-copy: the region every frame of the batch lies in (-1: none yet)
     uint64_t t_open_ns;    // when the first mbuf went in
     uint64_t stage_used;   // staged bytes
     uint32_t nrun;         // cnet: runs of equal-size bursts (each ends with at most one short burst)
@@ -5491,24 +5686,32 @@ struct MqSlot {
     uint8_t run_closed;
     void **mb;             // host
     uint8_t *h, *hd;       // pinned + mapped block (host view, device view)
-    uint8_t *d;            // device block (cnet classify outputs, zero-copy offsets)
+    uint8_t *d;            // device block (cnet classify outputs)
     hipEvent_t ev;
+};
+
+struct MqRegion {
+    const uint8_t *host;
+    uint64_t len;
+    int64_t delta; // device address - host address
 };
 
 struct cndp_gpu_mq {
     cndp_gpu_ctx_t *c;
     struct cndp_mq_conf conf;
     hipStream_t s;
-    const uint8_t *r_host, *r_dev; // zero-copy region (NULL: staged)
-    uint64_t r_len;
+    int zc;                        // zero-copy (conf.umem was a registered region)
+    MqRegion rg[CNDP_MAX_REGIONS]; // zero-copy: the context's regions when the queue was made
+    int nrg, rg_last;
     uint32_t stage;                // staged bytes reserved per frame
     uint32_t *flags, *flags_d;     // pinned completion flags (host / device view)
     uint32_t *tickets;             // device, one per slot
     // byte offsets inside each slot's pinned block (H) and device block (D)
-    uint64_t h_ptr, h_len, h_edge, h_rec, h_stage, h_bytes;
-    uint64_t d_off, d_len, d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_bytes;
+    uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_stage, h_bytes;
+    uint64_t d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_win, d_bytes;
     uint32_t head, open, in_flight, seq; // head: oldest slot not fully polled
     uint32_t pending;
+    int err;                       // a launch error not yet reported (returned by the next submit)
     MqSlot slot[CNDP_MQ_DEPTH_MAX];
 };
 
@@ -5521,15 +5724,41 @@ static uint64_t now_ns()
 
 static inline uint64_t al64(uint64_t x) { return (x + 63u) & ~63ull; }
 
+// the registered region holding [p, p + need), or -1
+static inline int mq_region(cndp_gpu_mq_t *q, const void *p, uint64_t need)
+{
+    const uint8_t *x = (const uint8_t *)p;
+    const MqRegion *r = &q->rg[q->rg_last];
+    if (q->nrg && x >= r->host && x + need <= r->host + r->len)
+        return q->rg_last;
+    for (int k = 0; k < q->nrg; k++)
+        if (x >= q->rg[k].host && x + need <= q->rg[k].host + q->rg[k].len) {
+            q->rg_last = k;
+            return k;
+        }
+    return -1;
+}
+
+// zero-copy frame word of host address f (0: outside every region)
+static inline uint64_t mq_frame_word(cndp_gpu_mq_t *q, const uint8_t *f)
+{
+    const int k = mq_region(q, f, 1);
+    if (k < 0)
+        return 0;
+    const uint64_t left = (uint64_t)(q->rg[k].host + q->rg[k].len - f);
+    return ((uint64_t)(intptr_t)(f + q->rg[k].delta) & MQ_ADDR_MASK) | ((left < 255u ? left : 255u) << 56);
+}
+
 extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *conf, cndp_gpu_mq_t **out)
 {
     if (!c || !conf || !out)
         return -EINVAL;
     *out = nullptr;
     struct cndp_mq_conf k = *conf;
-    if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP)
+    if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP &&
+        k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
-    if (k.flags & ~CNDP_MQ_F_HASH)
+    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA))
         return -EINVAL;
     k.batch = k.batch ? k.batch : 8192u;
     k.depth = k.depth ? k.depth : 4u;
@@ -5549,36 +5778,44 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->c = c;
     q->conf = k;
     if (k.umem) {
-        for (int j = 0; j < c->n_reg; j++)
-            if (c->reg[j].host == (uint8_t *)k.umem) {
-                q->r_host = c->reg[j].host;
-                q->r_dev = c->reg[j].dev;
-                q->r_len = c->reg[j].len;
-            }
-        if (!q->r_host) {
+        // zero-copy: every region the context holds (the UMEMs of all the
+        // graph's ports), conf.umem among them
+        bool named = false;
+        for (int j = 0; j < c->n_reg; j++) {
+            q->rg[q->nrg].host = c->reg[j].host;
+            q->rg[q->nrg].len = c->reg[j].len;
+            q->rg[q->nrg].delta = (int64_t)((intptr_t)c->reg[j].dev - (intptr_t)c->reg[j].host);
+            q->nrg++;
+            named = named || c->reg[j].host == (uint8_t *)k.umem;
+        }
+        if (!named) {
             free(q);
             return -EINVAL; // not registered with cndp_gpu_host_register
         }
+        q->zc = 1;
     }
     const uint64_t B = k.batch;
-    const bool cnet = k.mode == CNDP_MQ_CNET;
-    const bool zc = q->r_host != nullptr;
-    q->stage = zc ? 0u : cnet ? (uint32_t)al64(k.stage_max) : MQ_WIN4;
-    q->h_ptr = 0;                                       // zc: mbuf pointers; staged: frame offsets
-    q->h_len = al64(B * 8);                             // staged cnet: length fields
-    q->h_edge = q->h_len + (cnet && !zc ? al64(B * 8) : 0);
-    q->h_rec = q->h_edge + al64(B * 2);                 // staged: records
-    q->h_stage = q->h_rec + (zc ? 0 : al64(B * (cnet ? 16 : 8)));
+    const bool cnet = k.mode == CNDP_MQ_CNET, rw = k.mode == CNDP_MQ_IP4_REWRITE;
+    const bool zc = q->zc != 0;
+    q->stage = zc ? 0u
+             : cnet ? (uint32_t)al64(k.stage_max)
+             : k.mode == CNDP_MQ_IP4_LOOKUP ? MQ_W4 : k.mode == CNDP_MQ_MAC_SWAP ? MQ_SWAP : MQ_RW_STAGE;
+    q->h_mb = 0;                                          // zc: mbuf device addresses; rewrite: tail flags
+    q->h_off = al64(B * 8);                               // frame words / offsets
+    q->h_len = q->h_off + al64(B * 8);                    // cnet: length fields; rewrite: priv1
+    q->h_md = q->h_len + (cnet || rw ? al64(B * 8) : 0);  // cnet zc: metadata addresses
+    q->h_edge = q->h_md + (cnet && zc ? al64(B * 8) : 0);
+    q->h_rec = q->h_edge + al64(B * 2);                   // staged: records
+    q->h_stage = q->h_rec + (zc || rw || k.mode == CNDP_MQ_MAC_SWAP ? 0 : al64(B * (cnet ? 16 : 8)));
     q->h_bytes = q->h_stage + B * q->stage;
-    q->d_off = 0;                                       // zc cnet: offsets / lengths from the headers
-    q->d_len = al64(B * 8);
-    q->d_nh = q->d_len + al64(B * 8);
+    q->d_nh = 0;
     q->d_edge = q->d_nh + al64(B * 4);
     q->d_pt = q->d_edge + al64(B);
     q->d_rm = q->d_pt + al64(B * 4);
     q->d_hash = q->d_rm + al64(B * 4);
     q->d_ipl = q->d_hash + al64(B * 4);
-    q->d_bytes = cnet ? q->d_ipl + al64(B * 4) : 64;
+    q->d_win = q->d_ipl + al64(B * 4);
+    q->d_bytes = cnet ? q->d_win + (zc ? B * 64 : 0) : 64;
     r = -ENOMEM;
     if (hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) != hipSuccess)
         goto fail;
@@ -5645,11 +5882,13 @@ static MqSlot *mq_open_slot(cndp_gpu_mq_t *q)
     if (sl->state != MQ_FREE)
         return nullptr;
     sl->state = MQ_OPEN;
+    sl->failed = 0;
     sl->n = sl->polled = 0;
     sl->nrun = 0;
     sl->run_closed = 0;
     sl->stage_used = 0;
     sl->buf_len = 0;
+    sl->rg = -1;
     return sl;
 }
 
@@ -5672,30 +5911,35 @@ static MqTables mq_tables(cndp_gpu_ctx_t *c, uint32_t buf_len)
     return t;
 }
 
-static int mq_launch(cndp_gpu_mq_t *q)
+static int rw_sync(cndp_gpu_ctx_t *c, hipStream_t s);
+
+static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
 {
-    const uint32_t slot_i = q->open;
-    MqSlot *sl = &q->slot[slot_i];
-    if (sl->state != MQ_OPEN || sl->n == 0)
-        return 0;
     cndp_gpu_ctx_t *c = q->c;
     int r = set_device(c->dev);
     if (r)
         return r;
     hipStream_t s = q->s;
     const uint32_t n = sl->n;
-    const bool cnet = q->conf.mode == CNDP_MQ_CNET, zc = q->r_host != nullptr;
+    const bool cnet = q->conf.mode == CNDP_MQ_CNET, zc = q->zc != 0;
     uint8_t *HD = sl->hd, *D = sl->d;
     MqArgs a;
     memset(&a, 0, sizeof(a));
     a.n = n;
     a.zc = zc;
-    a.ptrs = (const uint64_t *)(HD + q->h_ptr);
-    a.delta = zc ? (int64_t)((intptr_t)q->r_dev - (intptr_t)q->r_host) : 0;
-    a.slab = zc ? q->r_dev : HD + q->h_stage;
-    a.slab_len = zc ? q->r_len : (sl->stage_used ? sl->stage_used : 64);
-    a.off = zc ? (const uint64_t *)(D + q->d_off) : (const uint64_t *)(HD + q->h_ptr);
-    a.lens = zc ? (u32x2 *)(D + q->d_len) : (u32x2 *)(HD + q->h_len);
+    a.mb = (const uint64_t *)(HD + q->h_mb);
+    a.off = (const uint64_t *)(HD + q->h_off);
+    a.lens = (const u32x2 *)(HD + q->h_len);
+    a.priv = (const uint64_t *)(HD + q->h_len);
+    a.md = zc && cnet && !(q->conf.flags & CNDP_MQ_F_NO_METADATA) ? (const uint64_t *)(HD + q->h_md) : nullptr;
+    if (zc && cnet) {
+        const MqRegion &g = q->rg[sl->rg >= 0 ? sl->rg : 0];
+        a.slab = g.host + g.delta;
+        a.slab_len = g.len;
+    } else {
+        a.slab = HD + q->h_stage;
+        a.slab_len = sl->stage_used ? sl->stage_used : 64;
+    }
     a.edges = (uint16_t *)(HD + q->h_edge);
     a.priv1 = (uint64_t *)(HD + q->h_rec);
     a.rec = (u32x4 *)(HD + q->h_rec);
@@ -5708,18 +5952,17 @@ static int mq_launch(cndp_gpu_mq_t *q)
     const uint32_t g = blocks_for(n, MQ_TPB);
     if (q->conf.mode == CNDP_MQ_MAC_SWAP) {
         hipLaunchKernelGGL(k_mq_mac_swap, dim3(g), dim3(MQ_TPB), 0, s, a);
-        HIP_TRY(hipGetLastError());
+    } else if (q->conf.mode == CNDP_MQ_IP4_REWRITE) {
+        if ((r = rw_sync(c, s)))
+            return r;
+        a.rw = c->d_rw_tbl;
+        hipLaunchKernelGGL(k_mq_ip4_rewrite, dim3(g), dim3(MQ_TPB), 0, s, a);
     } else if (!cnet) {
         if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
         a.tb = mq_tables(c, 0);
         hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
-        HIP_TRY(hipGetLastError());
     } else {
-        if (zc) {
-            hipLaunchKernelGGL(k_mq_cnet_pre, dim3(g), dim3(MQ_TPB), 0, s, a, (uint64_t *)(D + q->d_off));
-            HIP_TRY(hipGetLastError());
-        }
         // one classify per run of equal-size graph bursts, the ptype node's
         // speculation run with that burst size, its state carried in the
         // context from run to run and batch to batch
@@ -5741,8 +5984,10 @@ static int mq_launch(cndp_gpu_mq_t *q)
             b.hash = a.want_hash ? (uint32_t *)(D + q->d_hash) + i0 : nullptr;
             c->spec_burst = saved_B ? sl->run_B[k] : 0u;
             c->mq_iplen = (uint32_t *)(D + q->d_ipl) + i0;
+            c->mq_win = a.md ? (u32x4 *)(D + q->d_win) + 4ull * i0 : nullptr;
             r = cndp_gpu_classify(c, &b, s);
             c->mq_iplen = nullptr;
+            c->mq_win = nullptr;
             i0 += sl->run_n[k];
         }
         c->spec_burst = saved_B;
@@ -5753,15 +5998,37 @@ static int mq_launch(cndp_gpu_mq_t *q)
         a.hash = (const uint32_t *)(D + q->d_hash);
         a.edge8 = D + q->d_edge;
         a.iplen = (uint32_t *)(D + q->d_ipl);
+        a.win = (const u32x4 *)(D + q->d_win);
         a.tb = mq_tables(c, sl->buf_len);
         hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(MQ_TPB), 0, s, a);
-        HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sl->ev, s));
-    sl->state = MQ_FLIGHT;
-    q->in_flight++;
-    q->open = (q->open + 1) % q->conf.depth;
     return 0;
+}
+
+// launch the open slot; on failure its mbufs come back from poll with
+// CNDP_MQ_EDGE_NONE (each mbuf keeps exactly one owner) and the error is
+// returned
+static int mq_launch(cndp_gpu_mq_t *q)
+{
+    const uint32_t slot_i = q->open;
+    MqSlot *sl = &q->slot[slot_i];
+    if (sl->state != MQ_OPEN || sl->n == 0)
+        return 0;
+    const int r = mq_launch_kernels(q, sl, slot_i);
+    if (r) {
+        sl->failed = 1;
+        sl->state = MQ_DONE;
+        uint16_t *ed = (uint16_t *)(sl->h + q->h_edge);
+        for (uint32_t i = 0; i < sl->n; i++)
+            ed[i] = (uint16_t)MQ_EDGE_NONE;
+    } else {
+        sl->state = MQ_FLIGHT;
+        q->in_flight++;
+    }
+    q->open = (q->open + 1) % q->conf.depth;
+    return r;
 }
 
 extern "C" int cndp_gpu_mq_flush(cndp_gpu_mq_t *q)
@@ -5771,17 +6038,106 @@ extern "C" int cndp_gpu_mq_flush(cndp_gpu_mq_t *q)
     return mq_launch(q);
 }
 
+// eth_rx's metadata address of m: pktmbuf_metadata (pktmbuf.h:1209-1220)
+// through the node's hook, else its default m + sizeof(pktmbuf_t)
+static inline uint8_t *mq_md_host(const cndp_gpu_mq_t *q, uint8_t *m)
+{
+    return q->conf.metadata ? (uint8_t *)q->conf.metadata(m) : m + 64;
+}
+
+// one burst of k mbufs into the open slot sl (room checked by the caller)
+static void mq_fill(cndp_gpu_mq_t *q, MqSlot *sl, void *const *mbufs, uint32_t k)
+{
+    const uint32_t mode = q->conf.mode;
+    const bool cnet = mode == CNDP_MQ_CNET, rw = mode == CNDP_MQ_IP4_REWRITE, zc = q->zc != 0;
+    const bool want_md = cnet && zc && !(q->conf.flags & CNDP_MQ_F_NO_METADATA);
+    uint8_t *H = sl->h;
+    uint64_t *hmb = (uint64_t *)(H + q->h_mb), *hoff = (uint64_t *)(H + q->h_off);
+    uint64_t *hlen = (uint64_t *)(H + q->h_len), *hmd = (uint64_t *)(H + q->h_md);
+    const uint32_t vec = k & ~3u; // ip4_rewrite: the 4-wide loop's share of the burst
+    for (uint32_t i = 0; i < k; i++) {
+        // the mbuf headers MQ_PF ahead, the frames of the ones half as far
+        // (their buf_addr already in cache) where the host copies frame bytes
+        if (i + MQ_PF < k)
+            __builtin_prefetch((const uint8_t *)mbufs[i + MQ_PF], 1);
+        if (!zc && i + MQ_PF / 2 < k) {
+            const uint8_t *pm = (const uint8_t *)mbufs[i + MQ_PF / 2];
+            __builtin_prefetch(*(uint8_t *const *)(pm + MB_BUF_ADDR) + *(const uint16_t *)(pm + MB_DATA_OFF));
+        }
+        uint8_t *m = (uint8_t *)mbufs[i];
+        uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
+        const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
+        const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+        const uint16_t dlen = *(const uint16_t *)(m + MB_DATA_LEN);
+        const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
+        const uint32_t j = sl->n + i;
+        uint8_t *f = buf + doff; // pktmbuf_mtod
+        sl->mb[j] = m;
+        if (cnet) {
+            u32x2 l;
+            l.x = (uint32_t)dlen | (room << 16);
+            l.y = (uint32_t)blen | ((uint32_t)doff << 16);
+            ((u32x2 *)hlen)[j] = l;
+        }
+        if (rw) {
+            hmb[j] = i >= vec ? MQ_RW_TAIL : 0u;
+            hlen[j] = *(const uint64_t *)(m + MB_UDATA64); // node_mbuf_priv1
+        }
+        if (zc) {
+            if (!rw) {
+                const int km = mq_region(q, m, 64);
+                hmb[j] = km < 0 ? 0u : (uint64_t)(intptr_t)(m + q->rg[km].delta);
+            }
+            if (cnet) {
+                // frame offset in the batch's region (the first frame's);
+                // outside it: the region's end, which reads as zero bytes
+                const int kf = mq_region(q, f, 1);
+                if (sl->rg < 0 && kf >= 0)
+                    sl->rg = kf;
+                const MqRegion &g = q->rg[sl->rg >= 0 ? sl->rg : 0];
+                hoff[j] = kf >= 0 && kf == sl->rg ? (uint64_t)(f - g.host) : g.len;
+                if (want_md) {
+                    uint8_t *md = mq_md_host(q, m);
+                    const int kd = md ? mq_region(q, md, MQ_MD_LEN) : -1;
+                    hmd[j] = kd < 0 ? 0u : (uint64_t)(intptr_t)(md + q->rg[kd].delta);
+                }
+            } else {
+                hoff[j] = mq_frame_word(q, f);
+            }
+        } else {
+            // staged copy of the bytes the nodes can read (bounded by the buffer)
+            uint32_t at = 0, want;
+            if (cnet) {
+                const uint32_t cap = q->conf.stage_max > MQ_SHORT && mq_short_reach(f, room) ? MQ_SHORT
+                                                                                             : q->conf.stage_max;
+                want = room < cap ? room : cap;
+            } else if (mode == CNDP_MQ_IP4_LOOKUP) {
+                at = MQ_W4_AT;
+                want = MQ_W4;
+            } else {
+                want = q->stage;
+            }
+            const uint32_t cp = room > at ? (room - at < want ? room - at : want) : 0u;
+            uint8_t *dst = H + q->h_stage + sl->stage_used;
+            memcpy(dst, f + at, cp);
+            const uint64_t span = cnet ? al64(want ? want : 1) : (uint64_t)((want + 15u) & ~15u);
+            memset(dst + cp, 0, span - cp);
+            hoff[j] = sl->stage_used;
+            sl->stage_used += span;
+        }
+    }
+}
+
 extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t n)
 {
     if (!q || (n && !mbufs))
         return -EINVAL;
-    const bool cnet = q->conf.mode == CNDP_MQ_CNET, zc = q->r_host != nullptr;
-    if (zc) // zero-copy: the mbufs themselves must lie in the registered region
-        for (uint32_t i = 0; i < n; i++) {
-            const uint8_t *m = (const uint8_t *)mbufs[i];
-            if (m < q->r_host || m + 64 > q->r_host + q->r_len)
-                return -EINVAL;
-        }
+    if (q->err) { // a launch failed after the previous call accepted its mbufs
+        const int e = q->err;
+        q->err = 0;
+        return e;
+    }
+    const bool cnet = q->conf.mode == CNDP_MQ_CNET;
     uint32_t done = 0;
     while (done < n) {
         MqSlot *sl = mq_open_slot(q);
@@ -5793,9 +6149,12 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
         if (cnet && !full && sl->nrun == MQ_RUNS_MAX && !(sl->run_closed == 0 && k <= sl->run_B[sl->nrun - 1]))
             full = true;
         if (full) {
-            int r = mq_launch(q);
-            if (r)
-                return r;
+            const int r = mq_launch(q);
+            if (r) {
+                if (done)
+                    q->err = r;
+                return done ? (int)done : r;
+            }
             continue;
         }
         if (sl->n == 0) {
@@ -5805,50 +6164,7 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
             if (cnet)
                 sl->buf_len = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
         }
-        uint8_t *H = sl->h;
-        if (zc) {
-            memcpy(H + q->h_ptr + (size_t)sl->n * 8, mbufs + done, (size_t)k * 8);
-            memcpy(sl->mb + sl->n, mbufs + done, (size_t)k * sizeof(void *));
-        } else {
-            uint64_t *ho = (uint64_t *)(H + q->h_ptr);
-            u32x2 *hl = (u32x2 *)(H + q->h_len);
-            for (uint32_t i = 0; i < k; i++) {
-                // the mbuf headers MQ_PF ahead, the frames of the ones half as far
-                // (their buf_addr already in cache): a pool larger than the caches
-                // costs two misses per mbuf otherwise, one after the other
-                if (i + MQ_PF < k)
-                    __builtin_prefetch((const uint8_t *)mbufs[done + i + MQ_PF], 1);
-                if (i + MQ_PF / 2 < k) {
-                    const uint8_t *pm = (const uint8_t *)mbufs[done + i + MQ_PF / 2];
-                    __builtin_prefetch(*(uint8_t *const *)(pm + MB_BUF_ADDR) + *(const uint16_t *)(pm + MB_DATA_OFF));
-                }
-                uint8_t *m = (uint8_t *)mbufs[done + i];
-                const uint8_t *buf = *(uint8_t *const *)(m + MB_BUF_ADDR);
-                const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
-                const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
-                const uint16_t dlen = *(const uint16_t *)(m + MB_DATA_LEN);
-                const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
-                const uint32_t j = sl->n + i;
-                sl->mb[j] = m;
-                if (cnet) {
-                    u32x2 l;
-                    l.x = (uint32_t)dlen | (room << 16);
-                    l.y = (uint32_t)blen | ((uint32_t)doff << 16);
-                    hl[j] = l;
-                }
-                // staged copy of the bytes the nodes can read (bounded by the buffer)
-                const uint32_t cap = cnet && q->conf.stage_max > MQ_SHORT && mq_short_reach(buf + doff, room)
-                                         ? MQ_SHORT : q->conf.stage_max;
-                const uint32_t want = cnet ? (room < cap ? room : cap) : MQ_WIN4;
-                const uint32_t cp = room < want ? room : want;
-                uint8_t *dst = H + q->h_stage + sl->stage_used;
-                memcpy(dst, buf + doff, cp);
-                const uint64_t span = al64(want ? want : 1);
-                memset(dst + cp, 0, span - cp);
-                ho[j] = sl->stage_used;
-                sl->stage_used += span;
-            }
-        }
+        mq_fill(q, sl, mbufs + done, k);
         if (cnet) { // runs of equal-size bursts, each closed by a shorter one
             if (sl->nrun && !sl->run_closed && k == sl->run_B[sl->nrun - 1]) {
                 sl->run_n[sl->nrun - 1] += k;
@@ -5866,31 +6182,64 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
         done += k;
         q->pending += k;
         if (sl->n + MQ_BURST > q->conf.batch) { // no room for another full burst
-            int r = mq_launch(q);
-            if (r)
-                return r;
+            const int r = mq_launch(q);
+            if (r) { // this call's mbufs are in the failed slot: poll returns them
+                q->err = r;
+                return (int)done;
+            }
         }
     }
     return (int)done;
 }
 
-// staged: write one finished slot's records back into its mbufs
+// ipv4/ipv6_save_metadata on the host (ip4_input.c:33-48, ip6_input.c:32-48)
+// from the frame at the input node's mtod
+static void mq_save_md_host(uint8_t *md, const uint8_t *ip, bool v6)
+{
+    const uint8_t fam = v6 ? (uint8_t)MQ_AF_INET6 : (uint8_t)MQ_AF_INET, alen = v6 ? 16 : 4;
+    md[0] = md[20] = fam;
+    md[1] = md[21] = alen;
+    memcpy(md + 4, ip + (v6 ? 8 : 12), alen);
+    memcpy(md + 24, ip + (v6 ? 24 : 16), alen);
+}
+
+// one finished slot's results into its mbufs where the kernels did not
+// write them (staged: every field; zero-copy cnet: metadata the device could
+// not reach)
 static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
 {
+    const uint32_t mode = q->conf.mode;
+    const uint16_t *ed = (const uint16_t *)(sl->h + q->h_edge);
+    if (q->zc) {
+        if (mode != CNDP_MQ_CNET || (q->conf.flags & CNDP_MQ_F_NO_METADATA))
+            return;
+        const uint64_t *hmd = (const uint64_t *)(sl->h + q->h_md);
+        for (uint32_t i = i0; i < i1; i++) {
+            const uint32_t node = ed[i] >> 8;
+            if (hmd[i] || ed[i] == MQ_EDGE_NONE || (node != CNDP_MQ_NODE_IP4 && node != CNDP_MQ_NODE_IP6))
+                continue;
+            uint8_t *m = (uint8_t *)sl->mb[i], *md = mq_md_host(q, m);
+            if (md) // the mbuf fields are final: mtod is the input node's
+                mq_save_md_host(md, *(uint8_t **)(m + MB_BUF_ADDR) + *(const uint16_t *)(m + MB_DATA_OFF),
+                                node == CNDP_MQ_NODE_IP6);
+        }
+        return;
+    }
     const uint8_t *R = sl->h + q->h_rec;
-    if (q->conf.mode == CNDP_MQ_MAC_SWAP) { // the swapped addresses back into the frame
-        const uint64_t *ho = (const uint64_t *)(sl->h + q->h_ptr);
+    const uint64_t *ho = (const uint64_t *)(sl->h + q->h_off);
+    if (mode == CNDP_MQ_MAC_SWAP || mode == CNDP_MQ_IP4_REWRITE) { // the changed bytes back into the frame
+        const uint32_t span = mode == CNDP_MQ_MAC_SWAP ? 12u : MQ_RW_STAGE;
         for (uint32_t i = i0; i < i1; i++) {
             uint8_t *m = (uint8_t *)sl->mb[i];
             uint8_t *buf = *(uint8_t **)(m + MB_BUF_ADDR);
             const uint16_t doff = *(const uint16_t *)(m + MB_DATA_OFF);
             const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
             const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
-            memcpy(buf + doff, sl->h + q->h_stage + ho[i], room < 12 ? room : 12);
+            memcpy(buf + doff, sl->h + q->h_stage + ho[i], room < span ? room : span);
         }
         return;
     }
-    if (q->conf.mode == CNDP_MQ_IP4_LOOKUP) {
+    if (mode == CNDP_MQ_IP4_LOOKUP) {
         const uint64_t *priv1 = (const uint64_t *)R;
         for (uint32_t i = i0; i < i1; i++) { // node_mbuf_priv1 (ip4_lookup.c:144-154)
             if (i + MQ_PF < i1)
@@ -5901,6 +6250,7 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
     }
     const uint32_t *rec = (const uint32_t *)R;
     const bool wh = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
+    const bool md_on = !(q->conf.flags & CNDP_MQ_F_NO_METADATA);
     const uint16_t lport = q->conf.lport;
     for (uint32_t i = i0; i < i1; i++) {
         if (i + MQ_PF < i1)
@@ -5922,6 +6272,12 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
         *(uint16_t *)(m + MB_DATA_LEN) = (uint16_t)(w2 & 0xffffu); // adjusted, or the IP header's
         if (wh)
             *(uint32_t *)(m + MB_HASH) = rec[4 * i + 3];
+        const uint32_t node = w2 >> 24;
+        if (md_on && (node == CNDP_MQ_NODE_IP4 || node == CNDP_MQ_NODE_IP6)) {
+            uint8_t *md = mq_md_host(q, m);
+            if (md)
+                mq_save_md_host(md, *(uint8_t **)(m + MB_BUF_ADDR) + doff, node == CNDP_MQ_NODE_IP6);
+        }
     }
 }
 
@@ -5930,13 +6286,14 @@ extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges,
     if (!q || (max && (!mbufs || !edges)))
         return -EINVAL;
     // adaptive batching: a partly filled batch goes out when the GPU is idle
-    // or the batch has waited max_delay_us
+    // or the batch has waited max_delay_us (a failed launch is reported by
+    // the next submit; its mbufs come back below with CNDP_MQ_EDGE_NONE)
     MqSlot *op = &q->slot[q->open];
     if (op->state == MQ_OPEN && op->n &&
         (q->in_flight == 0 || now_ns() - op->t_open_ns >= (uint64_t)q->conf.max_delay_us * 1000u)) {
-        int r = mq_launch(q);
+        const int r = mq_launch(q);
         if (r)
-            return r;
+            q->err = r;
     }
     uint32_t got = 0;
     while (got < max) {
@@ -5951,7 +6308,7 @@ extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges,
         if (sl->state != MQ_DONE)
             break;
         const uint32_t take = sl->n - sl->polled < max - got ? sl->n - sl->polled : max - got;
-        if (q->r_host == nullptr)
+        if (!sl->failed)
             mq_writeback(q, sl, sl->polled, sl->polled + take);
         memcpy(mbufs + got, sl->mb + sl->polled, (size_t)take * sizeof(void *));
         memcpy(edges + got, (const uint16_t *)(sl->h + q->h_edge) + sl->polled, (size_t)take * 2);
@@ -6038,6 +6395,16 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return 0;
     case CNDP_TUNE_MBUF_HASH:
         c->mbuf_hash = value ? 1 : 0;
+        return 0;
+    case CNDP_TUNE_CNET_FOLD:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_cnet_fold = value;
+        return 0;
+    case CNDP_TUNE_SPEC_GRID:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_spec_grid = value;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

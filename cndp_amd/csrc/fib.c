@@ -595,14 +595,23 @@ int cne_fib_add(struct cne_fib *fib, uint32_t ip, uint8_t depth, uint64_t next_h
 {
     if (!fib || depth > CNE_FIB_MAXDEPTH)
         return -EINVAL;
-    return fib4_modify(fib, ip, depth, next_hop, CNE_FIB_ADD);
+    /* the host image and its dirty ranges change under dev_lock, so a device
+     * sync running on a worker thread never copies a half-painted range or
+     * clears the marks of a change it did not copy */
+    pthread_mutex_lock(&fib->t.dev_lock);
+    const int r = fib4_modify(fib, ip, depth, next_hop, CNE_FIB_ADD);
+    pthread_mutex_unlock(&fib->t.dev_lock);
+    return r;
 }
 
 int cne_fib_delete(struct cne_fib *fib, uint32_t ip, uint8_t depth)
 {
     if (!fib || depth > CNE_FIB_MAXDEPTH)
         return -EINVAL;
-    return fib4_modify(fib, ip, depth, 0, CNE_FIB_DEL);
+    pthread_mutex_lock(&fib->t.dev_lock);
+    const int r = fib4_modify(fib, ip, depth, 0, CNE_FIB_DEL);
+    pthread_mutex_unlock(&fib->t.dev_lock);
+    return r;
 }
 
 int cne_fib_lookup_bulk(struct cne_fib *fib, uint32_t *ips, uint64_t *next_hops, int n)
@@ -825,14 +834,20 @@ int cne_fib6_add(struct cne_fib6 *fib, const uint8_t ip[IPV6_ADDR_LEN], uint8_t 
 {
     if (!fib || !ip || depth > CNE_FIB6_MAXDEPTH)
         return -EINVAL;
-    return fib6_modify(fib, ip, depth, next_hop, CNE_FIB_ADD);
+    pthread_mutex_lock(&fib->t.dev_lock); /* see cne_fib_add */
+    const int r = fib6_modify(fib, ip, depth, next_hop, CNE_FIB_ADD);
+    pthread_mutex_unlock(&fib->t.dev_lock);
+    return r;
 }
 
 int cne_fib6_delete(struct cne_fib6 *fib, const uint8_t ip[IPV6_ADDR_LEN], uint8_t depth)
 {
     if (!fib || !ip || depth > CNE_FIB6_MAXDEPTH)
         return -EINVAL;
-    return fib6_modify(fib, ip, depth, 0, CNE_FIB_DEL);
+    pthread_mutex_lock(&fib->t.dev_lock);
+    const int r = fib6_modify(fib, ip, depth, 0, CNE_FIB_DEL);
+    pthread_mutex_unlock(&fib->t.dev_lock);
+    return r;
 }
 
 int cne_fib6_lookup_bulk(struct cne_fib6 *fib, uint8_t ips[][IPV6_ADDR_LEN], uint64_t *next_hops,

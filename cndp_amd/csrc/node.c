@@ -92,6 +92,15 @@ static int rw_alloc(void)
     return 0;
 }
 
+static int (*rw_next_hook)(uint16_t port_id, uint16_t next_index);
+
+void cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index))
+{
+    pthread_mutex_lock(&node_lock);
+    rw_next_hook = fn;
+    pthread_mutex_unlock(&node_lock);
+}
+
 int ip4_rewrite_set_next(uint16_t port_id, uint16_t next_index)
 {
     if (port_id >= CNDP_IP4_REWRITE_MAX_PORTS)
@@ -100,7 +109,12 @@ int ip4_rewrite_set_next(uint16_t port_id, uint16_t next_index)
     int r = rw_alloc();
     if (!r)
         ip4_rewrite_nm->next_index[port_id] = next_index;
+    int (*hook)(uint16_t, uint16_t) = rw_next_hook;
     pthread_mutex_unlock(&node_lock);
+    /* pktdev_ctrl.c:81-84 calls this right after adding the port's tx edge to
+     * ip4_rewrite: the GPU rewrite node mirrors that edge on its drain node */
+    if (!r && hook)
+        r = hook(port_id, next_index);
     return r;
 }
 

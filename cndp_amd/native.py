@@ -42,8 +42,11 @@ CNDP_TUNE_LOAD_NT = 10
 CNDP_TUNE_SPEC_SCAN = 11
 CNDP_STAT_CNET_WORKLIST, CNDP_STAT_CNET_UNIFORM = 1, 2
 CNDP_TUNE_MBUF_HASH = 12
-CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP = 0, 1, 2
-CNDP_MQ_F_HASH = 1
+CNDP_TUNE_CNET_FOLD = 13
+CNDP_TUNE_SPEC_GRID = 14
+CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
+CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA = 1, 2
+CNDP_MQ_EDGE_NONE = 0xFFFF
 CNDP_MQ_NODE_PTYPE, CNDP_MQ_NODE_IP4, CNDP_MQ_NODE_IP6 = 0, 1, 2
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF
 
@@ -87,7 +90,7 @@ class MqConf(Structure):
     """struct cndp_mq_conf (cndp_gpu.h)."""
     _fields_ = [("mode", c_uint32), ("flags", c_uint32), ("batch", c_uint32), ("depth", c_uint32),
                 ("max_delay_us", c_uint32), ("stage_max", c_uint32), ("umem", c_void_p),
-                ("lport", c_uint16), ("rsvd", c_uint16 * 3)]
+                ("lport", c_uint16), ("rsvd", c_uint16 * 3), ("metadata", c_void_p)]
 
 
 class NativeLibraryMissing(RuntimeError):

@@ -33,8 +33,13 @@
  *
  * Tuning from the environment: CNDP_GPU_DEVICE (0), CNDP_GPU_BATCH (8192),
  * CNDP_GPU_DEPTH (4), CNDP_GPU_DELAY_US (50).  Frames are read in place when
- * the application registered its UMEM with cndp_node_gpu_umem_add(), else
+ * the application registered its UMEMs with cndp_node_gpu_umem_add(), else
  * staged.  One GPU context and queue per cloned node (per port and graph).
+ *
+ * The input nodes' cnet_metadata (ipv4/ipv6_save_metadata, ip4_input.c:33-48,
+ * ip6_input.c:32-48), which tcp_input / udp_input read, is written at
+ * pktmbuf_metadata(m) for every frame this node sends on an ip4_input /
+ * ip6_input edge.
  */
 #include <errno.h>
 #include <stddef.h>
@@ -91,6 +96,12 @@ struct gpu_rx_ctx { /* node->ctx is CNE_NODE_CTX_SZ (16) bytes */
 };
 _Static_assert(sizeof(struct gpu_rx_ctx) <= CNE_NODE_CTX_SZ, "node context");
 #define GPU_RX_CTX(node) ((struct gpu_rx_ctx *)(node)->ctx)
+
+/* the queue's metadata hook: where ip4/ip6_input would write cnet_metadata */
+static void *rx_metadata(const void *m)
+{
+    return pktmbuf_metadata((const pktmbuf_t *)m);
+}
 
 static uint32_t env_u32(const char *name, uint32_t dflt)
 {
@@ -210,13 +221,14 @@ static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
     conf.batch = env_u32("CNDP_GPU_BATCH", 8192);
     conf.depth = env_u32("CNDP_GPU_DEPTH", 4);
     conf.max_delay_us = env_u32("CNDP_GPU_DELAY_US", 50);
+    conf.metadata = rx_metadata;
+    /* zero-copy: the kernels read the frames in the UMEMs (registration is
+     * shared and counted across the per-port contexts) */
     void *umem = NULL;
     uint64_t ulen = 0;
-    if (cndp_node_gpu_umem_get(0, &umem, &ulen) == 0) {
-        const int rr = cndp_gpu_host_register(st->gpu, umem, ulen, NULL);
-        if (rr == 0 || rr == -EEXIST)
-            conf.umem = umem; /* zero-copy: the kernels read the frames in the UMEM */
-    }
+    for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)
+        if (cndp_gpu_host_register(st->gpu, umem, ulen, NULL) == 0 && !conf.umem)
+            conf.umem = umem;
     if ((r = cndp_gpu_mq_create(st->gpu, &conf, &st->q)) < 0)
         goto fail;
     ctx->st = st;

@@ -27,7 +27,9 @@
  * Tuning from the environment (the application stays unchanged):
  *   CNDP_GPU_DEVICE (0), CNDP_GPU_BATCH (8192), CNDP_GPU_DEPTH (4),
  *   CNDP_GPU_DELAY_US (50).  Frames are read in place when the application
- *   registered its UMEM with cndp_node_gpu_umem_add(), else staged.
+ *   registered its UMEMs with cndp_node_gpu_umem_add() (every one of them:
+ *   the graph's ports may use different pools), else staged.  An mbuf the
+ *   queue cannot reach (outside every registered UMEM) leaves by pkt_drop.
  *
  * One GPU context and queue per graph (graphs are per lcore, cne_graph_worker.h
  * notes a graph is not shared between threads); contexts share the node FIB,
@@ -110,13 +112,13 @@ static struct gpu_graph_state *state_get(const struct cne_graph *graph)
     conf.batch = env_u32("CNDP_GPU_BATCH", 8192);
     conf.depth = env_u32("CNDP_GPU_DEPTH", 4);
     conf.max_delay_us = env_u32("CNDP_GPU_DELAY_US", 50);
+    /* zero-copy: the kernels read the frames in the UMEMs (registration is
+     * shared and counted across the graphs' contexts) */
     void *umem = NULL;
     uint64_t ulen = 0;
-    if (cndp_node_gpu_umem_get(0, &umem, &ulen) == 0) {
-        int r = cndp_gpu_host_register(st->gpu, umem, ulen, NULL);
-        if (r == 0 || r == -EEXIST)
-            conf.umem = umem; /* zero-copy: the kernels read the frames in the UMEM */
-    }
+    for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)
+        if (cndp_gpu_host_register(st->gpu, umem, ulen, NULL) == 0 && !conf.umem)
+            conf.umem = umem;
     if (cndp_gpu_mq_create(st->gpu, &conf, &st->q) < 0)
         goto fail;
     gs_by_graph[gid] = st;
@@ -154,7 +156,12 @@ static uint16_t gpu_drain(struct cne_graph *graph, struct cne_node *node, struct
             int j = i + 1;
             while (j < k && st->edge[j] == st->edge[i])
                 j++;
-            cne_node_enqueue(graph, node, (cne_edge_t)st->edge[i], &st->done[i], (uint16_t)(j - i));
+            /* a FIB value naming no edge of this node (ip4_lookup.c:150 takes
+             * val >> 16 as is) and an mbuf the queue could not reach
+             * (CNDP_MQ_EDGE_NONE) leave by pkt_drop */
+            const cne_edge_t e = st->edge[i] < CNE_NODE_IP4_LOOKUP_NEXT_MAX ? (cne_edge_t)st->edge[i]
+                                                                             : CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP;
+            cne_node_enqueue(graph, node, e, &st->done[i], (uint16_t)(j - i));
             i = j;
         }
         total = (uint16_t)(total + k);

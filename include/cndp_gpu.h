@@ -142,11 +142,14 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  *
  * Frame bytes: when conf.umem names a region registered with
  * cndp_gpu_host_register (the AF_XDP UMEM / pktmbuf pool, cne_lport.h:91),
- * the mbufs and their buffers must lie in it, and the host does no per-mbuf
- * work at all: the kernels read each mbuf header and frame where they lie and
- * write the results straight into the mbuf (zero-copy; submit refuses mbufs
- * outside the region with -EINVAL; an mbuf whose buffer points outside it
- * comes back untouched with edge CNDP_MQ_EDGE_NONE).  With conf.umem NULL,
+ * the queue works in place (zero-copy) over every region the context holds:
+ * the host reads each mbuf's header line -- the node handing the burst over
+ * has just touched it -- and passes the frame address (buf_addr + data_off),
+ * and the kernels read the frame bytes where they lie and write the results
+ * straight into the mbuf.  An mbuf or frame outside every registered region
+ * comes back untouched with edge CNDP_MQ_EDGE_NONE (cnet: the frames of one
+ * batch must share a region -- one pool per port -- others come back the
+ * same way).  With conf.umem NULL,
  * the host copies each frame into pinned staging (ip4_lookup: 64 B, enough for
  * every byte the node reads; cnet: 128 B for a frame whose header walk stays
  * there -- Ethernet with at most one tag, then IPv4 or IPv6 without extension
@@ -156,7 +159,9 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  * parse reads only for malformed extension-header lengths, are the next
  * staged frame's here (undefined in the reference either way).
  * Completion is a flag the batch's last kernel raises in pinned memory, so
- * poll costs a load, not a HIP call.
+ * poll costs a load, not a HIP call.  A batch whose launch fails comes back
+ * from poll with every edge CNDP_MQ_EDGE_NONE, so each accepted mbuf has one
+ * owner; the error is returned by the next submit.
  *
  * Modes and what is written back (pktmbuf_t layout, pktmbuf.h:102-204):
  *   CNDP_MQ_IP4_LOOKUP  the ip4_lookup node (ip4_lookup.c:48-256): udata64 =
@@ -175,12 +180,26 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  *                       CNDP_MQ_NODE_PTYPE with e = the ptype edge (pkt_drop 0,
  *                       punt 2, gtpu 5), or CNDP_MQ_NODE_IP4 / _IP6 with e =
  *                       the input node's edge (drop 0, forward 1, proto 2).
+ *                       Frames an input node takes also get its cnet_metadata
+ *                       (ipv4/ipv6_save_metadata, ip4_input.c:33-48,
+ *                       ip6_input.c:32-48): faddr / laddr {family, len, addr}
+ *                       at pktmbuf_metadata(m) -- conf.metadata(m) when set
+ *                       (the node passes pktmbuf_metadata), else m + 64, its
+ *                       default -- unless CNDP_MQ_F_NO_METADATA.
  *                       Each submit call is one graph burst (<= 256 mbufs;
  *                       larger calls are cut into 256s).
  *   CNDP_MQ_MAC_SWAP    cndpfwd's loopback mode (examples/cndpfwd/main.c:317-339):
  *                       destination and source MAC swapped in the frame
  *                       (swap_mac_addresses, main.h:303-315); edge 0 (tx).
  *                       Needs no FIB.
+ *   CNDP_MQ_IP4_REWRITE the ip4_rewrite node (ip4_rewrite.c:40-247) per submitted
+ *                       burst: the next hop's rewrite data at mtod, TTL - 1 and
+ *                       the checksum + htons(0x0100) from node_mbuf_priv1 in
+ *                       udata64 (the 4-wide loop's end-around carry for the
+ *                       first nb & ~3 mbufs of the burst, the tail loop's rule
+ *                       for the rest); edge = the next hop's tx_node
+ *                       (cne_node_ip4_rewrite_add / ip4_rewrite_set_next, the
+ *                       process-global table unless the context has its own).
  *   flag CNDP_MQ_F_HASH also store the Toeplitz flow hash in m->hash (no
  *                       reference node writes it, so it is off by default).
  */
@@ -189,7 +208,9 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
 #define CNDP_MQ_IP4_LOOKUP 0u
 #define CNDP_MQ_CNET 1u
 #define CNDP_MQ_MAC_SWAP 2u
+#define CNDP_MQ_IP4_REWRITE 3u
 #define CNDP_MQ_F_HASH (1u << 0)
+#define CNDP_MQ_F_NO_METADATA (1u << 1) /* cnet: leave cnet_metadata unwritten */
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u
 #define CNDP_MQ_NODE_IP6 2u
@@ -207,6 +228,9 @@ struct cndp_mq_conf {
     void *umem;            /* registered region the mbufs live in, or NULL */
     uint16_t lport;        /* cnet: m->lport (eth_rx.c:59) */
     uint16_t rsvd[3];
+    /* cnet: pktmbuf_metadata(m) (pktmbuf.h:1209-1220), or NULL for its
+     * default m + sizeof(pktmbuf_t) */
+    void *(*metadata)(const void *m);
 };
 
 int cndp_gpu_mq_create(cndp_gpu_ctx_t *ctx, const struct cndp_mq_conf *conf, cndp_gpu_mq_t **out);
@@ -214,7 +238,8 @@ int cndp_gpu_mq_create(cndp_gpu_ctx_t *ctx, const struct cndp_mq_conf *conf, cnd
 void cndp_gpu_mq_free(cndp_gpu_mq_t *q);
 /* Accepts up to n mbufs (a graph burst), returns how many (0 when every
  * batch slot is in flight or waiting to be polled), or a negative errno
- * (-EINVAL: an mbuf outside conf.umem, -EIO: a failed launch). */
+ * (-EINVAL: bad arguments; a failed launch: its HIP error as -EIO / -ENOMEM,
+ * returned by the call after the one that accepted the batch's mbufs). */
 int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t n);
 /* Launch the partly filled batch now (no-op when empty). */
 int cndp_gpu_mq_flush(cndp_gpu_mq_t *q);
@@ -253,7 +278,11 @@ int cndp_gpu_mac_swap(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *str
 
 /* Pin and map host memory for the device (zero-copy ingest: pass *dev_ptr
  * as cndp_batch.slab to cndp_gpu_classify and the kernel reads the frames
- * over PCIe in place).  -EEXIST if already registered. */
+ * over PCIe in place).  Registration is process-wide and reference counted:
+ * registering a region another context (or the application) registered
+ * takes a reference and returns 0; each unregister (and cndp_gpu_fini) drops
+ * one, the last one registered here unregisters.  -EEXIST for a larger range
+ * at an address already registered. */
 int cndp_gpu_host_register(cndp_gpu_ctx_t *ctx, void *ptr, uint64_t len, void **dev_ptr);
 int cndp_gpu_host_unregister(cndp_gpu_ctx_t *ctx, void *ptr);
 
@@ -308,7 +337,15 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           edges -- only the final node state is walked -- else maps of
  *                           8 entries when <= 8 ptype signatures occur, 64 up to 64, a
  *                           sequential walk beyond), 1 = always 64-entry maps, 2 = always
- *                           the sequential walk (default 0; 1 and 2 exist for tests) */
+ *                           the sequential walk (default 0; 1 and 2 exist for tests)
+ *   CNDP_TUNE_CNET_FOLD     cnet: where the frames the fast kernel leaves and the
+ *                           speculation classes pass run -- 0 = auto (in the fast
+ *                           kernel's last block when the previous call left no such
+ *                           frames, else a second launch), 1 = always the last block,
+ *                           2 = always the second launch (tests force both)
+ *   CNDP_TUNE_SPEC_GRID     cnet speculation local pass grid: 0 = auto (a small grid
+ *                           after a uniform batch), 1 = 2 blocks, 2 = one wave per
+ *                           4 chunks (tests force both) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -321,6 +358,8 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_LOAD_NT 10
 #define CNDP_TUNE_SPEC_SCAN 11
 #define CNDP_TUNE_MBUF_HASH 12
+#define CNDP_TUNE_CNET_FOLD 13
+#define CNDP_TUNE_SPEC_GRID 14
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words

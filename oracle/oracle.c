@@ -1263,3 +1263,90 @@ void orc_mac_swap(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint6
         }
     }
 }
+
+/* ---------------------------------------------------------------------------
+ * ip4_rewrite_node_process (ip4_rewrite.c:40-247) over one burst of
+ * pktmbuf_t pointers (one process() call, nb_objs = n): priv1 from udata64
+ * (node_private.h:24-35), the rewrite data at mtod (:85), TTL = priv.ttl - 1,
+ * the checksum from priv.cksum + htons(0x0100) -- the 4-wide loop's u32
+ * end-around carry for the first n & ~3 mbufs (:97-110), the tail loop's u16
+ * rule for the rest (:209-216); tx_edge = the next hop's tx_node.  Next hops
+ * past the 64-entry array read an unset (zero) entry.
+ * ------------------------------------------------------------------------- */
+static void rw_one(uint8_t *m, const struct orc_rewrite_nh *tbl, int vec4, uint16_t *tx)
+{
+    static const struct orc_rewrite_nh unset;
+    const uint64_t priv = *(const uint64_t *)(m + 56);
+    const uint16_t nh = (uint16_t)priv, ttl = (uint16_t)(priv >> 16);
+    const uint32_t ck32 = (uint32_t)(priv >> 32);
+    uint8_t *d = *(uint8_t *const *)(m + 8) + *(const uint16_t *)(m + 24); /* pktmbuf_mtod */
+    const struct orc_rewrite_nh *e = nh < 64 ? &tbl[nh] : &unset;
+    memcpy(d, e->rewrite_data, e->rewrite_len < 56 ? e->rewrite_len : 56);
+    uint16_t nck;
+    if (vec4) {
+        const uint32_t c32 = ck32 + 0x0001u; /* priv01.u32[1] += htons(0x0100) */
+        nck = (uint16_t)((c32 & 0xFFFFu) + (c32 >> 16));
+    } else {
+        uint16_t c16 = (uint16_t)(ck32 + 0x0001u);
+        c16 = (uint16_t)(c16 + (c16 >= 0xffff));
+        nck = c16;
+    }
+    d[14 + 8] = (uint8_t)(ttl - 1);
+    memcpy(d + 14 + 10, &nck, 2);
+    *tx = e->tx_node;
+}
+
+void orc_ip4_rewrite_node(void *const *mbufs, uint32_t n, const struct orc_rewrite_nh *tbl, uint16_t *tx_edge)
+{
+    const uint32_t vec = n & ~3u;
+    for (uint32_t i = 0; i < n; i++)
+        rw_one((uint8_t *)mbufs[i], tbl, i < vec, &tx_edge[i]);
+}
+
+/* The l3fwd-graph node pair on one core: per burst ip4_lookup's loop (as
+ * orc_ip4_lookup_mbufs) then ip4_rewrite_node_process over the burst's mbufs
+ * the lookup sent to edge 0, in order (the rewrite node's stream).  Returns
+ * seconds for `iters` passes. */
+double orc_l3fwd_nodes_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                             const uint32_t *tbl8, const struct orc_rewrite_nh *tbl, int iters)
+{
+    struct timespec t0, t1;
+    uint64_t sink = 0;
+    void *rw[256];
+    uint16_t tx[256];
+    if (burst == 0 || burst > 256)
+        burst = 256;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int it = 0; it < iters; it++) {
+        for (uint32_t b = 0; b < n; b += burst) {
+            const uint32_t cnt = n - b < burst ? n - b : burst;
+            uint32_t nrw = 0;
+            for (uint32_t k = 0; k < cnt; k += 4) {
+                const uint32_t m = cnt - k < 4 ? cnt - k : 4;
+                uint32_t dip[4];
+                uint64_t dst[4];
+                uint8_t *mb[4];
+                const uint8_t *ip[4];
+                for (uint32_t q = 0; q < m; q++) {
+                    mb[q] = (uint8_t *)mbufs[b + k + q];
+                    const uint8_t *buf = *(uint8_t *const *)(mb[q] + 8);
+                    ip[q] = buf + *(const uint16_t *)(mb[q] + 24) + 14;
+                    dip[q] = rd_be32(ip[q] + 16);
+                }
+                orc_dir24_8_lookup_bulk_pf(tbl24, tbl8, dip, m, dst);
+                for (uint32_t q = 0; q < m; q++) {
+                    const uint64_t ck = (uint64_t)ip[q][10] | ((uint64_t)ip[q][11] << 8);
+                    *(uint64_t *)(mb[q] + 56) = (dst[q] & 0xffffu) | ((uint64_t)ip[q][8] << 16) | (ck << 32);
+                    if ((dst[q] >> 16) == 0)
+                        rw[nrw++] = mb[q];
+                }
+            }
+            orc_ip4_rewrite_node(rw, nrw, tbl, tx);
+            for (uint32_t q = 0; q < nrw; q++)
+                sink += tx[q];
+        }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    (void)sink;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -153,6 +153,12 @@ void orc_ip4_rewrite(uint8_t *slab, uint64_t slab_len, uint64_t stride, const ui
                      uint32_t data_off, uint32_t n, const uint32_t *nh, uint32_t burst,
                      const struct orc_rewrite_nh *tbl, uint16_t *tx_edge);
 
+/* ip4_rewrite_node_process over one burst of pktmbuf_t pointers (nb_objs = n) */
+void orc_ip4_rewrite_node(void *const *mbufs, uint32_t n, const struct orc_rewrite_nh *tbl, uint16_t *tx_edge);
+/* ip4_lookup then ip4_rewrite per burst on one core (seconds for iters passes) */
+double orc_l3fwd_nodes_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                             const uint32_t *tbl8, const struct orc_rewrite_nh *tbl, int iters);
+
 /* cndpfwd loopback: swap_mac_addresses (examples/cndpfwd/main.h:303-315)
  * on every frame of the batch. */
 void orc_mac_swap(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint64_t *offsets,

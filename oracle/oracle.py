@@ -84,6 +84,9 @@ def lib():
         L.orc_ip4_rewrite.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32, c_void_p,
                                       c_uint32, c_void_p, c_void_p]
         L.orc_mac_swap.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]
+        L.orc_ip4_rewrite_node.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p]
+        L.orc_l3fwd_nodes_mbufs.restype = c_double
+        L.orc_l3fwd_nodes_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_int]
         _lib = L
     return _lib
 
@@ -274,6 +277,21 @@ def ip4_rewrite(slab: np.ndarray, n: int, nh: np.ndarray, table: np.ndarray, bur
     lib().orc_ip4_rewrite(slab.ctypes.data, slab.nbytes, stride, offs.ctypes.data if offs is not None else None,
                           data_off, n, nh.ctypes.data, burst, table.ctypes.data, tx.ctypes.data)
     return tx
+
+
+def ip4_rewrite_node(ptrs, n: int, table: np.ndarray) -> np.ndarray:
+    """ip4_rewrite_node_process over one burst of pktmbuf_t pointers (in place,
+    host memory); returns the tx edge of each mbuf."""
+    table = np.ascontiguousarray(table, dtype=REWRITE_NH)
+    tx = np.zeros(max(n, 1), np.uint16)
+    lib().orc_ip4_rewrite_node(ptrs, n, table.ctypes.data, tx.ctypes.data)
+    return tx[:n]
+
+
+def l3fwd_nodes_mbufs(ptrs, n: int, tables4, table: np.ndarray, burst: int = 256, iters: int = 1) -> float:
+    """ip4_lookup + ip4_rewrite node loop over pktmbuf_t pointers, one thread: seconds."""
+    table = np.ascontiguousarray(table, dtype=REWRITE_NH)
+    return lib().orc_l3fwd_nodes_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), table.ctypes.data, iters)
 
 
 def mac_swap(slab: np.ndarray, n: int, stride: int = 64, offsets=None, data_off: int = 0):

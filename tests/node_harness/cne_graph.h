@@ -1,6 +1,6 @@
 /*
  * Test-only stand-in for the subset of CNDP's graph API (lib/usr/clib/graph/
- * cne_graph.h) that cndp_amd/node/ip4_lookup_gpu.c uses, so the node source can
+ * cne_graph.h) that the GPU node sources (cndp_amd/node) use, so they can
  * be compiled and driven here and on the GPU box, where no CNDP tree exists.
  * Same type names, field names and signatures as the reference declares them
  * (cne_graph.h:32-42, :94-128, :427-472); the behaviour behind them is the
@@ -39,6 +39,12 @@ struct cne_node_register {
 };
 
 cne_node_t __cne_node_register(const struct cne_node_register *node);
+
+/* cne_graph.h:522-569 (edges of a registered node; the harness keeps them) */
+#define CNE_EDGE_ID_INVALID UINT16_MAX
+cne_edge_t cne_node_edge_count(cne_node_t id);
+cne_edge_t cne_node_edge_update(cne_node_t id, cne_edge_t from, const char **next_nodes, uint16_t nb_edges);
+cne_node_t cne_node_edge_get(cne_node_t id, char *next_nodes[]);
 
 #define CNE_NODE_REGISTER(node)                                                      \
     __attribute__((constructor)) static void cne_node_register_##node(void)         \

@@ -13,7 +13,7 @@
 
 #include "cne_graph_worker.h"
 
-#define MAX_REG 8
+#define MAX_REG 12
 #define MAX_OUT (1u << 22)
 
 static const struct cne_node_register *regs[MAX_REG];
@@ -67,11 +67,81 @@ static int find(const char *name)
 static const struct cne_node_register *slot_reg[MAX_REG];
 static int8_t slot_k[MAX_REG][MAX_EDGES], slot_s[MAX_REG][MAX_EDGES];
 
+/* edges set by cne_node_edge_update (cne_graph.h:540), per registration;
+ * dyn_n[r] == 0: the registration's own next_nodes */
+static char dyn_name[MAX_REG][MAX_EDGES][CNE_NODE_NAMESIZE];
+static char *dyn_ptr[MAX_REG][MAX_EDGES];
+static int dyn_n[MAX_REG];
+
+static int reg_of(cne_node_t id)
+{
+    for (int i = 0; i < n_regs; i++)
+        if (regs[i]->id == id)
+            return i;
+    return -1;
+}
+
+static int edge_count(int r) { return dyn_n[r] ? dyn_n[r] : regs[r]->nb_edges; }
+
+static const char *edge_name(int r, int e)
+{
+    if (e >= edge_count(r))
+        return "";
+    return dyn_n[r] ? dyn_name[r][e] : regs[r]->next_nodes[e];
+}
+
+cne_edge_t cne_node_edge_count(cne_node_t id)
+{
+    const int r = reg_of(id);
+    return r < 0 ? CNE_EDGE_ID_INVALID : (cne_edge_t)edge_count(r);
+}
+
+cne_edge_t cne_node_edge_update(cne_node_t id, cne_edge_t from, const char **next_nodes, uint16_t nb_edges)
+{
+    const int r = reg_of(id);
+    if (r < 0)
+        return CNE_EDGE_ID_INVALID;
+    const int cnt = edge_count(r);
+    if (!dyn_n[r]) // take over the registration's edges first
+        for (int e = 0; e < cnt && e < MAX_EDGES; e++)
+            strncpy(dyn_name[r][e], regs[r]->next_nodes[e], CNE_NODE_NAMESIZE - 1);
+    const int f = from == CNE_EDGE_ID_INVALID ? cnt : from;
+    if (f > cnt || f + nb_edges > MAX_EDGES)
+        return CNE_EDGE_ID_INVALID;
+    for (int k = 0; k < nb_edges; k++)
+        strncpy(dyn_name[r][f + k], next_nodes[k], CNE_NODE_NAMESIZE - 1);
+    dyn_n[r] = f + nb_edges > cnt ? f + nb_edges : cnt;
+    slot_reg[r] = NULL; // re-resolve this registration's edge buckets
+    return (cne_edge_t)dyn_n[r];
+}
+
+cne_node_t cne_node_edge_get(cne_node_t id, char *next_nodes[])
+{
+    const int r = reg_of(id);
+    if (r < 0)
+        return CNE_NODE_ID_INVALID;
+    const int cnt = edge_count(r);
+    if (!next_nodes)
+        return (cne_node_t)(sizeof(char *) * cnt);
+    for (int e = 0; e < cnt; e++) {
+        dyn_ptr[r][e] = (char *)edge_name(r, e);
+        next_nodes[e] = dyn_ptr[r][e];
+    }
+    return (cne_node_t)cnt;
+}
+
+/* forget every edge update (back to the registrations' edges) */
+void harness_edges_reset(void)
+{
+    memset(dyn_n, 0, sizeof(dyn_n));
+    memset(slot_reg, 0, sizeof(slot_reg));
+}
+
 static void slots_of(int r, const struct cne_node_register *reg)
 {
     slot_reg[r] = reg;
     for (int e = 0; e < MAX_EDGES; e++) {
-        const char *to = e < reg->nb_edges ? reg->next_nodes[e] : "";
+        const char *to = edge_name(r, e);
         slot_k[r][e] = (int8_t)(strcmp(to, "ip4_rewrite") == 0 ? 0 : strcmp(to, "pkt_drop") == 0 ? 1 : 2);
         slot_s[r][e] = (int8_t)name_slot(to);
     }
@@ -82,6 +152,55 @@ static void put(void **dst, uint32_t *n, void **objs, uint16_t nb)
     const uint32_t k = *n + nb <= MAX_OUT ? nb : MAX_OUT - *n;
     memcpy(dst + *n, objs, k * sizeof(void *));
     *n += k;
+}
+
+/* Chained walks (harness_chain(1)): an enqueue to an edge naming a node of
+ * this harness appends to that node's stream and marks it pending; pending
+ * nodes run, in the order they became pending, after each process / source
+ * turn -- cne_graph_walk's circular buffer (cne_graph_worker.h:125-170),
+ * streams growing past a burst as __cne_node_enqueue_prologue lets them. */
+static int chain_on;
+static void **strm[MAX_REG];
+static uint32_t strm_n[MAX_REG], strm_cap[MAX_REG];
+static int pend[MAX_REG * 4], pend_h, pend_t;
+
+void harness_chain(int on) { chain_on = on; }
+
+static int chain_to(const char *to, void **objs, uint16_t nb)
+{
+    int t = -1;
+    for (int i = 0; i < n_regs; i++)
+        if (strcmp(regs[i]->name, to) == 0 && !(regs[i]->flags & CNE_NODE_SOURCE_F))
+            t = i;
+    if (t < 0)
+        return 0;
+    if (strm_n[t] + nb > strm_cap[t]) {
+        const uint32_t cap = (strm_n[t] + nb) * 2;
+        void **a = realloc(strm[t], cap * sizeof(void *));
+        if (!a)
+            return 0;
+        strm[t] = a;
+        strm_cap[t] = cap;
+    }
+    if (strm_n[t] == 0)
+        pend[pend_t++ % (MAX_REG * 4)] = t;
+    memcpy(strm[t] + strm_n[t], objs, nb * sizeof(void *));
+    strm_n[t] += nb;
+    return 1;
+}
+
+static void run_pending(void)
+{
+    while (pend_h != pend_t) {
+        const int t = pend[pend_h++ % (MAX_REG * 4)];
+        const uint32_t cnt = strm_n[t];
+        void **objs = strm[t];
+        strm[t] = NULL; // the node's objs for this call; enqueues during it start a new stream
+        strm_n[t] = strm_cap[t] = 0;
+        if (cnt)
+            regs[t]->process(&g, &nodes[t], objs, (uint16_t)cnt);
+        free(objs);
+    }
 }
 
 void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16_t nb_objs)
@@ -97,6 +216,8 @@ void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16
         slots_of(r, node->reg);
     }
     const int e = next < MAX_EDGES ? next : MAX_EDGES - 1;
+    if (chain_on && chain_to(edge_name(r, e), objs, nb_objs))
+        return;
     put(out[slot_k[r][e]], &n_out[slot_k[r][e]], objs, nb_objs);
     if (slot_s[r][e] >= 0)
         put(e_out[slot_s[r][e]], &e_n[slot_s[r][e]], objs, nb_objs);
@@ -146,6 +267,7 @@ void harness_drop_clones(void)
     memset(slot_reg, 0, sizeof(slot_reg));
     while (n_regs > 0 && regs[n_regs - 1]->parent_id != CNE_NODE_ID_INVALID) {
         free((void *)regs[n_regs - 1]);
+        dyn_n[n_regs - 1] = 0;
         n_regs--;
     }
 }
@@ -188,7 +310,9 @@ int harness_process(const char *name, void **objs, uint16_t n)
     const int i = find(name);
     if (i < 0)
         return -1;
-    return regs[i]->process(&g, &nodes[i], objs, n);
+    const int r = regs[i]->process(&g, &nodes[i], objs, n);
+    run_pending();
+    return r;
 }
 
 /* the source nodes' turn of one cne_graph_walk */
@@ -198,6 +322,7 @@ int harness_walk_sources(void)
     for (int i = 0; i < n_regs; i++)
         if (regs[i]->flags & CNE_NODE_SOURCE_F)
             total += regs[i]->process(&g, &nodes[i], NULL, 0);
+    run_pending();
     return total;
 }
 
@@ -234,8 +359,8 @@ int harness_node_edges(int i, const char **names, int max)
     if (i < 0 || i >= n_regs)
         return -1;
     int k = 0;
-    for (; k < regs[i]->nb_edges && k < max; k++)
-        names[k] = regs[i]->next_nodes[k];
+    for (; k < edge_count(i) && k < max; k++)
+        names[k] = edge_name(i, k);
     return k;
 }
 
@@ -266,6 +391,7 @@ double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, 
             harness_walk_sources();
             const uint16_t c = (uint16_t)(n - b < burst ? n - b : burst);
             regs[i]->process(&g, &nodes[i], objs + b, c);
+            run_pending();
         }
         for (long spin = 0; n_out[0] + n_out[1] + n_out[2] < n; spin++) {
             if (spin > 100000000L)

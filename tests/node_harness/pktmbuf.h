@@ -1,6 +1,6 @@
 /*
  * Test-only stand-in for pktmbuf.h: the pktmbuf_t layout of pktmbuf.h:102-204
- * as the node source needs it (offsetof(pktmbuf_t, udata64)).
+ * as the node sources need it (offsetof(pktmbuf_t, udata64), pktmbuf_metadata).
  */
 #ifndef NODE_HARNESS_PKTMBUF_H
 #define NODE_HARNESS_PKTMBUF_H
@@ -22,4 +22,22 @@ typedef struct pktmbuf_s {
     uint64_t udata64;
 } pktmbuf_t;
 _Static_assert(sizeof(pktmbuf_t) == 64, "pktmbuf_t is one cache line");
+
+/* the two fields of pktmbuf_info_t (pktmbuf.h:77-88) pktmbuf_metadata reads
+ * (test-only layout: the harness builds these itself) */
+typedef struct pktmbuf_info_s {
+    uint32_t metadata_bufsz;
+    char *metadata;
+} pktmbuf_info_t;
+
+/* pktmbuf.h:1209-1220 */
+static inline void *pktmbuf_metadata(const pktmbuf_t *m)
+{
+    const pktmbuf_info_t *p;
+    if (!m)
+        return (void *)0;
+    if ((p = (const pktmbuf_info_t *)m->pooldata) != (void *)0 && p->metadata)
+        return p->metadata + (uint64_t)m->meta_index * p->metadata_bufsz;
+    return (char *)m + sizeof(pktmbuf_t);
+}
 #endif

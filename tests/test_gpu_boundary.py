@@ -179,3 +179,48 @@ def test_scratch_stream_order(gpu):
     for o, r in zip(outs, refs):
         assert_same(o, r)
     cl.close()
+
+
+def test_fib_add_while_lookup(gpu):
+    """cnet adds routes at run time while graphs walk: one thread adds and
+    deletes routes (cne_fib_add / _delete) while three threads call
+    cne_fib_lookup_bulk, which syncs the device mirror from the dirty ranges.
+    The ranges change under the table's lock, so no sync copies a
+    half-painted range or clears marks it did not copy: once the writer is
+    done, every lookup equals brute-force LPM over the final routes."""
+    from cndp_amd.fib import Fib
+    f = Fib("churn", N.CNE_FIB_DIR24_8, default_nh=3, max_routes=8192, nh_sz=N.CNE_FIB_DIR24_8_4B,
+            num_tbl8=1024)
+    rng = np.random.default_rng(77)
+    keys = (0x0B000000 | rng.integers(0, 1 << 24, size=1 << 14, dtype=np.uint64)).astype(np.uint32)
+    routes = {}
+    stop = threading.Event()
+    errors = []
+
+    def reader():
+        try:
+            while not stop.is_set():
+                f.lookup_bulk(keys[:4096])
+        except Exception as ex:  # noqa: BLE001
+            errors.append(repr(ex))
+
+    th = [threading.Thread(target=reader) for _ in range(3)]
+    for t in th:
+        t.start()
+    try:
+        for k in range(3000):
+            d = int(rng.choice([16, 20, 24, 24, 28, 32]))
+            ip = (0x0B000000 | int(rng.integers(0, 1 << 24))) & (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+            if k % 5 == 4 and routes:
+                (dip, dd) = list(routes)[int(rng.integers(0, len(routes)))]
+                assert f.delete(dip, dd) == 0
+                del routes[(dip, dd)]
+            elif f.add(ip, d, k + 10) == 0:
+                routes[(ip, d)] = k + 10
+    finally:
+        stop.set()
+        for t in th:
+            t.join()
+    assert not errors, errors
+    want = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], 3, keys)
+    assert np.array_equal(f.lookup_bulk(keys), want)

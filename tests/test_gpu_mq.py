@@ -5,12 +5,16 @@ oracle, on mbuf pools laid out like CNDP's (pktmbuf.h:102-204, pktmbuf.c:60-80).
   cnet input chain  lib/cnet/eth/eth_rx.c:35-63 (packet_type, ol_flags,
                     tx_offload, lport, pktmbuf_adj_offset), lib/cnet/ptype/ptype.c:48-210
                     (4-wide speculation over the submitted bursts), ip4_input.c /
-                    ip6_input.c:50-260 (data_len, edges)
+                    ip6_input.c:50-260 (data_len, edges, cnet_metadata :33-48 / :32-48)
+  ip4_rewrite node  lib/usr/clib/nodes/ip4_rewrite.c:40-247 (rewrite data, TTL,
+                    4-wide / tail checksum rule per burst, tx edge)
 
 Both frame paths run: zero-copy (the pool registered with
 cndp_gpu_host_register, kernels read the frames in host memory) and staged
 (frames copied into pinned staging).  Bursts are fed as a graph node would,
 draining the queue whenever it is full."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -188,13 +192,40 @@ def cnet_pool(n, routes, v6, zero_copy, shift=False):
     if not zero_copy:
         _no_reach_past_buffer(pool, range(0, n, 3), donor=2)
     pool.hdr["data_len"][::5] = 10
+    # pktmbuf_metadata(m) = m + 64 here (no pool metadata array): a pattern
+    # that shows which bytes the input nodes' save_metadata wrote
+    pool.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN] = MD_FILL
     return pool, pool.hdr.copy()
 
 
-def cnet_check(pool, orig, ref, t4, t6, lport):
-    """The mbuf fields eth_rx / the input nodes write, against the oracle
-    (ref: _cnet_expect); returns each mbuf's expected queue edge
-    (CNDP_MQ_EDGE(node, e))."""
+MD_LEN, MD_FILL = 40, 0xAB   # struct cnet_metadata {faddr, laddr} (cnet_meta.h:20-25)
+
+
+def md_expect(mem, n, mt, at_input, v6):
+    """The cnet_metadata bytes at m + 64 after the chain: for a frame an input
+    node took, ipv4/ipv6_save_metadata's faddr / laddr {family, len, address}
+    from the IP header at its mtod (ip4_input.c:33-48, ip6_input.c:32-48; AF_INET
+    2, AF_INET6 10); cin_port and the rest of the union untouched."""
+    want = np.full((n, MD_LEN), MD_FILL, np.uint8)
+    for i in np.nonzero(at_input)[0]:
+        o = int(mt[i])
+        if v6[i]:
+            want[i, 0:2] = (10, 16)
+            want[i, 20:22] = (10, 16)
+            want[i, 4:20] = mem[o + 8:o + 24]
+            want[i, 24:40] = mem[o + 24:o + 40]
+        else:
+            want[i, 0:2] = (2, 4)
+            want[i, 20:22] = (2, 4)
+            want[i, 4:8] = mem[o + 12:o + 16]
+            want[i, 24:28] = mem[o + 16:o + 20]
+    return want
+
+
+def cnet_check(pool, orig, ref, t4, t6, lport, check_md=True):
+    """The mbuf fields eth_rx / the input nodes write, and the input nodes'
+    cnet_metadata, against the oracle (ref: _cnet_expect); returns each mbuf's
+    expected queue edge (CNDP_MQ_EDGE(node, e))."""
     n = pool.n
     h = pool.hdr
     bad = np.nonzero(h["packet_type"] != ref["ptype"])[0]
@@ -238,6 +269,12 @@ def cnet_check(pool, orig, ref, t4, t6, lport):
             nh = int(O.dir24_8_lookup(t4[0], t4[1], dip)[0])
         e_in[i] = nh >> 24
     assert (at_input & ~adj).sum() > 0
+    if check_md:
+        got_md = pool.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN]
+        want_md = md_expect(pool.mem, n, mt, at_input, v6)
+        bad = np.nonzero(np.any(got_md != want_md, axis=1))[0]
+        assert bad.size == 0, f"{bad.size} cnet_metadata differ, first {bad[:4]}: " \
+                              f"{bytes(got_md[bad[0]]).hex()} want {bytes(want_md[bad[0]]).hex()}"
     node = np.where(at_input, np.where(v6, N.CNDP_MQ_NODE_IP6, N.CNDP_MQ_NODE_IP4), N.CNDP_MQ_NODE_PTYPE)
     return (node << 8) | np.where(at_input, e_in, e8 & 0x7F)
 
@@ -333,13 +370,18 @@ def test_mq_backpressure_and_errors(l3, gpu):
     assert got == 512 and q.pending == 0
     assert q.submit(pool.ptrs(range(512, 768))) == 256
     q.close()
-    # an mbuf outside the registered region is refused
+    # an mbuf outside every registered region is accepted and comes back
+    # untouched with CNDP_MQ_EDGE_NONE (the node sends it to pkt_drop)
     cl.host_register(pool.mem)
     try:
         q2 = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, umem=pool.base)
         other = MbufPool(4)
-        assert cl._L.cndp_gpu_mq_submit(q2.h, other.ptrs(range(4)), 4) == -22
+        other.fill(pktgen.packed_ipv4(4, routes=pktgen.l3fwd_routes(), seed=8))
+        other.hdr["udata64"] = 7
+        a, e = q2.run(other, np.arange(4), [4])
         q2.close()
+        assert np.array_equal(other.index_of(a), np.arange(4))
+        assert np.all(e == N.CNDP_MQ_EDGE_NONE) and np.all(other.hdr["udata64"] == 7)
     finally:
         cl.host_unregister(pool.mem)
     # bad configurations
@@ -386,3 +428,247 @@ def test_c1_cndpfwd_loopback(l3, gpu, zero_copy):
     assert np.array_equal(pool.mem, want)
     d = pool.data_pos().astype(np.int64)
     assert np.all(pool.mem[d[:, None] + np.arange(6, 12)] == 0xFF)   # broadcast now the source
+
+
+@pytest.mark.parametrize("fold,grid", [(1, 1), (1, 2), (2, 1), (2, 2)])
+def test_mq_cnet_branches(cn, gpu, fold, grid):
+    """The host-side launch choices made from hint words an earlier kernel
+    wrote -- where the frames off the fast path and the speculation classes
+    pass run (the fast kernel's last block or a second launch), and the local
+    pass's grid -- forced each way over one fixed mbuf batch: every field
+    equals the oracle's, on the first call after a node-state reset and on
+    the calls chained after it (ptype.c:48-210 state carried)."""
+    cl, routes, v6, t4, t6 = cn
+    n = 12000
+    pool, orig = cnet_pool(n, routes, v6, zero_copy=True)
+    bursts = _bursts(n, 33, "ragged")
+    order = np.arange(n)
+    cl.host_register(pool.mem)
+    try:
+        cl.set_tuning(cnet_spec=256, cnet_fold=fold, spec_grid=grid)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=4096, depth=2, umem=pool.base, lport=2)
+        ref = _cnet_expect(pool, order, bursts, t4, t6, 0, 2)
+        addrs, edges = q.run(pool, order, bursts)
+        q.close()
+    finally:
+        cl.set_tuning(cnet_fold=0, spec_grid=0)
+        cl.host_unregister(pool.mem)
+    assert np.array_equal(pool.index_of(addrs), order)
+    want_e = cnet_check(pool, orig, ref, t4, t6, 2)
+    assert np.array_equal(edges.astype(np.int64), want_e)
+
+
+@pytest.mark.parametrize("grid", [1, 2])
+def test_mq_cnet_uniform_branches(cn, gpu, grid):
+    """A uniform batch (every frame IPv4/UDP, GTP-U / GTP-C ports among them:
+    one low ptype byte under three edges) through the uniform speculation pass
+    on a forced small and full grid, from a reset node state and chained."""
+    cl, routes, v6, t4, t6 = cn
+    n = 8192
+    pool = MbufPool(n)
+    pool.fill(pktgen.packed_ipv4(n, routes=routes, seed=17))
+    d = pool.data_pos().astype(np.int64)
+    for i in range(3, n, 97):   # GTP-U / GTP-C destination ports in the plain UDP run
+        port = 2152 if i % 2 else 2123
+        pool.mem[d[i] + 36], pool.mem[d[i] + 37] = port >> 8, port & 0xFF
+    pool.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN] = MD_FILL
+    orig = pool.hdr.copy()
+    bursts = [256] * (n // 256)
+    cl.host_register(pool.mem)
+    try:
+        cl.set_tuning(cnet_spec=256, spec_grid=grid)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=2048, depth=2, umem=pool.base)
+        ref = _cnet_expect(pool, np.arange(n), bursts, t4, t6, 0, 0)
+        addrs, edges = q.run(pool, np.arange(n), bursts)
+        q.close()
+    finally:
+        cl.set_tuning(spec_grid=0)
+        cl.host_unregister(pool.mem)
+    # runts are part of cnet_pool, not of this batch: check without the
+    # runt assertion (every frame here keeps its L2 header)
+    h = pool.hdr
+    assert np.array_equal(h["packet_type"], ref["ptype"])
+    e8 = ref["edge"].astype(np.int64)
+    low = ref["ptype"] & 0xFF
+    node = np.where(e8 < 0x80, np.where((low == 0x41) | (low == 0xC1) | (low == 0xE1), 2, 1), 0)
+    assert np.array_equal(edges.astype(np.int64) >> 8, node)
+    assert np.array_equal(edges.astype(np.int64) & 0xFF, np.where(e8 < 0x80, e8, e8 & 0x7F))
+    mt = np.arange(n, dtype=np.int64) * 2048 + HDR + orig["data_off"].astype(np.int64) + 14
+    got_md = pool.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN]
+    assert np.array_equal(got_md, md_expect(pool.mem, n, mt, e8 < 0x80, np.zeros(n, bool)))
+    assert (node == 0).sum() > 0   # GTP-U frames the quirk did not re-route
+
+
+def _rewrite_setup(cl, seed):
+    """Rewrite table on the context (ip4_rewrite_set_next + cne_node_ip4_rewrite_add
+    semantics) and the same entries as the oracle's table."""
+    rng = np.random.default_rng(seed)
+    tbl = np.zeros(64, dtype=O.REWRITE_NH)
+    for p in range(4):
+        cl.rewrite_set_next(p, p + 1)
+    for nh in range(64):
+        if nh % 9 == 8:
+            continue   # unset entries: no data, edge 0
+        ln = int(rng.choice([12, 12, 12, 0, 14, 30, 56]))
+        data = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
+        port = nh % 4
+        assert cl.rewrite_add(nh, data, port) == 0
+        tbl[nh]["rewrite_len"] = ln
+        tbl[nh]["tx_node"] = port + 1
+        tbl[nh]["enabled"] = 1
+        tbl[nh]["rewrite_data"][:ln] = np.frombuffer(data, np.uint8)
+    return tbl
+
+
+@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
+def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
+    """The ip4_rewrite node over pktmbuf bursts, byte for byte against the
+    oracle's node loop run over the same bursts: next hops 0..69 (>= 64 and
+    unset entries leave by edge 0 unchanged but TTL / checksum), checksums
+    0xFFFE / 0xFFFF and cksum words with high bits set (the 4-wide u32 carry
+    against the tail's u16 rule, ip4_rewrite.c:97-110 / :209-216), TTL 0."""
+    cl, fib, t4 = l3
+    tbl = _rewrite_setup(cl, 3)
+    n = 9000
+    pools = [MbufPool(n), MbufPool(n)]
+    fr = _mixed_l3_frames(n, seed=21)
+    rng = np.random.default_rng(22)
+    ck = rng.integers(0, 1 << 16, n, dtype=np.uint64)
+    ck[::7] = 0xFFFF
+    ck[3::7] = 0xFFFE
+    ck[5::11] |= np.uint64(1) << np.uint64(16 + int(rng.integers(0, 16)))
+    priv = (rng.integers(0, 70, n, dtype=np.uint64) | (rng.integers(0, 256, n, dtype=np.uint64) << 16)
+            | (ck << 32))
+    priv[::13] &= ~np.uint64(0xFFFF << 16)   # TTL 0
+    for p in pools:
+        if kind == "shifted":
+            p.hdr["data_off"] = 256 + np.arange(n) % 61
+        p.fill(fr)
+        p.hdr["udata64"] = priv
+    gpool, opool = pools
+    bursts = _bursts(n, 23, kind)
+    order = np.random.default_rng(24).permutation(n)
+    pos = 0
+    want_tx = np.zeros(n, np.uint16)
+    for b in bursts:   # the oracle: one node process() per burst
+        idx = order[pos:pos + b]
+        want_tx[pos:pos + b] = O.ip4_rewrite_node(opool.ptrs(idx), b, tbl)
+        pos += b
+    umem = None
+    if zero_copy:
+        cl.host_register(gpool.mem)
+        umem = gpool.base
+    try:
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_REWRITE, batch=4096, depth=3, umem=umem)
+        addrs, edges = q.run(gpool, order, bursts)
+        q.close()
+    finally:
+        if zero_copy:
+            cl.host_unregister(gpool.mem)
+    assert np.array_equal(gpool.index_of(addrs), order)
+    assert np.array_equal(edges, want_tx)
+    bad = np.nonzero(np.any(gpool.mem.reshape(n, -1) != opool.mem.reshape(n, -1), axis=1))[0]
+    assert bad.size == 0, f"{bad.size} frames differ from the oracle's, first {bad[:4]}"
+    assert set(np.unique(edges).tolist()) == {0, 1, 2, 3, 4}
+
+
+def test_mq_zero_copy_regions(l3, gpu):
+    """Zero-copy over several registered regions (a graph's ports with pools
+    of their own): mbufs of two registered pools interleaved in one queue get
+    their results; an mbuf of an unregistered pool, and an mbuf whose buffer
+    lies outside every region, come back untouched with CNDP_MQ_EDGE_NONE."""
+    cl, fib, t4 = l3
+    n = 3000
+    pa, pb, pc = MbufPool(n), MbufPool(n), MbufPool(n)
+    for k, p in enumerate((pa, pb, pc)):
+        p.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=40 + k))
+        p.hdr["udata64"] = 0x5A5A
+    outside = np.zeros(4096, np.uint8)
+    pa.hdr["buf_addr"][7] = outside.ctypes.data   # header in a region, buffer not
+    cl.host_register(pa.mem)
+    cl.host_register(pb.mem)
+    try:
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, batch=2048, depth=3, umem=pb.base)
+        ptrs = (ctypes.c_void_p * (3 * n))()
+        src = np.empty(3 * n, np.int64)
+        for i in range(n):
+            for k, p in enumerate((pa, pb, pc)):
+                ptrs[3 * i + k] = p.addr(i)
+                src[3 * i + k] = k
+        got_a, got_e = [], []
+        for b0 in range(0, 3 * n, 256):
+            cnt = min(256, 3 * n - b0)
+            done = 0
+            while done < cnt:
+                k = q.submit(ctypes.addressof(ptrs) + (b0 + done) * 8, cnt - done)
+                done += k
+                a, e = q.poll()
+                got_a.append(a)
+                got_e.append(e)
+                if k == 0 and a.size == 0:
+                    q.wait()
+        while q.pending:
+            q.flush()
+            q.wait()
+            a, e = q.poll()
+            got_a.append(a)
+            got_e.append(e)
+        q.close()
+    finally:
+        cl.host_unregister(pa.mem)
+        cl.host_unregister(pb.mem)
+    a = np.concatenate(got_a)
+    e = np.concatenate(got_e)
+    assert np.array_equal(a, np.array([x for x in ptrs], np.uint64))
+    assert np.all(e[src == 2] == N.CNDP_MQ_EDGE_NONE) and np.all(pc.hdr["udata64"] == 0x5A5A)
+    assert e[3 * 7] == N.CNDP_MQ_EDGE_NONE and pa.hdr["udata64"][7] == 0x5A5A
+    for k, p in ((0, pa), (1, pb)):
+        d = p.data_pos().astype(np.int64)
+        dip = np.zeros(n, np.uint32)
+        for j in range(4):
+            dip = (dip << 8) | p.mem[d + 30 + j].astype(np.uint32)
+        val = O.dir24_8_lookup(t4[0], t4[1], dip).astype(np.uint64)
+        want = (val & 0xFFFF) | (p.mem[d + 22].astype(np.uint64) << 16) | \
+            ((p.mem[d + 24].astype(np.uint64) | (p.mem[d + 25].astype(np.uint64) << 8)) << 32)
+        ok = np.ones(n, bool)
+        if k == 0:
+            ok[7] = False
+        assert np.array_equal(p.hdr["udata64"][ok], want[ok])
+        assert np.array_equal(e[src == k][ok], (val[ok] >> 16).astype(np.uint16))
+
+
+def test_host_register_shared(l3, gpu):
+    """hipHostRegister is per process: a region registered through two
+    contexts (two graphs' nodes) is shared and reference counted -- both
+    contexts run zero-copy queues on it, one unregistering leaves the other
+    working, the last reference unregisters."""
+    from cndp_amd.classify import Classifier
+    cl, fib, t4 = l3
+    cl2 = Classifier(0)
+    cl2.set_fib(fib)
+    n = 2048
+    pool = MbufPool(n)
+    pool.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=50))
+    cl.host_register(pool.mem)
+    cl2.host_register(pool.mem)   # second context: a reference, not -EEXIST
+    try:
+        for c in (cl, cl2):
+            pool.hdr["udata64"] = 0
+            q = MbufQueue(c, N.CNDP_MQ_IP4_LOOKUP, batch=1024, depth=2, umem=pool.base)
+            a, e = q.run(pool, np.arange(n), [256] * (n // 256))
+            q.close()
+            assert np.all(e != N.CNDP_MQ_EDGE_NONE) and np.all(pool.hdr["udata64"] != 0)
+        cl.host_unregister(pool.mem)
+        pool.hdr["udata64"] = 0
+        q = MbufQueue(cl2, N.CNDP_MQ_IP4_LOOKUP, batch=1024, depth=2, umem=pool.base)
+        a, e = q.run(pool, np.arange(n), [256] * (n // 256))
+        q.close()
+        assert np.all(e != N.CNDP_MQ_EDGE_NONE) and np.all(pool.hdr["udata64"] != 0)
+    finally:
+        cl2.host_unregister(pool.mem)
+        cl2.close()
+    # unregistered by the last reference: registering again works
+    cl.host_register(pool.mem)
+    cl.host_unregister(pool.mem)
+    assert cl._L.cndp_gpu_host_unregister(cl.h, ctypes.c_void_p(pool.base)) == -2   # -ENOENT

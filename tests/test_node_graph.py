@@ -47,6 +47,7 @@ def test_node_registry():
         info[name.value.decode()] = (fl.value, ne.value, e0.value, e1.value)
     assert info["ip4_lookup"] == (0, 2, b"ip4_rewrite", b"pkt_drop")
     assert info["ip4_lookup_gpu_drain"] == (1, 2, b"ip4_rewrite", b"pkt_drop")
+    assert info["ip4_rewrite"] == (0, 1, b"pkt_drop", None)
     assert all(k.startswith("ip4") for k in info)
 
 
@@ -325,3 +326,236 @@ def test_cnet_node_clones_per_port(gpu):
     want_e = cnet_check(pool, orig, ref, t4, t6, lport)
     want = np.array([_edge_of_queue_code(int(e)) for e in want_e])
     assert np.array_equal(got, want)
+
+
+# ---- the GPU ip4_rewrite node (cndp_amd/node/ip4_rewrite_gpu.c) -----------
+def _rw_harness():
+    H = _harness()
+    H.cne_node_edge_update.restype = ctypes.c_uint16
+    H.cne_node_edge_update.argtypes = [ctypes.c_uint32, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint16]
+    H.cne_node_edge_count.restype = ctypes.c_uint16
+    H.cne_node_edge_count.argtypes = [ctypes.c_uint32]
+    H.harness_node_edges.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    H.harness_take_edge.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32]
+    H.harness_take_edge.restype = ctypes.c_uint32
+    return H
+
+
+def _node_ids(H):
+    name = ctypes.create_string_buffer(64)
+    fl, ne = ctypes.c_uint64(), ctypes.c_int()
+    e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
+    n = H.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+    ids = {}
+    for i in range(n):
+        H.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+        ids[name.value.decode()] = i
+    return ids
+
+
+def _eth_config(H, L, ports):
+    """cne_node_eth_config's part for ip4_rewrite (pktdev_ctrl.c:75-86): a
+    "pktdev_tx-<port>" edge added to ip4_rewrite per port, then
+    ip4_rewrite_set_next(port, its edge index)."""
+    rw = _node_ids(H)["ip4_rewrite"]
+    for p in ports:
+        nm = ctypes.c_char_p(f"pktdev_tx-{p}".encode())
+        assert H.cne_node_edge_update(rw, 0xFFFF, ctypes.byref(nm), 1) != 0xFFFF
+        assert L.ip4_rewrite_set_next(p, H.cne_node_edge_count(rw) - 1) == 0
+
+
+def _edges_of(H, i):
+    names = (ctypes.c_char_p * 16)()
+    k = H.harness_node_edges(i, names, 16)
+    return list(names[:k])
+
+
+def test_rewrite_node_registry():
+    """ip4_rewrite registered as ip4_rewrite.c:314-326 (edge 0 pkt_drop),
+    plus its drain source node; the tx edges cne_node_eth_config adds to
+    ip4_rewrite show up on the drain node too (the ip4_rewrite_set_next hook),
+    so the edge index a next hop's tx_node names is the same on both."""
+    H = _rw_harness()
+    L = N.lib()
+    ids = _node_ids(H)
+    name = ctypes.create_string_buffer(64)
+    fl, ne = ctypes.c_uint64(), ctypes.c_int()
+    e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
+    H.harness_node_info(ids["ip4_rewrite"], name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0),
+                        ctypes.byref(e1))
+    assert (fl.value, ne.value, e0.value) == (0, 1, b"pkt_drop")
+    H.harness_node_info(ids["ip4_rewrite_gpu_drain"], name, ctypes.byref(fl), ctypes.byref(ne),
+                        ctypes.byref(e0), ctypes.byref(e1))
+    assert (fl.value, ne.value, e0.value) == (1, 1, b"pkt_drop")
+    L.cndp_node_ip4_rewrite_reset()
+    try:
+        _eth_config(H, L, (0, 3))
+        want = [b"pkt_drop", b"pktdev_tx-0", b"pktdev_tx-3"]
+        assert _edges_of(H, ids["ip4_rewrite"]) == want
+        assert _edges_of(H, ids["ip4_rewrite_gpu_drain"]) == want
+        # the table behind cne_node_ip4_rewrite_add takes the tx edge of the port
+        data = (ctypes.c_uint8 * 12)(*range(12))
+        assert L.cne_node_ip4_rewrite_add(5, data, 12, 3) == 0
+        tx = ctypes.c_uint16()
+        assert L.cndp_node_ip4_rewrite_get(5, None, None, ctypes.byref(tx), None) == 0 and tx.value == 2
+        assert L.cne_node_ip4_rewrite_add(6, data, 12, 1) == -22   # port 1 has no tx edge
+    finally:
+        H.harness_edges_reset()
+        L.cndp_node_ip4_rewrite_reset()
+
+
+def _rw_table(L, seed, ports):
+    """Next hops through cne_node_ip4_rewrite_add (the process-global table the
+    GPU node follows) and the oracle's copy of it."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(seed)
+    tbl = np.zeros(64, dtype=O.REWRITE_NH)
+    for nh in range(64):
+        if nh % 9 == 8:
+            continue
+        ln = int(rng.choice([12, 12, 12, 0, 14, 30, 56]))
+        data = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
+        k = nh % len(ports)
+        assert L.cne_node_ip4_rewrite_add(nh, ctypes.create_string_buffer(data, max(ln, 1)), ln, ports[k]) == 0
+        tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = ln, k + 1, 1
+        tbl[nh]["rewrite_data"][:ln] = np.frombuffer(data, np.uint8)
+    return tbl
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_rewrite_node_graph_walk(gpu, zero_copy):
+    """Bursts into the GPU ip4_rewrite node's process(), graph walks drain it:
+    every mbuf leaves by its next hop's pktdev_tx-<port> edge (or pkt_drop),
+    in order per edge, and every frame equals the oracle node loop's over the
+    same bursts (rewrite data, TTL - 1, the 4-wide / tail checksum rule of
+    each burst)."""
+    from cndp_amd import pktgen
+    from cndp_amd.mbuf import MbufPool
+    from oracle import oracle as O
+    H = _rw_harness()
+    L = N.lib()
+    ports = (0, 2, 5)
+    n = 12000
+    gp, op = MbufPool(n), MbufPool(n)
+    rng = np.random.default_rng(61)
+    ck = rng.integers(0, 1 << 16, n, dtype=np.uint64)
+    ck[::5] = 0xFFFF
+    ck[2::5] = 0xFFFE
+    priv = rng.integers(0, 70, n, dtype=np.uint64) | (rng.integers(0, 256, n, dtype=np.uint64) << 16) | (ck << 32)
+    for p in (gp, op):
+        p.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=62))
+        p.hdr["udata64"] = priv
+    L.cndp_node_ip4_rewrite_reset()
+    L.cndp_node_gpu_umem_reset()
+    if zero_copy:
+        assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
+    os.environ["CNDP_GPU_BATCH"] = "2048"
+    bursts = []
+    try:
+        _eth_config(H, L, ports)
+        tbl = _rw_table(L, 63, ports)
+        assert H.harness_graph_create(11) == 0
+        pos = 0
+        while pos < n:
+            b = int(min(n - pos, rng.choice([256, 256, 256, 97, 4, 3, 1])))
+            bursts.append(b)
+            assert H.harness_process(b"ip4_rewrite", gp.ptrs(np.arange(pos, pos + b)), b) == b
+            H.harness_walk_sources()
+            pos += b
+        names = [b"pkt_drop"] + [f"pktdev_tx-{p}".encode() for p in ports]
+        buf = (ctypes.c_void_p * n)()
+        for _ in range(200000):
+            if sum(H.harness_take_edge(nm, buf, n) for nm in names) == n:
+                break
+            H.harness_walk_sources()
+        got = np.full(n, -1, np.int64)
+        for k, nm in enumerate(names):
+            m = H.harness_take_edge(nm, buf, n)
+            idx = gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))
+            assert np.all(np.diff(idx) > 0), f"{nm}: out of order"
+            got[idx] = k
+    finally:
+        H.harness_graph_destroy()
+        H.harness_edges_reset()
+        L.cndp_node_ip4_rewrite_reset()
+        L.cndp_node_gpu_umem_reset()
+        os.environ.pop("CNDP_GPU_BATCH", None)
+    want = np.zeros(n, np.int64)
+    pos = 0
+    for b in bursts:
+        want[pos:pos + b] = O.ip4_rewrite_node(op.ptrs(np.arange(pos, pos + b)), b, tbl)
+        pos += b
+    assert np.array_equal(got, want)
+    bad = np.nonzero(np.any(gp.mem.reshape(n, -1) != op.mem.reshape(n, -1), axis=1))[0]
+    assert bad.size == 0, f"{bad.size} frames differ, first {bad[:4]}"
+    assert set(np.unique(got).tolist()) == {0, 1, 2, 3}
+
+
+@pytest.mark.gpu
+def test_l3fwd_graph_chain(gpu):
+    """The l3fwd-graph chain with both GPU nodes, walked as cne_graph_walk
+    runs it (ip4_lookup's enqueues fill ip4_rewrite's stream, which runs in
+    the same walk): every mbuf ends at pkt_drop or its next hop's tx edge with
+    priv1 and the rewritten frame of the reference chain (checksums where the
+    4-wide and tail rules agree, i.e. not 0xFFFE / 0xFFFF, whose rule depends
+    on the stream split)."""
+    from cndp_amd import pktgen
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    from cndp_amd.mbuf import MbufPool
+    from oracle import oracle as O
+    H = _rw_harness()
+    H.harness_chain.argtypes = [ctypes.c_int]
+    L = N.lib()
+    ports = (0, 1, 2, 3)
+    n = 20000
+    gp, op = MbufPool(n), MbufPool(n)
+    for p in (gp, op):
+        p.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=71))
+    NodeFib.fini()
+    L.cndp_node_ip4_rewrite_reset()
+    L.cndp_node_gpu_umem_reset()
+    assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
+    os.environ["CNDP_GPU_BATCH"] = "4096"
+    routes = pktgen.l3fwd_routes()
+    try:
+        _eth_config(H, L, ports)
+        tbl = _rw_table(L, 72, ports)
+        H.harness_chain(1)
+        assert H.harness_graph_create(12) == 0
+        for ip, d, nh in routes:
+            assert cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
+        assert H.harness_drive(b"ip4_lookup", gp.ptrs(np.arange(n)), n, 256, 1) >= 0
+        names = [b"pkt_drop"] + [f"pktdev_tx-{p}".encode() for p in ports]
+        buf = (ctypes.c_void_p * n)()
+        got = np.full(n, -1, np.int64)
+        for k, nm in enumerate(names):
+            m = H.harness_take_edge(nm, buf, n)
+            got[gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))] = k
+    finally:
+        H.harness_chain(0)
+        H.harness_graph_destroy()
+        H.harness_edges_reset()
+        L.cndp_node_ip4_rewrite_reset()
+        L.cndp_node_gpu_umem_reset()
+        os.environ.pop("CNDP_GPU_BATCH", None)
+    # the reference chain on the oracle's copy: ip4_lookup then ip4_rewrite
+    t24, t8 = O.dir24_8_build(list(routes), N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
+    d = op.data_pos().astype(np.int64)
+    dip = np.zeros(n, np.uint32)
+    for k in range(4):
+        dip = (dip << 8) | op.mem[d + 30 + k].astype(np.uint32)
+    val = O.dir24_8_lookup(t24, t8, dip).astype(np.uint64)
+    ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
+    op.hdr["udata64"] = (val & 0xFFFF) | (op.mem[d + 22].astype(np.uint64) << 16) | (ck << 32)
+    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
+    rw = np.nonzero((val >> 16) == 0)[0]
+    tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
+    want = np.zeros(n, np.int64)
+    want[rw] = tx
+    assert np.array_equal(got, want)
+    ok = (ck != 0xFFFE) & (ck != 0xFFFF)
+    diff = np.any(gp.mem.reshape(n, -1) != op.mem.reshape(n, -1), axis=1)
+    assert not np.any(diff & ok)
+    assert rw.size > n // 2 and (got == 0).sum() > 0
+    NodeFib.fini()
