@@ -250,14 +250,24 @@ def cpu_baseline(state, budget_s: float = 10.0):
     iters = max(1, int(budget_s / max(tt, 1e-6)))
     tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=iters, cpus=cpus, **kw)
     multi = n * iters / tt / 1e6
+    extra = {}
+    if cnet:
+        # CNDP's own cnet chain hashes nothing (no cne_softrss caller, SURVEY
+        # §0.3): the same chain without the flow hash, beside the value (which
+        # does the GPU line's work, hash included)
+        th = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=iters, cpus=cpus, no_hash=True, **kw)
+        extra["no_hash_Mpps"] = round(n * iters / th / 1e6, 2)
+        extra["no_hash_note"] = ("the cnet chain without the Toeplitz flow hash, which CNDP's cnet nodes "
+                                 "never compute (the reference chain's own work)")
     chain = ("cnet chain per 256-burst (cne_get_ptype restatement, eth_rx fields, ptype-node speculation, "
-             "ip4/ip6_input length + checksum + DIR-24-8 / trie lookups, cne_softrss)" if cnet else
+             "ip4/ip6_input length + checksum + DIR-24-8 / trie lookups, plus the build's cne_softrss flow "
+             "hash the GPU line computes and CNDP's cnet nodes do not -- no_hash_Mpps drops it)" if cnet else
              "l3fwd node loop per 256-burst (ethertype parse, pkt_cls, ip4_lookup's 4-wide "
              "cne_fib_lookup_bulk with dir24_8.h's prefetching lookup" +
              (", skipped in C2" if mode == N.CNDP_MODE_HASH else "") + ", cne_softrss restatement, RETA)")
     return {"value": round(multi, 2), "unit": "Mpps", "cores": len(cpus), "kind": "port",
             "cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
-            "single_core_Mpps": round(single, 2),
+            "single_core_Mpps": round(single, 2), **extra,
             "sample": (f"oracle/oracle.c {chain} over {n} of the same frames x {iters} passes on "
                        f"{len(cpus)} pinned threads ({tt:.1f} s); 1 thread: {single:.2f} Mpps")}
 
@@ -466,6 +476,9 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     l3["cpu_chain"] = "the ip4_lookup node loop over the same mbufs (oracle/oracle.c orc_ip4_lookup_mbufs)"
     NodeFib.fini()
     res["l3fwd_ip4_lookup"] = l3
+    # ---- l3fwd: the ip4_lookup + ip4_rewrite node pair, chained as a graph
+    # walk runs them (ip4_lookup's enqueues fill ip4_rewrite's stream)
+    res["l3fwd_lookup_rewrite"] = l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes)
     del ptrs, pool
     # ---- cnet: eth_rx + ptype + ip4_input / ip6_input
     nc = n // 4
@@ -576,6 +589,72 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     res["c1_loopback"] = lat
     cl.close()
     return res
+
+
+def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
+    """GPU ip4_lookup + GPU ip4_rewrite nodes (tests/node_harness chained
+    walks: pktdev_rx bursts -> ip4_lookup -> ip4_rewrite -> pktdev_tx-<port>)
+    against the same two nodes' loops on one core (oracle/oracle.c
+    orc_l3fwd_nodes_mbufs).  Four tx ports, 12-B MAC rewrites for the 64 next
+    hops, as l3fwd-graph sets them up (fwd.c:160-201, pktdev_ctrl.c:75-86)."""
+    import ctypes
+    import random
+    from cndp_amd import native as N
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    from oracle import oracle as O
+    H.cne_node_edge_update.restype = ctypes.c_uint16
+    H.cne_node_edge_update.argtypes = [ctypes.c_uint32, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint16]
+    H.cne_node_edge_count.restype = ctypes.c_uint16
+    H.cne_node_edge_count.argtypes = [ctypes.c_uint32]
+    H.harness_chain.argtypes = [ctypes.c_int]
+    name = ctypes.create_string_buffer(64)
+    fl, ne, e0, e1 = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_char_p(), ctypes.c_char_p()
+    k = H.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+    rw_id = None
+    for i in range(k):
+        H.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+        if name.value == b"ip4_rewrite":
+            rw_id = i
+    L.cndp_node_ip4_rewrite_reset()
+    tbl = np.zeros(64, dtype=O.REWRITE_NH)
+    rnd = random.Random(7)
+    out = {}
+    try:
+        for p in range(4):
+            nm = ctypes.c_char_p(f"pktdev_tx-{p}".encode())
+            H.cne_node_edge_update(rw_id, 0xFFFF, ctypes.byref(nm), 1)
+            assert L.ip4_rewrite_set_next(p, H.cne_node_edge_count(rw_id) - 1) == 0
+        for nh in range(64):
+            data = bytes(rnd.randrange(256) for _ in range(12))
+            assert L.cne_node_ip4_rewrite_add(nh, ctypes.create_string_buffer(data, 12), 12, nh % 4) == 0
+            tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = 12, nh % 4 + 1, 1
+            tbl[nh]["rewrite_data"][:] = np.frombuffer(data + bytes(44), np.uint8)
+        H.harness_chain(1)
+        for zc in (True, False):
+            L.cndp_node_gpu_umem_reset()
+            if zc:
+                L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
+            assert H.harness_graph_create(30 + int(zc)) == 0
+            for ip, d, nh in routes:
+                cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+            H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
+            t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
+            H.harness_graph_destroy()
+            out["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+        fib = NodeFib()
+        t24, t8 = (x.copy() for x in fib.image())
+        O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, 1)
+        t = O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, passes)
+        out["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+        out["cpu_chain"] = ("ip4_lookup's loop then ip4_rewrite_node_process per 256-burst over the same "
+                            "mbufs, one core (oracle/oracle.c orc_l3fwd_nodes_mbufs)")
+    finally:
+        H.harness_chain(0)
+        H.harness_edges_reset()
+        L.cndp_node_gpu_umem_reset()
+        L.cndp_node_ip4_rewrite_reset()
+        NodeFib.fini()
+    return out
 
 
 def load_traffic(cfg: str):

@@ -18,6 +18,7 @@
 
 #include <errno.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -5338,6 +5339,8 @@ struct MqArgs {
     const u32x4 *win;       // cnet: each fast-parsed or general-parsed frame's first 64 bytes
     const struct cndp_rw_nh *rw; // rewrite: next-hop table (device)
     uint32_t lport, want_hash;
+    uint32_t devhdr;        // ip4_lookup zc, CNDP_MQ_F_DEVICE_HEADERS: the kernel reads each mbuf's
+    int64_t delta;          //   header itself (frames in [slab, slab + slab_len), device = host + delta)
     MqTables tb;
     uint32_t *ticket;       // device arrival counter of this slot
     uint32_t *flag;         // device view of the slot's pinned completion flag
@@ -5376,11 +5379,23 @@ __device__ __forceinline__ uint8_t *mq_frame(uint64_t w, uint32_t &avail)
 __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
-        const uint64_t w = a.off[i];
+        const uint64_t w = a.devhdr ? 0u : a.off[i];
         const uint8_t *p; // bytes 20..35 of the frame
         uint32_t avail;   // readable bytes from p
         uint64_t m = 0;
-        if (a.zc) {
+        if (a.zc && a.devhdr) {
+            m = a.mb[i];
+            const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
+            const uint64_t buf = m ? *(const uint64_t *)(dm + MB_BUF_ADDR) : 0u;
+            const uint32_t doff = m ? *(const uint16_t *)(dm + MB_DATA_OFF) : 0u;
+            const uint64_t fo = (uint64_t)((int64_t)(buf + doff) + a.delta - (int64_t)(uintptr_t)a.slab);
+            if (m == 0 || fo >= a.slab_len) {
+                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
+                continue;
+            }
+            p = a.slab + fo + MQ_W4_AT;
+            avail = a.slab_len - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(a.slab_len - fo > MQ_W4_AT ? a.slab_len - fo - MQ_W4_AT : 0);
+        } else if (a.zc) {
             m = a.mb[i];
             uint32_t fa;
             const uint8_t *f = mq_frame(w, fa);
@@ -5687,7 +5702,6 @@ struct MqSlot {
     void **mb;             // host
     uint8_t *h, *hd;       // pinned + mapped block (host view, device view)
     uint8_t *d;            // device block (cnet classify outputs)
-    hipEvent_t ev;
 };
 
 struct MqRegion {
@@ -5712,6 +5726,7 @@ struct cndp_gpu_mq {
     uint32_t head, open, in_flight, seq; // head: oldest slot not fully polled
     uint32_t pending;
     int err;                       // a launch error not yet reported (returned by the next submit)
+    uint64_t n_batches, n_mbufs;   // launched so far (cndp_gpu_mq_stat)
     MqSlot slot[CNDP_MQ_DEPTH_MAX];
 };
 
@@ -5758,7 +5773,7 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP &&
         k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
-    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA))
+    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS))
         return -EINVAL;
     k.batch = k.batch ? k.batch : 8192u;
     k.depth = k.depth ? k.depth : 4u;
@@ -5831,8 +5846,7 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
         if (!sl->mb || hipHostMalloc((void **)&sl->h, q->h_bytes, hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void **)&sl->hd, sl->h, 0) != hipSuccess ||
             hipMalloc((void **)&sl->d, q->d_bytes) != hipSuccess ||
-            hipMemset(sl->d, 0, q->d_bytes) != hipSuccess || // iplen starts cleared
-            hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess)
+            hipMemset(sl->d, 0, q->d_bytes) != hipSuccess) // iplen starts cleared
             goto fail;
     }
     // the clears done before the queue's own (non-blocking) stream first runs
@@ -5859,8 +5873,6 @@ extern "C" void cndp_gpu_mq_free(cndp_gpu_mq_t *q)
             hipHostFree(sl->h);
         if (sl->d)
             hipFree(sl->d);
-        if (sl->ev)
-            hipEventDestroy(sl->ev);
     }
     if (q->flags)
         hipHostFree(q->flags);
@@ -5961,6 +5973,15 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
         a.tb = mq_tables(c, 0);
+        if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // the frames in conf.umem's region
+            for (int k = 0; k < q->nrg; k++)
+                if (q->rg[k].host == (const uint8_t *)q->conf.umem) {
+                    a.devhdr = 1;
+                    a.slab = q->rg[k].host + q->rg[k].delta;
+                    a.slab_len = q->rg[k].len;
+                    a.delta = q->rg[k].delta;
+                }
+        }
         hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
     } else {
         // one classify per run of equal-size graph bursts, the ptype node's
@@ -6003,7 +6024,6 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(MQ_TPB), 0, s, a);
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(sl->ev, s));
     return 0;
 }
 
@@ -6027,6 +6047,8 @@ static int mq_launch(cndp_gpu_mq_t *q)
         sl->state = MQ_FLIGHT;
         q->in_flight++;
     }
+    q->n_batches++;
+    q->n_mbufs += sl->n;
     q->open = (q->open + 1) % q->conf.depth;
     return r;
 }
@@ -6051,10 +6073,20 @@ static void mq_fill(cndp_gpu_mq_t *q, MqSlot *sl, void *const *mbufs, uint32_t k
     const uint32_t mode = q->conf.mode;
     const bool cnet = mode == CNDP_MQ_CNET, rw = mode == CNDP_MQ_IP4_REWRITE, zc = q->zc != 0;
     const bool want_md = cnet && zc && !(q->conf.flags & CNDP_MQ_F_NO_METADATA);
+    const bool devhdr = zc && mode == CNDP_MQ_IP4_LOOKUP && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS);
     uint8_t *H = sl->h;
     uint64_t *hmb = (uint64_t *)(H + q->h_mb), *hoff = (uint64_t *)(H + q->h_off);
     uint64_t *hlen = (uint64_t *)(H + q->h_len), *hmd = (uint64_t *)(H + q->h_md);
     const uint32_t vec = k & ~3u; // ip4_rewrite: the 4-wide loop's share of the burst
+    if (devhdr) { // the kernel reads the headers (CNDP_MQ_F_DEVICE_HEADERS): pointers only
+        for (uint32_t i = 0; i < k; i++) {
+            uint8_t *m = (uint8_t *)mbufs[i];
+            const int km = mq_region(q, m, 64);
+            sl->mb[sl->n + i] = m;
+            hmb[sl->n + i] = km < 0 ? 0u : (uint64_t)(intptr_t)(m + q->rg[km].delta);
+        }
+        return;
+    }
     for (uint32_t i = 0; i < k; i++) {
         // the mbuf headers MQ_PF ahead, the frames of the ones half as far
         // (their buf_addr already in cache) where the host copies frame bytes
@@ -6285,15 +6317,22 @@ extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges,
 {
     if (!q || (max && (!mbufs || !edges)))
         return -EINVAL;
-    // adaptive batching: a partly filled batch goes out when the GPU is idle
-    // or the batch has waited max_delay_us (a failed launch is reported by
-    // the next submit; its mbufs come back below with CNDP_MQ_EDGE_NONE)
+    // adaptive batching: a partly filled batch goes out once it has waited
+    // max_delay_us, or earlier when the GPU is idle and the batch is half
+    // full or half that old -- not at the first poll after any burst: under
+    // a steady stream that launched a batch every few graph bursts, and the
+    // launches (several us of host time each) became the host's largest
+    // per-mbuf cost (a failed launch is reported by the next submit; its
+    // mbufs come back below with CNDP_MQ_EDGE_NONE)
     MqSlot *op = &q->slot[q->open];
-    if (op->state == MQ_OPEN && op->n &&
-        (q->in_flight == 0 || now_ns() - op->t_open_ns >= (uint64_t)q->conf.max_delay_us * 1000u)) {
-        const int r = mq_launch(q);
-        if (r)
-            q->err = r;
+    if (op->state == MQ_OPEN && op->n) {
+        const uint64_t age = now_ns() - op->t_open_ns, dmax = (uint64_t)q->conf.max_delay_us * 1000u;
+        const bool idle = q->in_flight == 0 && (op->n >= q->conf.batch / 2u || age >= dmax / 2u);
+        if (idle || age >= dmax) {
+            const int r = mq_launch(q);
+            if (r)
+                q->err = r;
+        }
     }
     uint32_t got = 0;
     while (got < max) {
@@ -6323,14 +6362,42 @@ extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges,
     return (int)got;
 }
 
+extern "C" int64_t cndp_gpu_mq_stat(const cndp_gpu_mq_t *q, int key)
+{
+    if (!q)
+        return -EINVAL;
+    switch (key) {
+    case CNDP_MQ_STAT_BATCHES:
+        return (int64_t)q->n_batches;
+    case CNDP_MQ_STAT_MBUFS:
+        return (int64_t)q->n_mbufs;
+    default:
+        return -EINVAL;
+    }
+}
+
+// The oldest batch's completion flag (the load poll makes), spun on: no HIP
+// event per batch (an event record cost as much host time as a launch).
+// Bounded: a batch not done within CNDP_MQ_WAIT_S seconds is an error.
+#define CNDP_MQ_WAIT_S 30
 extern "C" int cndp_gpu_mq_wait(cndp_gpu_mq_t *q)
 {
     if (!q)
         return -EINVAL;
-    MqSlot *sl = &q->slot[q->head];
+    const uint32_t hi = q->head;
+    MqSlot *sl = &q->slot[hi];
     if (sl->state != MQ_FLIGHT)
         return 0;
-    HIP_TRY(hipEventSynchronize(sl->ev));
+    const uint64_t t0 = now_ns();
+    for (uint32_t spin = 0; __atomic_load_n(&q->flags[hi * 16u], __ATOMIC_ACQUIRE) != sl->seq; spin++) {
+        if ((spin & 255u) == 255u) {
+            if (now_ns() - t0 > CNDP_MQ_WAIT_S * 1000000000ull)
+                return -ETIMEDOUT;
+            sched_yield();
+        } else {
+            __builtin_ia32_pause();
+        }
+    }
     return 0;
 }
 

@@ -45,8 +45,9 @@ CNDP_TUNE_MBUF_HASH = 12
 CNDP_TUNE_CNET_FOLD = 13
 CNDP_TUNE_SPEC_GRID = 14
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
-CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA = 1, 2
+CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS = 1, 2, 4
 CNDP_MQ_EDGE_NONE = 0xFFFF
+CNDP_MQ_STAT_BATCHES, CNDP_MQ_STAT_MBUFS = 1, 2
 CNDP_MQ_NODE_PTYPE, CNDP_MQ_NODE_IP4, CNDP_MQ_NODE_IP6 = 0, 1, 2
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF
 
@@ -179,6 +180,7 @@ def lib():
         "cndp_gpu_mq_poll": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
         "cndp_gpu_mq_wait": (c_int, [c_void_p]),
         "cndp_gpu_mq_pending": (c_uint32, [c_void_p]),
+        "cndp_gpu_mq_stat": (ctypes.c_int64, [c_void_p, c_int]),
         "cndp_gpu_get_stat": (ctypes.c_int64, [c_void_p, c_int]),
         "cndp_gpu_version": (c_char_p, []),
     }

@@ -137,8 +137,9 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  * mbufs -- with every field the replaced nodes write already written back --
  * plus the next edge of each, in submission order.  A graph's source node
  * (node/ip4_lookup_gpu.c) polls once per walk, which also launches a partly
- * filled batch when the GPU has nothing in flight or the batch is older
- * than max_delay_us.
+ * filled batch when it is older than max_delay_us, or when the GPU has
+ * nothing in flight and the batch holds batch / 8 mbufs or is older than
+ * max_delay_us / 5.
  *
  * Frame bytes: when conf.umem names a region registered with
  * cndp_gpu_host_register (the AF_XDP UMEM / pktmbuf pool, cne_lport.h:91),
@@ -211,6 +212,10 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
 #define CNDP_MQ_IP4_REWRITE 3u
 #define CNDP_MQ_F_HASH (1u << 0)
 #define CNDP_MQ_F_NO_METADATA (1u << 1) /* cnet: leave cnet_metadata unwritten */
+/* ip4_lookup zero-copy: the host hands over mbuf pointers only and the kernel
+ * reads each header (buf_addr, data_off) in place -- no host touch per mbuf,
+ * three dependent PCIe reads per mbuf instead of one (frames in conf.umem) */
+#define CNDP_MQ_F_DEVICE_HEADERS (1u << 2)
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u
 #define CNDP_MQ_NODE_IP6 2u
@@ -249,6 +254,11 @@ int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges, uint32_t m
 int cndp_gpu_mq_wait(cndp_gpu_mq_t *q);
 /* mbufs accepted and not yet returned by poll. */
 uint32_t cndp_gpu_mq_pending(const cndp_gpu_mq_t *q);
+/* Counters since create: batches launched (CNDP_MQ_STAT_BATCHES) and the
+ * mbufs in them (CNDP_MQ_STAT_MBUFS); -EINVAL for an unknown key. */
+#define CNDP_MQ_STAT_BATCHES 1
+#define CNDP_MQ_STAT_MBUFS 2
+int64_t cndp_gpu_mq_stat(const cndp_gpu_mq_t *q, int key);
 
 /* ip4_rewrite node on the device (ip4_rewrite.c).  Control plane mirrors
  * ip4_rewrite_set_next (:252-263) and cne_node_ip4_rewrite_add (:265-295):

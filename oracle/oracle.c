@@ -833,7 +833,9 @@ static void classify_one(const struct orc_classify_args *a, uint32_t i)
         uint32_t l4t = pt & 0xf00u;
         uint32_t ip = hl.l2_len;
         int l4ok = (l4t == PT_L4_TCP || l4t == PT_L4_UDP);
-        if (l3 != 0 && !(l3 & 0x40u))
+        if (a->no_hash)
+            ;
+        else if (l3 != 0 && !(l3 & 0x40u))
             hash = hash_v4(v, ip, l4ok, ip + hl.l3_len, a->rss_key);
         else if (l3 & 0x40u)
             hash = hash_v6(v, ip, l4ok, ip + hl.l3_len, a->rss_key);
@@ -1029,7 +1031,7 @@ static void *bench_worker(void *arg)
                 for (uint32_t q = 0; q < m; q++) {
                     const uint8_t *ip = ptrs[k + q] + 14;
                     uint32_t h = 0;
-                    if (ptype[k + q] == 0x90u) {
+                    if (ptype[k + q] == 0x90u && !a->no_hash) {
                         struct pv v = {ptrs[k + q], 128};
                         uint32_t ihl = ip[0] & 0xfu;
                         int l4ok = ihl >= 5 && (ip[9] == 6 || ip[9] == 17) &&

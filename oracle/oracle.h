@@ -120,6 +120,8 @@ struct orc_classify_args {
                                  * ptype node's speculative 4-wide loop (ptype.c:48-210) over
                                  * graph bursts of B packets, uint8_t fix_spec quirk included */
     uint16_t *spec_state;       /* in/out: the node's ctx->last_type (NULL = start at 0) */
+    uint32_t no_hash;           /* 1: skip the build's flow hash (hash 0, queue reta[0]) -- the
+                                 * reference's own chain runs no Toeplitz */
 };
 int orc_classify(const struct orc_classify_args *a);
 

@@ -40,7 +40,7 @@ class ClassifyArgs(Structure):
                 ("rss_key", c_void_p), ("reta", c_void_p), ("reta_size", c_uint32), ("n_bins", c_uint32),
                 ("nh", c_void_p), ("hash", c_void_p), ("queue", c_void_p), ("edge", c_void_p),
                 ("bins", c_void_p), ("ptype", c_void_p), ("rxmeta", c_void_p), ("spec_burst", c_uint32),
-                ("spec_state", c_void_p)]
+                ("spec_state", c_void_p), ("no_hash", c_uint32)]
 
 
 _lib = None
@@ -197,7 +197,7 @@ def get_ptype(pkt: bytes):
 
 
 def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, tables4=None,
-              tables6=None, key=None, reta=None, n_bins=64, spec_burst=0, spec_state=None):
+              tables6=None, key=None, reta=None, n_bins=64, spec_burst=0, spec_state=None, no_hash=False):
     from cndp_amd.native import MS_RSS_KEY
     key = np.frombuffer(key or MS_RSS_KEY, dtype=np.uint8).copy()
     reta = np.ascontiguousarray(reta if reta is not None else (np.arange(128) % 16), dtype=np.uint16)
@@ -218,6 +218,7 @@ def make_args(mode, slab, n, stride=64, offsets=None, data_off=0, buf_len=1984, 
                                             _p(out["edge"]), _p(out["bins"]))
     a.ptype, a.rxmeta = _p(out["ptype"]), _p(out["rxmeta"])
     a.spec_burst = spec_burst
+    a.no_hash = 1 if no_hash else 0
     if spec_state is not None:   # np.uint16 array of 1, updated in place
         a.spec_state = _p(spec_state)
     keep = (slab, off, key, reta, tables4, tables6, spec_state)  # keep buffers alive with the struct

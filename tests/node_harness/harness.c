@@ -378,6 +378,15 @@ static double now_s(void)
     return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
+/* time spent in the drives' source turns and process() calls (seconds) */
+static double prof_src, prof_proc;
+void harness_prof(double *src, double *proc)
+{
+    *src = prof_src;
+    *proc = prof_proc;
+    prof_src = prof_proc = 0.0;
+}
+
 double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, int passes)
 {
     const int i = find(name);
@@ -388,10 +397,14 @@ double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, 
         for (int k = 0; k < 3; k++)
             n_out[k] = 0;
         for (uint32_t b = 0; b < n; b += burst) {
+            const double a0 = now_s();
             harness_walk_sources();
+            const double a1 = now_s();
             const uint16_t c = (uint16_t)(n - b < burst ? n - b : burst);
             regs[i]->process(&g, &nodes[i], objs + b, c);
             run_pending();
+            prof_src += a1 - a0;
+            prof_proc += now_s() - a1;
         }
         for (long spin = 0; n_out[0] + n_out[1] + n_out[2] < n; spin++) {
             if (spin > 100000000L)
