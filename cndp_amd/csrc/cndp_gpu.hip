@@ -1406,14 +1406,14 @@ __device__ __forceinline__ void cs_issue(const KArgs &a, uint32_t tt, uint32_t n
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
     const uint64_t my_base = tt < n_tiles ? ct_base(a, tt * 64u + lane, off) : ~0ull;
-    uint64_t qb[4];
+    // each lane resolves its own frame's load address once; frames off the
+    // fast path load a dummy chunk of the (aligned, 36 KiB) Toeplitz table
+    // instead, so every load is unconditional
+    const uint64_t my_src = ct_fast(a, my_base) ? (uint64_t)(uintptr_t)(a.slab + my_base) : (uint64_t)(uintptr_t)a.ttab;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        qb[k] = __shfl(my_base, 16 * k + (int)fr_in_k);
-        // frames off the fast path load a dummy chunk of the (aligned,
-        // 36 KiB) Toeplitz table instead, so every load is unconditional
-        const uint8_t *src = ct_fast(a, qb[k]) ? a.slab + qb[k] + part * 16u : (const uint8_t *)a.ttab + part * 16u;
-        r[k] = ldg4<LNT>(src);
+        const uint64_t src = __shfl(my_src, 16 * k + (int)fr_in_k) + part * 16u;
+        r[k] = ldg4<LNT>((const uint8_t *)(uintptr_t)src);
     }
 }
 
@@ -1714,8 +1714,9 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
         if (tid < 256) {
             uint32_t *row = rows + tid * ROW_DW;
             row[WIN_DW] = 0;
-            for (uint32_t j = tid; j < n_wl; j += 256)
-                cnet_general(a, a.wl[j], row, s_t, s_reta, s_bins, s_sf, count);
+            for (uint32_t j = tid; j < n_wl; j += 256) // entries other blocks stored write-through
+                cnet_general(a, __hip_atomic_load(&a.wl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), row, s_t,
+                             s_reta, s_bins, s_sf, count);
         }
         __syncthreads();
         if (count)
@@ -1854,6 +1855,15 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 #define SPEC_RCNT 640
 #define SPEC_HINT 900 // the hint words last written to host memory
 #define SPEC_TAIL 16
+// a type another block of the running kernel stored (write-through, agent
+// scope): read at agent scope too, never from a line an XCD's L2 may hold
+// from before (spec_classes runs in the last block of the kernel whose other
+// blocks wrote the batch's last types)
+__device__ __forceinline__ uint32_t spec_ld(const uint16_t *pt, uint64_t i)
+{
+    return __hip_atomic_load(pt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void spec_step(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t &cur)
 {
     const uint32_t low = cur & 0xffu;
@@ -1956,8 +1966,8 @@ __device__ __forceinline__ void spec_classes(uint32_t t, uint32_t *flags, uint8_
             const uint32_t ng = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B) >> 2;
             int best = -1;
             for (uint32_t j = t; j < ng; j += 64) {
-                const uint32_t l0 = pt[b0 + 4 * j], l1 = pt[b0 + 4 * j + 1];
-                const uint32_t l2 = pt[b0 + 4 * j + 2], l3 = pt[b0 + 4 * j + 3];
+                const uint32_t l0 = spec_ld(pt, b0 + 4 * j), l1 = spec_ld(pt, b0 + 4 * j + 1);
+                const uint32_t l2 = spec_ld(pt, b0 + 4 * j + 2), l3 = spec_ld(pt, b0 + 4 * j + 3);
                 const uint32_t v = l0 & 0xffu;
                 const bool allq = (l1 & 0xffu) == v && (l2 & 0xffu) == v && (l3 & 0xffu) == v;
                 if (!allq && l2 == l3)
@@ -1973,13 +1983,14 @@ __device__ __forceinline__ void spec_classes(uint32_t t, uint32_t *flags, uint8_
         if (ub >= 0) {
             skip = 1;
             if (t == 0) { // walk from it to the batch end
-                uint32_t cur = pt[(uint64_t)ub * B + 4 * ug + 3];
+                uint32_t cur = spec_ld(pt, (uint64_t)ub * B + 4 * ug + 3);
                 uint32_t j = ug + 1;
                 for (uint64_t b = (uint64_t)ub; b < nb; b++, j = 0) {
                     const uint64_t b0 = b * B;
                     const uint32_t ng = (uint32_t)((uint64_t)n - b0 < B ? (uint64_t)n - b0 : B) >> 2;
                     for (; j < ng; j++)
-                        spec_step(pt[b0 + 4 * j], pt[b0 + 4 * j + 1], pt[b0 + 4 * j + 2], pt[b0 + 4 * j + 3], cur);
+                        spec_step(spec_ld(pt, b0 + 4 * j), spec_ld(pt, b0 + 4 * j + 1), spec_ld(pt, b0 + 4 * j + 2),
+                                  spec_ld(pt, b0 + 4 * j + 3), cur);
                 }
                 meta[-1] = cur;
             }
@@ -6281,6 +6292,7 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
         return;
     }
     const uint32_t *rec = (const uint32_t *)R;
+    const u32x2 *lens = (const u32x2 *)(sl->h + q->h_len); // data_off at submit (staging offset 0)
     const bool wh = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
     const bool md_on = !(q->conf.flags & CNDP_MQ_F_NO_METADATA);
     const uint16_t lport = q->conf.lport;
@@ -6306,9 +6318,14 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
             *(uint32_t *)(m + MB_HASH) = rec[4 * i + 3];
         const uint32_t node = w2 >> 24;
         if (md_on && (node == CNDP_MQ_NODE_IP4 || node == CNDP_MQ_NODE_IP6)) {
+            // the addresses from the staged copy of the frame (read in
+            // sequence, not the frame's own line again); the IP header sits
+            // where the adjusted data_off put it
             uint8_t *md = mq_md_host(q, m);
+            const uint8_t *st = sl->h + q->h_stage + ((const uint64_t *)(sl->h + q->h_off))[i];
             if (md)
-                mq_save_md_host(md, *(uint8_t **)(m + MB_BUF_ADDR) + doff, node == CNDP_MQ_NODE_IP6);
+                mq_save_md_host(md, st + (doff - (uint16_t)(lens[i].y >> 16)),
+                                node == CNDP_MQ_NODE_IP6);
         }
     }
 }
