@@ -51,6 +51,13 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
     return __builtin_amdgcn_alignbyte(hi, lo, s);
 }
 
+// lo16(x) + hi16(x) + acc in one v_dot2_u32_u16 (x . (1, 1) + acc)
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t hsum2(uint32_t x, uint32_t acc)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, x), (u16x2_t){1, 1}, acc, false);
+}
+
 // bounded global byte read (bytes past the slab end read as 0)
 __device__ __forceinline__ uint32_t gbyte(const uint8_t *p, uint64_t avail, uint64_t o)
 {
@@ -1572,12 +1579,13 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const bool do4 = f4 & ((pe == 3u) | (a.spec_nh != nullptr)); // ip4_input.c:121-140
         const bool do6 = !f4 & ((pe == 4u) | (a.spec_nh != nullptr)); // ip6_input.c:115-135
         const uint32_t dst = alignb(W[8], W[7], 2);
-        uint32_t sum = 0;
+        // the header's 10 16-bit words (bytes 14..33) are W[3]'s high half,
+        // both halves of W[4..7] and W[8]'s low half: four packed dot
+        // products with (1, 1) add the pairs (cne_ip.h:131-214)
+        uint32_t sum = (W[3] >> 16) + (W[8] & 0xffffu);
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const uint32_t x = alignb(W[4 + k], W[3 + k], 2);
-            sum += (x & 0xffffu) + (x >> 16);
-        }
+        for (int k = 4; k < 8; k++)
+            sum = hsum2(W[k], sum);
         sum = (sum >> 16) + (sum & 0xffffu);
         sum = (sum >> 16) + (sum & 0xffffu);
         const bool ok4 = (bswap16(W[4] & 0xffffu) < a.buf_len) & (((~sum) & 0xffffu) == 0u);
