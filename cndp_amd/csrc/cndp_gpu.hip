@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <errno.h>
 #include <pthread.h>
 #include <sched.h>
@@ -3349,35 +3350,62 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
 // ---------------------------------------------------------------------------
 // bulk lookups (cne_fib_lookup_bulk / cne_fib6_lookup_bulk semantics)
 // ---------------------------------------------------------------------------
+// Completion of a lookup whose next hops go to mapped host memory: every
+// block makes its stores visible to the host, the last one raises the flag
+// the calling thread spins on (no stream synchronize: its wake-up cost as
+// much as the lookups).  flag == nullptr: no completion.
+struct LkDone {
+    uint32_t *ticket, *flag;
+    uint32_t seq;
+};
+
+__device__ __forceinline__ void lk_complete(const LkDone &d)
+{
+    if (!d.flag)
+        return;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = atomicAdd(d.ticket, 1u);
+        if (t == gridDim.x - 1) {
+            *d.ticket = 0u; // ready for the next call (stream order)
+            __threadfence_system();
+            __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <typename E>
 __global__ __launch_bounds__(256) void k_lookup4(const E *__restrict__ t24, const E *__restrict__ t8,
                                                  const uint32_t *__restrict__ ips,
-                                                 uint64_t *__restrict__ nh, uint32_t n)
+                                                 uint64_t *__restrict__ nh, uint32_t n, LkDone d)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n)
-        return;
-    const uint32_t ip = ips[i];
-    uint64_t e = (uint64_t)t24[ip >> 8];
-    if (e & 1u)
-        e = (uint64_t)t8[(e >> 1) * 256u + (ip & 0xffu)];
-    nh[i] = e >> 1;
+    if (i < n) {
+        const uint32_t ip = ips[i];
+        uint64_t e = (uint64_t)t24[ip >> 8];
+        if (e & 1u)
+            e = (uint64_t)t8[(e >> 1) * 256u + (ip & 0xffu)];
+        nh[i] = e >> 1;
+    }
+    lk_complete(d);
 }
 
 template <typename E>
 __global__ __launch_bounds__(256) void k_lookup6(const E *__restrict__ t24, const E *__restrict__ t8,
                                                  const uint8_t *__restrict__ ips,
-                                                 uint64_t *__restrict__ nh, uint32_t n)
+                                                 uint64_t *__restrict__ nh, uint32_t n, LkDone d)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n)
-        return;
-    const uint8_t *ip = ips + (uint64_t)i * 16u;
-    uint64_t e = (uint64_t)t24[((uint32_t)ip[0] << 16) | ((uint32_t)ip[1] << 8) | ip[2]];
-    uint32_t j = 3;
-    while ((e & 1u) && j < 16)
-        e = (uint64_t)t8[(e >> 1) * 256u + ip[j++]];
-    nh[i] = e >> 1;
+    if (i < n) {
+        const uint8_t *ip = ips + (uint64_t)i * 16u;
+        uint64_t e = (uint64_t)t24[((uint32_t)ip[0] << 16) | ((uint32_t)ip[1] << 8) | ip[2]];
+        uint32_t j = 3;
+        while ((e & 1u) && j < 16)
+            e = (uint64_t)t8[(e >> 1) * 256u + ip[j++]];
+        nh[i] = e >> 1;
+    }
+    lk_complete(d);
 }
 
 // ---------------------------------------------------------------------------
@@ -3812,7 +3840,20 @@ extern "C" int cndp_gpu_set_fib(cndp_gpu_ctx_t *c, struct cne_fib *f4, struct cn
 // ---- table mirror -----------------------------------------------------------
 extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
 {
-    if (!t || t->dev_id < 0)
+    if (!t)
+        return;
+    // lookup staging exists once a lookup ran (even one whose mirror sync failed)
+    for (uint32_t k = 0; k < CNDP_LK_SLOTS; k++) {
+        struct cndp_tbl::cndp_lk_slot &sl = t->lk[k];
+        if (sl.stream)
+            hipStreamDestroy((hipStream_t)sl.stream);
+        if (sl.host)
+            hipHostFree(sl.host);
+        if (sl.ticket)
+            hipFree(sl.ticket);
+        memset(&sl, 0, sizeof(sl));
+    }
+    if (t->dev_id < 0)
         return;
     int cur = 0;
     hipGetDevice(&cur);
@@ -3827,13 +3868,13 @@ extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
         hipFree(t->dev_pages);
     if (t->lk_stream)
         hipStreamDestroy((hipStream_t)t->lk_stream);
-    if (t->lk_host)
-        hipHostFree(t->lk_host);
     if (t->lk_dbuf)
         hipFree(t->lk_dbuf);
     t->lk_stream = nullptr;
-    t->lk_host = t->lk_hdev = t->lk_dbuf = nullptr;
-    t->lk_cap = 0;
+    t->lk_dbuf = nullptr;
+    for (uint32_t k = 0; k < t->n_old; k++)
+        hipFree(t->dev_old[k]);
+    t->n_old = 0;
     hipSetDevice(cur);
     t->dev_dir16 = t->dev_pages = nullptr;
     t->dev_cap_pages = 0;
@@ -3922,6 +3963,23 @@ static int dir16_update(struct cndp_tbl *t, uint32_t k0, uint32_t k1)
     return 0;
 }
 
+// a device buffer being replaced: lookups that took its address under
+// dev_lock may launch after we return, so it is kept until the mirror is
+// freed (the oldest goes once CNDP_DEV_OLD are held: hipFree synchronizes
+// the device, and no caller holds an address across that many replacements)
+static int tbl_dev_retire(struct cndp_tbl *t, void *p)
+{
+    if (!p)
+        return 0;
+    if (t->n_old == CNDP_DEV_OLD) {
+        HIP_TRY(hipFree(t->dev_old[0]));
+        memmove(t->dev_old, t->dev_old + 1, (CNDP_DEV_OLD - 1) * sizeof(void *));
+        t->n_old--;
+    }
+    t->dev_old[t->n_old++] = p;
+    return 0;
+}
+
 static int dir16_sync(struct cndp_tbl *t, hipStream_t s, uint64_t d24_lo, uint64_t d24_hi)
 {
     if (d24_hi > d24_lo || !t->dir16) {
@@ -3935,8 +3993,9 @@ static int dir16_sync(struct cndp_tbl *t, hipStream_t s, uint64_t d24_lo, uint64
         t->dd_hi = 65536;
     }
     if (!t->dev_pages || t->dev_cap_pages < t->cap_pages) {
-        if (t->dev_pages)
-            HIP_TRY(hipFree(t->dev_pages));
+        int r = tbl_dev_retire(t, t->dev_pages);
+        if (r)
+            return r;
         t->dev_pages = nullptr;
         const uint32_t cap = t->cap_pages > 64 ? t->cap_pages : 64;
         HIP_TRY(hipMalloc(&t->dev_pages, (size_t)cap * 256 * 4));
@@ -3980,7 +4039,11 @@ static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
     } else if (t->dev_groups != groups) { // pool grew (DUMMY FIBs)
         void *n8 = nullptr;
         HIP_TRY(hipMalloc(&n8, (size_t)groups * CNDP_TBL8_GRP * esz));
-        HIP_TRY(hipFree(t->dev_tbl8));
+        int r = tbl_dev_retire(t, t->dev_tbl8);
+        if (r) {
+            hipFree(n8);
+            return r;
+        }
         t->dev_tbl8 = n8;
         t->dev_groups = groups;
         t->d8_lo = 0;
@@ -4026,71 +4089,88 @@ static inline uint32_t blocks_for(uint64_t n, uint32_t threads)
     return (uint32_t)((n + threads - 1) / threads);
 }
 
-static int tbl_lookup4_launch(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s);
-static int tbl_lookup6_launch(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n, hipStream_t s);
+// the device tables one lookup launch reads (taken under dev_lock; the
+// buffers stay valid after it: replaced ones are kept until the mirror is
+// freed, tbl_dev_retire)
+struct TblView {
+    const void *t24, *t8;
+    uint32_t nh_sz;
+};
+static inline TblView tbl_view(const struct cndp_tbl *t)
+{
+    return TblView{t->dev_tbl24, t->dev_tbl8, t->nh_sz};
+}
+static int tbl_lookup4_launch(TblView v, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s,
+                              LkDone d = LkDone{nullptr, nullptr, 0});
+static int tbl_lookup6_launch(TblView v, const uint8_t *ips, uint64_t *nh, uint32_t n, hipStream_t s,
+                              LkDone d = LkDone{nullptr, nullptr, 0});
 
 extern "C" int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh,
                                     uint32_t n, void *stream)
 {
-    int r = cndp_tbl_dev_sync(t, stream);
-    if (r)
-        return r;
-    return tbl_lookup4_launch(t, ips, nh, n, (hipStream_t)stream);
+    pthread_mutex_lock(&t->dev_lock);
+    const int r = tbl_dev_sync_locked(t, stream);
+    const TblView v = tbl_view(t);
+    pthread_mutex_unlock(&t->dev_lock);
+    return r ? r : tbl_lookup4_launch(v, ips, nh, n, (hipStream_t)stream);
 }
 
 extern "C" int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n,
                                     void *stream)
 {
-    int r = cndp_tbl_dev_sync(t, stream);
-    if (r)
-        return r;
-    return tbl_lookup6_launch(t, ips, nh, n, (hipStream_t)stream);
+    pthread_mutex_lock(&t->dev_lock);
+    const int r = tbl_dev_sync_locked(t, stream);
+    const TblView v = tbl_view(t);
+    pthread_mutex_unlock(&t->dev_lock);
+    return r ? r : tbl_lookup6_launch(v, ips, nh, n, (hipStream_t)stream);
 }
 
-static int tbl_lookup4_launch(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s)
+static int tbl_lookup4_launch(TblView v, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s,
+                              LkDone d)
 {
     if (n == 0)
         return 0;
     const uint32_t g = blocks_for(n, 256);
-    switch (t->nh_sz) {
+    switch (v.nh_sz) {
     case 0:
-        hipLaunchKernelGGL(k_lookup4<uint8_t>, dim3(g), dim3(256), 0, s, (const uint8_t *)t->dev_tbl24,
-                           (const uint8_t *)t->dev_tbl8, ips, nh, n);
+        hipLaunchKernelGGL(k_lookup4<uint8_t>, dim3(g), dim3(256), 0, s, (const uint8_t *)v.t24,
+                           (const uint8_t *)v.t8, ips, nh, n, d);
         break;
     case 1:
         hipLaunchKernelGGL(k_lookup4<uint16_t>, dim3(g), dim3(256), 0, s,
-                           (const uint16_t *)t->dev_tbl24, (const uint16_t *)t->dev_tbl8, ips, nh, n);
+                           (const uint16_t *)v.t24, (const uint16_t *)v.t8, ips, nh, n, d);
         break;
     case 2:
         hipLaunchKernelGGL(k_lookup4<uint32_t>, dim3(g), dim3(256), 0, s,
-                           (const uint32_t *)t->dev_tbl24, (const uint32_t *)t->dev_tbl8, ips, nh, n);
+                           (const uint32_t *)v.t24, (const uint32_t *)v.t8, ips, nh, n, d);
         break;
     default:
         hipLaunchKernelGGL(k_lookup4<uint64_t>, dim3(g), dim3(256), 0, s,
-                           (const uint64_t *)t->dev_tbl24, (const uint64_t *)t->dev_tbl8, ips, nh, n);
+                           (const uint64_t *)v.t24, (const uint64_t *)v.t8, ips, nh, n, d);
         break;
     }
     HIP_TRY(hipGetLastError());
     return 0;
 }
 
-static int tbl_lookup6_launch(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n, hipStream_t s)
+static int tbl_lookup6_launch(TblView v, const uint8_t *ips, uint64_t *nh, uint32_t n, hipStream_t s,
+                              LkDone d)
 {
     if (n == 0)
         return 0;
     const uint32_t g = blocks_for(n, 256);
-    switch (t->nh_sz) {
+    switch (v.nh_sz) {
     case 1:
         hipLaunchKernelGGL(k_lookup6<uint16_t>, dim3(g), dim3(256), 0, s,
-                           (const uint16_t *)t->dev_tbl24, (const uint16_t *)t->dev_tbl8, ips, nh, n);
+                           (const uint16_t *)v.t24, (const uint16_t *)v.t8, ips, nh, n, d);
         break;
     case 2:
         hipLaunchKernelGGL(k_lookup6<uint32_t>, dim3(g), dim3(256), 0, s,
-                           (const uint32_t *)t->dev_tbl24, (const uint32_t *)t->dev_tbl8, ips, nh, n);
+                           (const uint32_t *)v.t24, (const uint32_t *)v.t8, ips, nh, n, d);
         break;
     default:
         hipLaunchKernelGGL(k_lookup6<uint64_t>, dim3(g), dim3(256), 0, s,
-                           (const uint64_t *)t->dev_tbl24, (const uint64_t *)t->dev_tbl8, ips, nh, n);
+                           (const uint64_t *)v.t24, (const uint64_t *)v.t8, ips, nh, n, d);
         break;
     }
     HIP_TRY(hipGetLastError());
@@ -4101,18 +4181,120 @@ static int tbl_lookup6_launch(struct cndp_tbl *t, const uint8_t *ips, uint64_t *
 // reference lookup reads the table in place and cannot fail
 // (cne_fib.c:111-116); callers like examples/cndpfwd/l3-fwd.c:85 call it per
 // burst from every forwarding thread on one FIB and ignore the return code.
-// So: one lock per table (device mirror + staging), the mirror's own device
-// (not the caller's current one), staging allocated once per table, and on
-// any failure every next hop is set to the FIB default before the negative
-// errno is returned.  Small calls (the per-burst case) stage keys and next
-// hops in pinned, mapped host memory that the kernel reads and writes in
-// place: one launch and one stream wait, no DMA set-up.  Larger calls move
-// the keys and next hops by DMA through device scratch.
+// So: the mirror's own device (not the caller's current one), and on any
+// failure every next hop is set to the FIB default before the negative
+// errno is returned.  A small call (the per-burst case) takes one of the
+// table's staging slots for itself -- its own stream, pinned and mapped
+// staging that the kernel reads and writes in place, and a completion flag
+// the kernel raises there, which the caller spins on (no stream
+// synchronize: its wake-up cost as much as the lookups) -- and holds the
+// table lock only to sync the mirror and take the table addresses, so calls
+// from different threads overlap.  Larger calls move keys and next hops by
+// DMA through device scratch, under the table lock.
 #define LK_MAPPED_MAX 16384u   // lookups per round through mapped staging
 #define LK_DMA_CHUNK (1u << 20) // lookups per round through device scratch
+#define LK_FLAG_OFF ((size_t)LK_MAPPED_MAX * (16 + 8)) // the completion flag, after the staging
+#define LK_WAIT_S 10             // a mapped lookup not done by then is an error
 
-static int lookup_host_locked(struct cndp_tbl *t, const uint8_t *ips, uint32_t key_sz, uint64_t *nh,
-                              uint32_t n, int v6)
+static uint64_t now_ns();
+
+// spin on the mapped lookup's completion flag; on a timeout, the stream's
+// own status says why
+static int lk_wait(const uint32_t *flag, uint32_t seq, hipStream_t s)
+{
+    const uint64_t t0 = now_ns();
+    for (uint32_t spin = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; spin++) {
+        if ((spin & 255u) == 255u && now_ns() - t0 > LK_WAIT_S * 1000000000ull) {
+            HIP_TRY(hipStreamSynchronize(s));
+            return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? 0 : -EIO;
+        }
+        __builtin_ia32_pause();
+    }
+    return 0;
+}
+
+// a free staging slot, the calling thread's usual one first
+static struct cndp_tbl::cndp_lk_slot *lk_slot_take(struct cndp_tbl *t)
+{
+    static std::atomic<uint32_t> next_home{0};
+    static thread_local uint32_t home = next_home.fetch_add(1u) % CNDP_LK_SLOTS;
+    for (uint32_t spin = 0;; spin++) {
+        for (uint32_t k = 0; k < CNDP_LK_SLOTS; k++) {
+            struct cndp_tbl::cndp_lk_slot *sl = &t->lk[(home + k) % CNDP_LK_SLOTS];
+            if (!__atomic_load_n(&sl->busy, __ATOMIC_RELAXED) && !__atomic_exchange_n(&sl->busy, 1, __ATOMIC_ACQUIRE))
+                return sl;
+        }
+        if ((spin & 63u) == 63u)
+            sched_yield();
+        else
+            __builtin_ia32_pause();
+    }
+}
+
+static void lk_slot_give(struct cndp_tbl::cndp_lk_slot *sl)
+{
+    __atomic_store_n(&sl->busy, 0, __ATOMIC_RELEASE);
+}
+
+// the slot's stream, staging and ticket on the current device (first use)
+static int lk_slot_init(struct cndp_tbl::cndp_lk_slot *sl)
+{
+    if (!sl->stream) {
+        hipStream_t st = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        sl->stream = st;
+    }
+    if (!sl->host) {
+        void *h = nullptr, *d = nullptr;
+        HIP_TRY(hipHostMalloc(&h, LK_FLAG_OFF + 64, hipHostMallocMapped));
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            hipHostFree(h);
+            return -EIO;
+        }
+        *(volatile uint32_t *)((uint8_t *)h + LK_FLAG_OFF) = 0u;
+        sl->host = (uint8_t *)h;
+        sl->hdev = (uint8_t *)d;
+        sl->seq = 0;
+    }
+    if (!sl->ticket) {
+        HIP_TRY(hipMalloc((void **)&sl->ticket, sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(sl->ticket, 0, sizeof(uint32_t), (hipStream_t)sl->stream));
+    }
+    return 0;
+}
+
+static int lookup_mapped(struct cndp_tbl *t, const uint8_t *ips, uint32_t key_sz, uint64_t *nh, uint32_t n, int v6)
+{
+    struct cndp_tbl::cndp_lk_slot *sl = lk_slot_take(t);
+    int r = lk_slot_init(sl);
+    hipStream_t s = (hipStream_t)sl->stream;
+    TblView v{};
+    if (!r) {
+        pthread_mutex_lock(&t->dev_lock);
+        r = tbl_dev_sync_locked(t, s); // waits for its copies when the image was dirty
+        v = tbl_view(t);
+        pthread_mutex_unlock(&t->dev_lock);
+    }
+    if (!r) {
+        uint8_t *hk = sl->host, *hn = sl->host + (size_t)LK_MAPPED_MAX * key_sz;
+        memcpy(hk, ips, (size_t)n * key_sz);
+        const uint8_t *dk = sl->hdev;
+        uint64_t *dn = (uint64_t *)(sl->hdev + (size_t)LK_MAPPED_MAX * key_sz);
+        sl->seq = sl->seq + 1u ? sl->seq + 1u : 1u; // never the flag's initial 0
+        const LkDone d{sl->ticket, (uint32_t *)(sl->hdev + LK_FLAG_OFF), sl->seq};
+        r = v6 ? tbl_lookup6_launch(v, dk, dn, n, s, d) : tbl_lookup4_launch(v, (const uint32_t *)dk, dn, n, s, d);
+        if (!r)
+            r = lk_wait((const uint32_t *)(sl->host + LK_FLAG_OFF), sl->seq, s);
+        if (!r)
+            memcpy(nh, hn, (size_t)n * 8);
+    }
+    lk_slot_give(sl);
+    return r;
+}
+
+// caller holds t->dev_lock
+static int lookup_dma_locked(struct cndp_tbl *t, const uint8_t *ips, uint32_t key_sz, uint64_t *nh, uint32_t n,
+                             int v6)
 {
     if (!t->lk_stream) {
         hipStream_t st = nullptr;
@@ -4120,32 +4302,10 @@ static int lookup_host_locked(struct cndp_tbl *t, const uint8_t *ips, uint32_t k
         t->lk_stream = st;
     }
     hipStream_t s = (hipStream_t)t->lk_stream;
-    if (!t->lk_host) {
-        void *h = nullptr, *d = nullptr;
-        HIP_TRY(hipHostMalloc(&h, (size_t)LK_MAPPED_MAX * (16 + 8), hipHostMallocMapped));
-        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-            hipHostFree(h);
-            return -EIO;
-        }
-        t->lk_host = (uint8_t *)h;
-        t->lk_hdev = (uint8_t *)d;
-        t->lk_cap = LK_MAPPED_MAX;
-    }
     int r = tbl_dev_sync_locked(t, s);
     if (r)
         return r;
-    if (n <= LK_MAPPED_MAX) {
-        uint8_t *hk = t->lk_host, *hn = t->lk_host + (size_t)LK_MAPPED_MAX * key_sz;
-        memcpy(hk, ips, (size_t)n * key_sz);
-        const uint8_t *dk = t->lk_hdev;
-        uint64_t *dn = (uint64_t *)(t->lk_hdev + (size_t)LK_MAPPED_MAX * key_sz);
-        r = v6 ? tbl_lookup6_launch(t, dk, dn, n, s) : tbl_lookup4_launch(t, (const uint32_t *)dk, dn, n, s);
-        if (r)
-            return r;
-        HIP_TRY(hipStreamSynchronize(s));
-        memcpy(nh, hn, (size_t)n * 8);
-        return 0;
-    }
+    const TblView v = tbl_view(t);
     if (!t->lk_dbuf)
         HIP_TRY(hipMalloc((void **)&t->lk_dbuf, (size_t)LK_DMA_CHUNK * (16 + 8)));
     for (uint32_t i0 = 0; i0 < n; i0 += LK_DMA_CHUNK) {
@@ -4153,7 +4313,7 @@ static int lookup_host_locked(struct cndp_tbl *t, const uint8_t *ips, uint32_t k
         uint8_t *dk = t->lk_dbuf;
         uint64_t *dn = (uint64_t *)(t->lk_dbuf + (size_t)LK_DMA_CHUNK * key_sz);
         HIP_TRY(hipMemcpyAsync(dk, ips + (size_t)i0 * key_sz, (size_t)c * key_sz, hipMemcpyHostToDevice, s));
-        r = v6 ? tbl_lookup6_launch(t, dk, dn, c, s) : tbl_lookup4_launch(t, (const uint32_t *)dk, dn, c, s);
+        r = v6 ? tbl_lookup6_launch(v, dk, dn, c, s) : tbl_lookup4_launch(v, (const uint32_t *)dk, dn, c, s);
         if (r)
             return r;
         HIP_TRY(hipMemcpyAsync(nh + i0, dn, (size_t)c * 8, hipMemcpyDeviceToHost, s));
@@ -4168,15 +4328,17 @@ static int lookup_host_common(struct cndp_tbl *t, const void *ips, size_t key_sz
     int r = 0, ndev = 0, cur = -1;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         r = -ENODEV;
-    } else {
+    } else if (n) {
         hipGetDevice(&cur);
         pthread_mutex_lock(&t->dev_lock);
         const int dev = t->dev_id >= 0 ? t->dev_id : (cur >= 0 ? cur : 0);
         if (dev != cur && hipSetDevice(dev) != hipSuccess)
             r = -ENODEV;
-        if (!r)
-            r = lookup_host_locked(t, (const uint8_t *)ips, (uint32_t)key_sz, nh, n, v6);
+        if (!r && n > LK_MAPPED_MAX)
+            r = lookup_dma_locked(t, (const uint8_t *)ips, (uint32_t)key_sz, nh, n, v6);
         pthread_mutex_unlock(&t->dev_lock);
+        if (!r && n <= LK_MAPPED_MAX)
+            r = lookup_mapped(t, (const uint8_t *)ips, (uint32_t)key_sz, nh, n, v6);
         if (cur >= 0 && dev != cur)
             hipSetDevice(cur);
     }

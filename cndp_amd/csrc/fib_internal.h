@@ -25,6 +25,8 @@ extern "C" {
 
 #define CNDP_TBL24_ENT (1u << 24)
 #define CNDP_TBL8_GRP 256u
+#define CNDP_LK_SLOTS 16u   /* concurrent host-array lookups per table */
+#define CNDP_DEV_OLD 8u
 
 struct cndp_tbl {
     uint32_t nh_sz;     /* log2(entry bytes) */
@@ -58,15 +60,26 @@ struct cndp_tbl {
     void *dev_pages;
     uint32_t dev_cap_pages;
     /* host-array lookups (cne_fib_lookup_bulk): callers are many forwarding
-     * threads on one FIB (examples/cndpfwd/l3-fwd.c:85), so the device mirror
-     * state and the staging below are guarded by dev_lock */
+     * threads on one FIB (examples/cndpfwd/l3-fwd.c:85).  dev_lock guards the
+     * host image, its dirty ranges and the device mirror; each small call
+     * takes one of the staging slots below for itself, so calls from
+     * different threads run concurrently (own stream, staging and flag) */
     uint64_t def_nh;        /* written to every next hop of a lookup that cannot run */
     pthread_mutex_t dev_lock;
-    void *lk_stream;        /* hipStream_t (non-blocking) of host-array lookups */
-    uint8_t *lk_host;       /* pinned + mapped staging: keys, then 8-B next hops */
-    uint8_t *lk_hdev;       /* device address of lk_host */
-    uint8_t *lk_dbuf;       /* device scratch for large lookups (DMA path) */
-    uint64_t lk_cap;        /* lookups one staging round holds */
+    struct cndp_lk_slot {
+        int busy;           /* taken by one call (atomic exchange) */
+        void *stream;       /* hipStream_t (non-blocking) */
+        uint8_t *host;      /* pinned + mapped staging: keys, next hops, completion flag */
+        uint8_t *hdev;      /* device address of host */
+        uint32_t *ticket;   /* device arrival counter of the call's blocks */
+        uint32_t seq;       /* the value the flag takes next */
+    } lk[CNDP_LK_SLOTS];
+    void *lk_stream;        /* hipStream_t of large lookups (DMA path, under dev_lock) */
+    uint8_t *lk_dbuf;       /* device scratch for large lookups */
+    /* device buffers replaced while lookups on other threads may still hold
+     * their address (freed with the mirror) */
+    void *dev_old[CNDP_DEV_OLD];
+    uint32_t n_old;
 };
 
 struct cne_fib {

@@ -50,6 +50,34 @@ def main():
             res[f"{tag}_n{n}"] = {"median_us": round(float(np.median(t)) / 1e3, 2),
                                  "p99_us": round(float(np.percentile(t, 99)) / 1e3, 2),
                                  "Mlookups_per_s": round(n / (float(np.median(t)) / 1e3), 2)}
+    # per-burst callers on several threads (one FIB, 256-key calls): the
+    # aggregate rate, as cndpfwd's forwarding threads would see it
+    import threading
+    for T in (1, 2, 4, 8, 16):
+        stop = threading.Event()
+        counts = [0] * T
+
+        def worker(w):
+            ips = rng.integers(0, 2**32, size=256, dtype=np.uint64).astype(np.uint32)
+            out = np.zeros(256, np.uint64)
+            a = (f.h, ips.ctypes.data, out.ctypes.data, 256)
+            c = 0
+            while not stop.is_set():
+                L.cne_fib_lookup_bulk(*a)
+                c += 1
+            counts[w] = c
+
+        th = [threading.Thread(target=worker, args=(w,)) for w in range(T)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        time.sleep(1.0)
+        stop.set()
+        for t in th:
+            t.join()
+        dt = time.perf_counter() - t0
+        res[f"v4_n256_threads{T}"] = {"calls_per_s": round(sum(counts) / dt),
+                                      "Mlookups_per_s": round(sum(counts) * 256 / dt / 1e6, 2)}
     print(json.dumps(res, indent=1))
     if args.json:
         with open(args.json, "w") as fo:
