@@ -199,8 +199,10 @@ def test_fib_add_while_lookup(gpu):
 
     def reader():
         try:
-            while not stop.is_set():
-                f.lookup_bulk(keys[:4096])
+            k = 0
+            while not stop.is_set():  # per-burst and larger calls
+                f.lookup_bulk(keys[:4096] if k % 2 else keys[:256])
+                k += 1
         except Exception as ex:  # noqa: BLE001
             errors.append(repr(ex))
 
@@ -224,6 +226,16 @@ def test_fib_add_while_lookup(gpu):
     assert not errors, errors
     want = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], 3, keys)
     assert np.array_equal(f.lookup_bulk(keys), want)
+    # per-burst calls on staging slots of their own see the same mirror
+    for o in range(0, 4096, 1024):
+        assert np.array_equal(f.lookup_bulk(keys[o:o + 1024]), want[o:o + 1024])
+    ip, d = 0x0B123400, 24
+    assert f.add(ip, d, 99) == 0
+    routes[(ip, d)] = 99
+    probe = np.array([ip | 7, ip | 200], np.uint32)
+    want_p = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], 3, probe)
+    assert 99 in list(want_p) or len(routes) > 1
+    assert np.array_equal(f.lookup_bulk(probe), want_p)
 
 
 @pytest.mark.gpu
