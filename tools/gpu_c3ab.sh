@@ -1,14 +1,18 @@
 #!/bin/bash
-# A/B of the register-transpose tiles (diagnostic): the parity suite on the
-# "dpp" build (tools/abbuild.sh dpp -DCNDP_STREAM_DPP=1 -DCNDP_CNET_DPP=1),
-# then C3 / C4 / C5 timings of the default build ("base") against it.
+# A/B (diagnostic): the parity suite on the "dpp" build (tools/abbuild.sh dpp
+# -DCNDP_STREAM_DPP=1 -DCNDP_CNET_DPP=1) and the cnet tests on the "inl" build
+# (-DCNDP_SPEC_INLINE=1), then C3 / C4 / C5 timings against the default build.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 CNDP_GPU_LIB=$PWD/cndp_amd/lib/libcndp_gpu_dpp.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py \
-    -m gpu -x -q --timeout 300 -p no:cacheprovider > gpurun_out/parity.log 2>&1 \
-    || { echo "parity rc=$?"; tail -30 gpurun_out/parity.log; exit 1; }
-tail -3 gpurun_out/parity.log
+    -m gpu -x -q --timeout 300 -p no:cacheprovider > gpurun_out/parity_dpp.log 2>&1 \
+    || { echo "parity dpp rc=$?"; tail -30 gpurun_out/parity_dpp.log; exit 1; }
+tail -1 gpurun_out/parity_dpp.log
+CNDP_GPU_LIB=$PWD/cndp_amd/lib/libcndp_gpu_inl.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py \
+    -m gpu -x -q --timeout 300 -p no:cacheprovider -k "cnet or spec" > gpurun_out/parity_inl.log 2>&1 \
+    || { echo "parity inl rc=$?"; tail -30 gpurun_out/parity_inl.log; exit 1; }
+tail -1 gpurun_out/parity_inl.log
 tools/abrun.sh "--config c3 --steps 50 --warmup 5" base dpp || exit 1
-tools/abrun.sh "--config c4 --steps 30 --warmup 3" base dpp || exit 1
+tools/abrun.sh "--config c4 --steps 30 --warmup 3" base dpp inl || exit 1
 tools/abrun.sh "--config c5 --steps 20 --warmup 3" base dpp
