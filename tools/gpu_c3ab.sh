@@ -14,5 +14,5 @@ CNDP_GPU_LIB=$PWD/cndp_amd/lib/libcndp_gpu_inl.so timeout -k 10 600 python3 -u -
     || { echo "parity inl rc=$?"; tail -30 gpurun_out/parity_inl.log; exit 1; }
 tail -1 gpurun_out/parity_inl.log
 tools/abrun.sh "--config c3 --steps 50 --warmup 5" base dpp || exit 1
-tools/abrun.sh "--config c4 --steps 30 --warmup 3" base dpp inl || exit 1
-tools/abrun.sh "--config c5 --steps 20 --warmup 3" base dpp
+tools/abrun.sh "--config c4 --steps 30 --warmup 3" base dpp inl dpp640 || exit 1
+tools/abrun.sh "--config c5 --steps 20 --warmup 3" base dpp dpp640
