@@ -1425,15 +1425,8 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 // Frames that are not 16-B aligned or have < 64 bytes before the slab end
 // are staged with bounded byte loads (zero past the end), like Win.
 // ---------------------------------------------------------------------------
-#ifndef CT_THREADS // overridable for A/B builds (tools/abbuild.sh)
 #define CT_THREADS 512
-#endif
 #define CT_WAVES (CT_THREADS / 64)
-#ifdef CT_WAVES_PER_EU // A/B: ask the compiler for this many waves per SIMD
-#define CT_OCC __attribute__((amdgpu_waves_per_eu(CT_WAVES_PER_EU, CT_WAVES_PER_EU)))
-#else
-#define CT_OCC
-#endif
 
 // frame base (bytes from slab) of packet i, or ~0 when i >= n
 __device__ __forceinline__ uint64_t ct_base(const KArgs &a, uint64_t i, uint64_t off_i)
@@ -1852,7 +1845,7 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
 // META: ptype / rxmeta outputs requested (without them the kernel keeps
 // 14 VGPRs and 18 spilled SGPRs fewer)
 template <bool LNT, bool META>
-__global__ __launch_bounds__(CT_THREADS) CT_OCC void k_cnet_defer(KArgs a, uint32_t n_tiles)
+__global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
     // the window tiles (without CNDP_CNET_DPP), and the rows cnet_defer_tail
