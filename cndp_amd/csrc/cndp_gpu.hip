@@ -3207,9 +3207,6 @@ __device__ __forceinline__ void spec_chunk_pre(const KArgs &a, uint32_t B, uint6
     }
 }
 
-#ifndef CNDP_SPEC_INLINE
-#define CNDP_SPEC_INLINE 0
-#endif
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
                                                       uint8_t *done, uint32_t *R)
@@ -3265,14 +3262,6 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     uint32_t tw, pq0, pq1;
     spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
     cnet_lut_fill(s_lut, threadIdx.x, 256);
-#if CNDP_SPEC_INLINE
-    // the chunks that need their types are replayed here, by the wave that
-    // found their entering state (no list, no work left for k_spec_fallback)
-    __shared__ __attribute__((aligned(16))) uint32_t s_st[4][CH * 256];
-    const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
-    for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
-        s_bins[k] = 0;
-#endif
     __syncthreads();
     if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL])
         return;
@@ -3300,10 +3289,6 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
         }
         const uint32_t cn = spec_canon(s0 & 0xffu);
         if (odd || (cn != 0xFFu && cn != cnet_edge_l(s_lut, s0))) {
-#if CNDP_SPEC_INLINE
-            spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr);
-            __builtin_amdgcn_wave_barrier();
-#else
             // its types decide: k_spec_fallback reads them (and replays) from
             // the list, so this kernel carries no replay code (occupancy)
             if (lane == 0) {
@@ -3311,17 +3296,10 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 R[x * 2 * nch + 2 * k] = (uint32_t)c;
                 R[x * 2 * nch + 2 * k + 1] = s0;
             }
-#endif
         }
         if (lane == 0)
             done[c] = 1;
     }
-#if CNDP_SPEC_INLINE
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
-        if (s_bins[k])
-            atomicAdd(&a.bins[k], (unsigned long long)(long long)s_bins[k]);
-#endif
 }
 
 // Grid barrier of k_spec_fallback: bar[0] counts arrivals (monotonic within a
