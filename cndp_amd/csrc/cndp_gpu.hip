@@ -653,51 +653,6 @@ struct StreamLane { // one lane's packet in flight between stages
     bool sel;     // raw replaces e (resolved by the consumer, not at issue)
 };
 
-// Frame tile transpose in registers (CNDP_STREAM_DPP 1).  Load k of a tile
-// gives lane 4j + p part p (16 B) of frame 16k + j: a 4 x 4 block per quad of
-// lanes (lane bits 1:0 = part, load k = frame set).  Two butterfly stages
-// swap lane bit 0 with k's bit 0, then lane bit 1 with k's bit 1 (quad_perm
-// DPP moves and a select each), after which lane 4j + q holds part x of
-// frame 16q + j in output x: every lane owns one frame, f(lane) =
-// 16 (lane & 3) + (lane >> 2), and no LDS tile is needed.  Only the outputs
-// a caller asks for are formed (the compiler drops the rest).
-#ifndef CNDP_STREAM_DPP
-#define CNDP_STREAM_DPP 0
-#endif
-template <int QP>
-__device__ __forceinline__ uint32_t qperm(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, QP, 0xf, 0xf, true);
-}
-#define QP(a, b, c, d) ((a) | ((b) << 2) | ((c) << 4) | ((d) << 6))
-
-// plane = dword d of the four loads (A[k] = r[k].d); returns the quad
-// transpose's outputs B[0..3] (B[x] = part x, dword d of the lane's frame)
-__device__ __forceinline__ void quad_xpose(uint32_t lane, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                           uint32_t &b0, uint32_t &b1, uint32_t &b2, uint32_t &b3)
-{
-    // the DPP moves run with every lane active (their sources are other
-    // lanes): computed unconditionally, then selected -- a move inside a
-    // branch arm would read lanes that arm has switched off
-    const bool odd = (lane & 1u) != 0u, hi = (lane & 2u) != 0u;
-    const uint32_t m1 = qperm<QP(0, 0, 2, 2)>(a1), m0 = qperm<QP(1, 1, 3, 3)>(a0);
-    const uint32_t m3 = qperm<QP(0, 0, 2, 2)>(a3), m2 = qperm<QP(1, 1, 3, 3)>(a2);
-    const uint32_t c0 = odd ? m1 : a0, c1 = odd ? a1 : m0;
-    const uint32_t c2 = odd ? m3 : a2, c3 = odd ? a3 : m2;
-    const uint32_t n2 = qperm<QP(0, 1, 0, 1)>(c2), n3 = qperm<QP(0, 1, 0, 1)>(c3);
-    const uint32_t n0 = qperm<QP(2, 3, 2, 3)>(c0), n1 = qperm<QP(2, 3, 2, 3)>(c1);
-    b0 = hi ? n2 : c0;
-    b1 = hi ? n3 : c1;
-    b2 = hi ? c2 : n0;
-    b3 = hi ? c3 : n1;
-}
-
-// the lane's frame within its tile
-__device__ __forceinline__ uint32_t xpose_frame(uint32_t lane)
-{
-    return CNDP_STREAM_DPP ? 16u * (lane & 3u) + (lane >> 2) : lane;
-}
-
 template <int MODE, bool NTS, bool LNT, int P>
 __device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, uint64_t t0, uint64_t wstep,
                                             uint64_t nt_w, uint64_t j, uint32_t lane, u32x4 *tile,
@@ -735,44 +690,27 @@ __device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, ui
         nc.raw = t2[nc.sel ? i2 : 0u];
     }
     // A: tile c -- stage, parse, hash, gather 1
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t f = 16u * k + fr_in_k;
+        tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t sw = (lane >> 2) & 3u;
+    const u32x4 p0 = tile[lane * 4u + (0u ^ sw)];
+    const u32x4 p1 = tile[lane * 4u + (1u ^ sw)];
+    const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+    __builtin_amdgcn_wave_barrier();
     FastHdr h;
-    const uint32_t fl = xpose_frame(lane);
-    const uint64_t i = (c < n_tiles ? c : n_tiles - 1u) * 64u + fl;
+    const uint64_t i = (c < n_tiles ? c : n_tiles - 1u) * 64u + lane;
     h.p = base + i * 64u;
     h.avail = a.slab_len - (a.data_off + i * 64u);
-    if (CNDP_STREAM_DPP) {
-        // frame bytes 12..15 (part 0 dword 3), 20..31 (part 1 dwords 1..3),
-        // 32..39 (part 2 dwords 0..1): planes 3, 1, 2, 0
-        uint32_t x0, x1, x2, x3;
-        quad_xpose(lane, r[P][0].w, r[P][1].w, r[P][2].w, r[P][3].w, x0, x1, x2, x3);
-        h.w3 = x0;
-        h.w7 = x1;
-        quad_xpose(lane, r[P][0].y, r[P][1].y, r[P][2].y, r[P][3].y, x0, x1, x2, x3);
-        h.w5 = x1;
-        h.w9 = x2;
-        quad_xpose(lane, r[P][0].z, r[P][1].z, r[P][2].z, r[P][3].z, x0, x1, x2, x3);
-        h.w6 = x1;
-        quad_xpose(lane, r[P][0].x, r[P][1].x, r[P][2].x, r[P][3].x, x0, x1, x2, x3);
-        h.w8 = x2;
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t f = 16u * k + fr_in_k;
-            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t sw = (lane >> 2) & 3u;
-        const u32x4 p0 = tile[lane * 4u + (0u ^ sw)];
-        const u32x4 p1 = tile[lane * 4u + (1u ^ sw)];
-        const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
-        __builtin_amdgcn_wave_barrier();
-        h.w3 = p0.w;
-        h.w5 = p1.y;
-        h.w6 = p1.z;
-        h.w7 = p1.w;
-        h.w8 = p2.x;
-        h.w9 = p2.y;
-    }
+    h.w3 = p0.w;
+    h.w5 = p1.y;
+    h.w6 = p1.z;
+    h.w7 = p1.w;
+    h.w8 = p2.x;
+    h.w9 = p2.y;
     const uint32_t et = bswap16(h.w3 & 0xffffu);
     const uint32_t dst = alignb(h.w8, h.w7, 2);
     nb.et = et;
@@ -809,7 +747,7 @@ __device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, ui
     }
     // D: the stores of tile c-3
     if (dD)
-        fast_emit<MODE, NTS>(a, (c - 3u * wstep) * 64u + fl, etD, nhD, hsD, s_reta, s_bins, count);
+        fast_emit<MODE, NTS>(a, (c - 3u * wstep) * 64u + lane, etD, nhD, hsD, s_reta, s_bins, count);
     sd = nd;
     sc = nc;
     sb = nb;
@@ -1436,17 +1374,6 @@ __device__ __forceinline__ uint64_t ct_base(const KArgs &a, uint64_t i, uint64_t
     return (a.offsets ? off_i : i * a.stride) + a.data_off;
 }
 
-// The deferred cnet kernel's frame of a lane within its tile: with
-// CNDP_CNET_DPP the window tile is transposed in registers (quad_xpose),
-// as in the l3fwd stream kernel, and lane l owns frame 16 (l & 3) + (l >> 2)
-#ifndef CNDP_CNET_DPP
-#define CNDP_CNET_DPP 0
-#endif
-__device__ __forceinline__ uint32_t cnet_frame(uint32_t lane)
-{
-    return CNDP_CNET_DPP ? 16u * (lane & 3u) + (lane >> 2) : lane;
-}
-
 __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
 {
     // base + 64 <= slab_len (base = ~0 fails it) and 16-B aligned; bitwise
@@ -1486,25 +1413,11 @@ __device__ __forceinline__ void cs_issue(const KArgs &a, uint32_t tt, uint32_t n
                                          uint32_t lane, u32x4 (&r)[4])
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const uint64_t my_base = tt < n_tiles ? ct_base(a, tt * 64u + cnet_frame(lane), off) : ~0ull;
+    const uint64_t my_base = tt < n_tiles ? ct_base(a, tt * 64u + lane, off) : ~0ull;
     // each lane resolves its own frame's load address once; frames off the
     // fast path load a dummy chunk of the (aligned, 36 KiB) Toeplitz table
     // instead, so every load is unconditional
     const uint64_t my_src = ct_fast(a, my_base) ? (uint64_t)(uintptr_t)(a.slab + my_base) : (uint64_t)(uintptr_t)a.ttab;
-    if (CNDP_CNET_DPP) {
-        // load k of lane 4j + p is part p of frame 16k + j, which lane 4j + k
-        // owns: a broadcast within the quad (DPP), not a cross-wave shuffle
-        const uint32_t lo = (uint32_t)my_src, hi = (uint32_t)(my_src >> 32);
-        const uint32_t l0 = qperm<QP(0, 0, 0, 0)>(lo), h0 = qperm<QP(0, 0, 0, 0)>(hi);
-        const uint32_t l1 = qperm<QP(1, 1, 1, 1)>(lo), h1 = qperm<QP(1, 1, 1, 1)>(hi);
-        const uint32_t l2 = qperm<QP(2, 2, 2, 2)>(lo), h2 = qperm<QP(2, 2, 2, 2)>(hi);
-        const uint32_t l3 = qperm<QP(3, 3, 3, 3)>(lo), h3 = qperm<QP(3, 3, 3, 3)>(hi);
-        r[0] = ldg4<LNT>((const uint8_t *)(uintptr_t)((((uint64_t)h0 << 32) | l0) + part * 16u));
-        r[1] = ldg4<LNT>((const uint8_t *)(uintptr_t)((((uint64_t)h1 << 32) | l1) + part * 16u));
-        r[2] = ldg4<LNT>((const uint8_t *)(uintptr_t)((((uint64_t)h2 << 32) | l2) + part * 16u));
-        r[3] = ldg4<LNT>((const uint8_t *)(uintptr_t)((((uint64_t)h3 << 32) | l3) + part * 16u));
-        return;
-    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint64_t src = __shfl(my_src, 16 * k + (int)fr_in_k) + part * 16u;
@@ -1541,8 +1454,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     const uint32_t t = t0 + jt * wstep;
     // B: tile c-1 -- the rest of its chain (v4: page / tbl8, v6: tbl8 levels, trie.h:127-134)
     const bool bv = jt >= 1 && jt - 1 < nt_w;
-    const uint32_t fl = cnet_frame(lane);
-    const uint32_t ib = (t - wstep) * 64u + fl;
+    const uint32_t ib = (t - wstep) * 64u + lane;
     uint32_t eb = sb.e;
     {
         // one branch-free body for both families: the key bytes stream out of
@@ -1567,31 +1479,26 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         }
     }
     // A: tile c
-    const uint32_t i = t * 64u + fl;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t f = 16u * k + fr_in_k;
+        tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t i = t * 64u + lane;
     const bool live = jt < nt_w && i < a.n;
     const uint64_t base = live ? ct_base(a, i, off.o0) : ~0ull;
-    uint32_t W[16]; // W[4 p + d]: dword d of the frame's part p
-    if (CNDP_CNET_DPP) {
-        quad_xpose(lane, r[P][0].x, r[P][1].x, r[P][2].x, r[P][3].x, W[0], W[4], W[8], W[12]);
-        quad_xpose(lane, r[P][0].y, r[P][1].y, r[P][2].y, r[P][3].y, W[1], W[5], W[9], W[13]);
-        quad_xpose(lane, r[P][0].z, r[P][1].z, r[P][2].z, r[P][3].z, W[2], W[6], W[10], W[14]);
-        quad_xpose(lane, r[P][0].w, r[P][1].w, r[P][2].w, r[P][3].w, W[3], W[7], W[11], W[15]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t f = 16u * k + fr_in_k;
-            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t sw = (lane >> 2) & 3u;
+    const uint32_t sw = (lane >> 2) & 3u;
+    uint32_t W[16];
+    {
         const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
         const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
         W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
         W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
         W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
         W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
-        __builtin_amdgcn_wave_barrier();
     }
+    __builtin_amdgcn_wave_barrier();
     const uint32_t et = W[3] & 0xffffu;
     const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
     // straight-line tests (bitwise &, not &&: no branch tree)
@@ -1703,7 +1610,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     na.e = tb0[idx0]; // first gather, unconditional
     // offsets one tile further, then the windows of tile c+2
     {
-        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + fl;
+        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
         cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
     }
@@ -1848,11 +1755,7 @@ template <bool LNT, bool META>
 __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
     __shared__ uint32_t s_t[TAB_POS * 256];
-    // the window tiles (without CNDP_CNET_DPP), and the rows cnet_defer_tail
-    // parses the worklist in (256 x ROW_DW dwords)
-    constexpr uint32_t TILE_Q = CNDP_CNET_DPP ? (256u * ROW_DW + 3u) / 4u / CT_WAVES + 1u : 256u;
-    static_assert(CT_WAVES * TILE_Q * 4u >= 256u * ROW_DW, "the tail's rows fit");
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][TILE_Q];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
     __shared__ uint32_t s_sf[64];
@@ -1879,7 +1782,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     if (a.offsets) {
 #pragma unroll
         for (uint32_t s = 0; s < 3; s++) {
-            const uint32_t ts = t0 + s * wstep, is = ts * 64u + cnet_frame(lane);
+            const uint32_t ts = t0 + s * wstep, is = ts * 64u + lane;
             const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
             if (s == 0)
                 off.o0 = o;
