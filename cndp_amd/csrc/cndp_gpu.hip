@@ -5021,6 +5021,9 @@ __global__ __launch_bounds__(256) void k_mac_swap(uint8_t *slab, uint64_t slab_l
 #define MB_BUF_LEN 28
 #define MB_PTYPE 32
 #define MB_UDATA64 56
+static_assert(MB_BUF_ADDR == CNDP_MB_BUF_ADDR && MB_DATA_OFF == CNDP_MB_DATA_OFF && MB_BUF_LEN == CNDP_MB_BUF_LEN &&
+                  MB_UDATA64 == CNDP_MB_UDATA64,
+              "node.c reads the same pktmbuf_t fields");
 
 static int mbuf_stage_grow(cndp_gpu_ctx_t *c, uint32_t n)
 {
@@ -5555,6 +5558,52 @@ __device__ __forceinline__ uint8_t *mq_frame(uint64_t w, uint32_t &avail)
 // (in place, each mbuf costs a PCIe round trip; more CUs keep more in flight)
 #define MQ_TPB 64u
 
+// ip4_rewrite_node_process's work on one frame p (avail readable bytes) from
+// its node_mbuf_priv1 pv (ip4_rewrite.c:85-110, :201-216): the next hop's
+// rewrite data at mtod, TTL = priv1.ttl - 1 and the checksum from
+// priv1.cksum + htons(0x0100) -- the 4-wide loop's u32 end-around carry, or
+// with `tail` the tail loop's u16 `chksum += chksum >= 0xffff`.  Returns the
+// next hop's tx_node; next hops past the reference's 64-entry array act as
+// unset entries (no data, tx node 0).
+__device__ __forceinline__ uint32_t mq_rewrite_frame(uint8_t *p, uint32_t avail, uint64_t pv, bool tail,
+                                                     const struct cndp_rw_nh *rw)
+{
+    const uint32_t nh = (uint32_t)(pv & 0xffffu), ttl = (uint32_t)(pv >> 16) & 0xffffu;
+    const uint32_t ck32 = (uint32_t)(pv >> 32);
+    const bool set = nh < CNDP_RW_MAX_NH;
+    const struct cndp_rw_nh *e = &rw[set ? nh : 0u];
+    const uint32_t hdr = set ? *(const uint32_t *)e : 0u; // rewrite_len | tx_node << 16
+    uint32_t len = hdr & 0xffffu;
+    len = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
+    const uint32_t *src = (const uint32_t *)e->rewrite_data;
+    if (len <= avail && (((uintptr_t)p) & 3u) == 0 && (len & 3u) == 0) {
+        for (uint32_t k = 0; k < len / 4; k++)
+            ((uint32_t *)p)[k] = src[k];
+    } else {
+        for (uint32_t k = 0; k < len && k < avail; k++)
+            p[k] = e->rewrite_data[k];
+    }
+    uint32_t nck;
+    if (!tail) {
+        const uint32_t c32 = ck32 + 1u;
+        nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
+    } else {
+        const uint32_t c16 = (ck32 + 1u) & 0xffffu;
+        nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
+    }
+    if (avail > 22)
+        p[22] = (uint8_t)(ttl - 1u);
+    if (avail > 25 && (((uintptr_t)p) & 1u) == 0) {
+        *(uint16_t *)(p + 24) = (uint16_t)nck;
+    } else {
+        if (avail > 24)
+            p[24] = (uint8_t)nck;
+        if (avail > 25)
+            p[25] = (uint8_t)(nck >> 8);
+    }
+    return hdr >> 16;
+}
+
 // ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
 // mtod + 14 + 16, priv1 = {nh = val & 0xffff, ttl, hdr_checksum}, edge = val >> 16
 __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
@@ -5564,6 +5613,8 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
         const uint8_t *p; // bytes 20..35 of the frame
         uint32_t avail;   // readable bytes from p
         uint64_t m = 0;
+        uint8_t *fr = nullptr; // zc: the frame (mtod) and its readable bytes, for the fused rewrite
+        uint32_t fra = 0;
         if (a.zc && a.devhdr) {
             m = a.mb[i];
             const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
@@ -5576,16 +5627,20 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
             }
             p = a.slab + fo + MQ_W4_AT;
             avail = a.slab_len - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(a.slab_len - fo > MQ_W4_AT ? a.slab_len - fo - MQ_W4_AT : 0);
+            fr = (uint8_t *)a.slab + fo;
+            fra = a.slab_len - fo > 255u ? 255u : (uint32_t)(a.slab_len - fo);
         } else if (a.zc) {
             m = a.mb[i];
             uint32_t fa;
-            const uint8_t *f = mq_frame(w, fa);
+            uint8_t *f = mq_frame(w, fa);
             if (m == 0 || f == nullptr) {
                 a.edges[i] = (uint16_t)MQ_EDGE_NONE;
                 continue;
             }
             p = f + MQ_W4_AT;
             avail = fa > MQ_W4_AT ? fa - MQ_W4_AT : 0u;
+            fr = f;
+            fra = fa;
         } else {
             p = a.slab + w;
             avail = MQ_W4;
@@ -5605,7 +5660,15 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
                   gbyte(p, avail, 13);
         }
         const uint32_t val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
-        const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
+        uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
+        if (a.rw && (val >> 16) == CNE_NODE_IP4_LOOKUP_NEXT_REWRITE && fr) {
+            // CNDP_MQ_F_REWRITE: ip4_rewrite's bytes now, by the 4-wide rule
+            // (cndp_node_ip4_rewrite_fused applies the tail rule where it
+            // differs), and the mark in ttl's high byte, which ip4_rewrite's
+            // u8 TTL store drops
+            mq_rewrite_frame(fr, fra, priv1, false, a.rw);
+            priv1 |= (uint64_t)CNDP_PRIV1_REWRITTEN << 24;
+        }
         if (a.zc)
             *(uint64_t *)(m + MB_UDATA64) = priv1;
         else
@@ -5675,41 +5738,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_rewrite(MqArgs a)
             p = (uint8_t *)a.slab + a.off[i];
             avail = MQ_RW_STAGE;
         }
-        const uint64_t pv = a.priv[i];
-        const uint32_t nh = (uint32_t)(pv & 0xffffu), ttl = (uint32_t)(pv >> 16) & 0xffffu;
-        const uint32_t ck32 = (uint32_t)(pv >> 32);
-        const bool set = nh < CNDP_RW_MAX_NH;
-        const struct cndp_rw_nh *e = &a.rw[set ? nh : 0u];
-        const uint32_t hdr = set ? *(const uint32_t *)e : 0u; // rewrite_len | tx_node << 16
-        uint32_t len = hdr & 0xffffu;
-        len = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
-        const uint32_t *src = (const uint32_t *)e->rewrite_data;
-        if (len <= avail && (((uintptr_t)p) & 3u) == 0 && (len & 3u) == 0) {
-            for (uint32_t k = 0; k < len / 4; k++)
-                ((uint32_t *)p)[k] = src[k];
-        } else {
-            for (uint32_t k = 0; k < len && k < avail; k++)
-                p[k] = e->rewrite_data[k];
-        }
-        uint32_t nck;
-        if (!tail) {
-            const uint32_t c32 = ck32 + 1u;
-            nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
-        } else {
-            const uint32_t c16 = (ck32 + 1u) & 0xffffu;
-            nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
-        }
-        if (avail > 22)
-            p[22] = (uint8_t)(ttl - 1u);
-        if (avail > 25 && (((uintptr_t)p) & 1u) == 0) {
-            *(uint16_t *)(p + 24) = (uint16_t)nck;
-        } else {
-            if (avail > 24)
-                p[24] = (uint8_t)nck;
-            if (avail > 25)
-                p[25] = (uint8_t)(nck >> 8);
-        }
-        a.edges[i] = (uint16_t)(hdr >> 16);
+        a.edges[i] = (uint16_t)mq_rewrite_frame(p, avail, a.priv[i], tail, a.rw);
     }
     mq_complete(a);
 }
@@ -5954,7 +5983,10 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP &&
         k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
-    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS))
+    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_REWRITE))
+        return -EINVAL;
+    // the fused rewrite writes frames in place: ip4_lookup over registered UMEMs only
+    if ((k.flags & CNDP_MQ_F_REWRITE) && (k.mode != CNDP_MQ_IP4_LOOKUP || !k.umem))
         return -EINVAL;
     k.batch = k.batch ? k.batch : 8192u;
     k.depth = k.depth ? k.depth : 4u;
@@ -6154,6 +6186,11 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
         a.tb = mq_tables(c, 0);
+        if (q->conf.flags & CNDP_MQ_F_REWRITE) { // ip4_rewrite fused into the lookup pass
+            if ((r = rw_sync(c, s)))
+                return r;
+            a.rw = c->d_rw_tbl;
+        }
         if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // the frames in conf.umem's region
             for (int k = 0; k < q->nrg; k++)
                 if (q->rg[k].host == (const uint8_t *)q->conf.umem) {

@@ -58,6 +58,7 @@
 
 #include "cndp_gpu.h"
 #include "cndp_node.h"
+#include "gpu_node_enqueue.h"
 
 #define RX_BURST 256 /* CNE_GRAPH_BURST_SIZE (cne_graph.h:30) */
 
@@ -88,6 +89,7 @@ struct gpu_rx_state {
     void *rx[RX_BURST];
     void *done[RX_BURST];
     uint16_t edge[RX_BURST];
+    void *grp[RX_BURST]; /* a poll's mbufs grouped by edge */
 };
 
 struct gpu_rx_ctx { /* node->ctx is CNE_NODE_CTX_SZ (16) bytes */
@@ -131,7 +133,7 @@ static inline cne_edge_t rx_edge(uint16_t e)
                                      : ETH_RX_GPU_NEXT_PKT_DROP;
 }
 
-/* hand every finished mbuf on to its edge, runs of one edge at a time */
+/* hand every finished mbuf on to its edge, one enqueue per edge */
 static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct gpu_rx_state *st)
 {
     uint16_t total = 0;
@@ -139,15 +141,9 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
         const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, RX_BURST);
         if (k <= 0)
             break;
-        int i = 0;
-        while (i < k) {
-            const cne_edge_t e = rx_edge(st->edge[i]);
-            int j = i + 1;
-            while (j < k && rx_edge(st->edge[j]) == e)
-                j++;
-            cne_node_enqueue(graph, node, e, &st->done[i], (uint16_t)(j - i));
-            i = j;
-        }
+        for (int i = 0; i < k; i++)
+            st->edge[i] = rx_edge(st->edge[i]);
+        gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, ETH_RX_GPU_NEXT_MAX, st->grp);
         total = (uint16_t)(total + k);
         if (k < RX_BURST)
             break;

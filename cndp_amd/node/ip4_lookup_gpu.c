@@ -31,6 +31,14 @@
  *   the graph's ports may use different pools), else staged.  An mbuf the
  *   queue cannot reach (outside every registered UMEM) leaves by pkt_drop.
  *
+ * With the GPU ip4_rewrite node linked too (ip4_rewrite_gpu.c) and frames
+ * read in place, the queue also applies ip4_rewrite's bytes to the frames it
+ * sends to ip4_rewrite (CNDP_MQ_F_REWRITE: the rewrite reads nothing ip4_lookup
+ * has not already read, so the frame crosses PCIe once for both nodes) and
+ * ip4_rewrite then only fixes the tail loop's checksums and enqueues.  The
+ * frames an ip4_lookup edge other than ip4_rewrite takes are untouched.
+ * CNDP_GPU_FUSE_REWRITE=0 turns it off (two passes, as without the link).
+ *
  * One GPU context and queue per graph (graphs are per lcore, cne_graph_worker.h
  * notes a graph is not shared between threads); contexts share the node FIB,
  * whose device mirror libcndp_gpu keeps on one device per process.
@@ -47,6 +55,7 @@
 
 #include "cndp_gpu.h"
 #include "cndp_node.h"
+#include "gpu_node_enqueue.h"
 
 #define GPU_POLL_MAX 256
 #define GPU_GRAPHS_MAX 256 /* graph ids this module tracks */
@@ -61,7 +70,11 @@ struct gpu_graph_state {
     cndp_gpu_mq_t *q;
     void *done[GPU_POLL_MAX];
     uint16_t edge[GPU_POLL_MAX];
+    void *grp[GPU_POLL_MAX]; /* a poll's mbufs grouped by edge */
 };
+
+/* defined by ip4_rewrite_gpu.c when the GPU ip4_rewrite node is linked */
+extern const int cndp_ip4_rewrite_gpu_linked __attribute__((weak));
 
 static pthread_mutex_t gs_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct gpu_graph_state *gs_by_graph[GPU_GRAPHS_MAX];
@@ -119,6 +132,8 @@ static struct gpu_graph_state *state_get(const struct cne_graph *graph)
     for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)
         if (cndp_gpu_host_register(st->gpu, umem, ulen, NULL) == 0 && !conf.umem)
             conf.umem = umem;
+    if (conf.umem && &cndp_ip4_rewrite_gpu_linked && env_u32("CNDP_GPU_FUSE_REWRITE", 1))
+        conf.flags |= CNDP_MQ_F_REWRITE;
     if (cndp_gpu_mq_create(st->gpu, &conf, &st->q) < 0)
         goto fail;
     gs_by_graph[gid] = st;
@@ -143,7 +158,7 @@ static void state_release(const struct cne_graph *graph, struct gpu_graph_state 
     pthread_mutex_unlock(&gs_lock);
 }
 
-/* hand every finished mbuf on to its edge, runs of one edge at a time */
+/* hand every finished mbuf on to its edge, one enqueue per edge */
 static uint16_t gpu_drain(struct cne_graph *graph, struct cne_node *node, struct gpu_graph_state *st)
 {
     uint16_t total = 0;
@@ -151,19 +166,13 @@ static uint16_t gpu_drain(struct cne_graph *graph, struct cne_node *node, struct
         const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, GPU_POLL_MAX);
         if (k <= 0)
             break;
-        int i = 0;
-        while (i < k) {
-            int j = i + 1;
-            while (j < k && st->edge[j] == st->edge[i])
-                j++;
-            /* a FIB value naming no edge of this node (ip4_lookup.c:150 takes
-             * val >> 16 as is) and an mbuf the queue could not reach
-             * (CNDP_MQ_EDGE_NONE) leave by pkt_drop */
-            const cne_edge_t e = st->edge[i] < CNE_NODE_IP4_LOOKUP_NEXT_MAX ? (cne_edge_t)st->edge[i]
-                                                                             : CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP;
-            cne_node_enqueue(graph, node, e, &st->done[i], (uint16_t)(j - i));
-            i = j;
-        }
+        /* a FIB value naming no edge of this node (ip4_lookup.c:150 takes
+         * val >> 16 as is) and an mbuf the queue could not reach
+         * (CNDP_MQ_EDGE_NONE) leave by pkt_drop */
+        for (int i = 0; i < k; i++)
+            if (st->edge[i] >= CNE_NODE_IP4_LOOKUP_NEXT_MAX)
+                st->edge[i] = CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP;
+        gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, CNE_NODE_IP4_LOOKUP_NEXT_MAX, st->grp);
         total = (uint16_t)(total + k);
         if (k < GPU_POLL_MAX)
             break;
