@@ -456,8 +456,6 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     ptrs = pool.ptrs(np.arange(n))
     l3 = {}
     NodeFib.fini()
-    # the lookup node alone: without the rewrite fused into its pass
-    os.environ["CNDP_GPU_FUSE_REWRITE"] = "0"
     for zc in (True, False):
         L.cndp_node_gpu_umem_reset()
         if zc:
@@ -469,7 +467,6 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
         H.harness_graph_destroy()
         l3["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
-    os.environ.pop("CNDP_GPU_FUSE_REWRITE", None)
     L.cndp_node_gpu_umem_reset()
     fib = NodeFib()
     t24, t8 = (x.copy() for x in fib.image())
@@ -633,22 +630,17 @@ def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
             tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = 12, nh % 4 + 1, 1
             tbl[nh]["rewrite_data"][:] = np.frombuffer(data + bytes(44), np.uint8)
         H.harness_chain(1)
-        # zero-copy: the rewrite fused into the lookup pass (the default with
-        # both GPU nodes) and as a second pass of its own; staged: two passes
-        for key, zc, fuse in (("gpu_zero_copy_Mpps", True, 1), ("gpu_zero_copy_two_pass_Mpps", True, 0),
-                              ("gpu_staged_Mpps", False, 1)):
+        for zc in (True, False):
             L.cndp_node_gpu_umem_reset()
             if zc:
                 L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
-            os.environ["CNDP_GPU_FUSE_REWRITE"] = str(fuse)
-            assert H.harness_graph_create(30 + int(zc) + 2 * fuse) == 0
+            assert H.harness_graph_create(30 + int(zc)) == 0
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
             H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
             t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
             H.harness_graph_destroy()
-            os.environ.pop("CNDP_GPU_FUSE_REWRITE", None)
-            out[key] = round(n * passes / t / 1e6, 2) if t > 0 else None
+            out["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
         fib = NodeFib()
         t24, t8 = (x.copy() for x in fib.image())
         O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, 1)

@@ -5021,9 +5021,6 @@ __global__ __launch_bounds__(256) void k_mac_swap(uint8_t *slab, uint64_t slab_l
 #define MB_BUF_LEN 28
 #define MB_PTYPE 32
 #define MB_UDATA64 56
-static_assert(MB_BUF_ADDR == CNDP_MB_BUF_ADDR && MB_DATA_OFF == CNDP_MB_DATA_OFF && MB_BUF_LEN == CNDP_MB_BUF_LEN &&
-                  MB_UDATA64 == CNDP_MB_UDATA64,
-              "node.c reads the same pktmbuf_t fields");
 
 static int mbuf_stage_grow(cndp_gpu_ctx_t *c, uint32_t n)
 {
@@ -5613,8 +5610,6 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
         const uint8_t *p; // bytes 20..35 of the frame
         uint32_t avail;   // readable bytes from p
         uint64_t m = 0;
-        uint8_t *fr = nullptr; // zc: the frame (mtod) and its readable bytes, for the fused rewrite
-        uint32_t fra = 0;
         if (a.zc && a.devhdr) {
             m = a.mb[i];
             const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
@@ -5627,20 +5622,16 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
             }
             p = a.slab + fo + MQ_W4_AT;
             avail = a.slab_len - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(a.slab_len - fo > MQ_W4_AT ? a.slab_len - fo - MQ_W4_AT : 0);
-            fr = (uint8_t *)a.slab + fo;
-            fra = a.slab_len - fo > 255u ? 255u : (uint32_t)(a.slab_len - fo);
         } else if (a.zc) {
             m = a.mb[i];
             uint32_t fa;
-            uint8_t *f = mq_frame(w, fa);
+            const uint8_t *f = mq_frame(w, fa);
             if (m == 0 || f == nullptr) {
                 a.edges[i] = (uint16_t)MQ_EDGE_NONE;
                 continue;
             }
             p = f + MQ_W4_AT;
             avail = fa > MQ_W4_AT ? fa - MQ_W4_AT : 0u;
-            fr = f;
-            fra = fa;
         } else {
             p = a.slab + w;
             avail = MQ_W4;
@@ -5660,15 +5651,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
                   gbyte(p, avail, 13);
         }
         const uint32_t val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
-        uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
-        if (a.rw && (val >> 16) == CNE_NODE_IP4_LOOKUP_NEXT_REWRITE && fr) {
-            // CNDP_MQ_F_REWRITE: ip4_rewrite's bytes now, by the 4-wide rule
-            // (cndp_node_ip4_rewrite_fused applies the tail rule where it
-            // differs), and the mark in ttl's high byte, which ip4_rewrite's
-            // u8 TTL store drops
-            mq_rewrite_frame(fr, fra, priv1, false, a.rw);
-            priv1 |= (uint64_t)CNDP_PRIV1_REWRITTEN << 24;
-        }
+        const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
         if (a.zc)
             *(uint64_t *)(m + MB_UDATA64) = priv1;
         else
@@ -5983,10 +5966,7 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP &&
         k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
-    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_REWRITE))
-        return -EINVAL;
-    // the fused rewrite writes frames in place: ip4_lookup over registered UMEMs only
-    if ((k.flags & CNDP_MQ_F_REWRITE) && (k.mode != CNDP_MQ_IP4_LOOKUP || !k.umem))
+    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS))
         return -EINVAL;
     k.batch = k.batch ? k.batch : 8192u;
     k.depth = k.depth ? k.depth : 4u;
@@ -6186,11 +6166,6 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
             return r;
         a.tb = mq_tables(c, 0);
-        if (q->conf.flags & CNDP_MQ_F_REWRITE) { // ip4_rewrite fused into the lookup pass
-            if ((r = rw_sync(c, s)))
-                return r;
-            a.rw = c->d_rw_tbl;
-        }
         if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // the frames in conf.umem's region
             for (int k = 0; k < q->nrg; k++)
                 if (q->rg[k].host == (const uint8_t *)q->conf.umem) {

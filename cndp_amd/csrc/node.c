@@ -16,7 +16,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../include/cndp_gpu.h"
 #include "node_internal.h"
 
 static pthread_mutex_t node_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -177,49 +176,6 @@ void cndp_node_ip4_rewrite_reset(void)
     ip4_rewrite_nm = NULL;
     rw_gen++;
     pthread_mutex_unlock(&node_lock);
-}
-
-/* the rewrite node's half of the fused l3fwd pass (cndp_node.h) */
-int cndp_node_ip4_rewrite_fused(void *const *mbufs, uint16_t n, uint16_t *edges)
-{
-    if (!mbufs || !edges)
-        return -EINVAL;
-    /* one pass over the headers (the lookup pass wrote udata64 over PCIe, so
-     * each is a cache miss: prefetched a few mbufs ahead); the next-hop table
-     * is read without the lock, as ip4_rewrite_node_process reads
-     * ip4_rewrite_nm; nothing is written before every mark is seen */
-    const struct rw_main *nm = ip4_rewrite_nm;
-    for (uint16_t i = 0; i < n; i++) {
-        if (i + 8u < n)
-            __builtin_prefetch((const uint8_t *)mbufs[i + 8u] + CNDP_MB_UDATA64);
-        const uint64_t u = *(const uint64_t *)((const uint8_t *)mbufs[i] + CNDP_MB_UDATA64);
-        if (((u >> 24) & 0xffu) != CNDP_PRIV1_REWRITTEN)
-            return 0;
-        const uint32_t nh = (uint32_t)(u & 0xffffu);
-        edges[i] = nh < CNDP_IP4_REWRITE_MAX_NH && nm ? nm->nh[nh].tx_node : 0;
-    }
-    /* the tail loop's positions (ip4_rewrite.c:201) */
-    for (uint16_t i = (uint16_t)(n & ~3u); i < n; i++) {
-        uint8_t *m = (uint8_t *)mbufs[i];
-        const uint64_t u = *(const uint64_t *)(m + CNDP_MB_UDATA64);
-        const uint32_t ck32 = (uint32_t)(u >> 32);
-        /* the 4-wide loop's u32 end-around carry (what the GPU wrote) against
-         * the tail loop's u16 `chksum += chksum >= 0xffff` (:209-216) */
-        const uint32_t c32 = ck32 + 1u;
-        const uint32_t wide = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
-        const uint32_t c16 = (ck32 + 1u) & 0xffffu;
-        const uint32_t nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
-        if (nck == wide)
-            continue;
-        uint8_t *buf = *(uint8_t *const *)(m + CNDP_MB_BUF_ADDR);
-        const uint16_t off = *(const uint16_t *)(m + CNDP_MB_DATA_OFF);
-        const uint16_t len = *(const uint16_t *)(m + CNDP_MB_BUF_LEN);
-        if (buf && (uint32_t)off + 26u <= len) { /* hdr_checksum at mtod + 14 + 10 */
-            buf[off + 24] = (uint8_t)nck;
-            buf[off + 25] = (uint8_t)(nck >> 8);
-        }
-    }
-    return n;
 }
 
 uint64_t cndp_node_rw_snapshot(struct cndp_rw_nh *tbl)

@@ -22,12 +22,6 @@ struct cndp_rw_nh {
     uint8_t rewrite_data[CNDP_IP4_REWRITE_MAX_LEN];
 };
 
-/* pktmbuf_t fields the host side reads (pktmbuf.h:102-204) */
-#define CNDP_MB_BUF_ADDR 8
-#define CNDP_MB_DATA_OFF 24
-#define CNDP_MB_BUF_LEN 28
-#define CNDP_MB_UDATA64 56
-
 /* Copy the process-global rewrite table (64 entries) into tbl and return its
  * generation (bumped by every change; 0 = never written). */
 uint64_t cndp_node_rw_snapshot(struct cndp_rw_nh *tbl);

@@ -45,8 +45,7 @@ CNDP_TUNE_MBUF_HASH = 12
 CNDP_TUNE_CNET_FOLD = 13
 CNDP_TUNE_SPEC_GRID = 14
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
-CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS, CNDP_MQ_F_REWRITE = 1, 2, 4, 8
-CNDP_PRIV1_REWRITTEN = 0x80
+CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS = 1, 2, 4
 CNDP_MQ_EDGE_NONE = 0xFFFF
 CNDP_MQ_STAT_BATCHES, CNDP_MQ_STAT_MBUFS = 1, 2
 CNDP_MQ_NODE_PTYPE, CNDP_MQ_NODE_IP4, CNDP_MQ_NODE_IP6 = 0, 1, 2
@@ -150,7 +149,6 @@ def lib():
         "cndp_node_ip4_rewrite_get": (c_int, [c_uint16, c_void_p, POINTER(c_uint16), POINTER(c_uint16),
                                               POINTER(c_uint16)]),
         "cndp_node_ip4_rewrite_reset": (None, []),
-        "cndp_node_ip4_rewrite_fused": (c_int, [c_void_p, c_uint16, c_void_p]),
         "cndp_node_gpu_umem_add": (c_int, [c_void_p, c_uint64]),
         "cndp_node_gpu_umem_get": (c_int, [c_uint32, POINTER(c_void_p), POINTER(c_uint64)]),
         "cndp_node_gpu_umem_reset": (None, []),

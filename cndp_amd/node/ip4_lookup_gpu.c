@@ -31,14 +31,6 @@
  *   the graph's ports may use different pools), else staged.  An mbuf the
  *   queue cannot reach (outside every registered UMEM) leaves by pkt_drop.
  *
- * With the GPU ip4_rewrite node linked too (ip4_rewrite_gpu.c) and frames
- * read in place, the queue also applies ip4_rewrite's bytes to the frames it
- * sends to ip4_rewrite (CNDP_MQ_F_REWRITE: the rewrite reads nothing ip4_lookup
- * has not already read, so the frame crosses PCIe once for both nodes) and
- * ip4_rewrite then only fixes the tail loop's checksums and enqueues.  The
- * frames an ip4_lookup edge other than ip4_rewrite takes are untouched.
- * CNDP_GPU_FUSE_REWRITE=0 turns it off (two passes, as without the link).
- *
  * One GPU context and queue per graph (graphs are per lcore, cne_graph_worker.h
  * notes a graph is not shared between threads); contexts share the node FIB,
  * whose device mirror libcndp_gpu keeps on one device per process.
@@ -72,9 +64,6 @@ struct gpu_graph_state {
     uint16_t edge[GPU_POLL_MAX];
     void *grp[GPU_POLL_MAX]; /* a poll's mbufs grouped by edge */
 };
-
-/* defined by ip4_rewrite_gpu.c when the GPU ip4_rewrite node is linked */
-extern const int cndp_ip4_rewrite_gpu_linked __attribute__((weak));
 
 static pthread_mutex_t gs_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct gpu_graph_state *gs_by_graph[GPU_GRAPHS_MAX];
@@ -132,8 +121,6 @@ static struct gpu_graph_state *state_get(const struct cne_graph *graph)
     for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)
         if (cndp_gpu_host_register(st->gpu, umem, ulen, NULL) == 0 && !conf.umem)
             conf.umem = umem;
-    if (conf.umem && &cndp_ip4_rewrite_gpu_linked && env_u32("CNDP_GPU_FUSE_REWRITE", 1))
-        conf.flags |= CNDP_MQ_F_REWRITE;
     if (cndp_gpu_mq_create(st->gpu, &conf, &st->q) < 0)
         goto fail;
     gs_by_graph[gid] = st;

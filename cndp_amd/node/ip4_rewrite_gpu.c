@@ -18,11 +18,7 @@
  *     the next hop's tx_node as the next edge.
  * Each process() burst goes whole to an asynchronous queue (cndp_gpu_mq_*,
  * mode CNDP_MQ_IP4_REWRITE), so the burst boundaries the checksum rule
- * depends on are the node's own -- unless the GPU ip4_lookup node already
- * rewrote every frame of the burst in its own pass (CNDP_MQ_F_REWRITE, the
- * mark in udata64): then cndp_node_ip4_rewrite_fused fixes the checksums of
- * the burst's tail-loop positions where that rule differs and returns the
- * tx edges, on the host, with no second pass over the frames.  Finished mbufs come back in order and are
+ * depends on are the node's own.  Finished mbufs come back in order and are
  * enqueued to their tx edges by process() and by "ip4_rewrite_gpu_drain", a
  * source node every cne_graph_walk calls (also the flush of a partly filled
  * batch).  Its edges mirror ip4_rewrite's: the library calls back here from
@@ -49,7 +45,6 @@
 #include "gpu_node_enqueue.h"
 
 #define RW_POLL_MAX 256
-#define RW_FUSED_MAX 1024 /* a larger burst (its stream grew) takes the queue */
 #define RW_GRAPHS_MAX 256
 #define RW_EDGES_MAX 64 /* pkt_drop + one tx edge per port (CNE_MAX_ETHPORTS = 32) */
 #define DRAIN_NODE_NAME "ip4_rewrite_gpu_drain"
@@ -64,12 +59,8 @@ struct rw_graph_state {
     uint16_t nb_edges; /* ip4_rewrite's edge count at graph create */
     void *done[RW_POLL_MAX];
     uint16_t edge[RW_POLL_MAX];
-    uint16_t fedge[RW_FUSED_MAX]; /* tx edges of a burst the lookup pass rewrote */
-    void *grp[RW_FUSED_MAX];      /* a burst regrouped by edge */
+    void *grp[RW_POLL_MAX]; /* a poll's mbufs grouped by edge */
 };
-
-/* tells ip4_lookup_gpu.c that this node is linked (its fused pass) */
-const int cndp_ip4_rewrite_gpu_linked = 1;
 
 static pthread_mutex_t rw_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct rw_graph_state *rw_by_graph[RW_GRAPHS_MAX];
@@ -184,13 +175,6 @@ static uint16_t ip4_rewrite_gpu_process(struct cne_graph *graph, struct cne_node
                                         uint16_t nb_objs)
 {
     struct rw_graph_state *st = RW_NODE_STATE(node);
-    /* frames the GPU ip4_lookup pass rewrote: tail checksums and tx edges on
-     * the host, runs of one edge at a time */
-    if (nb_objs <= RW_FUSED_MAX && cndp_node_ip4_rewrite_fused(objs, nb_objs, st->fedge) == nb_objs) {
-        rw_enqueue(graph, node, st, objs, st->fedge, nb_objs);
-        rw_drain(graph, node, st);
-        return nb_objs;
-    }
     /* the queue takes the burst in 256s (a multiple of 4, so its nb_objs & ~3
      * split, the checksum rule, is the node's own); when every batch slot is
      * busy, drain and then wait for the oldest batch */

@@ -216,18 +216,6 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
  * reads each header (buf_addr, data_off) in place -- no host touch per mbuf,
  * three dependent PCIe reads per mbuf instead of one (frames in conf.umem) */
 #define CNDP_MQ_F_DEVICE_HEADERS (1u << 2)
-/* ip4_lookup, zero-copy only: a frame whose FIB value sends it to ip4_rewrite
- * (edge 0) also gets ip4_rewrite's bytes in the same pass -- the next hop's
- * rewrite data at mtod, TTL - 1, the checksum + htons(0x0100) by the 4-wide
- * loop's rule (ip4_rewrite.c:85-110) -- from the rewrite table the context
- * follows, and node_mbuf_priv1.ttl's high byte is set to
- * CNDP_PRIV1_REWRITTEN.  ip4_rewrite computes every byte it writes from
- * priv1 and writes only the low byte of ttl, so running either rewrite node
- * afterwards gives the same frame; the GPU ip4_rewrite node then only
- * applies the tail loop's checksum rule where it differs
- * (cndp_node_ip4_rewrite_fused) instead of a second pass over the frames. */
-#define CNDP_MQ_F_REWRITE (1u << 3)
-#define CNDP_PRIV1_REWRITTEN 0x80u /* in bits 24..31 of udata64 (ttl's high byte) */
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u
 #define CNDP_MQ_NODE_IP6 2u

@@ -100,16 +100,6 @@ void cndp_node_ip4_lookup_fini(void);
 int cndp_node_ip4_rewrite_get(uint16_t next_hop, uint8_t *rewrite_data, uint16_t *rewrite_len,
                               uint16_t *tx_node, uint16_t *enabled);
 void cndp_node_ip4_rewrite_reset(void);
-/* ip4_rewrite_node_process (ip4_rewrite.c:40-247) for a burst whose frames the
- * GPU ip4_lookup pass already rewrote (CNDP_MQ_F_REWRITE: every mbuf's
- * udata64 carries CNDP_PRIV1_REWRITTEN): the mbufs at the tail loop's
- * positions (the last nb_objs % 4) whose checksum rule differs from the 4-wide
- * loop's (priv1.cksum 0xFFFE / 0xFFFF) get the tail rule's checksum, and
- * edges[i] = the next hop's tx_node from the process-global table (0 for next
- * hops >= 64, as an unset entry).  Returns n, or 0 -- nothing written -- when
- * any mbuf of the burst lacks the mark (the caller then runs the whole burst
- * through the rewrite queue, so the burst's positions stay the node's own). */
-int cndp_node_ip4_rewrite_fused(void *const *mbufs, uint16_t n, uint16_t *edges);
 
 /* Host regions (AF_XDP UMEMs, the pktmbuf pool: lport_cfg_t.umem_addr /
  * umem_size, cne_lport.h:91) the GPU nodes may read frames from in place.

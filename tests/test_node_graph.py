@@ -85,7 +85,6 @@ def test_node_graph_walk(gpu, zero_copy):
         assert L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes) == 0
     os.environ["CNDP_GPU_BATCH"] = "2048"
     os.environ["CNDP_GPU_DEPTH"] = "3"
-    os.environ["CNDP_GPU_FUSE_REWRITE"] = "0"  # the lookup node alone (test_l3fwd_graph_chain fuses)
     try:
         assert H.harness_graph_create(3) == 0
         # routes after graph create, as l3fwd-graph does (fwd.c:160-201)
@@ -117,7 +116,6 @@ def test_node_graph_walk(gpu, zero_copy):
         H.harness_graph_destroy()
         os.environ.pop("CNDP_GPU_BATCH", None)
         os.environ.pop("CNDP_GPU_DEPTH", None)
-        os.environ.pop("CNDP_GPU_FUSE_REWRITE", None)
         L.cndp_node_gpu_umem_reset()
     vals = [(ip, d, nh) for ip, d, nh in routes]
     t24, t8 = O.dir24_8_build(vals, N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
@@ -495,16 +493,13 @@ def test_rewrite_node_graph_walk(gpu, zero_copy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fused", [True, False], ids=["fused", "two_pass"])
-def test_l3fwd_graph_chain(gpu, fused):
+def test_l3fwd_graph_chain(gpu):
     """The l3fwd-graph chain with both GPU nodes, walked as cne_graph_walk
     runs it (ip4_lookup's enqueues fill ip4_rewrite's stream, which runs in
     the same walk): every mbuf ends at pkt_drop or its next hop's tx edge with
     priv1 and the rewritten frame of the reference chain (checksums where the
     4-wide and tail rules agree, i.e. not 0xFFFE / 0xFFFF, whose rule depends
-    on the stream split; tests/test_rewrite_fused.py pins those for the fused
-    host half).  fused: the rewrite applied in the lookup pass
-    (CNDP_MQ_F_REWRITE, priv1 marked); two_pass: a queue pass per node."""
+    on the stream split)."""
     from cndp_amd import pktgen
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
@@ -522,13 +517,12 @@ def test_l3fwd_graph_chain(gpu, fused):
     L.cndp_node_gpu_umem_reset()
     assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
     os.environ["CNDP_GPU_BATCH"] = "4096"
-    os.environ["CNDP_GPU_FUSE_REWRITE"] = "1" if fused else "0"
     routes = pktgen.l3fwd_routes()
     try:
         _eth_config(H, L, ports)
         tbl = _rw_table(L, 72, ports)
         H.harness_chain(1)
-        assert H.harness_graph_create(12 + int(fused)) == 0
+        assert H.harness_graph_create(12) == 0
         for ip, d, nh in routes:
             assert cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
         assert H.harness_drive(b"ip4_lookup", gp.ptrs(np.arange(n)), n, 256, 1) >= 0
@@ -545,7 +539,6 @@ def test_l3fwd_graph_chain(gpu, fused):
         L.cndp_node_ip4_rewrite_reset()
         L.cndp_node_gpu_umem_reset()
         os.environ.pop("CNDP_GPU_BATCH", None)
-        os.environ.pop("CNDP_GPU_FUSE_REWRITE", None)
     # the reference chain on the oracle's copy: ip4_lookup then ip4_rewrite
     t24, t8 = O.dir24_8_build(list(routes), N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
     d = op.data_pos().astype(np.int64)
@@ -555,11 +548,8 @@ def test_l3fwd_graph_chain(gpu, fused):
     val = O.dir24_8_lookup(t24, t8, dip).astype(np.uint64)
     ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
     op.hdr["udata64"] = (val & 0xFFFF) | (op.mem[d + 22].astype(np.uint64) << 16) | (ck << 32)
+    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
     rw = np.nonzero((val >> 16) == 0)[0]
-    mark = np.zeros(n, np.uint64)
-    if fused:  # the frames the lookup pass rewrote carry the mark in ttl's high byte
-        mark[rw] = np.uint64(N.CNDP_PRIV1_REWRITTEN << 24)
-    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"] | mark)
     tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
     want = np.zeros(n, np.int64)
     want[rw] = tx

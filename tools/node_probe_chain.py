@@ -1,8 +1,8 @@
 """The l3fwd-graph node pair on the GPU (ip4_lookup -> ip4_rewrite, harness
-chained walks as bench.py's node_boundary drives them) with the rewrite fused
-into the lookup pass and as a second pass, beside the lookup node alone; host
-time split between the source-node turns and process() calls (which include
-the chained ip4_rewrite).  Diagnostic: python3 tools/node_probe_chain.py"""
+chained walks as bench.py's node_boundary drives them) beside the lookup node
+alone; host time split between the source-node turns and process() calls
+(which include the chained ip4_rewrite).  Diagnostic:
+python3 tools/node_probe_chain.py"""
 import ctypes
 import os
 import random
@@ -50,9 +50,8 @@ L.cndp_node_gpu_umem_reset()
 L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
 gid = 50
 for rep in range(2):
-    for label, chain, fuse in (("lookup alone", 0, 0), ("pair fused", 1, 1), ("pair two-pass", 1, 0)):
+    for label, chain in (("lookup alone", 0), ("lookup + rewrite", 1)):
         NodeFib.fini()
-        os.environ["CNDP_GPU_FUSE_REWRITE"] = str(fuse)
         H.harness_chain(chain)
         assert H.harness_graph_create(gid) == 0
         gid += 1
@@ -68,7 +67,6 @@ for rep in range(2):
               f"{src.value / n / passes * 1e9:.2f} ns, process {proc.value / n / passes * 1e9:.2f} ns", flush=True)
 H.harness_chain(0)
 H.harness_edges_reset()
-os.environ.pop("CNDP_GPU_FUSE_REWRITE", None)
 L.cndp_node_gpu_umem_reset()
 L.cndp_node_ip4_rewrite_reset()
 NodeFib.fini()
