@@ -3582,9 +3582,9 @@ struct cndp_gpu_ctx {
     int spec_reset;       // the node state (last_type) restarts at 0 on the next cnet call
     int mbuf_hash;        // CNDP_TUNE_MBUF_HASH: cndp_gpu_l3fwd_mbufs also writes m->hash
     // Stream order of the context's scratch (speculation state, worklist,
-    // partition scratch): every call that uses it records ev_scratch on its
-    // stream, and a call on another stream first waits for that event, so
-    // calls on different streams never overlap on the shared scratch.
+    // partition scratch): a call on another stream than the last user's
+    // records ev_scratch on that stream and waits for it, so calls on
+    // different streams never overlap on the shared scratch.
     hipEvent_t ev_scratch;
     hipStream_t scratch_stream;
     int scratch_used;
@@ -3678,16 +3678,25 @@ static int set_device(int dev)
     return 0;
 }
 
-// order this call after the previous scratch user if it ran on another stream
+// order this call after the previous scratch user if it ran on another stream.
+// The event is recorded on the previous user's stream only then, not after
+// every call: a record is a system-scope release in the stream (the L2 is
+// written back for the host to see), ~6 us in front of every cnet call's
+// first kernel (a device-scope release measured the same).  Recorded late,
+// it also covers whatever that stream ran since, which only orders more.
+// So a stream given to a call that used the scratch must outlive the next
+// call on another stream (cndp_gpu.h); the library's own streams (node
+// queues, the host path's) clear the context's record when they go.
 static int scratch_acquire(cndp_gpu_ctx_t *c, hipStream_t s)
 {
-    if (c->scratch_used && s != c->scratch_stream)
+    if (c->scratch_used && s != c->scratch_stream) {
+        HIP_TRY(hipEventRecord(c->ev_scratch, c->scratch_stream));
         HIP_TRY(hipStreamWaitEvent(s, c->ev_scratch, 0));
+    }
     return 0;
 }
 static int scratch_release(cndp_gpu_ctx_t *c, hipStream_t s)
 {
-    HIP_TRY(hipEventRecord(c->ev_scratch, s));
     c->scratch_stream = s;
     c->scratch_used = 1;
     return 0;
@@ -6071,8 +6080,13 @@ extern "C" void cndp_gpu_mq_free(cndp_gpu_mq_t *q)
         hipHostFree(q->flags);
     if (q->tickets)
         hipFree(q->tickets);
-    if (q->s)
+    if (q->s) {
+        // the context's last scratch user may be this stream (scratch_acquire
+        // would record on it): drained above, so nothing is left to order
+        if (q->c->scratch_used && q->c->scratch_stream == q->s)
+            q->c->scratch_used = 0;
         hipStreamDestroy(q->s);
+    }
     free(q);
 }
 

@@ -26,7 +26,11 @@
  * +256) or a packed slab (64-B slots).  Bytes at or past slab + slab_len
  * read as zero.  All batch pointers are DEVICE pointers (hipMalloc / torch);
  * work is enqueued on `stream` (a hipStream_t, NULL = null stream) and the
- * call returns without waiting.  Errors are negative errno values.
+ * call returns without waiting.  Errors are negative errno values.  Calls on
+ * one context that share its scratch (cnet mode, the bin partition) are
+ * ordered across streams: a call on another stream than the previous one's
+ * first waits for that stream, so a stream given to such a call must stay
+ * alive until the next such call on another stream (or cndp_gpu_fini).
  *
  * Per-packet outputs (SoA, any may be NULL except as noted):
  *   nh[i]    u32 FIB value (l3fwd: edge<<16 | nh id; cnet: edge<<24 | idx),
