@@ -692,6 +692,7 @@ def main():
     ap.add_argument("--cnet-tile", type=int, default=None)
     ap.add_argument("--cnet-spec", type=int, default=None)
     ap.add_argument("--spec-scan", type=int, default=None)
+    ap.add_argument("--spec-lists", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--dir16", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
@@ -713,7 +714,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16,
                   load_nt=args.load_nt, cnet_tile=args.cnet_tile, cnet_spec=args.cnet_spec,
-                  spec_scan=args.spec_scan)
+                  spec_scan=args.spec_scan, spec_lists=args.spec_lists)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 

@@ -156,6 +156,8 @@ struct KArgs {
     uint32_t *spec_ticket; // k_classify_cnet's block arrivals, 9 words 32 apart (0 between launches)
     uint32_t *spec_bar;    // k_spec_fallback's barrier words, reset by spec_classes
     uint8_t *spec_tile;    // per 64-frame tile: 0x80 | edge when every frame has that edge, else 0
+    uint32_t *spec_cwl;    // CNDP_TUNE_SPEC_LISTS: chunks with a non-canonical tile ([0] = count)
+    uint32_t *spec_cflag;  //   and a flag per chunk so each is listed once
     uint32_t *spec_hint;   // pinned host words (device view): the last call's worklist size class, uniform flag
     uint32_t spec_B;       // graph burst size
     uint32_t wl_fold;      // k_cnet_defer's last block parses the worklist and runs spec_classes
@@ -169,6 +171,15 @@ struct KArgs {
 
 #define FAST_THREADS 256
 #define SPEC_CH_K 4 // graph bursts per speculation chunk (SPEC_CH)
+// meta word (spec_meta index) of CNDP_TUNE_SPEC_LISTS:
+// what the fast kernel saw of the groups that could move
+// the node state off a common edge (ptype.c:122-130: a group's 4th type
+// becomes the state when the 3rd equals it or when its p_nxt edge is the
+// state's): bits 0-7 = the edges of such 4th types (fast-parsed, not bound
+// for their low byte's input node, 3rd type different), bit 8 = a 4th type
+// that equals the 3rd or is not known to the fast kernel.  k_spec_fallback
+// clears it for the next call.
+#define SPEC_MX 135
 // a packet ip4_lookup hands to ip4_rewrite (edge 0, ip4_lookup.c:150)
 __device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
@@ -1444,11 +1455,23 @@ struct CdLane {
     uint32_t q0, q1, q2, q3;
 };
 
+// CNDP_TUNE_SPEC_LISTS: list the chunks (SPEC_CH_K graph bursts) that tile tt
+// overlaps, each once a call (k_spec_local_t replays them, k_spec_fallback
+// clears the flags)
+__device__ void spec_list_tile(const KArgs &a, uint32_t tt)
+{
+    const uint32_t per = SPEC_CH_K * a.spec_B, f0 = tt * 64u, f1 = f0 + 63u < a.n ? f0 + 63u : a.n - 1u;
+    for (uint32_t c = f0 / per; c <= f1 / per; c++)
+        if (atomicExch(&a.spec_cflag[c], 1u) == 0u)
+            a.spec_cwl[1u + atomicAdd(&a.spec_cwl[0], 1u)] = c;
+}
+
 template <bool LNT, bool META, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
                                         CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
-                                        uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig)
+                                        uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig,
+                                        uint32_t *s_mx)
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
     const uint32_t t = t0 + jt * wstep;
@@ -1646,8 +1669,23 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 // or pkt_drop, nor left to the general parse
                 const bool odd = ib < a.n && !(bf && (pe == 3u || pe == 4u));
                 const bool canon = __ballot(odd) == 0ull;
-                if (lane == 0)
+                if (lane == 0) {
                     a.spec_tile[t - wstep] = (uint8_t)canon;
+                    if (!canon && a.spec_cwl)
+                        spec_list_tile(a, t - wstep);
+                }
+                if (a.spec_cwl) { // SPEC_MX: lane 4q + 3 looks at group q (bursts of a multiple of 4)
+                    const uint32_t w = (ib < a.n ? 1u << 25 : 0u) | (bf ? (1u << 24) | (pe << 16) | pt : 0u);
+                    const uint32_t w2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xAA, 0xf, 0xf, true); // lane 4q + 2
+                    if ((lane & 3u) == 3u && ((w >> 25) & 1u)) {
+                        const bool k3 = (w >> 24) & 1u, k2 = (w2 >> 24) & 1u, same = (w2 & 0xffffu) == pt;
+                        const bool notok3 = k3 && pe != 3u && pe != 4u;
+                        const uint32_t x = !k3 || (notok3 && (!k2 || same)) ? 1u << 8 : 0u;
+                        const uint32_t m = notok3 && k2 && !same ? 1u << pe : 0u;
+                        if (x | m)
+                            atomicOr(s_mx, x | m);
+                    }
+                }
             }
         }
         if (bf) {
@@ -1759,10 +1797,13 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
     __shared__ uint32_t s_sf[64];
+    __shared__ uint32_t s_mx; // SPEC_MX bits of this block
 
     const uint32_t tid = threadIdx.x;
     if (tid < 64)
         s_sf[tid] = 0;
+    if (tid == 0)
+        s_mx = 0;
     for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
         s_t[k] = a.ttab[k];
     for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
@@ -1802,10 +1843,10 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {
         cd_trip<LNT, META, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
-                        last_sig);
+                        last_sig, &s_mx);
         if (jt + 1 < trips)
             cd_trip<LNT, META, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
-                            count, last_sig);
+                            count, last_sig, &s_mx);
     }
     if (count || a.spec_flags)
         __syncthreads();
@@ -1815,6 +1856,8 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
     if (a.spec_flags && tid < 64 && s_sf[tid])
         atomicOr(&a.spec_flags[tid], s_sf[tid]);
+    if (a.spec_cwl && tid == 0 && s_mx)
+        atomicOr(&a.spec_meta[SPEC_MX], s_mx);
     if (a.wl_fold)
         cnet_defer_tail(a, (uint32_t *)&s_tile[0][0], s_t, s_reta, s_bins, s_sf, count);
 }
@@ -3115,8 +3158,9 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                                                       uint8_t *done, uint32_t *R)
 {
     static_assert(CH == SPEC_CH, "spec_chunk_pre");
-    __shared__ int s_bins[CNDP_BINS_MAX + 2]; // the uniform pass's bin moves
+    __shared__ int s_bins[CNDP_BINS_MAX + 2]; // the uniform pass's / listed chunks' bin moves
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
+    __shared__ __attribute__((aligned(16))) uint32_t s_st[4][CH * 256]; // a listed chunk's types
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // wave-uniform in SGPRs (the chunk index and all that derives from it)
     const uint64_t wid = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wv), W = (uint64_t)gridDim.x * 4;
@@ -3162,12 +3206,68 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 atomicAdd(&a.bins[k], (unsigned long long)(long long)lbins[k]);
         return;
     }
-    uint32_t tw, pq0, pq1;
-    spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
+    // CNDP_TUNE_SPEC_LISTS: when no group of the batch can take the node state
+    // off its low byte's common edge (SPEC_MX, the entering state, the other
+    // low bytes present), a frame can leave by another edge only inside a
+    // chunk the fast kernel listed, so only those are looked at (grid-uniform)
+    bool lists = false;
+    if (a.spec_cwl) {
+        const uint32_t mx = meta[SPEC_MX], M = mx & 0xffu, e_in = cnet_edge(s_in), cn = spec_canon(s_in & 0xffu);
+        lists = !(mx >> 8) && (cn == 0xFFu || cn == e_in) && !((M >> e_in) & 1u);
+        if (lists) { // a state of another low byte whose edge is in M could take such a 4th type
+            const uint32_t K = meta[0], sig = lane < K && lane < SPEC_KMAX ? meta[1 + lane] : 0u;
+            const bool clash = lane < K && (sig >> 3) != 0x11u && (sig >> 3) != 0x41u && ((M >> (sig & 7u)) & 1u);
+            lists = K <= SPEC_KMAX && __ballot(clash) == 0ull;
+        }
+    }
+    uint32_t tw = 1u, pq0 = 0u, pq1 = 0u;
+    if (!lists)
+        spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
     cnet_lut_fill(s_lut, threadIdx.x, 256);
+    const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
+    if (lists)
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            s_bins[k] = 0;
     __syncthreads();
     if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL])
         return;
+    if (lists) {
+        if (wid == 0) { // the final node state (meta[-1]): the walk in the last chunk
+            const uint64_t l0 = (nch - 1) * CH, l1 = l0 + CH < nb ? l0 + CH : nb;
+            uint32_t sf = 0;
+            if (spec_lookback(a.spec_t16, a.n, B, l0, l1, lane, s_lut, sf)) {
+                if (lane == 0)
+                    meta[-1] = sf;
+            } else if (lane == 0) {
+                spec_flag_full(meta);
+            }
+        }
+        const uint32_t nl = a.spec_cwl[0];
+        for (uint64_t k = wid; k < nl; k += W) {
+            const uint64_t c = a.spec_cwl[1 + k], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+            uint32_t s0 = s_in;
+            if (c > 0) { // the entering state: the walk in the previous chunk
+                uint32_t q0, q1;
+                spec_group_regs(a.spec_t16, (c0 - 1) * B, B, lane, q0, q1);
+                if (!spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, q0, q1)) {
+                    if (lane == 0) { // left to the full passes (done[] of the others is not read)
+                        done[c] = 0;
+                        spec_flag_full(meta);
+                    }
+                    continue;
+                }
+            }
+            spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0)
+                done[c] = 1;
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)(long long)s_bins[k]);
+        return;
+    }
     for (uint64_t c = wid; c < nch; c += W) {
         const uint32_t ctw = tw, cq0 = pq0, cq1 = pq1;
         spec_chunk_pre(a, B, nch, c + W, lane, tw, pq0, pq1); // the next chunk's loads, in flight meanwhile
@@ -3264,6 +3364,16 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
     // device atomics serialize, ~1 µs per hundred)
     __shared__ int s_lb[CNDP_BINS_MAX + 2];
     static_assert(SPEC_BLK * (SPEC_KMAX + 1) >= 4 * CH * 256, "staging fits the scan rows");
+    if (blockIdx.x == 0 && a.spec_cwl) { // the fast kernel's chunk list and SPEC_MX, empty for the next call
+        const uint32_t nl = a.spec_cwl[0];
+        for (uint32_t k = threadIdx.x; k < nl; k += 256u)
+            a.spec_cflag[a.spec_cwl[1 + k]] = 0u;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            a.spec_cwl[0] = 0u;
+            meta[SPEC_MX] = 0u;
+        }
+    }
     uint32_t rc[8], nrep = 0; // the 8 replay lists (k_spec_local_t)
 #pragma unroll
     for (int x = 0; x < 8; x++) {
@@ -3575,6 +3685,7 @@ struct cndp_gpu_ctx {
     int tune_spec_scan;   // CNDP_TUNE_SPEC_SCAN
     int tune_cnet_fold;   // CNDP_TUNE_CNET_FOLD: 0 hint, 1 always, 2 never
     int tune_spec_grid;   // CNDP_TUNE_SPEC_GRID: 0 hint, 1 shrunk (2 blocks), 2 full
+    int tune_spec_lists;  // CNDP_TUNE_SPEC_LISTS: 1 chunk lists from the fast kernel (default), 0 off
     int sf_clean, wl_clean; // signature flags / worklist count known zero (no memset needed)
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
     int tune_rw_wb;       // CNDP_TUNE_RW_WB: fused rewrite write-back 0 auto, 1 frame, 2 tile
@@ -3602,6 +3713,8 @@ struct cndp_gpu_ctx {
     uint8_t *sp_class;    // class id per signature (2048)
     uint32_t *sp_pt, *sp_nh, *sp_S, *sp_T, *sp_U; // sp_pt: the u16 types (speculation model)
     uint8_t *sp_done;     // per chunk: resolved by k_spec_local
+    uint32_t *sp_cwl;     // chunks the fast kernel lists ([0] = count), CNDP_TUNE_SPEC_LISTS
+    uint32_t *sp_cflag;   // per chunk: listed this call (cleared by k_spec_fallback)
     uint32_t *sp_R;       // chunks k_spec_local_t leaves to k_spec_fallback: (chunk, entering state)
     uint8_t *sp_tile;     // per 64-frame tile: the main kernel's canonical-tile word
     uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch uniform
@@ -3728,6 +3841,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_dir16 = 1;
     c->tune_cnet_tile = 1;
     c->tune_lnt = 1;
+    c->tune_spec_lists = 1;
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
     c->tune_rw_wb = 2;
@@ -3780,7 +3894,8 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
         hipFree(c->m_dres);
     if (c->d_rw_tbl)
         hipFree(c->d_rw_tbl);
-    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt, c->sp_nh, c->sp_S, c->sp_T, c->sp_U, c->sp_done, c->sp_tile, c->sp_R};
+    void *sp[] = {c->sp_small, c->sp_class, c->sp_pt,   c->sp_nh,  c->sp_S,    c->sp_T,
+                  c->sp_U,     c->sp_done,  c->sp_tile, c->sp_R,   c->sp_cwl, c->sp_cflag};
     for (void *q : sp)
         if (q)
             hipFree(q);
@@ -4423,12 +4538,21 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
             HIP_TRY(hipFree(c->sp_done));
         if (c->sp_R)
             HIP_TRY(hipFree(c->sp_R));
-        c->sp_S = c->sp_T = c->sp_U = c->sp_R = nullptr;
+        if (c->sp_cwl)
+            HIP_TRY(hipFree(c->sp_cwl));
+        if (c->sp_cflag)
+            HIP_TRY(hipFree(c->sp_cflag));
+        c->sp_S = c->sp_T = c->sp_U = c->sp_R = c->sp_cwl = c->sp_cflag = nullptr;
         c->sp_done = nullptr;
         c->sp_b_cap = 0;
         const uint64_t cap = nb + (nb >> 3) + 64;
         HIP_TRY(hipMalloc((void **)&c->sp_S, cap * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_done, cap));
+        // the chunk list and its flags start empty; k_spec_fallback empties them again
+        HIP_TRY(hipMalloc((void **)&c->sp_cwl, (cap + 1) * 4));
+        HIP_TRY(hipMemset(c->sp_cwl, 0, (cap + 1) * 4));
+        HIP_TRY(hipMalloc((void **)&c->sp_cflag, cap * 4));
+        HIP_TRY(hipMemset(c->sp_cflag, 0, cap * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_R, cap * 16 * 4)); // 8 lists of (chunk, state), chunks <= cap
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
         // inclusive burst prefixes + block totals + block start states
@@ -4566,6 +4690,12 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                                                                  k_cnet_defer<true, true>}};
             const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
             a.spec_tile = B ? c->sp_tile : nullptr; // written by this kernel only
+            // chunk lists (CNDP_TUNE_SPEC_LISTS): groups must be lane quads of the
+            // tiles (bursts of a multiple of 4) and the chunked passes run (B <= 256)
+            if (B && B <= 256 && (B & 3u) == 0 && c->tune_spec_lists && c->tune_spec_scan == 0) {
+                a.spec_cwl = c->sp_cwl;
+                a.spec_cflag = c->sp_cflag;
+            }
             // the previous call left no worklist: the main kernel's last block
             // takes this call's (if any) and the classes pass, no second launch.
             // The hint is a pinned word an earlier call's kernel wrote, maybe
@@ -6685,6 +6815,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 2)
             return -EINVAL;
         c->tune_spec_grid = value;
+        return 0;
+    case CNDP_TUNE_SPEC_LISTS:
+        if (value < 0 || value > 1)
+            return -EINVAL;
+        c->tune_spec_lists = value;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

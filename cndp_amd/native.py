@@ -44,6 +44,7 @@ CNDP_STAT_CNET_WORKLIST, CNDP_STAT_CNET_UNIFORM = 1, 2
 CNDP_TUNE_MBUF_HASH = 12
 CNDP_TUNE_CNET_FOLD = 13
 CNDP_TUNE_SPEC_GRID = 14
+CNDP_TUNE_SPEC_LISTS = 15
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
 CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS = 1, 2, 4
 CNDP_MQ_EDGE_NONE = 0xFFFF

@@ -359,7 +359,13 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           2 = always the second launch (tests force both)
  *   CNDP_TUNE_SPEC_GRID     cnet speculation local pass grid: 0 = auto (a small grid
  *                           after a uniform batch), 1 = 2 blocks, 2 = one wave per
- *                           4 chunks (tests force both) */
+ *                           4 chunks (tests force both)
+ *   CNDP_TUNE_SPEC_LISTS    cnet speculation, bursts of a multiple of 4 <= 256:
+ *                           1 = the fast kernel lists the chunks with a frame off its
+ *                           low byte's common edge and, when no group of the batch can
+ *                           move the node state off a common edge, the local pass
+ *                           replays only those (default); 0 = the local pass looks at
+ *                           every chunk (tests force both) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -374,6 +380,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_MBUF_HASH 12
 #define CNDP_TUNE_CNET_FOLD 13
 #define CNDP_TUNE_SPEC_GRID 14
+#define CNDP_TUNE_SPEC_LISTS 15
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words

@@ -742,6 +742,70 @@ def test_cnet_ptype_speculation(cnet, gpu, burst):
     ccl.set_tuning(cnet_spec=256)
 
 
+def _sparse_gtp(n, routes, v6, gpu, seed, pure_head=0):
+    """IMIX as the bench carries it (IPv4 + IPv6 UDP) but with GTP-U / GTP-C
+    frames every few hundred IPv4 frames and never two in a row, so no group
+    can move the ptype node's state off its low byte's common edge: the case
+    the chunk lists (CNDP_TUNE_SPEC_LISTS) take.  pure_head: that many plain
+    IPv4 UDP frames of one type first (no universal group there: a listed
+    chunk behind it has no entering state and goes to the full passes)."""
+    parts = []
+    if pure_head:
+        parts.append(pktgen.imix(pure_head, v4routes=routes, v6routes=v6, device="cpu", seed=seed + 7, v6_frac=0.0))
+    parts.append(pktgen.imix(n - pure_head, v4routes=routes, v6routes=v6, device="cpu", seed=seed, v6_frac=0.5))
+    slab = torch.cat([p.slab for p in parts])
+    offs, at = [], 0
+    for p in parts:
+        offs.append(p.offsets + at)
+        at += p.slab.numel()
+    offsets = torch.cat(offs)
+    is4 = (slab[offsets + 12] == 0x08) & (slab[offsets + 13] == 0x00)
+    slab[torch.where(is4, offsets + 36, offsets + 56)] = 0x12  # every UDP dport off the GTP ports
+    g = torch.Generator().manual_seed(seed)
+    pick = torch.rand(n, generator=g)
+    k = torch.arange(n)
+    gtpu = is4 & (pick < 0.004) & (k >= pure_head)
+    gtpc = is4 & (pick >= 0.004) & (pick < 0.006) & (k >= pure_head)
+    lone = ~torch.roll(gtpu | gtpc, 1) & ~torch.roll(gtpu | gtpc, -1)
+    gtpu, gtpc = gtpu & lone, gtpc & lone
+    for sel, port in ((gtpu, 2152), (gtpc, 2123)):
+        slab[offsets[sel] + 36] = port >> 8
+        slab[offsets[sel] + 37] = port & 0xFF
+    return pktgen.Frames(slab.to(gpu), n, offsets=offsets.to(gpu))
+
+
+@pytest.mark.parametrize("burst", [256, 64, 12, 4])
+@pytest.mark.parametrize("head", [0, 3000])
+def test_cnet_speculation_chunk_lists(cnet, gpu, burst, head):
+    """Sparse GTP in IMIX: the fast kernel lists the chunks with a frame off
+    its low byte's common edge and the local pass replays only those, when no
+    group can move the node state off its common edge -- == the restated node
+    loop over three chained calls (the first starts from state 0, whose
+    edge GTP-C shares, so it takes the full sweep; the later ones the lists),
+    and == the same calls with the lists off.  head: a single-type run first,
+    so a listed chunk behind it has no universal group to start from."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = _sparse_gtp(60000, routes, v6, gpu, seed=burst + head, pure_head=head)
+    plain = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)
+    full = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=burst)
+    assert (plain["edge"] != full["edge"]).sum() > 0, "input does not exercise the quirk"
+    cuts = [0, 20000 // burst * burst, 40000 // burst * burst, fr.n]
+    try:
+        for lists in (1, 0):
+            ccl.set_tuning(cnet_spec=0)
+            ccl.set_tuning(cnet_spec=burst, spec_lists=lists)  # a new graph: state 0
+            st = np.zeros(1, np.uint16)
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                part = pktgen.Frames(fr.slab, hi - lo, offsets=fr.offsets[lo:hi].contiguous())
+                ref = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=burst, spec_state=st)
+                out = ccl.alloc_outputs(part.n, 64, device=gpu, meta=True)
+                ccl.classify(part, N.CNDP_MODE_CNET, out=out)
+                torch.cuda.synchronize()
+                assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_lists=1)
+
+
 @pytest.mark.parametrize("burst", [256, 7, 1000])
 def test_cnet_speculation_batch_shortcut(cnet, gpu, burst):
     """Batches whose low ptype bytes each carry one p_nxt edge (plain IMIX:
