@@ -180,6 +180,8 @@ struct KArgs {
 // that equals the 3rd or is not known to the fast kernel.  k_spec_fallback
 // clears it for the next call.
 #define SPEC_MX 135
+#define SPEC_PTRS 151 // meta[151..154] (8-B aligned): the chunk list's and its flags' device pointers
+#define SPEC_ALLOW_LISTS 2u // KArgs::spec_allow bit: this call lists (spec_cwl / spec_cflag set)
 // a packet ip4_lookup hands to ip4_rewrite (edge 0, ip4_lookup.c:150)
 __device__ __forceinline__ bool nh_ready_rw(uint32_t v) { return v != 0xFFFFFFFFu && (v >> 16) == 0u; }
 #define TAB4_POS 12 /* Toeplitz positions for the IPv4 L4 tuple */
@@ -1455,15 +1457,32 @@ struct CdLane {
     uint32_t q0, q1, q2, q3;
 };
 
-// CNDP_TUNE_SPEC_LISTS: list the chunks (SPEC_CH_K graph bursts) that tile tt
-// overlaps, each once a call (k_spec_local_t replays them, k_spec_fallback
-// clears the flags)
-__device__ void spec_list_tile(const KArgs &a, uint32_t tt)
+// a non-canonical tile of the fast kernel (CNDP_TUNE_SPEC_LISTS), looked at
+// once the wave's loop is done so the loop holds no registers for it: its
+// chunks listed, and SPEC_MX bits 0..7 from its groups -- lane 4q + 3 looks at
+// group q (bursts of a multiple of 4).  A group whose 4th frame is off the
+// common edge moves the node state to that edge unless its 3rd type equals
+// the 4th (then to any edge: bit 8).  The loop already set bit 8 for a group
+// whose 4th frame, or whose 3rd beside an off-edge 4th, was not parsed there;
+// without it both types here are the fast kernel's own, stored by this lane.
+// The list's device pointers sit in meta (SPEC_PTRS).
+__device__ __forceinline__ void spec_odd_tile(const KArgs &a, uint32_t tt, uint32_t lane, uint32_t *s_mx)
 {
-    const uint32_t per = SPEC_CH_K * a.spec_B, f0 = tt * 64u, f1 = f0 + 63u < a.n ? f0 + 63u : a.n - 1u;
-    for (uint32_t c = f0 / per; c <= f1 / per; c++)
-        if (atomicExch(&a.spec_cflag[c], 1u) == 0u)
-            a.spec_cwl[1u + atomicAdd(&a.spec_cwl[0], 1u)] = c;
+    if (lane == 0) {
+        uint32_t *const cwl = *(uint32_t *const *)(a.spec_meta + SPEC_PTRS);
+        uint32_t *const cflag = *(uint32_t *const *)(a.spec_meta + SPEC_PTRS + 2);
+        const uint32_t per = SPEC_CH_K * a.spec_B, f0 = tt * 64u, f1 = f0 + 63u < a.n ? f0 + 63u : a.n - 1u;
+        for (uint32_t c = f0 / per; c <= f1 / per; c++)
+            if (atomicExch(&cflag[c], 1u) == 0u)
+                cwl[1u + atomicAdd(&cwl[0], 1u)] = c;
+    }
+    const uint32_t i = tt * 64u + lane;
+    const bool in = i < a.n;
+    const uint32_t pt = in ? (uint32_t)at16(a.spec_t16, i) : 0u;
+    const uint32_t p2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)pt, 0xAA, 0xf, 0xf, true); // lane 4q + 2
+    const uint32_t pe = cnet_edge(pt);
+    if ((lane & 3u) == 3u && in && pe != 3u && pe != 4u)
+        atomicOr(s_mx, p2 == pt ? 1u << 8 : 1u << pe);
 }
 
 template <bool LNT, bool META, int P>
@@ -1668,23 +1687,15 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 // byte 0x11 / 0x41) and bound for ip4_input / ip6_input, not GTP
                 // or pkt_drop, nor left to the general parse
                 const bool odd = ib < a.n && !(bf && (pe == 3u || pe == 4u));
-                const bool canon = __ballot(odd) == 0ull;
-                if (lane == 0) {
-                    a.spec_tile[t - wstep] = (uint8_t)canon;
-                    if (!canon && a.spec_cwl)
-                        spec_list_tile(a, t - wstep);
-                }
-                if (a.spec_cwl) { // SPEC_MX: lane 4q + 3 looks at group q (bursts of a multiple of 4)
-                    const uint32_t w = (ib < a.n ? 1u << 25 : 0u) | (bf ? (1u << 24) | (pe << 16) | pt : 0u);
-                    const uint32_t w2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xAA, 0xf, 0xf, true); // lane 4q + 2
-                    if ((lane & 3u) == 3u && ((w >> 25) & 1u)) {
-                        const bool k3 = (w >> 24) & 1u, k2 = (w2 >> 24) & 1u, same = (w2 & 0xffffu) == pt;
-                        const bool notok3 = k3 && pe != 3u && pe != 4u;
-                        const uint32_t x = !k3 || (notok3 && (!k2 || same)) ? 1u << 8 : 0u;
-                        const uint32_t m = notok3 && k2 && !same ? 1u << pe : 0u;
-                        if (x | m)
-                            atomicOr(s_mx, x | m);
-                    }
+                const uint64_t om = __ballot(odd);
+                if (lane == 0)
+                    a.spec_tile[t - wstep] = (uint8_t)(om == 0ull);
+                if (om && (a.spec_allow & SPEC_ALLOW_LISTS)) { // wave-uniform, rare
+                    // groups (lanes 4q + 3) whose 4th frame was not parsed here, or
+                    // is off the common edge beside a 3rd not parsed here (spec_odd_tile)
+                    const uint64_t nf = __ballot(ib < a.n && !bf), m3 = 0x8888888888888888ull;
+                    if (lane == 0 && ((nf & m3) | (om & m3 & (nf << 1))))
+                        atomicOr(s_mx, 1u << 8);
                 }
             }
         }
@@ -1848,7 +1859,20 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
             cd_trip<LNT, META, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
                             count, last_sig, &s_mx);
     }
-    if (count || a.spec_flags)
+    if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
+        // the wave's non-canonical tiles (its own tile words, its own types)
+        __threadfence_block();
+        for (uint32_t j0 = 0; j0 < nt_w; j0 += 64u) {
+            const uint32_t j = j0 + lane;
+            uint64_t om = __ballot(j < nt_w && a.spec_tile[t0 + j * wstep] == 0u);
+            while (om) {
+                const uint32_t jj = j0 + (uint32_t)(__ffsll((unsigned long long)om) - 1);
+                om &= om - 1ull;
+                spec_odd_tile(a, t0 + jj * wstep, lane, &s_mx);
+            }
+        }
+    }
+    if (count || a.spec_flags || (a.spec_allow & SPEC_ALLOW_LISTS))
         __syncthreads();
     if (count)
         for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
@@ -1856,7 +1880,7 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
     if (a.spec_flags && tid < 64 && s_sf[tid])
         atomicOr(&a.spec_flags[tid], s_sf[tid]);
-    if (a.spec_cwl && tid == 0 && s_mx)
+    if ((a.spec_allow & SPEC_ALLOW_LISTS) && tid == 0 && s_mx)
         atomicOr(&a.spec_meta[SPEC_MX], s_mx);
     if (a.wl_fold)
         cnet_defer_tail(a, (uint32_t *)&s_tile[0][0], s_t, s_reta, s_bins, s_sf, count);
@@ -2972,6 +2996,13 @@ __device__ __forceinline__ void spec_uniform_range(const KArgs &a, uint32_t B, u
 // summary from registers (16-B loads of 8 when the bursts allow), then --
 // when a frame could leave by another edge -- staged in LDS and replayed
 template <int CH>
+__device__ __forceinline__ void spec_chunk_load(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
+                                                u32x4 (&v)[CH * 256 / 512 > 0 ? CH * 256 / 512 : 1]);
+template <int CH>
+__device__ __forceinline__ void spec_chunk_types_v(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
+                                                   uint32_t lane, uint32_t *st, const uint16_t *s_lut, int *lbins,
+                                                   const u32x4 (&v)[CH * 256 / 512 > 0 ? CH * 256 / 512 : 1]);
+template <int CH>
 __device__ __forceinline__ void spec_chunk_types(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
                                                  uint32_t lane, uint32_t *st, const uint16_t *s_lut, int *lbins)
 {
@@ -2982,14 +3013,35 @@ __device__ __forceinline__ void spec_chunk_types(const KArgs &a, uint32_t B, uin
         return;
     }
     constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+    u32x4 v[R];
+    spec_chunk_load<CH>(a, B, c0, c1, lane, v);
+    spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, st, s_lut, lbins, v);
+}
+
+// the types of chunk [c0, c1) as 16-B loads of 8 (bursts of a multiple of 8)
+template <int CH>
+__device__ __forceinline__ void spec_chunk_load(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t lane,
+                                                u32x4 (&v)[CH * 256 / 512 > 0 ? CH * 256 / 512 : 1])
+{
+    constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
     const uint64_t p0 = c0 * B, p1 = c1 * B < a.n ? c1 * B : a.n;
     const uint32_t m = (uint32_t)(p1 - p0);
-    u32x4 v[R];
 #pragma unroll
     for (uint32_t r = 0; r < R; r++) {
         const uint32_t idx = (r * 64u + lane) * 8u;
         v[r] = idx + 8u <= m ? *(const u32x4 *)(a.spec_t16 + p0 + idx) : (u32x4){0, 0, 0, 0};
     }
+}
+
+// spec_chunk_types for bursts of a multiple of 8 from the loaded types v
+template <int CH>
+__device__ __forceinline__ void spec_chunk_types_v(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
+                                                   uint32_t lane, uint32_t *st, const uint16_t *s_lut, int *lbins,
+                                                   const u32x4 (&v)[CH * 256 / 512 > 0 ? CH * 256 / 512 : 1])
+{
+    constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+    const uint64_t p0 = c0 * B, p1 = c1 * B < a.n ? c1 * B : a.n;
+    const uint32_t m = (uint32_t)(p1 - p0);
     // the summary and the LDS staging (spec_stage_chunk's layout) from the
     // same registers: a replay does not load the types a second time
     unsigned long long em = 0;
@@ -3245,19 +3297,26 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
         const uint32_t nl = a.spec_cwl[0];
         for (uint64_t k = wid; k < nl; k += W) {
             const uint64_t c = a.spec_cwl[1 + k], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-            uint32_t s0 = s_in;
-            if (c > 0) { // the entering state: the walk in the previous chunk
-                uint32_t q0, q1;
+            // the chunk's types and the previous burst's groups in one round trip
+            constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+            u32x4 v[R];
+            const bool vec = (B & 7u) == 0;
+            if (vec)
+                spec_chunk_load<CH>(a, B, c0, c1, lane, v);
+            uint32_t s0 = s_in, q0 = 0, q1 = 0;
+            if (c > 0)
                 spec_group_regs(a.spec_t16, (c0 - 1) * B, B, lane, q0, q1);
-                if (!spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, q0, q1)) {
-                    if (lane == 0) { // left to the full passes (done[] of the others is not read)
-                        done[c] = 0;
-                        spec_flag_full(meta);
-                    }
-                    continue;
+            if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, q0, q1)) {
+                if (lane == 0) { // left to the full passes (done[] of the others is not read)
+                    done[c] = 0;
+                    spec_flag_full(meta);
                 }
+                continue;
             }
-            spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr);
+            if (vec)
+                spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr, v);
+            else
+                spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr);
             __builtin_amdgcn_wave_barrier();
             if (lane == 0)
                 done[c] = 1;
@@ -4553,6 +4612,8 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
         HIP_TRY(hipMemset(c->sp_cwl, 0, (cap + 1) * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_cflag, cap * 4));
         HIP_TRY(hipMemset(c->sp_cflag, 0, cap * 4));
+        const uint64_t ptrs[2] = {(uint64_t)(uintptr_t)c->sp_cwl, (uint64_t)(uintptr_t)c->sp_cflag};
+        HIP_TRY(hipMemcpy(c->sp_small + 1 + SPEC_PTRS, ptrs, sizeof(ptrs), hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc((void **)&c->sp_R, cap * 16 * 4)); // 8 lists of (chunk, state), chunks <= cap
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
         // inclusive burst prefixes + block totals + block start states
@@ -4695,6 +4756,7 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             if (B && B <= 256 && (B & 3u) == 0 && c->tune_spec_lists && c->tune_spec_scan == 0) {
                 a.spec_cwl = c->sp_cwl;
                 a.spec_cflag = c->sp_cflag;
+                a.spec_allow |= SPEC_ALLOW_LISTS;
             }
             // the previous call left no worklist: the main kernel's last block
             // takes this call's (if any) and the classes pass, no second launch.
