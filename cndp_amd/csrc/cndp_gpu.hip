@@ -2767,10 +2767,24 @@ __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t
 {
     uint32_t fm, fe;
     spec_replay_walk<CH>(a, B, c0, c1, s0, lane, st, fm, fe);
+#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 6
+    if (fm)
+        a.spec_t16[c0 * B + lane] = (uint16_t)fe;
+    return;
+#endif
     spec_replay_fix<CH>(a, B, c0, lane, st, fm, fe, lbins);
 }
 
 // the walk: fm = frames to fix (bit 4 * burst + j), fe = each burst's edge (3 bits)
+// A type is plain when its p_nxt is its low byte's common edge (spec_canon).
+// A group of four plain types entered in a plain state moves no frame: quiet,
+// its low bytes are the state's and their edge is the state's p_nxt.  The
+// state entering group g is the 4th type of the last group before g that set
+// it (a universal group always does), or the burst's entering state, so it
+// can be other than plain only when a group in [last universal before g, g)
+// has a 4th type that is not, or with no universal group before g, when the
+// entering state is not.  Only those lanes, the lanes holding a type that is
+// not plain and the last lane (the burst's exit state) walk.
 template <int CH>
 __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uint64_t c0, uint64_t c1, uint32_t s0,
                                                  uint32_t lane, const uint32_t *st, uint32_t &fm, uint32_t &fe)
@@ -2786,7 +2800,18 @@ __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uin
         const SpecGroups sg = spec_groups(sb, ng, lane);
         const uint32_t low0 = s0 & 0xffu;
         uint32_t nxt = s0; // the state after this lane's group
-        if (lane < ng) {
+        bool need = false;
+        {
+            u32x4 y = lane < ng ? *(const u32x4 *)(sb + 4 * lane) : (u32x4){0x30011u, 0x30011u, 0x30011u, 0x30011u};
+            const bool p0 = spec_canon(y.x & 0xffu) == (y.x >> 16), p1 = spec_canon(y.y & 0xffu) == (y.y >> 16);
+            const bool p2 = spec_canon(y.z & 0xffu) == (y.z >> 16), p3 = spec_canon(y.w & 0xffu) == (y.w >> 16);
+            const unsigned long long O = __ballot(!p3), below = (1ull << lane) - 1ull, ub = sg.U & below;
+            const uint32_t lu = ub ? 63u - (uint32_t)__clzll(ub) : 0u;
+            const bool s0p = spec_canon(low0) == cnet_edge(s0);
+            need = !(p0 && p1 && p2 && p3) || ((O & below) >> lu) != 0ull || (!s0p && ub == 0ull) ||
+                   lane + 1u == ng;
+        }
+        if (lane < ng && need) {
             // the state entering group `lane`
             uint32_t cur = s0, l = low0, e = cnet_edge(s0);
             const unsigned long long before = sg.U & ((1ull << lane) - 1ull);
@@ -2874,19 +2899,27 @@ __device__ __forceinline__ void spec_group_regs(const uint16_t *__restrict__ pt,
     }
 }
 
-// walk groups [g0, ng) of a burst held one group per lane (ptype.c:95-130)
+// walk groups [g0, ng) of a burst held one group per lane (ptype.c:95-130):
+// g0 and ng are wave-uniform, so the walk is a scalar loop (v_readlane) with
+// the 4th types' p_nxt looked up for all groups at once
 __device__ __forceinline__ void spec_walk_regs(uint32_t q0, uint32_t q1, uint32_t g0, uint32_t ng,
                                                const uint16_t *lut, uint32_t &cur)
 {
+    const uint32_t v = q0 & 0xffu;
+    const bool allq = ((q0 >> 16) & 0xffu) == v && (q1 & 0xffu) == v && ((q1 >> 16) & 0xffu) == v;
+    const uint32_t gq = (allq ? v : 0x1FFu) | ((q1 & 0xffffu) == (q1 >> 16) ? 0x200u : 0u);
+    const uint32_t d = (q1 >> 16) | (cnet_edge_l(lut, q1 >> 16) << 16);
+    uint32_t c = __builtin_amdgcn_readfirstlane(cur);
+    uint32_t E = __builtin_amdgcn_readfirstlane(cnet_edge_l(lut, c));
     for (uint32_t g = g0; g < ng; g++) {
-        const uint32_t a0 = __shfl(q0, (int)g), a1 = __shfl(q1, (int)g);
-        const uint32_t l0 = a0 & 0xffffu, l1 = a0 >> 16, l2 = a1 & 0xffffu, l3 = a1 >> 16;
-        const uint32_t low = cur & 0xffu;
-        const bool quiet =
-            (l0 & 0xffu) == low && (l1 & 0xffu) == low && (l2 & 0xffu) == low && (l3 & 0xffu) == low;
-        if (!quiet && (l2 == l3 || cnet_edge_l(lut, cur) == cnet_edge_l(lut, l3)))
-            cur = l3;
+        const uint32_t qg = (uint32_t)__builtin_amdgcn_readlane((int)gq, (int)g);
+        const uint32_t dg = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)g);
+        if ((qg & 0x1FFu) != (c & 0xffu) && ((qg & 0x200u) || E == (dg >> 16))) {
+            c = dg & 0xffffu;
+            E = dg >> 16;
+        }
     }
+    cur = c;
 }
 
 // the node state after bursts [b_lo, b_hi): the walk from the last universal
@@ -3069,6 +3102,11 @@ __device__ __forceinline__ void spec_chunk_types_v(const KArgs &a, uint32_t B, u
         *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
     }
     __builtin_amdgcn_wave_barrier();
+#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 5
+    if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0) && lane == 0)
+        a.spec_t16[p0] = 0;
+    return;
+#endif
     if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0))
         spec_replay<CH>(a, B, c0, c1, s0, lane, st, lbins);
 }
@@ -3272,6 +3310,10 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
             lists = K <= SPEC_KMAX && __ballot(clash) == 0ull;
         }
     }
+#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 1
+    if (lists)
+        return;
+#endif
     uint32_t tw = 1u, pq0 = 0u, pq1 = 0u;
     if (!lists)
         spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
@@ -3294,7 +3336,10 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 spec_flag_full(meta);
             }
         }
-        const uint32_t nl = a.spec_cwl[0];
+        uint32_t nl = a.spec_cwl[0];
+#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 2
+        nl = 0;
+#endif
         for (uint64_t k = wid; k < nl; k += W) {
             const uint64_t c = a.spec_cwl[1 + k], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
             // the chunk's types and the previous burst's groups in one round trip
@@ -3313,6 +3358,11 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 }
                 continue;
             }
+#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 3
+            if (lane == 0)
+                done[c] = v[0].x + s0;
+            continue;
+#endif
             if (vec)
                 spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr, v);
             else
@@ -3321,6 +3371,9 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
             if (lane == 0)
                 done[c] = 1;
         }
+#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 4
+        return;
+#endif
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
             if (s_bins[k])
