@@ -806,6 +806,73 @@ def test_cnet_speculation_chunk_lists(cnet, gpu, burst, head):
         ccl.set_tuning(cnet_spec=256, spec_lists=1)
 
 
+def _gtp_runs(n, routes, v6, seed, cut_targets):
+    """IMIX (30% IPv6) with runs of 2..7 GTP-U frames (every IPv4 frame of the
+    run) every ~500 frames, and a dense run before each cut target: groups
+    [v6, GTP-U, GTP-U, ...] move the ptype node's state to GTP-U, whose edge
+    is not its low byte's common one, and the plain IPv4 groups after them go
+    whole to gtpu_input."""
+    fr = pktgen.imix(n, v4routes=routes, v6routes=v6, device="cpu", seed=seed, v6_frac=0.3)
+    slab, offsets = fr.slab, fr.offsets
+    is4 = (slab[offsets + 12] == 0x08) & (slab[offsets + 13] == 0x00)
+    slab[torch.where(is4, offsets + 36, offsets + 56)] = 0x12  # every UDP dport off the GTP ports
+    g = torch.Generator().manual_seed(seed)
+    mark = torch.zeros(n, dtype=torch.bool)
+    for s0 in torch.randint(0, n - 8, (n // 500,), generator=g).tolist():
+        mark[s0:s0 + int(torch.randint(2, 8, (1,), generator=g))] = True
+    for c in cut_targets:
+        mark[c - 24:c] = True
+    sel = mark & is4
+    slab[offsets[sel] + 36] = 2152 >> 8
+    slab[offsets[sel] + 37] = 2152 & 0xFF
+    return pktgen.Frames(slab, n, offsets=offsets)
+
+
+@pytest.mark.parametrize("burst", [256, 64, 12])
+def test_cnet_speculation_gtp_state(cnet, gpu, burst):
+    """Runs of GTP-U frames move the node state off its low byte's common
+    edge (GTP-U shares IPv4/UDP's low byte 0x11); the quiet IPv4 groups that
+    follow leave by gtpu_input, and a call that ends in that state hands it
+    to the next one.  Three chained calls == the restated node loop, with the
+    chunk lists on and off (the replay walks only the lanes that can move a
+    frame: this is the case where many can)."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    n = 60000
+    targets = [20000 // burst * burst, 40000 // burst * burst]
+    fr = _gtp_runs(n, routes, v6, seed=burst, cut_targets=targets)
+    # cuts near the targets where the node state entering the next call is GTP-U
+    cuts = [0]
+    for t in targets:
+        for c in range(t - 24 * burst, t + 24 * burst + 1, burst):
+            st = np.zeros(1, np.uint16)
+            oracle_classify(O.MODE_CNET, pktgen.Frames(fr.slab, c, offsets=fr.offsets[:c].contiguous()),
+                            tables4=ct4, tables6=ct6, spec_burst=burst, spec_state=st)
+            if int(st[0]) == 0x8211 and c > cuts[-1]:
+                cuts.append(c)
+                break
+    assert len(cuts) == 3, "no cut enters a call in the GTP-U state"
+    cuts.append(n)
+    plain = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=0)
+    full = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=burst)
+    moved = (plain["edge"] != full["edge"]) & ((full["ptype"] & 0xFFFF) == 0x0211)
+    assert moved.sum() > 20, "input does not send plain IPv4 frames to gtpu_input"
+    gfr = pktgen.Frames(fr.slab.to(gpu), n, offsets=fr.offsets.to(gpu))
+    try:
+        for lists in (1, 0):
+            ccl.set_tuning(cnet_spec=0)
+            ccl.set_tuning(cnet_spec=burst, spec_lists=lists)  # a new graph: state 0
+            st = np.zeros(1, np.uint16)
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                part = pktgen.Frames(gfr.slab, hi - lo, offsets=gfr.offsets[lo:hi].contiguous())
+                ref = oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=burst, spec_state=st)
+                out = ccl.alloc_outputs(part.n, 64, device=gpu, meta=True)
+                ccl.classify(part, N.CNDP_MODE_CNET, out=out)
+                torch.cuda.synchronize()
+                assert_same(out, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_lists=1)
+
+
 @pytest.mark.parametrize("burst", [256, 7, 1000])
 def test_cnet_speculation_batch_shortcut(cnet, gpu, burst):
     """Batches whose low ptype bytes each carry one p_nxt edge (plain IMIX:
