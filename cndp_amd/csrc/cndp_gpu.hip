@@ -3300,6 +3300,9 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     // off its low byte's common edge (SPEC_MX, the entering state, the other
     // low bytes present), a frame can leave by another edge only inside a
     // chunk the fast kernel listed, so only those are looked at (grid-uniform)
+    // (SPEC_UNIF implies no SPEC_SKIP; SPEC_NOLOCAL without it: nothing here)
+    if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL])
+        return;
     bool lists = false;
     if (a.spec_cwl) {
         const uint32_t mx = meta[SPEC_MX], M = mx & 0xffu, e_in = cnet_edge(s_in), cn = spec_canon(s_in & 0xffu);
@@ -3314,6 +3317,11 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     if (lists)
         return;
 #endif
+    // the lists' blocks without a listed chunk (block 0 also walks the final
+    // state) leave before the table fill: most of the grid, block-uniform
+    const uint32_t nl = lists ? a.spec_cwl[0] : 0u;
+    if (lists && blockIdx.x != 0 && (uint64_t)blockIdx.x * 4 >= nl)
+        return;
     uint32_t tw = 1u, pq0 = 0u, pq1 = 0u;
     if (!lists)
         spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
@@ -3323,8 +3331,6 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
         for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
             s_bins[k] = 0;
     __syncthreads();
-    if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL])
-        return;
     if (lists) {
         if (wid == 0) { // the final node state (meta[-1]): the walk in the last chunk
             const uint64_t l0 = (nch - 1) * CH, l1 = l0 + CH < nb ? l0 + CH : nb;
@@ -3336,11 +3342,11 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 spec_flag_full(meta);
             }
         }
-        uint32_t nl = a.spec_cwl[0];
 #if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 2
-        nl = 0;
-#endif
+        for (uint64_t k = wid; k < 0u; k += W) {
+#else
         for (uint64_t k = wid; k < nl; k += W) {
+#endif
             const uint64_t c = a.spec_cwl[1 + k], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
             // the chunk's types and the previous burst's groups in one round trip
             constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
