@@ -2767,11 +2767,6 @@ __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t
 {
     uint32_t fm, fe;
     spec_replay_walk<CH>(a, B, c0, c1, s0, lane, st, fm, fe);
-#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 6
-    if (fm)
-        a.spec_t16[c0 * B + lane] = (uint16_t)fe;
-    return;
-#endif
     spec_replay_fix<CH>(a, B, c0, lane, st, fm, fe, lbins);
 }
 
@@ -3102,11 +3097,6 @@ __device__ __forceinline__ void spec_chunk_types_v(const KArgs &a, uint32_t B, u
         *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
     }
     __builtin_amdgcn_wave_barrier();
-#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 5
-    if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0) && lane == 0)
-        a.spec_t16[p0] = 0;
-    return;
-#endif
     if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0))
         spec_replay<CH>(a, B, c0, c1, s0, lane, st, lbins);
 }
@@ -3313,10 +3303,6 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
             lists = K <= SPEC_KMAX && __ballot(clash) == 0ull;
         }
     }
-#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 1
-    if (lists)
-        return;
-#endif
     // the lists' blocks without a listed chunk (block 0 also walks the final
     // state) leave before the table fill: most of the grid, block-uniform
     const uint32_t nl = lists ? a.spec_cwl[0] : 0u;
@@ -3342,11 +3328,7 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 spec_flag_full(meta);
             }
         }
-#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 2
-        for (uint64_t k = wid; k < 0u; k += W) {
-#else
         for (uint64_t k = wid; k < nl; k += W) {
-#endif
             const uint64_t c = a.spec_cwl[1 + k], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
             // the chunk's types and the previous burst's groups in one round trip
             constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
@@ -3364,11 +3346,6 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 }
                 continue;
             }
-#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 3
-            if (lane == 0)
-                done[c] = v[0].x + s0;
-            continue;
-#endif
             if (vec)
                 spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr, v);
             else
@@ -3377,9 +3354,6 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
             if (lane == 0)
                 done[c] = 1;
         }
-#if defined(LOCAL_LDIAG) && LOCAL_LDIAG == 4
-        return;
-#endif
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
             if (s_bins[k])
