@@ -1811,25 +1811,13 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     __shared__ uint32_t s_mx; // SPEC_MX bits of this block
 
     const uint32_t tid = threadIdx.x;
-    if (tid < 64)
-        s_sf[tid] = 0;
-    if (tid == 0)
-        s_mx = 0;
-    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
-        s_t[k] = a.ttab[k];
-    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
-        s_reta[k] = a.reta[k];
-    const bool count = a.bins != nullptr;
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
-            s_bins[k] = 0;
-    __syncthreads();
-
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     u32x4 *tile = s_tile[wv];
     const uint32_t wstep = gridDim.x * CT_WAVES;
     const uint32_t t0 = blockIdx.x * CT_WAVES + wv;
     const uint32_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
+    // the first offsets, then the first two frame tiles, in flight while the
+    // tables are copied to LDS
     CsOff off{0, 0, 0, 0};
     if (a.offsets) {
 #pragma unroll
@@ -1844,9 +1832,22 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
                 off.o2 = o;
         }
     }
+    if (tid < 64)
+        s_sf[tid] = 0;
+    if (tid == 0)
+        s_mx = 0;
+    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
+        s_t[k] = a.ttab[k];
     u32x4 r[2][4];
     cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
     cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
+    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+            s_bins[k] = 0;
+    __syncthreads();
     CdLane sb;
     sb.ptf = sb.h = sb.e = sb.rx = 0;
     sb.q0 = sb.q1 = sb.q2 = sb.q3 = 0;
