@@ -3312,6 +3312,21 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     uint32_t tw = 1u, pq0 = 0u, pq1 = 0u;
     if (!lists)
         spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
+    // lists: the wave's first listed chunk -- its types and the burst before
+    // it -- in flight during the table fill
+    constexpr uint32_t LR = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
+    const bool lvec = (B & 7u) == 0;
+    u32x4 lv[LR];
+    uint32_t lq0 = 0u, lq1 = 0u;
+    uint64_t lc = 0;
+    if (lists && wid < nl) {
+        lc = a.spec_cwl[1 + wid];
+        const uint64_t c0 = lc * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+        if (lvec)
+            spec_chunk_load<CH>(a, B, c0, c1, lane, lv);
+        if (lc > 0)
+            spec_group_regs(a.spec_t16, (c0 - 1) * B, B, lane, lq0, lq1);
+    }
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
     if (lists)
@@ -3330,17 +3345,20 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
             }
         }
         for (uint64_t k = wid; k < nl; k += W) {
-            const uint64_t c = a.spec_cwl[1 + k], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-            // the chunk's types and the previous burst's groups in one round trip
-            constexpr uint32_t R = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
-            u32x4 v[R];
-            const bool vec = (B & 7u) == 0;
-            if (vec)
-                spec_chunk_load<CH>(a, B, c0, c1, lane, v);
-            uint32_t s0 = s_in, q0 = 0, q1 = 0;
-            if (c > 0)
-                spec_group_regs(a.spec_t16, (c0 - 1) * B, B, lane, q0, q1);
-            if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, q0, q1)) {
+            if (k != wid) { // the chunk's types and the previous burst's groups in one round trip
+                lc = a.spec_cwl[1 + k];
+                const uint64_t d0 = lc * CH, d1 = d0 + CH < nb ? d0 + CH : nb;
+                if (lvec)
+                    spec_chunk_load<CH>(a, B, d0, d1, lane, lv);
+                lq0 = lq1 = 0u;
+                if (lc > 0)
+                    spec_group_regs(a.spec_t16, (d0 - 1) * B, B, lane, lq0, lq1);
+            }
+            const uint64_t c = lc, c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
+            const bool vec = lvec;
+            const u32x4(&v)[LR] = lv;
+            uint32_t s0 = s_in;
+            if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, lq0, lq1)) {
                 if (lane == 0) { // left to the full passes (done[] of the others is not read)
                     done[c] = 0;
                     spec_flag_full(meta);
