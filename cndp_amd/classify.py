@@ -130,6 +130,11 @@ class Classifier:
         N.check(self._L.cndp_gpu_classify(self.h, ctypes.byref(b), stream or None), "cndp_gpu_classify")
         return out
 
+    def stream_release(self, stream: int) -> None:
+        """cndp_gpu_stream_release: call before destroying a HIP stream given to
+        classify (torch's pooled streams are never destroyed)."""
+        N.check(self._L.cndp_gpu_stream_release(self.h, stream or None), "cndp_gpu_stream_release")
+
     @staticmethod
     def _hptr(x):
         """Address of a host buffer (numpy array or CPU torch tensor)."""

@@ -3810,6 +3810,7 @@ struct cndp_gpu_ctx {
     hipEvent_t ev_scratch;
     hipStream_t scratch_stream;
     int scratch_used;
+    int scratch_armed;    // ev_scratch already recorded (cndp_gpu_stream_release)
     // host regions registered through this context (zero-copy mbuf queues),
     // each holding `refs` references on the process-wide registration
     struct {
@@ -3911,10 +3912,15 @@ static int set_device(int dev)
 // So a stream given to a call that used the scratch must outlive the next
 // call on another stream (cndp_gpu.h); the library's own streams (node
 // queues, the host path's) clear the context's record when they go.
+// A caller that destroys such a stream first hands it back with
+// cndp_gpu_stream_release, which records the event on it there and then
+// (scratch_armed): the next call waits on that record instead of touching the
+// stream.
 static int scratch_acquire(cndp_gpu_ctx_t *c, hipStream_t s)
 {
-    if (c->scratch_used && s != c->scratch_stream) {
-        HIP_TRY(hipEventRecord(c->ev_scratch, c->scratch_stream));
+    if (c->scratch_used && (c->scratch_armed || s != c->scratch_stream)) {
+        if (!c->scratch_armed)
+            HIP_TRY(hipEventRecord(c->ev_scratch, c->scratch_stream));
         HIP_TRY(hipStreamWaitEvent(s, c->ev_scratch, 0));
     }
     return 0;
@@ -3923,6 +3929,22 @@ static int scratch_release(cndp_gpu_ctx_t *c, hipStream_t s)
 {
     c->scratch_stream = s;
     c->scratch_used = 1;
+    c->scratch_armed = 0;
+    return 0;
+}
+
+extern "C" int cndp_gpu_stream_release(cndp_gpu_ctx_t *c, void *stream)
+{
+    if (!c)
+        return -EINVAL;
+    if (!c->scratch_used || c->scratch_armed || c->scratch_stream != (hipStream_t)stream)
+        return 0;
+    int r;
+    if ((r = set_device(c->dev)))
+        return r;
+    HIP_TRY(hipEventRecord(c->ev_scratch, c->scratch_stream));
+    c->scratch_armed = 1;
+    c->scratch_stream = nullptr;
     return 0;
 }
 
@@ -4109,7 +4131,9 @@ extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
     t->lk_dbuf = nullptr;
     for (uint32_t k = 0; k < t->n_old; k++)
         hipFree(t->dev_old[k]);
-    t->n_old = 0;
+    free(t->dev_old);
+    t->dev_old = nullptr;
+    t->n_old = t->cap_old = 0;
     hipSetDevice(cur);
     t->dev_dir16 = t->dev_pages = nullptr;
     t->dev_cap_pages = 0;
@@ -4198,20 +4222,29 @@ static int dir16_update(struct cndp_tbl *t, uint32_t k0, uint32_t k1)
     return 0;
 }
 
-// a device buffer being replaced: lookups that took its address under
-// dev_lock may launch after we return, so it is kept until the mirror is
-// freed (the oldest goes once CNDP_DEV_OLD are held: hipFree synchronizes
-// the device, and no caller holds an address across that many replacements)
+// a device buffer being replaced (caller holds dev_lock): a launch that took
+// its address under dev_lock (tbl_acquire) may still be on its way, so it is
+// kept while any view of the table is held.  Once none is, every kept buffer
+// goes: no thread can take a new view without dev_lock, and hipFree waits for
+// the device, so the launches already enqueued have finished reading them.
 static int tbl_dev_retire(struct cndp_tbl *t, void *p)
 {
     if (!p)
         return 0;
-    if (t->n_old == CNDP_DEV_OLD) {
-        HIP_TRY(hipFree(t->dev_old[0]));
-        memmove(t->dev_old, t->dev_old + 1, (CNDP_DEV_OLD - 1) * sizeof(void *));
-        t->n_old--;
+    if (t->n_old == t->cap_old) {
+        const uint32_t cap = t->cap_old ? 2 * t->cap_old : 8;
+        void **n = (void **)realloc(t->dev_old, cap * sizeof(void *));
+        if (!n)
+            return -ENOMEM;
+        t->dev_old = n;
+        t->cap_old = cap;
     }
     t->dev_old[t->n_old++] = p;
+    if (__atomic_load_n(&t->views, __ATOMIC_ACQUIRE) == 0) {
+        for (uint32_t k = 0; k < t->n_old; k++)
+            HIP_TRY(hipFree(t->dev_old[k]));
+        t->n_old = 0;
+    }
     return 0;
 }
 
@@ -4324,16 +4357,34 @@ static inline uint32_t blocks_for(uint64_t n, uint32_t threads)
     return (uint32_t)((n + threads - 1) / threads);
 }
 
-// the device tables one lookup launch reads (taken under dev_lock; the
-// buffers stay valid after it: replaced ones are kept until the mirror is
-// freed, tbl_dev_retire)
+// the device tables one launch reads, taken under dev_lock right after the
+// sync (tbl_view inside a locked section, or tbl_acquire, which also holds a
+// view so the buffers outlive a replacement until tbl_release)
 struct TblView {
     const void *t24, *t8;
     uint32_t nh_sz;
+    const uint32_t *d16, *pages; // the /16 directory (4-B DIR-24-8 images), or null
 };
 static inline TblView tbl_view(const struct cndp_tbl *t)
 {
-    return TblView{t->dev_tbl24, t->dev_tbl8, t->nh_sz};
+    const bool dir = t->dev_dir16 && t->dev_pages;
+    return TblView{t->dev_tbl24, t->dev_tbl8, t->nh_sz, dir ? (const uint32_t *)t->dev_dir16 : nullptr,
+                   dir ? (const uint32_t *)t->dev_pages : nullptr};
+}
+static int tbl_acquire(struct cndp_tbl *t, hipStream_t s, TblView *v)
+{
+    pthread_mutex_lock(&t->dev_lock);
+    const int r = tbl_dev_sync_locked(t, s);
+    if (!r) {
+        *v = tbl_view(t);
+        __atomic_add_fetch(&t->views, 1u, __ATOMIC_RELAXED);
+    }
+    pthread_mutex_unlock(&t->dev_lock);
+    return r;
+}
+static inline void tbl_release(struct cndp_tbl *t)
+{
+    __atomic_sub_fetch(&t->views, 1u, __ATOMIC_RELEASE);
 }
 static int tbl_lookup4_launch(TblView v, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s,
                               LkDone d = LkDone{nullptr, nullptr, 0});
@@ -4343,21 +4394,25 @@ static int tbl_lookup6_launch(TblView v, const uint8_t *ips, uint64_t *nh, uint3
 extern "C" int cndp_tbl_lookup4_dev(struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh,
                                     uint32_t n, void *stream)
 {
-    pthread_mutex_lock(&t->dev_lock);
-    const int r = tbl_dev_sync_locked(t, stream);
-    const TblView v = tbl_view(t);
-    pthread_mutex_unlock(&t->dev_lock);
-    return r ? r : tbl_lookup4_launch(v, ips, nh, n, (hipStream_t)stream);
+    TblView v{};
+    int r = tbl_acquire(t, (hipStream_t)stream, &v);
+    if (r)
+        return r;
+    r = tbl_lookup4_launch(v, ips, nh, n, (hipStream_t)stream);
+    tbl_release(t);
+    return r;
 }
 
 extern "C" int cndp_tbl_lookup6_dev(struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n,
                                     void *stream)
 {
-    pthread_mutex_lock(&t->dev_lock);
-    const int r = tbl_dev_sync_locked(t, stream);
-    const TblView v = tbl_view(t);
-    pthread_mutex_unlock(&t->dev_lock);
-    return r ? r : tbl_lookup6_launch(v, ips, nh, n, (hipStream_t)stream);
+    TblView v{};
+    int r = tbl_acquire(t, (hipStream_t)stream, &v);
+    if (r)
+        return r;
+    r = tbl_lookup6_launch(v, ips, nh, n, (hipStream_t)stream);
+    tbl_release(t);
+    return r;
 }
 
 static int tbl_lookup4_launch(TblView v, const uint32_t *ips, uint64_t *nh, uint32_t n, hipStream_t s,
@@ -4504,12 +4559,9 @@ static int lookup_mapped(struct cndp_tbl *t, const uint8_t *ips, uint32_t key_sz
     int r = lk_slot_init(sl);
     hipStream_t s = (hipStream_t)sl->stream;
     TblView v{};
-    if (!r) {
-        pthread_mutex_lock(&t->dev_lock);
-        r = tbl_dev_sync_locked(t, s); // waits for its copies when the image was dirty
-        v = tbl_view(t);
-        pthread_mutex_unlock(&t->dev_lock);
-    }
+    bool held = false;
+    if (!r) // waits for its copies when the image was dirty
+        held = (r = tbl_acquire(t, s, &v)) == 0;
     if (!r) {
         uint8_t *hk = sl->host, *hn = sl->host + (size_t)LK_MAPPED_MAX * key_sz;
         memcpy(hk, ips, (size_t)n * key_sz);
@@ -4518,11 +4570,15 @@ static int lookup_mapped(struct cndp_tbl *t, const uint8_t *ips, uint32_t key_sz
         sl->seq = sl->seq + 1u ? sl->seq + 1u : 1u; // never the flag's initial 0
         const LkDone d{sl->ticket, (uint32_t *)(sl->hdev + LK_FLAG_OFF), sl->seq};
         r = v6 ? tbl_lookup6_launch(v, dk, dn, n, s, d) : tbl_lookup4_launch(v, (const uint32_t *)dk, dn, n, s, d);
+        tbl_release(t);
+        held = false;
         if (!r)
             r = lk_wait((const uint32_t *)(sl->host + LK_FLAG_OFF), sl->seq, s);
         if (!r)
             memcpy(nh, hn, (size_t)n * 8);
     }
+    if (held)
+        tbl_release(t);
     lk_slot_give(sl);
     return r;
 }
@@ -4679,6 +4735,9 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
 static int classify_l3(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, hipStream_t s, uint16_t *rw_tx,
                        bool *fused);
 
+static int classify_launch(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream, uint16_t *rw_tx,
+                           bool *fused, const TblView *v4, const TblView *v6);
+
 // rw_tx != nullptr asks for ip4_rewrite fused into the wave-tile kernel
 // (256-packet bursts); *fused says whether that kernel ran
 static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream, uint16_t *rw_tx,
@@ -4690,12 +4749,28 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
     r = set_device(c->dev);
     if (r)
         return r;
-    if (b->mode != CNDP_MODE_HASH && (r = cndp_tbl_dev_sync(&c->fib4->t, stream)))
+    // the tables this call's launches read, held until they are enqueued
+    struct cndp_tbl *t4 = b->mode != CNDP_MODE_HASH ? &c->fib4->t : nullptr;
+    struct cndp_tbl *t6 = b->mode == CNDP_MODE_CNET ? &c->fib6->t : nullptr;
+    TblView v4{}, v6{};
+    if (t4 && (r = tbl_acquire(t4, (hipStream_t)stream, &v4)))
         return r;
-    if (b->mode == CNDP_MODE_CNET && (r = cndp_tbl_dev_sync(&c->fib6->t, stream)))
+    if (t6 && (r = tbl_acquire(t6, (hipStream_t)stream, &v6))) {
+        tbl_release(t4);
         return r;
-    if (b->n == 0)
-        return 0;
+    }
+    r = b->n ? classify_launch(c, b, stream, rw_tx, fused, t4 ? &v4 : nullptr, t6 ? &v6 : nullptr) : 0;
+    if (t4)
+        tbl_release(t4);
+    if (t6)
+        tbl_release(t6);
+    return r;
+}
+
+static int classify_launch(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream, uint16_t *rw_tx,
+                           bool *fused, const TblView *v4, const TblView *v6)
+{
+    int r;
     KArgs a;
     memset(&a, 0, sizeof(a));
     a.slab = (const uint8_t *)b->slab;
@@ -4706,17 +4781,17 @@ static int classify_impl(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *st
     a.n = b->n;
     a.buf_len = b->buf_len;
     a.reta_mask = c->reta_size - 1;
-    if (c->fib4) {
-        a.tbl24 = (const uint32_t *)c->fib4->t.dev_tbl24;
-        a.tbl8 = (const uint32_t *)c->fib4->t.dev_tbl8;
-        if (c->tune_dir16 && c->fib4->t.dev_dir16 && c->fib4->t.dev_pages) {
-            a.dir16 = (const uint32_t *)c->fib4->t.dev_dir16;
-            a.pages = (const uint32_t *)c->fib4->t.dev_pages;
+    if (v4) {
+        a.tbl24 = (const uint32_t *)v4->t24;
+        a.tbl8 = (const uint32_t *)v4->t8;
+        if (c->tune_dir16 && v4->d16) {
+            a.dir16 = v4->d16;
+            a.pages = v4->pages;
         }
     }
-    if (c->fib6) {
-        a.tbl24_6 = (const uint32_t *)c->fib6->t.dev_tbl24;
-        a.tbl8_6 = (const uint32_t *)c->fib6->t.dev_tbl8;
+    if (v6) {
+        a.tbl24_6 = (const uint32_t *)v6->t24;
+        a.tbl8_6 = (const uint32_t *)v6->t8;
     }
     a.ttab = c->d_ttab;
     a.reta = c->d_reta;
@@ -6355,20 +6430,20 @@ static MqSlot *mq_open_slot(cndp_gpu_mq_t *q)
     return sl;
 }
 
-static MqTables mq_tables(cndp_gpu_ctx_t *c, uint32_t buf_len)
+// the node kernels' tables, from views taken with tbl_acquire (v6 may be null)
+static MqTables mq_tables(const cndp_gpu_ctx_t *c, const TblView &v4, const TblView *v6, uint32_t buf_len)
 {
     MqTables t;
     memset(&t, 0, sizeof(t));
-    struct cndp_tbl *t4 = &c->fib4->t;
-    t.t24 = (const uint32_t *)t4->dev_tbl24;
-    t.t8 = (const uint32_t *)t4->dev_tbl8;
-    if (c->tune_dir16 && t4->dev_dir16 && t4->dev_pages) {
-        t.d16 = (const uint32_t *)t4->dev_dir16;
-        t.pages = (const uint32_t *)t4->dev_pages;
+    t.t24 = (const uint32_t *)v4.t24;
+    t.t8 = (const uint32_t *)v4.t8;
+    if (c->tune_dir16 && v4.d16) {
+        t.d16 = v4.d16;
+        t.pages = v4.pages;
     }
-    if (c->fib6) {
-        t.t24_6 = (const uint32_t *)c->fib6->t.dev_tbl24;
-        t.t8_6 = (const uint32_t *)c->fib6->t.dev_tbl8;
+    if (v6) {
+        t.t24_6 = (const uint32_t *)v6->t24;
+        t.t8_6 = (const uint32_t *)v6->t8;
     }
     t.buf_len = buf_len;
     return t;
@@ -6421,9 +6496,10 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         a.rw = c->d_rw_tbl;
         hipLaunchKernelGGL(k_mq_ip4_rewrite, dim3(g), dim3(MQ_TPB), 0, s, a);
     } else if (!cnet) {
-        if ((r = cndp_tbl_dev_sync(&c->fib4->t, s)))
+        TblView v4{};
+        if ((r = tbl_acquire(&c->fib4->t, s, &v4)))
             return r;
-        a.tb = mq_tables(c, 0);
+        a.tb = mq_tables(c, v4, nullptr, 0);
         if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // the frames in conf.umem's region
             for (int k = 0; k < q->nrg; k++)
                 if (q->rg[k].host == (const uint8_t *)q->conf.umem) {
@@ -6434,6 +6510,7 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
                 }
         }
         hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
+        tbl_release(&c->fib4->t);
     } else {
         // one classify per run of equal-size graph bursts, the ptype node's
         // speculation run with that burst size, its state carried in the
@@ -6471,8 +6548,17 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         a.edge8 = D + q->d_edge;
         a.iplen = (uint32_t *)(D + q->d_ipl);
         a.win = (const u32x4 *)(D + q->d_win);
-        a.tb = mq_tables(c, sl->buf_len);
+        TblView v4{}, v6{};
+        if ((r = tbl_acquire(&c->fib4->t, s, &v4)))
+            return r;
+        if ((r = tbl_acquire(&c->fib6->t, s, &v6))) {
+            tbl_release(&c->fib4->t);
+            return r;
+        }
+        a.tb = mq_tables(c, v4, &v6, sl->buf_len);
         hipLaunchKernelGGL(k_mq_cnet_post, dim3(g), dim3(MQ_TPB), 0, s, a);
+        tbl_release(&c->fib4->t);
+        tbl_release(&c->fib6->t);
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -6489,6 +6575,12 @@ static int mq_launch(cndp_gpu_mq_t *q)
         return 0;
     const int r = mq_launch_kernels(q, sl, slot_i);
     if (r) {
+        // kernels of the batch's earlier runs may be enqueued and still read
+        // the slot's staging: let them finish before its mbufs go back; the
+        // speculation state they advanced part way restarts from 0
+        (void)hipStreamSynchronize(q->s);
+        if (q->conf.mode == CNDP_MQ_CNET)
+            q->c->spec_reset = 1;
         sl->failed = 1;
         sl->state = MQ_DONE;
         uint16_t *ed = (uint16_t *)(sl->h + q->h_edge);

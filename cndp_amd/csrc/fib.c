@@ -226,9 +226,15 @@ static int dir24_install(struct cndp_tbl *t, uint32_t p, uint32_t len, uint64_t 
         uint64_t first = p >> 8, cnt = 1ull << (24 - len);
         for (uint64_t i = first; i < first + cnt; i++) {
             uint64_t e = t24_get(t, i);
-            if (e & 1u)
-                group_free(t, e >> 1);
+            /* the entry is rewritten before its group is cleared, so a host
+             * lookup running on another thread (CNE_FIB_LOOKUP_DEFAULT takes
+             * no lock, as dir24_8.h's does not) never follows it into a
+             * zeroed group */
             ent_set(t, t->tbl24, i, nh << 1);
+            if (e & 1u) {
+                __atomic_thread_fence(__ATOMIC_RELEASE);
+                group_free(t, e >> 1);
+            }
         }
         dirty24(t, first, first + cnt);
         return 0;
@@ -244,6 +250,7 @@ static int dir24_install(struct cndp_tbl *t, uint32_t p, uint32_t len, uint64_t 
             ent_set(t, t->tbl8, base + k, e | 1u);
         dirty8(t, base, base + CNDP_TBL8_GRP);
         e = ((uint64_t)g << 1) | 1u;
+        __atomic_thread_fence(__ATOMIC_RELEASE); /* group filled before it is linked */
         t24_set(t, idx, e);
     }
     uint64_t g = e >> 1;
@@ -254,6 +261,7 @@ static int dir24_install(struct cndp_tbl *t, uint32_t p, uint32_t len, uint64_t 
     uint64_t v;
     if (group_uniform(t, g, &v)) { /* fold back, cf. dir24_8.c:189-247 */
         t24_set(t, idx, v & ~1ull);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
         group_free(t, g);
     }
     return 0;
@@ -267,8 +275,10 @@ static int trie_install(struct cndp_tbl *t, u128 p, uint32_t len, uint64_t nh)
     if (len <= 24) {
         uint64_t first = (uint64_t)(p >> 104), cnt = 1ull << (24 - len);
         for (uint64_t i = first; i < first + cnt; i++) {
-            trie_free_chain(t, t24_get(t, i));
-            ent_set(t, t->tbl24, i, nh << 1);
+            const uint64_t old = t24_get(t, i);
+            ent_set(t, t->tbl24, i, nh << 1); /* unlinked before it is freed */
+            __atomic_thread_fence(__ATOMIC_RELEASE);
+            trie_free_chain(t, old);
         }
         dirty24(t, first, first + cnt);
         return 0;
@@ -290,6 +300,7 @@ static int trie_install(struct cndp_tbl *t, u128 p, uint32_t len, uint64_t nh)
                 ent_set(t, t->tbl8, base + q, e);
             dirty8(t, base, base + CNDP_TBL8_GRP);
             e = ((uint64_t)g << 1) | 1u;
+            __atomic_thread_fence(__ATOMIC_RELEASE);
             if (ent_in8)
                 t8_set(t, ent, e);
             else
@@ -303,8 +314,10 @@ static int trie_install(struct cndp_tbl *t, u128 p, uint32_t len, uint64_t nh)
         if (rem <= 8) {
             uint64_t first = gbase + byte_at(p, k), cnt = 1ull << (8 - rem);
             for (uint64_t i = first; i < first + cnt; i++) {
-                trie_free_chain(t, t8_get(t, i));
+                const uint64_t old = t8_get(t, i);
                 ent_set(t, t->tbl8, i, nh << 1);
+                __atomic_thread_fence(__ATOMIC_RELEASE);
+                trie_free_chain(t, old);
             }
             dirty8(t, first, first + cnt);
             break;
@@ -318,11 +331,12 @@ static int trie_install(struct cndp_tbl *t, u128 p, uint32_t len, uint64_t nh)
         uint64_t v;
         if (!(e & 1u) || !group_uniform(t, e >> 1, &v))
             break;
-        group_free(t, e >> 1);
         if (in_tbl8[d])
             t8_set(t, path[d], v);
         else
             t24_set(t, path[d], v);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        group_free(t, e >> 1);
     }
     return 0;
 }
@@ -450,6 +464,96 @@ static int paint(struct cndp_tbl *t, const struct cndp_rib *rib, uint32_t width,
     free(h.lo);
     free(h.hi);
     return r;
+}
+
+/* ------------------------------------------------------------------------ */
+/* synchronous host lookups (the reference's CNE_FIB_LOOKUP_DEFAULT)         */
+/* ------------------------------------------------------------------------ */
+/* cne_fib.c:86 binds every DIR-24-8 FIB to dir24_8_get_lookup_fn(DEFAULT):
+ * a scalar loop over the table image that prefetches the tbl24 entry of the
+ * key `pf` positions ahead (dir24_8.h:118-148; 5/6/15/12 for 1/2/4/8-B
+ * entries).  cne_fib6.c:92 does the same with trie.h:119-138.  These read the
+ * host image that fib.c paints and the HBM mirror copies, so the answers are
+ * the GPU lookup's by construction.  Like the reference's they take no lock:
+ * the installers above link a group only after filling it and clear it only
+ * after unlinking it. */
+#define HOST_LK4(sfx, type, pf)                                                            \
+    static void host_lookup4_##sfx(const struct cndp_tbl *t, const uint32_t *ips,         \
+                                   uint64_t *nh, uint32_t n)                              \
+    {                                                                                      \
+        const type *t24 = (const type *)(const void *)t->tbl24;                            \
+        const type *t8 = (const type *)(const void *)t->tbl8;                              \
+        const uint32_t ahead = n < (pf) ? n : (pf);                                        \
+        uint32_t i;                                                                        \
+        for (i = 0; i < ahead; i++)                                                        \
+            __builtin_prefetch(&t24[ips[i] >> 8]);                                         \
+        for (i = 0; i < n; i++) {                                                          \
+            if (i + ahead < n)                                                             \
+                __builtin_prefetch(&t24[ips[i + ahead] >> 8]);                             \
+            uint64_t e = t24[ips[i] >> 8];                                                 \
+            if (__builtin_expect((e & 1u) != 0, 0))                                        \
+                e = t8[(uint8_t)ips[i] + (e >> 1) * CNDP_TBL8_GRP];                        \
+            nh[i] = e >> 1;                                                                \
+        }                                                                                  \
+    }
+HOST_LK4(1b, uint8_t, 5)
+HOST_LK4(2b, uint16_t, 6)
+HOST_LK4(4b, uint32_t, 15)
+HOST_LK4(8b, uint64_t, 12)
+
+#define HOST_LK6(sfx, type)                                                                \
+    static void host_lookup6_##sfx(const struct cndp_tbl *t, const uint8_t *ips,          \
+                                   uint64_t *nh, uint32_t n)                              \
+    {                                                                                      \
+        const type *t24 = (const type *)(const void *)t->tbl24;                            \
+        const type *t8 = (const type *)(const void *)t->tbl8;                              \
+        for (uint32_t i = 0; i < n; i++) {                                                 \
+            const uint8_t *a = ips + (size_t)i * 16;                                       \
+            uint64_t e = t24[(uint32_t)a[0] << 16 | (uint32_t)a[1] << 8 | a[2]];           \
+            for (uint32_t j = 3; (e & 1u) && j < 16; j++)                                  \
+                e = t8[a[j] + (e >> 1) * CNDP_TBL8_GRP];                                   \
+            nh[i] = e >> 1;                                                                \
+        }                                                                                  \
+    }
+HOST_LK6(1b, uint8_t)
+HOST_LK6(2b, uint16_t)
+HOST_LK6(4b, uint32_t)
+HOST_LK6(8b, uint64_t)
+
+static void host_lookup4(const struct cndp_tbl *t, const uint32_t *ips, uint64_t *nh, uint32_t n)
+{
+    switch (t->nh_sz) {
+    case 0:
+        host_lookup4_1b(t, ips, nh, n);
+        break;
+    case 1:
+        host_lookup4_2b(t, ips, nh, n);
+        break;
+    case 2:
+        host_lookup4_4b(t, ips, nh, n);
+        break;
+    default:
+        host_lookup4_8b(t, ips, nh, n);
+        break;
+    }
+}
+
+static void host_lookup6(const struct cndp_tbl *t, const uint8_t *ips, uint64_t *nh, uint32_t n)
+{
+    switch (t->nh_sz) {
+    case 0:
+        host_lookup6_1b(t, ips, nh, n);
+        break;
+    case 1:
+        host_lookup6_2b(t, ips, nh, n);
+        break;
+    case 2:
+        host_lookup6_4b(t, ips, nh, n);
+        break;
+    default:
+        host_lookup6_8b(t, ips, nh, n);
+        break;
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -620,15 +724,36 @@ int cne_fib_lookup_bulk(struct cne_fib *fib, uint32_t *ips, uint64_t *next_hops,
         return -EINVAL;
     if (n == 0)
         return 0;
-    return cndp_tbl_lookup4_host(&fib->t, ips, next_hops, (uint32_t)n);
+    if (fib->lookup_type == CNDP_FIB_LOOKUP_GPU)
+        return cndp_tbl_lookup4_host(&fib->t, ips, next_hops, (uint32_t)n);
+    if (fib->type == CNE_FIB_DUMMY) {
+        /* cne_fib.c:32-46 walks the RIB; the image painted from it gives the
+         * same answers.  Its group pool grows (realloc) on add, so this one
+         * reads under the table lock */
+        pthread_mutex_lock(&fib->t.dev_lock);
+        host_lookup4(&fib->t, ips, next_hops, (uint32_t)n);
+        pthread_mutex_unlock(&fib->t.dev_lock);
+        return 0;
+    }
+    host_lookup4(&fib->t, ips, next_hops, (uint32_t)n);
+    return 0;
 }
 
 void *cne_fib_get_dp(struct cne_fib *fib) { return fib ? &fib->t : NULL; }
 
 struct cne_rib *cne_fib_get_rib(struct cne_fib *fib) { return fib ? (struct cne_rib *)&fib->rib : NULL; }
 
+/* cne_fib.c:206-221: only DIR-24-8 FIBs select a lookup.  Every scalar or
+ * vector selector binds the host loop above (this build has no AVX-512 form;
+ * the reference's DEFAULT also falls back to the scalar loop without it).
+ * CNE_FIB_LOOKUP_GPU (an extension; DUMMY FIBs accept it too) sends every
+ * cne_fib_lookup_bulk to the device mirror instead. */
 int cne_fib_select_lookup(struct cne_fib *fib, enum cne_fib_lookup_type type)
 {
+    if (fib && fib->type == CNE_FIB_DUMMY && (int)type == CNDP_FIB_LOOKUP_GPU) {
+        fib->lookup_type = CNDP_FIB_LOOKUP_GPU;
+        return 0;
+    }
     if (!fib || fib->type != CNE_FIB_DIR24_8)
         return -EINVAL;
     switch (type) {
@@ -857,7 +982,16 @@ int cne_fib6_lookup_bulk(struct cne_fib6 *fib, uint8_t ips[][IPV6_ADDR_LEN], uin
         return -EINVAL;
     if (n == 0)
         return 0;
-    return cndp_tbl_lookup6_host(&fib->t, &ips[0][0], next_hops, (uint32_t)n);
+    if (fib->lookup_type == CNDP_FIB_LOOKUP_GPU)
+        return cndp_tbl_lookup6_host(&fib->t, &ips[0][0], next_hops, (uint32_t)n);
+    if (fib->type == CNE_FIB_DUMMY) { /* cne_fib6.c:34-48, see cne_fib_lookup_bulk */
+        pthread_mutex_lock(&fib->t.dev_lock);
+        host_lookup6(&fib->t, &ips[0][0], next_hops, (uint32_t)n);
+        pthread_mutex_unlock(&fib->t.dev_lock);
+        return 0;
+    }
+    host_lookup6(&fib->t, &ips[0][0], next_hops, (uint32_t)n);
+    return 0;
 }
 
 void *cne_fib6_get_dp(struct cne_fib6 *fib) { return fib ? &fib->t : NULL; }
@@ -868,8 +1002,13 @@ struct cne_rib6 *cne_fib6_get_rib(struct cne_fib6 *fib)
     return fib ? (struct cne_rib6 *)&fib->rib : NULL;
 }
 
+/* cne_fib6.c:208-223, as cne_fib_select_lookup */
 int cne_fib6_select_lookup(struct cne_fib6 *fib, enum cne_fib_lookup_type type)
 {
+    if (fib && fib->type == CNE_FIB_DUMMY && (int)type == CNDP_FIB_LOOKUP_GPU) {
+        fib->lookup_type = CNDP_FIB_LOOKUP_GPU;
+        return 0;
+    }
     if (!fib || fib->type != CNE_FIB_TRIE)
         return -EINVAL;
     switch (type) {

@@ -26,7 +26,6 @@ extern "C" {
 #define CNDP_TBL24_ENT (1u << 24)
 #define CNDP_TBL8_GRP 256u
 #define CNDP_LK_SLOTS 16u   /* concurrent host-array lookups per table */
-#define CNDP_DEV_OLD 8u
 
 struct cndp_tbl {
     uint32_t nh_sz;     /* log2(entry bytes) */
@@ -76,10 +75,12 @@ struct cndp_tbl {
     } lk[CNDP_LK_SLOTS];
     void *lk_stream;        /* hipStream_t of large lookups (DMA path, under dev_lock) */
     uint8_t *lk_dbuf;       /* device scratch for large lookups */
-    /* device buffers replaced while lookups on other threads may still hold
-     * their address (freed with the mirror) */
-    void *dev_old[CNDP_DEV_OLD];
-    uint32_t n_old;
+    /* device buffers replaced while launches on other threads may still hold
+     * their address: freed once no launch holds a view of the table (views,
+     * taken and counted under dev_lock, dropped after the launch) */
+    void **dev_old;
+    uint32_t n_old, cap_old;
+    uint32_t views;
 };
 
 struct cne_fib {

@@ -1,8 +1,12 @@
 """Python mirror of CNDP's FIB API (lib/usr/clib/fib/cne_fib.h, cne_fib6.h)
 over libcndp_gpu.so.  Same operation names, argument meaning and return
-codes (0 / negative errno); lookups run on the GPU.
+codes (0 / negative errno).  lookup_bulk answers from the host table image
+(CNE_FIB_LOOKUP_DEFAULT, as cne_fib.c:86 binds it) or, with
+lookup=CNE_FIB_LOOKUP_GPU, from the HBM mirror; batch classify always reads
+the mirror.
 
-    Fib(name, type=CNE_FIB_DIR24_8, default_nh, max_routes, nh_sz, num_tbl8)
+    Fib(name, type=CNE_FIB_DIR24_8, default_nh, max_routes, nh_sz, num_tbl8,
+        lookup=None)    lookup: a cne_fib_lookup_type passed to select_lookup
         .add(ip, depth, nh) -> int        cne_fib_add      (cne_fib.h:129)
         .delete(ip, depth) -> int         cne_fib_delete   (cne_fib.h:143)
         .lookup_bulk(ips) -> ndarray u64  cne_fib_lookup_bulk (cne_fib.h:162)
@@ -32,7 +36,7 @@ class Fib:
     """IPv4 FIB (DIR-24-8 or DUMMY)."""
 
     def __init__(self, name="fib", type=N.CNE_FIB_DIR24_8, default_nh=0, max_routes=1024,
-                 nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=256):
+                 nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=256, lookup=None):
         self._L = N.lib()
         conf = _conf(type, default_nh, max_routes, nh_sz, num_tbl8)
         self.h = self._L.cne_fib_create(name.encode() if name is not None else None,
@@ -41,6 +45,8 @@ class Fib:
             raise ValueError("cne_fib_create rejected the configuration")
         self.type = type
         self.default_nh = default_nh
+        if lookup is not None:
+            N.check(self.select_lookup(lookup), "cne_fib_select_lookup")
 
     @staticmethod
     def create_raw(name, conf: "N.FibConf"):
@@ -102,7 +108,7 @@ class Fib6:
     """IPv6 FIB (trie or DUMMY)."""
 
     def __init__(self, name="fib6", type=N.CNE_FIB_TRIE, default_nh=0, max_routes=1024,
-                 nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15):
+                 nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15, lookup=None):
         self._L = N.lib()
         conf = _conf(type, default_nh, max_routes, nh_sz, num_tbl8)
         self.h = self._L.cne_fib6_create(name.encode() if name is not None else None,
@@ -111,6 +117,8 @@ class Fib6:
             raise ValueError("cne_fib6_create rejected the configuration")
         self.type = type
         self.default_nh = default_nh
+        if lookup is not None:
+            N.check(self.select_lookup(lookup), "cne_fib6_select_lookup")
 
     @staticmethod
     def create_raw(name, conf):

@@ -160,6 +160,7 @@ def lib():
         "cndp_gpu_set_rss": (c_int, [c_void_p, c_char_p, c_uint32, c_void_p, c_uint32, c_uint32]),
         "cndp_gpu_set_fib": (c_int, [c_void_p, c_void_p, c_void_p]),
         "cndp_gpu_classify": (c_int, [c_void_p, POINTER(Batch), c_void_p]),
+        "cndp_gpu_stream_release": (c_int, [c_void_p, c_void_p]),
         "cndp_gpu_classify_host": (c_int, [c_void_p, POINTER(Batch)]),
         "cndp_gpu_host_register": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_void_p)]),
         "cndp_gpu_host_unregister": (c_int, [c_void_p, c_void_p]),

@@ -5,16 +5,27 @@
  * error behaviour of the reference call it replaces, so code written against
  * CNDP's lib/usr/clib/fib/cne_fib.h and cne_fib6.h builds and links against
  * this library unchanged.  The control plane (RIB + table build) runs on the
- * host; every lookup runs on the MI355X (the tables are mirrored to HBM and
- * kept in sync incrementally).  There is no CPU lookup path: without a usable
- * GPU, cne_fib_lookup_bulk / cne_fib6_lookup_bulk return -ENODEV.
+ * host and paints one table image in the reference's entry encoding; the
+ * image is mirrored to HBM and kept in sync incrementally, and every batch
+ * kernel (cndp_gpu.h, the graph nodes) reads the mirror.
+ *
+ * cne_fib_lookup_bulk / cne_fib6_lookup_bulk answer as the selected lookup
+ * says, as in the reference (cne_fib.c:86, cne_fib_select_lookup):
+ *   CNE_FIB_LOOKUP_DEFAULT and every scalar / vector selector -- synchronously
+ *     on the calling thread from the host image (the prefetching loop of
+ *     dir24_8.h:118-148 / trie.h:119-138).  This is what a FIB is created
+ *     with, so cnet's per-packet callers (ip4_forward, ip4_output, ARP, ND,
+ *     route) keep their CPU rate when this library replaces CNDP's FIB;
+ *   CNE_FIB_LOOKUP_GPU (extension, also accepted by DUMMY FIBs) -- a launch
+ *     on the device mirror per call; without a usable GPU it returns -ENODEV
+ *     and fills every next hop with the FIB default.
  *
  *   reference (CNDP v25.08.0)                    this library
  *   cne_fib.h:103   cne_fib_create               same
  *   cne_fib.h:113   cne_fib_free                 same
  *   cne_fib.h:129   cne_fib_add                  same
  *   cne_fib.h:143   cne_fib_delete               same
- *   cne_fib.h:162   cne_fib_lookup_bulk          same, GPU-backed (host arrays)
+ *   cne_fib.h:162   cne_fib_lookup_bulk          same (host image, or GPU when selected)
  *   cne_fib.h:173   cne_fib_get_dp               same (host table image)
  *   cne_fib.h:183   cne_fib_get_rib              returns the build's RIB
  *   cne_fib.h:197   cne_fib_select_lookup        same (+ CNE_FIB_LOOKUP_GPU)
@@ -83,8 +94,8 @@ enum cne_fib_dir24_8_nh_sz {
 /* cne_fib.h:60 */
 enum cne_fib_trie_nh_sz { CNE_FIB_TRIE_2B = 1, CNE_FIB_TRIE_4B, CNE_FIB_TRIE_8B };
 
-/* cne_fib.h:63-73, plus CNE_FIB_LOOKUP_GPU appended (every DIR-24-8 / trie
- * selector resolves to the GPU lookup of the same table) */
+/* cne_fib.h:63-73, plus CNE_FIB_LOOKUP_GPU appended (every reference selector
+ * binds the host loop; CNE_FIB_LOOKUP_GPU the device mirror) */
 enum cne_fib_lookup_type {
     CNE_FIB_LOOKUP_DEFAULT,
     CNE_FIB_LOOKUP_DIR24_8_SCALAR_MACRO,

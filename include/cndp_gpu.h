@@ -30,7 +30,8 @@
  * one context that share its scratch (cnet mode, the bin partition) are
  * ordered across streams: a call on another stream than the previous one's
  * first waits for that stream, so a stream given to such a call must stay
- * alive until the next such call on another stream (or cndp_gpu_fini).
+ * alive until the next such call on another stream (or cndp_gpu_fini), or be
+ * handed back with cndp_gpu_stream_release before it is destroyed.
  *
  * Per-packet outputs (SoA, any may be NULL except as noted):
  *   nh[i]    u32 FIB value (l3fwd: edge<<16 | nh id; cnet: edge<<24 | idx),
@@ -109,6 +110,12 @@ int cndp_gpu_set_fib(cndp_gpu_ctx_t *ctx, struct cne_fib *fib4, struct cne_fib6 
 /* Enqueue one classify pass over a device-resident batch. */
 int cndp_gpu_classify(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *stream);
 
+/* Hand back a stream before destroying it: if the context's last
+ * scratch-sharing call ran on `stream`, the ordering point is recorded on it
+ * now, so the next call (on any stream) waits for that work without touching
+ * `stream` again.  A no-op for any other stream. */
+int cndp_gpu_stream_release(cndp_gpu_ctx_t *ctx, void *stream);
+
 /* Same over HOST buffers (an AF_XDP UMEM, socket buffers): the slab is
  * streamed into a device mirror in 64 MiB segments while earlier packet
  * chunks are classified and their results copied back (three streams), and
@@ -142,8 +149,8 @@ int cndp_gpu_l3fwd_mbufs(cndp_gpu_ctx_t *ctx, void *const *mbufs, uint32_t n, ui
  * plus the next edge of each, in submission order.  A graph's source node
  * (node/ip4_lookup_gpu.c) polls once per walk, which also launches a partly
  * filled batch when it is older than max_delay_us, or when the GPU has
- * nothing in flight and the batch holds batch / 8 mbufs or is older than
- * max_delay_us / 5.
+ * nothing in flight and the batch holds batch / 2 mbufs or is older than
+ * max_delay_us / 2.
  *
  * Frame bytes: when conf.umem names a region registered with
  * cndp_gpu_host_register (the AF_XDP UMEM / pktmbuf pool, cne_lport.h:91),

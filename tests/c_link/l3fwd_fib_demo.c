@@ -5,9 +5,11 @@
  * addresses, next hop = tx port << 48 | MAC) compiled as plain C against
  * include/cndp_fib.h and linked to libcndp_gpu.so -- the link swap of
  * INTEGRATION.md §1 -- with every answer checked against a longest-prefix
- * match over the same rules.  Exit 0: all lookups right; 77: no GPU (the
- * lookups returned -ENODEV with the default next hop filled in); 1: a wrong
- * answer.
+ * match over the same rules, first in the selection a FIB is created with
+ * (the host image, as cne_fib.c:86 binds the scalar lookup), then with
+ * CNDP_FIB_LOOKUP_GPU.  Exit 0: all lookups right; 77: the default lookups
+ * right and no GPU (the GPU lookups returned -ENODEV with the default next hop
+ * filled in); 1: a wrong answer.
  */
 #include <errno.h>
 #include <stdint.h>
@@ -78,25 +80,39 @@ int main(void)
     for (int i = 0; i < N_IPS; i++)
         ips[i] = i % 2 ? rnd(&s) : (r[rnd(&s) % live].ip | (rnd(&s) & 0xFFu));
     int bad = 0;
-    for (int b = 0; b < N_IPS; b += BURST) { /* l3fwd_fib_lookup: one call per burst */
-        uint64_t nhop[BURST];
-        const int rc = cne_fib_lookup_bulk(fib, ips + b, nhop, BURST);
-        if (rc == -ENODEV) {
-            for (int i = 0; i < BURST; i++)
-                if (nhop[i] != config.default_nh)
-                    return 1;
-            printf("no GPU: lookups returned -ENODEV with the default next hop\n");
-            cne_fib_free(fib);
-            return 77;
+    /* first as created (CNE_FIB_LOOKUP_DEFAULT: the host image, cne_fib.c:86),
+     * then with the GPU extension selected */
+    for (int sel = 0; sel < 2; sel++) {
+        if (sel && cne_fib_select_lookup(fib, (enum cne_fib_lookup_type)CNDP_FIB_LOOKUP_GPU) != 0) {
+            fprintf(stderr, "cne_fib_select_lookup(GPU) failed\n");
+            return 1;
         }
-        for (int i = 0; i < BURST; i++) {
-            const uint64_t want = lpm(r, live, ips[b + i], config.default_nh);
-            if (nhop[i] != want && bad++ < 4)
-                fprintf(stderr, "ip %08x: nh %llx want %llx\n", ips[b + i], (unsigned long long)nhop[i],
-                        (unsigned long long)want);
+        for (int b = 0; b < N_IPS; b += BURST) { /* l3fwd_fib_lookup: one call per burst */
+            uint64_t nhop[BURST];
+            const int rc = cne_fib_lookup_bulk(fib, ips + b, nhop, BURST);
+            if (rc == -ENODEV && sel) {
+                for (int i = 0; i < BURST; i++)
+                    if (nhop[i] != config.default_nh)
+                        return 1;
+                printf("%s: default lookups right (%d wrong); no GPU: the GPU lookups returned "
+                       "-ENODEV with the default next hop\n", bad ? "FAIL" : "PASS", bad);
+                cne_fib_free(fib);
+                return bad ? 1 : 77;
+            }
+            if (rc != 0) {
+                fprintf(stderr, "cne_fib_lookup_bulk: %d\n", rc);
+                return 1;
+            }
+            for (int i = 0; i < BURST; i++) {
+                const uint64_t want = lpm(r, live, ips[b + i], config.default_nh);
+                if (nhop[i] != want && bad++ < 4)
+                    fprintf(stderr, "sel %d ip %08x: nh %llx want %llx\n", sel, ips[b + i],
+                            (unsigned long long)nhop[i], (unsigned long long)want);
+            }
         }
     }
     cne_fib_free(fib);
-    printf("%s: %d lookups over %d rules, %d wrong\n", bad ? "FAIL" : "PASS", N_IPS, live, bad);
+    printf("%s: %d lookups over %d rules in each selection, %d wrong\n", bad ? "FAIL" : "PASS", N_IPS, live,
+           bad);
     return bad ? 1 : 0;
 }

@@ -91,3 +91,22 @@ int harness_eth_rx_port(cne_node_t nid, uint16_t port_id)
     m->head = e;
     return 0;
 }
+
+/* cnet's other synchronous FIB callers, running on their own thread while the
+ * graph walks: ip4_forward.c:134-178 looks up 4 destinations per call in the
+ * ARP and route FIBs, ip4_output.c:87-118 / cnet_arp.c:77 / cnet_route4.c:77
+ * one key per call.  `rounds` passes over keys[0..n) in calls of per_call keys;
+ * the answers of the last pass land in out.  Returns 0 or the first error. */
+#include "cndp_fib.h"
+int harness_fib_caller(struct cne_fib *fib, const uint32_t *keys, uint64_t *out, uint32_t n,
+                       uint32_t per_call, uint32_t rounds)
+{
+    for (uint32_t r = 0; r < rounds; r++)
+        for (uint32_t o = 0; o < n; o += per_call) {
+            const uint32_t k = n - o < per_call ? n - o : per_call;
+            const int rc = cne_fib_lookup_bulk(fib, (uint32_t *)(uintptr_t)(keys + o), out + o, (int)k);
+            if (rc < 0)
+                return rc;
+        }
+    return 0;
+}

@@ -102,10 +102,120 @@ def test_select_lookup():
               N.CNE_FIB_LOOKUP_DIR24_8_VECTOR_AVX512):
         assert f.select_lookup(t) == 0
     assert f.select_lookup(N.CNE_FIB_LOOKUP_TRIE_SCALAR) < 0
+    # cne_fib.c:206-221: a DUMMY FIB selects nothing of the reference's; the
+    # GPU extension is accepted
     assert Fib("d", N.CNE_FIB_DUMMY).select_lookup(N.CNE_FIB_LOOKUP_DEFAULT) < 0
+    assert Fib("d", N.CNE_FIB_DUMMY).select_lookup(N.CNE_FIB_LOOKUP_GPU) == 0
     f6 = Fib6("y", N.CNE_FIB_TRIE)
     assert f6.select_lookup(N.CNE_FIB_LOOKUP_TRIE_SCALAR) == 0
     assert f6.select_lookup(N.CNE_FIB_LOOKUP_DIR24_8_SCALAR_MACRO) < 0
+    assert Fib6("d6", N.CNE_FIB_DUMMY).select_lookup(N.CNE_FIB_LOOKUP_GPU) == 0
+
+
+# ---- cne_fib_lookup_bulk with the reference's default selection -----------
+# cne_fib.c:86 / cne_fib6.c:92 bind the scalar loop of dir24_8.h:118-148 /
+# trie.h:119-138 at create time; this library answers those calls on the
+# calling thread from the host image (no GPU involved), so they run here.
+
+@pytest.mark.parametrize("kind", [("dummy", N.CNE_FIB_DUMMY, 0, 127), ("1B", N.CNE_FIB_DIR24_8, 0, 127),
+                                  ("2B", N.CNE_FIB_DIR24_8, 1, 255), ("4B", N.CNE_FIB_DIR24_8, 2, 256),
+                                  ("8B", N.CNE_FIB_DIR24_8, 3, 256)])
+def test_ladder4_default_lookup(kind):
+    """fib_test.c check_fib (:239-348) through cne_fib_lookup_bulk as created."""
+    from test_oracle_golden import _ladder4
+    _, t, nh_sz, ntbl8 = kind
+    f = Fib("lad", t, default_nh=100, max_routes=1 << 16, nh_sz=nh_sz, num_tbl8=ntbl8)
+    _ladder4(f.lookup_bulk, f.add, f.delete)
+
+
+@pytest.mark.parametrize("nh_sz", [0, 1, 2, 3])
+def test_default_lookup_vs_bruteforce(nh_sz):
+    rng = np.random.default_rng(40 + nh_sz)
+    maxnh = (1 << ((8 << nh_sz) - 1)) - 1
+    f = Fib("b", N.CNE_FIB_DIR24_8, default_nh=min(7, maxnh), max_routes=4096, nh_sz=nh_sz,
+            num_tbl8=min(127, maxnh) if nh_sz == 0 else 512)
+    routes = {}
+    for _ in range(400):
+        d = int(rng.integers(8, 33))
+        ip = int(rng.integers(0, 2**32))
+        ip = 0x0A000000 | (ip & 0x00FFFFFF) if rng.random() < 0.7 else ip
+        ip &= (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+        nh = int(rng.integers(0, maxnh + 1))
+        if f.add(ip, d, nh) == 0:
+            routes[(ip, d)] = nh
+    ips = rng.integers(0, 2**32, size=20000, dtype=np.uint64).astype(np.uint32)
+    ips[::2] = 0x0A000000 | (ips[::2] & 0x00FFFFFF)
+    want = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], min(7, maxnh), ips)
+    for n in (1, 3, 4, 15, 16, 17, 256, 20000):  # below, at and past the prefetch distance
+        assert np.array_equal(f.lookup_bulk(ips[:n]), want[:n]), n
+    for t in (N.CNE_FIB_LOOKUP_DIR24_8_SCALAR_MACRO, N.CNE_FIB_LOOKUP_DIR24_8_SCALAR_UNI,
+              N.CNE_FIB_LOOKUP_DIR24_8_VECTOR_AVX512, N.CNE_FIB_LOOKUP_DEFAULT):
+        assert f.select_lookup(t) == 0
+        assert np.array_equal(f.lookup_bulk(ips), want)
+
+
+def test_default_lookup6_golden():
+    """lpm6_data_test.h's 1000 rules and the reference's expected next hops,
+    through cne_fib6_lookup_bulk as created, for every trie width and DUMMY."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "lpm6_1000.npz"))
+    for t, nh_sz in ((N.CNE_FIB_TRIE, N.CNE_FIB_TRIE_2B), (N.CNE_FIB_TRIE, N.CNE_FIB_TRIE_4B),
+                     (N.CNE_FIB_TRIE, N.CNE_FIB_TRIE_8B), (N.CNE_FIB_DUMMY, 0)):
+        f6 = Fib6("l6", t, default_nh=0, max_routes=2000, nh_sz=nh_sz, num_tbl8=1 << 14)
+        for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
+            assert f6.add(bytes(ip), int(d), int(nh)) == 0
+        for n in (1, 4, 256, len(g["ip"])):
+            assert np.array_equal(f6.lookup_bulk(g["ip"][:n]), g["nh"][:n].astype(np.uint64))
+
+
+def test_default_lookup_while_routes_change():
+    """cnet adds ARP and route entries while graphs forward: one thread adds and
+    deletes routes while three call cne_fib_lookup_bulk (no lock on the lookup,
+    as in dir24_8.h).  A /24 under a /16 is the only thing that ever changes for
+    the probe keys, so every answer is one of the two next hops; afterwards the
+    lookups equal brute-force LPM over the final routes."""
+    import threading
+    f = Fib("churn", N.CNE_FIB_DIR24_8, default_nh=3, max_routes=8192, nh_sz=N.CNE_FIB_DIR24_8_4B,
+            num_tbl8=1024)
+    assert f.add(0x0B000000, 16, 50) == 0
+    rng = np.random.default_rng(78)
+    probe = (0x0B000000 | rng.integers(0, 1 << 16, size=4096, dtype=np.uint64)).astype(np.uint32)
+    stop = threading.Event()
+    bad = []
+
+    def reader():
+        k = 0
+        while not stop.is_set():
+            n = (4, 256, 4096)[k % 3]
+            got = f.lookup_bulk(probe[:n])
+            ok = (got >= 50) & (got < 50 + 1 + 3000)
+            if not ok.all():
+                bad.append(got[~ok][:4])
+                return
+            k += 1
+
+    th = [threading.Thread(target=reader) for _ in range(3)]
+    for t in th:
+        t.start()
+    routes = {(0x0B000000, 16): 50}
+    try:
+        for k in range(3000):
+            d = int(rng.choice([24, 25, 28, 32]))
+            ip = (0x0B000000 | int(rng.integers(0, 1 << 16))) & (0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF
+            if k % 4 == 3 and len(routes) > 1:
+                keys = [r for r in routes if r[1] > 16]
+                dip, dd = keys[int(rng.integers(0, len(keys)))]
+                assert f.delete(dip, dd) == 0
+                del routes[(dip, dd)]
+            elif f.add(ip, d, 51 + k) == 0:
+                routes[(ip, d)] = 51 + k
+    finally:
+        stop.set()
+        for t in th:
+            t.join()
+    assert not bad, bad[:3]
+    want = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], 3, probe)
+    assert np.array_equal(f.lookup_bulk(probe), want)
 
 
 def _host_lookup4(fib, ips):

@@ -32,3 +32,31 @@ def test_c_program_fib_lookups_on_gpu(gpu):
     r = _run()
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+
+
+RATE = os.path.join(HERE, "c_link", "fib_rate")
+
+
+def test_fib_rate_default_selection():
+    """tests/c_link/fib_rate, the default selection only: cnet's rt4 / arp /
+    nd6 FIBs looked up through cne_fib_lookup_bulk from plain C in 1-, 4- and
+    256-key calls on the host image, every answer checked (brute-force LPM for
+    rt4 and arp, the whole-array call for the rest)."""
+    import json
+    if not os.path.exists(RATE):
+        pytest.skip("fib_rate not built (build() makes it)")
+    r = subprocess.run([RATE, "--ms", "20"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout)
+    assert res["wrong"] == 0 and len(res["points"]) == 9
+
+
+@pytest.mark.gpu
+def test_fib_rate_both_selections(gpu):
+    """The same through CNE_FIB_LOOKUP_GPU as well: every GPU answer equals the
+    host image's."""
+    import json
+    r = subprocess.run([RATE, "--gpu", "--ms", "20"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout)
+    assert res["wrong"] == 0 and {p["sel"] for p in res["points"]} == {"default", "gpu"}

@@ -24,6 +24,7 @@ def test_node_fib_ladder_gpu(gpu):
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     NodeFib.fini()
     nf = NodeFib()
+    assert nf.select_lookup(N.CNE_FIB_LOOKUP_GPU) == 0
     try:
         _ladder4(nf.lookup_bulk, lambda ip, d, nh: cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE),
                  nf.delete, def_nh=N.IP4_LOOKUP_NEXT_PKT_DROP << 16)
@@ -31,10 +32,17 @@ def test_node_fib_ladder_gpu(gpu):
         NodeFib.fini()
 
 
-def _routes_fib(seed, nh_sz=N.CNE_FIB_DIR24_8_4B):
+# both selections of cne_fib_select_lookup: the device mirror and the host
+# image (CNE_FIB_LOOKUP_DEFAULT, what cne_fib_create binds)
+SELECTIONS = pytest.mark.parametrize("sel", [N.CNE_FIB_LOOKUP_GPU, N.CNE_FIB_LOOKUP_DEFAULT],
+                                     ids=["gpu", "host"])
+
+
+def _routes_fib(seed, nh_sz=N.CNE_FIB_DIR24_8_4B, sel=N.CNE_FIB_LOOKUP_GPU):
     from cndp_amd.fib import Fib
     rng = np.random.default_rng(seed)
-    f = Fib(f"t{seed}", N.CNE_FIB_DIR24_8, default_nh=9, max_routes=4096, nh_sz=nh_sz, num_tbl8=512)
+    f = Fib(f"t{seed}", N.CNE_FIB_DIR24_8, default_nh=9, max_routes=4096, nh_sz=nh_sz, num_tbl8=512,
+            lookup=sel)
     routes = {}
     for _ in range(500):
         d = int(rng.integers(8, 33))
@@ -45,12 +53,13 @@ def _routes_fib(seed, nh_sz=N.CNE_FIB_DIR24_8_4B):
     return f, [(ip, d, nh) for (ip, d), nh in routes.items()]
 
 
-def test_fib_lookup_bulk_many_threads(gpu):
+@SELECTIONS
+def test_fib_lookup_bulk_many_threads(gpu, sel):
     """examples/cndpfwd/l3-fwd.c:85 calls cne_fib_lookup_bulk per burst from
     every forwarding thread on one FIB.  Eight threads start on a FIB that has
     no device mirror yet (the first lookups race to create it) and issue
     4-, 256- and 5000-key calls; every answer equals brute-force LPM."""
-    f, routes = _routes_fib(21)
+    f, routes = _routes_fib(21, sel=sel)
     rng = np.random.default_rng(5)
     keys = rng.integers(0, 2**32, size=1 << 16, dtype=np.uint64).astype(np.uint32)
     keys[::2] = 0x0A000000 | (keys[::2] & 0x00FFFFFF)
@@ -80,9 +89,10 @@ def test_fib_lookup_bulk_many_threads(gpu):
     assert not errors, errors[:4]
 
 
-def test_fib_lookup_bulk_large_and_v6(gpu):
+@SELECTIONS
+def test_fib_lookup_bulk_large_and_v6(gpu, sel):
     """Calls above the mapped-staging size (DMA path, chunked) and IPv6."""
-    f, routes = _routes_fib(22)
+    f, routes = _routes_fib(22, sel=sel)
     rng = np.random.default_rng(6)
     ips = rng.integers(0, 2**32, size=(1 << 20) + 12345, dtype=np.uint64).astype(np.uint32)
     ips[::2] = 0x0A000000 | (ips[::2] & 0x00FFFFFF)
@@ -94,7 +104,8 @@ def test_fib_lookup_bulk_large_and_v6(gpu):
     import os
     from cndp_amd.fib import Fib6
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "lpm6_1000.npz"))
-    f6 = Fib6("l6b", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 14)
+    f6 = Fib6("l6b", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 14,
+              lookup=sel)
     for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
         assert f6.add(bytes(ip), int(d), int(nh)) == 0
     for n in (1, 4, 256, 20000):
@@ -181,7 +192,51 @@ def test_scratch_stream_order(gpu):
     cl.close()
 
 
-def test_fib_add_while_lookup(gpu):
+def test_scratch_stream_destroyed(gpu):
+    """A caller-created HIP stream that ran a cnet call is handed back with
+    cndp_gpu_stream_release and destroyed; the next calls (another such stream,
+    then the null stream) order after its work and carry the speculation state
+    exactly as if the calls ran one after another."""
+    from cndp_amd.classify import Classifier
+    from test_gpu_parity import _gtp_mix
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    cl = Classifier(0)
+    cl.set_fib(fib, fib6)
+    cl.set_tuning(cnet_spec=256)
+    fr = _gtp_mix(256 * 120, routes, v6, gpu, seed=4)
+    parts = 3
+    cut = [k * (fr.n // parts) // 256 * 256 for k in range(parts)] + [fr.n]
+    prts = [pktgen.Frames(fr.slab, cut[k + 1] - cut[k], offsets=fr.offsets[cut[k]:cut[k + 1]].contiguous())
+            for k in range(parts)]
+    outb = [cl.alloc_outputs(p.n, 64, device=gpu) for p in prts]
+    st = np.zeros(1, np.uint16)
+    refs = [oracle_classify(O.MODE_CNET, p, tables4=t4, tables6=t6, spec_burst=256, spec_state=st) for p in prts]
+    torch.cuda.synchronize()
+    outs = []
+    L = N.lib()
+    for k in range(parts):
+        if k < parts - 1:
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            outs.append(cl.classify(prts[k], N.CNDP_MODE_CNET, out=outb[k], stream=s.value))
+            assert L.cndp_gpu_stream_release(cl.h, s) == 0
+            assert hip.hipStreamDestroy(s) == 0
+        else:
+            outs.append(cl.classify(prts[k], N.CNDP_MODE_CNET, out=outb[k], stream=0))
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert_same(o, r)
+    assert L.cndp_gpu_stream_release(cl.h, None) == 0   # not the last user's: a no-op
+    cl.close()
+
+
+@SELECTIONS
+def test_fib_add_while_lookup(gpu, sel):
     """cnet adds routes at run time while graphs walk: one thread adds and
     deletes routes (cne_fib_add / _delete) while three threads call
     cne_fib_lookup_bulk, which syncs the device mirror from the dirty ranges.
@@ -190,7 +245,7 @@ def test_fib_add_while_lookup(gpu):
     done, every lookup equals brute-force LPM over the final routes."""
     from cndp_amd.fib import Fib
     f = Fib("churn", N.CNE_FIB_DIR24_8, default_nh=3, max_routes=8192, nh_sz=N.CNE_FIB_DIR24_8_4B,
-            num_tbl8=1024)
+            num_tbl8=1024, lookup=sel)
     rng = np.random.default_rng(77)
     keys = (0x0B000000 | rng.integers(0, 1 << 24, size=1 << 14, dtype=np.uint64)).astype(np.uint32)
     routes = {}
@@ -238,8 +293,8 @@ def test_fib_add_while_lookup(gpu):
     assert np.array_equal(f.lookup_bulk(probe), want_p)
 
 
-@pytest.mark.gpu
-def test_fib_lookup_threads(gpu):
+@SELECTIONS
+def test_fib_lookup_threads(gpu, sel):
     """examples/cndpfwd/l3-fwd.c:85 calls cne_fib_lookup_bulk per burst from
     every forwarding thread on one FIB.  Small calls take a staging slot of
     their own (stream, mapped staging, completion flag) and overlap; large
@@ -250,11 +305,12 @@ def test_fib_lookup_threads(gpu):
     from cndp_amd import pktgen
     from cndp_amd.fib import Fib, Fib6, node_ip4_route_add
     f = Fib("thr4", N.CNE_FIB_DIR24_8, default_nh=1 << 16, max_routes=1024, nh_sz=N.CNE_FIB_DIR24_8_4B,
-            num_tbl8=256)
+            num_tbl8=256, lookup=sel)
     routes = pktgen.l3fwd_routes()
     for ip, d, nh in routes:
         node_ip4_route_add(f, ip, d, nh, 0)
-    f6 = Fib6("thr6", N.CNE_FIB_TRIE, default_nh=0, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15)
+    f6 = Fib6("thr6", N.CNE_FIB_TRIE, default_nh=0, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15,
+              lookup=sel)
     for ip, d, i in pktgen.v6_routes():
         f6.add(ip, d, i)
     rng = np.random.default_rng(5)

@@ -396,6 +396,35 @@ def test_mq_backpressure_and_errors(l3, gpu):
     assert cl._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)) == -22
 
 
+def test_mq_idle_flush_threshold(l3, gpu):
+    """cndp_gpu.h's idle-flush rule: with nothing in flight, poll launches a
+    partly filled batch once it holds batch / 2 mbufs (or is max_delay_us / 2
+    old, far off here), not before (CNDP_MQ_STAT_BATCHES pins it)."""
+    cl, fib, t4 = l3
+    n = 1024
+    pool = MbufPool(n)
+    pool.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=17))
+    q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, batch=1024, depth=2, max_delay_us=20_000_000)
+    stat = lambda: cl._L.cndp_gpu_mq_stat(q.h, N.CNDP_MQ_STAT_BATCHES)  # noqa: E731
+    assert q.submit(pool.ptrs(range(0, 256))) == 256
+    assert q.submit(pool.ptrs(range(256, 511))) == 255
+    for _ in range(3):
+        a, _e = q.poll()
+        assert a.size == 0
+    assert stat() == 0                      # 511 < batch / 2: still filling
+    assert q.submit(pool.ptrs(range(511, 512))) == 1
+    a, _e = q.poll()                        # 512 = batch / 2 and idle: launched now
+    assert stat() == 1
+    import time
+    t0, got = time.time(), a.size
+    while got < 512 and time.time() - t0 < 10:
+        q.wait()
+        a, _e = q.poll()
+        got += a.size
+    assert got == 512
+    q.close()
+
+
 @pytest.mark.parametrize("zero_copy", [True, False])
 def test_c1_cndpfwd_loopback(l3, gpu, zero_copy):
     """C1 (BASELINE configs[0]): cndpfwd loopback mode over one 512-packet

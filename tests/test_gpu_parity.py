@@ -284,7 +284,7 @@ def test_fib_lookup_bulk_gpu_vs_bruteforce(gpu, nh_sz):
     rng = np.random.default_rng(nh_sz)
     maxnh = (1 << ((8 << nh_sz) - 1)) - 1
     f = Fib("b", N.CNE_FIB_DIR24_8, default_nh=min(7, maxnh), max_routes=4096, nh_sz=nh_sz,
-            num_tbl8=min(127, maxnh) if nh_sz == 0 else 512)
+            num_tbl8=min(127, maxnh) if nh_sz == 0 else 512, lookup=N.CNE_FIB_LOOKUP_GPU)
     routes = {}
     for _ in range(400):
         d = int(rng.integers(8, 33))
@@ -309,7 +309,8 @@ def test_fib_ladder_gpu():
     from cndp_amd.fib import Fib
     for t, nh_sz, ntbl8 in ((N.CNE_FIB_DUMMY, 0, 127), (N.CNE_FIB_DIR24_8, 0, 127), (N.CNE_FIB_DIR24_8, 1, 255),
                             (N.CNE_FIB_DIR24_8, 2, 256), (N.CNE_FIB_DIR24_8, 3, 256)):
-        f = Fib("lad", t, default_nh=100, max_routes=1 << 16, nh_sz=nh_sz, num_tbl8=ntbl8)
+        f = Fib("lad", t, default_nh=100, max_routes=1 << 16, nh_sz=nh_sz, num_tbl8=ntbl8,
+                lookup=N.CNE_FIB_LOOKUP_GPU)
         _ladder4(f.lookup_bulk, f.add, f.delete)
 
 
@@ -317,11 +318,12 @@ def test_lpm6_1000_rules_gpu(gpu):
     from cndp_amd.fib import Fib6
     g = np.load(os.path.join(GOLD, "lpm6_1000.npz"))
     for nh_sz in (N.CNE_FIB_TRIE_2B, N.CNE_FIB_TRIE_4B, N.CNE_FIB_TRIE_8B):
-        f6 = Fib6("l6", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=nh_sz, num_tbl8=1 << 14)
+        f6 = Fib6("l6", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=nh_sz, num_tbl8=1 << 14,
+                  lookup=N.CNE_FIB_LOOKUP_GPU)
         for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
             assert f6.add(bytes(ip), int(d), int(nh)) == 0
         assert np.array_equal(f6.lookup_bulk(g["ip"]), g["nh"].astype(np.uint64))
-    d6 = Fib6("d6", N.CNE_FIB_DUMMY, default_nh=0, max_routes=2000)
+    d6 = Fib6("d6", N.CNE_FIB_DUMMY, default_nh=0, max_routes=2000, lookup=N.CNE_FIB_LOOKUP_GPU)
     for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"]):
         assert d6.add(bytes(ip), int(d), int(nh)) == 0
     assert np.array_equal(d6.lookup_bulk(g["ip"]), g["nh"].astype(np.uint64))
@@ -330,7 +332,7 @@ def test_lpm6_1000_rules_gpu(gpu):
 def test_fib_incremental_sync_gpu(gpu):
     """Routes changed after the first GPU lookup are visible to the next one."""
     from cndp_amd.fib import Fib
-    f = Fib("inc", N.CNE_FIB_DIR24_8, default_nh=1, max_routes=64, num_tbl8=64)
+    f = Fib("inc", N.CNE_FIB_DIR24_8, default_nh=1, max_routes=64, num_tbl8=64, lookup=N.CNE_FIB_LOOKUP_GPU)
     ips = np.array([0x0A000001, 0x0A000081, 0x0B000001], np.uint32)
     assert list(f.lookup_bulk(ips)) == [1, 1, 1]
     f.add(0x0A000000, 8, 5)

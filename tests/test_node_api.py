@@ -224,12 +224,14 @@ def test_fib6_get_rib():
 
 
 def test_lookup_without_gpu_fills_default():
-    """No usable device: the lookup cannot run, so every next hop is the FIB
-    default (callers like l3-fwd.c:85 ignore the code) and -ENODEV returns."""
+    """CNE_FIB_LOOKUP_GPU selected and no usable device: the lookup cannot run,
+    so every next hop is the FIB default (callers like l3-fwd.c:85 ignore the
+    code) and -ENODEV returns."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("a GPU is present")
-    f = Fib("nogpu", N.CNE_FIB_DIR24_8, default_nh=77, max_routes=16, nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=16)
+    f = Fib("nogpu", N.CNE_FIB_DIR24_8, default_nh=77, max_routes=16, nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=16,
+            lookup=N.CNE_FIB_LOOKUP_GPU)
     ips = np.arange(300, dtype=np.uint32)
     out = np.full(300, 0xDEAD, np.uint64)
     assert f._L.cne_fib_lookup_bulk(f.h, ips.ctypes.data, out.ctypes.data, 300) == -19

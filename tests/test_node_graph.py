@@ -250,6 +250,82 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
     assert set(np.unique(got).tolist()) >= {0, 3, 4, 6}   # drop, gtpu_input, ip4_forward, ip6_forward
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("sel", [N.CNE_FIB_LOOKUP_DEFAULT, N.CNE_FIB_LOOKUP_GPU], ids=["host", "gpu"])
+def test_cnet_node_with_sync_fib_callers(gpu, sel):
+    """The link swap of INTEGRATION.md §3 as cnet runs it: the GPU eth_rx node
+    is bound to this_cnet's rt4 FIB while, on other threads, an
+    ip4_forward-style caller looks up 4 destinations per cne_fib_lookup_bulk
+    call in that same FIB (ip4_forward.c:134-178) and an ARP-style caller one
+    key per call in an arp-fib of /32 host entries (cnet_arp.c:77,195,
+    ip4_output.c:118).  In either selection of cne_fib_select_lookup every
+    synchronous answer equals brute-force LPM and every mbuf leaves the node
+    by the oracle's edge."""
+    import threading
+    from cndp_amd.fib import Fib
+    from helpers import CNET_DEF, cnet_fibs
+    from oracle import oracle as O
+    from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
+    H = _cnet_harness()
+    H.harness_fib_caller.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32]
+    L = N.lib()
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    assert fib.select_lookup(sel) == 0
+    arp = Fib("arp-fib", N.CNE_FIB_DIR24_8, default_nh=CNET_DEF, max_routes=1024, nh_sz=N.CNE_FIB_DIR24_8_4B,
+              num_tbl8=256, lookup=sel)
+    arp_routes = [((10 << 24) | (200 << 16) | i, 32, i) for i in range(1024)]
+    for ip, d, nh in arp_routes:
+        assert arp.add(ip, d, nh) == 0
+    rng = np.random.default_rng(12)
+    k4 = rng.integers(0, 2**32, size=8192, dtype=np.uint64).astype(np.uint32)
+    k4[::2] = np.array([ip for ip, _, _ in routes], np.uint32)[rng.integers(0, len(routes), 4096)] | \
+        rng.integers(0, 256, 4096).astype(np.uint32)
+    ka = ((10 << 24) | (200 << 16) | rng.integers(0, 1100, size=4096)).astype(np.uint32)
+    want4 = O.lpm4_bruteforce([(ip, d, nh) for ip, d, nh in v4vals], CNET_DEF, k4)
+    wanta = O.lpm4_bruteforce(arp_routes, CNET_DEF, ka)
+    out4 = np.zeros(k4.size, np.uint64)
+    outa = np.zeros(ka.size, np.uint64)
+    rcs = {}
+
+    def caller(tag, f, keys, out, per_call):
+        rcs[tag] = H.harness_fib_caller(f.h, keys.ctypes.data, out.ctypes.data, keys.size, per_call, 20)
+
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    n, port = 24000, 3
+    pool, orig = cnet_pool(n, routes, v6, True)
+    ref = _cnet_expect(pool, np.arange(n), _bursts(n, 0, "full"), t4, t6, 0, port)
+    L.cndp_node_gpu_umem_reset()
+    L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
+    H.harness_cnet_set(fib.h, fib6.h)
+    assert H.harness_eth_rx_port(0, port) == 0
+    assert H.harness_rx_load(port, pool.ptrs(np.arange(n)), n) == 0
+    th = [threading.Thread(target=caller, args=("fwd4", fib, k4, out4, 4)),
+          threading.Thread(target=caller, args=("arp1", arp, ka, outa, 1))]
+    try:
+        assert H.harness_graph_create(5) == 0
+        for t in th:
+            t.start()
+        assert H.harness_walk_until(n) >= 0
+        for t in th:
+            t.join()
+        assert H.harness_rx_left(port) == 0 and H.harness_total() == n
+        got = np.full(n, -1, np.int64)
+        buf = (ctypes.c_void_p * n)()
+        for k, name in enumerate(ETH_RX_EDGES):
+            m = H.harness_take_edge(name, buf, n)
+            got[pool.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))] = k
+    finally:
+        H.harness_graph_destroy()
+        L.cndp_node_gpu_umem_reset()
+    assert rcs == {"fwd4": 0, "arp1": 0}
+    assert np.array_equal(out4, want4)
+    assert np.array_equal(outa, wanta)
+    want_e = cnet_check(pool, orig, ref, t4, t6, port)
+    assert np.array_equal(got, np.array([_edge_of_queue_code(int(e)) for e in want_e]))
+
+
 def test_cnet_node_edges_match_reference_names():
     """The GPU eth_rx node's edges are exactly the reference's next nodes of
     ptype (p_nxt edge ids -> ptype.c:213-230 names), ip4_input / ip6_input

@@ -1,6 +1,14 @@
-"""Per-call latency of the host-array FIB lookups (cne_fib_lookup_bulk /
-cne_fib6_lookup_bulk) on the GPU: n = 4 (ip4_lookup's 4-wide call), 256 (a
-graph burst, examples/cndpfwd/l3-fwd.c:85), 64K; median / p99 over many calls.
+"""Rates of the host-array FIB lookups (cne_fib_lookup_bulk /
+cne_fib6_lookup_bulk) in both selections of cne_fib_select_lookup.
+
+* "c_rate": tests/c_link/fib_rate (plain C, no ctypes call in the timed loop):
+  per-thread Mlookups/s of the default selection (the host image, what a FIB is
+  created with, cne_fib.c:86) and of CNE_FIB_LOOKUP_GPU, for cnet's call shapes
+  -- 1 key (ip4_output.c:87,118, cnet_arp.c:77), 4 keys (ip4_forward.c:134-178,
+  ip4_lookup.c:141), 256 keys (a burst, examples/cndpfwd/l3-fwd.c:85) -- on
+  the rt4 / arp / nd6 FIBs cnet creates, and the default path on 1-8 threads.
+* the rest: per-call latency of the GPU selection from Python, n = 4, 256, 64K
+  (median / p99 over many calls) and 256-key calls from 1-16 threads.
 usage: python tools/fib_latency.py [--json out.json]"""
 import argparse
 import json
@@ -21,15 +29,23 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--calls", type=int, default=2000)
     args = ap.parse_args()
+    res = {}
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "c_link", "fib_rate")
+    import subprocess
+    import torch
+    r = subprocess.run([exe] + (["--gpu"] if torch.cuda.is_available() else []), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res["c_rate"] = json.loads(r.stdout)
     f = Fib("lat", N.CNE_FIB_DIR24_8, default_nh=1 << 16, max_routes=1024, nh_sz=N.CNE_FIB_DIR24_8_4B,
-            num_tbl8=256)
+            num_tbl8=256, lookup=N.CNE_FIB_LOOKUP_GPU)
     for ip, d, nh in pktgen.l3fwd_routes():
         node_ip4_route_add(f, ip, d, nh, 0)
-    f6 = Fib6("lat6", N.CNE_FIB_TRIE, default_nh=0, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15)
+    f6 = Fib6("lat6", N.CNE_FIB_TRIE, default_nh=0, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15,
+              lookup=N.CNE_FIB_LOOKUP_GPU)
     for ip, d, i in pktgen.v6_routes():
         f6.add(ip, d, i)
     rng = np.random.default_rng(0)
-    res = {}
     L = N.lib()
     for n in (4, 256, 65536):
         ips = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
