@@ -221,10 +221,16 @@ def host_cpus():
 
 
 def cpu_baseline(state, budget_s: float = 10.0):
-    """The oracle's per-burst chain on this host's cores (rank 0, N=1): the
-    l3fwd node loop (C2 / C3) or the cnet chain (C4 / C5), per 256-packet
-    burst, one pinned thread per CPU of the process's affinity set, and 1
-    thread.  Bounded sample of the same frames, repeated to ~budget_s."""
+    """The reference chain on this host's cores (rank 0, N=1), one pinned
+    thread per CPU of the process's affinity set, and 1 thread, over a bounded
+    sample of the same frames repeated to ~budget_s:
+      C2 / C3: the l3fwd node loop per 256-packet burst (oracle/oracle.c);
+      C4 / C5: the cnet chain as a graph walk runs it (oracle/cnet_chain.c:
+        eth_rx -> ptype -> ip4_input / ip6_input over pktmbuf_t pointers,
+        direct loads, the nodes' prefetching), with the reference's
+        cne_softrss as the flow hash the GPU line computes; no_hash_Mpps is
+        the same chain without it (CNDP's cnet nodes hash nothing), and
+        checker_Mpps the per-frame checker loop earlier rounds reported."""
     from cndp_amd import native as N
     from oracle import oracle as O
     fr, mode = state["frames"], state["mode"]
@@ -240,35 +246,55 @@ def cpu_baseline(state, budget_s: float = 10.0):
     else:
         slab = np.concatenate([fr.slab[: n * fr.stride].cpu().numpy(), np.zeros(2048, np.uint8)])
         kw.update(stride=fr.stride, data_off=fr.data_off)
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(fr.stride) + np.uint64(fr.data_off)
     cpus, model, quota = host_cpus()
     aff = len(cpus)
     if quota:  # a CPU quota below the affinity set: one pinned thread per CPU of the quota
         cpus = cpus[:max(1, int(-(-quota // 1)))]
-    t1 = O.burst_bench(mode, slab, n, nthreads=1, iters=1, cpus=cpus[:1], **kw)
-    single = n / t1 / 1e6
-    tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=1, cpus=cpus, **kw)
-    iters = max(1, int(budget_s / max(tt, 1e-6)))
-    tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=iters, cpus=cpus, **kw)
-    multi = n * iters / tt / 1e6
     extra = {}
     if cnet:
-        # CNDP's own cnet chain hashes nothing (no cne_softrss caller, SURVEY
-        # §0.3): the same chain without the flow hash, beside the value (which
-        # does the GPU line's work, hash included)
-        th = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=iters, cpus=cpus, no_hash=True, **kw)
+        lens = (fr.lengths[:n].cpu().numpy() if fr.lengths is not None
+                else np.full(n, min(fr.stride, 1500) if fr.stride else 1500)).astype(np.uint16)
+        hdr, ptrs = O.slab_mbufs(slab, offs, lens)
+        tabs = (kw["tables4"], kw["tables6"])
+
+        def run(threads, iters, h):
+            return O.cnet_chain(ptrs, n, lens, 0, *tabs, hash=h, nthreads=threads, iters=iters,
+                                cpus=cpus[:threads])
+        t1 = run(1, 1, True)
+        single = n / t1 / 1e6
+        tt = run(len(cpus), 1, True)
+        iters = max(1, int(budget_s / max(tt, 1e-6)))
+        tt = run(len(cpus), iters, True)
+        multi = n * iters / tt / 1e6
+        th = run(len(cpus), iters, False)
         extra["no_hash_Mpps"] = round(n * iters / th / 1e6, 2)
-        extra["no_hash_note"] = ("the cnet chain without the Toeplitz flow hash, which CNDP's cnet nodes "
-                                 "never compute (the reference chain's own work)")
-    chain = ("cnet chain per 256-burst (cne_get_ptype restatement, eth_rx fields, ptype-node speculation, "
-             "ip4/ip6_input length + checksum + DIR-24-8 / trie lookups, plus the build's cne_softrss flow "
-             "hash the GPU line computes and CNDP's cnet nodes do not -- no_hash_Mpps drops it)" if cnet else
-             "l3fwd node loop per 256-burst (ethertype parse, pkt_cls, ip4_lookup's 4-wide "
-             "cne_fib_lookup_bulk with dir24_8.h's prefetching lookup" +
-             (", skipped in C2" if mode == N.CNDP_MODE_HASH else "") + ", cne_softrss restatement, RETA)")
+        extra["no_hash_single_core_Mpps"] = round(n / run(1, 1, False) / 1e6, 2)
+        extra["no_hash_note"] = ("the same chain without the flow hash, which CNDP's cnet nodes never "
+                                 "compute (the reference chain's own work)")
+        tc = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=1, cpus=cpus, **kw)
+        extra["checker_Mpps"] = round(n / tc / 1e6, 2)
+        extra["checker_note"] = ("oracle/oracle.c's per-frame checker loop (bounds-checked byte reads, "
+                                 "no prefetching), the figure earlier rounds reported")
+        chain = ("cnet chain per 256-mbuf graph walk over pktmbuf_t pointers (oracle/cnet_chain.c: eth_rx "
+                 "mbuf_update with cne_get_ptype, ptype-node speculation, ip4/ip6_input length + checksum + "
+                 "metadata + 4-wide DIR-24-8 / trie lookups, the nodes' prefetching; plus the reference's "
+                 "cne_softrss flow hash the GPU line computes -- no_hash_Mpps drops it)")
+        del hdr
+    else:
+        t1 = O.burst_bench(mode, slab, n, nthreads=1, iters=1, cpus=cpus[:1], **kw)
+        single = n / t1 / 1e6
+        tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=1, cpus=cpus, **kw)
+        iters = max(1, int(budget_s / max(tt, 1e-6)))
+        tt = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=iters, cpus=cpus, **kw)
+        multi = n * iters / tt / 1e6
+        chain = ("l3fwd node loop per 256-burst (ethertype parse, pkt_cls, ip4_lookup's 4-wide "
+                 "cne_fib_lookup_bulk with dir24_8.h's prefetching lookup" +
+                 (", skipped in C2" if mode == N.CNDP_MODE_HASH else "") + ", cne_softrss restatement, RETA)")
     return {"value": round(multi, 2), "unit": "Mpps", "cores": len(cpus), "kind": "port",
             "cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
             "single_core_Mpps": round(single, 2), **extra,
-            "sample": (f"oracle/oracle.c {chain} over {n} of the same frames x {iters} passes on "
+            "sample": (f"{chain} over {n} of the same frames x {iters} passes on "
                        f"{len(cpus)} pinned threads ({tt:.1f} s); 1 thread: {single:.2f} Mpps")}
 
 
@@ -546,14 +572,19 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         cn["eth_rx_node_zero_copy_Mpps" if zc else "eth_rx_node_staged_Mpps"] = \
             round(nc * passes / t / 1e6, 2) if t > 0 else None
     L.cndp_node_gpu_umem_reset()
-    # the cnet chain on one core over the same frames (the pool as the slab)
+    # the reference cnet chain on one core over the same mbufs (oracle/cnet_chain.c:
+    # eth_rx -> ptype -> ip4_input / ip6_input per 256-mbuf walk, as the GPU
+    # nodes replace them; no flow hash, as neither writes one)
     pool.hdr[:] = hdr0
-    kw = {"tables4": tuple(x.copy() for x in f4.image()), "tables6": tuple(x.copy() for x in f6.image()),
-          "offsets": pool.data_pos().astype(np.uint64)}
+    t4c, t6c = tuple(x.copy() for x in f4.image()), tuple(x.copy() for x in f6.image())
     cpus, _, _ = host_cpus()
-    O.burst_bench(N.CNDP_MODE_CNET, pool.mem, nc, nthreads=1, iters=1, cpus=cpus[:1], **kw)
-    t = O.burst_bench(N.CNDP_MODE_CNET, pool.mem, nc, nthreads=1, iters=passes, cpus=cpus[:1], **kw)
+    rx_len = hdr0["data_len"].copy()
+    O.cnet_chain(ptrs, nc, rx_len, int(hdr0["data_off"][0]), t4c, t6c, cpus=cpus[:1])
+    t = O.cnet_chain(ptrs, nc, rx_len, int(hdr0["data_off"][0]), t4c, t6c, iters=passes, cpus=cpus[:1])
+    pool.hdr[:] = hdr0
     cn["cpu_1core_Mpps"] = round(nc * passes / t / 1e6, 2)
+    cn["cpu_chain"] = ("the reference cnet chain per 256-mbuf graph walk over the same pktmbuf_t pool, one "
+                       "core (oracle/cnet_chain.c)")
     cn["mbufs"] = nc
     cn["frames"] = "IMIX 64/570/1500 7:4:1, IPv4+IPv6"
     res["cnet"] = cn

@@ -36,6 +36,11 @@
  * the application registered its UMEMs with cndp_node_gpu_umem_add(), else
  * staged.  One GPU context and queue per cloned node (per port and graph).
  *
+ * Graph stats: ptype, ip4_input and ip6_input get the calls and objects they
+ * would have processed added to their node stats (cne_graph_worker.h:156-160)
+ * at each poll, so cne_graph_stats / the cluster stats show the traffic they
+ * stand for (see node_stat below).
+ *
  * The input nodes' cnet_metadata (ipv4/ipv6_save_metadata, ip4_input.c:33-48,
  * ip6_input.c:32-48), which tcp_input / udp_input read, is written at
  * pktmbuf_metadata(m) for every frame this node sends on an ip4_input /
@@ -86,6 +91,9 @@ static struct eth_rx_node_main eth_rx_main;
 struct gpu_rx_state {
     cndp_gpu_ctx_t *gpu;
     cndp_gpu_mq_t *q;
+    /* the replaced nodes in this graph (NULL when absent): their walk stats
+     * are credited with the objects they would have processed */
+    struct cne_node *st_ptype, *st_ip4, *st_ip6;
     void *rx[RX_BURST];
     void *done[RX_BURST];
     uint16_t edge[RX_BURST];
@@ -133,6 +141,21 @@ static inline cne_edge_t rx_edge(uint16_t e)
                                      : ETH_RX_GPU_NEXT_PKT_DROP;
 }
 
+/* cne_graph_walk counts, per node, the calls made to it and the objects they
+ * returned (cne_graph_worker.h:156-160), which cne_graph_stats and the cnet
+ * cluster stats print.  ptype, ip4_input and ip6_input never run under this
+ * node, so it counts for them: per poll, one call of ptype with every mbuf,
+ * and one call of each input node with the mbufs the ptype node routed to it
+ * (its speculation included).  Their total_cycles stay 0: no CPU time is
+ * spent in them. */
+static inline void node_stat(struct cne_node *n, uint16_t objs)
+{
+    if (n && objs) {
+        n->total_calls++;
+        n->total_objs += objs;
+    }
+}
+
 /* hand every finished mbuf on to its edge, one enqueue per edge */
 static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct gpu_rx_state *st)
 {
@@ -141,8 +164,20 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
         const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, RX_BURST);
         if (k <= 0)
             break;
-        for (int i = 0; i < k; i++)
-            st->edge[i] = rx_edge(st->edge[i]);
+        uint16_t n4 = 0, n6 = 0;
+        for (int i = 0; i < k; i++) {
+            const uint16_t e = st->edge[i];
+            if (e != CNDP_MQ_EDGE_NONE) {
+                n4 = (uint16_t)(n4 + (e >> 8 == CNDP_MQ_NODE_IP4));
+                n6 = (uint16_t)(n6 + (e >> 8 == CNDP_MQ_NODE_IP6));
+            }
+            st->edge[i] = rx_edge(e);
+        }
+        if (cne_graph_has_stats_feature()) {
+            node_stat(st->st_ptype, (uint16_t)k);
+            node_stat(st->st_ip4, n4);
+            node_stat(st->st_ip6, n6);
+        }
         gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, ETH_RX_GPU_NEXT_MAX, st->grp);
         total = (uint16_t)(total + k);
         if (k < RX_BURST)
@@ -189,7 +224,6 @@ static void rx_state_free(struct gpu_rx_state *st)
 
 static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
 {
-    (void)graph;
     struct gpu_rx_ctx *ctx = GPU_RX_CTX(node);
     memset(ctx, 0, sizeof(*ctx));
     for (eth_rx_node_elem_t *elem = eth_rx_main.head; elem; elem = elem->next)
@@ -227,6 +261,10 @@ static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
             conf.umem = umem;
     if ((r = cndp_gpu_mq_create(st->gpu, &conf, &st->q)) < 0)
         goto fail;
+    /* graph.c:291-295 lays the graph's nodes out before their init runs */
+    st->st_ptype = cne_graph_get_node_by_name(graph, "ptype");
+    st->st_ip4 = cne_graph_get_node_by_name(graph, "ip4_input");
+    st->st_ip6 = cne_graph_get_node_by_name(graph, "ip6_input");
     ctx->st = st;
     return 0;
 fail:

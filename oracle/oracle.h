@@ -132,6 +132,33 @@ double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, in
 double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iters, const int *cpus);
 double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
                             const uint32_t *tbl8, int iters);
+
+/* ---- the cnet chain as a graph walk runs it (oracle/cnet_chain.c) --------
+ * eth_rx -> ptype -> ip4_input / ip6_input per burst over pktmbuf_t pointer
+ * arrays, direct loads and the nodes' prefetching; the CPU baseline of C4/C5
+ * and of the cnet node boundary.  Each mbuf needs 64 B of cnet_metadata
+ * after its header (pktmbuf_metadata's default).  mbufs[i] gets data_off =
+ * rx_data_off and data_len = rx_len[i] before each pass (pktdev_rx).  Results:
+ * m->packet_type, ol_flags, tx_offload, lport, data_off/data_len, metadata,
+ * m->hash (ORC_CHAIN_HASH) and m->udata64 = edge << 32 | nh.  Shards over
+ * nthreads (pinned to cpus[t] when given); returns seconds for iters passes. */
+#define ORC_CHAIN_HASH 1u
+struct orc_cnet_chain_args {
+    void *const *mbufs;
+    uint32_t n;
+    uint32_t burst;             /* graph burst, <= 256 (0 = 256) */
+    const uint16_t *rx_len;     /* frame length of mbufs[i] */
+    uint16_t rx_data_off;
+    uint16_t lport;
+    uint32_t flags;             /* ORC_CHAIN_* */
+    const uint32_t *tbl24, *tbl8;     /* rt4 DIR-24-8 4 B */
+    const uint32_t *tbl24_6, *tbl8_6; /* rt6 trie 4 B */
+    const uint8_t *rss_key;
+    const uint16_t *reta;
+    uint32_t reta_size;
+    uint16_t *state;            /* in/out ptype ctx->last_type (thread 0's), or NULL */
+};
+double orc_cnet_chain(const struct orc_cnet_chain_args *a, int nthreads, int iters, const int *cpus);
 void orc_dir24_8_lookup_bulk_pf(const uint32_t *tbl24, const uint32_t *tbl8, const uint32_t *ips, uint32_t n,
                                 uint64_t *nh);
 

@@ -47,6 +47,61 @@ _lib = None
 _ref = None
 
 
+class ChainArgs(Structure):
+    """struct orc_cnet_chain_args (oracle.h)"""
+    _fields_ = [("mbufs", c_void_p), ("n", c_uint32), ("burst", c_uint32), ("rx_len", c_void_p),
+                ("rx_data_off", c_uint16), ("lport", c_uint16), ("flags", c_uint32),
+                ("tbl24", c_void_p), ("tbl8", c_void_p), ("tbl24_6", c_void_p), ("tbl8_6", c_void_p),
+                ("rss_key", c_void_p), ("reta", c_void_p), ("reta_size", c_uint32), ("state", c_void_p)]
+
+
+CHAIN_HASH = 1
+# a pktmbuf_t header (pktmbuf.h:102-204) + the 64-B cnet_metadata after it
+CHAIN_MBUF = np.dtype([("pooldata", "<u8"), ("buf_addr", "<u8"), ("hash", "<u4"), ("meta_index", "<u4"),
+                       ("data_off", "<u2"), ("lport", "<u2"), ("buf_len", "<u2"), ("data_len", "<u2"),
+                       ("packet_type", "<u4"), ("refcnt", "<u2"), ("rsvd16", "<u2"), ("tx_offload", "<u8"),
+                       ("ol_flags", "<u8"), ("udata64", "<u8"), ("metadata", "u1", (64,))])
+
+
+def slab_mbufs(slab: np.ndarray, offsets, lens, buf_len: int = 1984):
+    """pktmbuf_t headers for frames that lie in a slab (frame i at
+    slab + offsets[i], lens[i] bytes): buf_addr = the frame, data_off 0.
+    Returns (headers, pointer array); keep both alive while they are used."""
+    offsets = np.asarray(offsets, dtype=np.uint64)
+    n = len(offsets)
+    hdr = np.zeros(n, CHAIN_MBUF)
+    hdr["buf_addr"] = np.uint64(slab.ctypes.data) + offsets
+    hdr["buf_len"] = buf_len
+    hdr["data_len"] = np.asarray(lens, dtype=np.uint16)
+    hdr["refcnt"] = 1
+    ptrs = np.uint64(hdr.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(CHAIN_MBUF.itemsize)
+    return hdr, ptrs
+
+
+def cnet_chain(ptrs, n, rx_len, rx_data_off, tables4, tables6, burst=256, hash=False, key=None, reta=None,
+               state=None, nthreads=1, iters=1, cpus=None, lport=0) -> float:
+    """oracle/cnet_chain.c over n pktmbuf_t pointers (numpy u64 array or a
+    ctypes pointer array): seconds for iters passes on nthreads threads."""
+    from cndp_amd.native import MS_RSS_KEY
+    key = np.frombuffer(key or MS_RSS_KEY, dtype=np.uint8).copy()
+    reta = np.ascontiguousarray(reta if reta is not None else (np.arange(128) % 16), dtype=np.uint16)
+    rx_len = np.ascontiguousarray(rx_len, dtype=np.uint16)
+    a = ChainArgs()
+    a.mbufs = ptrs.ctypes.data if isinstance(ptrs, np.ndarray) else ctypes.addressof(ptrs)
+    a.n, a.burst, a.rx_len, a.rx_data_off, a.lport = n, burst, _p(rx_len), rx_data_off, lport
+    a.flags = CHAIN_HASH if hash else 0
+    a.tbl24, a.tbl8 = _p(tables4[0]), _p(tables4[1])
+    a.tbl24_6, a.tbl8_6 = _p(tables6[0]), _p(tables6[1])
+    a.rss_key, a.reta, a.reta_size = _p(key), _p(reta), len(reta)
+    if state is not None:   # np.uint16 array of 1, updated in place
+        a.state = _p(state)
+    cp = np.ascontiguousarray(cpus, dtype=np.int32) if cpus is not None else None
+    t = lib().orc_cnet_chain(ctypes.byref(a), nthreads, iters, _p(cp))
+    if t < 0:
+        raise ValueError("orc_cnet_chain rejected its arguments")
+    return t
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -85,6 +140,8 @@ def lib():
                                       c_uint32, c_void_p, c_void_p]
         L.orc_mac_swap.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]
         L.orc_ip4_rewrite_node.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p]
+        L.orc_cnet_chain.restype = c_double
+        L.orc_cnet_chain.argtypes = [POINTER(ChainArgs), c_int, c_int, c_void_p]
         L.orc_l3fwd_nodes_mbufs.restype = c_double
         L.orc_l3fwd_nodes_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_int]
         _lib = L

@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #define CNE_NODE_NAMESIZE 64
+#define CNE_GRAPH_NAMESIZE 64
 #define CNE_NODE_ID_INVALID UINT32_MAX
 #define CNE_NODE_SOURCE_F (1ULL << 0)
 #define CNE_NODE_CTX_SZ 16
@@ -45,6 +46,10 @@ cne_node_t __cne_node_register(const struct cne_node_register *node);
 cne_edge_t cne_node_edge_count(cne_node_t id);
 cne_edge_t cne_node_edge_update(cne_node_t id, cne_edge_t from, const char **next_nodes, uint16_t nb_edges);
 cne_node_t cne_node_edge_get(cne_node_t id, char *next_nodes[]);
+
+/* cne_graph.h:370 (the node of this name in this graph) and :649 */
+struct cne_node *cne_graph_get_node_by_name(const struct cne_graph *graph, const char *node_name);
+static inline int cne_graph_has_stats_feature(void) { return 1; }
 
 #define CNE_NODE_REGISTER(node)                                                      \
     __attribute__((constructor)) static void cne_node_register_##node(void)         \

@@ -9,11 +9,16 @@
 
 struct cne_graph {
     cne_graph_t id;
+    char name[CNE_GRAPH_NAMESIZE];
 };
 
 struct cne_node {
     uint8_t ctx[CNE_NODE_CTX_SZ];
     cne_node_t id;
+    char name[CNE_NODE_NAMESIZE];
+    uint64_t total_cycles; /* the per-node stats cne_graph_walk keeps (cne_graph_worker.h:156-160) */
+    uint64_t total_calls;
+    uint64_t total_objs;
     const struct cne_node_register *reg;
 };
 

@@ -5,6 +5,7 @@
  * route FIBs (this_cnet), and pkt_ctrl.c's per-port registration of the node.
  */
 #include <stdlib.h>
+#include <string.h>
 
 #include "cne_graph.h"
 #include "cnet.h"
@@ -109,4 +110,31 @@ int harness_fib_caller(struct cne_fib *fib, const uint32_t *keys, uint64_t *out,
                 return rc;
         }
     return 0;
+}
+
+/* The nodes eth_rx_gpu.c stands in for, as cnet registers them (ptype.c:213,
+ * ip4_input.c:274, ip6_input.c:275), so they are in the graph with stats of
+ * their own; eth_rx_gpu never enqueues to them.  Registered on request (after
+ * eth_rx, which keeps node id 0). */
+static uint16_t idle_process(struct cne_graph *graph, struct cne_node *node, void **objs, uint16_t nb)
+{
+    (void)graph;
+    (void)node;
+    (void)objs;
+    return nb;
+}
+static struct cne_node_register stub_ptype = {.name = "ptype", .process = idle_process};
+static struct cne_node_register stub_ip4 = {.name = "ip4_input", .process = idle_process};
+static struct cne_node_register stub_ip6 = {.name = "ip6_input", .process = idle_process};
+void harness_register_input_nodes(void)
+{
+    static int done;
+    if (done)
+        return;
+    done = 1;
+    struct cne_node_register *r[3] = {&stub_ptype, &stub_ip4, &stub_ip6};
+    for (int i = 0; i < 3; i++) {
+        r[i]->parent_id = CNE_NODE_ID_INVALID;
+        r[i]->id = __cne_node_register(r[i]);
+    }
 }

@@ -276,6 +276,7 @@ void harness_drop_clones(void)
 int harness_graph_create(int gid)
 {
     g.id = (cne_graph_t)gid;
+    snprintf(g.name, sizeof(g.name), "worker-%d", gid);
     for (int k = 0; k < 3; k++) {
         if (!out[k] && !(out[k] = malloc(sizeof(void *) * MAX_OUT)))
             return -12;
@@ -288,11 +289,33 @@ int harness_graph_create(int gid)
         memset(&nodes[i], 0, sizeof(nodes[i]));
         nodes[i].id = regs[i]->id;
         nodes[i].reg = regs[i];
+        memcpy(nodes[i].name, regs[i]->name, CNE_NODE_NAMESIZE - 1);
         int r = regs[i]->init ? regs[i]->init(&g, &nodes[i]) : 0;
         if (r)
             return r;
         inited[i] = 1;
     }
+    return 0;
+}
+
+struct cne_node *cne_graph_get_node_by_name(const struct cne_graph *graph, const char *node_name)
+{
+    if (graph != &g)
+        return NULL;
+    for (int i = 0; i < n_regs; i++)
+        if (strncmp(nodes[i].name, node_name, CNE_NODE_NAMESIZE) == 0)
+            return &nodes[i];
+    return NULL;
+}
+
+/* the stats a graph walk keeps for the named node */
+int harness_node_stats(const char *name, uint64_t *calls, uint64_t *objs)
+{
+    struct cne_node *n = cne_graph_get_node_by_name(&g, name);
+    if (!n)
+        return -1;
+    *calls = n->total_calls;
+    *objs = n->total_objs;
     return 0;
 }
 

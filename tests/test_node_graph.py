@@ -175,7 +175,8 @@ def test_cnet_node_registry():
     name = ctypes.create_string_buffer(64)
     fl, ne = ctypes.c_uint64(), ctypes.c_int()
     e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
-    assert H.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1)) == 1
+    # (node 0; tests that register the replaced input nodes add more after it)
+    assert H.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1)) >= 1
     assert name.value == b"eth_rx" and fl.value == 1 and ne.value == len(ETH_RX_EDGES)
     names = (ctypes.c_char_p * 16)()
     k = H.harness_node_edges(0, names, 16)
@@ -324,6 +325,49 @@ def test_cnet_node_with_sync_fib_callers(gpu, sel):
     assert np.array_equal(outa, wanta)
     want_e = cnet_check(pool, orig, ref, t4, t6, port)
     assert np.array_equal(got, np.array([_edge_of_queue_code(int(e)) for e in want_e]))
+
+
+@pytest.mark.gpu
+def test_cnet_node_stats(gpu):
+    """With ptype, ip4_input and ip6_input in the graph (as cnet registers
+    them), the GPU eth_rx node credits their walk stats
+    (cne_graph_worker.h:156-160) with what they would have processed: ptype
+    every mbuf, each input node the mbufs the ptype node routed to it."""
+    from helpers import CNET_DEF, cnet_fibs
+    from oracle import oracle as O
+    from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
+    H = _cnet_harness()
+    H.harness_node_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    H.harness_register_input_nodes()
+    L = N.lib()
+    fib, fib6, routes, v6, v4vals, v6vals = cnet_fibs()
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
+    n, port = 20000, 2
+    pool, orig = cnet_pool(n, routes, v6, True)
+    ref = _cnet_expect(pool, np.arange(n), _bursts(n, 0, "full"), t4, t6, 0, port)
+    L.cndp_node_gpu_umem_reset()
+    L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
+    H.harness_cnet_set(fib.h, fib6.h)
+    assert H.harness_eth_rx_port(0, port) == 0
+    assert H.harness_rx_load(port, pool.ptrs(np.arange(n)), n) == 0
+    stats = {}
+    try:
+        assert H.harness_graph_create(6) == 0
+        assert H.harness_walk_until(n) >= 0
+        for name in (b"ptype", b"ip4_input", b"ip6_input"):
+            c, o = ctypes.c_uint64(), ctypes.c_uint64()
+            assert H.harness_node_stats(name, ctypes.byref(c), ctypes.byref(o)) == 0
+            stats[name] = (c.value, o.value)
+    finally:
+        H.harness_graph_destroy()
+        L.cndp_node_gpu_umem_reset()
+    want_e = np.asarray(cnet_check(pool, orig, ref, t4, t6, port), np.int64)
+    node = want_e >> 8
+    assert stats[b"ptype"][1] == n and stats[b"ptype"][0] >= 1
+    assert stats[b"ip4_input"][1] == int((node == N.CNDP_MQ_NODE_IP4).sum()) > 0
+    assert stats[b"ip6_input"][1] == int((node == N.CNDP_MQ_NODE_IP6).sum()) > 0
 
 
 def test_cnet_node_edges_match_reference_names():
