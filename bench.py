@@ -482,24 +482,49 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     ptrs = pool.ptrs(np.arange(n))
     l3 = {}
     NodeFib.fini()
-    for zc in (True, False):
-        L.cndp_node_gpu_umem_reset()
-        if zc:
-            L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
-        assert H.harness_graph_create(10 + int(zc)) == 0
-        for ip, d, nh in routes:
-            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
-        H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
-        t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
-        H.harness_graph_destroy()
-        l3["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+    H.harness_rx_parse.argtypes = [ctypes.c_int]
+    # Interleaved A/B, two rounds: the zero-copy node with the host resolving
+    # frame addresses from the mbuf header (default) or the kernel reading the
+    # headers itself (CNDP_MQ_F_DEVICE_HEADERS); each with and without
+    # pktdev_rx's soft parse run on the burst first (pktdev_rx.c:36-101, as the
+    # l3fwd-graph walk pktdev_rx -> pkt_cls -> ip4_lookup does, so the header
+    # lines are in the core's cache).  Then staged.  Median of the rounds.
+    variants = [("gpu_zero_copy", True, 0, 0), ("gpu_zero_copy_rx_parse", True, 0, 1),
+                ("gpu_zero_copy_device_headers", True, N.CNDP_MQ_F_DEVICE_HEADERS, 0),
+                ("gpu_zero_copy_device_headers_rx_parse", True, N.CNDP_MQ_F_DEVICE_HEADERS, 1),
+                ("gpu_staged", False, 0, 0), ("gpu_staged_rx_parse", False, 0, 1)]
+    ab = {v[0]: [] for v in variants}
+    gid = 10
+    for rnd in range(2):
+        for name, zc, flags, rxp in variants:
+            L.cndp_node_gpu_umem_reset()
+            if zc:
+                L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
+            os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
+            gid += 1
+            assert H.harness_graph_create(gid) == 0
+            for ip, d, nh in routes:
+                cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+            H.harness_rx_parse(rxp)
+            H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
+            t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
+            H.harness_rx_parse(0)
+            H.harness_graph_destroy()
+            ab[name].append(n * passes / t / 1e6 if t > 0 else 0.0)
+    os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+    for name, v in ab.items():
+        l3[name + "_Mpps"] = round(float(np.median(v)), 2) if min(v) > 0 else None
+    l3["ab_rounds"] = {k: [round(x, 2) for x in v] for k, v in ab.items()}
     L.cndp_node_gpu_umem_reset()
     fib = NodeFib()
     t24, t8 = (x.copy() for x in fib.image())
     O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, 1)
     t = O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
     l3["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
-    l3["cpu_chain"] = "the ip4_lookup node loop over the same mbufs (oracle/oracle.c orc_ip4_lookup_mbufs)"
+    t = O.rx_ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
+    l3["cpu_1core_rx_parse_Mpps"] = round(n * passes / t / 1e6, 2)
+    l3["cpu_chain"] = ("the ip4_lookup node loop over the same mbufs (oracle/oracle.c orc_ip4_lookup_mbufs); "
+                       "_rx_parse: pktdev_rx's soft parse on each burst first, on both sides")
     NodeFib.fini()
     res["l3fwd_ip4_lookup"] = l3
     # ---- l3fwd: the ip4_lookup + ip4_rewrite node pair, chained as a graph

@@ -1485,6 +1485,24 @@ __device__ __forceinline__ void spec_odd_tile(const KArgs &a, uint32_t tt, uint3
         atomicOr(s_mx, p2 == pt ? 1u << 8 : 1u << pe);
 }
 
+// The per-frame output pointers, read from the kernarg segment where they are
+// used (an opaque copy of the segment pointer per trip keeps the compiler from
+// hoisting them): a scalar load each instead of SGPRs held across the loop,
+// which the kernel does not have (spilled to VGPR lanes otherwise).
+#ifndef CD_RELOAD
+#define CD_RELOAD 1
+#endif
+__device__ __forceinline__ const KArgs &kargs_fresh(const KArgs &a)
+{
+#if CD_RELOAD
+    const KArgs *p = (const KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+#else
+    return a;
+#endif
+}
+
 template <bool LNT, bool META, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
@@ -1553,14 +1571,15 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const bool slow = live && !fast;
         const unsigned long long m = __ballot(slow);
         if (m) {
+            const KArgs &o = kargs_fresh(a);
             uint32_t w0 = 0;
             if (lane == (uint32_t)(__ffsll(m) - 1))
-                w0 = atomicAdd(a.wl_n, (uint32_t)__popcll(m));
+                w0 = atomicAdd(o.wl_n, (uint32_t)__popcll(m));
             w0 = __shfl(w0, __ffsll(m) - 1);
             if (slow)
                 // write-through (agent-scope) store: k_cnet_defer's last block
                 // may read it without a release by this one (cnet_defer_tail)
-                __hip_atomic_store(&a.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))], (uint32_t)i,
+                __hip_atomic_store(&o.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))], (uint32_t)i,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -1658,6 +1677,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     }
     // B's results
     {
+        const KArgs &o = kargs_fresh(a);
         const uint32_t pt = sb.ptf & 0xffffu, pe = sb.ptf >> 19;
         const bool bf = bv && (sb.ptf & (1u << 18));
         const bool din = (sb.ptf & (3u << 16)) != 0u;
@@ -1666,22 +1686,22 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             nh = eb >> 1;
             edge = nh >> 24;
         }
-        if (a.spec_nh) {
-            if (bf && din && (!a.nh || (pe != 3u && pe != 4u)))
-                at32(a.spec_nh, ib) = eb >> 1;
+        if (o.spec_nh) {
+            if (bf && din && (!o.nh || (pe != 3u && pe != 4u)))
+                at32(o.spec_nh, ib) = eb >> 1;
             if (bf) {
                 // the last SPEC_TAIL bursts' types are read by spec_classes in
                 // this kernel's last block when it folds: write-through stores
                 if (a.wl_fold && ib >= a.tail_lo)
-                    __hip_atomic_store(&at16(a.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
+                    __hip_atomic_store(&at16(o.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 else
-                    __builtin_nontemporal_store((uint16_t)pt, &at16(a.spec_t16, ib));
+                    __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
             }
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
-            if (a.spec_tile && bv) {
+            if (o.spec_tile && bv) {
                 // the tile's word for the speculation passes (spec_canon): 1 when
                 // every frame has its low byte's common edge -- parsed here (low
                 // byte 0x11 / 0x41) and bound for ip4_input / ip6_input, not GTP
@@ -1689,7 +1709,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 const bool odd = ib < a.n && !(bf && (pe == 3u || pe == 4u));
                 const uint64_t om = __ballot(odd);
                 if (lane == 0)
-                    a.spec_tile[t - wstep] = (uint8_t)(om == 0ull);
+                    o.spec_tile[t - wstep] = (uint8_t)(om == 0ull);
                 if (om && (a.spec_allow & SPEC_ALLOW_LISTS)) { // wave-uniform, rare
                     // groups (lanes 4q + 3) whose 4th frame was not parsed here, or
                     // is off the common edge beside a 3rd not parsed here (spec_odd_tile)
@@ -1701,22 +1721,22 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         }
         if (bf) {
             const uint32_t q = s_reta[sb.h & a.reta_mask];
-            if (META && a.ptype)
-                __builtin_nontemporal_store(pt, &at32(a.ptype, ib));
-            if (META && a.rxmeta)
-                __builtin_nontemporal_store(sb.rx, &at32(a.rxmeta, ib));
-            if (META && a.iplen)
-                __builtin_nontemporal_store(sb.ipl, &at32(a.iplen, ib));
+            if (META && o.ptype)
+                __builtin_nontemporal_store(pt, &at32(o.ptype, ib));
+            if (META && o.rxmeta)
+                __builtin_nontemporal_store(sb.rx, &at32(o.rxmeta, ib));
+            if (META && o.iplen)
+                __builtin_nontemporal_store(sb.ipl, &at32(o.iplen, ib));
             // non-temporal stores: the outputs are written once and must not
             // push the FIB tables of the gather chains out of L2 (C4 -4.5%)
-            if (a.nh)
-                __builtin_nontemporal_store(nh, &at32(a.nh, ib));
-            if (a.hash)
-                __builtin_nontemporal_store(sb.h, &at32(a.hash, ib));
-            if (a.queue)
-                __builtin_nontemporal_store((uint16_t)q, &at16(a.queue, ib));
-            if (a.edge)
-                __builtin_nontemporal_store((uint8_t)edge, &a.edge[ib]);
+            if (o.nh)
+                __builtin_nontemporal_store(nh, &at32(o.nh, ib));
+            if (o.hash)
+                __builtin_nontemporal_store(sb.h, &at32(o.hash, ib));
+            if (o.queue)
+                __builtin_nontemporal_store((uint16_t)q, &at16(o.queue, ib));
+            if (o.edge)
+                __builtin_nontemporal_store((uint8_t)edge, &o.edge[ib]);
             if (count)
                 atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
         }

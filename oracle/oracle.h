@@ -132,6 +132,8 @@ double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, in
 double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iters, const int *cpus);
 double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
                             const uint32_t *tbl8, int iters);
+double orc_rx_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                               const uint32_t *tbl8, int iters);
 
 /* ---- the cnet chain as a graph walk runs it (oracle/cnet_chain.c) --------
  * eth_rx -> ptype -> ip4_input / ip6_input per burst over pktmbuf_t pointer

@@ -140,6 +140,8 @@ def lib():
                                       c_uint32, c_void_p, c_void_p]
         L.orc_mac_swap.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]
         L.orc_ip4_rewrite_node.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p]
+        L.orc_rx_ip4_lookup_mbufs.restype = c_double
+        L.orc_rx_ip4_lookup_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_int]
         L.orc_cnet_chain.restype = c_double
         L.orc_cnet_chain.argtypes = [POINTER(ChainArgs), c_int, c_int, c_void_p]
         L.orc_l3fwd_nodes_mbufs.restype = c_double
@@ -311,6 +313,11 @@ def dir24_8_lookup_bulk_pf(t24, t8, ips) -> np.ndarray:
 def ip4_lookup_mbufs(ptrs, n, tables4, burst=256, iters=1) -> float:
     """The ip4_lookup node's CPU loop over pktmbuf_t pointers (one thread): seconds."""
     return lib().orc_ip4_lookup_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), iters)
+
+
+def rx_ip4_lookup_mbufs(ptrs, n, tables4, burst=256, iters=1) -> float:
+    """pktdev_rx's soft parse then the ip4_lookup node loop per burst (one thread): seconds."""
+    return lib().orc_rx_ip4_lookup_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), iters)
 
 
 def l3fwd_burst_bench(slab, n, stride, tables4, nthreads=1, iters=1, **kw) -> float:
