@@ -483,15 +483,15 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     l3 = {}
     NodeFib.fini()
     H.harness_rx_parse.argtypes = [ctypes.c_int]
-    # Interleaved A/B, two rounds: the zero-copy node with the host resolving
-    # frame addresses from the mbuf header (default) or the kernel reading the
-    # headers itself (CNDP_MQ_F_DEVICE_HEADERS); each with and without
+    # Interleaved A/B, two rounds: the zero-copy node with the kernel reading
+    # each mbuf header itself (CNDP_MQ_F_DEVICE_HEADERS, the node's default) or
+    # the host resolving frame addresses from the headers; each with and without
     # pktdev_rx's soft parse run on the burst first (pktdev_rx.c:36-101, as the
     # l3fwd-graph walk pktdev_rx -> pkt_cls -> ip4_lookup does, so the header
     # lines are in the core's cache).  Then staged.  Median of the rounds.
-    variants = [("gpu_zero_copy", True, 0, 0), ("gpu_zero_copy_rx_parse", True, 0, 1),
-                ("gpu_zero_copy_device_headers", True, N.CNDP_MQ_F_DEVICE_HEADERS, 0),
-                ("gpu_zero_copy_device_headers_rx_parse", True, N.CNDP_MQ_F_DEVICE_HEADERS, 1),
+    D = N.CNDP_MQ_F_DEVICE_HEADERS  # the node's default
+    variants = [("gpu_zero_copy", True, D, 0), ("gpu_zero_copy_rx_parse", True, D, 1),
+                ("gpu_zero_copy_host_headers", True, 0, 0), ("gpu_zero_copy_host_headers_rx_parse", True, 0, 1),
                 ("gpu_staged", False, 0, 0), ("gpu_staged_rx_parse", False, 0, 1)]
     ab = {v[0]: [] for v in variants}
     gid = 10

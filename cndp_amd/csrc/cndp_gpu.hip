@@ -59,10 +59,20 @@ __device__ __forceinline__ uint32_t hsum2(uint32_t x, uint32_t acc)
     return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, x), (u16x2_t){1, 1}, acc, false);
 }
 
+// global address space for buffer pointers (see gp() below)
+#ifndef GP_GLOBAL
+#define GP_GLOBAL 1 /* 0: generic pointers (A/B builds) */
+#endif
+#if GP_GLOBAL
+#define GAS __attribute__((address_space(1)))
+#else
+#define GAS
+#endif
+
 // bounded global byte read (bytes past the slab end read as 0)
 __device__ __forceinline__ uint32_t gbyte(const uint8_t *p, uint64_t avail, uint64_t o)
 {
-    return o < avail ? (uint32_t)p[o] : 0u;
+    return o < avail ? (uint32_t)((const GAS uint8_t *)p)[o] : 0u;
 }
 // 4 bytes at o assembled little-endian, bounded
 __device__ __forceinline__ uint32_t gld32(const uint8_t *p, uint64_t avail, uint64_t o)
@@ -95,7 +105,8 @@ __device__ __forceinline__ uint32_t lpm4d(const uint32_t *__restrict__ d16,
 }
 
 // Toeplitz byte table access: T[b][v] at tab[b * 256 + v]
-__device__ __forceinline__ uint32_t tz4(const uint32_t *tab, uint32_t b, uint32_t x)
+template <typename TP>
+__device__ __forceinline__ uint32_t tz4(TP tab, uint32_t b, uint32_t x)
 {
     // the 4 stream bytes b..b+3 held little-endian in x (byte b = x & 0xff)
     return tab[(b + 0) * 256 + (x & 0xffu)] ^ tab[(b + 1) * 256 + ((x >> 8) & 0xffu)] ^
@@ -210,11 +221,12 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t nh, uint32_t edge, uint32_t 
 __device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip, bool l4,
                                    const uint32_t *__restrict__ ttab)
 {
+    const GAS uint32_t *gt = (const GAS uint32_t *)ttab;
     uint32_t h = 0;
     for (uint32_t k = 0; k < 8; k++)
-        h ^= tz4(ttab, 4 * k, gld32(p, avail, ip + 8 + 4 * k));
+        h ^= tz4(gt, 4 * k, gld32(p, avail, ip + 8 + 4 * k));
     if (l4)
-        h ^= tz4(ttab, 32, gld32(p, avail, ip + 40));
+        h ^= tz4(gt, 32, gld32(p, avail, ip + 40));
     return h;
 }
 
@@ -231,25 +243,43 @@ __device__ uint32_t hash_v6_global(const uint8_t *p, uint64_t avail, uint32_t ip
 //       before the first dependent LPM gather: more bytes in flight).
 // ---------------------------------------------------------------------------
 
+// Every buffer a kernel touches is device memory or host memory mapped for
+// the device (hipMalloc, hipHostMalloc, hipHostRegister): global, never LDS or
+// scratch.  Pointers that reach a load or store through integer arithmetic,
+// __shfl or an opaque copy lose that to the compiler, which then emits FLAT
+// instructions: a FLAT access counts in both vmcnt and lgkmcnt, so every
+// later wait for an LDS result (the Toeplitz tables, the tile) waits for the
+// frame loads in flight as well.  gp() restores the global address space.
+template <typename T>
+__device__ __forceinline__ GAS T *gp(T *p)
+{
+    return (GAS T *)p;
+}
+template <typename T>
+__device__ __forceinline__ const GAS T *gp(const T *p)
+{
+    return (const GAS T *)p;
+}
+
 template <bool NT>
 __device__ __forceinline__ u32x4 ldg4(const uint8_t *p)
 {
     if (NT)
-        return __builtin_nontemporal_load((const u32x4 *)p);
-    return *(const u32x4 *)p;
+        return __builtin_nontemporal_load(gp((const u32x4 *)p));
+    return *gp((const u32x4 *)p);
 }
 template <bool NT>
 __device__ __forceinline__ u32x2 ldg2(const uint8_t *p)
 {
     if (NT)
-        return __builtin_nontemporal_load((const u32x2 *)p);
-    return *(const u32x2 *)p;
+        return __builtin_nontemporal_load(gp((const u32x2 *)p));
+    return *gp((const u32x2 *)p);
 }
 template <bool NT, typename T>
 __device__ __forceinline__ void stg(T *p, T v)
 {
     if (NT)
-        __builtin_nontemporal_store(v, p);
+        __builtin_nontemporal_store(v, gp(p));
     else
         *p = v;
 }
@@ -1408,13 +1438,13 @@ __device__ __forceinline__ bool ct_fast(const KArgs &a, uint64_t base)
 // element i of a per-frame output through a 32-bit byte offset (a scalar base
 // + zero-extended VGPR offset: one store, no 64-bit address per lane); the
 // deferred kernel runs only for n < 2^30, so i * 4 fits
-__device__ __forceinline__ uint32_t &at32(uint32_t *p, uint32_t i)
+__device__ __forceinline__ GAS uint32_t &at32(uint32_t *p, uint32_t i)
 {
-    return *(uint32_t *)((char *)p + (uint32_t)(i << 2));
+    return *(GAS uint32_t *)((GAS char *)gp(p) + (uint32_t)(i << 2));
 }
-__device__ __forceinline__ uint16_t &at16(uint16_t *p, uint32_t i)
+__device__ __forceinline__ GAS uint16_t &at16(uint16_t *p, uint32_t i)
 {
-    return *(uint16_t *)((char *)p + (uint32_t)(i << 1));
+    return *(GAS uint16_t *)((GAS char *)gp(p) + (uint32_t)(i << 1));
 }
 
 struct CsOff { // this lane's frame offsets for tiles t, t+1, t+2 and the load for t+3
@@ -1492,14 +1522,15 @@ __device__ __forceinline__ void spec_odd_tile(const KArgs &a, uint32_t tt, uint3
 #ifndef CD_RELOAD
 #define CD_RELOAD 1
 #endif
-__device__ __forceinline__ const KArgs &kargs_fresh(const KArgs &a)
+#define KAS __attribute__((address_space(4)))
+__device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 {
 #if CD_RELOAD
-    const KArgs *p = (const KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    const KAS KArgs *p = (const KAS KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
     return *p;
 #else
-    return a;
+    return *(const KAS KArgs *)&a;
 #endif
 }
 
@@ -1571,7 +1602,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const bool slow = live && !fast;
         const unsigned long long m = __ballot(slow);
         if (m) {
-            const KArgs &o = kargs_fresh(a);
+            const KAS KArgs &o = kargs_fresh(a);
             uint32_t w0 = 0;
             if (lane == (uint32_t)(__ffsll(m) - 1))
                 w0 = atomicAdd(o.wl_n, (uint32_t)__popcll(m));
@@ -1677,7 +1708,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     }
     // B's results
     {
-        const KArgs &o = kargs_fresh(a);
+        const KAS KArgs &o = kargs_fresh(a);
         const uint32_t pt = sb.ptf & 0xffffu, pe = sb.ptf >> 19;
         const bool bf = bv && (sb.ptf & (1u << 18));
         const bool din = (sb.ptf & (3u << 16)) != 0u;
@@ -5869,7 +5900,11 @@ struct MqArgs {
     const struct cndp_rw_nh *rw; // rewrite: next-hop table (device)
     uint32_t lport, want_hash;
     uint32_t devhdr;        // ip4_lookup zc, CNDP_MQ_F_DEVICE_HEADERS: the kernel reads each mbuf's
-    int64_t delta;          //   header itself (frames in [slab, slab + slab_len), device = host + delta)
+    uint32_t nrg;           //   header itself; its frame lies in one of the nrg registered regions
+    struct {                //   (host address range, device = host + delta)
+        uint64_t host, len;
+        int64_t delta;
+    } rg[CNDP_MAX_REGIONS];
     MqTables tb;
     uint32_t *ticket;       // device arrival counter of this slot
     uint32_t *flag;         // device view of the slot's pinned completion flag
@@ -5961,15 +5996,24 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
         if (a.zc && a.devhdr) {
             m = a.mb[i];
             const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
-            const uint64_t buf = m ? *(const uint64_t *)(dm + MB_BUF_ADDR) : 0u;
-            const uint32_t doff = m ? *(const uint16_t *)(dm + MB_DATA_OFF) : 0u;
-            const uint64_t fo = (uint64_t)((int64_t)(buf + doff) + a.delta - (int64_t)(uintptr_t)a.slab);
-            if (m == 0 || fo >= a.slab_len) {
+            const uint64_t buf = m ? *gp((const uint64_t *)(dm + MB_BUF_ADDR)) : 0u;
+            const uint32_t doff = m ? *gp((const uint16_t *)(dm + MB_DATA_OFF)) : 0u;
+            const uint64_t fh = buf + doff; // pktmbuf_mtod, a host address
+            uint64_t fo = ~0ull, rlen = 0;
+            int64_t delta = 0;
+            for (uint32_t k = 0; k < a.nrg; k++) // the frame's registered region
+                if (fh - a.rg[k].host < a.rg[k].len) {
+                    fo = fh - a.rg[k].host;
+                    rlen = a.rg[k].len;
+                    delta = a.rg[k].delta;
+                    break;
+                }
+            if (m == 0 || fo == ~0ull) {
                 a.edges[i] = (uint16_t)MQ_EDGE_NONE;
                 continue;
             }
-            p = a.slab + fo + MQ_W4_AT;
-            avail = a.slab_len - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(a.slab_len - fo > MQ_W4_AT ? a.slab_len - fo - MQ_W4_AT : 0);
+            p = (const uint8_t *)(uintptr_t)(fh + delta) + MQ_W4_AT;
+            avail = rlen - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(rlen - fo > MQ_W4_AT ? rlen - fo - MQ_W4_AT : 0);
         } else if (a.zc) {
             m = a.mb[i];
             uint32_t fa;
@@ -5988,7 +6032,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
         if (avail >= 16 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p) & 63u) <= 48u) {
             // ttl, checksum and dst in one load inside one 64-B line: the
             // frame's only PCIe read when it is read in place
-            const u32x4a4 q = *(const u32x4a4 *)p;
+            const u32x4a4 q = *(const GAS u32x4a4 *)p;
             ttl = (q.x >> 16) & 0xffu;
             ck = q.y & 0xffffu;
             dip = bswap32(alignb(q.w, q.z, 2));
@@ -6001,7 +6045,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
         const uint32_t val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
         const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
         if (a.zc)
-            *(uint64_t *)(m + MB_UDATA64) = priv1;
+            *gp((uint64_t *)(m + MB_UDATA64)) = priv1;
         else
             a.priv1[i] = priv1;
         a.edges[i] = (uint16_t)(val >> 16);
@@ -6520,14 +6564,14 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = tbl_acquire(&c->fib4->t, s, &v4)))
             return r;
         a.tb = mq_tables(c, v4, nullptr, 0);
-        if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // the frames in conf.umem's region
-            for (int k = 0; k < q->nrg; k++)
-                if (q->rg[k].host == (const uint8_t *)q->conf.umem) {
-                    a.devhdr = 1;
-                    a.slab = q->rg[k].host + q->rg[k].delta;
-                    a.slab_len = q->rg[k].len;
-                    a.delta = q->rg[k].delta;
-                }
+        if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // frames in any registered region
+            a.devhdr = 1;
+            a.nrg = (uint32_t)q->nrg;
+            for (int k = 0; k < q->nrg; k++) {
+                a.rg[k].host = (uint64_t)(uintptr_t)q->rg[k].host;
+                a.rg[k].len = q->rg[k].len;
+                a.rg[k].delta = q->rg[k].delta;
+            }
         }
         hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
         tbl_release(&c->fib4->t);

@@ -67,6 +67,33 @@
 
 #define RX_BURST 256 /* CNE_GRAPH_BURST_SIZE (cne_graph.h:30) */
 
+/* ETH_RX_GPU_PROF (diagnostic builds only): where the node's host thread
+ * spends its time -- [0] pktdev_rx_burst, [1] cndp_gpu_mq_submit, [2] poll,
+ * [3] edge mapping + stats, [4] the per-edge enqueue, [5] waits -- in seconds,
+ * read and cleared by eth_rx_gpu_prof() */
+#ifdef ETH_RX_GPU_PROF
+#include <time.h>
+static double prof_t[6];
+static inline double prof_now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+#define PROF_T0() double prof_a = prof_now(), prof_b
+#define PROF_LAP(k) (prof_b = prof_now(), prof_t[k] += prof_b - prof_a, prof_a = prof_b)
+void eth_rx_gpu_prof(double *out)
+{
+    for (int k = 0; k < 6; k++) {
+        out[k] = prof_t[k];
+        prof_t[k] = 0.0;
+    }
+}
+#else
+#define PROF_T0() (void)0
+#define PROF_LAP(k) (void)0
+#endif
+
 /* this node's edges: the next nodes of ptype, ip4_input and ip6_input */
 enum eth_rx_gpu_next {
     ETH_RX_GPU_NEXT_PKT_DROP,    /* ptype / ip4_input / ip6_input ..._PKT_DROP */
@@ -161,7 +188,9 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
 {
     uint16_t total = 0;
     for (;;) {
+        PROF_T0();
         const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, RX_BURST);
+        PROF_LAP(2);
         if (k <= 0)
             break;
         uint16_t n4 = 0, n6 = 0;
@@ -178,7 +207,9 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
             node_stat(st->st_ip4, n4);
             node_stat(st->st_ip6, n6);
         }
+        PROF_LAP(3);
         gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, ETH_RX_GPU_NEXT_MAX, st->grp);
+        PROF_LAP(4);
         total = (uint16_t)(total + k);
         if (k < RX_BURST)
             break;
@@ -193,20 +224,28 @@ static uint16_t eth_rx_gpu_process(struct cne_graph *graph, struct cne_node *nod
     struct gpu_rx_ctx *ctx = GPU_RX_CTX(node);
     struct gpu_rx_state *st = ctx->st;
     rx_drain(graph, node, st); /* free slots first */
+    PROF_T0();
     const uint16_t count = pktdev_rx_burst(ctx->port_id, (pktmbuf_t **)st->rx, RX_BURST);
+    PROF_LAP(0);
     if (count == PKTDEV_ADMIN_STATE_DOWN)
         return count;
     uint16_t done = 0;
     while (done < count) {
         const int k = cndp_gpu_mq_submit(st->q, st->rx + done, (uint32_t)(count - done));
+        PROF_LAP(1);
         if (k < 0) { /* the device failed: the mbufs still have to go somewhere */
             cne_node_enqueue(graph, node, ETH_RX_GPU_NEXT_PKT_DROP, st->rx + done, (uint16_t)(count - done));
             break;
         }
         done = (uint16_t)(done + k);
-        if (done < count && rx_drain(graph, node, st) == 0 && cndp_gpu_mq_wait(st->q) < 0) {
-            cne_node_enqueue(graph, node, ETH_RX_GPU_NEXT_PKT_DROP, st->rx + done, (uint16_t)(count - done));
-            break;
+        if (done < count && rx_drain(graph, node, st) == 0) {
+            PROF_T0();
+            const int w = cndp_gpu_mq_wait(st->q);
+            PROF_LAP(5);
+            if (w < 0) {
+                cne_node_enqueue(graph, node, ETH_RX_GPU_NEXT_PKT_DROP, st->rx + done, (uint16_t)(count - done));
+                break;
+            }
         }
     }
     rx_drain(graph, node, st);

@@ -225,7 +225,9 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
 #define CNDP_MQ_F_NO_METADATA (1u << 1) /* cnet: leave cnet_metadata unwritten */
 /* ip4_lookup zero-copy: the host hands over mbuf pointers only and the kernel
  * reads each header (buf_addr, data_off) in place -- no host touch per mbuf,
- * three dependent PCIe reads per mbuf instead of one (frames in conf.umem) */
+ * three dependent PCIe reads per mbuf instead of one; frames in any region the
+ * context registered.  The GPU ip4_lookup node's default (ip4_lookup_gpu.c):
+ * its host thread, not the device, bounds the node rate. */
 #define CNDP_MQ_F_DEVICE_HEADERS (1u << 2)
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u

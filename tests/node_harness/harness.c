@@ -285,11 +285,14 @@ int harness_graph_create(int gid)
     for (uint32_t k = 0; k < n_names; k++)
         e_n[k] = 0;
     n_total = 0;
+    /* every node laid out before any init runs (graph.c:291-295) */
     for (int i = 0; i < n_regs; i++) {
         memset(&nodes[i], 0, sizeof(nodes[i]));
         nodes[i].id = regs[i]->id;
         nodes[i].reg = regs[i];
         memcpy(nodes[i].name, regs[i]->name, CNE_NODE_NAMESIZE - 1);
+    }
+    for (int i = 0; i < n_regs; i++) {
         int r = regs[i]->init ? regs[i]->init(&g, &nodes[i]) : 0;
         if (r)
             return r;

@@ -74,11 +74,14 @@ def _mixed_l3_frames(n, seed):
     return pktgen.Frames(slab.reshape(-1), n, stride=64)
 
 
-@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
     """"shifted": data_off = 256 + (i mod 61), so frames start at every
-    alignment and line position (the kernel's one-load and byte-wise reads)."""
+    alignment and line position (the kernel's one-load and byte-wise reads).
+    "device_headers": zero-copy with CNDP_MQ_F_DEVICE_HEADERS (the kernel reads
+    each mbuf header itself)."""
+    flags = N.CNDP_MQ_F_DEVICE_HEADERS if zero_copy == "device_headers" else 0
     cl, fib, t4 = l3
     n = 20000
     pool = MbufPool(n)
@@ -92,7 +95,7 @@ def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
         cl.host_register(pool.mem)
         umem = pool.base
     try:
-        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, batch=4096, depth=3, umem=umem)
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, flags=flags, batch=4096, depth=3, umem=umem)
         order = np.random.default_rng(9).permutation(n)  # mbufs come in any order
         addrs, edges = q.run(pool, order, _bursts(n, 5, kind))
         q.close()
@@ -602,11 +605,13 @@ def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
     assert set(np.unique(edges).tolist()) == {0, 1, 2, 3, 4}
 
 
-def test_mq_zero_copy_regions(l3, gpu):
+@pytest.mark.parametrize("flags", [0, N.CNDP_MQ_F_DEVICE_HEADERS], ids=["host_headers", "device_headers"])
+def test_mq_zero_copy_regions(l3, gpu, flags):
     """Zero-copy over several registered regions (a graph's ports with pools
     of their own): mbufs of two registered pools interleaved in one queue get
     their results; an mbuf of an unregistered pool, and an mbuf whose buffer
-    lies outside every region, come back untouched with CNDP_MQ_EDGE_NONE."""
+    lies outside every region, come back untouched with CNDP_MQ_EDGE_NONE.
+    Both header forms: resolved on the host, or read by the kernel."""
     cl, fib, t4 = l3
     n = 3000
     pa, pb, pc = MbufPool(n), MbufPool(n), MbufPool(n)
@@ -618,7 +623,7 @@ def test_mq_zero_copy_regions(l3, gpu):
     cl.host_register(pa.mem)
     cl.host_register(pb.mem)
     try:
-        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, batch=2048, depth=3, umem=pb.base)
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, flags=flags, batch=2048, depth=3, umem=pb.base)
         ptrs = (ctypes.c_void_p * (3 * n))()
         src = np.empty(3 * n, np.int64)
         for i in range(n):
