@@ -1534,6 +1534,18 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #endif
 }
 
+#ifndef CD_PIN
+#define CD_PIN 1
+#endif
+template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
+{
+    const GAS T *g = (const GAS T *)p;
+#if CD_PIN
+    asm volatile("" : "+s"(g));
+#endif
+    return g;
+}
+
 template <bool LNT, bool META, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
@@ -1552,8 +1564,13 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         // q0..q3, the level count and the table pair are fixed per lane
         const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
         uint32_t rem = d6 ? 13u : (a.dir16 ? 2u : 1u);
-        const uint32_t *tb = d6 ? a.tbl8_6 : (a.dir16 ? a.pages : a.tbl8);
-        const uint32_t *const tb2 = d6 ? a.tbl8_6 : a.tbl8;
+        // the table pointers pinned in SGPRs before the per-lane select:
+        // otherwise the select is of their kernarg addresses and the pointer
+        // itself a vector load each trip, waited for at the chain's first level
+        const GAS uint32_t *const t6 = sgpr_pin(a.tbl8_6), *const t8 = sgpr_pin(a.tbl8);
+        const GAS uint32_t *const t4 = sgpr_pin(a.dir16 ? a.pages : a.tbl8);
+        const GAS uint32_t *tb = d6 ? t6 : t4;
+        const GAS uint32_t *const tb2 = d6 ? t6 : t8;
         uint32_t q0 = sb.q0, q1 = sb.q1, q2 = sb.q2, q3 = sb.q3;
         bool more = bv & (d4 | d6) & ((eb & 1u) != 0u);
         while (__any(more)) {
@@ -1700,7 +1717,9 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         na.ptf = pt | flags | (1u << 18) | (pe << 19);
     }
     na.e = tb0[idx0]; // first gather, unconditional
-    // offsets one tile further, then the windows of tile c+2
+    // offsets one tile further, then the windows of tile c+2 (issued after
+    // the first gather: the next trip's wait for the gather leaves them in
+    // flight when no lane of the wave needs a further level)
     {
         const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;

@@ -168,6 +168,23 @@ static inline cne_edge_t rx_edge(uint16_t e)
                                      : ETH_RX_GPU_NEXT_PKT_DROP;
 }
 
+/* rx_edge as a table over the queue's three nodes (the per-mbuf branches
+ * mispredicted on IMIX, where IPv4 and IPv6 frames alternate): filled once */
+static uint8_t rx_edge_tab[3][256];
+
+static void rx_edge_tab_fill(void)
+{
+    for (unsigned n = 0; n < 3; n++)
+        for (unsigned x = 0; x < 256; x++)
+            rx_edge_tab[n][x] = (uint8_t)rx_edge((uint16_t)(n << 8 | x));
+}
+
+static inline uint16_t rx_edge_fast(uint16_t e)
+{
+    const unsigned node = e >> 8;
+    return node < 3 ? rx_edge_tab[node][e & 0xffu] : ETH_RX_GPU_NEXT_PKT_DROP;
+}
+
 /* cne_graph_walk counts, per node, the calls made to it and the objects they
  * returned (cne_graph_worker.h:156-160), which cne_graph_stats and the cnet
  * cluster stats print.  ptype, ip4_input and ip6_input never run under this
@@ -194,13 +211,11 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
         if (k <= 0)
             break;
         uint16_t n4 = 0, n6 = 0;
-        for (int i = 0; i < k; i++) {
+        for (int i = 0; i < k; i++) { /* EDGE_NONE's node is 0xff: counted by neither */
             const uint16_t e = st->edge[i];
-            if (e != CNDP_MQ_EDGE_NONE) {
-                n4 = (uint16_t)(n4 + (e >> 8 == CNDP_MQ_NODE_IP4));
-                n6 = (uint16_t)(n6 + (e >> 8 == CNDP_MQ_NODE_IP6));
-            }
-            st->edge[i] = rx_edge(e);
+            n4 = (uint16_t)(n4 + (e >> 8 == CNDP_MQ_NODE_IP4));
+            n6 = (uint16_t)(n6 + (e >> 8 == CNDP_MQ_NODE_IP6));
+            st->edge[i] = rx_edge_fast(e);
         }
         if (cne_graph_has_stats_feature()) {
             node_stat(st->st_ptype, (uint16_t)k);
@@ -276,6 +291,7 @@ static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
     struct gpu_rx_state *st = calloc(1, sizeof(*st));
     if (!st)
         return -ENOMEM;
+    rx_edge_tab_fill();
     int r = cndp_gpu_init((int)env_u32("CNDP_GPU_DEVICE", 0), &st->gpu);
     if (r < 0) {
         free(st);

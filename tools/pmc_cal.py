@@ -36,10 +36,11 @@ def short(name):
 
 
 def load(d):
-    vals = {}  # kernel -> counter -> [values per dispatch]
+    vals = {}  # "<program>:<kernel>" -> counter -> [values per dispatch]
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
+        prog = os.path.relpath(f, d).split(os.sep)[0].split("_")[0]  # probe / c4 / c5 (pass dirs <prog>_<pass>)
         for r in csv.DictReader(open(f)):
-            k = short(r["Kernel_Name"])
+            k = prog + ":" + short(r["Kernel_Name"])
             vals.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return vals
 
@@ -70,7 +71,8 @@ def main():
         if "WRITE_SIZE" in m:
             r["write_B"] = m["WRITE_SIZE"] * 1024
         for kk, known in KNOWN.items():
-            if k == kk or k.startswith(kk):
+            kn = k.split(":", 1)[1]
+            if kn == kk or kn.startswith(kk):
                 r["known_read_B"] = known
                 for f in ("fetch_B", "req_B", "dram_B"):
                     if f in r:
