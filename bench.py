@@ -547,12 +547,14 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     ptrs = pool.ptrs(np.arange(nc))
     hdr0 = pool.hdr.copy()
     cn = {}
-    for zc in (True, False):
+    D = N.CNDP_MQ_F_DEVICE_HEADERS
+
+    def cnet_queue(zc, flags):
         umem = None
         if zc:
             cl.host_register(pool.mem)
             umem = pool.base
-        q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=8192, depth=4, umem=umem)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=flags, batch=8192, depth=4, umem=umem)
         # eth_rx advances data_off by l2_len in every mbuf it returns: each pass
         # starts from the received mbufs again (headers restored outside the clock)
         t = 0.0
@@ -566,7 +568,8 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         q.close()
         if zc:
             cl.host_unregister(pool.mem)
-        cn["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(nc * passes / t / 1e6, 2) if t > 0 else None
+        return round(nc * passes / t / 1e6, 2) if t > 0 else None
+
     # the same through the GPU eth_rx graph node (cndp_amd/node/eth_rx_gpu.c):
     # graph walks pull 256-mbuf bursts from the port, finished mbufs leave on
     # the ptype / ip4_input / ip6_input edges
@@ -578,11 +581,16 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     HC.harness_walk_until.restype = ctypes.c_double
     HC.harness_cnet_set(f4.h, f6.h)
     HC.harness_eth_rx_port(0, 0)
-    for zc in (True, False):
+
+    gids = iter(range(40, 80))
+
+    def cnet_node(zc, flags):
+        gid = next(gids)
         L.cndp_node_gpu_umem_reset()
         if zc:
             L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
-        assert HC.harness_graph_create(20 + int(zc)) == 0
+        os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
+        assert HC.harness_graph_create(gid) == 0
         t = 0.0
         for p in range(passes + 1):  # pass 0 warms up
             pool.hdr[:] = hdr0
@@ -594,8 +602,25 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
                 break
             t += dt if p else 0.0
         HC.harness_graph_destroy()
-        cn["eth_rx_node_zero_copy_Mpps" if zc else "eth_rx_node_staged_Mpps"] = \
-            round(nc * passes / t / 1e6, 2) if t > 0 else None
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+        return round(nc * passes / t / 1e6, 2) if t > 0 else None
+
+    # interleaved, two rounds (box noise), the median reported and both kept;
+    # the device-header queue is the eth_rx node's default (its host thread
+    # hands over mbuf pointers only), host headers the round-3 path
+    cvars = [("gpu_zero_copy", lambda: cnet_queue(True, D)),
+             ("gpu_zero_copy_host_headers", lambda: cnet_queue(True, 0)),
+             ("gpu_staged", lambda: cnet_queue(False, 0)),
+             ("eth_rx_node_zero_copy", lambda: cnet_node(True, D)),
+             ("eth_rx_node_zero_copy_host_headers", lambda: cnet_node(True, 0)),
+             ("eth_rx_node_staged", lambda: cnet_node(False, 0))]
+    rounds = {k: [] for k, _ in cvars}
+    for _ in range(2):
+        for k, fn in cvars:
+            rounds[k].append(fn())
+    for k, v in rounds.items():
+        cn[k + "_Mpps"] = round(float(np.median(v)), 2) if all(v) else None
+    cn["ab_rounds"] = rounds
     L.cndp_node_gpu_umem_reset()
     # the reference cnet chain on one core over the same mbufs (oracle/cnet_chain.c:
     # eth_rx -> ptype -> ip4_input / ip6_input per 256-mbuf walk, as the GPU

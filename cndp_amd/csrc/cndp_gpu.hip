@@ -1537,6 +1537,21 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #ifndef CD_PIN
 #define CD_PIN 1
 #endif
+// timing-only ablations (tools/abbuild.sh -DCD_ABL=<bits>; wrong results,
+// but every index stays in bounds): 1 no Toeplitz, 2 no chain levels, 4 no
+// first gather (and so no chain), 16 no result stores but the edge
+#ifndef CD_ABL
+#define CD_ABL 0
+#endif
+// 1: tile c+2's windows issued right after tile c is staged (before its
+// parse) instead of after its first gather (A/B)
+#ifndef CD_WEARLY
+#define CD_WEARLY 0
+#endif
+// the chain's levels unrolled (1) or a loop over a shifting key (0, round 3)
+#ifndef CD_UNROLL
+#define CD_UNROLL 1
+#endif
 template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
 {
     const GAS T *g = (const GAS T *)p;
@@ -1569,11 +1584,34 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         // itself a vector load each trip, waited for at the chain's first level
         const GAS uint32_t *const t6 = sgpr_pin(a.tbl8_6), *const t8 = sgpr_pin(a.tbl8);
         const GAS uint32_t *const t4 = sgpr_pin(a.dir16 ? a.pages : a.tbl8);
+        bool more = bv & (d4 | d6) & ((eb & 1u) != 0u);
+#if CD_UNROLL
+        // the levels unrolled: each level's key byte at a fixed place, the
+        // family's last level a lane mask (v4: 1, 2 with the /16 directory;
+        // v6: 13), and from the third level on only IPv6 lanes are left, so
+        // the table base is uniform (t6) -- 5 VALU a level instead of 13
+        (void)rem;
+        const uint32_t q[4] = {sb.q0, sb.q1, sb.q2, sb.q3};
+        // "more" as bit 0 of a VGPR: one AND with the entry a level (a lane
+        // mask turned into a ballot costs a select and a compare)
+        const uint32_t g0 = d6 || a.dir16 != nullptr ? 1u : 0u, g1 = d6 ? 1u : 0u;
+        uint32_t mv = more ? 1u : 0u;
+#pragma unroll
+        for (int k = 0; k < 13; k++) {
+            const bool live = mv != 0u; // mv is 0 or 1
+            if ((CD_ABL & 2) || !__builtin_amdgcn_ballot_w64(live))
+                break;
+            // ((eb >> 1) << 8) | key byte k: bytes 1..3 of eb << 7, byte k & 3 of its word
+            const uint32_t idx = __builtin_amdgcn_perm(eb << 7, q[k >> 2], 0x07060500u | (uint32_t)(k & 3));
+            if (live)
+                eb = k == 0 ? (d6 ? t6 : t4)[idx] : k == 1 ? (d6 ? t6 : t8)[idx] : t6[idx];
+            mv &= k == 0 ? eb & g0 : k == 1 ? eb & g1 : eb;
+        }
+#else
         const GAS uint32_t *tb = d6 ? t6 : t4;
         const GAS uint32_t *const tb2 = d6 ? t6 : t8;
         uint32_t q0 = sb.q0, q1 = sb.q1, q2 = sb.q2, q3 = sb.q3;
-        bool more = bv & (d4 | d6) & ((eb & 1u) != 0u);
-        while (__any(more)) {
+        while (!(CD_ABL & 2) && __any(more)) {
             const uint32_t idx = ((eb >> 1) << 8) | (q0 & 0xffu);
             if (more)
                 eb = tb[idx];
@@ -1585,6 +1623,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             rem--;
             more = more & ((eb & 1u) != 0u) & (rem != 0u);
         }
+#endif
     }
     // A: tile c
 #pragma unroll
@@ -1592,6 +1631,14 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const uint32_t f = 16u * k + fr_in_k;
         tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
     }
+#if CD_WEARLY
+    // the windows of tile c+2 as soon as their registers are free
+    {
+        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
+        off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
+        cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
+    }
+#endif
     __builtin_amdgcn_wave_barrier();
     const uint32_t i = t * 64u + lane;
     const bool live = jt < nt_w && i < a.n;
@@ -1680,7 +1727,8 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                     break;
                 uint32_t u = k < 2 ? (f4 ? V[k + 1] : V[k]) : k == 2 ? (f4 ? (l4ok ? V[3] : 0u) : V[2])
                            : k < 8 ? (f4 ? 0u : V[k]) : (f4 || !l4ok ? 0u : V[8]);
-                na.h ^= tz4(s_t, 4 * k, u);
+                if (!(CD_ABL & 1))
+                    na.h ^= tz4(s_t, 4 * k, u);
             }
         }
         // both families' input-node pieces, straight-line, then selects: the
@@ -1716,15 +1764,18 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             tb0 = a.dir16 ? a.dir16 : a.tbl24;
         na.ptf = pt | flags | (1u << 18) | (pe << 19);
     }
-    na.e = tb0[idx0]; // first gather, unconditional
+    // (the ablation's stand-in has bit 0 clear: no chain level follows it)
+    na.e = (CD_ABL & 4) ? (idx0 & 0xffu) << 1 : tb0[idx0]; // first gather, unconditional
     // offsets one tile further, then the windows of tile c+2 (issued after
     // the first gather: the next trip's wait for the gather leaves them in
     // flight when no lane of the wave needs a further level)
+#if !CD_WEARLY
     {
         const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
         cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
     }
+#endif
     // B's results
     {
         const KAS KArgs &o = kargs_fresh(a);
@@ -1779,11 +1830,11 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 __builtin_nontemporal_store(sb.ipl, &at32(o.iplen, ib));
             // non-temporal stores: the outputs are written once and must not
             // push the FIB tables of the gather chains out of L2 (C4 -4.5%)
-            if (o.nh)
+            if (!(CD_ABL & 16) && o.nh)
                 __builtin_nontemporal_store(nh, &at32(o.nh, ib));
-            if (o.hash)
+            if (!(CD_ABL & 16) && o.hash)
                 __builtin_nontemporal_store(sb.h, &at32(o.hash, ib));
-            if (o.queue)
+            if (!(CD_ABL & 16) && o.queue)
                 __builtin_nontemporal_store((uint16_t)q, &at16(o.queue, ib));
             if (o.edge)
                 __builtin_nontemporal_store((uint8_t)edge, &o.edge[ib]);
@@ -5842,6 +5893,7 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 #define MQ_ADDR_MASK ((1ull << 56) - 1ull) // frame word: device address | readable bytes (<= 255) << 56
 #define MQ_RW_TAIL 1ull     // ip4_rewrite: the frame takes the tail loop's checksum rule
 #define MQ_MD_LEN 40u       // struct cnet_metadata {faddr, laddr} (cnet_meta.h:20-25, cne_inet.h:37-45)
+#define CNDP_MQ_POOLS 4u    // cnet device headers: pools whose pktmbuf_metadata is the default m + 64
 #define MQ_AF_INET 2u
 #define MQ_AF_INET6 10u
 
@@ -5918,12 +5970,21 @@ struct MqArgs {
     const u32x4 *win;       // cnet: each fast-parsed or general-parsed frame's first 64 bytes
     const struct cndp_rw_nh *rw; // rewrite: next-hop table (device)
     uint32_t lport, want_hash;
-    uint32_t devhdr;        // ip4_lookup zc, CNDP_MQ_F_DEVICE_HEADERS: the kernel reads each mbuf's
-    uint32_t nrg;           //   header itself; its frame lies in one of the nrg registered regions
-    struct {                //   (host address range, device = host + delta)
-        uint64_t host, len;
+    uint32_t devhdr;        // zc, CNDP_MQ_F_DEVICE_HEADERS: the kernels read each mbuf's header
+    uint32_t nrg;           //   themselves; ip4_lookup: its frame lies in one of the nrg registered
+    struct {                //   regions (host address range, device = host + delta); cnet: rg[0]
+        uint64_t host, len; //   is the batch's region
         int64_t delta;
     } rg[CNDP_MAX_REGIONS];
+    // cnet with device headers (k_mq_cnet_hdr): the frame offsets, length
+    // fields and metadata addresses it derives (device arrays, the metadata
+    // addresses also into the pinned array poll reads); pktmbuf_metadata is
+    // m + 64 for the mbufs of md_pool[0..n_pool) (all of them with md_all)
+    uint64_t *w_off;
+    u32x2 *w_lens;
+    uint64_t *w_md, *w_mdh;
+    uint32_t n_pool, md_all;
+    uint64_t md_pool[CNDP_MQ_POOLS];
     MqTables tb;
     uint32_t *ticket;       // device arrival counter of this slot
     uint32_t *flag;         // device view of the slot's pinned completion flag
@@ -6219,6 +6280,47 @@ __device__ void mq_save_md(uint8_t *d, const u32x4 *w, const uint8_t *fr, uint64
 // frame to the edge of a type with the same low byte (ptype.c:109-110).
 // Zero-copy: the eth_rx fields (eth_rx.c:35-63), data_len and the metadata go
 // straight into the mbuf; staged: into records for poll.
+// cnet with CNDP_MQ_F_DEVICE_HEADERS: what mq_fill derives on the host from
+// each mbuf's header line, read here instead (one 32-B read per mbuf: pooldata,
+// buf_addr, data_off, buf_len, data_len, pktmbuf.h:102-112) -- the frame's
+// offset in the batch's region (its end when outside), the length fields, and
+// the metadata address when the mbuf's pool keeps it at m + 64
+// (pktmbuf_metadata's default, pktmbuf.h:1209-1220); else 0, and poll writes
+// the metadata through conf.metadata
+__global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_hdr(MqArgs a)
+{
+    const uint64_t host = a.rg[0].host, len = a.rg[0].len;
+    for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
+        const uint64_t m = a.mb[i];
+        uint64_t fo = len, md = 0;
+        u32x2 l = {0u, 0u};
+        if (m) {
+            const u32x4 h0 = *gp((const u32x4 *)(uintptr_t)m);        // pooldata, buf_addr
+            const u32x4 h1 = *gp((const u32x4 *)(uintptr_t)(m + 16)); // hash, meta_index, data_off .. data_len
+            const uint64_t pool = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+            const uint64_t buf = (uint64_t)h0.z | ((uint64_t)h0.w << 32);
+            const uint32_t doff = h1.z & 0xffffu, blen = h1.w & 0xffffu, dlen = h1.w >> 16;
+            const uint32_t room = blen > doff ? blen - doff : 0u;
+            const uint64_t f = buf + doff; // pktmbuf_mtod, a host address
+            if (f - host < len)
+                fo = f - host;
+            l.x = dlen | (room << 16);
+            l.y = blen | (doff << 16);
+            bool def = a.md_all != 0u;
+            for (uint32_t k = 0; k < a.n_pool; k++)
+                def = def || pool == a.md_pool[k];
+            md = def ? m + 64u : 0u;
+        }
+        a.w_off[i] = fo;
+        a.w_lens[i] = l;
+        if (a.w_md) {
+            a.w_md[i] = md;
+            a.w_mdh[i] = md; // pinned: poll's writeback reads it
+        }
+    }
+    __threadfence_system();
+}
+
 __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
@@ -6326,7 +6428,12 @@ struct cndp_gpu_mq {
     uint32_t *tickets;             // device, one per slot
     // byte offsets inside each slot's pinned block (H) and device block (D)
     uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_stage, h_bytes;
-    uint64_t d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_win, d_bytes;
+    uint64_t d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_win, d_off, d_len, d_md, d_bytes;
+    int devhdr;                    // zc with CNDP_MQ_F_DEVICE_HEADERS (ip4_lookup, cnet)
+    // cnet device headers: pools seen whose conf.metadata(m) is m + 64 (and
+    // those whose is not), learnt from the first mbuf of a burst
+    uint32_t n_pool, n_pool_ext;
+    uint64_t pool[CNDP_MQ_POOLS], pool_ext[CNDP_MQ_POOLS];
     uint32_t head, open, in_flight, seq; // head: oldest slot not fully polled
     uint32_t pending;
     int err;                       // a launch error not yet reported (returned by the next submit)
@@ -6434,7 +6541,11 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->d_hash = q->d_rm + al64(B * 4);
     q->d_ipl = q->d_hash + al64(B * 4);
     q->d_win = q->d_ipl + al64(B * 4);
-    q->d_bytes = cnet ? q->d_win + (zc ? B * 64 : 0) : 64;
+    q->devhdr = zc && (k.flags & CNDP_MQ_F_DEVICE_HEADERS) && (k.mode == CNDP_MQ_IP4_LOOKUP || cnet);
+    q->d_off = q->d_win + (zc ? B * 64 : 0);
+    q->d_len = q->d_off + (cnet && q->devhdr ? al64(B * 8) : 0);
+    q->d_md = q->d_len + (cnet && q->devhdr ? al64(B * 8) : 0);
+    q->d_bytes = cnet ? q->d_md + (q->devhdr ? al64(B * 8) : 0) : 64;
     r = -ENOMEM;
     if (hipStreamCreateWithFlags(&q->s, hipStreamNonBlocking) != hipSuccess)
         goto fail;
@@ -6583,7 +6694,7 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = tbl_acquire(&c->fib4->t, s, &v4)))
             return r;
         a.tb = mq_tables(c, v4, nullptr, 0);
-        if (zc && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS)) { // frames in any registered region
+        if (q->devhdr) { // frames in any registered region
             a.devhdr = 1;
             a.nrg = (uint32_t)q->nrg;
             for (int k = 0; k < q->nrg; k++) {
@@ -6598,6 +6709,26 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         // one classify per run of equal-size graph bursts, the ptype node's
         // speculation run with that burst size, its state carried in the
         // context from run to run and batch to batch
+        if (q->devhdr) { // the headers read on the device first (k_mq_cnet_hdr)
+            const MqRegion &br = q->rg[sl->rg >= 0 ? sl->rg : 0];
+            a.devhdr = 1;
+            a.nrg = 1;
+            a.rg[0].host = (uint64_t)(uintptr_t)br.host;
+            a.rg[0].len = br.len;
+            a.rg[0].delta = br.delta;
+            a.w_off = (uint64_t *)(D + q->d_off);
+            a.w_lens = (u32x2 *)(D + q->d_len);
+            a.w_md = a.md ? (uint64_t *)(D + q->d_md) : nullptr;
+            a.w_mdh = (uint64_t *)(HD + q->h_md);
+            a.md_all = q->conf.metadata == nullptr;
+            a.n_pool = q->n_pool;
+            for (uint32_t k = 0; k < q->n_pool; k++)
+                a.md_pool[k] = q->pool[k];
+            hipLaunchKernelGGL(k_mq_cnet_hdr, dim3(g), dim3(MQ_TPB), 0, s, a);
+            a.off = a.w_off;
+            a.lens = a.w_lens;
+            a.md = a.w_md;
+        }
         const uint32_t saved_B = c->spec_burst;
         uint32_t i0 = 0;
         for (uint32_t k = 0; k < sl->nrun && !r; k++) {
@@ -6693,23 +6824,50 @@ static inline uint8_t *mq_md_host(const cndp_gpu_mq_t *q, uint8_t *m)
     return q->conf.metadata ? (uint8_t *)q->conf.metadata(m) : m + 64;
 }
 
+// cnet device headers: whether m's pool keeps pktmbuf_metadata at m + 64, from
+// conf.metadata on the first mbuf of a burst whose pool (pooldata, word 0 of
+// the header) is new -- one header read per burst, not per mbuf.  A pool not
+// in either list (both full) has its mbufs' metadata written by poll.
+static void mq_learn_pool(cndp_gpu_mq_t *q, void *m)
+{
+    const uint64_t pool = *(const uint64_t *)m;
+    for (uint32_t k = 0; k < q->n_pool; k++)
+        if (q->pool[k] == pool)
+            return;
+    for (uint32_t k = 0; k < q->n_pool_ext; k++)
+        if (q->pool_ext[k] == pool)
+            return;
+    if ((uint8_t *)q->conf.metadata(m) == (uint8_t *)m + 64) {
+        if (q->n_pool < CNDP_MQ_POOLS)
+            q->pool[q->n_pool++] = pool;
+    } else if (q->n_pool_ext < CNDP_MQ_POOLS) {
+        q->pool_ext[q->n_pool_ext++] = pool;
+    }
+}
+
 // one burst of k mbufs into the open slot sl (room checked by the caller)
 static void mq_fill(cndp_gpu_mq_t *q, MqSlot *sl, void *const *mbufs, uint32_t k)
 {
     const uint32_t mode = q->conf.mode;
     const bool cnet = mode == CNDP_MQ_CNET, rw = mode == CNDP_MQ_IP4_REWRITE, zc = q->zc != 0;
     const bool want_md = cnet && zc && !(q->conf.flags & CNDP_MQ_F_NO_METADATA);
-    const bool devhdr = zc && mode == CNDP_MQ_IP4_LOOKUP && (q->conf.flags & CNDP_MQ_F_DEVICE_HEADERS);
+    const bool devhdr = q->devhdr != 0;
     uint8_t *H = sl->h;
     uint64_t *hmb = (uint64_t *)(H + q->h_mb), *hoff = (uint64_t *)(H + q->h_off);
     uint64_t *hlen = (uint64_t *)(H + q->h_len), *hmd = (uint64_t *)(H + q->h_md);
     const uint32_t vec = k & ~3u; // ip4_rewrite: the 4-wide loop's share of the burst
-    if (devhdr) { // the kernel reads the headers (CNDP_MQ_F_DEVICE_HEADERS): pointers only
+    if (devhdr) { // the kernels read the headers (CNDP_MQ_F_DEVICE_HEADERS): pointers only
+        // cnet: the default metadata (m + 64) must lie in the mbuf's region too
+        const uint64_t need = want_md ? 64u + 64u + MQ_MD_LEN : 64u;
+        if (want_md && q->conf.metadata && k)
+            mq_learn_pool(q, mbufs[0]);
         for (uint32_t i = 0; i < k; i++) {
             uint8_t *m = (uint8_t *)mbufs[i];
-            const int km = mq_region(q, m, 64);
+            const int km = mq_region(q, m, need);
             sl->mb[sl->n + i] = m;
             hmb[sl->n + i] = km < 0 ? 0u : (uint64_t)(intptr_t)(m + q->rg[km].delta);
+            if (cnet && sl->rg < 0 && km >= 0) // the batch's region: its first mbuf's
+                sl->rg = km;
         }
         return;
     }

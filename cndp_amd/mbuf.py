@@ -108,13 +108,20 @@ class MbufPool:
 class MbufQueue:
     """cndp_gpu_mq_* over a Classifier's context."""
 
+    METADATA_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p)
+
     def __init__(self, cl, mode: int, flags: int = 0, batch: int = 8192, depth: int = 4,
-                 max_delay_us: int = 50, umem=None, lport: int = 0, stage_max: int = 0):
+                 max_delay_us: int = 50, umem=None, lport: int = 0, stage_max: int = 0, metadata=None):
+        """metadata: cnet's pktmbuf_metadata hook, a Python function of the mbuf
+        address returning the metadata address (None: m + 64)."""
         self._L = N.lib()
         c = N.MqConf()
         c.mode, c.flags, c.batch, c.depth = mode, flags, batch, depth
         c.max_delay_us, c.stage_max, c.lport = max_delay_us, stage_max, lport
         c.umem = umem
+        self._md_fn = self.METADATA_FN(metadata) if metadata else None  # kept alive with the queue
+        if self._md_fn:
+            c.metadata = ctypes.cast(self._md_fn, ctypes.c_void_p)
         h = ctypes.c_void_p()
         N.check(self._L.cndp_gpu_mq_create(cl.h, ctypes.byref(c), ctypes.byref(h)), "cndp_gpu_mq_create")
         self.h = h

@@ -223,11 +223,18 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
 #define CNDP_MQ_IP4_REWRITE 3u
 #define CNDP_MQ_F_HASH (1u << 0)
 #define CNDP_MQ_F_NO_METADATA (1u << 1) /* cnet: leave cnet_metadata unwritten */
-/* ip4_lookup zero-copy: the host hands over mbuf pointers only and the kernel
- * reads each header (buf_addr, data_off) in place -- no host touch per mbuf,
- * three dependent PCIe reads per mbuf instead of one; frames in any region the
- * context registered.  The GPU ip4_lookup node's default (ip4_lookup_gpu.c):
- * its host thread, not the device, bounds the node rate. */
+/* Zero-copy ip4_lookup and cnet: the host hands over mbuf pointers only and
+ * the kernels read each header (buf_addr, data_off, the lengths) in place --
+ * no host touch per mbuf, dependent PCIe reads per mbuf instead of one.
+ * ip4_lookup: frames in any region the context registered.  cnet: a batch's
+ * region is its first mbuf's (frames elsewhere come back with
+ * CNDP_MQ_EDGE_NONE), and cnet_metadata is written by the device for the
+ * mbufs of pools whose conf.metadata(m) is m + 64 -- learnt per pool
+ * (pooldata, header word 0) from the first mbuf of a burst, so the hook must
+ * depend on the mbuf's pool only, as pktmbuf_metadata does -- and by poll
+ * through the hook for the others.  The default of the GPU ip4_lookup and
+ * eth_rx nodes: their host thread, not the device, bounds the node rate
+ * (DESIGN.md §6). */
 #define CNDP_MQ_F_DEVICE_HEADERS (1u << 2)
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u

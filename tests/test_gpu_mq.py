@@ -282,14 +282,18 @@ def cnet_check(pool, orig, ref, t4, t6, lport, check_md=True):
     return (node << 8) | np.where(at_input, e_in, e8 & 0x7F)
 
 
-@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_cnet(cn, gpu, zero_copy, kind):
+    """"device_headers": zero-copy with CNDP_MQ_F_DEVICE_HEADERS (k_mq_cnet_hdr
+    reads each mbuf's header on the device)."""
     cl, routes, v6, t4, t6 = cn
     n = 24000
-    pool, orig = cnet_pool(n, routes, v6, zero_copy, shift=kind == "shifted")
+    pool, orig = cnet_pool(n, routes, v6, bool(zero_copy), shift=kind == "shifted")
     umem = None
     flags = N.CNDP_MQ_F_HASH if kind == "ragged" else 0
+    if zero_copy == "device_headers":
+        flags |= N.CNDP_MQ_F_DEVICE_HEADERS
     if zero_copy:
         cl.host_register(pool.mem)
         umem = pool.base
@@ -316,6 +320,60 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
     # every node and edge kind shows up
     assert {0, 1, 2} <= set(np.unique(node).tolist())
     assert (want_e == ((N.CNDP_MQ_NODE_PTYPE << 8) | 5)).sum() > 0   # gtpu
+
+
+def test_mq_cnet_device_headers_metadata_hook(cn, gpu):
+    """CNDP_MQ_F_DEVICE_HEADERS with a pktmbuf_metadata hook: mbufs of a pool
+    whose metadata is the default m + 64 get it from the device, those of a
+    pool with a metadata array (pktmbuf.h:1216-1217) from poll through the
+    hook -- both as the host-header path writes them."""
+    cl, routes, v6, t4, t6 = cn
+    n = 6000
+    pool, orig = cnet_pool(n, routes, v6, True)
+    pool_a, pool_b = 0x1111000, 0x2222000
+    pool.hdr["pooldata"][:] = pool_a
+    pool.hdr["pooldata"][1::3] = pool_b
+    orig = pool.hdr.copy()
+    ext = np.full((n, MD_LEN), MD_FILL, np.uint8)   # pool_b's metadata array
+    ext_base = ext.ctypes.data
+    base = pool.base
+
+    def hook(m):
+        i = (m - base) // 2048
+        return m + 64 if int(pool.hdr["pooldata"][i]) == pool_a else ext_base + i * MD_LEN
+
+    order = np.arange(n)
+    bursts = _bursts(n, 5, "full")
+    cl.host_register(pool.mem)
+    try:
+        cl.set_tuning(cnet_spec=256)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=N.CNDP_MQ_F_DEVICE_HEADERS, batch=2048, depth=3,
+                      umem=pool.base, lport=3, metadata=hook)
+        ref = _cnet_expect(pool, order, bursts, t4, t6, 0, 3)
+        addrs, edges = q.run(pool, order, bursts)
+        q.close()
+    finally:
+        cl.host_unregister(pool.mem)
+    assert np.array_equal(pool.index_of(addrs), order)
+    want_e = cnet_check(pool, orig, ref, t4, t6, 3, check_md=False)
+    assert np.array_equal(edges.astype(np.int64), want_e)
+    # the metadata: pool_a's at m + 64, pool_b's in the array (and m + 64 untouched)
+    h = pool.hdr
+    l2 = (ref["rxmeta"] & 0x7F).astype(np.int64)
+    adj = (l2 <= orig["data_len"].astype(np.int64)) & \
+          (l2 + orig["data_off"].astype(np.int64) <= orig["buf_len"].astype(np.int64))
+    mt = np.arange(n, dtype=np.int64) * 2048 + HDR + np.where(adj, orig["data_off"] + l2, orig["data_off"])
+    at_input = ref["edge"].astype(np.int64) < 0x80
+    low = ref["ptype"] & 0xFF
+    v6m = (low == 0x41) | (low == 0xC1) | (low == 0xE1)
+    want = md_expect(pool.mem, n, mt, at_input, v6m)
+    in_b = h["pooldata"] == pool_b
+    got_a = pool.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN]
+    assert np.array_equal(got_a[~in_b], want[~in_b])
+    assert np.all(got_a[in_b] == MD_FILL)
+    assert np.array_equal(ext[in_b], want[in_b])
+    assert np.all(ext[~in_b] == MD_FILL)
+    assert at_input[in_b].sum() > 100 and at_input[~in_b].sum() > 100
 
 
 @pytest.mark.parametrize("zero_copy", [True, False])

@@ -207,12 +207,14 @@ def _edge_of_queue_code(e):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("zero_copy", [True, "host_headers", False])
 def test_cnet_node_graph_walk(gpu, zero_copy):
     """Graph walks over the GPU eth_rx node: it pulls 256-mbuf bursts from its
     port, and every mbuf leaves by the edge the reference's ptype /
     ip4_input / ip6_input would have sent it to, with the fields eth_rx and the
-    input nodes write (the oracle over the same bursts, node state from 0)."""
+    input nodes write (the oracle over the same bursts, node state from 0).
+    Zero-copy with the node's default device headers, and with the host
+    reading them (CNDP_GPU_MQ_FLAGS=0)."""
     from helpers import CNET_DEF, cnet_fibs
     from oracle import oracle as O
     from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
@@ -222,9 +224,11 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
     t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
     t6 = O.trie_build(v6vals, CNET_DEF, 1 << 15)
     n, port = 24000, 3
-    pool, orig = cnet_pool(n, routes, v6, zero_copy)
+    pool, orig = cnet_pool(n, routes, v6, bool(zero_copy))
     ref = _cnet_expect(pool, np.arange(n), _bursts(n, 0, "full"), t4, t6, 0, port)
     L.cndp_node_gpu_umem_reset()
+    if zero_copy == "host_headers":
+        os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
     if zero_copy:
         L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
     H.harness_cnet_set(fib.h, fib6.h)
@@ -233,6 +237,7 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
     assert H.harness_rx_load(port, ptrs, n) == 0
     try:
         assert H.harness_graph_create(5) == 0
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         assert H.harness_walk_until(n) >= 0
         assert H.harness_rx_left(port) == 0 and H.harness_total() == n
         got = np.full(n, -1, np.int64)
@@ -243,6 +248,7 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
             assert np.all(np.diff(idx) > 0), f"{name}: out of receive order"
             got[idx] = k
     finally:
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         H.harness_graph_destroy()
         L.cndp_node_gpu_umem_reset()
     want_e = cnet_check(pool, orig, ref, t4, t6, port)

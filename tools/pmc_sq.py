@@ -1,38 +1,36 @@
-"""Per-kernel means of the SQ counters in rocprofv3 counter_collection.csv
-files (this library's kernels only), with the derived wave lifetime split.
-SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
-(MI355X_MICROARCH.md); the derived columns are per wave, in cycles."""
-import collections
+#!/usr/bin/env python3
+"""Summarise tools/pmc_sq.sh: per program and kernel, the median over its
+dispatches of each SQ counter, and per-wave figures (counter / SQ_WAVES).
+    python tools/pmc_sq.py gpurun_out/sq_<tag> [--json out]"""
 import csv
-import re
+import glob
+import json
+import os
+import statistics
 import sys
 
-OURS = re.compile(r"\bk_\w+")
 
-
-def main(paths):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for p in paths:
-        with open(p) as f:
-            for r in csv.DictReader(f):
-                m = OURS.search(r["Kernel_Name"])
-                if not m:
-                    continue
-                name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-                acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for name, ctr in sorted(acc.items()):
-        mean = {k: sum(v) / len(v) for k, v in ctr.items()}
-        line = [f"{name:40s}"] + [f"{k}={v:.4g}" for k, v in sorted(mean.items())]
-        waves = mean.get("SQ_WAVES", 0)
-        if waves:
-            for k in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-                if k in mean:
-                    line.append(f"{k}/wave(cyc)={4 * mean[k] / waves:.0f}")
-            for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS"):
-                if k in mean:
-                    line.append(f"{k}/wave={mean[k] / waves:.0f}")
-        print(" ".join(line))
+def main():
+    d = sys.argv[1]
+    vals = {}
+    for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
+        prog = os.path.relpath(f, d).split(os.sep)[0].rsplit("_p", 1)[0]
+        for r in csv.DictReader(open(f)):
+            k = prog + ":" + r["Kernel_Name"].replace("void ", "").split("(")[0]
+            vals.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    res = {}
+    for k, cs in sorted(vals.items()):
+        m = {c: statistics.median(v) for c, v in cs.items()}
+        w = m.get("SQ_WAVES")
+        r = {"counters": m}
+        if w:
+            r["per_wave"] = {c: round(v / w, 1) for c, v in m.items() if c != "SQ_WAVES"}
+        res[k] = r
+        print(k, json.dumps(r.get("per_wave", m)))
+    if "--json" in sys.argv:
+        with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+            json.dump(res, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    main()
