@@ -1543,15 +1543,6 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #ifndef CD_ABL
 #define CD_ABL 0
 #endif
-// 1: tile c+2's windows issued right after tile c is staged (before its
-// parse) instead of after its first gather (A/B)
-#ifndef CD_WEARLY
-#define CD_WEARLY 0
-#endif
-// the chain's levels unrolled (1) or a loop over a shifting key (0, round 3)
-#ifndef CD_UNROLL
-#define CD_UNROLL 1
-#endif
 template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
 {
     const GAS T *g = (const GAS T *)p;
@@ -1585,29 +1576,6 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const GAS uint32_t *const t6 = sgpr_pin(a.tbl8_6), *const t8 = sgpr_pin(a.tbl8);
         const GAS uint32_t *const t4 = sgpr_pin(a.dir16 ? a.pages : a.tbl8);
         bool more = bv & (d4 | d6) & ((eb & 1u) != 0u);
-#if CD_UNROLL
-        // the levels unrolled: each level's key byte at a fixed place, the
-        // family's last level a lane mask (v4: 1, 2 with the /16 directory;
-        // v6: 13), and from the third level on only IPv6 lanes are left, so
-        // the table base is uniform (t6) -- 5 VALU a level instead of 13
-        (void)rem;
-        const uint32_t q[4] = {sb.q0, sb.q1, sb.q2, sb.q3};
-        // "more" as bit 0 of a VGPR: one AND with the entry a level (a lane
-        // mask turned into a ballot costs a select and a compare)
-        const uint32_t g0 = d6 || a.dir16 != nullptr ? 1u : 0u, g1 = d6 ? 1u : 0u;
-        uint32_t mv = more ? 1u : 0u;
-#pragma unroll
-        for (int k = 0; k < 13; k++) {
-            const bool live = mv != 0u; // mv is 0 or 1
-            if ((CD_ABL & 2) || !__builtin_amdgcn_ballot_w64(live))
-                break;
-            // ((eb >> 1) << 8) | key byte k: bytes 1..3 of eb << 7, byte k & 3 of its word
-            const uint32_t idx = __builtin_amdgcn_perm(eb << 7, q[k >> 2], 0x07060500u | (uint32_t)(k & 3));
-            if (live)
-                eb = k == 0 ? (d6 ? t6 : t4)[idx] : k == 1 ? (d6 ? t6 : t8)[idx] : t6[idx];
-            mv &= k == 0 ? eb & g0 : k == 1 ? eb & g1 : eb;
-        }
-#else
         const GAS uint32_t *tb = d6 ? t6 : t4;
         const GAS uint32_t *const tb2 = d6 ? t6 : t8;
         uint32_t q0 = sb.q0, q1 = sb.q1, q2 = sb.q2, q3 = sb.q3;
@@ -1623,7 +1591,6 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             rem--;
             more = more & ((eb & 1u) != 0u) & (rem != 0u);
         }
-#endif
     }
     // A: tile c
 #pragma unroll
@@ -1631,14 +1598,6 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         const uint32_t f = 16u * k + fr_in_k;
         tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
     }
-#if CD_WEARLY
-    // the windows of tile c+2 as soon as their registers are free
-    {
-        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
-        off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
-        cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
-    }
-#endif
     __builtin_amdgcn_wave_barrier();
     const uint32_t i = t * 64u + lane;
     const bool live = jt < nt_w && i < a.n;
@@ -1769,13 +1728,11 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     // offsets one tile further, then the windows of tile c+2 (issued after
     // the first gather: the next trip's wait for the gather leaves them in
     // flight when no lane of the wave needs a further level)
-#if !CD_WEARLY
     {
         const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
         cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
     }
-#endif
     // B's results
     {
         const KAS KArgs &o = kargs_fresh(a);
