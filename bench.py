@@ -606,13 +606,14 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         return round(nc * passes / t / 1e6, 2) if t > 0 else None
 
     # interleaved, two rounds (box noise), the median reported and both kept;
-    # the device-header queue is the eth_rx node's default (its host thread
-    # hands over mbuf pointers only), host headers the round-3 path
-    cvars = [("gpu_zero_copy", lambda: cnet_queue(True, D)),
-             ("gpu_zero_copy_host_headers", lambda: cnet_queue(True, 0)),
+    # host headers (the eth_rx node's default) against the device reading
+    # them (CNDP_MQ_F_DEVICE_HEADERS: k_mq_cnet_hdr, one more launch and a
+    # PCIe read per mbuf before the classify)
+    cvars = [("gpu_zero_copy", lambda: cnet_queue(True, 0)),
+             ("gpu_zero_copy_device_headers", lambda: cnet_queue(True, D)),
              ("gpu_staged", lambda: cnet_queue(False, 0)),
-             ("eth_rx_node_zero_copy", lambda: cnet_node(True, D)),
-             ("eth_rx_node_zero_copy_host_headers", lambda: cnet_node(True, 0)),
+             ("eth_rx_node_zero_copy", lambda: cnet_node(True, 0)),
+             ("eth_rx_node_zero_copy_device_headers", lambda: cnet_node(True, D)),
              ("eth_rx_node_staged", lambda: cnet_node(False, 0))]
     rounds = {k: [] for k, _ in cvars}
     for _ in range(2):
@@ -711,17 +712,28 @@ def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
             tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = 12, nh % 4 + 1, 1
             tbl[nh]["rewrite_data"][:] = np.frombuffer(data + bytes(44), np.uint8)
         H.harness_chain(1)
-        for zc in (True, False):
+        # the two queues' header forms (lookup / rewrite): both on the device
+        # (the nodes' defaults), the rewrite's on the host, both on the host;
+        # then staged
+        D = N.CNDP_MQ_F_DEVICE_HEADERS
+        for gid, (key, zc, fl, frw) in enumerate((("gpu_zero_copy", True, D, D),
+                                                  ("gpu_zero_copy_rewrite_host_headers", True, D, 0),
+                                                  ("gpu_zero_copy_host_headers", True, 0, 0),
+                                                  ("gpu_staged", False, 0, 0))):
             L.cndp_node_gpu_umem_reset()
             if zc:
                 L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
-            assert H.harness_graph_create(30 + int(zc)) == 0
+            os.environ["CNDP_GPU_MQ_FLAGS"] = str(fl)
+            os.environ["CNDP_GPU_RW_MQ_FLAGS"] = str(frw)
+            assert H.harness_graph_create(30 + gid) == 0
+            os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+            os.environ.pop("CNDP_GPU_RW_MQ_FLAGS", None)
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
             H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
             t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
             H.harness_graph_destroy()
-            out["gpu_zero_copy_Mpps" if zc else "gpu_staged_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+            out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
         fib = NodeFib()
         t24, t8 = (x.copy() for x in fib.image())
         O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, 1)

@@ -6140,6 +6140,33 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_rewrite(MqArgs a)
         const bool tail = (a.mb[i] & MQ_RW_TAIL) != 0u;
         uint8_t *p;
         uint32_t avail;
+        uint64_t pv;
+        if (a.devhdr) { // the mbuf's device address | tail flag: its header read here
+            const uint64_t m = a.mb[i] & ~MQ_RW_TAIL;
+            uint64_t fh = 0, fo = ~0ull, rlen = 0;
+            int64_t delta = 0;
+            if (m) {
+                const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
+                fh = *gp((const uint64_t *)(dm + MB_BUF_ADDR)) + *gp((const uint16_t *)(dm + MB_DATA_OFF));
+                for (uint32_t k = 0; k < a.nrg; k++) // the frame's registered region
+                    if (fh - a.rg[k].host < a.rg[k].len) {
+                        fo = fh - a.rg[k].host;
+                        rlen = a.rg[k].len;
+                        delta = a.rg[k].delta;
+                        break;
+                    }
+            }
+            if (fo == ~0ull) {
+                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
+                continue;
+            }
+            pv = *gp((const uint64_t *)((const uint8_t *)(uintptr_t)m + MB_UDATA64)); // node_mbuf_priv1
+            p = (uint8_t *)(uintptr_t)(fh + delta);
+            avail = rlen - fo < 255u ? (uint32_t)(rlen - fo) : 255u;
+            a.edges[i] = (uint16_t)mq_rewrite_frame(p, avail, pv, tail, a.rw);
+            continue;
+        }
+        pv = a.priv[i];
         if (a.zc) {
             p = mq_frame(a.off[i], avail);
             if (p == nullptr) {
@@ -6150,7 +6177,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_rewrite(MqArgs a)
             p = (uint8_t *)a.slab + a.off[i];
             avail = MQ_RW_STAGE;
         }
-        a.edges[i] = (uint16_t)mq_rewrite_frame(p, avail, a.priv[i], tail, a.rw);
+        a.edges[i] = (uint16_t)mq_rewrite_frame(p, avail, pv, tail, a.rw);
     }
     mq_complete(a);
 }
@@ -6498,7 +6525,7 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->d_hash = q->d_rm + al64(B * 4);
     q->d_ipl = q->d_hash + al64(B * 4);
     q->d_win = q->d_ipl + al64(B * 4);
-    q->devhdr = zc && (k.flags & CNDP_MQ_F_DEVICE_HEADERS) && (k.mode == CNDP_MQ_IP4_LOOKUP || cnet);
+    q->devhdr = zc && (k.flags & CNDP_MQ_F_DEVICE_HEADERS) && k.mode != CNDP_MQ_MAC_SWAP;
     q->d_off = q->d_win + (zc ? B * 64 : 0);
     q->d_len = q->d_off + (cnet && q->devhdr ? al64(B * 8) : 0);
     q->d_md = q->d_len + (cnet && q->devhdr ? al64(B * 8) : 0);
@@ -6645,6 +6672,15 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = rw_sync(c, s)))
             return r;
         a.rw = c->d_rw_tbl;
+        if (q->devhdr) { // frames in any registered region
+            a.devhdr = 1;
+            a.nrg = (uint32_t)q->nrg;
+            for (int k = 0; k < q->nrg; k++) {
+                a.rg[k].host = (uint64_t)(uintptr_t)q->rg[k].host;
+                a.rg[k].len = q->rg[k].len;
+                a.rg[k].delta = q->rg[k].delta;
+            }
+        }
         hipLaunchKernelGGL(k_mq_ip4_rewrite, dim3(g), dim3(MQ_TPB), 0, s, a);
     } else if (!cnet) {
         TblView v4{};
@@ -6823,6 +6859,8 @@ static void mq_fill(cndp_gpu_mq_t *q, MqSlot *sl, void *const *mbufs, uint32_t k
             const int km = mq_region(q, m, need);
             sl->mb[sl->n + i] = m;
             hmb[sl->n + i] = km < 0 ? 0u : (uint64_t)(intptr_t)(m + q->rg[km].delta);
+            if (rw && km >= 0 && i >= vec) // ip4_rewrite's tail loop (bit 0: mbufs are 64-B aligned)
+                hmb[sl->n + i] |= MQ_RW_TAIL;
             if (cnet && sl->rg < 0 && km >= 0) // the batch's region: its first mbuf's
                 sl->rg = km;
         }

@@ -307,10 +307,10 @@ static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
     conf.depth = env_u32("CNDP_GPU_DEPTH", 4);
     conf.max_delay_us = env_u32("CNDP_GPU_DELAY_US", 50);
     conf.metadata = rx_metadata;
-    /* the kernels read each mbuf header themselves (k_mq_cnet_hdr): the host
-     * thread hands over pointers only; CNDP_GPU_MQ_FLAGS=0 for the host-header
-     * path */
-    conf.flags = env_u32("CNDP_GPU_MQ_FLAGS", CNDP_MQ_F_DEVICE_HEADERS);
+    /* the host resolves each frame from the mbuf header (measured faster here
+     * than the device reading the headers over PCIe: 70-75 against 61 Mpps,
+     * DESIGN.md §6); CNDP_GPU_MQ_FLAGS=4 for CNDP_MQ_F_DEVICE_HEADERS */
+    conf.flags = env_u32("CNDP_GPU_MQ_FLAGS", 0);
     /* zero-copy: the kernels read the frames in the UMEMs (registration is
      * shared and counted across the per-port contexts) */
     void *umem = NULL;

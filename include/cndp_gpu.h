@@ -233,8 +233,9 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
  * (pooldata, header word 0) from the first mbuf of a burst, so the hook must
  * depend on the mbuf's pool only, as pktmbuf_metadata does -- and by poll
  * through the hook for the others.  The default of the GPU ip4_lookup and
- * eth_rx nodes: their host thread, not the device, bounds the node rate
- * (DESIGN.md §6). */
+ * ip4_rewrite nodes, whose host thread, not the device, bounds the node rate;
+ * not of eth_rx, whose batch the extra header pass over PCIe slows more than
+ * the host saves. */
 #define CNDP_MQ_F_DEVICE_HEADERS (1u << 2)
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u

@@ -610,7 +610,7 @@ def _rewrite_setup(cl, seed):
     return tbl
 
 
-@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
     """The ip4_rewrite node over pktmbuf bursts, byte for byte against the
@@ -649,8 +649,9 @@ def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
     if zero_copy:
         cl.host_register(gpool.mem)
         umem = gpool.base
+    flags = N.CNDP_MQ_F_DEVICE_HEADERS if zero_copy == "device_headers" else 0
     try:
-        q = MbufQueue(cl, N.CNDP_MQ_IP4_REWRITE, batch=4096, depth=3, umem=umem)
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_REWRITE, flags=flags, batch=4096, depth=3, umem=umem)
         addrs, edges = q.run(gpool, order, bursts)
         q.close()
     finally:

@@ -207,14 +207,14 @@ def _edge_of_queue_code(e):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, "host_headers", False])
+@pytest.mark.parametrize("zero_copy", [True, "device_headers", False])
 def test_cnet_node_graph_walk(gpu, zero_copy):
     """Graph walks over the GPU eth_rx node: it pulls 256-mbuf bursts from its
     port, and every mbuf leaves by the edge the reference's ptype /
     ip4_input / ip6_input would have sent it to, with the fields eth_rx and the
     input nodes write (the oracle over the same bursts, node state from 0).
-    Zero-copy with the node's default device headers, and with the host
-    reading them (CNDP_GPU_MQ_FLAGS=0)."""
+    Zero-copy with the node's default host headers, and with the device
+    reading them (CNDP_GPU_MQ_FLAGS=4, CNDP_MQ_F_DEVICE_HEADERS)."""
     from helpers import CNET_DEF, cnet_fibs
     from oracle import oracle as O
     from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
@@ -227,8 +227,8 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
     pool, orig = cnet_pool(n, routes, v6, bool(zero_copy))
     ref = _cnet_expect(pool, np.arange(n), _bursts(n, 0, "full"), t4, t6, 0, port)
     L.cndp_node_gpu_umem_reset()
-    if zero_copy == "host_headers":
-        os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
+    if zero_copy == "device_headers":
+        os.environ["CNDP_GPU_MQ_FLAGS"] = str(N.CNDP_MQ_F_DEVICE_HEADERS)
     if zero_copy:
         L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
     H.harness_cnet_set(fib.h, fib6.h)
@@ -549,13 +549,14 @@ def _rw_table(L, seed, ports):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("zero_copy", [True, "host_headers", False])
 def test_rewrite_node_graph_walk(gpu, zero_copy):
     """Bursts into the GPU ip4_rewrite node's process(), graph walks drain it:
     every mbuf leaves by its next hop's pktdev_tx-<port> edge (or pkt_drop),
     in order per edge, and every frame equals the oracle node loop's over the
     same bursts (rewrite data, TTL - 1, the 4-wide / tail checksum rule of
-    each burst)."""
+    each burst).  Zero-copy with the node's default device headers and with
+    the host reading them (CNDP_GPU_MQ_FLAGS=0)."""
     from cndp_amd import pktgen
     from cndp_amd.mbuf import MbufPool
     from oracle import oracle as O
@@ -577,11 +578,14 @@ def test_rewrite_node_graph_walk(gpu, zero_copy):
     if zero_copy:
         assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
     os.environ["CNDP_GPU_BATCH"] = "2048"
+    if zero_copy == "host_headers":
+        os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
     bursts = []
     try:
         _eth_config(H, L, ports)
         tbl = _rw_table(L, 63, ports)
         assert H.harness_graph_create(11) == 0
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         pos = 0
         while pos < n:
             b = int(min(n - pos, rng.choice([256, 256, 256, 97, 4, 3, 1])))
@@ -607,6 +611,7 @@ def test_rewrite_node_graph_walk(gpu, zero_copy):
         L.cndp_node_ip4_rewrite_reset()
         L.cndp_node_gpu_umem_reset()
         os.environ.pop("CNDP_GPU_BATCH", None)
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
     want = np.zeros(n, np.int64)
     pos = 0
     for b in bursts:

@@ -8,6 +8,8 @@ phase of the node's process(): pktdev_rx_burst, cndp_gpu_mq_submit, poll,
 edge mapping + stats, the per-edge enqueue, waits; the rest of the walk (the
 harness's own enqueue bookkeeping) is the difference to the walk time.  The
 queue alone (no node: submit / poll from a loop) is timed beside it.
+CNDP_GPU_MQ_FLAGS selects the queue's flags for both (default 0, host headers;
+4 device headers).
 usage: python tools/node_probe_cnet.py [--passes 4] [--json out]"""
 import argparse
 import ctypes
@@ -88,7 +90,9 @@ def main():
     cl = Classifier(0)
     cl.set_fib(f4, f6)
     cl.host_register(pool.mem)
-    q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=8192, depth=4, umem=pool.base)
+    flags = int(os.environ.get("CNDP_GPU_MQ_FLAGS", 0))  # as the node takes it
+    res["queue_flags"] = flags
+    q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=flags, batch=8192, depth=4, umem=pool.base)
     t = 0.0
     for p in range(args.passes + 1):
         pool.hdr[:] = hdr0
