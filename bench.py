@@ -163,7 +163,11 @@ def run_step(st, stream=None, k: int = 0):
 
 
 def parity_sample(state, k: int = 1 << 16) -> bool:
-    """Cheap spot check of the first k packets against the oracle (untimed)."""
+    """Cheap spot check against the oracle (untimed): k packets at the start of
+    the batch, in its middle and at its end.  Every output at the start; in the
+    other two windows the stateless ones -- all of them for l3fwd / hash, the
+    flow hash for cnet, whose edges and next hops depend on the ptype node's
+    state carried from the batch's start."""
     from cndp_amd import native as N
     from oracle import oracle as O
     fr = state["frames"]
@@ -171,29 +175,34 @@ def parity_sample(state, k: int = 1 << 16) -> bool:
     cl = state["cl"]
     t24, t8 = (x.copy() for x in state["fib"].image())
     kw = dict(tables4=(t24, t8))
-    if state["mode"] == N.CNDP_MODE_CNET:
+    cnet = state["mode"] == N.CNDP_MODE_CNET
+    if cnet:
         kw["tables6"] = tuple(x.copy() for x in state["fib6"].image())
         # the ptype-node model is stateful: restart it (last_type = 0), redo
         # one pass, and compare with the node loop from the same state
         kw["spec_burst"] = 256
         cl.set_tuning(cnet_spec=256)
         cl.classify(fr, state["mode"], out=state["out"])
-    if fr.offsets is not None:
-        offs = fr.offsets[:k].cpu().numpy().astype(np.uint64)
-        end = int(offs[-1]) + 2048
-        slab = fr.slab[:min(end, fr.slab.numel())].cpu().numpy()
-        ref = O.classify(state["mode"], slab, k, offsets=offs, **kw)
-    else:
-        slab = fr.slab[:k * fr.stride].cpu().numpy()
-        ref = O.classify(state["mode"], slab, k, stride=fr.stride, data_off=fr.data_off, **kw)
     out = state["out"]
     torch.cuda.synchronize()
     ok = True
-    for key, dt in (("nh", np.uint32), ("hash", np.uint32), ("queue", np.uint16), ("edge", np.uint8)):
-        if out.get(key) is None:
-            continue
-        g = out[key][:k].cpu().numpy().view(dt)
-        ok &= bool(np.array_equal(g, ref[key]))
+    starts = sorted({0, (fr.n // 2) // 256 * 256, (fr.n - k) // 256 * 256})
+    for w, i0 in enumerate(starts):
+        if fr.offsets is not None:
+            offs = fr.offsets[i0:i0 + k].cpu().numpy().astype(np.uint64)
+            lo = int(offs.min())
+            end = int(offs.max()) + 2048
+            slab = fr.slab[lo:min(end, fr.slab.numel())].cpu().numpy()
+            ref = O.classify(state["mode"], slab, k, offsets=offs - np.uint64(lo), **kw)
+        else:
+            slab = fr.slab[i0 * fr.stride:(i0 + k) * fr.stride].cpu().numpy()
+            ref = O.classify(state["mode"], slab, k, stride=fr.stride, data_off=fr.data_off, **kw)
+        keys = ("nh", "hash", "queue", "edge") if (i0 == 0 or not cnet) else ("hash",)
+        for key, dt in (("nh", np.uint32), ("hash", np.uint32), ("queue", np.uint16), ("edge", np.uint8)):
+            if key not in keys or out.get(key) is None:
+                continue
+            g = out[key][i0:i0 + k].cpu().numpy().view(dt)
+            ok &= bool(np.array_equal(g, ref[key]))
     return ok
 
 
@@ -530,6 +539,7 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     # ---- l3fwd: the ip4_lookup + ip4_rewrite node pair, chained as a graph
     # walk runs them (ip4_lookup's enqueues fill ip4_rewrite's stream)
     res["l3fwd_lookup_rewrite"] = l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes)
+    res["l3fwd_rx_chain"] = l3fwd_rx_chain(L, pool, ptrs, n, passes, routes)
     del ptrs, pool
     # ---- cnet: eth_rx + ptype + ip4_input / ip6_input
     nc = n // 4
@@ -671,6 +681,71 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     res["c1_loopback"] = lat
     cl.close()
     return res
+
+
+def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
+    """l3fwd-graph's receive chain pktdev_rx -> pkt_cls -> ip4_lookup as the
+    GPU pktdev_rx node runs it (cndp_amd/node/pktdev_rx_gpu.c, CNDP_MQ_F_RX_PARSE:
+    the soft parse, pkt_cls and the lookup in one kernel over the mbufs where
+    they lie; graph walks pull 256-mbuf bursts from the port and the mbufs
+    leave on ip4_rewrite / pkt_drop), against the same three nodes' loops on
+    one core over the same mbufs (oracle/oracle.c orc_l3rx_chain_mbufs)."""
+    import ctypes
+    from cndp_amd import native as N
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    from oracle import oracle as O
+    HR = ctypes.CDLL(os.path.join(ROOT, "tests", "node_harness", "librx_harness.so"))
+    HR.harness_rx_load.argtypes = [ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint32]
+    HR.harness_pktdev_rx_port.argtypes = [ctypes.c_uint32, ctypes.c_uint16]
+    HR.harness_walk_until.argtypes = [ctypes.c_uint64]
+    HR.harness_walk_until.restype = ctypes.c_double
+    HR.harness_register_cls_node()
+    name = ctypes.create_string_buffer(64)
+    fl, ne, e0, e1 = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_char_p(), ctypes.c_char_p()
+    k = HR.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+    rx_id = None
+    for i in range(k):
+        HR.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+        if name.value == b"pktdev_rx":
+            rx_id = i
+    out = {}
+    D = N.CNDP_MQ_F_DEVICE_HEADERS
+    hdr0 = pool.hdr.copy()
+    assert HR.harness_pktdev_rx_port(rx_id, 0) == 0
+    for gid, (key, zc, flags) in enumerate((("gpu_zero_copy", True, D), ("gpu_zero_copy_host_headers", True, 0),
+                                            ("gpu_staged", False, 0))):
+        L.cndp_node_gpu_umem_reset()
+        if zc:
+            L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
+        os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
+        assert HR.harness_graph_create(50 + gid) == 0
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+        for ip, d, nh in routes:
+            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+        t = 0.0
+        for p in range(passes + 1):  # pass 0 warms up
+            pool.hdr[:] = hdr0
+            HR.harness_rx_load(0, ptrs, n)
+            HR.harness_reset_counts()
+            dt = HR.harness_walk_until(n)
+            if dt < 0:
+                t = -1.0
+                break
+            t += dt if p else 0.0
+        HR.harness_graph_destroy()
+        out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+    L.cndp_node_gpu_umem_reset()
+    pool.hdr[:] = hdr0
+    fib = NodeFib()
+    t24, t8 = (x.copy() for x in fib.image())
+    O.l3rx_chain_mbufs(ptrs, n, (t24, t8))
+    t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes)
+    out["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+    out["cpu_chain"] = ("pktdev_rx's soft parse, pkt_cls and the ip4_lookup node loop per 256-burst over the "
+                        "same mbufs, one core (oracle/oracle.c orc_l3rx_chain_mbufs)")
+    pool.hdr[:] = hdr0
+    NodeFib.fini()
+    return out
 
 
 def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):

@@ -5841,6 +5841,8 @@ extern "C" int cndp_gpu_bin_partition(cndp_gpu_ctx_t *c, const uint16_t *bin_of,
 #define MQ_BURST 256u       // CNE_GRAPH_BURST_SIZE (cne_graph.h:30)
 #define MQ_W4_AT 20u        // ip4_lookup reads bytes 22..33 (ttl, checksum, dst): the window 20..35
 #define MQ_W4 16u
+#define MQ_W4R_AT 12u       // ip4_lookup with CNDP_MQ_F_RX_PARSE: the ethertype too, the window 12..35
+#define MQ_W4R 24u
 #define MQ_SWAP 16u         // mac swap: staged bytes (it touches 0..11)
 #define MQ_RW_STAGE 64u     // ip4_rewrite: staged bytes (rewrite data <= 56, TTL / checksum at 22..25)
 #define MQ_RUNS_MAX 512u    // cnet: runs of equal-size bursts per batch
@@ -5927,6 +5929,7 @@ struct MqArgs {
     const u32x4 *win;       // cnet: each fast-parsed or general-parsed frame's first 64 bytes
     const struct cndp_rw_nh *rw; // rewrite: next-hop table (device)
     uint32_t lport, want_hash;
+    uint32_t rxparse;       // ip4_lookup, CNDP_MQ_F_RX_PARSE: pktdev_rx's soft parse + pkt_cls first
     uint32_t devhdr;        // zc, CNDP_MQ_F_DEVICE_HEADERS: the kernels read each mbuf's header
     uint32_t nrg;           //   themselves; ip4_lookup: its frame lies in one of the nrg registered
     struct {                //   regions (host address range, device = host + delta); cnet: rg[0]
@@ -6029,6 +6032,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
         const uint64_t w = a.devhdr ? 0u : a.off[i];
         const uint8_t *p; // bytes 20..35 of the frame
         uint32_t avail;   // readable bytes from p
+        uint32_t eavail;  // readable bytes from the ethertype (frame byte 12, p - 8)
         uint64_t m = 0;
         if (a.zc && a.devhdr) {
             m = a.mb[i];
@@ -6051,6 +6055,7 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
             }
             p = (const uint8_t *)(uintptr_t)(fh + delta) + MQ_W4_AT;
             avail = rlen - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(rlen - fo > MQ_W4_AT ? rlen - fo - MQ_W4_AT : 0);
+            eavail = rlen - fo > MQ_W4R_AT + 2 ? 2u : (uint32_t)(rlen - fo > MQ_W4R_AT ? rlen - fo - MQ_W4R_AT : 0);
         } else if (a.zc) {
             m = a.mb[i];
             uint32_t fa;
@@ -6061,9 +6066,25 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
             }
             p = f + MQ_W4_AT;
             avail = fa > MQ_W4_AT ? fa - MQ_W4_AT : 0u;
-        } else {
-            p = a.slab + w;
+            eavail = fa > MQ_W4R_AT ? fa - MQ_W4R_AT : 0u;
+        } else { // staged: the window from MQ_W4R_AT with the soft parse, else from MQ_W4_AT
+            p = a.slab + w + (a.rxparse ? MQ_W4_AT - MQ_W4R_AT : 0u);
             avail = MQ_W4;
+            eavail = 2u;
+        }
+        if (a.rxparse) {
+            // pktdev_rx's eth_pkt_parse_cb (pktdev_rx.c:24-34, :88-100):
+            // packet_type = l3_ptype(ether_type, 0); then pkt_cls
+            // (pkt_cls.c:19-31): only IPv4 (0x90) goes on to ip4_lookup
+            const uint8_t *e = p - (MQ_W4_AT - MQ_W4R_AT);
+            const uint32_t et = eavail >= 2 ? ((uint32_t)gbyte(e, eavail, 0) << 8) | gbyte(e, eavail, 1) : 0u;
+            const uint32_t pt = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
+            if (a.zc)
+                *gp((uint32_t *)(m + MB_PTYPE)) = pt;
+            if (pt != 0x90u) {
+                a.edges[i] = (uint16_t)CNDP_MQ_EDGE_CLS_DROP;
+                continue;
+            }
         }
         uint32_t ttl, ck, dip;
         if (avail >= 16 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p) & 63u) <= 48u) {
@@ -6468,7 +6489,9 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP &&
         k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
-    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS))
+    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_RX_PARSE))
+        return -EINVAL;
+    if ((k.flags & CNDP_MQ_F_RX_PARSE) && k.mode != CNDP_MQ_IP4_LOOKUP)
         return -EINVAL;
     k.batch = k.batch ? k.batch : 8192u;
     k.depth = k.depth ? k.depth : 4u;
@@ -6509,7 +6532,8 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     const bool zc = q->zc != 0;
     q->stage = zc ? 0u
              : cnet ? (uint32_t)al64(k.stage_max)
-             : k.mode == CNDP_MQ_IP4_LOOKUP ? MQ_W4 : k.mode == CNDP_MQ_MAC_SWAP ? MQ_SWAP : MQ_RW_STAGE;
+             : k.mode == CNDP_MQ_IP4_LOOKUP ? ((k.flags & CNDP_MQ_F_RX_PARSE) ? 32u : MQ_W4)
+             : k.mode == CNDP_MQ_MAC_SWAP ? MQ_SWAP : MQ_RW_STAGE;
     q->h_mb = 0;                                          // zc: mbuf device addresses; rewrite: tail flags
     q->h_off = al64(B * 8);                               // frame words / offsets
     q->h_len = q->h_off + al64(B * 8);                    // cnet: length fields; rewrite: priv1
@@ -6687,6 +6711,7 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
         if ((r = tbl_acquire(&c->fib4->t, s, &v4)))
             return r;
         a.tb = mq_tables(c, v4, nullptr, 0);
+        a.rxparse = (q->conf.flags & CNDP_MQ_F_RX_PARSE) != 0;
         if (q->devhdr) { // frames in any registered region
             a.devhdr = 1;
             a.nrg = (uint32_t)q->nrg;
@@ -6923,8 +6948,9 @@ static void mq_fill(cndp_gpu_mq_t *q, MqSlot *sl, void *const *mbufs, uint32_t k
                                                                                              : q->conf.stage_max;
                 want = room < cap ? room : cap;
             } else if (mode == CNDP_MQ_IP4_LOOKUP) {
-                at = MQ_W4_AT;
-                want = MQ_W4;
+                const bool rxp = (q->conf.flags & CNDP_MQ_F_RX_PARSE) != 0;
+                at = rxp ? MQ_W4R_AT : MQ_W4_AT;
+                want = rxp ? MQ_W4R : MQ_W4;
             } else {
                 want = q->stage;
             }
@@ -7052,10 +7078,19 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
     }
     if (mode == CNDP_MQ_IP4_LOOKUP) {
         const uint64_t *priv1 = (const uint64_t *)R;
+        const bool rxp = (q->conf.flags & CNDP_MQ_F_RX_PARSE) != 0;
         for (uint32_t i = i0; i < i1; i++) { // node_mbuf_priv1 (ip4_lookup.c:144-154)
             if (i + MQ_PF < i1)
                 __builtin_prefetch((uint8_t *)sl->mb[i + MQ_PF] + MB_UDATA64, 1);
-            *(uint64_t *)((uint8_t *)sl->mb[i] + MB_UDATA64) = priv1[i];
+            uint8_t *m = (uint8_t *)sl->mb[i];
+            if (rxp) { // the soft parse's packet_type, from the staged ethertype
+                const uint8_t *e = sl->h + q->h_stage + ho[i];
+                const uint32_t et = ((uint32_t)e[0] << 8) | e[1];
+                *(uint32_t *)(m + MB_PTYPE) = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
+                if (ed[i] == CNDP_MQ_EDGE_CLS_DROP) // pkt_cls dropped it: ip4_lookup never saw it
+                    continue;
+            }
+            *(uint64_t *)(m + MB_UDATA64) = priv1[i];
         }
         return;
     }

@@ -237,6 +237,14 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
  * not of eth_rx, whose batch the extra header pass over PCIe slows more than
  * the host saves. */
 #define CNDP_MQ_F_DEVICE_HEADERS (1u << 2)
+/* ip4_lookup: the l3fwd-graph receive chain in front of it too -- pktdev_rx's
+ * soft parse (eth_pkt_parse_cb, pktdev_rx.c:24-34, :37-103: packet_type =
+ * l3_ptype(ether_type, 0), written into the mbuf) and pkt_cls (pkt_cls.c:19-31:
+ * only IPv4 goes on to ip4_lookup); an mbuf pkt_cls sends to pkt_drop comes
+ * back with edge CNDP_MQ_EDGE_CLS_DROP and its udata64 untouched.  For a source
+ * node that replaces pktdev_rx -> pkt_cls -> ip4_lookup (pktdev_rx_gpu.c). */
+#define CNDP_MQ_F_RX_PARSE (1u << 3)
+#define CNDP_MQ_EDGE_CLS_DROP 0xFFFEu
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u
 #define CNDP_MQ_NODE_IP6 2u

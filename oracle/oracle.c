@@ -1207,6 +1207,73 @@ double orc_rx_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, c
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
+/* l3fwd-graph's receive chain per graph burst, as one core runs it:
+ * pktdev_rx's soft parse (pktdev_rx.c:24-34, :37-103: packet_type =
+ * l3_ptype(ether_type, 0) into m->packet_type @32), pkt_cls (pkt_cls.c:19-31:
+ * p_nxt[packet_type & 0xff] -- the IPv4 types (0x10, 0x30, 0x90, with or
+ * without L2_ETHER 0x01) to ip4_lookup, everything else to pkt_drop), then
+ * the ip4_lookup node loop (ip4_lookup.c:108-154) over the burst's IPv4
+ * mbufs, which pkt_cls hands on in order.  edges (optional, n entries, in
+ * mbuf order): the FIB value >> 16 for the mbufs ip4_lookup saw, 0xFFFE for
+ * those pkt_cls dropped.  Returns seconds for `iters` passes. */
+static inline int orc_cls_ip4(uint32_t pt)
+{
+    const uint32_t l = pt & 0xffu; /* pkt_cls.c:19-31 */
+    return l == 0x10u || l == 0x30u || l == 0x90u || l == 0x11u || l == 0x31u || l == 0x91u;
+}
+
+double orc_l3rx_chain_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                            const uint32_t *tbl8, int iters, uint16_t *edges)
+{
+    struct timespec t0, t1;
+    void *ip4[256];
+    uint32_t at[256];
+    if (burst == 0 || burst > 256)
+        burst = 256;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int it = 0; it < iters; it++) {
+        for (uint32_t b = 0; b < n; b += burst) {
+            const uint32_t cnt = n - b < burst ? n - b : burst;
+            for (uint32_t k = 0; k < cnt; k++) {
+                if (k + 8 < cnt)
+                    __builtin_prefetch(mbufs[b + k + 8]);
+                if (k + 4 < cnt) {
+                    const uint8_t *pm = mbufs[b + k + 4];
+                    __builtin_prefetch(*(uint8_t *const *)(pm + 8) + *(const uint16_t *)(pm + 24));
+                }
+                uint8_t *m = mbufs[b + k];
+                const uint8_t *eh = *(uint8_t *const *)(m + 8) + *(const uint16_t *)(m + 24);
+                const uint16_t et = rd_be16(eh + 12);
+                *(uint32_t *)(m + 32) = et == 0x0800 ? 0x90u : et == 0x86DD ? 0xE0u : 0u;
+            }
+            uint32_t n4 = 0;
+            for (uint32_t k = 0; k < cnt; k++) {
+                const uint8_t *m = mbufs[b + k];
+                if (orc_cls_ip4(*(const uint32_t *)(m + 32))) {
+                    at[n4] = b + k;
+                    ip4[n4++] = mbufs[b + k];
+                } else if (edges) {
+                    edges[b + k] = 0xFFFEu;
+                }
+            }
+            orc_ip4_lookup_mbufs(ip4, n4, n4, tbl24, tbl8, 1);
+            if (edges)
+                for (uint32_t q = 0; q < n4; q++) {
+                    /* the edge is the FIB value >> 16: rebuilt from priv1's nh
+                     * and the lookup of the same address (dir24_8.h:118-148) */
+                    const uint8_t *m = ip4[q];
+                    const uint8_t *ip = *(uint8_t *const *)(m + 8) + *(const uint16_t *)(m + 24) + 14;
+                    uint64_t v;
+                    const uint32_t dip = rd_be32(ip + 16);
+                    orc_dir24_8_lookup_bulk_pf(tbl24, tbl8, &dip, 1, &v);
+                    edges[at[q]] = (uint16_t)(v >> 16);
+                }
+        }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, int iters)
 {
     if (nthreads < 1)

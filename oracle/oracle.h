@@ -134,6 +134,8 @@ double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, cons
                             const uint32_t *tbl8, int iters);
 double orc_rx_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
                                const uint32_t *tbl8, int iters);
+double orc_l3rx_chain_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                            const uint32_t *tbl8, int iters, uint16_t *edges);
 
 /* ---- the cnet chain as a graph walk runs it (oracle/cnet_chain.c) --------
  * eth_rx -> ptype -> ip4_input / ip6_input per burst over pktmbuf_t pointer

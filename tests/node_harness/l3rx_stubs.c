@@ -1,0 +1,48 @@
+/*
+ * Test-only: what the GPU pktdev_rx node source (cndp_amd/node/pktdev_rx_gpu.c)
+ * needs from the rest of l3fwd-graph, for tests/test_node_graph.py:
+ * pktdev_ctrl.c's per-port registration of the node's clones, and the pkt_cls
+ * node it stands in for (registered idle, so it is in the graph with stats of
+ * its own, as l3fwd-graph has it).
+ */
+#include <stdlib.h>
+
+#include "cne_graph.h"
+#include "pktdev_rx_priv.h"
+
+/* pktdev_ctrl.c:40-64: node nid receives from port port_id */
+int harness_pktdev_rx_port(cne_node_t nid, uint16_t port_id)
+{
+    struct pktdev_rx_node_main *m = pktdev_rx_get_node_data_get();
+    for (pktdev_rx_node_elem_t *e = m->head; e; e = e->next)
+        if (e->nid == nid) { /* re-registration (a later test): update */
+            e->ctx.port_id = port_id;
+            return 0;
+        }
+    pktdev_rx_node_elem_t *e = calloc(1, sizeof(*e));
+    if (!e)
+        return -12;
+    e->ctx.port_id = port_id;
+    e->nid = nid;
+    e->next = m->head;
+    m->head = e;
+    return 0;
+}
+
+static uint16_t idle_process(struct cne_graph *graph, struct cne_node *node, void **objs, uint16_t nb)
+{
+    (void)graph;
+    (void)node;
+    (void)objs;
+    return nb;
+}
+static struct cne_node_register stub_cls = {.name = "pkt_cls", .process = idle_process};
+void harness_register_cls_node(void)
+{
+    static int done;
+    if (done)
+        return;
+    done = 1;
+    stub_cls.parent_id = CNE_NODE_ID_INVALID;
+    stub_cls.id = __cne_node_register(&stub_cls);
+}

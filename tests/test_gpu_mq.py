@@ -118,6 +118,48 @@ def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
     assert (edges == 1).sum() > 0 and (edges == 0).sum() > 0
 
 
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
+@pytest.mark.parametrize("kind", ["full", "shifted"])
+def test_mq_ip4_lookup_rx_parse(l3, gpu, zero_copy, kind):
+    """CNDP_MQ_F_RX_PARSE: the queue also does l3fwd-graph's pktdev_rx soft
+    parse (packet_type from the ethertype, pktdev_rx.c:24-34) and pkt_cls
+    (only IPv4 goes on to ip4_lookup, pkt_cls.c:19-31) -- against the oracle's
+    chain over the same mbufs: packet_type everywhere, priv1 only where
+    ip4_lookup ran, edge CNDP_MQ_EDGE_CLS_DROP where pkt_cls dropped."""
+    flags = N.CNDP_MQ_F_RX_PARSE | (N.CNDP_MQ_F_DEVICE_HEADERS if zero_copy == "device_headers" else 0)
+    cl, fib, t4 = l3
+    n = 12000
+    gp, op = MbufPool(n), MbufPool(n)
+    fr = _mixed_l3_frames(n, seed=31)
+    for p in (gp, op):
+        if kind == "shifted":
+            p.hdr["data_off"] = 256 + np.arange(n) % 61
+        p.fill(fr)
+        p.hdr["udata64"] = 0xABABABABABABABAB
+        p.hdr["packet_type"] = 0x77
+    umem = None
+    if zero_copy:
+        cl.host_register(gp.mem)
+        umem = gp.base
+    try:
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, flags=flags, batch=4096, depth=3, umem=umem)
+        order = np.random.default_rng(32).permutation(n)
+        addrs, edges = q.run(gp, order, _bursts(n, 33, kind))
+        q.close()
+    finally:
+        if zero_copy:
+            cl.host_unregister(gp.mem)
+    idx = gp.index_of(addrs)
+    assert np.array_equal(idx, order)
+    e = np.zeros(n, np.uint16)
+    O.l3rx_chain_mbufs(op.ptrs(np.arange(n)), n, t4, edges=e)
+    assert np.array_equal(gp.hdr["packet_type"], op.hdr["packet_type"])
+    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
+    assert np.array_equal(edges, e[idx])
+    assert (e == N.CNDP_MQ_EDGE_CLS_DROP).sum() > 100 and (e == 0).sum() > n // 2 and (e == 1).sum() > 0
+    assert set(np.unique(op.hdr["packet_type"]).tolist()) == {0, 0x90, 0xE0}
+
+
 def _cnet_expect(pool, order, bursts, t4, t6, hash_flag, lport):
     """Oracle results for the mbufs in submission order: one oracle call per
     run of equal-size bursts (closed by one shorter burst), the ptype node

@@ -690,3 +690,146 @@ def test_l3fwd_graph_chain(gpu):
     assert not np.any(diff & ok)
     assert rw.size > n // 2 and (got == 0).sum() > 0
     NodeFib.fini()
+
+
+# ---- the l3fwd-graph receive chain node (cndp_amd/node/pktdev_rx_gpu.c) ------
+RX_HARNESS = os.path.join(HERE, "node_harness", "librx_harness.so")
+PKTDEV_RX_EDGES = [b"ip4_lookup", b"pkt_cls", b"ip4_rewrite", b"pkt_drop"]
+
+
+def _rx_harness():
+    if not os.path.exists(RX_HARNESS):
+        pytest.skip("rx node harness not built (build() makes it)")
+    N.lib()
+    H = ctypes.CDLL(RX_HARNESS)
+    H.harness_node_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(ctypes.c_char_p)]
+    H.harness_node_edges.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    H.harness_take_edge.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32]
+    H.harness_take_edge.restype = ctypes.c_uint32
+    H.harness_rx_load.argtypes = [ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint32]
+    H.harness_rx_left.restype = ctypes.c_uint32
+    H.harness_pktdev_rx_port.argtypes = [ctypes.c_uint32, ctypes.c_uint16]
+    H.harness_walk_until.argtypes = [ctypes.c_uint64]
+    H.harness_walk_until.restype = ctypes.c_double
+    H.harness_node_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    H.harness_chain.argtypes = [ctypes.c_int]
+    H.cne_node_edge_update.restype = ctypes.c_uint16
+    H.cne_node_edge_update.argtypes = [ctypes.c_uint32, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint16]
+    H.cne_node_edge_count.restype = ctypes.c_uint16
+    H.cne_node_edge_count.argtypes = [ctypes.c_uint32]
+    H.harness_register_cls_node()
+    return H
+
+
+def test_rx_node_registry():
+    """The node replacing lib/usr/clib/nodes/pktdev_rx.c: registered as
+    "pktdev_rx", a source node (pktdev_rx.c:186-199) that pktdev_ctrl.c clones
+    per port; its first two edges are the reference's (ip4_lookup, pkt_cls,
+    pktdev_rx_priv.h), then the two it sends on (ip4_rewrite, pkt_drop)."""
+    H = _rx_harness()
+    ids = _node_ids(H)
+    i = ids["pktdev_rx"]
+    name = ctypes.create_string_buffer(64)
+    fl, ne = ctypes.c_uint64(), ctypes.c_int()
+    e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
+    H.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+    assert name.value == b"pktdev_rx" and fl.value == 1 and ne.value == 4
+    assert _edges_of(H, i) == PKTDEV_RX_EDGES
+    assert {"ip4_lookup", "ip4_rewrite", "pkt_cls"} <= set(ids)
+
+
+def test_rx_node_init_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    H = _rx_harness()
+    assert H.harness_graph_create(0) == -19   # -ENODEV: there is no CPU path behind the node
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [True, "host_headers", False])
+def test_rx_node_graph_walk(gpu, zero_copy):
+    """Graph walks over the GPU pktdev_rx node chained into the GPU
+    ip4_rewrite node: it pulls 256-mbuf bursts from its port and every mbuf
+    ends where l3fwd-graph's pktdev_rx -> pkt_cls -> ip4_lookup -> ip4_rewrite
+    walk sends it (pkt_drop, or its next hop's tx edge) with the soft parse's
+    packet_type, ip4_lookup's priv1 (IPv4 only) and the rewritten frame of the
+    oracle chain; pkt_cls and ip4_lookup get the stats of the mbufs they stand
+    for.  Mixed frames: routed IPv4, IPv6, VLAN, ARP and fuzz."""
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    from cndp_amd.mbuf import MbufPool
+    from cndp_amd import pktgen
+    from oracle import oracle as O
+    from test_gpu_mq import _mixed_l3_frames
+    H = _rx_harness()
+    L = N.lib()
+    ports, port = (0, 1, 2, 3), 2
+    n = 20000
+    gp, op = MbufPool(n), MbufPool(n)
+    fr = _mixed_l3_frames(n, seed=81)
+    for p in (gp, op):
+        p.fill(fr)
+        p.hdr["udata64"] = 0x5A5A5A5A
+    NodeFib.fini()
+    L.cndp_node_ip4_rewrite_reset()
+    L.cndp_node_gpu_umem_reset()
+    if zero_copy:
+        assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
+    os.environ["CNDP_GPU_BATCH"] = "4096"
+    if zero_copy == "host_headers":
+        os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
+    routes = pktgen.l3fwd_routes()
+    ids = _node_ids(H)
+    assert H.harness_pktdev_rx_port(ids["pktdev_rx"], port) == 0
+    assert H.harness_rx_load(port, gp.ptrs(np.arange(n)), n) == 0
+    try:
+        _eth_config(H, L, ports)
+        tbl = _rw_table(L, 82, ports)
+        H.harness_chain(1)
+        assert H.harness_graph_create(13) == 0
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+        for ip, d, nh in routes:
+            assert cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
+        assert H.harness_walk_until(n) >= 0
+        assert H.harness_rx_left(port) == 0
+        names = [b"pkt_drop"] + [f"pktdev_tx-{p}".encode() for p in ports]
+        buf = (ctypes.c_void_p * n)()
+        got = np.full(n, -1, np.int64)
+        for k, nm in enumerate(names):
+            m = H.harness_take_edge(nm, buf, n)
+            got[gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))] = k
+        stats = {}
+        for nm in (b"pkt_cls", b"ip4_lookup"):
+            c, o = ctypes.c_uint64(), ctypes.c_uint64()
+            assert H.harness_node_stats(nm, ctypes.byref(c), ctypes.byref(o)) == 0
+            stats[nm] = o.value
+    finally:
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+        H.harness_chain(0)
+        H.harness_graph_destroy()
+        H.harness_edges_reset()
+        L.cndp_node_ip4_rewrite_reset()
+        L.cndp_node_gpu_umem_reset()
+        os.environ.pop("CNDP_GPU_BATCH", None)
+    # the reference chain on the oracle's copy
+    t24, t8 = O.dir24_8_build(list(routes), N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
+    e = np.zeros(n, np.uint16)
+    O.l3rx_chain_mbufs(op.ptrs(np.arange(n)), n, (t24, t8), edges=e)
+    assert np.array_equal(gp.hdr["packet_type"], op.hdr["packet_type"])
+    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
+    rw = np.nonzero(e == 0)[0]
+    tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
+    want = np.zeros(n, np.int64)
+    want[rw] = tx
+    assert np.array_equal(got, want)
+    d = op.data_pos().astype(np.int64)
+    ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
+    ok = (ck != 0xFFFE) & (ck != 0xFFFF)
+    diff = np.any(gp.mem.reshape(n, -1)[:, 64:] != op.mem.reshape(n, -1)[:, 64:], axis=1)
+    assert not np.any(diff & ok)
+    assert stats[b"pkt_cls"] == n and stats[b"ip4_lookup"] == int((e != 0xFFFE).sum())
+    assert (e == 0xFFFE).sum() > 100 and rw.size > n // 2 and (got == 0).sum() > 0
+    NodeFib.fini()
