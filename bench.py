@@ -734,16 +734,69 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
             t += dt if p else 0.0
         HR.harness_graph_destroy()
         out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
-    L.cndp_node_gpu_umem_reset()
+    # the whole l3fwd-graph node chain on the device: the rx node chained into
+    # the GPU ip4_rewrite node (four tx ports, 12-B MAC rewrites for the 64
+    # next hops, as l3fwd-graph sets them up, fwd.c:160-201)
+    import random
+    HR.harness_chain.argtypes = [ctypes.c_int]
+    HR.cne_node_edge_update.restype = ctypes.c_uint16
+    HR.cne_node_edge_update.argtypes = [ctypes.c_uint32, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint16]
+    HR.cne_node_edge_count.restype = ctypes.c_uint16
+    HR.cne_node_edge_count.argtypes = [ctypes.c_uint32]
+    rw_id = None
+    for i in range(k):
+        HR.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
+        if name.value == b"ip4_rewrite":
+            rw_id = i
+    L.cndp_node_ip4_rewrite_reset()
+    tbl = np.zeros(64, dtype=O.REWRITE_NH)
+    rnd = random.Random(8)
+    try:
+        for p in range(4):
+            nm = ctypes.c_char_p(f"pktdev_tx-{p}".encode())
+            HR.cne_node_edge_update(rw_id, 0xFFFF, ctypes.byref(nm), 1)
+            assert L.ip4_rewrite_set_next(p, HR.cne_node_edge_count(rw_id) - 1) == 0
+        for nh in range(64):
+            data = bytes(rnd.randrange(256) for _ in range(12))
+            assert L.cne_node_ip4_rewrite_add(nh, ctypes.create_string_buffer(data, 12), 12, nh % 4) == 0
+            tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = 12, nh % 4 + 1, 1
+            tbl[nh]["rewrite_data"][:] = np.frombuffer(data + bytes(44), np.uint8)
+        L.cndp_node_gpu_umem_reset()
+        L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
+        HR.harness_chain(1)
+        assert HR.harness_graph_create(60) == 0
+        for ip, d, nh in routes:
+            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+        t = 0.0
+        for p in range(passes + 1):  # pass 0 warms up
+            pool.hdr[:] = hdr0
+            HR.harness_rx_load(0, ptrs, n)
+            HR.harness_reset_counts()
+            dt = HR.harness_walk_until(n)
+            if dt < 0:
+                t = -1.0
+                break
+            t += dt if p else 0.0
+        HR.harness_graph_destroy()
+        out["gpu_with_rewrite_zero_copy_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+    finally:
+        HR.harness_chain(0)
+        L.cndp_node_gpu_umem_reset()
     pool.hdr[:] = hdr0
     fib = NodeFib()
     t24, t8 = (x.copy() for x in fib.image())
     O.l3rx_chain_mbufs(ptrs, n, (t24, t8))
     t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes)
     out["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
-    out["cpu_chain"] = ("pktdev_rx's soft parse, pkt_cls and the ip4_lookup node loop per 256-burst over the "
-                        "same mbufs, one core (oracle/oracle.c orc_l3rx_chain_mbufs)")
     pool.hdr[:] = hdr0
+    O.l3rx_chain_mbufs(ptrs, n, (t24, t8), rewrite=tbl)
+    t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes, rewrite=tbl)
+    out["cpu_1core_with_rewrite_Mpps"] = round(n * passes / t / 1e6, 2)
+    out["cpu_chain"] = ("pktdev_rx's soft parse, pkt_cls and the ip4_lookup node loop per 256-burst over the "
+                        "same mbufs, one core (oracle/oracle.c orc_l3rx_chain_mbufs); _with_rewrite: then "
+                        "ip4_rewrite_node_process over the mbufs ip4_lookup sent to it")
+    pool.hdr[:] = hdr0
+    L.cndp_node_ip4_rewrite_reset()
     NodeFib.fini()
     return out
 

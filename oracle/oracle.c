@@ -1213,21 +1213,50 @@ double orc_rx_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, c
  * p_nxt[packet_type & 0xff] -- the IPv4 types (0x10, 0x30, 0x90, with or
  * without L2_ETHER 0x01) to ip4_lookup, everything else to pkt_drop), then
  * the ip4_lookup node loop (ip4_lookup.c:108-154) over the burst's IPv4
- * mbufs, which pkt_cls hands on in order.  edges (optional, n entries, in
- * mbuf order): the FIB value >> 16 for the mbufs ip4_lookup saw, 0xFFFE for
- * those pkt_cls dropped.  Returns seconds for `iters` passes. */
+ * mbufs, which pkt_cls hands on in order, and with rwt the ip4_rewrite node
+ * (ip4_rewrite.c:40-247) over the ones ip4_lookup sent to it, in order.
+ * edges (optional, n entries, in mbuf order): the FIB value >> 16 for the
+ * mbufs ip4_lookup saw, 0xFFFE for those pkt_cls dropped.  Returns seconds
+ * for `iters` passes. */
 static inline int orc_cls_ip4(uint32_t pt)
 {
     const uint32_t l = pt & 0xffu; /* pkt_cls.c:19-31 */
     return l == 0x10u || l == 0x30u || l == 0x90u || l == 0x11u || l == 0x31u || l == 0x91u;
 }
 
+/* ip4_lookup's loop over mbufs[0..n) (as orc_ip4_lookup_mbufs), each mbuf's
+ * next edge (FIB value >> 16) into edge[] */
+static void orc_l3_lookup_edges(void *const *mbufs, uint32_t n, const uint32_t *tbl24, const uint32_t *tbl8,
+                                uint16_t *edge)
+{
+    for (uint32_t k = 0; k < n; k += 4) {
+        const uint32_t m = n - k < 4 ? n - k : 4;
+        uint32_t dip[4];
+        uint64_t dst[4];
+        uint8_t *mb[4];
+        const uint8_t *ip[4];
+        for (uint32_t q = 0; q < m; q++) {
+            mb[q] = (uint8_t *)mbufs[k + q];
+            const uint8_t *buf = *(uint8_t *const *)(mb[q] + 8);
+            ip[q] = buf + *(const uint16_t *)(mb[q] + 24) + 14;
+            dip[q] = rd_be32(ip[q] + 16);
+        }
+        orc_dir24_8_lookup_bulk_pf(tbl24, tbl8, dip, m, dst);
+        for (uint32_t q = 0; q < m; q++) {
+            const uint64_t ck = (uint64_t)ip[q][10] | ((uint64_t)ip[q][11] << 8);
+            *(uint64_t *)(mb[q] + 56) = (dst[q] & 0xffffu) | ((uint64_t)ip[q][8] << 16) | (ck << 32);
+            edge[k + q] = (uint16_t)(dst[q] >> 16);
+        }
+    }
+}
+
 double orc_l3rx_chain_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
-                            const uint32_t *tbl8, int iters, uint16_t *edges)
+                            const uint32_t *tbl8, int iters, uint16_t *edges, const struct orc_rewrite_nh *rwt)
 {
     struct timespec t0, t1;
-    void *ip4[256];
+    void *ip4[256], *rw[256];
     uint32_t at[256];
+    uint16_t e4[256], tx[256];
     if (burst == 0 || burst > 256)
         burst = 256;
     clock_gettime(CLOCK_MONOTONIC, &t0);
@@ -1256,18 +1285,17 @@ double orc_l3rx_chain_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, cons
                     edges[b + k] = 0xFFFEu;
                 }
             }
-            orc_ip4_lookup_mbufs(ip4, n4, n4, tbl24, tbl8, 1);
+            orc_l3_lookup_edges(ip4, n4, tbl24, tbl8, e4);
+            if (rwt) {
+                uint32_t nrw = 0;
+                for (uint32_t q = 0; q < n4; q++)
+                    if (e4[q] == 0)
+                        rw[nrw++] = ip4[q];
+                orc_ip4_rewrite_node(rw, nrw, rwt, tx);
+            }
             if (edges)
-                for (uint32_t q = 0; q < n4; q++) {
-                    /* the edge is the FIB value >> 16: rebuilt from priv1's nh
-                     * and the lookup of the same address (dir24_8.h:118-148) */
-                    const uint8_t *m = ip4[q];
-                    const uint8_t *ip = *(uint8_t *const *)(m + 8) + *(const uint16_t *)(m + 24) + 14;
-                    uint64_t v;
-                    const uint32_t dip = rd_be32(ip + 16);
-                    orc_dir24_8_lookup_bulk_pf(tbl24, tbl8, &dip, 1, &v);
-                    edges[at[q]] = (uint16_t)(v >> 16);
-                }
+                for (uint32_t q = 0; q < n4; q++)
+                    edges[at[q]] = e4[q];
         }
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);

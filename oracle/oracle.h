@@ -134,8 +134,6 @@ double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, cons
                             const uint32_t *tbl8, int iters);
 double orc_rx_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
                                const uint32_t *tbl8, int iters);
-double orc_l3rx_chain_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
-                            const uint32_t *tbl8, int iters, uint16_t *edges);
 
 /* ---- the cnet chain as a graph walk runs it (oracle/cnet_chain.c) --------
  * eth_rx -> ptype -> ip4_input / ip6_input per burst over pktmbuf_t pointer
@@ -182,6 +180,8 @@ struct orc_rewrite_nh {
     uint16_t rsvd;
     uint8_t rewrite_data[56];
 };
+double orc_l3rx_chain_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
+                            const uint32_t *tbl8, int iters, uint16_t *edges, const struct orc_rewrite_nh *rwt);
 void orc_ip4_rewrite(uint8_t *slab, uint64_t slab_len, uint64_t stride, const uint64_t *offsets,
                      uint32_t data_off, uint32_t n, const uint32_t *nh, uint32_t burst,
                      const struct orc_rewrite_nh *tbl, uint16_t *tx_edge);

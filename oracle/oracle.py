@@ -143,7 +143,8 @@ def lib():
         L.orc_rx_ip4_lookup_mbufs.restype = c_double
         L.orc_rx_ip4_lookup_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_int]
         L.orc_l3rx_chain_mbufs.restype = c_double
-        L.orc_l3rx_chain_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_int, c_void_p]
+        L.orc_l3rx_chain_mbufs.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_int, c_void_p,
+                                           c_void_p]
         L.orc_cnet_chain.restype = c_double
         L.orc_cnet_chain.argtypes = [POINTER(ChainArgs), c_int, c_int, c_void_p]
         L.orc_l3fwd_nodes_mbufs.restype = c_double
@@ -322,13 +323,14 @@ def rx_ip4_lookup_mbufs(ptrs, n, tables4, burst=256, iters=1) -> float:
     return lib().orc_rx_ip4_lookup_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), iters)
 
 
-def l3rx_chain_mbufs(ptrs, n, tables4, burst=256, iters=1, edges=None) -> float:
+def l3rx_chain_mbufs(ptrs, n, tables4, burst=256, iters=1, edges=None, rewrite=None) -> float:
     """l3fwd-graph's receive chain per burst on one thread (pktdev_rx's soft
-    parse, pkt_cls, the ip4_lookup loop over the IPv4 mbufs): seconds; edges
-    (uint16 array of n, optional) gets each mbuf's next edge -- FIB value >> 16,
-    or 0xFFFE where pkt_cls dropped it."""
+    parse, pkt_cls, the ip4_lookup loop over the IPv4 mbufs; with rewrite, a
+    REWRITE_NH table, the ip4_rewrite node over the ones sent to it): seconds;
+    edges (uint16 array of n, optional) gets each mbuf's ip4_lookup edge --
+    FIB value >> 16, or 0xFFFE where pkt_cls dropped it."""
     return lib().orc_l3rx_chain_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), iters,
-                                      None if edges is None else _p(edges))
+                                      None if edges is None else _p(edges), _p(rewrite))
 
 
 def l3fwd_burst_bench(slab, n, stride, tables4, nthreads=1, iters=1, **kw) -> float:
