@@ -764,23 +764,31 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
         L.cndp_node_gpu_umem_reset()
         L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
         HR.harness_chain(1)
-        assert HR.harness_graph_create(60) == 0
-        for ip, d, nh in routes:
-            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
-        t = 0.0
-        for p in range(passes + 1):  # pass 0 warms up
-            pool.hdr[:] = hdr0
-            HR.harness_rx_load(0, ptrs, n)
-            HR.harness_reset_counts()
-            dt = HR.harness_walk_until(n)
-            if dt < 0:
-                t = -1.0
-                break
-            t += dt if p else 0.0
-        HR.harness_graph_destroy()
-        out["gpu_with_rewrite_zero_copy_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+        # ip4_rewrite in the receive node's kernel (CNDP_MQ_F_REWRITE, the
+        # node's default zero-copy), or as the GPU ip4_rewrite node behind it
+        for gid, (key, fuse) in enumerate((("gpu_with_rewrite_zero_copy", "1"),
+                                           ("gpu_with_rewrite_node_zero_copy", "0"))):
+            os.environ["CNDP_GPU_RX_REWRITE"] = fuse
+            assert HR.harness_graph_create(60 + gid) == 0
+            os.environ.pop("CNDP_GPU_RX_REWRITE", None)
+            for ip, d, nh in routes:
+                cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+            t = 0.0
+            for p in range(passes + 1):  # pass 0 warms up
+                pool.hdr[:] = hdr0
+                HR.harness_rx_load(0, ptrs, n)
+                HR.harness_reset_counts()
+                dt = HR.harness_walk_until(n)
+                if dt < 0:
+                    t = -1.0
+                    break
+                t += dt if p else 0.0
+            HR.harness_graph_destroy()
+            out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
     finally:
+        os.environ.pop("CNDP_GPU_RX_REWRITE", None)
         HR.harness_chain(0)
+        HR.harness_edges_reset()
         L.cndp_node_gpu_umem_reset()
     pool.hdr[:] = hdr0
     fib = NodeFib()

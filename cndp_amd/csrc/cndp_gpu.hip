@@ -5930,6 +5930,7 @@ struct MqArgs {
     const struct cndp_rw_nh *rw; // rewrite: next-hop table (device)
     uint32_t lport, want_hash;
     uint32_t rxparse;       // ip4_lookup, CNDP_MQ_F_RX_PARSE: pktdev_rx's soft parse + pkt_cls first
+    const uint32_t *bstart; // CNDP_MQ_F_REWRITE: each submitted burst's first mbuf, then n
     uint32_t devhdr;        // zc, CNDP_MQ_F_DEVICE_HEADERS: the kernels read each mbuf's header
     uint32_t nrg;           //   themselves; ip4_lookup: its frame lies in one of the nrg registered
     struct {                //   regions (host address range, device = host + delta); cnet: rg[0]
@@ -6026,87 +6027,153 @@ __device__ __forceinline__ uint32_t mq_rewrite_frame(uint8_t *p, uint32_t avail,
 
 // ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
 // mtod + 14 + 16, priv1 = {nh = val & 0xffff, ttl, hdr_checksum}, edge = val >> 16
+// one mbuf through the queue's ip4_lookup mode: the frame's readable
+// window, with CNDP_MQ_F_RX_PARSE the soft parse and pkt_cls first, then the
+// lookup and node_mbuf_priv1 (written into the mbuf, or the record when
+// staged).  Zero-copy also hands back the frame (mtod) and its readable bytes
+// (<= 255) for a rewrite.
+#define MQ_L3_NONE 0u   // the mbuf or its frame is outside every registered region
+#define MQ_L3_CLS 1u    // pkt_cls sent it to pkt_drop (not IPv4)
+#define MQ_L3_LOOKED 2u // ip4_lookup ran: val
+struct MqL3 {
+    uint32_t st, val;
+    uint64_t priv1;
+    uint8_t *frame;
+    uint32_t favail;
+};
+__device__ __forceinline__ MqL3 mq_l3_one(const MqArgs &a, uint32_t i)
+{
+    MqL3 r{MQ_L3_NONE, 0u, 0ull, nullptr, 0u};
+    const uint64_t w = a.devhdr ? 0u : a.off[i];
+    const uint8_t *p; // bytes 20..35 of the frame
+    uint32_t avail;   // readable bytes from p
+    uint32_t eavail;  // readable bytes from the ethertype (frame byte 12, p - 8)
+    uint64_t m = 0;
+    if (a.zc && a.devhdr) {
+        m = a.mb[i];
+        const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
+        const uint64_t buf = m ? *gp((const uint64_t *)(dm + MB_BUF_ADDR)) : 0u;
+        const uint32_t doff = m ? *gp((const uint16_t *)(dm + MB_DATA_OFF)) : 0u;
+        const uint64_t fh = buf + doff; // pktmbuf_mtod, a host address
+        uint64_t fo = ~0ull, rlen = 0;
+        int64_t delta = 0;
+        for (uint32_t k = 0; k < a.nrg; k++) // the frame's registered region
+            if (fh - a.rg[k].host < a.rg[k].len) {
+                fo = fh - a.rg[k].host;
+                rlen = a.rg[k].len;
+                delta = a.rg[k].delta;
+                break;
+            }
+        if (m == 0 || fo == ~0ull)
+            return r;
+        r.frame = (uint8_t *)(uintptr_t)(fh + delta);
+        r.favail = rlen - fo < 255u ? (uint32_t)(rlen - fo) : 255u;
+        p = r.frame + MQ_W4_AT;
+        avail = rlen - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(rlen - fo > MQ_W4_AT ? rlen - fo - MQ_W4_AT : 0);
+        eavail = rlen - fo > MQ_W4R_AT + 2 ? 2u : (uint32_t)(rlen - fo > MQ_W4R_AT ? rlen - fo - MQ_W4R_AT : 0);
+    } else if (a.zc) {
+        m = a.mb[i];
+        uint32_t fa;
+        uint8_t *f = mq_frame(w, fa);
+        if (m == 0 || f == nullptr)
+            return r;
+        r.frame = f;
+        r.favail = fa;
+        p = f + MQ_W4_AT;
+        avail = fa > MQ_W4_AT ? fa - MQ_W4_AT : 0u;
+        eavail = fa > MQ_W4R_AT ? fa - MQ_W4R_AT : 0u;
+    } else { // staged: the window from MQ_W4R_AT with the soft parse, else from MQ_W4_AT
+        p = a.slab + w + (a.rxparse ? MQ_W4_AT - MQ_W4R_AT : 0u);
+        avail = MQ_W4;
+        eavail = 2u;
+    }
+    if (a.rxparse) {
+        // pktdev_rx's eth_pkt_parse_cb (pktdev_rx.c:24-34, :88-100):
+        // packet_type = l3_ptype(ether_type, 0); then pkt_cls
+        // (pkt_cls.c:19-31): only IPv4 (0x90) goes on to ip4_lookup
+        const uint8_t *e = p - (MQ_W4_AT - MQ_W4R_AT);
+        const uint32_t et = eavail >= 2 ? ((uint32_t)gbyte(e, eavail, 0) << 8) | gbyte(e, eavail, 1) : 0u;
+        const uint32_t pt = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
+        if (a.zc)
+            *gp((uint32_t *)(m + MB_PTYPE)) = pt;
+        if (pt != 0x90u) {
+            r.st = MQ_L3_CLS;
+            return r;
+        }
+    }
+    uint32_t ttl, ck, dip;
+    if (avail >= 16 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p) & 63u) <= 48u) {
+        // ttl, checksum and dst in one load inside one 64-B line: the
+        // frame's only PCIe read when it is read in place
+        const u32x4a4 q = *(const GAS u32x4a4 *)p;
+        ttl = (q.x >> 16) & 0xffu;
+        ck = q.y & 0xffffu;
+        dip = bswap32(alignb(q.w, q.z, 2));
+    } else {
+        ttl = gbyte(p, avail, 2);
+        ck = gbyte(p, avail, 4) | (gbyte(p, avail, 5) << 8);
+        dip = (gbyte(p, avail, 10) << 24) | (gbyte(p, avail, 11) << 16) | (gbyte(p, avail, 12) << 8) |
+              gbyte(p, avail, 13);
+    }
+    r.val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
+    r.priv1 = (uint64_t)(r.val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
+    if (a.zc)
+        *gp((uint64_t *)(m + MB_UDATA64)) = r.priv1;
+    else
+        a.priv1[i] = r.priv1;
+    r.st = MQ_L3_LOOKED;
+    return r;
+}
+
 __global__ __launch_bounds__(MQ_TPB) void k_mq_ip4_lookup(MqArgs a)
 {
     for (uint32_t i = blockIdx.x * MQ_TPB + threadIdx.x; i < a.n; i += gridDim.x * MQ_TPB) {
-        const uint64_t w = a.devhdr ? 0u : a.off[i];
-        const uint8_t *p; // bytes 20..35 of the frame
-        uint32_t avail;   // readable bytes from p
-        uint32_t eavail;  // readable bytes from the ethertype (frame byte 12, p - 8)
-        uint64_t m = 0;
-        if (a.zc && a.devhdr) {
-            m = a.mb[i];
-            const uint8_t *dm = (const uint8_t *)(uintptr_t)m;
-            const uint64_t buf = m ? *gp((const uint64_t *)(dm + MB_BUF_ADDR)) : 0u;
-            const uint32_t doff = m ? *gp((const uint16_t *)(dm + MB_DATA_OFF)) : 0u;
-            const uint64_t fh = buf + doff; // pktmbuf_mtod, a host address
-            uint64_t fo = ~0ull, rlen = 0;
-            int64_t delta = 0;
-            for (uint32_t k = 0; k < a.nrg; k++) // the frame's registered region
-                if (fh - a.rg[k].host < a.rg[k].len) {
-                    fo = fh - a.rg[k].host;
-                    rlen = a.rg[k].len;
-                    delta = a.rg[k].delta;
-                    break;
-                }
-            if (m == 0 || fo == ~0ull) {
-                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
-                continue;
-            }
-            p = (const uint8_t *)(uintptr_t)(fh + delta) + MQ_W4_AT;
-            avail = rlen - fo > MQ_W4_AT + 16 ? 16u : (uint32_t)(rlen - fo > MQ_W4_AT ? rlen - fo - MQ_W4_AT : 0);
-            eavail = rlen - fo > MQ_W4R_AT + 2 ? 2u : (uint32_t)(rlen - fo > MQ_W4R_AT ? rlen - fo - MQ_W4R_AT : 0);
-        } else if (a.zc) {
-            m = a.mb[i];
-            uint32_t fa;
-            const uint8_t *f = mq_frame(w, fa);
-            if (m == 0 || f == nullptr) {
-                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
-                continue;
-            }
-            p = f + MQ_W4_AT;
-            avail = fa > MQ_W4_AT ? fa - MQ_W4_AT : 0u;
-            eavail = fa > MQ_W4R_AT ? fa - MQ_W4R_AT : 0u;
-        } else { // staged: the window from MQ_W4R_AT with the soft parse, else from MQ_W4_AT
-            p = a.slab + w + (a.rxparse ? MQ_W4_AT - MQ_W4R_AT : 0u);
-            avail = MQ_W4;
-            eavail = 2u;
-        }
-        if (a.rxparse) {
-            // pktdev_rx's eth_pkt_parse_cb (pktdev_rx.c:24-34, :88-100):
-            // packet_type = l3_ptype(ether_type, 0); then pkt_cls
-            // (pkt_cls.c:19-31): only IPv4 (0x90) goes on to ip4_lookup
-            const uint8_t *e = p - (MQ_W4_AT - MQ_W4R_AT);
-            const uint32_t et = eavail >= 2 ? ((uint32_t)gbyte(e, eavail, 0) << 8) | gbyte(e, eavail, 1) : 0u;
-            const uint32_t pt = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
-            if (a.zc)
-                *gp((uint32_t *)(m + MB_PTYPE)) = pt;
-            if (pt != 0x90u) {
-                a.edges[i] = (uint16_t)CNDP_MQ_EDGE_CLS_DROP;
-                continue;
-            }
-        }
-        uint32_t ttl, ck, dip;
-        if (avail >= 16 && (((uintptr_t)p) & 3u) == 0 && (((uintptr_t)p) & 63u) <= 48u) {
-            // ttl, checksum and dst in one load inside one 64-B line: the
-            // frame's only PCIe read when it is read in place
-            const u32x4a4 q = *(const GAS u32x4a4 *)p;
-            ttl = (q.x >> 16) & 0xffu;
-            ck = q.y & 0xffffu;
-            dip = bswap32(alignb(q.w, q.z, 2));
-        } else {
-            ttl = gbyte(p, avail, 2);
-            ck = gbyte(p, avail, 4) | (gbyte(p, avail, 5) << 8);
-            dip = (gbyte(p, avail, 10) << 24) | (gbyte(p, avail, 11) << 16) | (gbyte(p, avail, 12) << 8) |
-                  gbyte(p, avail, 13);
-        }
-        const uint32_t val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
-        const uint64_t priv1 = (uint64_t)(val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
-        if (a.zc)
-            *gp((uint64_t *)(m + MB_UDATA64)) = priv1;
+        const MqL3 r = mq_l3_one(a, i);
+        a.edges[i] = (uint16_t)(r.st == MQ_L3_NONE  ? MQ_EDGE_NONE
+                                : r.st == MQ_L3_CLS ? CNDP_MQ_EDGE_CLS_DROP
+                                                    : r.val >> 16);
+    }
+    mq_complete(a);
+}
+
+// CNDP_MQ_F_REWRITE: one block per submitted burst (<= MQ_BURST mbufs), the
+// lookup of every mbuf, then ip4_rewrite_node_process (ip4_rewrite.c:40-247)
+// over the ones ip4_lookup sent to it, in burst order: a block-wide rank among
+// them picks the 4-wide loop's checksum rule for the first (count & ~3) and
+// the tail loop's for the rest, as when ip4_rewrite gets the burst's stream in
+// one call; the rewrite goes into the frame where it lies (zero-copy only).
+#define MQ_L3_TPB MQ_BURST
+__global__ __launch_bounds__(MQ_L3_TPB) void k_mq_l3fwd_burst(MqArgs a)
+{
+    __shared__ uint32_t s_w[MQ_L3_TPB / 64];
+    const uint32_t i0 = a.bstart[blockIdx.x], i1 = a.bstart[blockIdx.x + 1];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t i = i0 + t;
+    const bool in = i < i1;
+    MqL3 r{MQ_L3_NONE, 0u, 0ull, nullptr, 0u};
+    if (in)
+        r = mq_l3_one(a, i);
+    const bool to_rw = in && r.st == MQ_L3_LOOKED && (r.val >> 16) == 0u; // CNE_NODE_IP4_LOOKUP_NEXT_REWRITE
+    const unsigned long long bal = __ballot(to_rw);
+    if (lane == 0)
+        s_w[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), total = 0;
+    for (uint32_t k = 0; k < MQ_L3_TPB / 64; k++) {
+        before += k < wv ? s_w[k] : 0u;
+        total += s_w[k];
+    }
+    if (in) {
+        uint32_t e;
+        if (r.st == MQ_L3_NONE)
+            e = MQ_EDGE_NONE;
+        else if (r.st == MQ_L3_CLS)
+            e = CNDP_MQ_EDGE_CLS_DROP;
+        else if (!to_rw)
+            e = CNDP_MQ_EDGE_LOOKUP_DROP;
         else
-            a.priv1[i] = priv1;
-        a.edges[i] = (uint16_t)(val >> 16);
+            e = mq_rewrite_frame(r.frame, r.favail, r.priv1, before >= (total & ~3u), a.rw);
+        a.edges[i] = (uint16_t)e;
     }
     mq_complete(a);
 }
@@ -6410,6 +6477,7 @@ struct MqSlot {
     uint32_t nrun;         // cnet: runs of equal-size bursts (each ends with at most one short burst)
     uint32_t run_B[MQ_RUNS_MAX], run_n[MQ_RUNS_MAX];
     uint8_t run_closed;
+    uint32_t nb;           // CNDP_MQ_F_REWRITE: submitted bursts (their starts at h_bst)
     void **mb;             // host
     uint8_t *h, *hd;       // pinned + mapped block (host view, device view)
     uint8_t *d;            // device block (cnet classify outputs)
@@ -6432,7 +6500,7 @@ struct cndp_gpu_mq {
     uint32_t *flags, *flags_d;     // pinned completion flags (host / device view)
     uint32_t *tickets;             // device, one per slot
     // byte offsets inside each slot's pinned block (H) and device block (D)
-    uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_stage, h_bytes;
+    uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_stage, h_bst, h_bytes;
     uint64_t d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_win, d_off, d_len, d_md, d_bytes;
     int devhdr;                    // zc with CNDP_MQ_F_DEVICE_HEADERS (ip4_lookup, cnet)
     // cnet device headers: pools seen whose conf.metadata(m) is m + 64 (and
@@ -6491,7 +6559,9 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
         return -EINVAL;
     if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_RX_PARSE))
         return -EINVAL;
-    if ((k.flags & CNDP_MQ_F_RX_PARSE) && k.mode != CNDP_MQ_IP4_LOOKUP)
+    if ((k.flags & (CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE)) && k.mode != CNDP_MQ_IP4_LOOKUP)
+        return -EINVAL;
+    if ((k.flags & CNDP_MQ_F_REWRITE) && !k.umem) // the rewrite goes into the frame where it lies
         return -EINVAL;
     k.batch = k.batch ? k.batch : 8192u;
     k.depth = k.depth ? k.depth : 4u;
@@ -6541,7 +6611,8 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->h_edge = q->h_md + (cnet && zc ? al64(B * 8) : 0);
     q->h_rec = q->h_edge + al64(B * 2);                   // staged: records
     q->h_stage = q->h_rec + (zc || rw || k.mode == CNDP_MQ_MAC_SWAP ? 0 : al64(B * (cnet ? 16 : 8)));
-    q->h_bytes = q->h_stage + B * q->stage;
+    q->h_bst = q->h_stage + B * q->stage;                 // CNDP_MQ_F_REWRITE: burst starts
+    q->h_bytes = q->h_bst + ((k.flags & CNDP_MQ_F_REWRITE) ? al64((B + 1) * 4) : 0);
     q->d_nh = 0;
     q->d_edge = q->d_nh + al64(B * 4);
     q->d_pt = q->d_edge + al64(B);
@@ -6626,6 +6697,7 @@ static MqSlot *mq_open_slot(cndp_gpu_mq_t *q)
     sl->n = sl->polled = 0;
     sl->nrun = 0;
     sl->run_closed = 0;
+    sl->nb = 0;
     sl->stage_used = 0;
     sl->buf_len = 0;
     sl->rg = -1;
@@ -6712,6 +6784,16 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
             return r;
         a.tb = mq_tables(c, v4, nullptr, 0);
         a.rxparse = (q->conf.flags & CNDP_MQ_F_RX_PARSE) != 0;
+        const bool fuse = (q->conf.flags & CNDP_MQ_F_REWRITE) != 0;
+        if (fuse) {
+            if ((r = rw_sync(c, s))) {
+                tbl_release(&c->fib4->t);
+                return r;
+            }
+            a.rw = c->d_rw_tbl;
+            ((uint32_t *)(sl->h + q->h_bst))[sl->nb] = n;
+            a.bstart = (const uint32_t *)(HD + q->h_bst);
+        }
         if (q->devhdr) { // frames in any registered region
             a.devhdr = 1;
             a.nrg = (uint32_t)q->nrg;
@@ -6721,7 +6803,10 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
                 a.rg[k].delta = q->rg[k].delta;
             }
         }
-        hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
+        if (fuse)
+            hipLaunchKernelGGL(k_mq_l3fwd_burst, dim3(sl->nb), dim3(MQ_L3_TPB), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_mq_ip4_lookup, dim3(g), dim3(MQ_TPB), 0, s, a);
         tbl_release(&c->fib4->t);
     } else {
         // one classify per run of equal-size graph bursts, the ptype node's
@@ -7001,6 +7086,8 @@ extern "C" int cndp_gpu_mq_submit(cndp_gpu_mq_t *q, void *const *mbufs, uint32_t
             if (cnet)
                 sl->buf_len = *(const uint16_t *)((const uint8_t *)mbufs[done] + MB_BUF_LEN);
         }
+        if (q->conf.flags & CNDP_MQ_F_REWRITE) // this burst's first mbuf (the kernel's block)
+            ((uint32_t *)(sl->h + q->h_bst))[sl->nb++] = sl->n;
         mq_fill(q, sl, mbufs + done, k);
         if (cnet) { // runs of equal-size bursts, each closed by a shorter one
             if (sl->nrun && !sl->run_closed && k == sl->run_B[sl->nrun - 1]) {

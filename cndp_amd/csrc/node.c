@@ -92,12 +92,17 @@ static int rw_alloc(void)
     return 0;
 }
 
-static int (*rw_next_hook)(uint16_t port_id, uint16_t next_index);
+#define RW_HOOKS_MAX 4
+static int (*rw_next_hook[RW_HOOKS_MAX])(uint16_t port_id, uint16_t next_index);
 
 void cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index))
 {
     pthread_mutex_lock(&node_lock);
-    rw_next_hook = fn;
+    for (int k = 0; k < RW_HOOKS_MAX && fn; k++)
+        if (rw_next_hook[k] == fn || !rw_next_hook[k]) {
+            rw_next_hook[k] = fn;
+            break;
+        }
     pthread_mutex_unlock(&node_lock);
 }
 
@@ -109,12 +114,15 @@ int ip4_rewrite_set_next(uint16_t port_id, uint16_t next_index)
     int r = rw_alloc();
     if (!r)
         ip4_rewrite_nm->next_index[port_id] = next_index;
-    int (*hook)(uint16_t, uint16_t) = rw_next_hook;
+    int (*hook[RW_HOOKS_MAX])(uint16_t, uint16_t);
+    memcpy(hook, rw_next_hook, sizeof(hook));
     pthread_mutex_unlock(&node_lock);
     /* pktdev_ctrl.c:81-84 calls this right after adding the port's tx edge to
-     * ip4_rewrite: the GPU rewrite node mirrors that edge on its drain node */
-    if (!r && hook)
-        r = hook(port_id, next_index);
+     * ip4_rewrite: the GPU rewrite node mirrors that edge on its drain node,
+     * the GPU receive node on its own (and its clones') */
+    for (int k = 0; k < RW_HOOKS_MAX && !r; k++)
+        if (hook[k])
+            r = hook[k](port_id, next_index);
     return r;
 }
 

@@ -47,8 +47,10 @@ CNDP_TUNE_SPEC_GRID = 14
 CNDP_TUNE_SPEC_LISTS = 15
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
 CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS, CNDP_MQ_F_RX_PARSE = 1, 2, 4, 8
+CNDP_MQ_F_REWRITE = 16
 CNDP_MQ_EDGE_NONE = 0xFFFF
 CNDP_MQ_EDGE_CLS_DROP = 0xFFFE
+CNDP_MQ_EDGE_LOOKUP_DROP = 0xFFFD
 CNDP_MQ_STAT_BATCHES, CNDP_MQ_STAT_MBUFS = 1, 2
 CNDP_MQ_NODE_PTYPE, CNDP_MQ_NODE_IP4, CNDP_MQ_NODE_IP6 = 0, 1, 2
 CNDP_MBUF_EDGE_CLS_DROP = 0xFFFF

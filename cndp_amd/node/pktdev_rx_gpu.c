@@ -24,6 +24,18 @@
  * the reference's pkt_cls and ip4_lookup would have used: ip4_rewrite, or
  * pkt_drop (non-IPv4 from pkt_cls; a route to the drop edge from ip4_lookup).
  *
+ * With the frames in registered UMEM (zero-copy) the queue also runs
+ * ip4_rewrite (CNDP_MQ_F_REWRITE): the rewrite data, TTL and checksum go into
+ * each frame the lookup sends to ip4_rewrite, with the 4-wide / tail checksum
+ * rule of ip4_rewrite getting the burst's stream in one call, and the mbuf
+ * leaves directly on its next hop's pktdev_tx edge.  For that this node
+ * carries, after its own four edges, a copy of ip4_rewrite's edge list
+ * (pkt_drop, pktdev_tx-<port>...), kept by a hook on ip4_rewrite_set_next
+ * (pktdev_ctrl.c:81-86) on the node and its per-port clones.  ip4_rewrite
+ * stays registered and idle and gets the stats of the mbufs it stands for.
+ * CNDP_GPU_RX_REWRITE=0 keeps ip4_rewrite as the next node (staged frames
+ * always do).
+ *
  * Why: the host thread never touches a frame.  In the reference chain the
  * soft parse reads each frame's Ethernet header and writes packet_type on the
  * core, which leaves the lines the GPU ip4_lookup node then reads over PCIe
@@ -46,9 +58,10 @@
  * registered its UMEMs with cndp_node_gpu_umem_add(), else staged.  One GPU
  * context and queue per cloned node (per port and graph).
  *
- * Graph stats: pkt_cls and ip4_lookup get the calls and objects they would
- * have processed added to their node stats (cne_graph_worker.h:156-160) at
- * each poll -- every mbuf for pkt_cls, the IPv4 ones for ip4_lookup.
+ * Graph stats: pkt_cls and ip4_lookup (and ip4_rewrite, fused) get the calls
+ * and objects they would have processed added to their node stats
+ * (cne_graph_worker.h:156-160) at each poll -- every mbuf for pkt_cls, the
+ * IPv4 ones for ip4_lookup, the ones sent on to it for ip4_rewrite.
  */
 #include <errno.h>
 #include <stddef.h>
@@ -69,12 +82,15 @@
 
 #define RX_BURST 256 /* CNE_GRAPH_BURST_SIZE (cne_graph.h:30) */
 
-/* the reference's two edges (pktdev_rx_priv.h), then the two this node uses */
+/* the reference's two edges (pktdev_rx_priv.h), then the two this node uses,
+ * then (with the rewrite on the device) ip4_rewrite's edges */
 enum {
     PKTDEV_RX_GPU_NEXT_REWRITE = PKTDEV_RX_NEXT_MAX, /* ip4_lookup's CNE_NODE_IP4_LOOKUP_NEXT_REWRITE */
     PKTDEV_RX_GPU_NEXT_PKT_DROP,                     /* pkt_cls's and ip4_lookup's pkt_drop */
     PKTDEV_RX_GPU_NEXT_MAX,
+    PKTDEV_RX_GPU_NEXT_TX0 = PKTDEV_RX_GPU_NEXT_MAX, /* ip4_rewrite's edge 0 (pkt_drop), 1, ... */
 };
+#define RX_EDGES_MAX 64 /* GPU_NODE_EDGES_MAX */
 
 static struct pktdev_rx_node_main pktdev_rx_main;
 
@@ -83,7 +99,9 @@ struct gpu_rx_state {
     cndp_gpu_mq_t *q;
     /* the replaced nodes in this graph (NULL when absent): their walk stats
      * are credited with the objects they would have processed */
-    struct cne_node *st_cls, *st_lookup;
+    struct cne_node *st_cls, *st_lookup, *st_rewrite;
+    int fused;          /* CNDP_MQ_F_REWRITE: the queue's edges are ip4_rewrite's */
+    uint16_t nb_edges;  /* this node's edges at graph create */
     void *rx[RX_BURST];
     void *done[RX_BURST];
     uint16_t edge[RX_BURST];
@@ -119,20 +137,35 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
         const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, RX_BURST);
         if (k <= 0)
             break;
-        uint16_t n4 = 0;
-        for (int i = 0; i < k; i++) {
-            const uint16_t e = st->edge[i];
-            /* IPv4 (ip4_lookup ran): its value >> 16, 0 = rewrite; pkt_cls's
-             * drop, an unreachable mbuf and a value naming no edge: pkt_drop */
-            n4 = (uint16_t)(n4 + (e < CNDP_MQ_EDGE_CLS_DROP));
-            st->edge[i] = e == CNE_NODE_IP4_LOOKUP_NEXT_REWRITE ? PKTDEV_RX_GPU_NEXT_REWRITE
-                                                                : PKTDEV_RX_GPU_NEXT_PKT_DROP;
+        uint16_t n4 = 0, nrw = 0;
+        if (st->fused) {
+            for (int i = 0; i < k; i++) {
+                /* ip4_rewrite's tx_node: that edge of the copied list (past
+                 * it: pkt_drop); pkt_cls's and ip4_lookup's drops and an
+                 * unreachable mbuf: pkt_drop */
+                const uint16_t e = st->edge[i];
+                n4 = (uint16_t)(n4 + (e < CNDP_MQ_EDGE_CLS_DROP));
+                nrw = (uint16_t)(nrw + (e < CNDP_MQ_EDGE_LOOKUP_DROP));
+                st->edge[i] = e < CNDP_MQ_EDGE_LOOKUP_DROP && PKTDEV_RX_GPU_NEXT_TX0 + e < st->nb_edges
+                                  ? (uint16_t)(PKTDEV_RX_GPU_NEXT_TX0 + e)
+                                  : PKTDEV_RX_GPU_NEXT_PKT_DROP;
+            }
+        } else {
+            for (int i = 0; i < k; i++) {
+                const uint16_t e = st->edge[i];
+                /* IPv4 (ip4_lookup ran): its value >> 16, 0 = rewrite; pkt_cls's
+                 * drop, an unreachable mbuf and a value naming no edge: pkt_drop */
+                n4 = (uint16_t)(n4 + (e < CNDP_MQ_EDGE_CLS_DROP));
+                st->edge[i] = e == CNE_NODE_IP4_LOOKUP_NEXT_REWRITE ? PKTDEV_RX_GPU_NEXT_REWRITE
+                                                                    : PKTDEV_RX_GPU_NEXT_PKT_DROP;
+            }
         }
         if (cne_graph_has_stats_feature()) {
             node_stat(st->st_cls, (uint16_t)k);
             node_stat(st->st_lookup, n4);
+            node_stat(st->st_rewrite, nrw);
         }
-        gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, PKTDEV_RX_GPU_NEXT_MAX, st->grp);
+        gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, st->nb_edges, st->grp);
         total = (uint16_t)(total + k);
         if (k < RX_BURST)
             break;
@@ -210,11 +243,20 @@ static int pktdev_rx_gpu_init(const struct cne_graph *graph, struct cne_node *no
     for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)
         if (cndp_gpu_host_register(st->gpu, umem, ulen, NULL) == 0 && !conf.umem)
             conf.umem = umem;
+    st->nb_edges = (uint16_t)cne_node_edge_count(node->id);
+    if (st->nb_edges > RX_EDGES_MAX)
+        st->nb_edges = RX_EDGES_MAX;
+    /* ip4_rewrite on the device when the frames are in place and this node
+     * carries ip4_rewrite's edges (ip4_rewrite_set_next ran, rx_mirror_edges) */
+    st->fused = conf.umem && st->nb_edges > PKTDEV_RX_GPU_NEXT_TX0 && env_u32("CNDP_GPU_RX_REWRITE", 1);
+    if (st->fused)
+        conf.flags |= CNDP_MQ_F_REWRITE;
     if ((r = cndp_gpu_mq_create(st->gpu, &conf, &st->q)) < 0)
         goto fail;
     /* graph.c:291-295 lays the graph's nodes out before their init runs */
     st->st_cls = cne_graph_get_node_by_name(graph, "pkt_cls");
     st->st_lookup = cne_graph_get_node_by_name(graph, "ip4_lookup");
+    st->st_rewrite = st->fused ? cne_graph_get_node_by_name(graph, "ip4_rewrite") : NULL;
     ctx->st = st;
     return 0;
 fail:
@@ -246,6 +288,37 @@ static struct cne_node_register pktdev_rx_node_base = {
         },
 };
 CNE_NODE_REGISTER(pktdev_rx_node_base);
+
+/* ip4_rewrite_set_next's hook (pktdev_ctrl.c:81-86 calls it right after it
+ * added a port's pktdev_tx edge to ip4_rewrite): this node and every clone of
+ * it take ip4_rewrite's edge list after their own four, so the tx_node the
+ * queue returns names the same next node here */
+static int rx_mirror_edges(uint16_t port_id, uint16_t next_index)
+{
+    (void)port_id;
+    (void)next_index;
+    const cne_node_t rw = cne_node_from_name("ip4_rewrite");
+    if (rw == CNE_NODE_ID_INVALID)
+        return 0; /* no ip4_rewrite node in this build: nothing to mirror */
+    char *names[RX_EDGES_MAX]; /* cne_node_edge_get hands out the node's own name pointers */
+    const cne_edge_t n = cne_node_edge_count(rw);
+    if (n == CNE_EDGE_ID_INVALID || n > RX_EDGES_MAX - PKTDEV_RX_GPU_NEXT_TX0)
+        return -EINVAL;
+    if (cne_node_edge_get(rw, names) != n)
+        return -EINVAL;
+    if (cne_node_edge_update(pktdev_rx_node_base.id, PKTDEV_RX_GPU_NEXT_TX0, (const char **)names, n) ==
+        CNE_EDGE_ID_INVALID)
+        return -EINVAL;
+    for (pktdev_rx_node_elem_t *e = pktdev_rx_main.head; e; e = e->next)
+        if (cne_node_edge_update(e->nid, PKTDEV_RX_GPU_NEXT_TX0, (const char **)names, n) == CNE_EDGE_ID_INVALID)
+            return -EINVAL;
+    return 0;
+}
+
+__attribute__((constructor)) static void rx_gpu_hook(void)
+{
+    cndp_node_ip4_rewrite_next_hook(rx_mirror_edges);
+}
 
 /* pktdev_rx_priv.h: what pktdev_ctrl.c uses to clone the node per port */
 struct pktdev_rx_node_main *pktdev_rx_get_node_data_get(void)

@@ -245,6 +245,15 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
  * node that replaces pktdev_rx -> pkt_cls -> ip4_lookup (pktdev_rx_gpu.c). */
 #define CNDP_MQ_F_RX_PARSE (1u << 3)
 #define CNDP_MQ_EDGE_CLS_DROP 0xFFFEu
+/* ip4_lookup, zero-copy only: ip4_rewrite too (ip4_rewrite.c:40-247) over
+ * the mbufs ip4_lookup sends to it, per submitted burst -- the burst's first
+ * (its count & ~3) of them take the 4-wide loop's checksum rule, the rest the
+ * tail's, as when ip4_rewrite gets that burst's stream in one call -- with
+ * the rewrite data, TTL and checksum written into the frame; edge = the next
+ * hop's tx_node (ip4_rewrite's edge index, 0 pkt_drop); an mbuf ip4_lookup
+ * sent elsewhere (pkt_drop) comes back with CNDP_MQ_EDGE_LOOKUP_DROP. */
+#define CNDP_MQ_F_REWRITE (1u << 4)
+#define CNDP_MQ_EDGE_LOOKUP_DROP 0xFFFDu
 #define CNDP_MQ_NODE_PTYPE 0u
 #define CNDP_MQ_NODE_IP4 1u
 #define CNDP_MQ_NODE_IP6 2u

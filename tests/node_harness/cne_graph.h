@@ -46,6 +46,7 @@ cne_node_t __cne_node_register(const struct cne_node_register *node);
 cne_edge_t cne_node_edge_count(cne_node_t id);
 cne_edge_t cne_node_edge_update(cne_node_t id, cne_edge_t from, const char **next_nodes, uint16_t nb_edges);
 cne_node_t cne_node_edge_get(cne_node_t id, char *next_nodes[]);
+cne_node_t cne_node_from_name(const char *name); /* cne_graph.h:500 */
 
 /* cne_graph.h:370 (the node of this name in this graph) and :649 */
 struct cne_node *cne_graph_get_node_by_name(const struct cne_graph *graph, const char *node_name);

@@ -90,6 +90,13 @@ static const char *edge_name(int r, int e)
     return dyn_n[r] ? dyn_name[r][e] : regs[r]->next_nodes[e];
 }
 
+/* cne_graph.h:500: the id of the registered node of this name */
+cne_node_t cne_node_from_name(const char *name)
+{
+    const int r = find(name);
+    return r < 0 ? CNE_NODE_ID_INVALID : regs[r]->id;
+}
+
 cne_edge_t cne_node_edge_count(cne_node_t id)
 {
     const int r = reg_of(id);

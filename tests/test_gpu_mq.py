@@ -706,6 +706,62 @@ def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
     assert set(np.unique(edges).tolist()) == {0, 1, 2, 3, 4}
 
 
+@pytest.mark.parametrize("headers", ["host", "device"])
+@pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
+def test_mq_l3fwd_fused(l3, gpu, headers, kind):
+    """CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE: l3fwd-graph's pktdev_rx soft
+    parse, pkt_cls, ip4_lookup and ip4_rewrite in one queue pass, ip4_rewrite
+    per submitted burst as when it gets that burst's stream in one call -- byte
+    for byte against the oracle's node loops over the same bursts (checksums
+    0xFFFE / 0xFFFF and high-bit cksum words seeded, where the 4-wide and
+    tail rules differ), edges = the next hop's tx_node, LOOKUP_DROP, CLS_DROP."""
+    cl, fib, t4 = l3
+    tbl = _rewrite_setup(cl, 41)
+    n = 12000
+    gp, op = MbufPool(n), MbufPool(n)
+    fr = _mixed_l3_frames(n, seed=42)
+    for p in (gp, op):
+        if kind == "shifted":
+            p.hdr["data_off"] = 256 + np.arange(n) % 61
+        p.fill(fr)
+        p.hdr["udata64"] = 0x1234
+        d = p.data_pos().astype(np.int64)
+        for sel, lo in ((np.arange(n) % 53 == 5, 0xFE), (np.arange(n) % 59 == 7, 0xFF)):
+            p.mem[d[sel] + 24] = lo
+            p.mem[d[sel] + 25] = 0xFF
+    flags = N.CNDP_MQ_F_RX_PARSE | N.CNDP_MQ_F_REWRITE | (N.CNDP_MQ_F_DEVICE_HEADERS if headers == "device" else 0)
+    bursts = _bursts(n, 43, kind)
+    order = np.random.default_rng(44).permutation(n)
+    cl.host_register(gp.mem)
+    try:
+        q = MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, flags=flags, batch=4096, depth=3, umem=gp.base)
+        addrs, edges = q.run(gp, order, bursts)
+        q.close()
+    finally:
+        cl.host_unregister(gp.mem)
+    assert np.array_equal(gp.index_of(addrs), order)
+    # the oracle: per submitted burst, the receive chain, then ip4_rewrite over
+    # the burst's mbufs ip4_lookup sent to it, in order
+    want = np.zeros(n, np.uint16)
+    pos = 0
+    for b in bursts:
+        idx = order[pos:pos + b]
+        e = np.zeros(b, np.uint16)
+        O.l3rx_chain_mbufs(op.ptrs(idx), b, t4, burst=256, edges=e)
+        rw = idx[e == 0]
+        tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
+        eb = np.where(e == N.CNDP_MQ_EDGE_CLS_DROP, e, N.CNDP_MQ_EDGE_LOOKUP_DROP).astype(np.uint16)
+        eb[e == 0] = tx
+        want[pos:pos + b] = eb
+        pos += b
+    assert np.array_equal(edges, want)
+    assert np.array_equal(gp.hdr["packet_type"], op.hdr["packet_type"])
+    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
+    bad = np.nonzero(np.any(gp.mem.reshape(n, -1)[:, HDR:] != op.mem.reshape(n, -1)[:, HDR:], axis=1))[0]
+    assert bad.size == 0, f"{bad.size} frames differ from the oracle's, first {bad[:4]}"
+    assert {N.CNDP_MQ_EDGE_CLS_DROP, N.CNDP_MQ_EDGE_LOOKUP_DROP, 0, 1, 2, 3, 4} <= set(np.unique(edges).tolist())
+
+
 @pytest.mark.parametrize("flags", [0, N.CNDP_MQ_F_DEVICE_HEADERS], ids=["host_headers", "device_headers"])
 def test_mq_zero_copy_regions(l3, gpu, flags):
     """Zero-copy over several registered regions (a graph's ports with pools

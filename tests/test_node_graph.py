@@ -737,7 +737,8 @@ def test_rx_node_registry():
     e0, e1 = ctypes.c_char_p(), ctypes.c_char_p()
     H.harness_node_info(i, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
     assert name.value == b"pktdev_rx" and fl.value == 1 and ne.value == 4
-    assert _edges_of(H, i) == PKTDEV_RX_EDGES
+    # (after its own four: ip4_rewrite's edges, once ip4_rewrite_set_next ran)
+    assert _edges_of(H, i)[:4] == PKTDEV_RX_EDGES
     assert {"ip4_lookup", "ip4_rewrite", "pkt_cls"} <= set(ids)
 
 
@@ -750,15 +751,20 @@ def test_rx_node_init_fails_loudly_without_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, "host_headers", False])
+@pytest.mark.parametrize("zero_copy", [True, "host_headers", "no_rewrite", False])
 def test_rx_node_graph_walk(gpu, zero_copy):
-    """Graph walks over the GPU pktdev_rx node chained into the GPU
-    ip4_rewrite node: it pulls 256-mbuf bursts from its port and every mbuf
-    ends where l3fwd-graph's pktdev_rx -> pkt_cls -> ip4_lookup -> ip4_rewrite
-    walk sends it (pkt_drop, or its next hop's tx edge) with the soft parse's
-    packet_type, ip4_lookup's priv1 (IPv4 only) and the rewritten frame of the
-    oracle chain; pkt_cls and ip4_lookup get the stats of the mbufs they stand
-    for.  Mixed frames: routed IPv4, IPv6, VLAN, ARP and fuzz."""
+    """Graph walks over the GPU pktdev_rx node: it pulls 256-mbuf bursts from
+    its port and every mbuf ends where l3fwd-graph's pktdev_rx -> pkt_cls ->
+    ip4_lookup -> ip4_rewrite walk sends it (pkt_drop, or its next hop's tx
+    edge) with the soft parse's packet_type, ip4_lookup's priv1 (IPv4 only)
+    and the rewritten frame of the oracle chain; pkt_cls, ip4_lookup (and
+    ip4_rewrite) get the stats of the mbufs they stand for.  Zero-copy, the
+    node runs ip4_rewrite itself (CNDP_MQ_F_REWRITE), per receive burst as
+    ip4_rewrite gets it in one call, so every frame matches the oracle's
+    per-burst chain byte for byte; "no_rewrite" (CNDP_GPU_RX_REWRITE=0) and
+    staged frames go on to the GPU ip4_rewrite node, whose bursts are its
+    queue's polls (checksums 0xFFFE / 0xFFFF, whose rule depends on that
+    split, not compared).  Mixed frames: routed IPv4, IPv6, VLAN, ARP, fuzz."""
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
     from cndp_amd import pktgen
@@ -773,6 +779,12 @@ def test_rx_node_graph_walk(gpu, zero_copy):
     for p in (gp, op):
         p.fill(fr)
         p.hdr["udata64"] = 0x5A5A5A5A
+        # header checksums 0xFFFE / 0xFFFF, where the 4-wide and tail rules of
+        # ip4_rewrite differ (ip4_rewrite.c:97-110 / :209-216)
+        d = p.data_pos().astype(np.int64)
+        for sel, lo in ((np.arange(n) % 97 == 5, 0xFE), (np.arange(n) % 89 == 7, 0xFF)):
+            p.mem[d[sel] + 24] = lo
+            p.mem[d[sel] + 25] = 0xFF
     NodeFib.fini()
     L.cndp_node_ip4_rewrite_reset()
     L.cndp_node_gpu_umem_reset()
@@ -781,16 +793,21 @@ def test_rx_node_graph_walk(gpu, zero_copy):
     os.environ["CNDP_GPU_BATCH"] = "4096"
     if zero_copy == "host_headers":
         os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
+    if zero_copy == "no_rewrite":
+        os.environ["CNDP_GPU_RX_REWRITE"] = "0"
+    fused = zero_copy in (True, "host_headers")
     routes = pktgen.l3fwd_routes()
     ids = _node_ids(H)
     assert H.harness_pktdev_rx_port(ids["pktdev_rx"], port) == 0
     assert H.harness_rx_load(port, gp.ptrs(np.arange(n)), n) == 0
     try:
-        _eth_config(H, L, ports)
+        _eth_config(H, L, ports)   # ip4_rewrite's tx edges; the hook copies them onto pktdev_rx
+        assert _edges_of(H, ids["pktdev_rx"]) == PKTDEV_RX_EDGES + _edges_of(H, ids["ip4_rewrite"])
         tbl = _rw_table(L, 82, ports)
         H.harness_chain(1)
         assert H.harness_graph_create(13) == 0
         os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+        os.environ.pop("CNDP_GPU_RX_REWRITE", None)
         for ip, d, nh in routes:
             assert cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
         assert H.harness_walk_until(n) >= 0
@@ -800,36 +817,95 @@ def test_rx_node_graph_walk(gpu, zero_copy):
         got = np.full(n, -1, np.int64)
         for k, nm in enumerate(names):
             m = H.harness_take_edge(nm, buf, n)
-            got[gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))] = k
+            idx = gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))
+            assert np.all(np.diff(idx) > 0), f"{nm}: out of receive order"
+            got[idx] = k
         stats = {}
-        for nm in (b"pkt_cls", b"ip4_lookup"):
+        for nm in (b"pkt_cls", b"ip4_lookup", b"ip4_rewrite"):
             c, o = ctypes.c_uint64(), ctypes.c_uint64()
             assert H.harness_node_stats(nm, ctypes.byref(c), ctypes.byref(o)) == 0
             stats[nm] = o.value
     finally:
         os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+        os.environ.pop("CNDP_GPU_RX_REWRITE", None)
         H.harness_chain(0)
         H.harness_graph_destroy()
         H.harness_edges_reset()
         L.cndp_node_ip4_rewrite_reset()
         L.cndp_node_gpu_umem_reset()
         os.environ.pop("CNDP_GPU_BATCH", None)
-    # the reference chain on the oracle's copy
+    # the reference chain on the oracle's copy: the receive chain per 256-mbuf
+    # burst, then ip4_rewrite over each burst's mbufs ip4_lookup sent to it
     t24, t8 = O.dir24_8_build(list(routes), N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
     e = np.zeros(n, np.uint16)
     O.l3rx_chain_mbufs(op.ptrs(np.arange(n)), n, (t24, t8), edges=e)
     assert np.array_equal(gp.hdr["packet_type"], op.hdr["packet_type"])
     assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
-    rw = np.nonzero(e == 0)[0]
-    tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
     want = np.zeros(n, np.int64)
-    want[rw] = tx
+    for b0 in range(0, n, 256):
+        ib = np.arange(b0, min(b0 + 256, n))
+        rw = ib[e[ib] == 0]
+        want[rw] = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
     assert np.array_equal(got, want)
     d = op.data_pos().astype(np.int64)
     ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
-    ok = (ck != 0xFFFE) & (ck != 0xFFFF)
+    ok = np.ones(n, bool) if fused else (ck != 0xFFFE) & (ck != 0xFFFF)
     diff = np.any(gp.mem.reshape(n, -1)[:, 64:] != op.mem.reshape(n, -1)[:, 64:], axis=1)
     assert not np.any(diff & ok)
     assert stats[b"pkt_cls"] == n and stats[b"ip4_lookup"] == int((e != 0xFFFE).sum())
-    assert (e == 0xFFFE).sum() > 100 and rw.size > n // 2 and (got == 0).sum() > 0
+    nrw = int((e == 0).sum())
+    assert (e == 0xFFFE).sum() > 100 and nrw > n // 2 and (got == 0).sum() > 0
+    if fused:
+        assert stats[b"ip4_rewrite"] == nrw
+        rw_all = np.nonzero(e == 0)[0]
+        assert ((ck[rw_all] == 0xFFFE) | (ck[rw_all] == 0xFFFF)).sum() > 0   # the rule-dependent ones, compared
     NodeFib.fini()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("harness", ["rx", "cnet"])
+def test_rx_nodes_idle_and_admin_down(gpu, harness):
+    """The two GPU receive nodes on an idle port return 0 and enqueue nothing;
+    on a port whose admin state is down they pass pktdev_rx_burst's
+    PKTDEV_ADMIN_STATE_DOWN through (pktdev_rx.c:107-125, eth_rx.c:112-130)
+    and enqueue nothing; a later burst on the same port still comes out."""
+    from cndp_amd import pktgen
+    from cndp_amd.mbuf import MbufPool
+    L = N.lib()
+    if harness == "rx":
+        H = _rx_harness()
+        nid = _node_ids(H)["pktdev_rx"]
+        assert H.harness_pktdev_rx_port(nid, 5) == 0
+        frames = pktgen.packed_ipv4(300, routes=pktgen.l3fwd_routes(), seed=91)
+    else:
+        from helpers import cnet_fibs
+        H = _cnet_harness()
+        fib, fib6, routes, v6, _, _ = cnet_fibs()
+        H.harness_cnet_set(fib.h, fib6.h)
+        nid = 0
+        assert H.harness_eth_rx_port(nid, 5) == 0
+        frames = pktgen.imix(300, v4routes=routes, v6routes=v6, seed=91)
+    H.harness_process.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint16]
+    H.harness_process.restype = ctypes.c_int
+    H.harness_rx_down.argtypes = [ctypes.c_uint16, ctypes.c_int]
+    pool = MbufPool(300)
+    pool.fill(frames)
+    L.cndp_node_gpu_umem_reset()
+    assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes)) == 0
+    name = b"pktdev_rx" if harness == "rx" else b"eth_rx"
+    try:
+        assert H.harness_graph_create(14) == 0
+        assert H.harness_rx_load(5, None, 0) == 0
+        H.harness_reset_counts()
+        assert H.harness_process(name, None, 0) == 0 and H.harness_total() == 0
+        assert H.harness_rx_load(5, pool.ptrs(np.arange(300)), 300) == 0
+        H.harness_rx_down(5, 1)
+        assert H.harness_process(name, None, 0) == 0xFFFF and H.harness_total() == 0
+        assert H.harness_rx_left(5) == 300
+        H.harness_rx_down(5, 0)
+        assert H.harness_walk_until(300) >= 0
+        assert H.harness_total() == 300 and H.harness_rx_left(5) == 0
+    finally:
+        H.harness_rx_down(5, 0)
+        H.harness_graph_destroy()
+        L.cndp_node_gpu_umem_reset()
