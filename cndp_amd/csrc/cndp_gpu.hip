@@ -6557,7 +6557,8 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.mode != CNDP_MQ_IP4_LOOKUP && k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_MAC_SWAP &&
         k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
-    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_RX_PARSE))
+    if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_RX_PARSE |
+                    CNDP_MQ_F_REWRITE))
         return -EINVAL;
     if ((k.flags & (CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE)) && k.mode != CNDP_MQ_IP4_LOOKUP)
         return -EINVAL;
