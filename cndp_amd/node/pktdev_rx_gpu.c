@@ -101,6 +101,7 @@ struct gpu_rx_state {
      * are credited with the objects they would have processed */
     struct cne_node *st_cls, *st_lookup, *st_rewrite;
     int fused;          /* CNDP_MQ_F_REWRITE: the queue's edges are ip4_rewrite's */
+    int tx0_drop;       /* fused and ip4_rewrite's edge 0 is pkt_drop */
     uint16_t nb_edges;  /* this node's edges at graph create */
     void *rx[RX_BURST];
     void *done[RX_BURST];
@@ -146,7 +147,8 @@ static uint16_t rx_drain(struct cne_graph *graph, struct cne_node *node, struct 
                 const uint16_t e = st->edge[i];
                 n4 = (uint16_t)(n4 + (e < CNDP_MQ_EDGE_CLS_DROP));
                 nrw = (uint16_t)(nrw + (e < CNDP_MQ_EDGE_LOOKUP_DROP));
-                st->edge[i] = e < CNDP_MQ_EDGE_LOOKUP_DROP && PKTDEV_RX_GPU_NEXT_TX0 + e < st->nb_edges
+                st->edge[i] = e < CNDP_MQ_EDGE_LOOKUP_DROP && PKTDEV_RX_GPU_NEXT_TX0 + e < st->nb_edges &&
+                                      !(e == 0 && st->tx0_drop)
                                   ? (uint16_t)(PKTDEV_RX_GPU_NEXT_TX0 + e)
                                   : PKTDEV_RX_GPU_NEXT_PKT_DROP;
             }
@@ -249,8 +251,15 @@ static int pktdev_rx_gpu_init(const struct cne_graph *graph, struct cne_node *no
     /* ip4_rewrite on the device when the frames are in place and this node
      * carries ip4_rewrite's edges (ip4_rewrite_set_next ran, rx_mirror_edges) */
     st->fused = conf.umem && st->nb_edges > PKTDEV_RX_GPU_NEXT_TX0 && env_u32("CNDP_GPU_RX_REWRITE", 1);
-    if (st->fused)
+    if (st->fused) {
         conf.flags |= CNDP_MQ_F_REWRITE;
+        /* ip4_rewrite's edge 0 is pkt_drop (ip4_rewrite.c's next_nodes): its
+         * drops then take this node's own pkt_drop edge, so pkt_drop gets one
+         * enqueue per poll in receive order */
+        char *names[RX_EDGES_MAX];
+        st->tx0_drop = cne_node_edge_get(node->id, names) == st->nb_edges &&
+                       strcmp(names[PKTDEV_RX_GPU_NEXT_TX0], "pkt_drop") == 0;
+    }
     if ((r = cndp_gpu_mq_create(st->gpu, &conf, &st->q)) < 0)
         goto fail;
     /* graph.c:291-295 lays the graph's nodes out before their init runs */

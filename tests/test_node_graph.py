@@ -818,7 +818,11 @@ def test_rx_node_graph_walk(gpu, zero_copy):
         for k, nm in enumerate(names):
             m = H.harness_take_edge(nm, buf, n)
             idx = gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))
-            assert np.all(np.diff(idx) > 0), f"{nm}: out of receive order"
+            # pkt_drop takes drops from two nodes when ip4_rewrite runs as its
+            # own node (rx node, then the rewrite node's polls), as the
+            # reference's pkt_drop stream does (pkt_cls, ip4_lookup, ip4_rewrite)
+            if fused or nm != b"pkt_drop":
+                assert np.all(np.diff(idx) > 0), f"{nm}: out of receive order"
             got[idx] = k
         stats = {}
         for nm in (b"pkt_cls", b"ip4_lookup", b"ip4_rewrite"):

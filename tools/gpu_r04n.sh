@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 session N: the node-path GPU tests after the CNDP_MQ_F_REWRITE flag
-# fix, then probe8 (window reads by slab allocation / load flavour).
+# Round-4 session N: the node-path GPU tests, probe8 (window reads by slab
+# allocation / load flavour), then the whole GPU suite and the default bench.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 OUT=gpurun_out
 mkdir -p $OUT
@@ -18,6 +18,10 @@ step() { # name timeout cmd...
     fi
     return $rc
 }
-step pytest_nodes 400 python3 -u -m pytest tests/test_gpu_mq.py tests/test_node_graph.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread || exit 1
+step pytest_nodes 400 python3 -u -m pytest tests/test_gpu_mq.py tests/test_node_graph.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
 step probe8 400 bash tools/probe8.sh 24
+cat $OUT/${TAG}_probe8.log
+step pytest 600 python3 -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread --deselect tests/test_gpu_mq.py --deselect tests/test_node_graph.py
+step bench 600 python3 -u bench.py || exit 1
+grep '^{' $OUT/${TAG}_bench.log > $OUT/${TAG}_bench.json || true
 echo done
