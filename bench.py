@@ -71,14 +71,26 @@ def setup_dist():
     return world, rank, local
 
 
+FRAME_MEM = {"c2": None, "c3": None, "c3rw": None, "c4": None, "c5": None}
+
+
+def frame_mem_name(cfg: str) -> str:
+    m = FRAME_MEM.get(cfg)
+    return "torch tensor (hipMalloc)" if m is None else f"cndp_gpu_frames_alloc ({m})"
+
+
 def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac: float = 0.9,
-                ring: int = 0):
+                ring: int = 0, frame_mem: str | None = "default"):
     from cndp_amd import native as N
     from cndp_amd import pktgen
     from cndp_amd.classify import Classifier
     from cndp_amd.fib import Fib, Fib6, node_ip4_add_input, node_ip4_route_add, node_ip6_add_input
 
     desc, n, algo = CONFIGS[cfg]
+    # where the frames live: a torch (hipMalloc) tensor, or device frame memory
+    # from cndp_gpu_frames_alloc ("uncached", the receive-ring memory a NIC's
+    # peer DMA fills; "cached")
+    fm = FRAME_MEM.get(cfg) if frame_mem == "default" else (None if frame_mem == "torch" else frame_mem)
     if n_override:
         n = n_override
     seed = pktgen.SEED + rank
@@ -94,7 +106,7 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
         state["fib"] = fib
         state["mode"] = N.CNDP_MODE_HASH if cfg == "c2" else N.CNDP_MODE_L3FWD
         state["frames"] = pktgen.packed_ipv4(n, routes=routes, seed=seed, device=dev,
-                                             in_route_frac=in_route_frac)
+                                             in_route_frac=in_route_frac, frame_mem=fm)
     else:
         nr = 1024
         fib = Fib("rt4-fib", N.CNE_FIB_DIR24_8, default_nh=(0 << 24) | (nr + 1), max_routes=nr,
@@ -109,9 +121,10 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
         cl.set_fib(fib, fib6)
         state.update(fib=fib, fib6=fib6, v6routes=v6, mode=N.CNDP_MODE_CNET)
         if cfg == "c4":
-            state["frames"] = pktgen.imix(n, seed=seed, v4routes=routes, v6routes=v6, device=dev)
+            state["frames"] = pktgen.imix(n, seed=seed, v4routes=routes, v6routes=v6, device=dev, frame_mem=fm)
         else:
-            fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed, device=dev)
+            fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed, device=dev,
+                                    frame_mem=fm)
             pktgen.corrupt_cksum(fr, 1024, seed)
             state["frames"] = fr
     # l3fwd / hash: the graph edge is nh >> 16 (no separate edge stream);
@@ -130,11 +143,13 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     for r in range(1, R):
         if cfg in ("c2", "c3", "c3rw"):
             fr = pktgen.packed_ipv4(n, routes=routes, seed=seed + 1000 * r, device=dev,
-                                    in_route_frac=in_route_frac)
+                                    in_route_frac=in_route_frac, frame_mem=fm)
         elif cfg == "c4":
-            fr = pktgen.imix(n, seed=seed + 1000 * r, v4routes=routes, v6routes=state["v6routes"], device=dev)
+            fr = pktgen.imix(n, seed=seed + 1000 * r, v4routes=routes, v6routes=state["v6routes"], device=dev,
+                             frame_mem=fm)
         else:
-            fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed + 1000 * r, device=dev)
+            fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed + 1000 * r, device=dev,
+                                    frame_mem=fm)
             pktgen.corrupt_cksum(fr, 1024, seed + 1000 * r)
         o = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
         o["bins"] = state["out"]["bins"]
@@ -439,7 +454,7 @@ def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, p
     value = n * world * steps / elapsed / 1e6
     res = {"config": cfg, "workload": st["desc"], "value": round(value, 2),
            "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "packets_per_gpu": n,
-           "ring_batches": len(st["ring"]), "parity_sample_vs_oracle": ok,
+           "ring_batches": len(st["ring"]), "frame_memory": frame_mem_name(cfg), "parity_sample_vs_oracle": ok,
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(cfg),
                         "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_pkt": st["algo"]}}
@@ -913,6 +928,9 @@ def main():
                     help="other configs measured after the headline (comma list, '' = none)")
     ap.add_argument("--no-imix", action="store_true", help="same as --extra ''")
     ap.add_argument("--no-node", action="store_true", help="skip the pktmbuf node-boundary rates")
+    ap.add_argument("--frame-mem", default="default", choices=["default", "torch", "uncached", "cached"],
+                    help="frame slabs: torch (hipMalloc) tensors or cndp_gpu_frames_alloc memory; "
+                         "default = FRAME_MEM per config")
     ap.add_argument("--in-route-frac", type=float, default=0.9,
                     help="share of DIPs inside the route set (SURVEY §8(d): 0.9)")
     ap.add_argument("--ring", type=int, default=0,
@@ -928,6 +946,9 @@ def main():
     ap.add_argument("--unroll", type=int, default=None)
     ap.add_argument("--bpc", type=int, default=None)
     args = ap.parse_args()
+    if args.frame_mem != "default":
+        for k in FRAME_MEM:
+            FRAME_MEM[k] = None if args.frame_mem == "torch" else args.frame_mem
     if args.no_imix:
         args.extra = ""
 
@@ -1042,7 +1063,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic (seeded counter-hash frames generated in HBM)",
             "config": {"workload": st["desc"], "config": args.config, "packets_per_gpu": n,
-                       "frame_layout": layout,
+                       "frame_layout": layout, "frame_memory": frame_mem_name(args.config),
                        "ring_batches": ring_len,
                        "routes": len(st["routes"]), "parallelism": f"dp{world} (replicated FIB, sharded batches)",
                        "parity_sample_vs_oracle": parity,

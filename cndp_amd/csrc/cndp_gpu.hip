@@ -5652,6 +5652,34 @@ extern "C" int cndp_gpu_mac_swap(cndp_gpu_ctx_t *c, const struct cndp_batch *b, 
     return 0;
 }
 
+// Device frame memory (cndp_gpu.h): the HBM a NIC's peer DMA or a host copy
+// fills with frames and the classify kernels read in place.  Uncached
+// (hipDeviceMallocUncached, MTYPE UC): no GPU L2 line of it can go stale under
+// a peer's writes, and the kernels' sparse 64-B window reads (C4 IMIX, C5
+// 1536-B strides) allocate no L2 lines -- DESIGN.md §6 (round 4) measures them
+// faster than from hipMalloc memory.  CNDP_FRAMES_CACHED takes plain hipMalloc.
+extern "C" int cndp_gpu_frames_alloc(int device, uint64_t bytes, uint32_t flags, void **dptr)
+{
+    if (dptr)
+        *dptr = nullptr;
+    if (!dptr || !bytes || (flags & ~CNDP_FRAMES_CACHED))
+        return -EINVAL;
+    if (device >= 0 && set_device(device))
+        return -ENODEV;
+    if (flags & CNDP_FRAMES_CACHED)
+        HIP_TRY(hipMalloc(dptr, bytes));
+    else
+        HIP_TRY(hipExtMallocWithFlags(dptr, bytes, hipDeviceMallocUncached));
+    return 0;
+}
+
+extern "C" int cndp_gpu_frames_free(void *dptr)
+{
+    if (dptr)
+        HIP_TRY(hipFree(dptr));
+    return 0;
+}
+
 // Pin + map host memory (an AF_XDP UMEM region, a socket buffer pool) so the
 // device reads frames from it in place (zero-copy ingest) and DMA runs at
 // full rate.  *dev_ptr is the device-side address of `ptr`.

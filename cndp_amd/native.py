@@ -33,6 +33,7 @@ CNDP_EDGE_CLS_DROP = 0xFF
 CNDP_RSS_KEY_LEN = 40
 CNDP_RETA_MAX = 512
 CNDP_BINS_MAX = 1024
+CNDP_FRAMES_CACHED = 1
 CNDP_TUNE_NT, CNDP_TUNE_UNROLL, CNDP_TUNE_BLOCKS_PER_CU, CNDP_TUNE_TILE, CNDP_TUNE_DIR16 = 1, 2, 3, 4, 5
 CNDP_TUNE_CNET_TILE = 6
 CNDP_TUNE_HOST_CHUNK = 7
@@ -167,6 +168,8 @@ def lib():
         "cndp_gpu_classify_host": (c_int, [c_void_p, POINTER(Batch)]),
         "cndp_gpu_host_register": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_void_p)]),
         "cndp_gpu_host_unregister": (c_int, [c_void_p, c_void_p]),
+        "cndp_gpu_frames_alloc": (c_int, [c_int, c_uint64, c_uint32, POINTER(c_void_p)]),
+        "cndp_gpu_frames_free": (c_int, [c_void_p]),
         "cndp_gpu_l3fwd_mbufs": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
         "cndp_gpu_ip4_rewrite_set_next": (c_int, [c_void_p, c_uint16, c_uint16]),
         "cndp_gpu_ip4_rewrite_add": (c_int, [c_void_p, c_uint16, c_void_p, c_uint8, c_uint16]),

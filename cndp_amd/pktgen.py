@@ -209,10 +209,54 @@ class Frames:
         return self.n * 64
 
 
+class _FrameMemory:
+    """cndp_gpu_frames_alloc memory (include/cndp_gpu.h) exposed to torch
+    through __cuda_array_interface__; torch holds this object until the
+    tensor's storage dies, and its finalizer frees the memory."""
+
+    def __init__(self, nbytes: int, index: int, cached: bool):
+        import ctypes
+        from . import native as N
+        self._L = N.lib()
+        p = ctypes.c_void_p()
+        N.check(self._L.cndp_gpu_frames_alloc(index, nbytes, N.CNDP_FRAMES_CACHED if cached else 0,
+                                              ctypes.byref(p)), "cndp_gpu_frames_alloc")
+        self.ptr = p.value
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 2, "strides": None}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._L.cndp_gpu_frames_free(self.ptr)
+            self.ptr = None
+
+
+def frame_slab(nbytes: int, device="cpu", cached: bool = False) -> torch.Tensor:
+    """A zeroed uint8 frame slab: on a GPU, device frame memory from
+    cndp_gpu_frames_alloc (uncached unless `cached`: the receive-ring memory
+    the classify kernels read windows from); on the CPU a
+    plain tensor."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = torch.as_tensor(_FrameMemory(nbytes, idx, cached), device=device)
+    t.zero_()
+    return t
+
+
+def _slab(nbytes: int, device, frame_mem: str | None) -> torch.Tensor:
+    # frame_mem: None = a torch tensor, "uncached" / "cached" = cndp_gpu_frames_alloc memory
+    if frame_mem is None or torch.device(device).type != "cuda":
+        return torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    return frame_slab(nbytes, device, cached=frame_mem == "cached")
+
+
 def packed_ipv4(n: int, slot: int = 64, frame_len: int = 60, seed: int = SEED, routes=None,
-                device="cpu", in_route_frac: float = 0.9, chunk: int = 1 << 22) -> Frames:
+                device="cpu", in_route_frac: float = 0.9, chunk: int = 1 << 22,
+                frame_mem: str | None = None) -> Frames:
     """C2/C3 (slot 64) and C5 (slot 1536, frame 1500) fixed-stride slabs."""
-    slab = torch.zeros(n * slot, dtype=torch.uint8, device=device)
+    slab = _slab(n * slot, device, frame_mem)
     view = slab.view(n, slot)
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
@@ -239,7 +283,7 @@ IMIX_WEIGHTS = (7, 4, 1)
 
 
 def imix(n: int, seed: int = SEED, v4routes=None, v6routes=None, device="cpu",
-         v6_frac: float = 0.5) -> Frames:
+         v6_frac: float = 0.5, frame_mem: str | None = None) -> Frames:
     """C4: IMIX 64/570/1500 at 7:4:1, IPv4/IPv6 mix, packed at roundup(len, 64)."""
     idx = torch.arange(n, dtype=torch.int64, device=device)
     pick = rnd(seed, idx, 40) % 12
@@ -248,7 +292,7 @@ def imix(n: int, seed: int = SEED, v4routes=None, v6routes=None, device="cpu",
     slot = (size + 63) // 64 * 64
     offsets = torch.cumsum(slot, 0) - slot
     total = int(offsets[-1] + slot[-1]) if n else 0
-    slab = torch.zeros(max(total, 64), dtype=torch.uint8, device=device)
+    slab = _slab(max(total, 64), device, frame_mem)
     rows = slab.view(-1, 64)
     frame_len = size - 4
     is6 = (rnd(seed, idx, 41) % 1000) < int(round(v6_frac * 1000))

@@ -334,6 +334,16 @@ int cndp_gpu_mac_swap(cndp_gpu_ctx_t *ctx, const struct cndp_batch *b, void *str
 int cndp_gpu_host_register(cndp_gpu_ctx_t *ctx, void *ptr, uint64_t len, void **dev_ptr);
 int cndp_gpu_host_unregister(cndp_gpu_ctx_t *ctx, void *ptr);
 
+/* Device frame memory for device-resident batches (the receive ring a NIC's
+ * peer DMA or a host copy fills; cndp_batch.slab points into it): HBM of
+ * device `device` (-1 = current), uncached on the GPU by default, so a peer's
+ * writes need no GPU cache maintenance and the classify kernels' 64-B window
+ * reads allocate no L2 lines (faster for IMIX / jumbo strides).
+ * CNDP_FRAMES_CACHED: plain device memory.  -EINVAL, -ENODEV, -EIO. */
+#define CNDP_FRAMES_CACHED 1u
+int cndp_gpu_frames_alloc(int device, uint64_t bytes, uint32_t flags, void **dptr);
+int cndp_gpu_frames_free(void *dptr);
+
 /* Stable partition of packet indices by bin (the per-edge streams a graph
  * walk would build): bin_of[i] in [0, n_bins+2) (device), outputs
  * bin_start[n_bins+3] (exclusive prefix, device) and order[n] (device).

@@ -372,3 +372,18 @@ def test_l3fwd_routes_image_matches_oracle():
     ips = rng.integers(0, 2**32, size=1 << 16, dtype=np.uint64).astype(np.uint32)
     ips[::2] = (10 << 24) | (ips[::2] & 0x0004FFFF)
     assert np.array_equal(_host_lookup4(f, ips), O.dir24_8_lookup(t24, t8, ips))
+
+
+def test_frames_alloc_argument_checks():
+    """cndp_gpu_frames_alloc rejects a zero size, unknown flags and a NULL
+    out pointer before it touches a device (CPU-safe)."""
+    L = N.lib()
+    p = ctypes.c_void_p(1)
+    assert L.cndp_gpu_frames_alloc(-1, 0, 0, ctypes.byref(p)) == -22 and p.value is None
+    assert L.cndp_gpu_frames_alloc(-1, 4096, 0x10, ctypes.byref(p)) == -22
+    assert L.cndp_gpu_frames_alloc(-1, 4096, 0, None) == -22
+    assert L.cndp_gpu_frames_free(None) == 0
+    import torch
+    from cndp_amd import pktgen
+    t = pktgen.frame_slab(1000, "cpu")
+    assert t.dtype == torch.uint8 and t.numel() == 1000 and int(t.sum()) == 0

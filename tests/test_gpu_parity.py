@@ -128,6 +128,30 @@ def test_cnet_imix_c4_parity(cnet, gpu):
     assert (ref["edge"] == 1).mean() > 0.5
 
 
+@pytest.mark.parametrize("cached", [False, True])
+def test_frame_memory_parity(cnet, l3, gpu, cached):
+    """Frames in cndp_gpu_frames_alloc memory (uncached by default: what a
+    NIC's peer DMA fills): C4 IMIX and C5-shaped 1536-B frames through the
+    cnet kernels and C3 frames through l3fwd, bit for bit against the oracle,
+    the same as from a torch (hipMalloc) slab."""
+    cl, routes, v6, t4, t6 = cnet
+    for mk in (lambda **k: pktgen.imix(1 << 17, v4routes=routes, v6routes=v6, **k),
+               lambda **k: pktgen.packed_ipv4(1 << 16, slot=1536, frame_len=1500, routes=routes, **k)):
+        fr = mk(device=gpu)
+        fm = pktgen.Frames(pktgen.frame_slab(fr.slab.numel(), gpu, cached=cached), fr.n, stride=fr.stride,
+                           offsets=fr.offsets, data_off=fr.data_off, lengths=fr.lengths)
+        fm.slab.copy_(fr.slab)
+        ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+        for ct in CNET_KERNELS:
+            cl.set_tuning(cnet_tile=ct)
+            assert_same(run_gpu(cl, fm, N.CNDP_MODE_CNET), ref)
+    cl3, t43 = l3[0], l3[2]
+    fr = pktgen.packed_ipv4(1 << 18, routes=pktgen.l3fwd_routes(), device=gpu)
+    fm = pktgen.Frames(pktgen.frame_slab(fr.slab.numel(), gpu, cached=cached), fr.n, stride=64)
+    fm.slab.copy_(fr.slab)
+    assert_same(run_gpu(cl3, fm, N.CNDP_MODE_L3FWD), oracle_classify(O.MODE_L3FWD, fr, tables4=t43))
+
+
 def test_cnet_deep_v6_chains(gpu):
     """cnet trie chains through every tbl8 level: the lpm6_1000 rule set
     (/1../128, fib6_test.c / lpm6_data_test.h) behind ip6_input's edge values,

@@ -785,6 +785,9 @@ def test_rx_node_graph_walk(gpu, zero_copy):
         for sel, lo in ((np.arange(n) % 97 == 5, 0xFE), (np.arange(n) % 89 == 7, 0xFF)):
             p.mem[d[sel] + 24] = lo
             p.mem[d[sel] + 25] = 0xFF
+    # the header checksums before the rewrite (the rule-dependent ones)
+    d = op.data_pos().astype(np.int64)
+    ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
     NodeFib.fini()
     L.cndp_node_ip4_rewrite_reset()
     L.cndp_node_gpu_umem_reset()
@@ -851,8 +854,6 @@ def test_rx_node_graph_walk(gpu, zero_copy):
         rw = ib[e[ib] == 0]
         want[rw] = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
     assert np.array_equal(got, want)
-    d = op.data_pos().astype(np.int64)
-    ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
     ok = np.ones(n, bool) if fused else (ck != 0xFFFE) & (ck != 0xFFFF)
     diff = np.any(gp.mem.reshape(n, -1)[:, 64:] != op.mem.reshape(n, -1)[:, 64:], axis=1)
     assert not np.any(diff & ok)
