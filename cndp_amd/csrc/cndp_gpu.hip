@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <errno.h>
 #include <pthread.h>
@@ -25,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <vector>
 
 #include "fib_internal.h"
 #include "node_internal.h"
@@ -4188,6 +4190,10 @@ extern "C" void cndp_tbl_dev_free(struct cndp_tbl *t)
             hipFree(sl.ticket);
         memset(&sl, 0, sizeof(sl));
     }
+    if (t->paint_host)
+        hipHostFree(t->paint_host);
+    t->paint_host = nullptr;
+    t->paint_cap = 0;
     if (t->dev_id < 0)
         return;
     int cur = 0;
@@ -4360,6 +4366,166 @@ static int dir16_sync(struct cndp_tbl *t, hipStream_t s, uint64_t d24_lo, uint64
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Device painter of the FIB mirror (SURVEY §8(f) row 4, dir24_8.c:249-453):
+// the entry ranges a route change touched since the last sync, merged, are
+// cut into maximal runs of one value -- filled on the device from a 24-B
+// command -- and the short runs between them, copied from a payload.  The
+// commands and payload sit in pinned mapped host memory the kernel reads, one
+// block per command; the ranges are disjoint, so the blocks need no order.
+// ---------------------------------------------------------------------------
+struct TblCmd {
+    uint64_t first;  // entry index in tbl24 / tbl8
+    uint32_t count;  // entries
+    uint32_t op;     // bit 0: tbl8 (else tbl24); bit 1: copy (arg = payload byte offset), else fill (arg = value)
+    uint64_t arg;
+};
+#define PAINT_RUN_MIN 8u      // a run this long is filled, shorter ones are copied
+#define PAINT_FILL_MAX 65536u // entries per fill command (large ranges spread over blocks)
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_tbl_paint(const TblCmd *cmds, uint32_t n, const uint8_t *payload, T *t24,
+                                                   T *t8)
+{
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+        const TblCmd k = cmds[c];
+        T *const dst = ((k.op & 1u) ? t8 : t24) + k.first;
+        if (k.op & 2u) {
+            const T *const src = (const T *)(payload + k.arg);
+            for (uint32_t i = threadIdx.x; i < k.count; i += blockDim.x)
+                dst[i] = src[i];
+        } else {
+            const T v = (T)k.arg;
+            for (uint32_t i = threadIdx.x; i < k.count; i += blockDim.x)
+                dst[i] = v;
+        }
+    }
+}
+
+static inline uint64_t host_ent(const uint8_t *base, uint32_t nh_sz, uint64_t i)
+{
+    switch (nh_sz) {
+    case 0:
+        return base[i];
+    case 1:
+        return ((const uint16_t *)(const void *)base)[i];
+    case 2:
+        return ((const uint32_t *)(const void *)base)[i];
+    default:
+        return ((const uint64_t *)(const void *)base)[i];
+    }
+}
+
+// merge a table's logged ranges (sorted, touching ones joined) in place;
+// returns how many remain
+static uint32_t paint_merge(struct cndp_range *r, uint32_t n)
+{
+    std::sort(r, r + n, [](const cndp_range &a, const cndp_range &b) { return a.lo < b.lo; });
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        if (m && r[k].lo <= r[m - 1].hi) {
+            if (r[k].hi > r[m - 1].hi)
+                r[m - 1].hi = r[k].hi;
+        } else {
+            r[m++] = r[k];
+        }
+    }
+    return m;
+}
+
+// the commands of one table's merged ranges, appended to cmds / payload
+static void paint_plan(const struct cndp_tbl *t, uint32_t which, const uint8_t *img, const struct cndp_range *r,
+                       uint32_t n, std::vector<TblCmd> &cmds, std::vector<uint8_t> &payload)
+{
+    const uint32_t esz = 1u << t->nh_sz;
+    auto copy = [&](uint64_t lo, uint64_t hi) {
+        if (hi <= lo)
+            return;
+        const uint64_t off = (payload.size() + 7u) & ~7ull;
+        payload.resize(off + (hi - lo) * esz);
+        memcpy(payload.data() + off, img + lo * esz, (hi - lo) * esz);
+        cmds.push_back(TblCmd{lo, (uint32_t)(hi - lo), which | 2u, off});
+    };
+    for (uint32_t k = 0; k < n; k++) {
+        uint64_t i = r[k].lo, cs = i; // cs: start of the pending copy segment
+        while (i < r[k].hi) {
+            const uint64_t v = host_ent(img, t->nh_sz, i);
+            uint64_t j = i + 1;
+            while (j < r[k].hi && host_ent(img, t->nh_sz, j) == v)
+                j++;
+            if (j - i >= PAINT_RUN_MIN) {
+                copy(cs, i);
+                for (uint64_t f = i; f < j; f += PAINT_FILL_MAX) {
+                    const uint64_t c = j - f < PAINT_FILL_MAX ? j - f : PAINT_FILL_MAX;
+                    cmds.push_back(TblCmd{f, (uint32_t)c, which, v});
+                }
+                cs = j;
+            }
+            i = j;
+        }
+        copy(cs, r[k].hi);
+    }
+}
+
+// paint the logged changes of the tables whose mirror is not new (paint24 /
+// paint8) on the device; returns 1 when it did, 0 when the bounding-range
+// copy is cheaper, < 0 on error.  Caller holds dev_lock.
+static int tbl_dev_paint(struct cndp_tbl *t, hipStream_t s, bool paint24, bool paint8)
+{
+    std::vector<TblCmd> cmds;
+    std::vector<uint8_t> payload;
+    const uint32_t esz = 1u << t->nh_sz;
+    if (paint24)
+        paint_plan(t, 0, t->tbl24, t->log24, paint_merge(t->log24, t->n_log24), cmds, payload);
+    if (paint8)
+        paint_plan(t, 1, t->tbl8, t->log8, paint_merge(t->log8, t->n_log8), cmds, payload);
+    const uint64_t cmd_bytes = cmds.size() * sizeof(TblCmd), bytes = cmd_bytes + payload.size();
+    const uint64_t span = ((paint24 && t->d24_hi > t->d24_lo) ? (t->d24_hi - t->d24_lo) * esz : 0) +
+                          ((paint8 && t->d8_hi > t->d8_lo) ? (t->d8_hi - t->d8_lo) * esz : 0);
+    if (cmds.empty() || bytes >= span)
+        return 0;
+    if (bytes > t->paint_cap) {
+        if (t->paint_host)
+            HIP_TRY(hipHostFree(t->paint_host));
+        t->paint_host = nullptr;
+        t->paint_cap = 0;
+        const uint64_t cap = bytes > (1u << 16) ? bytes + bytes / 2 : (1u << 16);
+        HIP_TRY(hipHostMalloc(&t->paint_host, cap, hipHostMallocMapped));
+        t->paint_cap = cap;
+    }
+    uint8_t *h = (uint8_t *)t->paint_host;
+    memcpy(h, cmds.data(), cmd_bytes);
+    if (!payload.empty())
+        memcpy(h + cmd_bytes, payload.data(), payload.size());
+    void *hd = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&hd, t->paint_host, 0));
+    const TblCmd *dc = (const TblCmd *)hd;
+    const uint8_t *dp = (const uint8_t *)hd + cmd_bytes;
+    const uint32_t n = (uint32_t)cmds.size(), g = n < 1024u ? n : 1024u;
+    switch (t->nh_sz) {
+    case 0:
+        hipLaunchKernelGGL(k_tbl_paint<uint8_t>, dim3(g), dim3(256), 0, s, dc, n, dp, (uint8_t *)t->dev_tbl24,
+                           (uint8_t *)t->dev_tbl8);
+        break;
+    case 1:
+        hipLaunchKernelGGL(k_tbl_paint<uint16_t>, dim3(g), dim3(256), 0, s, dc, n, dp, (uint16_t *)t->dev_tbl24,
+                           (uint16_t *)t->dev_tbl8);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_tbl_paint<uint32_t>, dim3(g), dim3(256), 0, s, dc, n, dp, (uint32_t *)t->dev_tbl24,
+                           (uint32_t *)t->dev_tbl8);
+        break;
+    default:
+        hipLaunchKernelGGL(k_tbl_paint<uint64_t>, dim3(g), dim3(256), 0, s, dc, n, dp, (uint64_t *)t->dev_tbl24,
+                           (uint64_t *)t->dev_tbl8);
+        break;
+    }
+    HIP_TRY(hipGetLastError());
+    t->sync_bytes += bytes;
+    t->sync_cmds += n;
+    return 1;
+}
+
 // caller holds t->dev_lock
 static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
 {
@@ -4373,6 +4539,8 @@ static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
     if (t->dev_id >= 0 && t->dev_id != dev)
         return -EXDEV; // a FIB mirror lives on one device
     hipStream_t s = (hipStream_t)stream;
+    // a mirror (or tbl8 pool) allocated by this sync is copied whole
+    bool paint24 = t->dev_id >= 0, paint8 = t->dev_id >= 0 && t->dev_groups == groups;
     if (t->dev_id < 0) {
         HIP_TRY(hipMalloc(&t->dev_tbl24, (size_t)CNDP_TBL24_ENT * esz));
         HIP_TRY(hipMalloc(&t->dev_tbl8, (size_t)groups * CNDP_TBL8_GRP * esz));
@@ -4395,13 +4563,23 @@ static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
         t->d8_lo = 0;
         t->d8_hi = (uint64_t)groups * CNDP_TBL8_GRP;
     }
-    if (t->d24_hi > t->d24_lo) {
+    paint24 = paint24 && t->n_log24 <= CNDP_TBL_LOG && t->d24_hi > t->d24_lo;
+    paint8 = paint8 && t->n_log8 <= CNDP_TBL_LOG && t->d8_hi > t->d8_lo;
+    int painted = 0;
+    if (paint24 || paint8) {
+        painted = tbl_dev_paint(t, s, paint24, paint8);
+        if (painted < 0)
+            return painted;
+    }
+    if (t->d24_hi > t->d24_lo && !(painted && paint24)) {
         HIP_TRY(hipMemcpyAsync((uint8_t *)t->dev_tbl24 + t->d24_lo * esz, t->tbl24 + t->d24_lo * esz,
                                (t->d24_hi - t->d24_lo) * esz, hipMemcpyHostToDevice, s));
+        t->sync_bytes += (t->d24_hi - t->d24_lo) * esz;
     }
-    if (t->d8_hi > t->d8_lo) {
+    if (t->d8_hi > t->d8_lo && !(painted && paint8)) {
         HIP_TRY(hipMemcpyAsync((uint8_t *)t->dev_tbl8 + t->d8_lo * esz, t->tbl8 + t->d8_lo * esz,
                                (t->d8_hi - t->d8_lo) * esz, hipMemcpyHostToDevice, s));
+        t->sync_bytes += (t->d8_hi - t->d8_lo) * esz;
     }
     // (the /16 directory exists for 4-B DIR-24-8 tables only: a trie table
     // without one is not dirty -- that test made every cnet call wait here)
@@ -4412,11 +4590,13 @@ static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
         if (r)
             return r;
     }
-    // the host image may change right after we return: finish the copies
+    // the host image (and the painter's staging) may change right after we
+    // return: finish the copies and the paint
     if (dirty)
         HIP_TRY(hipStreamSynchronize(s));
     t->d24_lo = t->d8_lo = ~0ULL;
     t->d24_hi = t->d8_hi = 0;
+    t->n_log24 = t->n_log8 = 0;
     return 0;
 }
 

@@ -59,12 +59,35 @@ static inline void ent_set(struct cndp_tbl *t, uint8_t *base, uint64_t i, uint64
     }
 }
 
+/* a changed range for the device painter: merged into the last one when they
+ * touch (the painters walk a route's range in order), else appended; past
+ * CNDP_TBL_LOG the count only marks the overflow */
+static inline void log_range(struct cndp_range *log, uint32_t *n, uint64_t lo, uint64_t hi)
+{
+    if (*n > CNDP_TBL_LOG)
+        return;
+    if (*n) {
+        struct cndp_range *l = &log[*n - 1];
+        if (lo <= l->hi && hi >= l->lo) {
+            l->lo = lo < l->lo ? lo : l->lo;
+            l->hi = hi > l->hi ? hi : l->hi;
+            return;
+        }
+    }
+    if (*n < CNDP_TBL_LOG) {
+        log[*n].lo = lo;
+        log[*n].hi = hi;
+    }
+    (*n)++;
+}
+
 static inline void dirty24(struct cndp_tbl *t, uint64_t lo, uint64_t hi)
 {
     if (lo < t->d24_lo)
         t->d24_lo = lo;
     if (hi > t->d24_hi)
         t->d24_hi = hi;
+    log_range(t->log24, &t->n_log24, lo, hi);
 }
 
 static inline void dirty8(struct cndp_tbl *t, uint64_t lo, uint64_t hi)
@@ -73,6 +96,7 @@ static inline void dirty8(struct cndp_tbl *t, uint64_t lo, uint64_t hi)
         t->d8_lo = lo;
     if (hi > t->d8_hi)
         t->d8_hi = hi;
+    log_range(t->log8, &t->n_log8, lo, hi);
 }
 
 static inline uint64_t t24_get(const struct cndp_tbl *t, uint64_t i) { return ent_get(t, t->tbl24, i); }
@@ -795,6 +819,27 @@ int cndp_fib_lookup_dev(struct cne_fib *fib, const uint32_t *ips, uint64_t *next
     if (!fib || (n && (!ips || !next_hops)))
         return -EINVAL;
     return cndp_tbl_lookup4_dev(&fib->t, ips, next_hops, n, stream);
+}
+
+static int tbl_sync_stats(struct cndp_tbl *t, uint64_t *bytes, uint64_t *cmds)
+{
+    pthread_mutex_lock(&t->dev_lock);
+    if (bytes)
+        *bytes = t->sync_bytes;
+    if (cmds)
+        *cmds = t->sync_cmds;
+    pthread_mutex_unlock(&t->dev_lock);
+    return 0;
+}
+
+int cndp_fib_sync_stats(struct cne_fib *fib, uint64_t *bytes, uint64_t *cmds)
+{
+    return fib ? tbl_sync_stats(&fib->t, bytes, cmds) : -EINVAL;
+}
+
+int cndp_fib6_sync_stats(struct cne_fib6 *fib, uint64_t *bytes, uint64_t *cmds)
+{
+    return fib ? tbl_sync_stats(&fib->t, bytes, cmds) : -EINVAL;
 }
 
 int cndp_fib_stats(struct cne_fib *fib, uint32_t *routes, uint32_t *tbl8_used, uint32_t *rsvd)

@@ -26,6 +26,11 @@ extern "C" {
 #define CNDP_TBL24_ENT (1u << 24)
 #define CNDP_TBL8_GRP 256u
 #define CNDP_LK_SLOTS 16u   /* concurrent host-array lookups per table */
+#define CNDP_TBL_LOG 64u    /* changed entry ranges kept per table between syncs */
+
+struct cndp_range {
+    uint64_t lo, hi;
+};
 
 struct cndp_tbl {
     uint32_t nh_sz;     /* log2(entry bytes) */
@@ -38,6 +43,16 @@ struct cndp_tbl {
     uint32_t cur_tbl8s;
     /* dirty entry ranges [lo, hi) pending upload */
     uint64_t d24_lo, d24_hi, d8_lo, d8_hi;
+    /* the same changes as a list of ranges (the device painter of
+     * cndp_tbl_dev_sync: fills / copies of just these entries); more than
+     * CNDP_TBL_LOG ranges since the last sync falls back to copying the
+     * bounding ranges above */
+    struct cndp_range log24[CNDP_TBL_LOG], log8[CNDP_TBL_LOG];
+    uint32_t n_log24, n_log8;  /* > CNDP_TBL_LOG: overflowed */
+    uint64_t sync_bytes;       /* host -> device bytes of all syncs (stat) */
+    uint64_t sync_cmds;        /* device painter commands of all syncs (stat) */
+    void *paint_host;          /* pinned + mapped painter staging: commands, then payload */
+    uint64_t paint_cap;
     /* device mirror */
     int dev_id;
     void *dev_tbl24;

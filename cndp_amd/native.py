@@ -142,6 +142,8 @@ def lib():
         "cndp_fib6_lookup_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
         "cndp_fib_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
         "cndp_fib6_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+        "cndp_fib_sync_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+        "cndp_fib6_sync_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
         # cndp_node.h
         "cne_node_ip4_route_add": (c_int, [c_uint32, c_uint8, c_uint16, c_int]),
         "cne_node_ip4_rewrite_add": (c_int, [c_uint16, c_void_p, c_uint8, c_uint16]),

@@ -39,7 +39,8 @@
  * prototypes that follow are then checked by the compiler against the
  * reference declarations (tests/test_abi.py::test_prototypes_match_reference).
  * Extensions (device-resident batches, no reference counterpart):
- *   cndp_fib_lookup_dev / cndp_fib6_lookup_dev, cndp_fib_sync / cndp_fib6_sync.
+ *   cndp_fib_lookup_dev / cndp_fib6_lookup_dev, cndp_fib_sync / cndp_fib6_sync,
+ *   cndp_fib_sync_stats / cndp_fib6_sync_stats.
  */
 #ifndef CNDP_FIB_H
 #define CNDP_FIB_H
@@ -180,6 +181,14 @@ int cndp_fib6_lookup_dev(struct cne_fib6 *fib, const uint8_t *ips16, uint64_t *n
 /* counters: tbl8 groups in use / reserved (cne_fib internal state) */
 int cndp_fib_stats(struct cne_fib *fib, uint32_t *routes, uint32_t *tbl8_used, uint32_t *rsvd);
 int cndp_fib6_stats(struct cne_fib6 *fib, uint32_t *routes, uint32_t *tbl8_used, uint32_t *rsvd);
+
+/* device mirror traffic: host -> device bytes and device painter commands of
+ * every sync so far.  A sync paints only the entry ranges changed since the
+ * previous one on the device (fills of uniform runs, copies of the rest, the
+ * way dir24_8.c:249-453 writes them), or copies the bounding ranges of the
+ * changes when there were more than 64 separate ranges or the mirror is new. */
+int cndp_fib_sync_stats(struct cne_fib *fib, uint64_t *bytes, uint64_t *cmds);
+int cndp_fib6_sync_stats(struct cne_fib6 *fib, uint64_t *bytes, uint64_t *cmds);
 
 #ifdef __cplusplus
 }

@@ -347,3 +347,64 @@ def test_fib_lookup_threads(gpu, sel):
     for t in th:
         t.join()
     assert not errors, errors[:5]
+
+
+def _sync_stats(f):
+    b, c = ctypes.c_uint64(), ctypes.c_uint64()
+    assert N.lib().cndp_fib_sync_stats(f.h, ctypes.byref(b), ctypes.byref(c)) == 0
+    return b.value, c.value
+
+
+@pytest.mark.parametrize("nh_sz", [N.CNE_FIB_DIR24_8_1B, N.CNE_FIB_DIR24_8_2B, N.CNE_FIB_DIR24_8_4B,
+                                   N.CNE_FIB_DIR24_8_8B])
+def test_fib_device_paint(gpu, nh_sz):
+    """Route changes between GPU lookups are painted on the device (SURVEY §8(f)
+    row 4): a /8 and /24s at both ends of the address space plus a /28 and a
+    /32 inside one tbl8 group cost fill / copy commands over their own ranges
+    (cndp_fib_sync_stats), not the 14.6 M-entry span between them; deletes the
+    same; more than 64 separate ranges take the bounding copy.  After every
+    step all answers of the GPU selection equal brute-force LPM."""
+    from cndp_amd.fib import Fib
+    esz = 1 << nh_sz
+    f = Fib(f"paint{nh_sz}", N.CNE_FIB_DIR24_8, default_nh=3, max_routes=1024, nh_sz=nh_sz, num_tbl8=64,
+            lookup=N.CNE_FIB_LOOKUP_GPU)
+    routes = {}
+    rng = np.random.default_rng(11 + nh_sz)
+    keys = rng.integers(0, 2**32, size=1 << 15, dtype=np.uint64).astype(np.uint32)
+
+    def add(ip, d, nh):
+        assert f.add(ip, d, nh) == 0
+        routes[(ip, d)] = nh
+
+    def check(extra=()):
+        k = np.concatenate([keys, np.array([ip | off for (ip, d) in routes for off in (0, 1, 15, 255)]
+                                           + list(extra), np.uint64).astype(np.uint32)])
+        want = O.lpm4_bruteforce([(ip, d, nh) for (ip, d), nh in routes.items()], 3, k)
+        assert np.array_equal(f.lookup_bulk(k), want)
+
+    add(0x0A000000, 16, 4)
+    check()                                  # the first lookup copies the new mirror whole
+    b0, c0 = _sync_stats(f)
+    assert b0 >= (1 << 24) * esz and c0 == 0
+    add(0x01000000, 8, 5)
+    add(0xDFFFFF00, 24, 6)
+    add(0x00000100, 24, 7)
+    add(0x0A010210, 28, 8)
+    add(0x0A010221, 32, 9)
+    check()
+    b1, c1 = _sync_stats(f)
+    assert 0 < c1 - c0 < 64 and b1 - b0 < 64 * 1024, (b1 - b0, c1 - c0)
+    for key in ((0x01000000, 8), (0x0A010221, 32)):
+        assert f.delete(*key) == 0
+        del routes[key]
+    check([0x01020304, 0x0A010221])
+    b2, c2 = _sync_stats(f)
+    assert 0 < c2 - c1 < 64 and b2 - b1 < 64 * 1024, (b2 - b1, c2 - c1)
+    # 200 scattered /24s: more ranges than the log keeps, the bounding copy
+    for _ in range(200):
+        ip, nh = int(rng.integers(0, 1 << 24)) << 8, int(rng.integers(0, 100))
+        if (ip, 24) not in routes:
+            add(ip, 24, nh)
+    check()
+    b3, c3 = _sync_stats(f)
+    assert c3 == c2 and b3 - b2 > 1 << 20

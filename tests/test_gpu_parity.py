@@ -502,9 +502,12 @@ def test_dir16_on_off_identical(l3, cnet, gpu):
     ccl.set_tuning(dir16=1)
 
 
-def test_route_churn_between_batches(gpu):
+@pytest.mark.parametrize("per_round", [150, 8])
+def test_route_churn_between_batches(gpu, per_round):
     """Routes added / deleted between classify calls: the mirror (tbl24, tbl8,
-    /16 directory and its pages) follows incrementally, results == oracle."""
+    /16 directory and its pages) follows incrementally, results == oracle --
+    8 changes a round are painted on the device (the range log), 150 take the
+    bounding-range copy."""
     from cndp_amd.classify import Classifier
     from cndp_amd.fib import Fib
     rng = np.random.default_rng(77)
@@ -515,7 +518,7 @@ def test_route_churn_between_batches(gpu):
     live = {}
     fr = pktgen.packed_ipv4(1 << 17, routes=pktgen.l3fwd_routes(), device=gpu, seed=8, in_route_frac=0.5)
     for rnd_ in range(6):
-        for _ in range(150):
+        for _ in range(per_round if rnd_ else 150):
             if live and rng.random() < 0.4:
                 key = list(live)[int(rng.integers(0, len(live)))]
                 assert fib.delete(*key) == 0
