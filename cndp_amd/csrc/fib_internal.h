@@ -26,7 +26,7 @@ extern "C" {
 #define CNDP_TBL24_ENT (1u << 24)
 #define CNDP_TBL8_GRP 256u
 #define CNDP_LK_SLOTS 16u   /* concurrent host-array lookups per table */
-#define CNDP_TBL_LOG 64u    /* changed entry ranges kept per table between syncs */
+#define CNDP_TBL_LOG 1024u  /* changed entry ranges kept per table between syncs */
 
 struct cndp_range {
     uint64_t lo, hi;

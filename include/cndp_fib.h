@@ -186,7 +186,7 @@ int cndp_fib6_stats(struct cne_fib6 *fib, uint32_t *routes, uint32_t *tbl8_used,
  * every sync so far.  A sync paints only the entry ranges changed since the
  * previous one on the device (fills of uniform runs, copies of the rest, the
  * way dir24_8.c:249-453 writes them), or copies the bounding ranges of the
- * changes when there were more than 64 separate ranges or the mirror is new. */
+ * changes when there were more than 1024 separate ranges or the mirror is new. */
 int cndp_fib_sync_stats(struct cne_fib *fib, uint64_t *bytes, uint64_t *cmds);
 int cndp_fib6_sync_stats(struct cne_fib6 *fib, uint64_t *bytes, uint64_t *cmds);
 

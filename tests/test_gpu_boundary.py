@@ -362,11 +362,11 @@ def test_fib_device_paint(gpu, nh_sz):
     row 4): a /8 and /24s at both ends of the address space plus a /28 and a
     /32 inside one tbl8 group cost fill / copy commands over their own ranges
     (cndp_fib_sync_stats), not the 14.6 M-entry span between them; deletes the
-    same; more than 64 separate ranges take the bounding copy.  After every
+    same; more than 1024 separate ranges take the bounding copy.  After every
     step all answers of the GPU selection equal brute-force LPM."""
     from cndp_amd.fib import Fib
     esz = 1 << nh_sz
-    f = Fib(f"paint{nh_sz}", N.CNE_FIB_DIR24_8, default_nh=3, max_routes=1024, nh_sz=nh_sz, num_tbl8=64,
+    f = Fib(f"paint{nh_sz}", N.CNE_FIB_DIR24_8, default_nh=3, max_routes=4096, nh_sz=nh_sz, num_tbl8=64,
             lookup=N.CNE_FIB_LOOKUP_GPU)
     routes = {}
     rng = np.random.default_rng(11 + nh_sz)
@@ -400,8 +400,17 @@ def test_fib_device_paint(gpu, nh_sz):
     check([0x01020304, 0x0A010221])
     b2, c2 = _sync_stats(f)
     assert 0 < c2 - c1 < 64 and b2 - b1 < 64 * 1024, (b2 - b1, c2 - c1)
-    # 200 scattered /24s: more ranges than the log keeps, the bounding copy
-    for _ in range(200):
+    # 300 scattered /24s are painted; 1100 are more ranges than the log keeps:
+    # the bounding copy
+    for _ in range(300):
+        ip, nh = int(rng.integers(0, 1 << 24)) << 8, int(rng.integers(0, 100))
+        if (ip, 24) not in routes:
+            add(ip, 24, nh)
+    check()
+    b2b, c2b = _sync_stats(f)
+    assert c2b - c2 >= 250 and b2b - b2 < 64 * 1024
+    b2, c2 = b2b, c2b
+    for _ in range(1100):
         ip, nh = int(rng.integers(0, 1 << 24)) << 8, int(rng.integers(0, 100))
         if (ip, 24) not in routes:
             add(ip, 24, nh)
