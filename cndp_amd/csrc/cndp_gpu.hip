@@ -1970,342 +1970,6 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 }
 
 // ---------------------------------------------------------------------------
-// cnet kernel, LDS-DMA form (CNDP_TUNE_CNET_TILE 2): k_cnet_defer's two
-// stages with the frame windows staged by global_load_lds_dwordx4 straight
-// into the wave's LDS tile -- no VGPRs hold windows in flight -- and the
-// Toeplitz hash from nibble tables (4.5 KiB, conflict-free 16-entry rows), so
-// a 256-thread block needs ~22 KiB of LDS and the kernel fits six or seven
-// waves a SIMD where k_cnet_defer holds four (the window stream's rate needs
-// six).  One tile in flight per wave: trip c waits for
-// tile c (DMA'd a trip earlier), reads it, DMAs tile c+1 into the same
-// buffer, then parses c.  The tile holds frame f's 16-B part j at 4f +
-// (j ^ ((f >> 2) & 3)) (the XOR swizzle of k_cnet_defer's tile, put on the
-// DMA's per-lane source address since its LDS side is lane-linear).
-// ---------------------------------------------------------------------------
-#define DT_THREADS 256
-#define DT_WAVES (DT_THREADS / 64)
-
-__device__ __forceinline__ uint32_t tzn(const uint32_t *tn, uint32_t b, uint32_t x)
-{
-    // the 4 stream bytes b..b+3 little-endian in x; N[q][u] at tn[q * 16 + u],
-    // q = 2 * position (+1 for the low nibble)
-    uint32_t h = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t v = (x >> (8 * j)) & 0xffu, q = 2u * (b + j);
-        h ^= tn[q * 16u + (v >> 4)] ^ tn[(q + 1u) * 16u + (v & 15u)];
-    }
-    return h;
-}
-
-template <bool LNT>
-__device__ __forceinline__ void dd_issue(const KArgs &a, uint32_t tt, uint32_t n_tiles, uint64_t off, uint32_t lane,
-                                         u32x4 *tile)
-{
-    const uint32_t fr_in_k = lane >> 2, slot = lane & 3u;
-    const uint64_t my_base = tt < n_tiles ? ct_base(a, tt * 64u + lane, off) : ~0ull;
-    // frames off the fast path DMA a dummy chunk of the (aligned) Toeplitz table
-    const uint64_t my_src = ct_fast(a, my_base) ? (uint64_t)(uintptr_t)(a.slab + my_base) : (uint64_t)(uintptr_t)a.ttab;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t f = 16u * k + fr_in_k;
-        const uint64_t src = __shfl(my_src, (int)f) + ((slot ^ ((f >> 2) & 3u)) * 16u);
-        __builtin_amdgcn_global_load_lds((const void *)(uintptr_t)src, tile + 64 * k, 16, 0, LNT ? 2 : 0);
-    }
-}
-
-template <bool LNT, bool META>
-__device__ __forceinline__ void dd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles, uint32_t nt_w,
-                                        uint32_t jt, uint32_t lane, u32x4 *tile, CsOff &off, CdLane &sb,
-                                        const uint32_t *s_tn, const uint16_t *s_reta, uint32_t *s_bins,
-                                        uint32_t *s_sf, bool count, uint32_t &last_sig, uint32_t *s_mx)
-{
-    const uint32_t t = t0 + jt * wstep;
-    // B: tile c-1 -- the rest of its chain (waits for its first gather and so
-    // for tile c's DMA, issued before it a trip earlier)
-    const bool bv = jt >= 1 && jt - 1 < nt_w;
-    const uint32_t ib = (t - wstep) * 64u + lane;
-    uint32_t eb = sb.e;
-    {
-        const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
-        uint32_t rem = d6 ? 13u : (a.dir16 ? 2u : 1u);
-        const GAS uint32_t *const t6 = sgpr_pin(a.tbl8_6), *const t8 = sgpr_pin(a.tbl8);
-        const GAS uint32_t *const t4 = sgpr_pin(a.dir16 ? a.pages : a.tbl8);
-        bool more = bv & (d4 | d6) & ((eb & 1u) != 0u);
-        const GAS uint32_t *tb = d6 ? t6 : t4;
-        const GAS uint32_t *const tb2 = d6 ? t6 : t8;
-        uint32_t q0 = sb.q0, q1 = sb.q1, q2 = sb.q2, q3 = sb.q3;
-        while (__any(more)) {
-            const uint32_t idx = ((eb >> 1) << 8) | (q0 & 0xffu);
-            if (more)
-                eb = tb[idx];
-            tb = tb2;
-            q0 = alignb(q1, q0, 1);
-            q1 = alignb(q2, q1, 1);
-            q2 = alignb(q3, q2, 1);
-            q3 >>= 8;
-            rem--;
-            more = more & ((eb & 1u) != 0u) & (rem != 0u);
-        }
-    }
-    // A: tile c -- its DMA is done (the chain's waits may not have covered it)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t i = t * 64u + lane;
-    const bool live = jt < nt_w && i < a.n;
-    const uint64_t base = live ? ct_base(a, i, off.o0) : ~0ull;
-    const uint32_t sw = (lane >> 2) & 3u;
-    uint32_t W[16];
-    {
-        const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
-        const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
-        W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
-        W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
-        W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
-        W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
-    }
-    // every lane's reads of the tile are done before the DMA of tile c+1 overwrites it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    {
-        const uint32_t t2 = t + 2u * wstep, i2 = t2 * 64u + lane;
-        off.o2 = a.offsets && t2 < n_tiles && i2 < a.n ? a.offsets[i2] : 0;
-        dd_issue<LNT>(a, t + wstep, n_tiles, off.o1, lane, tile);
-    }
-    const uint32_t et = W[3] & 0xffffu;
-    const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-    const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
-    const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
-                    (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
-    const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
-    const bool fast = live & ct_fast(a, base) & (f4 | f6);
-    {
-        const bool slow = live && !fast;
-        const unsigned long long m = __ballot(slow);
-        if (m) {
-            const KAS KArgs &o = kargs_fresh(a);
-            uint32_t w0 = 0;
-            if (lane == (uint32_t)(__ffsll(m) - 1))
-                w0 = atomicAdd(o.wl_n, (uint32_t)__popcll(m));
-            w0 = __shfl(w0, __ffsll(m) - 1);
-            if (slow)
-                __hip_atomic_store(&o.wl[w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))], (uint32_t)i,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    CdLane na;
-    na.ptf = 0;
-    na.h = 0;
-    na.rx = 0;
-    na.q0 = na.q1 = na.q2 = na.q3 = 0;
-    uint32_t idx0 = 0;
-    const uint32_t *tb0 = a.tbl24_6;
-    if (fast) {
-        const uint32_t proto = f4 ? p4 : p6;
-        uint32_t pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
-        const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
-        const bool udp = proto == 17u, gtpu = udp & (dport == BE16C(2152u)), gtpc = udp & (dport == BE16C(2123u));
-        pt |= gtpu ? 0x8000u : gtpc ? 0x7000u : 0u;
-        const uint32_t pe = (proto == 6u) | (udp & !gtpc) ? (gtpu ? 5u : f4 ? 3u : 4u) : 0u;
-        const bool l4ok = proto == 6u || proto == 17u;
-        Lens lens{14u, f4 ? 20u : 40u, 0u};
-        if (META && a.rxmeta) {
-            lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
-                    : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
-                         : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
-            na.rx = rx_meta(lens, W[0], W[1], et);
-        }
-        if (META && a.iplen)
-            na.ipl = (1u << 16) | bswap16(f4 ? (W[4] & 0xffffu) : (W[4] >> 16));
-        if (META && a.win) {
-            u32x4 *dw = a.win + 4ull * i;
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                dw[k] = (u32x4){W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
-        }
-        uint32_t flags = 0;
-        {
-            uint32_t V[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++)
-                V[k] = alignb(W[6 + k], W[5 + k], 2);
-            const bool any6 = __any(f6);
-#pragma unroll
-            for (int k = 0; k < 9; k++) {
-                if (k >= 3 && !any6)
-                    break;
-                uint32_t u = k < 2 ? (f4 ? V[k + 1] : V[k]) : k == 2 ? (f4 ? (l4ok ? V[3] : 0u) : V[2])
-                           : k < 8 ? (f4 ? 0u : V[k]) : (f4 || !l4ok ? 0u : V[8]);
-                na.h ^= tzn(s_tn, 4 * k, u);
-            }
-        }
-        const bool do4 = f4 & ((pe == 3u) | (a.spec_nh != nullptr));
-        const bool do6 = !f4 & ((pe == 4u) | (a.spec_nh != nullptr));
-        const uint32_t dst = alignb(W[8], W[7], 2);
-        uint32_t sum = (W[3] >> 16) + (W[8] & 0xffffu);
-#pragma unroll
-        for (int k = 4; k < 8; k++)
-            sum = hsum2(W[k], sum);
-        sum = (sum >> 16) + (sum & 0xffffu);
-        sum = (sum >> 16) + (sum & 0xffffu);
-        const bool ok4 = (bswap16(W[4] & 0xffffu) < a.buf_len) & (((~sum) & 0xffffu) == 0u);
-        const uint32_t d4 = ok4 ? bswap32(dst) : 0u;
-        const bool ok6 = bswap16(W[4] >> 16) < a.buf_len;
-        const uint32_t d0 = ok6 ? alignb(W[10], W[9], 2) : 0u, d1 = ok6 ? alignb(W[11], W[10], 2) : 0u;
-        const uint32_t d2 = ok6 ? alignb(W[12], W[11], 2) : 0u, d3 = ok6 ? alignb(W[13], W[12], 2) : 0u;
-        const uint32_t q04 = ok4 ? dst >> (a.dir16 ? 16 : 24) : 0u;
-        na.q0 = do4 ? q04 : do6 ? alignb(d1, d0, 3) : 0u;
-        na.q1 = do6 ? alignb(d2, d1, 3) : 0u;
-        na.q2 = do6 ? alignb(d3, d2, 3) : 0u;
-        na.q3 = do6 ? d3 >> 24 : 0u;
-        flags = do4 ? 1u << 16 : do6 ? 1u << 17 : 0u;
-        const uint32_t i4 = a.dir16 ? d4 >> 16 : d4 >> 8;
-        const uint32_t i6 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu);
-        idx0 = do4 ? i4 : do6 ? i6 : 0u;
-        if (do4)
-            tb0 = a.dir16 ? a.dir16 : a.tbl24;
-        na.ptf = pt | flags | (1u << 18) | (pe << 19);
-    }
-    na.e = tb0[idx0]; // first gather, unconditional
-    // B's results
-    {
-        const KAS KArgs &o = kargs_fresh(a);
-        const uint32_t pt = sb.ptf & 0xffffu, pe = sb.ptf >> 19;
-        const bool bf = bv && (sb.ptf & (1u << 18));
-        const bool din = (sb.ptf & (3u << 16)) != 0u;
-        uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
-        if (din && (pe == 3u || pe == 4u)) {
-            nh = eb >> 1;
-            edge = nh >> 24;
-        }
-        if (o.spec_nh) {
-            if (bf && din && (!o.nh || (pe != 3u && pe != 4u)))
-                at32(o.spec_nh, ib) = eb >> 1;
-            if (bf) {
-                if (a.wl_fold && ib >= a.tail_lo)
-                    __hip_atomic_store(&at16(o.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                else
-                    __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
-            }
-            const uint32_t sg = ((pt & 0xffu) << 3) | pe;
-            spec_mark(s_sf, bf && sg != last_sig, sg);
-            last_sig = bf ? sg : last_sig;
-            if (o.spec_tile && bv) {
-                const bool odd = ib < a.n && !(bf && (pe == 3u || pe == 4u));
-                const uint64_t om = __ballot(odd);
-                if (lane == 0)
-                    o.spec_tile[t - wstep] = (uint8_t)(om == 0ull);
-                if (om && (a.spec_allow & SPEC_ALLOW_LISTS)) {
-                    const uint64_t nf = __ballot(ib < a.n && !bf), m3 = 0x8888888888888888ull;
-                    if (lane == 0 && ((nf & m3) | (om & m3 & (nf << 1))))
-                        atomicOr(s_mx, 1u << 8);
-                }
-            }
-        }
-        if (bf) {
-            const uint32_t q = s_reta[sb.h & a.reta_mask];
-            if (META && o.ptype)
-                __builtin_nontemporal_store(pt, &at32(o.ptype, ib));
-            if (META && o.rxmeta)
-                __builtin_nontemporal_store(sb.rx, &at32(o.rxmeta, ib));
-            if (META && o.iplen)
-                __builtin_nontemporal_store(sb.ipl, &at32(o.iplen, ib));
-            if (o.nh)
-                __builtin_nontemporal_store(nh, &at32(o.nh, ib));
-            if (o.hash)
-                __builtin_nontemporal_store(sb.h, &at32(o.hash, ib));
-            if (o.queue)
-                __builtin_nontemporal_store((uint16_t)q, &at16(o.queue, ib));
-            if (o.edge)
-                __builtin_nontemporal_store((uint8_t)edge, &o.edge[ib]);
-            if (count)
-                atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, q, a.n_bins)], 1u);
-        }
-    }
-    sb = na;
-    off.o0 = off.o1;
-    off.o1 = off.o2;
-}
-
-// s_bins (n_bins + 2 words) in dynamic LDS: the block's footprint stays ~22 KiB
-template <bool LNT, bool META>
-#ifndef DT_WPE
-#define DT_WPE 6
-#endif
-__global__ __launch_bounds__(DT_THREADS) __attribute__((amdgpu_waves_per_eu(META ? DT_WPE - 1 : DT_WPE))) void k_cnet_dma(KArgs a,
-                                                                                                uint32_t n_tiles)
-{
-    __shared__ uint32_t s_tn[2 * TAB_POS * 16];
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[DT_WAVES][256];
-    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
-    __shared__ uint32_t s_sf[64];
-    __shared__ uint32_t s_mx;
-    extern __shared__ uint32_t s_bins[];
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
-    u32x4 *tile = s_tile[wv];
-    const uint32_t wstep = gridDim.x * DT_WAVES;
-    const uint32_t t0 = blockIdx.x * DT_WAVES + wv;
-    const uint32_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
-    CsOff off{0, 0, 0, 0};
-    if (a.offsets) {
-        const uint32_t i0 = t0 * 64u + lane, i1 = (t0 + wstep) * 64u + lane;
-        off.o0 = t0 < n_tiles && i0 < a.n ? a.offsets[i0] : 0;
-        off.o1 = t0 + wstep < n_tiles && i1 < a.n ? a.offsets[i1] : 0;
-    }
-    if (tid < 64)
-        s_sf[tid] = 0;
-    if (tid == 0)
-        s_mx = 0;
-    dd_issue<LNT>(a, t0, n_tiles, off.o0, lane, tile);
-    for (uint32_t k = tid; k < 2 * TAB_POS * 16; k += DT_THREADS)
-        s_tn[k] = a.ttab[TABN_OFF + k];
-    for (uint32_t k = tid; k <= a.reta_mask; k += DT_THREADS)
-        s_reta[k] = a.reta[k];
-    const bool count = a.bins != nullptr;
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += DT_THREADS)
-            s_bins[k] = 0;
-    __syncthreads();
-    CdLane sb;
-    sb.ptf = sb.h = sb.e = sb.rx = 0;
-    sb.q0 = sb.q1 = sb.q2 = sb.q3 = 0;
-    uint32_t last_sig = 0xFFFFFFFFu;
-    const uint32_t trips = nt_w ? nt_w + 1 : 0;
-    for (uint32_t jt = 0; jt < trips; jt++)
-        dd_trip<LNT, META>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, off, sb, s_tn, s_reta, s_bins, s_sf, count,
-                           last_sig, &s_mx);
-    // the DMA of the tile past the wave's last one (a dummy or out-of-range
-    // tile) lands before the LDS is reused or the wave ends
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
-        __threadfence_block();
-        for (uint32_t j0 = 0; j0 < nt_w; j0 += 64u) {
-            const uint32_t j = j0 + lane;
-            uint64_t om = __ballot(j < nt_w && a.spec_tile[t0 + j * wstep] == 0u);
-            while (om) {
-                const uint32_t jj = j0 + (uint32_t)(__ffsll((unsigned long long)om) - 1);
-                om &= om - 1ull;
-                spec_odd_tile(a, t0 + jj * wstep, lane, &s_mx);
-            }
-        }
-    }
-    __syncthreads();
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += DT_THREADS)
-            if (s_bins[k])
-                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    if (a.spec_flags && tid < 64 && s_sf[tid])
-        atomicOr(&a.spec_flags[tid], s_sf[tid]);
-    if ((a.spec_allow & SPEC_ALLOW_LISTS) && tid == 0 && s_mx)
-        atomicOr(&a.spec_meta[SPEC_MX], s_mx);
-    if (a.wl_fold) // the general parse of the worklist hashes from the global byte tables
-        cnet_defer_tail<DT_THREADS, 128>(a, (uint32_t *)&s_tile[0][0], a.ttab, s_reta, s_bins, s_sf, count);
-}
-
-// ---------------------------------------------------------------------------
 // cnet ptype-node speculation (ptype.c:48-210) as a post-pass over the
 // per-packet ptypes the classify kernel wrote.  In each graph burst of B
 // packets the node walks 4-packet groups against its state last_type: a
@@ -5507,22 +5171,8 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 a.wl_fold = 1;
                 a.tail_lo = (uint32_t)t0;
             }
-            if (c->tune_cnet_tile == 2) {
-                // LDS-DMA form: 256-thread blocks, ~22 KiB of LDS each (CNDP_TUNE_BLOCKS_PER_CU, default 6)
-                static void (*const mfns[2][2])(KArgs, uint32_t) = {{k_cnet_dma<false, false>,
-                                                                     k_cnet_dma<false, true>},
-                                                                    {k_cnet_dma<true, false>,
-                                                                     k_cnet_dma<true, true>}};
-                uint64_t gm = (n_tiles + DT_WAVES - 1) / DT_WAVES;
-                const uint32_t mb = c->tune_bpc ? (uint32_t)c->tune_bpc : 6u;
-                if (gm > (uint64_t)c->num_cu * mb)
-                    gm = (uint64_t)c->num_cu * mb;
-                hipLaunchKernelGGL(mfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gm), dim3(DT_THREADS),
-                                   (a.n_bins + 2) * 4, s, a, (uint32_t)n_tiles);
-            } else {
-                hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
-                                   0, s, a, (uint32_t)n_tiles);
-            }
+            hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
+                               0, s, a, (uint32_t)n_tiles);
             if (!a.wl_fold)
                 hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         } else {
@@ -7917,7 +7567,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_dir16 = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_CNET_TILE:
-        if (value < 0 || value > 2)
+        if (value < 0 || value > 1)
             return -EINVAL;
         c->tune_cnet_tile = value;
         return 0;

@@ -372,9 +372,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *   CNDP_TUNE_CNET_TILE     cnet kernel: 1 = deferred-chain wave tile (fast path, the FIB
  *                           chain of each tile finished one loop trip later, two window
  *                           tiles in flight) + the general per-lane parse of the frames it
- *                           leaves (default), 2 = the same with the windows staged by
- *                           LDS DMA and nibble Toeplitz tables (256-thread blocks, six a
- *                           CU), 0 = the general per-lane parse for every frame
+ *                           leaves (default), 0 = the general per-lane parse for every frame
  *   CNDP_TUNE_HOST_CHUNK    packets per pipelined chunk of cndp_gpu_classify_host
  *                           (>= 1024, default 1M)
  *   CNDP_TUNE_CNET_SPEC     cnet: graph burst size B of the ptype node's speculative
