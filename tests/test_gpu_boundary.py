@@ -417,3 +417,53 @@ def test_fib_device_paint(gpu, nh_sz):
     check()
     b3, c3 = _sync_stats(f)
     assert c3 == c2 and b3 - b2 > 1 << 20
+
+
+def test_fib6_device_paint(gpu):
+    """The trie mirror under churn: the lpm6_1000 rules (lpm6_data_test.h) are
+    loaded, looked up on the GPU (the new mirror is copied whole), then
+    deleted and re-added in small batches between GPU lookups -- each sync
+    paints only those routes' tbl24 / tbl8 ranges (cndp_fib6_sync_stats) --
+    with every answer against brute-force LPM and the reference's golden next
+    hops at the end."""
+    import os
+    from cndp_amd.fib import Fib6
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "lpm6_1000.npz"))
+    f6 = Fib6("paint6", N.CNE_FIB_TRIE, default_nh=0, max_routes=2000, nh_sz=N.CNE_FIB_TRIE_4B,
+              num_tbl8=1 << 14, lookup=N.CNE_FIB_LOOKUP_GPU)
+    rules = [(bytes(ip), int(d), int(nh)) for ip, d, nh in zip(g["rule_ip"], g["rule_depth"], g["rule_nh"])]
+    for ip, d, nh in rules:
+        assert f6.add(ip, d, nh) == 0
+    keys = g["ip"][:4000]
+    assert np.array_equal(f6.lookup_bulk(keys), g["nh"][:4000].astype(np.uint64))
+
+    def stats():
+        b, c = ctypes.c_uint64(), ctypes.c_uint64()
+        assert N.lib().cndp_fib6_sync_stats(f6.h, ctypes.byref(b), ctypes.byref(c)) == 0
+        return b.value, c.value
+
+    rng = np.random.default_rng(8)
+    live = {(ip, d): nh for ip, d, nh in rules}
+    b0, c0 = stats()
+    painted = 0
+    for step in range(6):
+        pick = rng.choice(len(rules), size=5, replace=False)
+        for k in pick:
+            ip, d, nh = rules[k]
+            if (ip, d) in live:
+                assert f6.delete(ip, d) == 0
+                del live[(ip, d)]
+            else:
+                assert f6.add(ip, d, nh) == 0
+                live[(ip, d)] = nh
+        want = O.lpm6_bruteforce([(ip, d, nh) for (ip, d), nh in live.items()], 0, keys)
+        assert np.array_equal(f6.lookup_bulk(keys), want)
+        b1, c1 = stats()
+        painted += c1 > c0
+        assert b1 - b0 < (1 << 20), (step, b1 - b0)  # never the 64 MiB+ bounding copy
+        b0, c0 = b1, c1
+    assert painted >= 4
+    for (ip, d, nh) in rules:
+        if (ip, d) not in live:
+            assert f6.add(ip, d, nh) == 0
+    assert np.array_equal(f6.lookup_bulk(g["ip"]), g["nh"].astype(np.uint64))
