@@ -472,6 +472,56 @@ def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, p
     return res
 
 
+def fib_update(reps: int = 15) -> dict:
+    """Route churn between batches: K route adds at
+    scattered prefixes, then the first GPU-selection lookup, which syncs the
+    HBM mirror -- the device painter of the changed ranges against the
+    bounding-range copy (CNDP_FIB_PAINT=0).  Medians of `reps`: the call's
+    µs (a 4-key lookup alone is ~10 µs) and the bytes the sync moved."""
+    import ctypes
+    import numpy as np
+    from cndp_amd import native as N
+    from cndp_amd.fib import Fib
+
+    def stats(f):
+        b, c = ctypes.c_uint64(), ctypes.c_uint64()
+        N.lib().cndp_fib_sync_stats(f.h, ctypes.byref(b), ctypes.byref(c))
+        return b.value, c.value
+
+    res = {"what": "K scattered route adds (/16../32) then one 4-key GPU-selection lookup (mirror sync + lookup)"}
+    old = os.environ.get("CNDP_FIB_PAINT")
+    try:
+        for mode, env in (("device_paint", "1"), ("bounding_copy", "0")):
+            os.environ["CNDP_FIB_PAINT"] = env
+            rng = np.random.default_rng(3)
+            f = Fib(f"upd_{mode}", N.CNE_FIB_DIR24_8, default_nh=1 << 16, max_routes=1 << 16,
+                    nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=4096, lookup=N.CNE_FIB_LOOKUP_GPU)
+            keys = rng.integers(0, 2**32, size=4, dtype=np.uint64).astype(np.uint32)
+            f.lookup_bulk(keys)
+            for k in (8, 64):
+                rows = []
+                for _ in range(reps):
+                    for _ in range(k):
+                        d = int(rng.choice([16, 24, 24, 24, 28, 32]))
+                        ip = int(rng.integers(0, 2**32)) & ((0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF)
+                        f.add(ip, d, int(rng.integers(0, 1 << 15)))
+                    b0, _ = stats(f)
+                    t = time.perf_counter()
+                    f.lookup_bulk(keys)
+                    dt = time.perf_counter() - t
+                    rows.append((dt * 1e6, stats(f)[0] - b0))
+                a = np.array(rows)
+                res.setdefault(mode, {})[f"changes_{k}"] = {"median_us": round(float(np.median(a[:, 0])), 1),
+                                                            "median_bytes": int(np.median(a[:, 1]))}
+            del f
+    finally:
+        if old is None:
+            os.environ.pop("CNDP_FIB_PAINT", None)
+        else:
+            os.environ["CNDP_FIB_PAINT"] = old
+    return res
+
+
 def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     """The graph-node boundary over pktmbuf_t bursts (rank 0, N=1).  One host
     thread drives, as one lcore's graph walk would:
@@ -1010,7 +1060,7 @@ def main():
     layout = ("packed 64-B slots" if fr.offsets is None and fr.stride == 64
               else ("IMIX packed at roundup(len,64)" if fr.offsets is not None else f"{fr.stride}-B slots"))
     ring_len = len(st["ring"])
-    cpu = e2e = nb = None
+    cpu = e2e = nb = fu = None
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline and args.config != "c3rw":
             cpu = cpu_baseline(st, args.cpu_budget)
@@ -1048,6 +1098,11 @@ def main():
             log(f"[bench] node boundary: {nb}")
         except Exception as ex:  # reported, never fatal for the headline line
             nb = {"error": repr(ex)}
+        try:
+            fu = fib_update()
+            log(f"[bench] fib update: {fu}")
+        except Exception as ex:  # reported, never fatal for the headline line
+            fu = {"error": repr(ex)}
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -1077,6 +1132,7 @@ def main():
             "configs": extra,
             "node_boundary": nb,
             "host_memory_e2e": e2e,
+            "fib_update": fu,
         }
         print(json.dumps(res), flush=True)
     if world > 1:

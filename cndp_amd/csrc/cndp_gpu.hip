@@ -4571,7 +4571,8 @@ static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
         t->d8_hi = (uint64_t)groups * CNDP_TBL8_GRP;
     }
     // CNDP_FIB_PAINT=0: always the bounding-range copy (A/B of the painter)
-    static const bool paint_on = !getenv("CNDP_FIB_PAINT") || atoi(getenv("CNDP_FIB_PAINT")) != 0;
+    const char *pe = getenv("CNDP_FIB_PAINT");
+    const bool paint_on = !pe || atoi(pe) != 0;
     paint24 = paint_on && paint24 && t->n_log24 <= CNDP_TBL_LOG && t->d24_hi > t->d24_lo;
     if (paint24) // merged once here: the painter and the /16 directory walk the same ranges
         t->n_log24 = paint_merge(t->log24, t->n_log24);
