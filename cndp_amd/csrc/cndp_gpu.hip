@@ -5859,12 +5859,19 @@ extern "C" int cndp_gpu_frames_alloc(int device, uint64_t bytes, uint32_t flags,
         *dptr = nullptr;
     if (!dptr || !bytes || (flags & ~CNDP_FRAMES_CACHED))
         return -EINVAL;
-    if (device >= 0 && set_device(device))
+    int cur = -1;
+    if (device >= 0 && (hipGetDevice(&cur) != hipSuccess || set_device(device)))
         return -ENODEV;
-    if (flags & CNDP_FRAMES_CACHED)
-        HIP_TRY(hipMalloc(dptr, bytes));
-    else
-        HIP_TRY(hipExtMallocWithFlags(dptr, bytes, hipDeviceMallocUncached));
+    const hipError_t e = (flags & CNDP_FRAMES_CACHED) ? hipMalloc(dptr, bytes)
+                                                      : hipExtMallocWithFlags(dptr, bytes, hipDeviceMallocUncached);
+    if (cur >= 0 && cur != device)
+        hipSetDevice(cur); // the caller's current device is left as it was
+    if (e != hipSuccess) {
+        *dptr = nullptr;
+        fprintf(stderr, "cndp_gpu: frames alloc of %llu B failed: %s\n", (unsigned long long)bytes,
+                hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
+    }
     return 0;
 }
 

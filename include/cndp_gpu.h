@@ -339,7 +339,8 @@ int cndp_gpu_host_unregister(cndp_gpu_ctx_t *ctx, void *ptr);
  * device `device` (-1 = current), uncached on the GPU by default, so a peer's
  * writes need no GPU cache maintenance and the classify kernels' 64-B window
  * reads allocate no L2 lines (faster for IMIX / jumbo strides).
- * CNDP_FRAMES_CACHED: plain device memory.  -EINVAL, -ENODEV, -EIO. */
+ * CNDP_FRAMES_CACHED: plain device memory.  The calling thread's current device is
+ * unchanged.  -EINVAL, -ENODEV, -ENOMEM, -EIO. */
 #define CNDP_FRAMES_CACHED 1u
 int cndp_gpu_frames_alloc(int device, uint64_t bytes, uint32_t flags, void **dptr);
 int cndp_gpu_frames_free(void *dptr);
