@@ -1970,410 +1970,6 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
 }
 
 // ---------------------------------------------------------------------------
-// cnet kernel, pipelined-chain form (CNDP_TUNE_CNET_TILE 2).  k_cnet_defer
-// resolves a tile's FIB chain inside one loop trip: every dependent level
-// waits vmcnt(0), i.e. for every load issued before it, the next tile's
-// windows included, so a trip costs (chain levels + the window latency).
-// Here the chain is software-pipelined across trips: a tile's first gather
-// is issued in stage A of trip c, its level k by stage S_k in trip c + k, and
-// every load a trip issues is consumed in the next one, oldest first.  For
-// hipcc's waits to stay partial (vmcnt(N) that leaves the newest windows in
-// flight) every VMEM load of a trip is unconditional (dummy index where a
-// lane has nothing to load), and the stores and atomics are issued from
-// inline asm, outside the compiler's count, so they may sit under branches.
-// Results that do not depend on the chain are stored at A; nh / edge when a
-// lane's chain ends.  v4 needs at most 2 levels (/16 page, tbl8), v6 up to
-// 13: S1..S5 issue levels 1..5 from key bytes held since A; a lane still
-// extended after level 5 goes to the worklist (the general parse redoes it).
-// ---------------------------------------------------------------------------
-#define CP_NS 6 // chain stages S1..S6 (tiles in flight behind A)
-
-// vector stores / atomics from asm: base (wave-uniform) + 32-bit byte offset
-__device__ __forceinline__ void cp_st32(const void *base, uint32_t off, uint32_t v)
-{
-    asm volatile("global_store_dword %0, %1, %2 nt" ::"v"(off), "v"(v), "s"(base) : "memory");
-}
-__device__ __forceinline__ void cp_st32_wt(const void *base, uint32_t off, uint32_t v) // write-through (agent scope)
-{
-    asm volatile("global_store_dword %0, %1, %2 sc1" ::"v"(off), "v"(v), "s"(base) : "memory");
-}
-__device__ __forceinline__ void cp_st16(const void *base, uint32_t off, uint32_t v)
-{
-    asm volatile("global_store_short %0, %1, %2 nt" ::"v"(off), "v"(v), "s"(base) : "memory");
-}
-__device__ __forceinline__ void cp_st16_wt(const void *base, uint32_t off, uint32_t v)
-{
-    asm volatile("global_store_short %0, %1, %2 sc1" ::"v"(off), "v"(v), "s"(base) : "memory");
-}
-__device__ __forceinline__ void cp_st8(const void *base, uint32_t off, uint32_t v)
-{
-    asm volatile("global_store_byte %0, %1, %2 nt" ::"v"(off), "v"(v), "s"(base) : "memory");
-}
-// returning atomic add; the asm drains the counter itself (rare paths only)
-__device__ __forceinline__ uint32_t cp_atomic_add(const void *base, uint32_t v)
-{
-    uint32_t old;
-    asm volatile("global_atomic_add %0, %1, %2, %3 sc0\n\ts_waitcnt vmcnt(0)"
-                 : "=v"(old)
-                 : "v"(0u), "v"(v), "s"(base)
-                 : "memory");
-    return old;
-}
-
-struct CpSt {
-    uint32_t v; // the entry loaded by the previous stage (bit 0: extended)
-    uint32_t k; // the next key bytes, next lowest
-    uint32_t m; // pt (16) | do4 << 16 | do6 << 17 | live chain << 18 | pe << 19 (3) | zero key << 22 | key byte after k << 24
-};
-
-// a lane's chain result: nh, edge, the speculation's input-node value, bins
-__device__ __forceinline__ void cp_result(const KArgs &a, uint32_t ib, uint32_t m, uint32_t e, uint32_t *s_bins,
-                                          bool count)
-{
-    const KAS KArgs &o = kargs_fresh(a);
-    const uint32_t pe = (m >> 19) & 7u;
-    const bool din = (m & (3u << 16)) != 0u;
-    uint32_t nh = CNDP_NH_INVALID, edge = 0x80u | pe;
-    if (din && (pe == 3u || pe == 4u)) {
-        nh = e >> 1;
-        edge = nh >> 24;
-    }
-    if (o.spec_nh && din && (!o.nh || (pe != 3u && pe != 4u)))
-        cp_st32(o.spec_nh, ib << 2, e >> 1);
-    if (o.nh)
-        cp_st32(o.nh, ib << 2, nh);
-    if (o.edge)
-        cp_st8(o.edge, ib, edge);
-    if (count)
-        atomicAdd(&s_bins[bin_of<CNDP_MODE_CNET>(nh, edge, 0u, a.n_bins)], 1u);
-}
-
-// S_L (L = 1..5): consume level L-1's entry; a lane whose chain ends stores its
-// results, the others issue level L.  The load is issued for every lane.
-template <int L>
-__device__ __forceinline__ void cp_stage(const KArgs &a, CpSt &st, uint32_t ib, uint32_t *s_bins, bool count)
-{
-    const bool live = (st.m & (1u << 18)) != 0u;
-    const bool d6 = (st.m & (1u << 17)) != 0u;
-    const bool lv_ok = d6 || (L == 1) || (L == 2 && a.dir16 != nullptr);
-    const uint32_t e = st.v;
-    const bool more = live & lv_ok & ((e & 1u) != 0u);
-    if (live && !more) { // the chain ended at level L-1
-        cp_result(a, ib, st.m, e, s_bins, count);
-    }
-    const GAS uint32_t *const t6 = sgpr_pin(a.tbl8_6);
-    const GAS uint32_t *const t4 = sgpr_pin(L == 1 && a.dir16 ? a.pages : a.tbl8);
-    const uint32_t idx = more ? ((e >> 1) << 8) | (st.k & 0xffu) : 0u;
-    st.v = (d6 ? t6 : t4)[idx]; // unconditional
-    st.k = (st.k >> 8) | (st.m & 0xff000000u);
-    st.m = more ? st.m & 0x00ffffffu : 0u;
-}
-
-template <bool LNT, bool META, int P>
-__device__ __forceinline__ void cp_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
-                                        uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4], CsOff &off,
-                                        CpSt (&st)[CP_NS], const uint32_t *s_t, const uint16_t *s_reta,
-                                        uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig,
-                                        uint32_t *s_mx, bool with_a)
-{
-    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const uint32_t t = t0 + jt * wstep;
-    // S6: the tile of trip jt - 6 consumes its level-5 entry; a lane still
-    // extended (a v6 route longer than /64) goes to the worklist
-    {
-        const CpSt &s6 = st[5];
-        const uint32_t ib = (t - 6u * wstep) * 64u + lane;
-        const bool live = (s6.m & (1u << 18)) != 0u;
-        const bool deep = live & ((s6.v & 1u) != 0u);
-        if (live && !deep)
-            cp_result(a, ib, s6.m, s6.v, s_bins, count);
-        const unsigned long long dm = __ballot(deep);
-        if (dm) { // rare: the general parse finishes these frames
-            const KAS KArgs &o = kargs_fresh(a);
-            uint32_t w0 = 0;
-            if (lane == (uint32_t)(__ffsll(dm) - 1))
-                w0 = cp_atomic_add(o.wl_n, (uint32_t)__popcll(dm));
-            w0 = __shfl(w0, __ffsll(dm) - 1);
-            if (deep)
-                cp_st32_wt(o.wl, (w0 + (uint32_t)__popcll(dm & ((1ull << lane) - 1ull))) << 2, ib);
-        }
-    }
-    // S5 .. S1, oldest load first
-    cp_stage<5>(a, st[4], (t - 5u * wstep) * 64u + lane, s_bins, count);
-    cp_stage<4>(a, st[3], (t - 4u * wstep) * 64u + lane, s_bins, count);
-    cp_stage<3>(a, st[2], (t - 3u * wstep) * 64u + lane, s_bins, count);
-    cp_stage<2>(a, st[1], (t - 2u * wstep) * 64u + lane, s_bins, count);
-    cp_stage<1>(a, st[0], (t - 1u * wstep) * 64u + lane, s_bins, count);
-    CpSt na{0, 0, 0};
-    if (with_a) {
-        // A: tile c
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t f = 16u * k + fr_in_k;
-            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t i = t * 64u + lane;
-        const bool live = i < a.n;
-        const uint64_t base = live ? ct_base(a, i, off.o0) : ~0ull;
-        const uint32_t sw = (lane >> 2) & 3u;
-        uint32_t W[16];
-        {
-            const u32x4 c0 = tile[lane * 4u + (0u ^ sw)], c1 = tile[lane * 4u + (1u ^ sw)];
-            const u32x4 c2 = tile[lane * 4u + (2u ^ sw)], c3 = tile[lane * 4u + (3u ^ sw)];
-            W[0] = c0.x; W[1] = c0.y; W[2] = c0.z; W[3] = c0.w;
-            W[4] = c1.x; W[5] = c1.y; W[6] = c1.z; W[7] = c1.w;
-            W[8] = c2.x; W[9] = c2.y; W[10] = c2.z; W[11] = c2.w;
-            W[12] = c3.x; W[13] = c3.y; W[14] = c3.z; W[15] = c3.w;
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t et = W[3] & 0xffffu;
-        const uint32_t p4 = W[5] >> 24, p6 = W[5] & 0xffu;
-        const uint32_t l4b4 = pt_l4(p4), l4b6 = pt_l4(p6);
-        const bool f4 = (et == BE16C(0x0800u)) & (((W[3] >> 16) & 0xffu) == 0x45u) &
-                        (((W[5] & 0xffffu) & BE16C(0x3fffu)) == 0u) & (l4b4 != 0u);
-        const bool f6 = (et == BE16C(0x86DDu)) & (l4b6 != 0u);
-        const bool fast = live & ct_fast(a, base) & (f4 | f6);
-        {
-            const bool slow = live && !fast;
-            const unsigned long long m = __ballot(slow);
-            if (m) {
-                const KAS KArgs &o = kargs_fresh(a);
-                uint32_t w0 = 0;
-                if (lane == (uint32_t)(__ffsll(m) - 1))
-                    w0 = cp_atomic_add(o.wl_n, (uint32_t)__popcll(m));
-                w0 = __shfl(w0, __ffsll(m) - 1);
-                if (slow)
-                    cp_st32_wt(o.wl, (w0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) << 2, i);
-            }
-        }
-        uint32_t idx0 = 0, pt = 0, pe = 0, h = 0, rx = 0, ipl = 0;
-        bool do4 = false;
-        if (fast) {
-            const uint32_t proto = f4 ? p4 : p6;
-            pt = (f4 ? 0x11u : 0x41u) | (f4 ? l4b4 : l4b6);
-            const uint32_t dport = f4 ? (W[9] & 0xffffu) : (W[14] & 0xffffu);
-            const bool udp = proto == 17u, gtpu = udp & (dport == BE16C(2152u)), gtpc = udp & (dport == BE16C(2123u));
-            pt |= gtpu ? 0x8000u : gtpc ? 0x7000u : 0u;
-            pe = (proto == 6u) | (udp & !gtpc) ? (gtpu ? 5u : f4 ? 3u : 4u) : 0u;
-            const bool l4ok = proto == 6u || proto == 17u;
-            if (META && a.rxmeta) {
-                Lens lens{14u, f4 ? 20u : 40u, 0u};
-                lens.l4 = proto == 17u ? 8u : proto == 132u ? 12u
-                        : f4 ? ((W[11] >> 16) & 0xf0u) >> 2
-                             : (gbyte(a.slab + base, a.slab_len - base, 66) & 0xf0u) >> 2;
-                rx = rx_meta(lens, W[0], W[1], et);
-            }
-            if (META && a.iplen)
-                ipl = (1u << 16) | bswap16(f4 ? (W[4] & 0xffffu) : (W[4] >> 16));
-            if (META && a.win) {
-                u32x4 *dw = a.win + 4ull * i;
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    dw[k] = (u32x4){W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]};
-            }
-            {
-                uint32_t V[9];
-#pragma unroll
-                for (int k = 0; k < 9; k++)
-                    V[k] = alignb(W[6 + k], W[5 + k], 2);
-                const bool any6 = __any(f6);
-#pragma unroll
-                for (int k = 0; k < 9; k++) {
-                    if (k >= 3 && !any6)
-                        break;
-                    uint32_t u = k < 2 ? (f4 ? V[k + 1] : V[k]) : k == 2 ? (f4 ? (l4ok ? V[3] : 0u) : V[2])
-                               : k < 8 ? (f4 ? 0u : V[k]) : (f4 || !l4ok ? 0u : V[8]);
-                    h ^= tz4(s_t, 4 * k, u);
-                }
-            }
-            do4 = f4 & ((pe == 3u) | (a.spec_nh != nullptr));
-            const bool do6 = !f4 & ((pe == 4u) | (a.spec_nh != nullptr));
-            const uint32_t dst = alignb(W[8], W[7], 2);
-            uint32_t sum = (W[3] >> 16) + (W[8] & 0xffffu);
-#pragma unroll
-            for (int k = 4; k < 8; k++)
-                sum = hsum2(W[k], sum);
-            sum = (sum >> 16) + (sum & 0xffffu);
-            sum = (sum >> 16) + (sum & 0xffffu);
-            const bool ok4 = (bswap16(W[4] & 0xffffu) < a.buf_len) & (((~sum) & 0xffffu) == 0u);
-            const uint32_t d4 = ok4 ? bswap32(dst) : 0u;
-            const bool ok6 = bswap16(W[4] >> 16) < a.buf_len;
-            const uint32_t d0 = ok6 ? alignb(W[10], W[9], 2) : 0u, d1 = ok6 ? alignb(W[11], W[10], 2) : 0u;
-            const uint32_t d2 = ok6 ? alignb(W[12], W[11], 2) : 0u;
-            const uint32_t q04 = ok4 ? dst >> (a.dir16 ? 16 : 24) : 0u; // network bytes 2, 3
-            na.k = do4 ? q04 : do6 ? alignb(d1, d0, 3) : 0u;             // v6: address bytes 3..6
-            const uint32_t khi = do6 ? (alignb(d2, d1, 3) & 0xffu) : 0u; // v6: byte 7
-            const uint32_t i4 = a.dir16 ? d4 >> 16 : d4 >> 8;
-            const uint32_t i6 = ((d0 & 0xffu) << 16) | (d0 & 0xff00u) | ((d0 >> 16) & 0xffu); // trie.h:126
-            idx0 = do4 ? i4 : do6 ? i6 : 0u;
-            na.m = pt | (do4 ? 1u << 16 : do6 ? 1u << 17 : 0u) | (1u << 18) | (pe << 19) |
-                   ((do6 && !ok6) ? 1u << 22 : 0u) | (khi << 24);
-        }
-        // the first gather, unconditional (tbl24 of the trie for v6 and the
-        // lanes without a lookup, the /16 directory or tbl24 for v4)
-        {
-            const GAS uint32_t *const g6 = sgpr_pin(a.tbl24_6);
-            const GAS uint32_t *const g4 = sgpr_pin(a.dir16 ? a.dir16 : a.tbl24);
-            na.v = (do4 ? g4 : g6)[idx0];
-        }
-        // A's results: everything that does not depend on the chain
-        {
-            const KAS KArgs &o = kargs_fresh(a);
-            if (o.spec_nh) {
-                if (fast) {
-                    if (a.wl_fold && i >= a.tail_lo)
-                        cp_st16_wt(o.spec_t16, i << 1, pt);
-                    else
-                        cp_st16(o.spec_t16, i << 1, pt);
-                }
-                const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
-                spec_mark(s_sf, fast && sg != last_sig, sg);
-                last_sig = fast ? sg : last_sig;
-                if (o.spec_tile) {
-                    const bool odd = live && !(fast && (pe == 3u || pe == 4u));
-                    const uint64_t om = __ballot(odd);
-                    if (lane == 0)
-                        cp_st8(o.spec_tile, t, om == 0ull ? 1u : 0u);
-                    if (om && (a.spec_allow & SPEC_ALLOW_LISTS)) { // wave-uniform, rare
-                        const uint64_t nf = __ballot(live && !fast), m3 = 0x8888888888888888ull;
-                        if (lane == 0 && ((nf & m3) | (om & m3 & (nf << 1))))
-                            atomicOr(s_mx, 1u << 8);
-                    }
-                }
-            }
-            if (fast) {
-                const uint32_t q = s_reta[h & a.reta_mask];
-                if (META && o.ptype)
-                    cp_st32(o.ptype, i << 2, pt);
-                if (META && o.rxmeta)
-                    cp_st32(o.rxmeta, i << 2, rx);
-                if (META && o.iplen)
-                    cp_st32(o.iplen, i << 2, ipl);
-                if (o.hash)
-                    cp_st32(o.hash, i << 2, h);
-                if (o.queue)
-                    cp_st16(o.queue, i << 1, q);
-            }
-        }
-        // offsets one tile further (unconditional: a dummy word without
-        // offsets), then the windows of tile c+2
-        {
-            const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
-            const bool have = a.offsets && t3 < n_tiles && i3 < a.n;
-            const GAS uint64_t *const ob = sgpr_pin(a.offsets ? a.offsets : (const uint64_t *)a.ttab);
-            const uint64_t o3 = ob[have ? i3 : 0u];
-            off.o3 = have ? o3 : 0;
-            cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
-        }
-        off.o0 = off.o1;
-        off.o1 = off.o2;
-        off.o2 = off.o3;
-    }
-#pragma unroll
-    for (int k = CP_NS - 1; k > 0; k--)
-        st[k] = st[k - 1];
-    st[0] = na;
-}
-
-template <bool LNT, bool META>
-__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_cnet_pipe(KArgs a,
-                                                                                          uint32_t n_tiles)
-{
-    __shared__ uint32_t s_t[TAB_POS * 256];
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
-    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
-    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
-    __shared__ uint32_t s_sf[64];
-    __shared__ uint32_t s_mx;
-
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
-    u32x4 *tile = s_tile[wv];
-    const uint32_t wstep = gridDim.x * CT_WAVES;
-    const uint32_t t0 = blockIdx.x * CT_WAVES + wv;
-    const uint32_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
-    CsOff off{0, 0, 0, 0};
-    if (a.offsets) {
-#pragma unroll
-        for (uint32_t s = 0; s < 3; s++) {
-            const uint32_t ts = t0 + s * wstep, is = ts * 64u + lane;
-            const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
-            if (s == 0)
-                off.o0 = o;
-            else if (s == 1)
-                off.o1 = o;
-            else
-                off.o2 = o;
-        }
-    }
-    if (tid < 64)
-        s_sf[tid] = 0;
-    if (tid == 0)
-        s_mx = 0;
-    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
-        s_t[k] = a.ttab[k];
-    u32x4 r[2][4];
-    cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
-    cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
-    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
-        s_reta[k] = a.reta[k];
-    const bool count = a.bins != nullptr;
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
-            s_bins[k] = 0;
-    __syncthreads();
-    CpSt st[CP_NS];
-#pragma unroll
-    for (int k = 0; k < CP_NS; k++)
-        st[k] = CpSt{0, 0, 0};
-    uint32_t last_sig = 0xFFFFFFFFu;
-    // the wave's tiles (stage A every trip), then CP_NS trips that drain the chain
-    uint32_t jt = 0;
-    for (; jt + 1 < nt_w; jt += 2) {
-        cp_trip<LNT, META, 0>(a, t0, wstep, n_tiles, jt, lane, tile, r, off, st, s_t, s_reta, s_bins, s_sf, count,
-                              last_sig, &s_mx, true);
-        cp_trip<LNT, META, 1>(a, t0, wstep, n_tiles, jt + 1, lane, tile, r, off, st, s_t, s_reta, s_bins, s_sf, count,
-                              last_sig, &s_mx, true);
-    }
-    if (jt < nt_w) {
-        cp_trip<LNT, META, 0>(a, t0, wstep, n_tiles, jt, lane, tile, r, off, st, s_t, s_reta, s_bins, s_sf, count,
-                              last_sig, &s_mx, true);
-        jt++;
-    }
-    if (nt_w)
-        for (uint32_t d = 0; d < CP_NS; d++, jt++)
-            cp_trip<LNT, META, 0>(a, t0, wstep, n_tiles, jt, lane, tile, r, off, st, s_t, s_reta, s_bins, s_sf, count,
-                                  last_sig, &s_mx, false);
-    // the asm stores are outside hipcc's count: drain them before the tail
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
-        __threadfence_block();
-        for (uint32_t j0 = 0; j0 < nt_w; j0 += 64u) {
-            const uint32_t j = j0 + lane;
-            uint64_t om = __ballot(j < nt_w && a.spec_tile[t0 + j * wstep] == 0u);
-            while (om) {
-                const uint32_t jj = j0 + (uint32_t)(__ffsll((unsigned long long)om) - 1);
-                om &= om - 1ull;
-                spec_odd_tile(a, t0 + jj * wstep, lane, &s_mx);
-            }
-        }
-    }
-    if (count || a.spec_flags || (a.spec_allow & SPEC_ALLOW_LISTS))
-        __syncthreads();
-    if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
-            if (s_bins[k])
-                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
-    if (a.spec_flags && tid < 64 && s_sf[tid])
-        atomicOr(&a.spec_flags[tid], s_sf[tid]);
-    if ((a.spec_allow & SPEC_ALLOW_LISTS) && tid == 0 && s_mx)
-        atomicOr(&a.spec_meta[SPEC_MX], s_mx);
-    if (a.wl_fold)
-        cnet_defer_tail<CT_THREADS, 256>(a, (uint32_t *)&s_tile[0][0], s_t, s_reta, s_bins, s_sf, count);
-}
-
-// ---------------------------------------------------------------------------
 // cnet ptype-node speculation (ptype.c:48-210) as a post-pass over the
 // per-packet ptypes the classify kernel wrote.  In each graph burst of B
 // packets the node walks 4-packet groups against its state last_type: a
@@ -5576,12 +5172,8 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 a.wl_fold = 1;
                 a.tail_lo = (uint32_t)t0;
             }
-            static void (*const pfns[2][2])(KArgs, uint32_t) = {{k_cnet_pipe<false, false>,
-                                                                 k_cnet_pipe<false, true>},
-                                                                {k_cnet_pipe<true, false>,
-                                                                 k_cnet_pipe<true, true>}};
-            hipLaunchKernelGGL((c->tune_cnet_tile == 2 ? pfns : dfns)[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0],
-                               dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, (uint32_t)n_tiles);
+            hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
+                               0, s, a, (uint32_t)n_tiles);
             if (!a.wl_fold)
                 hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         } else {
@@ -7983,7 +7575,7 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         c->tune_dir16 = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_CNET_TILE:
-        if (value < 0 || value > 2)
+        if (value < 0 || value > 1)
             return -EINVAL;
         c->tune_cnet_tile = value;
         return 0;

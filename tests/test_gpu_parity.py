@@ -17,7 +17,7 @@ from helpers import (CNET_DEF, L3FWD_DEF, assert_same, cnet_fibs, l3fwd_fib, l3f
                      oracle_classify)
 
 pytestmark = pytest.mark.gpu
-CNET_KERNELS = (0, 2, 1)  # per-lane general parse, pipelined chain, deferred chain + worklist (default, set last)
+CNET_KERNELS = (0, 1)  # per-lane general parse, deferred chain + worklist (default, set last)
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
