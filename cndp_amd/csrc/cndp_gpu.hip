@@ -4451,7 +4451,11 @@ static void paint_plan(const struct cndp_tbl *t, uint32_t which, const uint8_t *
         const uint64_t off = (payload.size() + 7u) & ~7ull;
         payload.resize(off + (hi - lo) * esz);
         memcpy(payload.data() + off, img + lo * esz, (hi - lo) * esz);
-        cmds.push_back(TblCmd{lo, (uint32_t)(hi - lo), which | 2u, off});
+        // long copies spread over blocks like fills
+        for (uint64_t f = lo; f < hi; f += PAINT_FILL_MAX) {
+            const uint64_t c = hi - f < PAINT_FILL_MAX ? hi - f : PAINT_FILL_MAX;
+            cmds.push_back(TblCmd{f, (uint32_t)c, which | 2u, off + (f - lo) * esz});
+        }
     };
     for (uint32_t k = 0; k < n; k++) {
         uint64_t i = r[k].lo, cs = i; // cs: start of the pending copy segment

@@ -257,7 +257,8 @@ static int pktdev_rx_gpu_init(const struct cne_graph *graph, struct cne_node *no
          * drops then take this node's own pkt_drop edge, so pkt_drop gets one
          * enqueue per poll in receive order */
         char *names[RX_EDGES_MAX];
-        st->tx0_drop = cne_node_edge_get(node->id, names) == st->nb_edges &&
+        st->tx0_drop = cne_node_edge_count(node->id) <= RX_EDGES_MAX &&
+                       cne_node_edge_get(node->id, names) == st->nb_edges &&
                        strcmp(names[PKTDEV_RX_GPU_NEXT_TX0], "pkt_drop") == 0;
     }
     if ((r = cndp_gpu_mq_create(st->gpu, &conf, &st->q)) < 0)
