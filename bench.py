@@ -221,6 +221,47 @@ def parity_sample(state, k: int = 1 << 16) -> bool:
     return ok
 
 
+def parity_full(state, max_slab_bytes: int = 8 << 30):
+    """The whole batch against the oracle (untimed): every per-packet output
+    (nh, hash, queue, edge) and the bin counters of one classify call, cnet
+    from the ptype node's initial state like the oracle's node loop -- when the
+    slab fits the host comfortably (C2, C3, C4; C5's 48 GiB shard keeps the
+    sampled windows and the full-size test).  None when skipped."""
+    from cndp_amd import native as N
+    from oracle import oracle as O
+    fr = state["frames"]
+    if fr.slab.numel() > max_slab_bytes:
+        return None
+    t0 = time.perf_counter()
+    cl, out = state["cl"], state["out"]
+    kw = dict(tables4=tuple(x.copy() for x in state["fib"].image()))
+    cnet = state["mode"] == N.CNDP_MODE_CNET
+    if cnet:
+        kw["tables6"] = tuple(x.copy() for x in state["fib6"].image())
+        kw["spec_burst"] = 256
+        cl.set_tuning(cnet_spec=256)  # the node state back to 0, as the oracle starts
+    o = dict(out)
+    o["bins"] = torch.zeros_like(out["bins"])
+    cl.classify(fr, state["mode"], out=o)
+    torch.cuda.synchronize()
+    slab = fr.slab.cpu().numpy()
+    if fr.offsets is not None:
+        ref = O.classify(state["mode"], slab, fr.n, offsets=fr.offsets.cpu().numpy().astype(np.uint64),
+                         data_off=fr.data_off, **kw)
+    else:
+        ref = O.classify(state["mode"], slab, fr.n, stride=fr.stride, data_off=fr.data_off, **kw)
+    del slab
+    diff = {}
+    for key, dt in (("nh", np.uint32), ("hash", np.uint32), ("queue", np.uint16), ("edge", np.uint8),
+                    ("bins", np.uint64)):
+        if o.get(key) is None:
+            continue
+        g = o[key].cpu().numpy().view(dt)
+        diff[key] = int(np.sum(g != ref[key]))
+    return {"frames": fr.n, "equal": all(v == 0 for v in diff.values()), "mismatches": diff,
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
 def host_cpus():
     """CPUs this process may run on, the CPU model, and the cgroup CPU quota."""
     cpus = sorted(os.sched_getaffinity(0))
@@ -426,7 +467,8 @@ def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, p
         run_step(st, stream, k)
     torch.cuda.synchronize()
     ok = parity_sample(st) if parity and rank == 0 else None
-    # the parity sample restarts the cnet node model (state 0): one call
+    full = parity_full(st) if parity and rank == 0 else None
+    # the parity checks restart the cnet node model (state 0): one call
     # settles it again, as the warmup did, before the timed windows
     for k in range(max(1, warmup)):
         run_step(st, stream, k)
@@ -455,6 +497,7 @@ def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, p
     res = {"config": cfg, "workload": st["desc"], "value": round(value, 2),
            "unit": "Mpps", "ms_per_step": round(elapsed / steps * 1e3, 4), "packets_per_gpu": n,
            "ring_batches": len(st["ring"]), "frame_memory": frame_mem_name(cfg), "parity_sample_vs_oracle": ok,
+           "parity_full_batch_vs_oracle": full,
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(cfg),
                         "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_pkt": st["algo"]}}
@@ -1026,10 +1069,13 @@ def main():
         run_step(st, None, k)
     torch.cuda.synchronize()
     parity = None
+    parity_all = None
     if rank == 0 and not args.no_parity:
         parity = parity_sample(st)
         log(f"[bench] parity sample vs oracle: {parity}")
-        run_step(st, None, 0)  # the sample restarted the cnet node model: settle it untimed
+        parity_all = parity_full(st)
+        log(f"[bench] full batch vs oracle: {parity_all}")
+        run_step(st, None, 0)  # the checks restarted the cnet node model: settle it untimed
     out["bins"].zero_()
 
     if world > 1:
@@ -1125,7 +1171,7 @@ def main():
                        "frame_layout": layout, "frame_memory": frame_mem_name(args.config),
                        "ring_batches": ring_len,
                        "routes": len(st["routes"]), "parallelism": f"dp{world} (replicated FIB, sharded batches)",
-                       "parity_sample_vs_oracle": parity,
+                       "parity_sample_vs_oracle": parity, "parity_full_batch_vs_oracle": parity_all,
                        "bins_total": int(bins.sum())},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
