@@ -225,12 +225,13 @@ def parity_full(state, max_slab_bytes: int = 8 << 30):
     """The whole batch against the oracle (untimed): every per-packet output
     (nh, hash, queue, edge) and the bin counters of one classify call, cnet
     from the ptype node's initial state like the oracle's node loop -- when the
-    slab fits the host comfortably (C2, C3, C4; C5's 48 GiB shard keeps the
-    sampled windows and the full-size test).  None when skipped."""
+    slab fits the host comfortably (C2, C3, C4), or in 1M-frame pieces for a
+    strided slab that does not (C5's 48 GiB shard).  None when skipped."""
     from cndp_amd import native as N
     from oracle import oracle as O
     fr = state["frames"]
-    if fr.slab.numel() > max_slab_bytes:
+    chunked = fr.slab.numel() > max_slab_bytes
+    if chunked and fr.offsets is not None:
         return None
     t0 = time.perf_counter()
     cl, out = state["cl"], state["out"]
@@ -244,22 +245,39 @@ def parity_full(state, max_slab_bytes: int = 8 << 30):
     o["bins"] = torch.zeros_like(out["bins"])
     cl.classify(fr, state["mode"], out=o)
     torch.cuda.synchronize()
-    slab = fr.slab.cpu().numpy()
-    if fr.offsets is not None:
-        ref = O.classify(state["mode"], slab, fr.n, offsets=fr.offsets.cpu().numpy().astype(np.uint64),
-                         data_off=fr.data_off, **kw)
+    keys = [(k, dt) for k, dt in (("nh", np.uint32), ("hash", np.uint32), ("queue", np.uint16), ("edge", np.uint8))
+            if o.get(k) is not None]
+    diff = {k: 0 for k, _ in keys}
+    if not chunked:
+        slab = fr.slab.cpu().numpy()
+        if fr.offsets is not None:
+            ref = O.classify(state["mode"], slab, fr.n, offsets=fr.offsets.cpu().numpy().astype(np.uint64),
+                             data_off=fr.data_off, **kw)
+        else:
+            ref = O.classify(state["mode"], slab, fr.n, stride=fr.stride, data_off=fr.data_off, **kw)
+        del slab
+        for key, dt in keys:
+            diff[key] = int(np.sum(o[key].cpu().numpy().view(dt) != ref[key]))
+        ref_bins = ref["bins"]
     else:
-        ref = O.classify(state["mode"], slab, fr.n, stride=fr.stride, data_off=fr.data_off, **kw)
-    del slab
-    diff = {}
-    for key, dt in (("nh", np.uint32), ("hash", np.uint32), ("queue", np.uint16), ("edge", np.uint8),
-                    ("bins", np.uint64)):
-        if o.get(key) is None:
-            continue
-        g = o[key].cpu().numpy().view(dt)
-        diff[key] = int(np.sum(g != ref[key]))
+        # C5: the shard in 1M-frame pieces (1.5 GiB of slab each), the ptype
+        # node's state carried from piece to piece as the node carries it
+        # across bursts -- the same walk as one call
+        state16 = np.zeros(1, np.uint16)
+        ref_bins = None
+        step = 1 << 20
+        for c0 in range(0, fr.n, step):
+            c1 = min(fr.n, c0 + step)
+            slab = fr.slab[c0 * fr.stride:c1 * fr.stride].cpu().numpy()
+            ref = O.classify(state["mode"], slab, c1 - c0, stride=fr.stride, data_off=fr.data_off,
+                             spec_state=state16 if cnet else None, **kw)
+            del slab
+            for key, dt in keys:
+                diff[key] += int(np.sum(o[key][c0:c1].cpu().numpy().view(dt) != ref[key]))
+            ref_bins = ref["bins"] if ref_bins is None else ref_bins + ref["bins"]
+    diff["bins"] = int(np.sum(o["bins"].cpu().numpy().view(np.uint64) != ref_bins))
     return {"frames": fr.n, "equal": all(v == 0 for v in diff.values()), "mismatches": diff,
-            "seconds": round(time.perf_counter() - t0, 1)}
+            "pieces": -(-fr.n // (1 << 20)) if chunked else 1, "seconds": round(time.perf_counter() - t0, 1)}
 
 
 def host_cpus():
