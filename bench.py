@@ -651,9 +651,13 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         l3[name + "_Mpps"] = round(float(np.median(v)), 2) if min(v) > 0 else None
     l3["ab_rounds"] = {k: [round(x, 2) for x in v] for k, v in ab.items()}
     L.cndp_node_gpu_umem_reset()
+    gpu_priv1 = pool.hdr["udata64"].copy()  # node_mbuf_priv1 as the GPU node left it
     fib = NodeFib()
     t24, t8 = (x.copy() for x in fib.image())
+    pool.hdr["udata64"] = 0
     O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, 1)
+    # every mbuf's priv1 from the GPU node against the CPU node loop's
+    l3["results_equal_cpu_node"] = bool(np.array_equal(gpu_priv1, pool.hdr["udata64"]))
     t = O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
     l3["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
     t = O.rx_ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
@@ -719,6 +723,10 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     HC.harness_eth_rx_port(0, 0)
 
     gids = iter(range(40, 80))
+    # the fields eth_rx / ptype / ip4_input / ip6_input write, after the GPU
+    # node's first pass from a fresh graph (ptype node state 0)
+    cnet_fields = ("packet_type", "ol_flags", "tx_offload", "lport", "data_off", "data_len")
+    snap = {}
 
     def cnet_node(zc, flags):
         gid = next(gids)
@@ -736,6 +744,8 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
             if dt < 0:
                 t = -1.0
                 break
+            if p == 0 and not snap:
+                snap.update({f: pool.hdr[f].copy() for f in cnet_fields})
             t += dt if p else 0.0
         HC.harness_graph_destroy()
         os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
@@ -767,6 +777,9 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     cpus, _, _ = host_cpus()
     rx_len = hdr0["data_len"].copy()
     O.cnet_chain(ptrs, nc, rx_len, int(hdr0["data_off"][0]), t4c, t6c, cpus=cpus[:1])
+    # every field the replaced nodes write, GPU eth_rx node (first pass) against the CPU chain
+    cn["results_equal_cpu_chain"] = bool(snap) and all(np.array_equal(snap[f], pool.hdr[f]) for f in cnet_fields)
+    pool.hdr[:] = hdr0
     t = O.cnet_chain(ptrs, nc, rx_len, int(hdr0["data_off"][0]), t4c, t6c, iters=passes, cpus=cpus[:1])
     pool.hdr[:] = hdr0
     cn["cpu_1core_Mpps"] = round(nc * passes / t / 1e6, 2)
