@@ -875,8 +875,17 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
                 t = -1.0
                 break
             t += dt if p else 0.0
+        if key == "gpu_zero_copy":  # what the receive chain wrote into every mbuf
+            snap = (pool.hdr["packet_type"].copy(), pool.hdr["udata64"].copy())
         HR.harness_graph_destroy()
         out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+    # the same three nodes' loops on the CPU over the same (not yet rewritten)
+    # frames: every mbuf's packet_type and node_mbuf_priv1 compared
+    pool.hdr[:] = hdr0
+    t24c, t8c = (x.copy() for x in NodeFib().image())
+    O.l3rx_chain_mbufs(ptrs, n, (t24c, t8c))
+    out["results_equal_cpu_chain"] = bool(np.array_equal(snap[0], pool.hdr["packet_type"]) and
+                                          np.array_equal(snap[1], pool.hdr["udata64"]))
     # the whole l3fwd-graph node chain on the device: the rx node chained into
     # the GPU ip4_rewrite node (four tx ports, 12-B MAC rewrites for the 64
     # next hops, as l3fwd-graph sets them up, fwd.c:160-201)
