@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 session O: node tests again, torch interop check, C4 / C5 on
-# uncached / fine-grained frame slabs (interleaved A/B).
+# Round-4 session R: FIB churn with / without the device painter; probe8 C5/C4
+# window reads at 4, 6 and 8 waves a SIMD.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-TAG=${1:-r04o}
+TAG=${1:-r04r}
 step() { # name timeout cmd...
     local name=$1 to=$2; shift 2
     echo "[$(date +%T)] >>> $name"
@@ -18,7 +18,7 @@ step() { # name timeout cmd...
     fi
     return $rc
 }
-step pytest_nodes 400 python3 -u -m pytest tests/test_node_graph.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
-step cai 120 python3 -u tools/cai_check.py || exit 1
-step ab_unc 400 python3 -u tools/ab_uncached.py c4 c5 c3
+step churn_paint 200 python3 -u tools/fib_churn.py || exit 1
+CNDP_FIB_PAINT=0 step churn_copy 200 python3 -u tools/fib_churn.py || exit 1
+for b in 4 6 8; do step probe8_bpc$b 200 ./tools/probe8 25 $b 1 || exit 1; done
 echo done

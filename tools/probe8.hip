@@ -152,6 +152,8 @@ __global__ void k_fill(uint32_t *p, uint64_t n32)
 int main(int argc, char **argv)
 {
     const int lg = argc > 1 ? atoi(argv[1]) : 24;
+    const int bpc = argc > 2 ? atoi(argv[2]) : 8;     // 256-thread blocks per CU (8 = 8 waves a SIMD)
+    const int only_def = argc > 3 ? atoi(argv[3]) : 0; // 1: hipMalloc slabs, nt loads only
     const uint32_t n5 = 1u << lg, n4 = 1u << lg;
     const uint64_t stride = 1536;
     const uint64_t bytes5 = (uint64_t)n5 * stride;
@@ -178,13 +180,13 @@ int main(int argc, char **argv)
     int dev, ncu;
     CK(hipGetDevice(&dev));
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const int grid = ncu * 8;
+    const int grid = ncu * bpc;
     printf("C5 %u frames x %llu B (%.2f GB windows), C4 %u IMIX frames (%.2f GB slab), grid %d\n", n5,
            (unsigned long long)stride, n5 * 64.0 / 1e9, n4, tot / 1e9, grid);
     const unsigned flags[3] = {hipDeviceMallocDefault, hipDeviceMallocFinegrained, hipDeviceMallocUncached};
     uint32_t ref5 = 0, ref4 = 0;
     bool have = false;
-    for (int m = 0; m < 3; m++) {
+    for (int m = 0; m < (only_def ? 1 : 3); m++) {
         uint8_t *slab = nullptr;
         hipError_t e = m == 0 ? hipMalloc((void **)&slab, bytes) : hipExtMallocWithFlags((void **)&slab, bytes, flags[m]);
         if (e != hipSuccess) {
@@ -193,7 +195,7 @@ int main(int argc, char **argv)
         }
         hipLaunchKernelGGL(k_fill, dim3(ncu * 16), dim3(256), 0, 0, (uint32_t *)slab, bytes / 4);
         CK(hipDeviceSynchronize());
-        for (int ld = 0; ld < 3; ld++) {
+        for (int ld = only_def ? 1 : 0; ld < (only_def ? 2 : 3); ld++) {
             for (int rep = 0; rep < 2; rep++) {
                 CK(hipMemset(acc, 0, 8));
                 float t5 = ld == 0 ? run_c5<0>(slab, stride, n5, o4, o1, acc, grid, 10)
