@@ -1000,22 +1000,30 @@ def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
             tbl[nh]["rewrite_len"], tbl[nh]["tx_node"], tbl[nh]["enabled"] = 12, nh % 4 + 1, 1
             tbl[nh]["rewrite_data"][:] = np.frombuffer(data + bytes(44), np.uint8)
         H.harness_chain(1)
-        # the two queues' header forms (lookup / rewrite): both on the device
-        # (the nodes' defaults), the rewrite's on the host, both on the host;
-        # then staged
+        # zero-copy default: ip4_lookup's queue runs ip4_rewrite too
+        # (CNDP_MQ_F_REWRITE, mbufs straight to the pktdev_tx edges), lookup
+        # headers on the device / on the host; then the GPU ip4_rewrite node
+        # behind it (CNDP_GPU_LOOKUP_REWRITE=0) with the two queues' header
+        # forms (lookup / rewrite): both on the device (the nodes' defaults),
+        # the rewrite's on the host, both on the host; then staged
         D = N.CNDP_MQ_F_DEVICE_HEADERS
-        for gid, (key, zc, fl, frw) in enumerate((("gpu_zero_copy", True, D, D),
-                                                  ("gpu_zero_copy_rewrite_host_headers", True, D, 0),
-                                                  ("gpu_zero_copy_host_headers", True, 0, 0),
-                                                  ("gpu_staged", False, 0, 0))):
+        for gid, (key, zc, fl, frw, lrw) in enumerate((
+                ("gpu_zero_copy", True, D, D, 1),
+                ("gpu_zero_copy_lookup_host_headers", True, 0, D, 1),
+                ("gpu_zero_copy_rewrite_node", True, D, D, 0),
+                ("gpu_zero_copy_rewrite_node_rewrite_host_headers", True, D, 0, 0),
+                ("gpu_zero_copy_rewrite_node_host_headers", True, 0, 0, 0),
+                ("gpu_staged", False, 0, 0, 0))):
             L.cndp_node_gpu_umem_reset()
             if zc:
                 L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
             os.environ["CNDP_GPU_MQ_FLAGS"] = str(fl)
             os.environ["CNDP_GPU_RW_MQ_FLAGS"] = str(frw)
+            os.environ["CNDP_GPU_LOOKUP_REWRITE"] = str(lrw)
             assert H.harness_graph_create(30 + gid) == 0
             os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
             os.environ.pop("CNDP_GPU_RW_MQ_FLAGS", None)
+            os.environ.pop("CNDP_GPU_LOOKUP_REWRITE", None)
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
             H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
@@ -1029,6 +1037,9 @@ def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
         out["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
         out["cpu_chain"] = ("ip4_lookup's loop then ip4_rewrite_node_process per 256-burst over the same "
                             "mbufs, one core (oracle/oracle.c orc_l3fwd_nodes_mbufs)")
+        out["gpu_paths"] = ("gpu_zero_copy*: ip4_rewrite run by ip4_lookup's queue (CNDP_MQ_F_REWRITE, "
+                            "the default with registered UMEM); *_rewrite_node*: the GPU ip4_rewrite node "
+                            "behind the GPU ip4_lookup node (CNDP_GPU_LOOKUP_REWRITE=0)")
     finally:
         H.harness_chain(0)
         H.harness_edges_reset()

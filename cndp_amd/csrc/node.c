@@ -92,7 +92,7 @@ static int rw_alloc(void)
     return 0;
 }
 
-#define RW_HOOKS_MAX 4
+#define RW_HOOKS_MAX 16 /* one per GPU node module and harness library loaded in a process */
 static int (*rw_next_hook[RW_HOOKS_MAX])(uint16_t port_id, uint16_t next_index);
 
 void cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index))

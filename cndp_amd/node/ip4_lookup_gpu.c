@@ -31,6 +31,21 @@
  *   the graph's ports may use different pools), else staged.  An mbuf the
  *   queue cannot reach (outside every registered UMEM) leaves by pkt_drop.
  *
+ * With the frames in registered UMEM (zero-copy) the queue also runs
+ * ip4_rewrite (CNDP_MQ_F_REWRITE), as pktdev_rx_gpu.c does for the receive
+ * chain: the rewrite data, TTL and checksum go into each frame the lookup
+ * sends to ip4_rewrite, and the mbuf leaves directly on its next hop's
+ * pktdev_tx edge.  For that both nodes here carry, after ip4_lookup's two
+ * edges, a copy of ip4_rewrite's edge list (pkt_drop, pktdev_tx-<port>...),
+ * kept by a hook on ip4_rewrite_set_next (pktdev_ctrl.c:81-86).  ip4_rewrite
+ * stays registered and idle and gets the stats of the mbufs it stands for.
+ * Its checksum rule (4-wide loop for the first count & ~3 mbufs it gets, the
+ * tail loop's for the rest, ip4_rewrite.c:97-110, :209-216) is applied per
+ * process() call of this node, as when ip4_rewrite gets the stream this call
+ * sends it -- per 256-mbuf piece (CNE_GRAPH_BURST_SIZE) of a call larger than
+ * that.  CNDP_GPU_LOOKUP_REWRITE=0 keeps ip4_rewrite as the next node (staged
+ * frames always do).
+ *
  * One GPU context and queue per graph (graphs are per lcore, cne_graph_worker.h
  * notes a graph is not shared between threads); contexts share the node FIB,
  * whose device mirror libcndp_gpu keeps on one device per process.
@@ -40,6 +55,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <cne_graph.h>
 #include <cne_graph_worker.h>
@@ -52,6 +68,9 @@
 #define GPU_POLL_MAX 256
 #define GPU_GRAPHS_MAX 256 /* graph ids this module tracks */
 #define DRAIN_NODE_NAME "ip4_lookup_gpu_drain"
+/* ip4_lookup's two edges, then (with the rewrite on the device) ip4_rewrite's */
+#define LOOKUP_GPU_NEXT_TX0 CNE_NODE_IP4_LOOKUP_NEXT_MAX
+#define LOOKUP_EDGES_MAX GPU_NODE_EDGES_MAX
 
 /* ip4_lookup.c:38: the rewrite node reads priv1 at this offset */
 int node_mbuf_priv1_dynfield_offset = -1;
@@ -60,6 +79,10 @@ struct gpu_graph_state {
     int refs; /* the two nodes of one graph */
     cndp_gpu_ctx_t *gpu;
     cndp_gpu_mq_t *q;
+    struct cne_node *st_rewrite; /* fused: the idle ip4_rewrite, credited in its stats */
+    int fused;                   /* CNDP_MQ_F_REWRITE: the queue's edges are ip4_rewrite's */
+    int tx0_drop;                /* fused and ip4_rewrite's edge 0 is pkt_drop */
+    uint16_t nb_edges;           /* the nodes' edges at graph create */
     void *done[GPU_POLL_MAX];
     uint16_t edge[GPU_POLL_MAX];
     void *grp[GPU_POLL_MAX]; /* a poll's mbufs grouped by edge */
@@ -88,8 +111,9 @@ static void state_put(struct gpu_graph_state *st)
     }
 }
 
-/* the state of this graph, created by whichever of the two nodes starts first */
-static struct gpu_graph_state *state_get(const struct cne_graph *graph)
+/* the state of this graph, created by whichever of the two nodes starts first
+ * (both carry the same edges) */
+static struct gpu_graph_state *state_get(const struct cne_graph *graph, const struct cne_node *node)
 {
     const unsigned gid = graph->id;
     if (gid >= GPU_GRAPHS_MAX)
@@ -125,6 +149,23 @@ static struct gpu_graph_state *state_get(const struct cne_graph *graph)
     for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)
         if (cndp_gpu_host_register(st->gpu, umem, ulen, NULL) == 0 && !conf.umem)
             conf.umem = umem;
+    const cne_edge_t ne = cne_node_edge_count(node->id);
+    st->nb_edges = ne == CNE_EDGE_ID_INVALID ? CNE_NODE_IP4_LOOKUP_NEXT_MAX
+                   : ne > LOOKUP_EDGES_MAX   ? LOOKUP_EDGES_MAX
+                                             : (uint16_t)ne;
+    /* ip4_rewrite on the device when the frames are in place and the nodes
+     * carry ip4_rewrite's edges (ip4_rewrite_set_next ran, lk_mirror_edges) */
+    st->fused = conf.umem && st->nb_edges > LOOKUP_GPU_NEXT_TX0 && env_u32("CNDP_GPU_LOOKUP_REWRITE", 1);
+    if (st->fused) {
+        conf.flags |= CNDP_MQ_F_REWRITE;
+        /* ip4_rewrite's edge 0 is pkt_drop (ip4_rewrite.c's next_nodes): its
+         * drops take ip4_lookup's own pkt_drop edge, one enqueue per poll */
+        char *names[LOOKUP_EDGES_MAX];
+        st->tx0_drop = ne <= LOOKUP_EDGES_MAX && cne_node_edge_get(node->id, names) == ne &&
+                       strcmp(names[LOOKUP_GPU_NEXT_TX0], "pkt_drop") == 0;
+        /* graph.c:291-295 lays the graph's nodes out before their init runs */
+        st->st_rewrite = cne_graph_get_node_by_name(graph, "ip4_rewrite");
+    }
     if (cndp_gpu_mq_create(st->gpu, &conf, &st->q) < 0)
         goto fail;
     gs_by_graph[gid] = st;
@@ -157,13 +198,32 @@ static uint16_t gpu_drain(struct cne_graph *graph, struct cne_node *node, struct
         const int k = cndp_gpu_mq_poll(st->q, st->done, st->edge, GPU_POLL_MAX);
         if (k <= 0)
             break;
-        /* a FIB value naming no edge of this node (ip4_lookup.c:150 takes
-         * val >> 16 as is) and an mbuf the queue could not reach
-         * (CNDP_MQ_EDGE_NONE) leave by pkt_drop */
-        for (int i = 0; i < k; i++)
-            if (st->edge[i] >= CNE_NODE_IP4_LOOKUP_NEXT_MAX)
-                st->edge[i] = CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP;
-        gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k, CNE_NODE_IP4_LOOKUP_NEXT_MAX, st->grp);
+        if (st->fused) {
+            /* ip4_rewrite's tx_node: that edge of the copied list (past it:
+             * pkt_drop); ip4_lookup's drops and an unreachable mbuf: pkt_drop */
+            uint16_t nrw = 0;
+            for (int i = 0; i < k; i++) {
+                const uint16_t e = st->edge[i];
+                nrw = (uint16_t)(nrw + (e < CNDP_MQ_EDGE_LOOKUP_DROP));
+                st->edge[i] = e < CNDP_MQ_EDGE_LOOKUP_DROP && LOOKUP_GPU_NEXT_TX0 + e < st->nb_edges &&
+                                      !(e == 0 && st->tx0_drop)
+                                  ? (uint16_t)(LOOKUP_GPU_NEXT_TX0 + e)
+                                  : CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP;
+            }
+            if (st->st_rewrite && nrw && cne_graph_has_stats_feature()) {
+                st->st_rewrite->total_calls++;
+                st->st_rewrite->total_objs += nrw;
+            }
+        } else {
+            /* a FIB value naming no edge of this node (ip4_lookup.c:150 takes
+             * val >> 16 as is) and an mbuf the queue could not reach
+             * (CNDP_MQ_EDGE_NONE) leave by pkt_drop */
+            for (int i = 0; i < k; i++)
+                if (st->edge[i] >= CNE_NODE_IP4_LOOKUP_NEXT_MAX)
+                    st->edge[i] = CNE_NODE_IP4_LOOKUP_NEXT_PKT_DROP;
+        }
+        gpu_enqueue_by_edge(graph, node, st->done, st->edge, (uint16_t)k,
+                            st->fused ? st->nb_edges : CNE_NODE_IP4_LOOKUP_NEXT_MAX, st->grp);
         total = (uint16_t)(total + k);
         if (k < GPU_POLL_MAX)
             break;
@@ -197,7 +257,7 @@ static uint16_t ip4_lookup_gpu_process(struct cne_graph *graph, struct cne_node 
 static int ip4_lookup_gpu_init(const struct cne_graph *graph, struct cne_node *node)
 {
     node_mbuf_priv1_dynfield_offset = offsetof(pktmbuf_t, udata64); /* ip4_lookup.c:322 */
-    struct gpu_graph_state *st = state_get(graph);
+    struct gpu_graph_state *st = state_get(graph, node);
     if (!st)
         return -ENODEV; /* no CPU path behind this node: fail loudly at graph create */
     GPU_NODE_STATE(node) = st;
@@ -236,7 +296,7 @@ static uint16_t ip4_lookup_gpu_drain_process(struct cne_graph *graph, struct cne
 
 static int ip4_lookup_gpu_drain_init(const struct cne_graph *graph, struct cne_node *node)
 {
-    struct gpu_graph_state *st = state_get(graph);
+    struct gpu_graph_state *st = state_get(graph, node);
     if (!st)
         return -ENODEV;
     GPU_NODE_STATE(node) = st;
@@ -257,3 +317,33 @@ static struct cne_node_register ip4_lookup_gpu_drain_node = {
         },
 };
 CNE_NODE_REGISTER(ip4_lookup_gpu_drain_node);
+
+/* ip4_rewrite_set_next's hook (pktdev_ctrl.c:81-86 calls it right after it
+ * added a port's pktdev_tx edge to ip4_rewrite): both nodes take ip4_rewrite's
+ * edge list after ip4_lookup's two, so the tx_node the queue returns names the
+ * same next node here */
+static int lk_mirror_edges(uint16_t port_id, uint16_t next_index)
+{
+    (void)port_id;
+    (void)next_index;
+    const cne_node_t rw = cne_node_from_name("ip4_rewrite");
+    if (rw == CNE_NODE_ID_INVALID)
+        return 0; /* no ip4_rewrite node in this build: nothing to mirror */
+    char *names[LOOKUP_EDGES_MAX]; /* cne_node_edge_get hands out the node's own name pointers */
+    const cne_edge_t n = cne_node_edge_count(rw);
+    if (n == CNE_EDGE_ID_INVALID || n > LOOKUP_EDGES_MAX - LOOKUP_GPU_NEXT_TX0)
+        return -EINVAL;
+    if (cne_node_edge_get(rw, names) != n)
+        return -EINVAL;
+    if (cne_node_edge_update(ip4_lookup_node.id, LOOKUP_GPU_NEXT_TX0, (const char **)names, n) ==
+            CNE_EDGE_ID_INVALID ||
+        cne_node_edge_update(ip4_lookup_gpu_drain_node.id, LOOKUP_GPU_NEXT_TX0, (const char **)names, n) ==
+            CNE_EDGE_ID_INVALID)
+        return -EINVAL;
+    return 0;
+}
+
+__attribute__((constructor)) static void lk_gpu_hook(void)
+{
+    cndp_node_ip4_rewrite_next_hook(lk_mirror_edges);
+}

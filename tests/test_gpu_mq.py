@@ -706,15 +706,18 @@ def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
     assert set(np.unique(edges).tolist()) == {0, 1, 2, 3, 4}
 
 
+@pytest.mark.parametrize("rx_parse", [True, False], ids=["rx_chain", "lookup"])
 @pytest.mark.parametrize("headers", ["host", "device"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
-def test_mq_l3fwd_fused(l3, gpu, headers, kind):
+def test_mq_l3fwd_fused(l3, gpu, headers, kind, rx_parse):
     """CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE: l3fwd-graph's pktdev_rx soft
     parse, pkt_cls, ip4_lookup and ip4_rewrite in one queue pass, ip4_rewrite
     per submitted burst as when it gets that burst's stream in one call -- byte
     for byte against the oracle's node loops over the same bursts (checksums
     0xFFFE / 0xFFFF and high-bit cksum words seeded, where the 4-wide and
-    tail rules differ), edges = the next hop's tx_node, LOOKUP_DROP, CLS_DROP."""
+    tail rules differ), edges = the next hop's tx_node, LOOKUP_DROP, CLS_DROP.
+    lookup: CNDP_MQ_F_REWRITE alone (the GPU ip4_lookup node's fused mode):
+    every mbuf through ip4_lookup's loop, packet_type untouched."""
     cl, fib, t4 = l3
     tbl = _rewrite_setup(cl, 41)
     n = 12000
@@ -729,7 +732,8 @@ def test_mq_l3fwd_fused(l3, gpu, headers, kind):
         for sel, lo in ((np.arange(n) % 53 == 5, 0xFE), (np.arange(n) % 59 == 7, 0xFF)):
             p.mem[d[sel] + 24] = lo
             p.mem[d[sel] + 25] = 0xFF
-    flags = N.CNDP_MQ_F_RX_PARSE | N.CNDP_MQ_F_REWRITE | (N.CNDP_MQ_F_DEVICE_HEADERS if headers == "device" else 0)
+    flags = ((N.CNDP_MQ_F_RX_PARSE if rx_parse else 0) | N.CNDP_MQ_F_REWRITE |
+             (N.CNDP_MQ_F_DEVICE_HEADERS if headers == "device" else 0))
     bursts = _bursts(n, 43, kind)
     order = np.random.default_rng(44).permutation(n)
     cl.host_register(gp.mem)
@@ -747,7 +751,15 @@ def test_mq_l3fwd_fused(l3, gpu, headers, kind):
     for b in bursts:
         idx = order[pos:pos + b]
         e = np.zeros(b, np.uint16)
-        O.l3rx_chain_mbufs(op.ptrs(idx), b, t4, burst=256, edges=e)
+        if rx_parse:
+            O.l3rx_chain_mbufs(op.ptrs(idx), b, t4, burst=256, edges=e)
+        else:  # ip4_lookup's loop over every mbuf; its edge = FIB value >> 16
+            O.ip4_lookup_mbufs(op.ptrs(idx), b, t4, burst=256)
+            d = op.data_pos()[idx].astype(np.int64)
+            dip = np.zeros(b, np.uint32)
+            for k in range(4):
+                dip = (dip << 8) | op.mem[d + 30 + k].astype(np.uint32)
+            e = (O.dir24_8_lookup(t4[0], t4[1], dip) >> 16).astype(np.uint16)
         rw = idx[e == 0]
         tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
         eb = np.where(e == N.CNDP_MQ_EDGE_CLS_DROP, e, N.CNDP_MQ_EDGE_LOOKUP_DROP).astype(np.uint16)
@@ -759,7 +771,10 @@ def test_mq_l3fwd_fused(l3, gpu, headers, kind):
     assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
     bad = np.nonzero(np.any(gp.mem.reshape(n, -1)[:, HDR:] != op.mem.reshape(n, -1)[:, HDR:], axis=1))[0]
     assert bad.size == 0, f"{bad.size} frames differ from the oracle's, first {bad[:4]}"
-    assert {N.CNDP_MQ_EDGE_CLS_DROP, N.CNDP_MQ_EDGE_LOOKUP_DROP, 0, 1, 2, 3, 4} <= set(np.unique(edges).tolist())
+    seen = {N.CNDP_MQ_EDGE_LOOKUP_DROP, 0, 1, 2, 3, 4} | ({N.CNDP_MQ_EDGE_CLS_DROP} if rx_parse else set())
+    assert seen <= set(np.unique(edges).tolist())
+    if not rx_parse:
+        assert N.CNDP_MQ_EDGE_CLS_DROP not in set(np.unique(edges).tolist())
 
 
 @pytest.mark.parametrize("flags", [0, N.CNDP_MQ_F_DEVICE_HEADERS], ids=["host_headers", "device_headers"])

@@ -530,6 +530,32 @@ def test_rewrite_node_registry():
         L.cndp_node_ip4_rewrite_reset()
 
 
+def test_rewrite_edge_mirrors_every_library():
+    """Both harness libraries loaded in one process (five hooks on
+    ip4_rewrite_set_next: each library's ip4_lookup and ip4_rewrite, the
+    receive node): every hook runs, so in each library ip4_rewrite's drain
+    node and ip4_lookup (and its drain node) carry ip4_rewrite's edges after
+    their own -- the edge indices the queues return mean the same there."""
+    Hn, Hr = _rw_harness(), _rx_harness()
+    L = N.lib()
+    L.cndp_node_ip4_rewrite_reset()
+    try:
+        for H in (Hn, Hr):
+            _eth_config(H, L, (0, 3))
+        want = [b"pkt_drop", b"pktdev_tx-0", b"pktdev_tx-3"]
+        for H in (Hn, Hr):
+            ids = _node_ids(H)
+            assert _edges_of(H, ids["ip4_rewrite"]) == want
+            assert _edges_of(H, ids["ip4_rewrite_gpu_drain"]) == want
+            for nm in ("ip4_lookup", "ip4_lookup_gpu_drain"):
+                assert _edges_of(H, ids[nm]) == [b"ip4_rewrite", b"pkt_drop"] + want
+        assert _edges_of(Hr, _node_ids(Hr)["pktdev_rx"]) == PKTDEV_RX_EDGES + want
+    finally:
+        for H in (Hn, Hr):
+            H.harness_edges_reset()
+        L.cndp_node_ip4_rewrite_reset()
+
+
 def _rw_table(L, seed, ports):
     """Next hops through cne_node_ip4_rewrite_add (the process-global table the
     GPU node follows) and the oracle's copy of it."""
@@ -624,13 +650,20 @@ def test_rewrite_node_graph_walk(gpu, zero_copy):
 
 
 @pytest.mark.gpu
-def test_l3fwd_graph_chain(gpu):
+@pytest.mark.parametrize("fused", [True, False], ids=["rewrite_in_lookup", "rewrite_node"])
+def test_l3fwd_graph_chain(gpu, fused):
     """The l3fwd-graph chain with both GPU nodes, walked as cne_graph_walk
     runs it (ip4_lookup's enqueues fill ip4_rewrite's stream, which runs in
     the same walk): every mbuf ends at pkt_drop or its next hop's tx edge with
-    priv1 and the rewritten frame of the reference chain (checksums where the
-    4-wide and tail rules agree, i.e. not 0xFFFE / 0xFFFF, whose rule depends
-    on the stream split)."""
+    priv1 and the rewritten frame of the reference chain.  rewrite_in_lookup
+    (the zero-copy default): ip4_lookup's queue runs ip4_rewrite itself
+    (CNDP_MQ_F_REWRITE) and its mbufs leave on the mirrored pktdev_tx edges,
+    byte for byte the reference pair per 256-mbuf walk (the 4-wide / tail
+    checksum rule of the stream each call sends ip4_rewrite), in order per
+    edge, with ip4_rewrite's stats credited.  rewrite_node
+    (CNDP_GPU_LOOKUP_REWRITE=0): the GPU ip4_rewrite node gets the stream,
+    checked where the two checksum rules agree (not 0xFFFE / 0xFFFF, whose
+    rule depends on the stream split)."""
     from cndp_amd import pktgen
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
@@ -643,12 +676,22 @@ def test_l3fwd_graph_chain(gpu):
     gp, op = MbufPool(n), MbufPool(n)
     for p in (gp, op):
         p.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=71))
+        # header checksums 0xFFFE / 0xFFFF, where the two rules differ
+        d = p.data_pos().astype(np.int64)
+        for sel, lo in ((np.arange(n) % 97 == 5, 0xFE), (np.arange(n) % 89 == 7, 0xFF)):
+            p.mem[d[sel] + 24] = lo
+            p.mem[d[sel] + 25] = 0xFF
     NodeFib.fini()
     L.cndp_node_ip4_rewrite_reset()
     L.cndp_node_gpu_umem_reset()
     assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
     os.environ["CNDP_GPU_BATCH"] = "4096"
+    if not fused:
+        os.environ["CNDP_GPU_LOOKUP_REWRITE"] = "0"
     routes = pktgen.l3fwd_routes()
+    H.harness_node_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    calls, objs = ctypes.c_uint64(), ctypes.c_uint64()
     try:
         _eth_config(H, L, ports)
         tbl = _rw_table(L, 72, ports)
@@ -662,7 +705,11 @@ def test_l3fwd_graph_chain(gpu):
         got = np.full(n, -1, np.int64)
         for k, nm in enumerate(names):
             m = H.harness_take_edge(nm, buf, n)
-            got[gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))] = k
+            idx = gp.index_of(np.array([x or 0 for x in buf[:m]], np.uint64))
+            if fused:
+                assert np.all(np.diff(idx) > 0), f"{nm}: out of order"
+            got[idx] = k
+        assert H.harness_node_stats(b"ip4_rewrite", ctypes.byref(calls), ctypes.byref(objs)) == 0
     finally:
         H.harness_chain(0)
         H.harness_graph_destroy()
@@ -670,6 +717,7 @@ def test_l3fwd_graph_chain(gpu):
         L.cndp_node_ip4_rewrite_reset()
         L.cndp_node_gpu_umem_reset()
         os.environ.pop("CNDP_GPU_BATCH", None)
+        os.environ.pop("CNDP_GPU_LOOKUP_REWRITE", None)
     # the reference chain on the oracle's copy: ip4_lookup then ip4_rewrite
     t24, t8 = O.dir24_8_build(list(routes), N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
     d = op.data_pos().astype(np.int64)
@@ -681,13 +729,19 @@ def test_l3fwd_graph_chain(gpu):
     op.hdr["udata64"] = (val & 0xFFFF) | (op.mem[d + 22].astype(np.uint64) << 16) | (ck << 32)
     assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
     rw = np.nonzero((val >> 16) == 0)[0]
-    tx = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
     want = np.zeros(n, np.int64)
-    want[rw] = tx
+    if fused:  # ip4_rewrite per walk: the stream each 256-mbuf ip4_lookup call sends it
+        for b in range(0, n, 256):
+            sel = rw[(rw >= b) & (rw < b + 256)]
+            want[sel] = O.ip4_rewrite_node(op.ptrs(sel), len(sel), tbl)
+        ok = np.ones(n, bool)
+        assert calls.value > 0 and objs.value == rw.size
+    else:
+        want[rw] = O.ip4_rewrite_node(op.ptrs(rw), len(rw), tbl)
+        ok = (ck != 0xFFFE) & (ck != 0xFFFF)
     assert np.array_equal(got, want)
-    ok = (ck != 0xFFFE) & (ck != 0xFFFF)
     diff = np.any(gp.mem.reshape(n, -1)[:, 64:] != op.mem.reshape(n, -1)[:, 64:], axis=1)  # buffers (buf_addr differs)
-    assert not np.any(diff & ok)
+    assert not np.any(diff & ok), f"{int((diff & ok).sum())} frames differ"
     assert rw.size > n // 2 and (got == 0).sum() > 0
     NodeFib.fini()
 
