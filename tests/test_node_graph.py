@@ -650,8 +650,9 @@ def test_rewrite_node_graph_walk(gpu, zero_copy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fused", [True, False], ids=["rewrite_in_lookup", "rewrite_node"])
-def test_l3fwd_graph_chain(gpu, fused):
+@pytest.mark.parametrize("fused,burst", [(True, 256), (True, 600), (False, 256)],
+                         ids=["rewrite_in_lookup", "rewrite_in_lookup_600", "rewrite_node"])
+def test_l3fwd_graph_chain(gpu, fused, burst):
     """The l3fwd-graph chain with both GPU nodes, walked as cne_graph_walk
     runs it (ip4_lookup's enqueues fill ip4_rewrite's stream, which runs in
     the same walk): every mbuf ends at pkt_drop or its next hop's tx edge with
@@ -663,7 +664,9 @@ def test_l3fwd_graph_chain(gpu, fused):
     edge, with ip4_rewrite's stats credited.  rewrite_node
     (CNDP_GPU_LOOKUP_REWRITE=0): the GPU ip4_rewrite node gets the stream,
     checked where the two checksum rules agree (not 0xFFFE / 0xFFFF, whose
-    rule depends on the stream split)."""
+    rule depends on the stream split).  _600: 600-mbuf process() calls (a
+    graph whose pkt_cls gathered several ports' bursts), whose rewrite rule
+    applies per 256-mbuf piece of the call."""
     from cndp_amd import pktgen
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
@@ -699,7 +702,7 @@ def test_l3fwd_graph_chain(gpu, fused):
         assert H.harness_graph_create(12) == 0
         for ip, d, nh in routes:
             assert cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
-        assert H.harness_drive(b"ip4_lookup", gp.ptrs(np.arange(n)), n, 256, 1) >= 0
+        assert H.harness_drive(b"ip4_lookup", gp.ptrs(np.arange(n)), n, burst, 1) >= 0
         names = [b"pkt_drop"] + [f"pktdev_tx-{p}".encode() for p in ports]
         buf = (ctypes.c_void_p * n)()
         got = np.full(n, -1, np.int64)
@@ -730,10 +733,11 @@ def test_l3fwd_graph_chain(gpu, fused):
     assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
     rw = np.nonzero((val >> 16) == 0)[0]
     want = np.zeros(n, np.int64)
-    if fused:  # ip4_rewrite per walk: the stream each 256-mbuf ip4_lookup call sends it
-        for b in range(0, n, 256):
-            sel = rw[(rw >= b) & (rw < b + 256)]
-            want[sel] = O.ip4_rewrite_node(op.ptrs(sel), len(sel), tbl)
+    if fused:  # ip4_rewrite per walk: the stream each ip4_lookup call (256-mbuf piece) sends it
+        for c in range(0, n, burst):
+            for b in range(c, min(c + burst, n), 256):
+                sel = rw[(rw >= b) & (rw < min(b + 256, c + burst))]
+                want[sel] = O.ip4_rewrite_node(op.ptrs(sel), len(sel), tbl)
         ok = np.ones(n, bool)
         assert calls.value > 0 and objs.value == rw.size
     else:
