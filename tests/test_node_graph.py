@@ -750,6 +750,94 @@ def test_l3fwd_graph_chain(gpu, fused, burst):
     NodeFib.fini()
 
 
+@pytest.mark.gpu
+def test_l3fwd_fused_unreachable_mbufs(gpu):
+    """ip4_lookup with ip4_rewrite in its queue, mbufs of an unregistered pool
+    mixed into its calls: those leave by pkt_drop untouched (header, priv1,
+    frame), are not counted for ip4_rewrite, and do not shift the checksum
+    rule of the others -- each call's reachable mbufs sent to ip4_rewrite are
+    rewritten as ip4_rewrite would over that stream."""
+    from cndp_amd import pktgen
+    from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
+    from cndp_amd.mbuf import MbufPool
+    from oracle import oracle as O
+    H = _rw_harness()
+    H.harness_chain.argtypes = [ctypes.c_int]
+    L = N.lib()
+    ports = (0, 1, 2, 3)
+    n, m = 6000, 600
+    gp, op, xp = MbufPool(n), MbufPool(n), MbufPool(m)
+    for p in (gp, op):
+        p.fill(pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), seed=73))
+        p.hdr["udata64"] = 0x77
+        d = p.data_pos().astype(np.int64)
+        for sel, lo in ((np.arange(n) % 31 == 5, 0xFE), (np.arange(n) % 37 == 7, 0xFF)):
+            p.mem[d[sel] + 24] = lo
+            p.mem[d[sel] + 25] = 0xFF
+    xp.fill(pktgen.packed_ipv4(m, routes=pktgen.l3fwd_routes(), seed=74))
+    xp.hdr["udata64"] = 0x99
+    x_before = xp.mem.copy()
+    # the call stream: every 11th slot an outsider
+    seq, gi, xi = [], 0, 0
+    while gi < n:
+        if len(seq) % 11 == 10 and xi < m:
+            seq.append(("x", xi)); xi += 1
+        else:
+            seq.append(("g", gi)); gi += 1
+    ptrs = (ctypes.c_void_p * len(seq))()
+    for k, (w, i) in enumerate(seq):
+        ptrs[k] = (gp if w == "g" else xp).addr(i)
+    NodeFib.fini()
+    L.cndp_node_ip4_rewrite_reset()
+    L.cndp_node_gpu_umem_reset()
+    assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
+    os.environ["CNDP_GPU_BATCH"] = "2048"
+    routes = pktgen.l3fwd_routes()
+    try:
+        _eth_config(H, L, ports)
+        tbl = _rw_table(L, 75, ports)
+        H.harness_chain(1)
+        assert H.harness_graph_create(14) == 0
+        for ip, dd, nh in routes:
+            assert cne_node_ip4_route_add(ip, dd, nh, N.IP4_LOOKUP_NEXT_REWRITE) == 0
+        assert H.harness_drive(b"ip4_lookup", ptrs, len(seq), 256, 1) >= 0
+        names = [b"pkt_drop"] + [f"pktdev_tx-{p}".encode() for p in ports]
+        buf = (ctypes.c_void_p * len(seq))()
+        got = {}
+        for k, nm in enumerate(names):
+            for a in buf[:H.harness_take_edge(nm, buf, len(seq))]:
+                got[a] = k
+    finally:
+        H.harness_chain(0)
+        H.harness_graph_destroy()
+        H.harness_edges_reset()
+        L.cndp_node_ip4_rewrite_reset()
+        L.cndp_node_gpu_umem_reset()
+        os.environ.pop("CNDP_GPU_BATCH", None)
+    assert len(got) == len(seq)
+    assert all(got[xp.addr(i)] == 0 for i in range(xi))
+    assert np.array_equal(xp.mem, x_before)
+    # the reference pair over each 256-slot call's reachable mbufs
+    t24, t8 = O.dir24_8_build(list(routes), N.IP4_LOOKUP_NEXT_PKT_DROP << 16, 256)
+    d = op.data_pos().astype(np.int64)
+    dip = np.zeros(n, np.uint32)
+    for k in range(4):
+        dip = (dip << 8) | op.mem[d + 30 + k].astype(np.uint32)
+    val = O.dir24_8_lookup(t24, t8, dip).astype(np.uint64)
+    ck = op.mem[d + 24].astype(np.uint64) | (op.mem[d + 25].astype(np.uint64) << 8)
+    op.hdr["udata64"] = (val & 0xFFFF) | (op.mem[d + 22].astype(np.uint64) << 16) | (ck << 32)
+    assert np.array_equal(gp.hdr["udata64"], op.hdr["udata64"])
+    want = np.zeros(n, np.int64)
+    for c in range(0, len(seq), 256):
+        mine = np.array([i for w, i in seq[c:c + 256] if w == "g"], np.int64)
+        sel = mine[(val[mine] >> 16) == 0]
+        want[sel] = O.ip4_rewrite_node(op.ptrs(sel), len(sel), tbl)
+    assert np.array_equal(np.array([got[gp.addr(i)] for i in range(n)]), want)
+    diff = np.any(gp.mem.reshape(n, -1)[:, 64:] != op.mem.reshape(n, -1)[:, 64:], axis=1)
+    assert not np.any(diff), f"{int(diff.sum())} frames differ"
+    NodeFib.fini()
+
+
 # ---- the l3fwd-graph receive chain node (cndp_amd/node/pktdev_rx_gpu.c) ------
 RX_HARNESS = os.path.join(HERE, "node_harness", "librx_harness.so")
 PKTDEV_RX_EDGES = [b"ip4_lookup", b"pkt_cls", b"ip4_rewrite", b"pkt_drop"]
