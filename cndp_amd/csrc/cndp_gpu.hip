@@ -123,6 +123,7 @@ __device__ __forceinline__ uint32_t tz4(TP tab, uint32_t b, uint32_t x)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); // dword-aligned 16-B load
 typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 struct KArgs {
@@ -6231,7 +6232,9 @@ __device__ __forceinline__ uint32_t mq_rewrite_frame(uint8_t *p, uint32_t avail,
     uint32_t len = hdr & 0xffffu;
     len = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
     const uint32_t *src = (const uint32_t *)e->rewrite_data;
-    if (len <= avail && (((uintptr_t)p) & 3u) == 0 && (len & 3u) == 0) {
+    if (len == 12u && len <= avail && (((uintptr_t)p) & 3u) == 0) { // the usual MAC pair: one store
+        *(u32x3a4 *)p = (u32x3a4){src[0], src[1], src[2]};
+    } else if (len <= avail && (((uintptr_t)p) & 3u) == 0 && (len & 3u) == 0) {
         for (uint32_t k = 0; k < len / 4; k++)
             ((uint32_t *)p)[k] = src[k];
     } else {
@@ -6259,6 +6262,54 @@ __device__ __forceinline__ uint32_t mq_rewrite_frame(uint8_t *p, uint32_t avail,
     return hdr >> 16;
 }
 
+// the same with the frame's bytes 20..27 already in registers (the lookup's
+// one-load window, p 4-aligned, avail > 35): the new TTL and checksum go out
+// with the bytes around them unchanged as one 8-B store at p + 20, and the
+// usual 12-B rewrite data as one 12-B store -- two PCIe writes per frame
+// instead of five (each store of a lane is a transaction of its own in place)
+__device__ __forceinline__ uint32_t mq_rewrite_frame_w(uint8_t *p, uint32_t avail, uint64_t pv, bool tail,
+                                                       const struct cndp_rw_nh *rw, uint32_t w20, uint32_t w24)
+{
+    const uint32_t nh = (uint32_t)(pv & 0xffffu), ttl = (uint32_t)(pv >> 16) & 0xffffu;
+    const uint32_t ck32 = (uint32_t)(pv >> 32);
+    const bool set = nh < CNDP_RW_MAX_NH;
+    const struct cndp_rw_nh *e = &rw[set ? nh : 0u];
+    const uint32_t hdr = set ? *(const uint32_t *)e : 0u; // rewrite_len | tx_node << 16
+    uint32_t len = hdr & 0xffffu;
+    len = len < CNDP_RW_MAX_LEN ? len : CNDP_RW_MAX_LEN;
+    const uint32_t *src = (const uint32_t *)e->rewrite_data;
+    if (len == 12u) {
+        *(u32x3a4 *)p = (u32x3a4){src[0], src[1], src[2]};
+    } else if (len <= avail && (len & 3u) == 0) {
+        for (uint32_t k = 0; k < len / 4; k++)
+            ((uint32_t *)p)[k] = src[k];
+    } else {
+        for (uint32_t k = 0; k < len && k < avail; k++)
+            p[k] = e->rewrite_data[k];
+    }
+    uint32_t nck;
+    if (!tail) {
+        const uint32_t c32 = ck32 + 1u;
+        nck = ((c32 & 0xffffu) + (c32 >> 16)) & 0xffffu;
+    } else {
+        const uint32_t c16 = (ck32 + 1u) & 0xffffu;
+        nck = (c16 + (c16 >= 0xffffu ? 1u : 0u)) & 0xffffu;
+    }
+    // rewrite data longer than 20 bytes covers some of bytes 20..27: those
+    // bytes are the data's (the reference then writes TTL / checksum over it)
+    if (len > 20u) {
+        const uint32_t m20 = len >= 24u ? ~0u : (1u << (8u * (len - 20u))) - 1u;
+        w20 = (src[5] & m20) | (w20 & ~m20);
+        if (len > 24u) {
+            const uint32_t m24 = len >= 28u ? ~0u : (1u << (8u * (len - 24u))) - 1u;
+            w24 = (src[6] & m24) | (w24 & ~m24);
+        }
+    }
+    *(u32x2a4 *)(p + 20) = (u32x2a4){(w20 & 0xff00ffffu) | (((ttl - 1u) & 0xffu) << 16),
+                                     (w24 & 0xffff0000u) | nck};
+    return hdr >> 16;
+}
+
 // ip4_lookup_node_process_vec, per packet (ip4_lookup.c:108-154): dip at
 // mtod + 14 + 16, priv1 = {nh = val & 0xffff, ttl, hdr_checksum}, edge = val >> 16
 // one mbuf through the queue's ip4_lookup mode: the frame's readable
@@ -6274,10 +6325,12 @@ struct MqL3 {
     uint64_t priv1;
     uint8_t *frame;
     uint32_t favail;
+    uint32_t w20, w24; // zero-copy, one-load window: frame bytes 20..27 (else w20 = w24 = 0, q16 false)
+    bool q16;
 };
 __device__ __forceinline__ MqL3 mq_l3_one(const MqArgs &a, uint32_t i)
 {
-    MqL3 r{MQ_L3_NONE, 0u, 0ull, nullptr, 0u};
+    MqL3 r{MQ_L3_NONE, 0u, 0ull, nullptr, 0u, 0u, 0u, false};
     const uint64_t w = a.devhdr ? 0u : a.off[i];
     const uint8_t *p; // bytes 20..35 of the frame
     uint32_t avail;   // readable bytes from p
@@ -6343,6 +6396,9 @@ __device__ __forceinline__ MqL3 mq_l3_one(const MqArgs &a, uint32_t i)
         ttl = (q.x >> 16) & 0xffu;
         ck = q.y & 0xffffu;
         dip = bswap32(alignb(q.w, q.z, 2));
+        r.w20 = q.x;
+        r.w24 = q.y;
+        r.q16 = a.zc != 0;
     } else {
         ttl = gbyte(p, avail, 2);
         ck = gbyte(p, avail, 4) | (gbyte(p, avail, 5) << 8);
@@ -6384,7 +6440,7 @@ __global__ __launch_bounds__(MQ_L3_TPB) void k_mq_l3fwd_burst(MqArgs a)
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t i = i0 + t;
     const bool in = i < i1;
-    MqL3 r{MQ_L3_NONE, 0u, 0ull, nullptr, 0u};
+    MqL3 r{MQ_L3_NONE, 0u, 0ull, nullptr, 0u, 0u, 0u, false};
     if (in)
         r = mq_l3_one(a, i);
     const bool to_rw = in && r.st == MQ_L3_LOOKED && (r.val >> 16) == 0u; // CNE_NODE_IP4_LOOKUP_NEXT_REWRITE
@@ -6405,6 +6461,8 @@ __global__ __launch_bounds__(MQ_L3_TPB) void k_mq_l3fwd_burst(MqArgs a)
             e = CNDP_MQ_EDGE_CLS_DROP;
         else if (!to_rw)
             e = CNDP_MQ_EDGE_LOOKUP_DROP;
+        else if (r.q16)
+            e = mq_rewrite_frame_w(r.frame, r.favail, r.priv1, before >= (total & ~3u), a.rw, r.w20, r.w24);
         else
             e = mq_rewrite_frame(r.frame, r.favail, r.priv1, before >= (total & ~3u), a.rw);
         a.edges[i] = (uint16_t)e;

@@ -641,7 +641,7 @@ def _rewrite_setup(cl, seed):
     for nh in range(64):
         if nh % 9 == 8:
             continue   # unset entries: no data, edge 0
-        ln = int(rng.choice([12, 12, 12, 0, 14, 30, 56]))
+        ln = int(rng.choice([12, 12, 12, 0, 14, 22, 26, 30, 56]))
         data = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
         port = nh % 4
         assert cl.rewrite_add(nh, data, port) == 0

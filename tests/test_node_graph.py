@@ -565,7 +565,7 @@ def _rw_table(L, seed, ports):
     for nh in range(64):
         if nh % 9 == 8:
             continue
-        ln = int(rng.choice([12, 12, 12, 0, 14, 30, 56]))
+        ln = int(rng.choice([12, 12, 12, 0, 14, 22, 26, 30, 56]))
         data = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
         k = nh % len(ports)
         assert L.cne_node_ip4_rewrite_add(nh, ctypes.create_string_buffer(data, max(ln, 1)), ln, ports[k]) == 0
