@@ -886,6 +886,13 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
     O.l3rx_chain_mbufs(ptrs, n, (t24c, t8c))
     out["results_equal_cpu_chain"] = bool(np.array_equal(snap[0], pool.hdr["packet_type"]) and
                                           np.array_equal(snap[1], pool.hdr["udata64"]))
+    if not out["results_equal_cpu_chain"]:
+        bad_pt = np.nonzero(snap[0] != pool.hdr["packet_type"])[0]
+        bad_u = np.nonzero(snap[1] != pool.hdr["udata64"])[0]
+        out["results_mismatches"] = {"packet_type": int(bad_pt.size), "udata64": int(bad_u.size),
+                                     "first": [int(i) for i in np.union1d(bad_pt, bad_u)[:4]],
+                                     "gpu_udata64": [hex(int(snap[1][i])) for i in bad_u[:4]],
+                                     "cpu_udata64": [hex(int(pool.hdr["udata64"][i])) for i in bad_u[:4]]}
     # the whole l3fwd-graph node chain on the device: the rx node chained into
     # the GPU ip4_rewrite node (four tx ports, 12-B MAC rewrites for the 64
     # next hops, as l3fwd-graph sets them up, fwd.c:160-201)

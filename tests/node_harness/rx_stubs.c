@@ -13,6 +13,12 @@
 static void **rxq[PORTS];
 static uint32_t rx_n[PORTS], rx_pos[PORTS];
 static int rx_down[PORTS];
+static int rx_writes; /* harness_rx_driver_writes */
+
+/* as xskdev's receive (xskdev.c:296-297, __get_mbuf_rx_aligned) each
+ * returned mbuf gets data_len and data_off written, so its header line is in
+ * the receiving core's cache, dirty, when the node sees it (values kept) */
+void harness_rx_driver_writes(int on) { rx_writes = on; }
 
 /* the next mbufs of port lport_id, at most nb_pkts of them */
 uint16_t pktdev_rx_burst(uint16_t lport_id, pktmbuf_t **rx_pkts, const uint16_t nb_pkts)
@@ -23,8 +29,15 @@ uint16_t pktdev_rx_burst(uint16_t lport_id, pktmbuf_t **rx_pkts, const uint16_t 
         return PKTDEV_ADMIN_STATE_DOWN;
     uint32_t k = rx_n[lport_id] - rx_pos[lport_id];
     k = k < nb_pkts ? k : nb_pkts;
-    for (uint32_t i = 0; i < k; i++)
-        rx_pkts[i] = (pktmbuf_t *)rxq[lport_id][rx_pos[lport_id] + i];
+    for (uint32_t i = 0; i < k; i++) {
+        pktmbuf_t *m = (pktmbuf_t *)rxq[lport_id][rx_pos[lport_id] + i];
+        if (rx_writes) {
+            volatile uint16_t *dl = &m->data_len, *dof = &m->data_off;
+            *dl = *dl;
+            *dof = *dof;
+        }
+        rx_pkts[i] = m;
+    }
     rx_pos[lport_id] += k;
     return (uint16_t)k;
 }
