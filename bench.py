@@ -843,6 +843,9 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
     HR.harness_walk_until.argtypes = [ctypes.c_uint64]
     HR.harness_walk_until.restype = ctypes.c_double
     HR.harness_register_cls_node()
+    # edges copied into this harness by an earlier ip4_rewrite_set_next in the
+    # process (the rx node's hook) would make the first runs fuse ip4_rewrite
+    HR.harness_edges_reset()
     name = ctypes.create_string_buffer(64)
     fl, ne, e0, e1 = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_char_p(), ctypes.c_char_p()
     k = HR.harness_node_info(0, name, ctypes.byref(fl), ctypes.byref(ne), ctypes.byref(e0), ctypes.byref(e1))
