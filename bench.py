@@ -131,6 +131,8 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     # cnet keeps the edge output (its drop/forward/proto edge is not in nh
     # for packets the ptype node sends elsewhere)
     state["out"] = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
+    if cfg == "c2":  # parse + hash + RSS queue: no next-hop output (hash mode's nh is a constant)
+        state["out"]["nh"] = None
     # Ring of batches: step k classifies batch k % R, as a NIC ring hands over
     # fresh buffers.  R is sized so that the ring's frames and results are
     # several times the 256 MiB Infinity Cache: no step is served results or
@@ -153,6 +155,8 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
             pktgen.corrupt_cksum(fr, 1024, seed + 1000 * r)
         o = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
         o["bins"] = state["out"]["bins"]
+        if cfg == "c2":
+            o["nh"] = None
         state["ring"].append((fr, o))
     if cfg == "c3rw":
         import random
@@ -472,8 +476,86 @@ def e2e_host(st, reps: int = 5, frames=None):
     return res
 
 
+def probe_ceiling(st, stream, steps: int, kern_ms: float) -> dict:
+    """The same-box ceiling of this config's memory traffic (untimed for the
+    line, measured right after the kernel's timed windows): the access-shape
+    probes of cndp_amd/csrc/roofline_probe.hip move the kernel's frame reads
+    and result stores over the same ring of batches and outputs, and nothing
+    else.  A few launch shapes are tried; the fastest is the ceiling.
+    kernel_over_probe = kernel_ms / probe_ms tells this box's HBM apart from
+    the kernel.  For C4 / C5 a second probe stores only the 4-B next hop
+    SURVEY §8(d) counts, pricing the extra result bytes the kernel writes."""
+    import ctypes
+    P = ctypes.CDLL(os.path.join(ROOT, "cndp_amd", "lib", "libcndp_probe.so"))
+    P.cndp_probe_slots.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    P.cndp_probe_windows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_uint64] + [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.c_void_p]
+    ring = st["ring"]
+    sid = stream.cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    fr0 = ring[0][0]
+    cnet = fr0.offsets is not None or fr0.stride != 64
+    t16 = torch.empty(fr0.n, dtype=torch.int16, device=fr0.slab.device) if cnet else None
+
+    def timed(launch):
+        for k in range(3):
+            assert launch(k) == 0
+        best = None
+        for _ in range(2):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for k in range(steps):
+                launch(k)
+            b.record(stream)
+            torch.cuda.synchronize()
+            ms = a.elapsed_time(b) / steps
+            best = ms if best is None else min(best, ms)
+        return best
+
+    rows = {}
+    if not cnet:
+        for pf in (1, 2):
+            for bpc in (2, 4):
+                def launch(k, pf=pf, bpc=bpc):
+                    fr, o = ring[k % len(ring)]
+                    return P.cndp_probe_slots(fr.slab.data_ptr(), fr.n, ptr(o.get("nh")), ptr(o.get("hash")),
+                                              ptr(o.get("queue")), pf, bpc, sid)
+                rows[f"slots_pf{pf}_bpc{bpc}"] = timed(launch)
+        shape = ("packed 64-B slots: 4 x 1 KiB nt loads per 64-frame wave tile through the LDS tile, the "
+                 "kernel's result stores (nh / hash / queue as allocated), nothing else")
+    else:
+        def wlaunch(bpc, algo_only):
+            def launch(k):
+                fr, o = ring[k % len(ring)]
+                offs = fr.offsets.data_ptr() if fr.offsets is not None else None
+                if algo_only:
+                    outs = (ptr(o.get("nh")), None, None, None, None)
+                else:
+                    outs = (ptr(o.get("nh")), ptr(o.get("hash")), ptr(o.get("queue")), ptr(o.get("edge")), ptr(t16))
+                return P.cndp_probe_windows(fr.slab.data_ptr(), fr.stride, offs, fr.data_off, fr.n, *outs, bpc, sid)
+            return launch
+        for bpc in (4, 8):
+            rows[f"windows_bpc{bpc}"] = timed(wlaunch(bpc, False))
+        shape = ("the first 64 B of each frame (4 lanes a frame, 16 frames a load instruction, nt loads"
+                 + (", u64 offsets read coalesced" if fr0.offsets is not None else f", {fr0.stride}-B stride")
+                 + "), the kernel's result stores (nh / hash / queue / edge + the 2-B packet type of the "
+                 "speculation model), nothing else")
+    best = min(rows, key=rows.get)
+    res = {"probe_ms": round(rows[best], 5), "kernel_over_probe": round(kern_ms / rows[best], 4),
+           "probe_variant": best, "probe_variants_ms": {k: round(v, 5) for k, v in rows.items()},
+           "probe_shape": shape}
+    if cnet:
+        bpc = int(best.rsplit("bpc", 1)[1])
+        res["probe_nh_only_ms"] = round(timed(wlaunch(bpc, True)), 5)
+        res["probe_nh_only_note"] = ("the same windows with only the 4-B next hop stored (SURVEY §8(d)'s "
+                                     "algorithmic bytes): probe_ms - this = the cost of the other result bytes")
+    del t16
+    return res
+
+
 def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, parity: bool,
-                cpu: bool, cpu_budget: float):
+                cpu: bool, cpu_budget: float, probe: bool = True):
     """One more BASELINE config measured like the headline: ring of batches,
     one event pair around `steps` back-to-back launches, max over ranks, with
     its roofline object (traffic from profiles/pmc_<cfg>.json) and, on rank 0
@@ -519,6 +601,11 @@ def config_line(cfg: str, dev, rank: int, world: int, steps: int, warmup: int, p
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(cfg),
                         "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_pkt": st["algo"]}}
+    if probe and rank == 0:
+        try:
+            res["roofline"].update(probe_ceiling(st, stream, steps, kern_ms))
+        except Exception as ex:  # reported, never fatal
+            res["roofline"]["probe_error"] = repr(ex)
     if cfg == "c5":  # the 1500-B point also as wire-equivalent bandwidth
         pps = value * 1e6
         res["wire_Gbps"] = {"l2_1500B": round(pps * 1500 * 8 / 1e9, 1),
@@ -583,6 +670,14 @@ def fib_update(reps: int = 15) -> dict:
     return res
 
 
+HEADER_STATE_NOTE = (
+    "primary keys: every burst's mbuf headers were written on the host core just before the node saw them, as "
+    "a real receive leaves them (xskdev.c:296-297 data_len / data_off; for the l3fwd nodes behind pktdev_rx also "
+    "its soft parse's packet_type) -- on the GPU legs by the test harness's receive stub / driver, on the CPU "
+    "legs by the oracle loops -- so header lines are dirty in that core's cache; cold_*: no such writes, the "
+    "lines in whatever state the previous pass left them")
+
+
 def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     """The graph-node boundary over pktmbuf_t bursts (rank 0, N=1).  One host
     thread drives, as one lcore's graph walk would:
@@ -615,23 +710,27 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     pool = MbufPool(n)
     pool.fill(pktgen.packed_ipv4(n, routes=routes, seed=99))
     ptrs = pool.ptrs(np.arange(n))
-    l3 = {}
+    l3 = {"header_state": HEADER_STATE_NOTE}
     NodeFib.fini()
     H.harness_rx_parse.argtypes = [ctypes.c_int]
-    # Interleaved A/B, two rounds: the zero-copy node with the kernel reading
-    # each mbuf header itself (CNDP_MQ_F_DEVICE_HEADERS, the node's default) or
-    # the host resolving frame addresses from the headers; each with and without
-    # pktdev_rx's soft parse run on the burst first (pktdev_rx.c:36-101, as the
-    # l3fwd-graph walk pktdev_rx -> pkt_cls -> ip4_lookup does, so the header
-    # lines are in the core's cache).  Then staged.  Median of the rounds.
+    H.harness_driver_writes.argtypes = [ctypes.c_int]
+    # Interleaved A/B, two rounds, medians.  Primary form: each burst's mbuf
+    # headers written first as a graph on this lcore leaves them -- the
+    # receive driver's data_len / data_off stores (xskdev.c:296-297) and
+    # pktdev_rx's soft parse (pktdev_rx.c:36-101) -- then the GPU ip4_lookup
+    # node with the kernel reading each header itself (CNDP_MQ_F_DEVICE_HEADERS,
+    # the node's default) or the host resolving the frame addresses, or staged.
+    # cold_*: the same without the header writes (the lines as the previous
+    # pass left them).
     D = N.CNDP_MQ_F_DEVICE_HEADERS  # the node's default
-    variants = [("gpu_zero_copy", True, D, 0), ("gpu_zero_copy_rx_parse", True, D, 1),
-                ("gpu_zero_copy_host_headers", True, 0, 0), ("gpu_zero_copy_host_headers_rx_parse", True, 0, 1),
-                ("gpu_staged", False, 0, 0), ("gpu_staged_rx_parse", False, 0, 1)]
+    variants = [("gpu_zero_copy", True, D, 1), ("gpu_zero_copy_host_headers", True, 0, 1), ("gpu_staged", False, 0, 1),
+                ("cold_gpu_zero_copy", True, D, 0), ("cold_gpu_zero_copy_host_headers", True, 0, 0),
+                ("cold_gpu_staged", False, 0, 0)]
     ab = {v[0]: [] for v in variants}
     gid = 10
+    snap = None
     for rnd in range(2):
-        for name, zc, flags, rxp in variants:
+        for name, zc, flags, drv in variants:
             L.cndp_node_gpu_umem_reset()
             if zc:
                 L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
@@ -640,9 +739,14 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
             assert H.harness_graph_create(gid) == 0
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
-            H.harness_rx_parse(rxp)
-            H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
+            H.harness_driver_writes(drv)
+            H.harness_rx_parse(drv)
+            pool.hdr["udata64"] = 0
+            H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up (and the results checked below)
+            if rnd == 0 and name == "gpu_zero_copy":
+                snap = pool.hdr["udata64"].copy()  # node_mbuf_priv1 as the GPU node left it, primary form
             t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
+            H.harness_driver_writes(0)
             H.harness_rx_parse(0)
             H.harness_graph_destroy()
             ab[name].append(n * passes / t / 1e6 if t > 0 else 0.0)
@@ -651,19 +755,28 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
         l3[name + "_Mpps"] = round(float(np.median(v)), 2) if min(v) > 0 else None
     l3["ab_rounds"] = {k: [round(x, 2) for x in v] for k, v in ab.items()}
     L.cndp_node_gpu_umem_reset()
-    gpu_priv1 = pool.hdr["udata64"].copy()  # node_mbuf_priv1 as the GPU node left it
+    gpu_priv1 = pool.hdr["udata64"].copy()  # after the last (cold, staged) run
     fib = NodeFib()
     t24, t8 = (x.copy() for x in fib.image())
     pool.hdr["udata64"] = 0
     O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, 1)
-    # every mbuf's priv1 from the GPU node against the CPU node loop's
-    l3["results_equal_cpu_node"] = bool(np.array_equal(gpu_priv1, pool.hdr["udata64"]))
-    t = O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
-    l3["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+    # every mbuf's priv1 from the GPU node (primary form, and the last cold
+    # run) against the CPU node loop's
+    l3["results_equal_cpu_node"] = bool(snap is not None and np.array_equal(snap, pool.hdr["udata64"]))
+    l3["cold_results_equal_cpu_node"] = bool(np.array_equal(gpu_priv1, pool.hdr["udata64"]))
+    # the CPU legs in the same two header states (primary: driver writes +
+    # soft parse before each burst, as the GPU legs had them)
+    O.set_driver_writes(True)
+    O.rx_ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, 1)
     t = O.rx_ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
-    l3["cpu_1core_rx_parse_Mpps"] = round(n * passes / t / 1e6, 2)
-    l3["cpu_chain"] = ("the ip4_lookup node loop over the same mbufs (oracle/oracle.c orc_ip4_lookup_mbufs); "
-                       "_rx_parse: pktdev_rx's soft parse on each burst first, on both sides")
+    l3["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+    O.set_driver_writes(False)
+    O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, 1)
+    t = O.ip4_lookup_mbufs(ptrs, n, (t24, t8), burst, passes)
+    l3["cold_cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+    l3["cpu_chain"] = ("the ip4_lookup node loop over the same mbufs on one core (oracle/oracle.c "
+                       "orc_ip4_lookup_mbufs); primary form with the receive driver's header writes and "
+                       "pktdev_rx's soft parse before each burst (orc_rx_ip4_lookup_mbufs), as the GPU legs")
     NodeFib.fini()
     res["l3fwd_ip4_lookup"] = l3
     # ---- l3fwd: the ip4_lookup + ip4_rewrite node pair, chained as a graph
@@ -726,15 +839,20 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     # the fields eth_rx / ptype / ip4_input / ip6_input write, after the GPU
     # node's first pass from a fresh graph (ptype node state 0)
     cnet_fields = ("packet_type", "ol_flags", "tx_offload", "lport", "data_off", "data_len")
-    snap = {}
+    snap, snap_cold = {}, {}
 
-    def cnet_node(zc, flags):
+    HC.harness_rx_driver_writes.argtypes = [ctypes.c_int]
+
+    def cnet_node(zc, flags, drv=1):
         gid = next(gids)
         L.cndp_node_gpu_umem_reset()
         if zc:
             L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
         os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
         assert HC.harness_graph_create(gid) == 0
+        # the receive stub's data_len / data_off writes (xskdev.c:296-297), as
+        # the CPU chain's receive does (oracle/cnet_chain.c walk)
+        HC.harness_rx_driver_writes(drv)
         t = 0.0
         for p in range(passes + 1):  # pass 0 warms up
             pool.hdr[:] = hdr0
@@ -744,9 +862,12 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
             if dt < 0:
                 t = -1.0
                 break
-            if p == 0 and not snap:
+            if p == 0 and drv and not snap:
                 snap.update({f: pool.hdr[f].copy() for f in cnet_fields})
+            if p == 0 and not drv and not snap_cold:
+                snap_cold.update({f: pool.hdr[f].copy() for f in cnet_fields})
             t += dt if p else 0.0
+        HC.harness_rx_driver_writes(0)
         HC.harness_graph_destroy()
         os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         return round(nc * passes / t / 1e6, 2) if t > 0 else None
@@ -755,12 +876,14 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     # host headers (the eth_rx node's default) against the device reading
     # them (CNDP_MQ_F_DEVICE_HEADERS: k_mq_cnet_hdr, one more launch and a
     # PCIe read per mbuf before the classify)
-    cvars = [("gpu_zero_copy", lambda: cnet_queue(True, 0)),
-             ("gpu_zero_copy_device_headers", lambda: cnet_queue(True, D)),
-             ("gpu_staged", lambda: cnet_queue(False, 0)),
-             ("eth_rx_node_zero_copy", lambda: cnet_node(True, 0)),
+    cvars = [("eth_rx_node_zero_copy", lambda: cnet_node(True, 0)),
              ("eth_rx_node_zero_copy_device_headers", lambda: cnet_node(True, D)),
-             ("eth_rx_node_staged", lambda: cnet_node(False, 0))]
+             ("eth_rx_node_staged", lambda: cnet_node(False, 0)),
+             ("cold_eth_rx_node_zero_copy", lambda: cnet_node(True, 0, 0)),
+             ("cold_eth_rx_node_zero_copy_device_headers", lambda: cnet_node(True, D, 0)),
+             ("queue_zero_copy", lambda: cnet_queue(True, 0)),
+             ("queue_zero_copy_device_headers", lambda: cnet_queue(True, D)),
+             ("queue_staged", lambda: cnet_queue(False, 0))]
     rounds = {k: [] for k, _ in cvars}
     for _ in range(2):
         for k, fn in cvars:
@@ -779,6 +902,10 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     O.cnet_chain(ptrs, nc, rx_len, int(hdr0["data_off"][0]), t4c, t6c, cpus=cpus[:1])
     # every field the replaced nodes write, GPU eth_rx node (first pass) against the CPU chain
     cn["results_equal_cpu_chain"] = bool(snap) and all(np.array_equal(snap[f], pool.hdr[f]) for f in cnet_fields)
+    cn["cold_results_equal_cpu_chain"] = bool(snap_cold) and all(np.array_equal(snap_cold[f], pool.hdr[f])
+                                                                 for f in cnet_fields)
+    cn["header_state"] = HEADER_STATE_NOTE + ("; queue_*: the cnet queue alone (harness_mq_drive), no receive, "
+                                              "cold headers")
     pool.hdr[:] = hdr0
     t = O.cnet_chain(ptrs, nc, rx_len, int(hdr0["data_off"][0]), t4c, t6c, iters=passes, cpus=cpus[:1])
     pool.hdr[:] = hdr0
@@ -858,44 +985,64 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
     D = N.CNDP_MQ_F_DEVICE_HEADERS
     hdr0 = pool.hdr.copy()
     assert HR.harness_pktdev_rx_port(rx_id, 0) == 0
-    for gid, (key, zc, flags) in enumerate((("gpu_zero_copy", True, D), ("gpu_zero_copy_host_headers", True, 0),
-                                            ("gpu_staged", False, 0))):
-        L.cndp_node_gpu_umem_reset()
-        if zc:
-            L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
-        os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
-        assert HR.harness_graph_create(50 + gid) == 0
-        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
-        for ip, d, nh in routes:
-            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
-        t = 0.0
-        for p in range(passes + 1):  # pass 0 warms up
-            pool.hdr[:] = hdr0
-            HR.harness_rx_load(0, ptrs, n)
-            HR.harness_reset_counts()
-            dt = HR.harness_walk_until(n)
-            if dt < 0:
-                t = -1.0
-                break
-            t += dt if p else 0.0
-        if key == "gpu_zero_copy":  # what the receive chain wrote into every mbuf
-            snap = (pool.hdr["packet_type"].copy(), pool.hdr["udata64"].copy())
-        HR.harness_graph_destroy()
-        out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
+    HR.harness_rx_driver_writes.argtypes = [ctypes.c_int]
+    # primary form: the receive stub writes every returned mbuf's data_len /
+    # data_off as xskdev's receive does (xskdev.c:296-297), so the node sees
+    # header lines dirty in this core's cache (pktdev_rx.c:107-125); cold_*:
+    # without those writes.  Interleaved, two rounds, medians.
+    variants = (("gpu_zero_copy", True, D, 1), ("gpu_zero_copy_host_headers", True, 0, 1), ("gpu_staged", False, 0, 1),
+                ("cold_gpu_zero_copy", True, D, 0), ("cold_gpu_zero_copy_host_headers", True, 0, 0))
+    ab = {v[0]: [] for v in variants}
+    snaps = {}
+    gid = 50
+    for rnd in range(2):
+        for key, zc, flags, drv in variants:
+            L.cndp_node_gpu_umem_reset()
+            if zc:
+                L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
+            os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
+            gid += 1
+            assert HR.harness_graph_create(gid) == 0
+            os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+            for ip, d, nh in routes:
+                cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+            HR.harness_rx_driver_writes(drv)
+            t = 0.0
+            for p in range(passes + 1):  # pass 0 warms up
+                pool.hdr[:] = hdr0
+                HR.harness_rx_load(0, ptrs, n)
+                HR.harness_reset_counts()
+                dt = HR.harness_walk_until(n)
+                if dt < 0:
+                    t = -1.0
+                    break
+                t += dt if p else 0.0
+            HR.harness_rx_driver_writes(0)
+            if rnd == 0 and key in ("gpu_zero_copy", "cold_gpu_zero_copy"):  # what the chain wrote into every mbuf
+                snaps[key] = (pool.hdr["packet_type"].copy(), pool.hdr["udata64"].copy())
+            HR.harness_graph_destroy()
+            ab[key].append(n * passes / t / 1e6 if t > 0 else 0.0)
+    for key, v in ab.items():
+        out[key + "_Mpps"] = round(float(np.median(v)), 2) if min(v) > 0 else None
+    out["ab_rounds"] = {k: [round(x, 2) for x in v] for k, v in ab.items()}
     # the same three nodes' loops on the CPU over the same (not yet rewritten)
-    # frames: every mbuf's packet_type and node_mbuf_priv1 compared
+    # frames: every mbuf's packet_type and node_mbuf_priv1 compared, for the
+    # GPU chain's primary and cold forms
     pool.hdr[:] = hdr0
     t24c, t8c = (x.copy() for x in NodeFib().image())
     O.l3rx_chain_mbufs(ptrs, n, (t24c, t8c))
-    out["results_equal_cpu_chain"] = bool(np.array_equal(snap[0], pool.hdr["packet_type"]) and
-                                          np.array_equal(snap[1], pool.hdr["udata64"]))
-    if not out["results_equal_cpu_chain"]:
-        bad_pt = np.nonzero(snap[0] != pool.hdr["packet_type"])[0]
-        bad_u = np.nonzero(snap[1] != pool.hdr["udata64"])[0]
-        out["results_mismatches"] = {"packet_type": int(bad_pt.size), "udata64": int(bad_u.size),
-                                     "first": [int(i) for i in np.union1d(bad_pt, bad_u)[:4]],
-                                     "gpu_udata64": [hex(int(snap[1][i])) for i in bad_u[:4]],
-                                     "cpu_udata64": [hex(int(pool.hdr["udata64"][i])) for i in bad_u[:4]]}
+    for key, rk in (("gpu_zero_copy", "results_equal_cpu_chain"), ("cold_gpu_zero_copy", "cold_results_equal_cpu_chain")):
+        snap = snaps.get(key)
+        out[rk] = bool(snap is not None and np.array_equal(snap[0], pool.hdr["packet_type"]) and
+                       np.array_equal(snap[1], pool.hdr["udata64"]))
+        if snap is not None and not out[rk]:
+            bad_pt = np.nonzero(snap[0] != pool.hdr["packet_type"])[0]
+            bad_u = np.nonzero(snap[1] != pool.hdr["udata64"])[0]
+            out[rk.replace("equal_cpu_chain", "mismatches")] = {
+                "packet_type": int(bad_pt.size), "udata64": int(bad_u.size),
+                "first": [int(i) for i in np.union1d(bad_pt, bad_u)[:4]],
+                "gpu_udata64": [hex(int(snap[1][i])) for i in bad_u[:4]],
+                "cpu_udata64": [hex(int(pool.hdr["udata64"][i])) for i in bad_u[:4]]}
     # the whole l3fwd-graph node chain on the device: the rx node chained into
     # the GPU ip4_rewrite node (four tx ports, 12-B MAC rewrites for the 64
     # next hops, as l3fwd-graph sets them up, fwd.c:160-201)
@@ -927,11 +1074,14 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
         L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
         HR.harness_chain(1)
         # ip4_rewrite in the receive node's kernel (CNDP_MQ_F_REWRITE, the
-        # node's default zero-copy), or as the GPU ip4_rewrite node behind it
+        # node's default zero-copy), or as the GPU ip4_rewrite node behind it;
+        # driver-written headers (cold_*: without)
         for gid, (key, fuse) in enumerate((("gpu_with_rewrite_zero_copy", "1"),
-                                           ("gpu_with_rewrite_node_zero_copy", "0"))):
+                                           ("gpu_with_rewrite_node_zero_copy", "0"),
+                                           ("cold_gpu_with_rewrite_zero_copy", "1"))):
             os.environ["CNDP_GPU_RX_REWRITE"] = fuse
-            assert HR.harness_graph_create(60 + gid) == 0
+            HR.harness_rx_driver_writes(0 if key.startswith("cold_") else 1)
+            assert HR.harness_graph_create(70 + gid) == 0
             os.environ.pop("CNDP_GPU_RX_REWRITE", None)
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
@@ -949,19 +1099,24 @@ def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
             out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
     finally:
         os.environ.pop("CNDP_GPU_RX_REWRITE", None)
+        HR.harness_rx_driver_writes(0)
         HR.harness_chain(0)
         HR.harness_edges_reset()
         L.cndp_node_gpu_umem_reset()
-    pool.hdr[:] = hdr0
     fib = NodeFib()
     t24, t8 = (x.copy() for x in fib.image())
-    O.l3rx_chain_mbufs(ptrs, n, (t24, t8))
-    t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes)
-    out["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
-    pool.hdr[:] = hdr0
-    O.l3rx_chain_mbufs(ptrs, n, (t24, t8), rewrite=tbl)
-    t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes, rewrite=tbl)
-    out["cpu_1core_with_rewrite_Mpps"] = round(n * passes / t / 1e6, 2)
+    for pre, drv in (("", True), ("cold_", False)):
+        O.set_driver_writes(drv)
+        pool.hdr[:] = hdr0
+        O.l3rx_chain_mbufs(ptrs, n, (t24, t8))
+        t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes)
+        out[pre + "cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+        pool.hdr[:] = hdr0
+        O.l3rx_chain_mbufs(ptrs, n, (t24, t8), rewrite=tbl)
+        t = O.l3rx_chain_mbufs(ptrs, n, (t24, t8), iters=passes, rewrite=tbl)
+        out[pre + "cpu_1core_with_rewrite_Mpps"] = round(n * passes / t / 1e6, 2)
+    O.set_driver_writes(False)
+    out["header_state"] = HEADER_STATE_NOTE
     out["cpu_chain"] = ("pktdev_rx's soft parse, pkt_cls and the ip4_lookup node loop per 256-burst over the "
                         "same mbufs, one core (oracle/oracle.c orc_l3rx_chain_mbufs); _with_rewrite: then "
                         "ip4_rewrite_node_process over the mbufs ip4_lookup sent to it")
@@ -1016,14 +1171,18 @@ def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
         # behind it (CNDP_GPU_LOOKUP_REWRITE=0) with the two queues' header
         # forms (lookup / rewrite): both on the device (the nodes' defaults),
         # the rewrite's on the host, both on the host; then staged
+        # primary form: the receive driver's header writes before each burst
+        # (harness_driver_writes, xskdev.c:296-297), cold_*: without them
         D = N.CNDP_MQ_F_DEVICE_HEADERS
+        H.harness_driver_writes.argtypes = [ctypes.c_int]
         for gid, (key, zc, fl, frw, lrw) in enumerate((
                 ("gpu_zero_copy", True, D, D, 1),
                 ("gpu_zero_copy_lookup_host_headers", True, 0, D, 1),
                 ("gpu_zero_copy_rewrite_node", True, D, D, 0),
                 ("gpu_zero_copy_rewrite_node_rewrite_host_headers", True, D, 0, 0),
                 ("gpu_zero_copy_rewrite_node_host_headers", True, 0, 0, 0),
-                ("gpu_staged", False, 0, 0, 0))):
+                ("gpu_staged", False, 0, 0, 0),
+                ("cold_gpu_zero_copy", True, D, D, 1))):
             L.cndp_node_gpu_umem_reset()
             if zc:
                 L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes)
@@ -1036,15 +1195,21 @@ def l3fwd_pair(H, L, pool, ptrs, n, burst, passes, routes):
             os.environ.pop("CNDP_GPU_LOOKUP_REWRITE", None)
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+            H.harness_driver_writes(0 if key.startswith("cold_") else 1)
             H.harness_drive(b"ip4_lookup", ptrs, n, burst, 1)  # warm-up
             t = H.harness_drive(b"ip4_lookup", ptrs, n, burst, passes)
+            H.harness_driver_writes(0)
             H.harness_graph_destroy()
             out[key + "_Mpps"] = round(n * passes / t / 1e6, 2) if t > 0 else None
         fib = NodeFib()
         t24, t8 = (x.copy() for x in fib.image())
-        O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, 1)
-        t = O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, passes)
-        out["cpu_1core_Mpps"] = round(n * passes / t / 1e6, 2)
+        for key, drv in (("cpu_1core_Mpps", True), ("cold_cpu_1core_Mpps", False)):
+            O.set_driver_writes(drv)
+            O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, 1)
+            t = O.l3fwd_nodes_mbufs(ptrs, n, (t24, t8), tbl, burst, passes)
+            out[key] = round(n * passes / t / 1e6, 2)
+        O.set_driver_writes(False)
+        out["header_state"] = HEADER_STATE_NOTE
         out["cpu_chain"] = ("ip4_lookup's loop then ip4_rewrite_node_process per 256-burst over the same "
                             "mbufs, one core (oracle/oracle.c orc_l3fwd_nodes_mbufs)")
         out["gpu_paths"] = ("gpu_zero_copy*: ip4_rewrite run by ip4_lookup's queue (CNDP_MQ_F_REWRITE, "
@@ -1086,6 +1251,7 @@ def main():
                     help="other configs measured after the headline (comma list, '' = none)")
     ap.add_argument("--no-imix", action="store_true", help="same as --extra ''")
     ap.add_argument("--no-node", action="store_true", help="skip the pktmbuf node-boundary rates")
+    ap.add_argument("--no-probe", action="store_true", help="skip the same-box access-shape probes")
     ap.add_argument("--frame-mem", default="default", choices=["default", "torch", "uncached", "cached"],
                     help="frame slabs: torch (hipMalloc) tensors or cndp_gpu_frames_alloc memory; "
                          "default = FRAME_MEM per config")
@@ -1162,6 +1328,13 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     elapsed, kern_ms = D.max_over_ranks([elapsed, kern_ms], dev)
+    probe = None
+    if rank == 0 and not args.no_probe and args.config != "c3rw":
+        try:
+            probe = probe_ceiling(st, stream, args.steps, kern_ms)
+            log(f"[bench] same-box probe: {probe}")
+        except Exception as ex:  # reported, never fatal for the headline line
+            probe = {"probe_error": repr(ex)}
 
     n = st["n"]
     total_pkts = n * world * args.steps
@@ -1197,7 +1370,7 @@ def main():
     for c in todo:
         try:
             extra[c] = config_line(c, dev, rank, world, max(5, args.steps // 2), args.warmup, not args.no_parity,
-                                   not args.no_cpu_baseline, min(args.cpu_budget, 5.0))
+                                   not args.no_cpu_baseline, min(args.cpu_budget, 5.0), not args.no_probe)
             if rank == 0:
                 log(f"[bench] {c} line: {extra[c]}")
         except Exception as ex:  # reported, never fatal for the headline line
@@ -1238,7 +1411,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(args.config),
                          "kernel_ms": round(kern_ms, 5),
-                         "algorithmic_bytes_per_pkt": st["algo"]},
+                         "algorithmic_bytes_per_pkt": st["algo"], **(probe or {})},
             "cpu_baseline": cpu,
             "configs": extra,
             "node_boundary": nb,

@@ -130,6 +130,8 @@ int orc_classify(const struct orc_classify_args *a);
  * Multi-threaded over nthreads contiguous shards; returns elapsed seconds. */
 double orc_l3fwd_burst_bench(const struct orc_classify_args *a, int nthreads, int iters);
 double orc_burst_bench(const struct orc_classify_args *a, int nthreads, int iters, const int *cpus);
+/* receive-driver header writes before each burst of the mbuf node loops (oracle.c) */
+void orc_set_driver_writes(int on);
 double orc_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,
                             const uint32_t *tbl8, int iters);
 double orc_rx_ip4_lookup_mbufs(void *const *mbufs, uint32_t n, uint32_t burst, const uint32_t *tbl24,

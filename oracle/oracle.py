@@ -313,6 +313,13 @@ def dir24_8_lookup_bulk_pf(t24, t8, ips) -> np.ndarray:
     return out
 
 
+def set_driver_writes(on: bool) -> None:
+    """Receive-driver header writes (xskdev.c:296-297: data_len / data_off of
+    every mbuf, values kept) before each burst of the l3fwd mbuf node loops
+    below -- the header-cache state a real graph walk gives its nodes."""
+    lib().orc_set_driver_writes(1 if on else 0)
+
+
 def ip4_lookup_mbufs(ptrs, n, tables4, burst=256, iters=1) -> float:
     """The ip4_lookup node's CPU loop over pktmbuf_t pointers (one thread): seconds."""
     return lib().orc_ip4_lookup_mbufs(ptrs, n, burst, _p(tables4[0]), _p(tables4[1]), iters)

@@ -337,12 +337,38 @@ void harness_graph_destroy(void)
     memset(inited, 0, sizeof(inited));
 }
 
-/* one burst into the named node's process() */
+/* Receive-driver header writes for the bursts handed to a node's process()
+ * by harness_process / harness_drive (harness_driver_writes(1)): every mbuf's
+ * data_len and data_off written, values kept, as xskdev's receive does
+ * (xskdev.c:296-297) before pktdev_rx sees the burst -- so the header lines
+ * are dirty in this core's cache when the node reads them, as in a graph
+ * whose receive runs on this lcore.  (The receive nodes' stub, rx_stubs.c,
+ * does the same in pktdev_rx_burst: harness_rx_driver_writes.) */
+static int drv_on;
+void harness_driver_writes(int on) { drv_on = on; }
+static void drv_touch(void **objs, uint16_t n)
+{
+    for (uint16_t k = 0; k < n; k++) {
+        volatile uint16_t *dl = (volatile uint16_t *)((uint8_t *)objs[k] + 30);
+        volatile uint16_t *dof = (volatile uint16_t *)((uint8_t *)objs[k] + 24);
+        *dl = *dl;
+        *dof = *dof;
+    }
+}
+static int rx_parse_on;
+static void rx_parse(void **pkts, uint16_t n);
+
+/* one burst into the named node's process() (with the driver's writes and
+ * pktdev_rx's soft parse first when they are on) */
 int harness_process(const char *name, void **objs, uint16_t n)
 {
     const int i = find(name);
     if (i < 0)
         return -1;
+    if (drv_on)
+        drv_touch(objs, n);
+    if (rx_parse_on)
+        rx_parse(objs, n);
     const int r = regs[i]->process(&g, &nodes[i], objs, n);
     run_pending();
     return r;
@@ -426,7 +452,6 @@ void harness_prof(double *src, double *proc)
  * mbuf header lines are in this core's cache when the node sees them, as in
  * l3fwd-graph (pktdev_rx -> pkt_cls -> ip4_lookup).  pktmbuf_t: buf_addr @8,
  * data_off @24, packet_type @32 (pktmbuf.h:102-204). */
-static int rx_parse_on;
 void harness_rx_parse(int on) { rx_parse_on = on; }
 #define MB_MTOD(m) (*(uint8_t *const *)((const uint8_t *)(m) + 8) + *(const uint16_t *)((const uint8_t *)(m) + 24))
 static inline uint32_t l3_ptype(uint16_t et)
@@ -470,6 +495,8 @@ double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, 
             harness_walk_sources();
             const double a1 = now_s();
             const uint16_t c = (uint16_t)(n - b < burst ? n - b : burst);
+            if (drv_on)
+                drv_touch(objs + b, c);
             if (rx_parse_on)
                 rx_parse(objs + b, c);
             regs[i]->process(&g, &nodes[i], objs + b, c);

@@ -32,6 +32,8 @@ def test_bench_json_line(gpu):
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    # the same-box access-shape probe (cndp_amd/csrc/roofline_probe.hip)
+    assert r["probe_ms"] > 0 and abs(r["kernel_over_probe"] - r["kernel_ms"] / r["probe_ms"]) < 2e-3
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference") and cb["sample"]
     assert d["config"]["bins_total"] == 3 * (1 << 20)  # the timed steps: every packet binned once a step

@@ -61,8 +61,13 @@ def test_node_init_fails_loudly_without_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("zero_copy", [True, False, "driver_writes"])
 def test_node_graph_walk(gpu, zero_copy):
+    """driver_writes: zero-copy with each burst's mbuf headers written first as
+    a graph on this lcore leaves them -- xskdev's data_len / data_off stores
+    (xskdev.c:296-297) and pktdev_rx's soft parse (packet_type,
+    pktdev_rx.c:36-101) -- so the device reads header lines held dirty in the
+    host core's cache."""
     from cndp_amd import pktgen
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
@@ -83,6 +88,11 @@ def test_node_graph_walk(gpu, zero_copy):
     pool.fill(pktgen.Frames(slab.reshape(-1), n, stride=64))
     if zero_copy:
         assert L.cndp_node_gpu_umem_add(pool.base, pool.mem.nbytes) == 0
+    dw = zero_copy == "driver_writes"
+    H.harness_driver_writes.argtypes = [ctypes.c_int]
+    H.harness_rx_parse.argtypes = [ctypes.c_int]
+    H.harness_driver_writes(int(dw))
+    H.harness_rx_parse(int(dw))
     os.environ["CNDP_GPU_BATCH"] = "2048"
     os.environ["CNDP_GPU_DEPTH"] = "3"
     try:
@@ -113,6 +123,8 @@ def test_node_graph_walk(gpu, zero_copy):
         assert H.harness_count(2) == 0
         assert len(got[0]) + len(got[1]) == n
     finally:
+        H.harness_driver_writes(0)
+        H.harness_rx_parse(0)
         H.harness_graph_destroy()
         os.environ.pop("CNDP_GPU_BATCH", None)
         os.environ.pop("CNDP_GPU_DEPTH", None)
@@ -128,6 +140,9 @@ def test_node_graph_walk(gpu, zero_copy):
     ttl = bb[d + 22].astype(np.uint64)
     ck = bb[d + 24].astype(np.uint64) | (bb[d + 25].astype(np.uint64) << 8)
     assert np.array_equal(pool.hdr["udata64"], (val & 0xFFFF) | (ttl << 16) | (ck << 32))
+    if dw:  # the soft parse's packet_type, written by the host, survived the node
+        et = (bb[d + 12].astype(np.uint32) << 8) | bb[d + 13]
+        assert np.array_equal(pool.hdr["packet_type"], np.where(et == 0x0800, 0x90, np.where(et == 0x86DD, 0xE0, 0)))
     for k in (0, 1):
         assert np.all((val[got[k]] >> 16) == k)
         # each edge's stream keeps the arrival order (a subsequence of it)
@@ -207,14 +222,18 @@ def _edge_of_queue_code(e):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, "device_headers", False])
+@pytest.mark.parametrize("zero_copy", [True, "device_headers", False, "driver_writes",
+                                       "driver_writes_device_headers"])
 def test_cnet_node_graph_walk(gpu, zero_copy):
     """Graph walks over the GPU eth_rx node: it pulls 256-mbuf bursts from its
     port, and every mbuf leaves by the edge the reference's ptype /
     ip4_input / ip6_input would have sent it to, with the fields eth_rx and the
     input nodes write (the oracle over the same bursts, node state from 0).
     Zero-copy with the node's default host headers, and with the device
-    reading them (CNDP_GPU_MQ_FLAGS=4, CNDP_MQ_F_DEVICE_HEADERS)."""
+    reading them (CNDP_GPU_MQ_FLAGS=4, CNDP_MQ_F_DEVICE_HEADERS); driver_writes*:
+    the same with the receive stub writing each mbuf's data_len / data_off as
+    xskdev's receive does (xskdev.c:296-297), so eth_rx gets header lines
+    dirty in the host core's cache, as in a real graph (eth_rx.c:111-131)."""
     from helpers import CNET_DEF, cnet_fibs
     from oracle import oracle as O
     from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
@@ -227,10 +246,12 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
     pool, orig = cnet_pool(n, routes, v6, bool(zero_copy))
     ref = _cnet_expect(pool, np.arange(n), _bursts(n, 0, "full"), t4, t6, 0, port)
     L.cndp_node_gpu_umem_reset()
-    if zero_copy == "device_headers":
+    if zero_copy in ("device_headers", "driver_writes_device_headers"):
         os.environ["CNDP_GPU_MQ_FLAGS"] = str(N.CNDP_MQ_F_DEVICE_HEADERS)
     if zero_copy:
         L.cndp_node_gpu_umem_add(ctypes.c_void_p(pool.base), ctypes.c_uint64(pool.mem.nbytes))
+    H.harness_rx_driver_writes.argtypes = [ctypes.c_int]
+    H.harness_rx_driver_writes(int(str(zero_copy).startswith("driver_writes")))
     H.harness_cnet_set(fib.h, fib6.h)
     assert H.harness_eth_rx_port(0, port) == 0
     ptrs = pool.ptrs(np.arange(n))
@@ -248,6 +269,7 @@ def test_cnet_node_graph_walk(gpu, zero_copy):
             assert np.all(np.diff(idx) > 0), f"{name}: out of receive order"
             got[idx] = k
     finally:
+        H.harness_rx_driver_writes(0)
         os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         H.harness_graph_destroy()
         L.cndp_node_gpu_umem_reset()
@@ -897,7 +919,8 @@ def test_rx_node_init_fails_loudly_without_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, "host_headers", "no_rewrite", False])
+@pytest.mark.parametrize("zero_copy", [True, "host_headers", "no_rewrite", False, "driver_writes",
+                                       "driver_writes_host_headers"])
 def test_rx_node_graph_walk(gpu, zero_copy):
     """Graph walks over the GPU pktdev_rx node: it pulls 256-mbuf bursts from
     its port and every mbuf ends where l3fwd-graph's pktdev_rx -> pkt_cls ->
@@ -910,7 +933,11 @@ def test_rx_node_graph_walk(gpu, zero_copy):
     per-burst chain byte for byte; "no_rewrite" (CNDP_GPU_RX_REWRITE=0) and
     staged frames go on to the GPU ip4_rewrite node, whose bursts are its
     queue's polls (checksums 0xFFFE / 0xFFFF, whose rule depends on that
-    split, not compared).  Mixed frames: routed IPv4, IPv6, VLAN, ARP, fuzz."""
+    split, not compared).  Mixed frames: routed IPv4, IPv6, VLAN, ARP, fuzz.
+    driver_writes*: the receive stub writes each mbuf's data_len / data_off
+    as xskdev's receive does (xskdev.c:296-297), so the node gets header lines
+    dirty in the host core's cache, as pktdev_rx.c:107-125 does in a real
+    graph."""
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
     from cndp_amd import pktgen
@@ -940,11 +967,13 @@ def test_rx_node_graph_walk(gpu, zero_copy):
     if zero_copy:
         assert L.cndp_node_gpu_umem_add(ctypes.c_void_p(gp.base), ctypes.c_uint64(gp.mem.nbytes)) == 0
     os.environ["CNDP_GPU_BATCH"] = "4096"
-    if zero_copy == "host_headers":
+    if zero_copy in ("host_headers", "driver_writes_host_headers"):
         os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
     if zero_copy == "no_rewrite":
         os.environ["CNDP_GPU_RX_REWRITE"] = "0"
-    fused = zero_copy in (True, "host_headers")
+    fused = zero_copy in (True, "host_headers", "driver_writes", "driver_writes_host_headers")
+    H.harness_rx_driver_writes.argtypes = [ctypes.c_int]
+    H.harness_rx_driver_writes(int(str(zero_copy).startswith("driver_writes")))
     routes = pktgen.l3fwd_routes()
     ids = _node_ids(H)
     assert H.harness_pktdev_rx_port(ids["pktdev_rx"], port) == 0
@@ -979,6 +1008,7 @@ def test_rx_node_graph_walk(gpu, zero_copy):
             assert H.harness_node_stats(nm, ctypes.byref(c), ctypes.byref(o)) == 0
             stats[nm] = o.value
     finally:
+        H.harness_rx_driver_writes(0)
         os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         os.environ.pop("CNDP_GPU_RX_REWRITE", None)
         H.harness_chain(0)
