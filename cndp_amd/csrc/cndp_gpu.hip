@@ -4309,11 +4309,25 @@ static int dir16_update(struct cndp_tbl *t, uint32_t k0, uint32_t k1)
     return 0;
 }
 
-// a device buffer being replaced (caller holds dev_lock): a launch that took
-// its address under dev_lock (tbl_acquire) may still be on its way, so it is
-// kept while any view of the table is held.  Once none is, every kept buffer
-// goes: no thread can take a new view without dev_lock, and hipFree waits for
-// the device, so the launches already enqueued have finished reading them.
+// Device buffers replaced by a sync (caller holds dev_lock): a launch that
+// took an address under dev_lock (tbl_acquire) may still be on its way, so a
+// replaced buffer is kept while any view of the table is held.  Once none is,
+// every kept buffer goes: no thread can take a new view without dev_lock, and
+// hipFree waits for the device, so the launches already enqueued have finished
+// reading them.  Swept at every retire and at the start of every sync (each
+// launch that reads the table syncs first), so a retired DUMMY tbl8 pool or
+// /16 page array does not stay in HBM until the next growth.
+static int tbl_dev_sweep(struct cndp_tbl *t)
+{
+    if (t->n_old && __atomic_load_n(&t->views, __ATOMIC_ACQUIRE) == 0) {
+        const uint32_t n = t->n_old;
+        t->n_old = 0;
+        for (uint32_t k = 0; k < n; k++)
+            HIP_TRY(hipFree(t->dev_old[k]));
+    }
+    return 0;
+}
+
 static int tbl_dev_retire(struct cndp_tbl *t, void *p)
 {
     if (!p)
@@ -4327,12 +4341,7 @@ static int tbl_dev_retire(struct cndp_tbl *t, void *p)
         t->cap_old = cap;
     }
     t->dev_old[t->n_old++] = p;
-    if (__atomic_load_n(&t->views, __ATOMIC_ACQUIRE) == 0) {
-        for (uint32_t k = 0; k < t->n_old; k++)
-            HIP_TRY(hipFree(t->dev_old[k]));
-        t->n_old = 0;
-    }
-    return 0;
+    return tbl_dev_sweep(t);
 }
 
 // the /16 directory after tbl24 entries [r[k].lo, r[k].hi) changed (the
@@ -4550,6 +4559,9 @@ static int tbl_dev_sync_locked(struct cndp_tbl *t, void *stream)
     const uint32_t groups = t->cap_groups + 1;
     if (t->dev_id >= 0 && t->dev_id != dev)
         return -EXDEV; // a FIB mirror lives on one device
+    int rs = tbl_dev_sweep(t); // buffers retired while views were held
+    if (rs)
+        return rs;
     hipStream_t s = (hipStream_t)stream;
     // a mirror (or tbl8 pool) allocated by this sync is copied whole
     bool paint24 = t->dev_id >= 0, paint8 = t->dev_id >= 0 && t->dev_groups == groups;
@@ -7264,8 +7276,13 @@ static void mq_fill(cndp_gpu_mq_t *q, MqSlot *sl, void *const *mbufs, uint32_t k
             hmb[sl->n + i] = km < 0 ? 0u : (uint64_t)(intptr_t)(m + q->rg[km].delta);
             if (rw && km >= 0 && i >= vec) // ip4_rewrite's tail loop (bit 0: mbufs are 64-B aligned)
                 hmb[sl->n + i] |= MQ_RW_TAIL;
-            if (cnet && sl->rg < 0 && km >= 0) // the batch's region: its first mbuf's
-                sl->rg = km;
+            if (cnet && sl->rg < 0 && km >= 0) {
+                // the batch's region is its first frame's (as on the host-header
+                // path), which the host reads from that one header: mbuf headers
+                // may sit in another registered region than their buffers
+                const uint8_t *f = *(uint8_t *const *)(m + MB_BUF_ADDR) + *(const uint16_t *)(m + MB_DATA_OFF);
+                sl->rg = mq_region(q, f, 1);
+            }
         }
         return;
     }

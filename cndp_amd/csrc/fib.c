@@ -767,11 +767,14 @@ void *cne_fib_get_dp(struct cne_fib *fib) { return fib ? &fib->t : NULL; }
 
 struct cne_rib *cne_fib_get_rib(struct cne_fib *fib) { return fib ? (struct cne_rib *)&fib->rib : NULL; }
 
-/* cne_fib.c:206-221: only DIR-24-8 FIBs select a lookup.  Every scalar or
- * vector selector binds the host loop above (this build has no AVX-512 form;
- * the reference's DEFAULT also falls back to the scalar loop without it).
- * CNE_FIB_LOOKUP_GPU (an extension; DUMMY FIBs accept it too) sends every
- * cne_fib_lookup_bulk to the device mirror instead. */
+/* cne_fib.c:206-221: only DIR-24-8 FIBs select a lookup.  Every scalar
+ * selector binds the host loop above.  CNE_FIB_LOOKUP_DIR24_8_VECTOR_AVX512 is
+ * -EINVAL, as the reference answers it unless the application raised the
+ * SIMD width to 512 bits (dir24_8.c:63-69: get_vector_fn is NULL at the
+ * default CNE_VECT_SIMD_256, cne_cpuflags.c:24, cne_vect_generic.h:205) --
+ * this library has no such knob and no AVX-512 form.  CNE_FIB_LOOKUP_GPU (an
+ * extension; DUMMY FIBs accept it too) sends every cne_fib_lookup_bulk to the
+ * device mirror instead. */
 int cne_fib_select_lookup(struct cne_fib *fib, enum cne_fib_lookup_type type)
 {
     if (fib && fib->type == CNE_FIB_DUMMY && (int)type == CNDP_FIB_LOOKUP_GPU) {
@@ -785,7 +788,6 @@ int cne_fib_select_lookup(struct cne_fib *fib, enum cne_fib_lookup_type type)
     case CNE_FIB_LOOKUP_DIR24_8_SCALAR_MACRO:
     case CNE_FIB_LOOKUP_DIR24_8_SCALAR_INLINE:
     case CNE_FIB_LOOKUP_DIR24_8_SCALAR_UNI:
-    case CNE_FIB_LOOKUP_DIR24_8_VECTOR_AVX512:
     case CNE_FIB_LOOKUP_GPU:
         fib->lookup_type = (int)type;
         return 0;
@@ -1047,7 +1049,8 @@ struct cne_rib6 *cne_fib6_get_rib(struct cne_fib6 *fib)
     return fib ? (struct cne_rib6 *)&fib->rib : NULL;
 }
 
-/* cne_fib6.c:208-223, as cne_fib_select_lookup */
+/* cne_fib6.c:208-223, as cne_fib_select_lookup (TRIE_VECTOR_AVX512: -EINVAL
+ * at the default SIMD width, trie.c:47-53) */
 int cne_fib6_select_lookup(struct cne_fib6 *fib, enum cne_fib_lookup_type type)
 {
     if (fib && fib->type == CNE_FIB_DUMMY && (int)type == CNDP_FIB_LOOKUP_GPU) {
@@ -1059,7 +1062,6 @@ int cne_fib6_select_lookup(struct cne_fib6 *fib, enum cne_fib_lookup_type type)
     switch (type) {
     case CNE_FIB_LOOKUP_DEFAULT:
     case CNE_FIB_LOOKUP_TRIE_SCALAR:
-    case CNE_FIB_LOOKUP_TRIE_VECTOR_AVX512:
     case CNE_FIB_LOOKUP_GPU:
         fib->lookup_type = (int)type;
         return 0;

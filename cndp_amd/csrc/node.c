@@ -92,18 +92,45 @@ static int rw_alloc(void)
     return 0;
 }
 
-#define RW_HOOKS_MAX 16 /* one per GPU node module and harness library loaded in a process */
+/* one per GPU node module loaded in a process (each registers from its
+ * constructor and removes itself from its destructor, so a module unloaded by
+ * dlclose leaves no pointer behind) */
+#define RW_HOOKS_MAX CNDP_NODE_RW_HOOKS_MAX
 static int (*rw_next_hook[RW_HOOKS_MAX])(uint16_t port_id, uint16_t next_index);
 
-void cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index))
+int cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index))
 {
+    if (!fn)
+        return -EINVAL;
+    int r = -ENOSPC, free_k = -1;
     pthread_mutex_lock(&node_lock);
-    for (int k = 0; k < RW_HOOKS_MAX && fn; k++)
-        if (rw_next_hook[k] == fn || !rw_next_hook[k]) {
-            rw_next_hook[k] = fn;
+    for (int k = 0; k < RW_HOOKS_MAX; k++) {
+        if (rw_next_hook[k] == fn) {
+            r = 0;
             break;
         }
+        if (!rw_next_hook[k] && free_k < 0)
+            free_k = k;
+    }
+    if (r && free_k >= 0) {
+        rw_next_hook[free_k] = fn;
+        r = 0;
+    }
     pthread_mutex_unlock(&node_lock);
+    return r;
+}
+
+int cndp_node_ip4_rewrite_next_unhook(int (*fn)(uint16_t port_id, uint16_t next_index))
+{
+    int r = -ENOENT;
+    pthread_mutex_lock(&node_lock);
+    for (int k = 0; k < RW_HOOKS_MAX && fn; k++)
+        if (rw_next_hook[k] == fn) {
+            rw_next_hook[k] = NULL;
+            r = 0;
+        }
+    pthread_mutex_unlock(&node_lock);
+    return r;
 }
 
 int ip4_rewrite_set_next(uint16_t port_id, uint16_t next_index)

@@ -288,3 +288,9 @@ __attribute__((constructor)) static void rw_gpu_hook(void)
 {
     cndp_node_ip4_rewrite_next_hook(rw_mirror_edges);
 }
+
+/* unloaded (dlclose): ip4_rewrite_set_next must not call into this module */
+__attribute__((destructor)) static void rw_gpu_hook_off(void)
+{
+    cndp_node_ip4_rewrite_next_unhook(rw_mirror_edges);
+}

@@ -330,6 +330,12 @@ __attribute__((constructor)) static void rx_gpu_hook(void)
     cndp_node_ip4_rewrite_next_hook(rx_mirror_edges);
 }
 
+/* unloaded (dlclose): ip4_rewrite_set_next must not call into this module */
+__attribute__((destructor)) static void rx_gpu_hook_off(void)
+{
+    cndp_node_ip4_rewrite_next_unhook(rx_mirror_edges);
+}
+
 /* pktdev_rx_priv.h: what pktdev_ctrl.c uses to clone the node per port */
 struct pktdev_rx_node_main *pktdev_rx_get_node_data_get(void)
 {

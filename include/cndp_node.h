@@ -74,12 +74,17 @@ int cne_node_ip4_rewrite_add(uint16_t next_hop, uint8_t *rewrite_data, uint8_t r
 /* pktdev_ctrl.c:81-86 calls this for each port's pktdev_tx edge;
  * -EINVAL for port_id >= 32 (the reference writes out of bounds). */
 int ip4_rewrite_set_next(uint16_t port_id, uint16_t next_index);
-/* Adds fn (up to 4 distinct hooks; again: no-op) to the calls
- * ip4_rewrite_set_next makes after it stored the next index.  The GPU
- * ip4_rewrite node (cndp_amd/node/ip4_rewrite_gpu.c) uses it to give its
- * drain source node the tx edges pktdev_ctrl.c:81 adds, the GPU pktdev_rx
- * node (pktdev_rx_gpu.c) to give them to itself and its clones. */
-void cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index));
+/* Adds fn to the calls ip4_rewrite_set_next makes after it stored the next
+ * index: 0 (also when fn is already there), -EINVAL for NULL, -ENOSPC when
+ * CNDP_NODE_RW_HOOKS_MAX distinct hooks are registered.  The GPU ip4_rewrite
+ * node (cndp_amd/node/ip4_rewrite_gpu.c) uses it to give its drain source
+ * node the tx edges pktdev_ctrl.c:81 adds, the GPU pktdev_rx and ip4_lookup
+ * nodes to give them to themselves; each registers from its constructor and
+ * removes the hook from its destructor (cndp_node_ip4_rewrite_next_unhook:
+ * 0, or -ENOENT when fn is not registered). */
+#define CNDP_NODE_RW_HOOKS_MAX 16
+int cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index));
+int cndp_node_ip4_rewrite_next_unhook(int (*fn)(uint16_t port_id, uint16_t next_index));
 /* nh = idx | (depth == 32 ? PROTO : FORWARD) << 24, then cne_fib_add /
  * cne_fib6_add.  cne_node_ip6_add_input keeps the reference's depth == 32
  * test (ip6_input.c:268) for IPv6 as well. */

@@ -418,6 +418,40 @@ def test_mq_cnet_device_headers_metadata_hook(cn, gpu):
     assert at_input[in_b].sum() > 100 and at_input[~in_b].sum() > 100
 
 
+@pytest.mark.parametrize("flags", [0, N.CNDP_MQ_F_DEVICE_HEADERS], ids=["host_headers", "device_headers"])
+def test_mq_cnet_headers_and_frames_in_separate_regions(cn, gpu, flags):
+    """The mbuf headers in one registered region, their buffers (buf_addr) in
+    another: the batch's region is its first frame's in both header forms, so
+    every mbuf is classified exactly as with one pool (the oracle over the
+    frames; cnet_metadata at the header's m + 64)."""
+    cl, routes, v6, t4, t6 = cn
+    n = 6000
+    pool, orig = cnet_pool(n, routes, v6, True)   # the frames (and the oracle's view)
+    hp = MbufPool(n)                              # the headers
+    hp.hdr[:] = pool.hdr
+    hp.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN] = MD_FILL
+    order = np.arange(n)
+    bursts = _bursts(n, 7, "full")
+    cl.host_register(pool.mem)
+    cl.host_register(hp.mem)
+    try:
+        cl.set_tuning(cnet_spec=256)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=flags, batch=2048, depth=3, umem=hp.base, lport=2)
+        ref = _cnet_expect(pool, order, bursts, t4, t6, 0, 2)
+        addrs, edges = q.run(hp, order, bursts)
+        q.close()
+    finally:
+        cl.host_unregister(hp.mem)
+        cl.host_unregister(pool.mem)
+    assert np.array_equal(hp.index_of(addrs), order)
+    assert not np.any(edges == N.CNDP_MQ_EDGE_NONE)
+    # the headers and metadata as the chain left them, seen through the frame pool
+    pool.hdr[:] = hp.hdr
+    pool.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN] = hp.mem.reshape(n, -1)[:, HDR:HDR + MD_LEN]
+    want_e = cnet_check(pool, orig, ref, t4, t6, 2)
+    assert np.array_equal(edges.astype(np.int64), want_e)
+
+
 @pytest.mark.parametrize("zero_copy", [True, False])
 def test_mq_cnet_fast_path(cn, gpu, zero_copy):
     """IMIX mbufs in a UMEM-layout pool (data at +256) take the fast parse,

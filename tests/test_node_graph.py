@@ -1090,3 +1090,55 @@ def test_rx_nodes_idle_and_admin_down(gpu, harness):
         H.harness_rx_down(5, 0)
         H.harness_graph_destroy()
         L.cndp_node_gpu_umem_reset()
+
+
+def test_rewrite_hooks_unregistered_on_unload():
+    """Each GPU node module hooks ip4_rewrite_set_next from its constructor and
+    removes the hook from its destructor: a harness library loaded a second
+    time (its own copy) and unloaded again leaves no hook behind, so a later
+    ip4_rewrite_set_next neither calls into unmapped code nor edits that
+    library's edges; a full hook table answers -ENOSPC, an unknown hook
+    -ENOENT."""
+    import shutil
+    import _ctypes
+    L = N.lib()
+    _harness()   # the regular harness instance stays loaded throughout
+    Hook = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint16, ctypes.c_uint16)
+    L.cndp_node_ip4_rewrite_next_hook.argtypes = [Hook]
+    L.cndp_node_ip4_rewrite_next_unhook.argtypes = [Hook]
+    calls = []
+    probe = Hook(lambda p, e: calls.append((p, e)) or 0)
+    # count the free slots with a probe hook of our own
+    fill = [Hook(lambda p, e: 0) for _ in range(20)]
+    took = [f for f in fill if L.cndp_node_ip4_rewrite_next_hook(f) == 0]
+    free_before = len(took)
+    assert 0 < free_before < 20 and L.cndp_node_ip4_rewrite_next_hook(fill[-1]) == -28   # -ENOSPC
+    for f in took:
+        assert L.cndp_node_ip4_rewrite_next_unhook(f) == 0
+    assert L.cndp_node_ip4_rewrite_next_unhook(fill[0]) == -2                            # -ENOENT
+    # a second copy of the l3fwd harness: its two node modules hook on load
+    cp = os.path.join(HERE, "node_harness", "libnode_harness_copy.so")
+    shutil.copyfile(HARNESS, cp)
+    try:
+        h = ctypes.CDLL(cp)
+        took = [f for f in fill if L.cndp_node_ip4_rewrite_next_hook(f) == 0]
+        assert len(took) == free_before - 2     # ip4_lookup_gpu.c and ip4_rewrite_gpu.c of the copy
+        for f in took:
+            L.cndp_node_ip4_rewrite_next_unhook(f)
+        _ctypes.dlclose(h._handle)
+        del h
+    finally:
+        os.remove(cp)
+    took = [f for f in fill if L.cndp_node_ip4_rewrite_next_hook(f) == 0]
+    assert len(took) == free_before             # the copy's hooks went with it
+    for f in took:
+        L.cndp_node_ip4_rewrite_next_unhook(f)
+    # and ip4_rewrite_set_next runs the remaining hooks only (none unmapped)
+    assert L.cndp_node_ip4_rewrite_next_hook(probe) == 0
+    try:
+        L.cndp_node_ip4_rewrite_reset()
+        assert L.ip4_rewrite_set_next(3, 1) == 0
+        assert calls == [(3, 1)]
+    finally:
+        L.cndp_node_ip4_rewrite_next_unhook(probe)
+        L.cndp_node_ip4_rewrite_reset()
