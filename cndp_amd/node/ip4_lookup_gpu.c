@@ -94,6 +94,7 @@ static struct gpu_graph_state *gs_by_graph[GPU_GRAPHS_MAX];
 struct gpu_node_ctx { /* node->ctx is CNE_NODE_CTX_SZ (16) bytes */
     struct gpu_graph_state *st;
 };
+_Static_assert(sizeof(struct gpu_node_ctx) <= CNE_NODE_CTX_SZ, "node context");
 #define GPU_NODE_STATE(node) (((struct gpu_node_ctx *)(node)->ctx)->st)
 
 static uint32_t env_u32(const char *name, uint32_t dflt)

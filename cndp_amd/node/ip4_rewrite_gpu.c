@@ -68,6 +68,7 @@ static struct rw_graph_state *rw_by_graph[RW_GRAPHS_MAX];
 struct rw_node_ctx { /* node->ctx is CNE_NODE_CTX_SZ (16) bytes */
     struct rw_graph_state *st;
 };
+_Static_assert(sizeof(struct rw_node_ctx) <= CNE_NODE_CTX_SZ, "node context");
 #define RW_NODE_STATE(node) (((struct rw_node_ctx *)(node)->ctx)->st)
 
 static uint32_t env_u32(const char *name, uint32_t dflt)
