@@ -115,6 +115,21 @@ __device__ __forceinline__ uint32_t tz4(TP tab, uint32_t b, uint32_t x)
            tab[(b + 2) * 256 + ((x >> 16) & 0xffu)] ^ tab[(b + 3) * 256 + (x >> 24)];
 }
 
+// the same from the nibble tables N[q][u] (tab[q * 16 + u], TABN_OFF in the
+// global table): 8 reads a word instead of 4, but a wave's 32 lanes read at
+// most 16 distinct dwords of one 16-dword row, so no LDS bank conflicts
+template <typename TP>
+__device__ __forceinline__ uint32_t tz4n(TP tab, uint32_t b, uint32_t x)
+{
+    uint32_t h = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t v = (x >> (8 * j)) & 0xffu, q = 2 * (b + j);
+        h ^= tab[q * 16 + (v >> 4)] ^ tab[(q + 1) * 16 + (v & 15u)];
+    }
+    return h;
+}
+
 #define CNDP_RW_MAX_NH CNDP_IP4_REWRITE_MAX_NH       // CNE_GRAPH_IP4_REWRITE_MAX_NH
 #define CNDP_RW_MAX_LEN CNDP_IP4_REWRITE_MAX_LEN     // CNE_GRAPH_IP4_REWRITE_MAX_LEN
 #define CNDP_RW_MAX_PORTS CNDP_IP4_REWRITE_MAX_PORTS // CNE_MAX_ETHPORTS
@@ -1409,8 +1424,19 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 // Frames that are not 16-B aligned or have < 64 bytes before the slab end
 // are staged with bounded byte loads (zero past the end), like Win.
 // ---------------------------------------------------------------------------
+#ifndef CT_THREADS
 #define CT_THREADS 512
+#endif
 #define CT_WAVES (CT_THREADS / 64)
+// CD_MINW > 0: ask the compiler for that many waves a SIMD (A/B builds)
+#ifndef CD_MINW
+#define CD_MINW 0
+#endif
+#if CD_MINW
+#define CD_BOUNDS __launch_bounds__(CT_THREADS, CD_MINW)
+#else
+#define CD_BOUNDS __launch_bounds__(CT_THREADS)
+#endif
 
 // frame base (bytes from slab) of packet i, or ~0 when i >= n
 __device__ __forceinline__ uint64_t ct_base(const KArgs &a, uint64_t i, uint64_t off_i)
@@ -1546,6 +1572,12 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #ifndef CD_ABL
 #define CD_ABL 0
 #endif
+// CD_NIB 1: k_cnet_defer's Toeplitz from the nibble tables (4.5 KiB of LDS,
+// conflict-free reads) instead of the byte tables (36 KiB, random banks)
+#ifndef CD_NIB
+#define CD_NIB 0
+#endif
+#define CD_TAB_WORDS (CD_NIB ? 2 * TAB_POS * 16 : TAB_POS * 256)
 template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
 {
     const GAS T *g = (const GAS T *)p;
@@ -1690,7 +1722,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 uint32_t u = k < 2 ? (f4 ? V[k + 1] : V[k]) : k == 2 ? (f4 ? (l4ok ? V[3] : 0u) : V[2])
                            : k < 8 ? (f4 ? 0u : V[k]) : (f4 || !l4ok ? 0u : V[8]);
                 if (!(CD_ABL & 1))
-                    na.h ^= tz4(s_t, 4 * k, u);
+                    na.h ^= CD_NIB ? tz4n(s_t, 4 * k, u) : tz4(s_t, 4 * k, u);
             }
         }
         // both families' input-node pieces, straight-line, then selects: the
@@ -1884,9 +1916,9 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
 // META: ptype / rxmeta outputs requested (without them the kernel keeps
 // 14 VGPRs and 18 spilled SGPRs fewer)
 template <bool LNT, bool META>
-__global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_tiles)
+__global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
-    __shared__ uint32_t s_t[TAB_POS * 256];
+    __shared__ uint32_t s_t[CD_TAB_WORDS];
     __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
@@ -1919,8 +1951,8 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
         s_sf[tid] = 0;
     if (tid == 0)
         s_mx = 0;
-    for (uint32_t k = tid; k < TAB_POS * 256; k += CT_THREADS)
-        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k < CD_TAB_WORDS; k += CT_THREADS)
+        s_t[k] = a.ttab[(CD_NIB ? TABN_OFF : 0) + k];
     u32x4 r[2][4];
     cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
     cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
@@ -1967,7 +1999,10 @@ __global__ __launch_bounds__(CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_t
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && tid == 0 && s_mx)
         atomicOr(&a.spec_meta[SPEC_MX], s_mx);
     if (a.wl_fold)
-        cnet_defer_tail<CT_THREADS, 256>(a, (uint32_t *)&s_tile[0][0], s_t, s_reta, s_bins, s_sf, count);
+        // (the general parse takes the byte tables: from LDS, or global memory
+        // when LDS holds the nibble tables)
+        cnet_defer_tail<CT_THREADS, 256>(a, (uint32_t *)&s_tile[0][0], CD_NIB ? a.ttab : s_t, s_reta, s_bins, s_sf,
+                                         count);
 }
 
 // ---------------------------------------------------------------------------
