@@ -130,9 +130,12 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     # l3fwd / hash: the graph edge is nh >> 16 (no separate edge stream);
     # cnet keeps the edge output (its drop/forward/proto edge is not in nh
     # for packets the ptype node sends elsewhere)
-    state["out"] = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
-    if cfg == "c2":  # parse + hash + RSS queue: no next-hop output (hash mode's nh is a constant)
-        state["out"]["nh"] = None
+    # the per-packet outputs each config's workload asks for, as SURVEY §8(d)
+    # counts them: C2 hash + queue (hash mode's nh is a constant), C3 / C4 nh +
+    # hash + queue, C5 the verdict / next hop alone (parse + checksum verify +
+    # LPM: no flow hash)
+    state["out"] = cl.alloc_outputs(n, 64, device=dev, edge=False)
+    trim_outputs(cfg, state["out"])
     # Ring of batches: step k classifies batch k % R, as a NIC ring hands over
     # fresh buffers.  R is sized so that the ring's frames and results are
     # several times the 256 MiB Infinity Cache: no step is served results or
@@ -153,10 +156,9 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
             fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed + 1000 * r, device=dev,
                                     frame_mem=fm)
             pktgen.corrupt_cksum(fr, 1024, seed + 1000 * r)
-        o = cl.alloc_outputs(n, 64, device=dev, edge=cfg in ("c4", "c5"))
+        o = cl.alloc_outputs(n, 64, device=dev, edge=False)
         o["bins"] = state["out"]["bins"]
-        if cfg == "c2":
-            o["nh"] = None
+        trim_outputs(cfg, o)
         state["ring"].append((fr, o))
     if cfg == "c3rw":
         import random
@@ -167,6 +169,17 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
             assert cl.rewrite_add(nh, bytes(rnd_.randrange(256) for _ in range(12)), nh % 4) == 0
         state["tx"] = torch.empty(n, dtype=torch.int16, device=dev)
     return state
+
+
+OUTPUTS = {"c2": ("hash", "queue"), "c3": ("nh", "hash", "queue"), "c3rw": ("nh", "hash", "queue"),
+           "c4": ("nh", "hash", "queue"), "c5": ("nh",)}
+
+
+def trim_outputs(cfg: str, out: dict) -> None:
+    """Drop the per-packet outputs config cfg does not ask for (OUTPUTS)."""
+    for k in ("nh", "hash", "queue", "edge"):
+        if k not in OUTPUTS[cfg]:
+            out[k] = None
 
 
 def run_step(st, stream=None, k: int = 0):
@@ -348,25 +361,30 @@ def cpu_baseline(state, budget_s: float = 10.0):
         def run(threads, iters, h):
             return O.cnet_chain(ptrs, n, lens, 0, *tabs, hash=h, nthreads=threads, iters=iters,
                                 cpus=cpus[:threads])
-        t1 = run(1, 1, True)
+        # the flow hash on the CPU too when the GPU line outputs it (C4), not
+        # when it does not (C5: parse + checksum verify + LPM)
+        wh = state["out"].get("hash") is not None
+        t1 = run(1, 1, wh)
         single = n / t1 / 1e6
-        tt = run(len(cpus), 1, True)
+        tt = run(len(cpus), 1, wh)
         iters = max(1, int(budget_s / max(tt, 1e-6)))
-        tt = run(len(cpus), iters, True)
+        tt = run(len(cpus), iters, wh)
         multi = n * iters / tt / 1e6
-        th = run(len(cpus), iters, False)
-        extra["no_hash_Mpps"] = round(n * iters / th / 1e6, 2)
-        extra["no_hash_single_core_Mpps"] = round(n / run(1, 1, False) / 1e6, 2)
-        extra["no_hash_note"] = ("the same chain without the flow hash, which CNDP's cnet nodes never "
-                                 "compute (the reference chain's own work)")
+        if wh:
+            th = run(len(cpus), iters, False)
+            extra["no_hash_Mpps"] = round(n * iters / th / 1e6, 2)
+            extra["no_hash_single_core_Mpps"] = round(n / run(1, 1, False) / 1e6, 2)
+            extra["no_hash_note"] = ("the same chain without the flow hash, which CNDP's cnet nodes never "
+                                     "compute (the reference chain's own work)")
         tc = O.burst_bench(mode, slab, n, nthreads=len(cpus), iters=1, cpus=cpus, **kw)
         extra["checker_Mpps"] = round(n / tc / 1e6, 2)
         extra["checker_note"] = ("oracle/oracle.c's per-frame checker loop (bounds-checked byte reads, "
                                  "no prefetching), the figure earlier rounds reported")
         chain = ("cnet chain per 256-mbuf graph walk over pktmbuf_t pointers (oracle/cnet_chain.c: eth_rx "
                  "mbuf_update with cne_get_ptype, ptype-node speculation, ip4/ip6_input length + checksum + "
-                 "metadata + 4-wide DIR-24-8 / trie lookups, the nodes' prefetching; plus the reference's "
-                 "cne_softrss flow hash the GPU line computes -- no_hash_Mpps drops it)")
+                 "metadata + 4-wide DIR-24-8 / trie lookups, the nodes' prefetching" +
+                 ("; plus the reference's cne_softrss flow hash the GPU line computes -- no_hash_Mpps drops it)"
+                  if wh else ")"))
         del hdr
     else:
         t1 = O.burst_bench(mode, slab, n, nthreads=1, iters=1, cpus=cpus[:1], **kw)
@@ -1264,6 +1282,7 @@ def main():
     ap.add_argument("--cnet-spec", type=int, default=None)
     ap.add_argument("--spec-scan", type=int, default=None)
     ap.add_argument("--spec-lists", type=int, default=None)
+    ap.add_argument("--spec-types", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--dir16", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
@@ -1288,7 +1307,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16,
                   load_nt=args.load_nt, cnet_tile=args.cnet_tile, cnet_spec=args.cnet_spec,
-                  spec_scan=args.spec_scan, spec_lists=args.spec_lists)
+                  spec_scan=args.spec_scan, spec_lists=args.spec_lists, spec_types=args.spec_types)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 

@@ -192,6 +192,12 @@ struct KArgs {
     uint32_t wl_fold;      // k_cnet_defer's last block parses the worklist and runs spec_classes
     uint32_t tail_lo;      // with wl_fold: the first frame of the last SPEC_TAIL bursts
     uint32_t spec_allow;   // batch shortcuts allowed (CNDP_TUNE_SPEC_SCAN auto)
+    // canonical tiles' types as 2-bit codes (CNDP_TUNE_SPEC_TYPES): per tile 16 B,
+    // the ballots of "IPv6" and "UDP" over its frames, tile word SPEC_TW_CODES and
+    // no spec_t16 stores; frames >= spec_keep_lo always store their types
+    uint8_t *spec_c2;
+    uint32_t spec_codes;
+    uint32_t spec_keep_lo;
     // fused ip4_rewrite (k_classify_tile<..., RW = true>)
     const struct cndp_rw_nh *rw_tbl;
     uint16_t *tx_edge;
@@ -1587,6 +1593,15 @@ template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
     return g;
 }
 
+// the four packet types a canonical tile holds (spec_canon): Ethernet + IPv4 /
+// IPv6 (0x11 / 0x41) with TCP / UDP (0x100 / 0x200, pktmbuf_ptype.h), coded as
+// IPv6 bit | UDP bit; SPEC_TW_CODES marks a tile whose types went out coded
+#define SPEC_TW_CODES 3u
+__device__ __forceinline__ bool spec_code_type(uint32_t pt)
+{
+    return pt == 0x111u || pt == 0x211u || pt == 0x141u || pt == 0x241u;
+}
+
 template <bool LNT, bool META, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
@@ -1708,8 +1723,10 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         uint32_t flags = 0;
         // Toeplitz, one instruction stream for both families: the v6 words
         // are V[0..7] + L4 V[8], the v4 ones V[1..2] + L4 V[3] (a zero word
-        // adds nothing); positions past the v4 tuple only when the wave has v6
-        {
+        // adds nothing); positions past the v4 tuple only when the wave has v6.
+        // Skipped when the call asks for neither the hash nor the queue
+        // (launch-uniform; the bins of cnet mode do not use the queue).
+        if (a.hash || a.queue) {
             uint32_t V[9];
 #pragma unroll
             for (int k = 0; k < 9; k++)
@@ -1782,18 +1799,10 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         if (o.spec_nh) {
             if (bf && din && (!o.nh || (pe != 3u && pe != 4u)))
                 at32(o.spec_nh, ib) = eb >> 1;
-            if (bf) {
-                // the last SPEC_TAIL bursts' types are read by spec_classes in
-                // this kernel's last block when it folds: write-through stores
-                if (a.wl_fold && ib >= a.tail_lo)
-                    __hip_atomic_store(&at16(o.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                else
-                    __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
-            }
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
+            bool codes = false;
             if (o.spec_tile && bv) {
                 // the tile's word for the speculation passes (spec_canon): 1 when
                 // every frame has its low byte's common edge -- parsed here (low
@@ -1801,8 +1810,22 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 // or pkt_drop, nor left to the general parse
                 const bool odd = ib < a.n && !(bf && (pe == 3u || pe == 4u));
                 const uint64_t om = __ballot(odd);
+                // such a tile's types are IPv4 / IPv6 x TCP / UDP: with
+                // a.spec_codes (the previous call was a uniform batch, whose
+                // passes never read a canonical tile's types) they go out as two
+                // ballots, 16 B a tile, instead of 128 B of types (k_spec_expand
+                // writes the types should this batch need them after all)
+                codes = a.spec_codes && om == 0ull && (t - wstep + 1u) * 64u <= a.spec_keep_lo &&
+                        __ballot(ib < a.n && !spec_code_type(pt)) == 0ull;
+                if (codes) {
+                    const uint64_t m6 = __ballot((pt & 0xf0u) == 0x40u), mu = __ballot((pt & 0xf00u) == 0x200u);
+                    if (lane == 0)
+                        __builtin_nontemporal_store((u32x4){(uint32_t)m6, (uint32_t)(m6 >> 32), (uint32_t)mu,
+                                                            (uint32_t)(mu >> 32)},
+                                                    (u32x4 *)(a.spec_c2 + 16u * (t - wstep)));
+                }
                 if (lane == 0)
-                    o.spec_tile[t - wstep] = (uint8_t)(om == 0ull);
+                    o.spec_tile[t - wstep] = codes ? (uint8_t)SPEC_TW_CODES : (uint8_t)(om == 0ull);
                 if (om && (a.spec_allow & SPEC_ALLOW_LISTS)) { // wave-uniform, rare
                     // groups (lanes 4q + 3) whose 4th frame was not parsed here, or
                     // is off the common edge beside a 3rd not parsed here (spec_odd_tile)
@@ -1810,6 +1833,15 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                     if (lane == 0 && ((nf & m3) | (om & m3 & (nf << 1))))
                         atomicOr(s_mx, 1u << 8);
                 }
+            }
+            if (bf && !codes) {
+                // the last SPEC_TAIL bursts' types are read by spec_classes in
+                // this kernel's last block when it folds: write-through stores
+                if (a.wl_fold && ib >= a.tail_lo)
+                    __hip_atomic_store(&at16(o.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
             }
         }
         if (bf) {
@@ -3534,6 +3566,35 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     }
 }
 
+// CNDP_TUNE_SPEC_TYPES: the types of the tiles k_cnet_defer coded
+// (SPEC_TW_CODES: IPv6 bit and UDP bit per frame, 16 B a tile) written out
+// as spec_t16, when this batch's speculation passes read them after all.
+// They do not when the batch resolved by its last universal group
+// (meta[SPEC_SKIP]: nothing runs) or is uniform with an entering state on its
+// low byte's common edge (k_spec_local_t's uniform pass reads the types of the
+// other tiles only) -- the case the host codes for, a uniform batch before --
+// and the kernel returns at once.
+__global__ __launch_bounds__(256) void k_spec_expand(KArgs a, uint32_t n_tiles, const uint32_t *meta)
+{
+    if (meta[SPEC_SKIP])
+        return;
+    if (meta[SPEC_UNIF]) {
+        const uint32_t T = meta[SPEC_IN] & 0xffffu;
+        if (spec_canon(T & 0xffu) == cnet_edge(T))
+            return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6); t < n_tiles; t += gridDim.x * 4u) {
+        if (a.spec_tile[t] != SPEC_TW_CODES) // wave-uniform
+            continue;
+        const u32x4 c = *(const u32x4 *)(a.spec_c2 + 16u * t);
+        const uint32_t w6 = lane < 32u ? c.x : c.y, wu = lane < 32u ? c.z : c.w;
+        const uint32_t b = lane & 31u, i = t * 64u + lane;
+        if (i < a.n)
+            a.spec_t16[i] = (uint16_t)((((w6 >> b) & 1u) ? 0x41u : 0x11u) | (((wu >> b) & 1u) ? 0x200u : 0x100u));
+    }
+}
+
 // Grid barrier of k_spec_fallback: bar[0] counts arrivals (monotonic within a
 // launch), bar[1] is the generation the last arriver publishes; spec_classes
 // zeroes both every call.  Each wave's stores are drained, then lane 0
@@ -3947,6 +4008,8 @@ struct cndp_gpu_ctx {
     uint32_t *sp_cflag;   // per chunk: listed this call (cleared by k_spec_fallback)
     uint32_t *sp_R;       // chunks k_spec_local_t leaves to k_spec_fallback: (chunk, entering state)
     uint8_t *sp_tile;     // per 64-frame tile: the main kernel's canonical-tile word
+    uint8_t *sp_c2;       // per 64-frame tile: 16 B of type codes (CNDP_TUNE_SPEC_TYPES)
+    int tune_spec_types;  // CNDP_TUNE_SPEC_TYPES: 0 auto, 1 always the types, 2 always codes
     uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch uniform
     uint64_t sp_n_cap, sp_b_cap;
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
@@ -4146,7 +4209,7 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
     if (c->d_rw_tbl)
         hipFree(c->d_rw_tbl);
     void *sp[] = {c->sp_small, c->sp_class, c->sp_pt,   c->sp_nh,  c->sp_S,    c->sp_T,
-                  c->sp_U,     c->sp_done,  c->sp_tile, c->sp_R,   c->sp_cwl, c->sp_cflag};
+                  c->sp_U,     c->sp_done,  c->sp_tile, c->sp_R,   c->sp_cwl, c->sp_cflag, c->sp_c2};
     for (void *q : sp)
         if (q)
             hipFree(q);
@@ -5010,13 +5073,16 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
             HIP_TRY(hipFree(c->sp_nh));
         if (c->sp_tile)
             HIP_TRY(hipFree(c->sp_tile));
+        if (c->sp_c2)
+            HIP_TRY(hipFree(c->sp_c2));
         c->sp_pt = c->sp_nh = nullptr;
-        c->sp_tile = nullptr;
+        c->sp_tile = c->sp_c2 = nullptr;
         c->sp_n_cap = 0;
         const uint64_t cap = n + (n >> 3) + 1024;
         HIP_TRY(hipMalloc((void **)&c->sp_pt, cap * 2));
         HIP_TRY(hipMalloc((void **)&c->sp_nh, cap * 4));
         HIP_TRY(hipMalloc((void **)&c->sp_tile, cap / 64 + 1));
+        HIP_TRY(hipMalloc((void **)&c->sp_c2, (cap / 64 + 1) * 16));
         c->sp_n_cap = cap;
     }
     if (nb > c->sp_b_cap) {
@@ -5224,10 +5290,22 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 a.wl_fold = 1;
                 a.tail_lo = (uint32_t)t0;
             }
+            // canonical tiles' types as codes (CNDP_TUNE_SPEC_TYPES): auto after a
+            // uniform batch, whose passes read none of them
+            if (a.spec_tile && B <= 256) {
+                const uint64_t nb = ((uint64_t)b->n + B - 1) / B;
+                a.spec_c2 = c->sp_c2;
+                a.spec_keep_lo = nb > SPEC_TAIL ? (uint32_t)((nb - SPEC_TAIL) * B) : 0u;
+                a.spec_codes = c->tune_spec_types == 2 ||
+                               (c->tune_spec_types == 0 && c->sp_hint && ((volatile uint32_t *)c->sp_hint)[1]);
+            }
             hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
                                0, s, a, (uint32_t)n_tiles);
             if (!a.wl_fold)
                 hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
+            if (a.spec_codes) // the coded types, should the passes read them after all
+                hipLaunchKernelGGL(k_spec_expand, dim3((uint32_t)c->num_cu * 2u), dim3(256), 0, s, a,
+                                   (uint32_t)n_tiles, (const uint32_t *)(c->sp_small + 1));
         } else {
             hipLaunchKernelGGL(k_classify_cnet<false>, dim3(g), dim3(CNET_THREADS), 0, s, a);
         }
@@ -7729,6 +7807,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 1)
             return -EINVAL;
         c->tune_spec_lists = value;
+        return 0;
+    case CNDP_TUNE_SPEC_TYPES:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_spec_types = value;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

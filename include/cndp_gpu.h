@@ -410,7 +410,14 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           low byte's common edge and, when no group of the batch can
  *                           move the node state off a common edge, the local pass
  *                           replays only those (default); 0 = the local pass looks at
- *                           every chunk (tests force both) */
+ *                           every chunk (tests force both)
+ *   CNDP_TUNE_SPEC_TYPES    cnet speculation: how the fast kernel keeps the packet types
+ *                           of a tile whose every frame is on its low byte's common edge
+ *                           (IPv4 / IPv6 x TCP / UDP) -- 0 = auto (as 2-bit codes, 16 B a
+ *                           tile, when the previous call was a uniform batch, whose
+ *                           passes read no such type; a batch that needs them after all
+ *                           gets them written out by one more launch), 1 = always the
+ *                           types, 2 = always codes (tests force all three) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -426,6 +433,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_CNET_FOLD 13
 #define CNDP_TUNE_SPEC_GRID 14
 #define CNDP_TUNE_SPEC_LISTS 15
+#define CNDP_TUNE_SPEC_TYPES 16
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words

@@ -981,6 +981,43 @@ def test_cnet_speculation_uniform(cnet, gpu, burst):
         ccl.set_tuning(cnet_spec=256, spec_scan=0)
 
 
+@pytest.mark.parametrize("types", [0, 2, 1], ids=["auto", "codes", "types"])
+def test_cnet_speculation_coded_types(cnet, gpu, types):
+    """CNDP_TUNE_SPEC_TYPES: the fast kernel keeps the types of tiles whose
+    every frame is on its low byte's common edge as 2-bit codes (auto: after a
+    uniform batch; codes: always) and k_spec_expand writes them out when the
+    batch's passes read them after all.  Calls of different shapes chained on
+    one node state -- uniform (the C5 shape), sparse GTP in IMIX (chunk lists),
+    GTP-U runs (a state off the common edge), uniform again after them, plain
+    IMIX (the batch shortcut) -- == the restated node loop in every mode, so a
+    uniform batch's hint followed by one that is not is covered."""
+    ccl, routes, v6, ct4, ct6 = cnet
+    uni = pktgen.packed_ipv4(24000, routes=routes, device=gpu, seed=77)
+    rows = uni.slab.view(uni.n, uni.stride)
+    idx = torch.arange(uni.n, device=gpu)
+    rows[:, 36] = 0x12
+    for every, first, lo in ((997, 5, 0x68), (1499, 11, 0x4B)):  # GTP-U, GTP-C
+        sel = (idx % every) == first
+        rows[sel, 36] = 0x08
+        rows[sel, 37] = lo
+    sparse = _sparse_gtp(30000, routes, v6, gpu, seed=78)
+    runs = _gtp_runs(30000, routes, v6, seed=79, cut_targets=[15000])
+    runs = pktgen.Frames(runs.slab.to(gpu), runs.n, offsets=runs.offsets.to(gpu))
+    mixed = pktgen.imix(20000, v4routes=routes, v6routes=v6, device=gpu, seed=80)
+    seq = [uni, uni, sparse, uni, runs, uni, uni, mixed, sparse]
+    try:
+        ccl.set_tuning(cnet_spec=256, spec_types=types)  # also resets the node state
+        st = np.zeros(1, np.uint16)
+        for k, fr in enumerate(seq):
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=256, spec_state=st)
+            o = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+            ccl.classify(fr, N.CNDP_MODE_CNET, out=o)
+            torch.cuda.synchronize()
+            assert_same(o, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_types=0)
+
+
 def test_cnet_speculation_local_and_full(cnet, gpu):
     """The local pass resolves a chunk from the last universal group of the
     chunk before it; chunks behind single-type runs (no universal group) are
