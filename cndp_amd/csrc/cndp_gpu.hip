@@ -1584,6 +1584,10 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #define CD_NIB 0
 #endif
 #define CD_TAB_WORDS (CD_NIB ? 2 * TAB_POS * 16 : TAB_POS * 256)
+// CD_HSKIP 1: no Toeplitz in a call that stores neither the hash nor the queue
+#ifndef CD_HSKIP
+#define CD_HSKIP 1
+#endif
 template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
 {
     const GAS T *g = (const GAS T *)p;
@@ -1602,7 +1606,7 @@ __device__ __forceinline__ bool spec_code_type(uint32_t pt)
     return pt == 0x111u || pt == 0x211u || pt == 0x141u || pt == 0x241u;
 }
 
-template <bool LNT, bool META, int P>
+template <bool LNT, bool META, bool CODES, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
                                         CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
@@ -1726,7 +1730,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         // adds nothing); positions past the v4 tuple only when the wave has v6.
         // Skipped when the call asks for neither the hash nor the queue
         // (launch-uniform; the bins of cnet mode do not use the queue).
-        if (a.hash || a.queue) {
+        if (!CD_HSKIP || a.hash || a.queue) {
             uint32_t V[9];
 #pragma unroll
             for (int k = 0; k < 9; k++)
@@ -1799,6 +1803,15 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         if (o.spec_nh) {
             if (bf && din && (!o.nh || (pe != 3u && pe != 4u)))
                 at32(o.spec_nh, ib) = eb >> 1;
+            if (!CODES && bf) {
+                // the last SPEC_TAIL bursts' types are read by spec_classes in
+                // this kernel's last block when it folds: write-through stores
+                if (a.wl_fold && ib >= a.tail_lo)
+                    __hip_atomic_store(&at16(o.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
+            }
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
             spec_mark(s_sf, bf && sg != last_sig, sg);
             last_sig = bf ? sg : last_sig;
@@ -1815,7 +1828,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 // passes never read a canonical tile's types) they go out as two
                 // ballots, 16 B a tile, instead of 128 B of types (k_spec_expand
                 // writes the types should this batch need them after all)
-                codes = a.spec_codes && om == 0ull && (t - wstep + 1u) * 64u <= a.spec_keep_lo &&
+                codes = CODES && om == 0ull && (t - wstep + 1u) * 64u <= a.spec_keep_lo &&
                         __ballot(ib < a.n && !spec_code_type(pt)) == 0ull;
                 if (codes) {
                     const uint64_t m6 = __ballot((pt & 0xf0u) == 0x40u), mu = __ballot((pt & 0xf00u) == 0x200u);
@@ -1834,9 +1847,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                         atomicOr(s_mx, 1u << 8);
                 }
             }
-            if (bf && !codes) {
-                // the last SPEC_TAIL bursts' types are read by spec_classes in
-                // this kernel's last block when it folds: write-through stores
+            if (CODES && bf && !codes) {
                 if (a.wl_fold && ib >= a.tail_lo)
                     __hip_atomic_store(&at16(o.spec_t16, ib), (uint16_t)pt, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1947,7 +1958,7 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
 
 // META: ptype / rxmeta outputs requested (without them the kernel keeps
 // 14 VGPRs and 18 spilled SGPRs fewer)
-template <bool LNT, bool META>
+template <bool LNT, bool META, bool CODES>
 __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
     __shared__ uint32_t s_t[CD_TAB_WORDS];
@@ -2001,10 +2012,10 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     uint32_t last_sig = 0xFFFFFFFFu;
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {
-        cd_trip<LNT, META, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
+        cd_trip<LNT, META, CODES, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
                         last_sig, &s_mx);
         if (jt + 1 < trips)
-            cd_trip<LNT, META, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
+            cd_trip<LNT, META, CODES, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
                             count, last_sig, &s_mx);
     }
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
@@ -5263,10 +5274,13 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 2u;
             if (gd > (uint64_t)c->num_cu * bpc)
                 gd = (uint64_t)c->num_cu * bpc;
-            static void (*const dfns[2][2])(KArgs, uint32_t) = {{k_cnet_defer<false, false>,
-                                                                 k_cnet_defer<false, true>},
-                                                                {k_cnet_defer<true, false>,
-                                                                 k_cnet_defer<true, true>}};
+            // [load_nt][meta out][codes] (codes with non-temporal loads only: load_nt 0
+            // is an A/B knob, and the codes only save stores)
+            static void (*const dfns[2][2][2])(KArgs, uint32_t) = {
+                {{k_cnet_defer<false, false, false>, k_cnet_defer<false, false, false>},
+                 {k_cnet_defer<false, true, false>, k_cnet_defer<false, true, false>}},
+                {{k_cnet_defer<true, false, false>, k_cnet_defer<true, false, true>},
+                 {k_cnet_defer<true, true, false>, k_cnet_defer<true, true, true>}}};
             const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
             a.spec_tile = B ? c->sp_tile : nullptr; // written by this kernel only
             // chunk lists (CNDP_TUNE_SPEC_LISTS): groups must be lane quads of the
@@ -5299,8 +5313,10 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 a.spec_codes = c->tune_spec_types == 2 ||
                                (c->tune_spec_types == 0 && c->sp_hint && ((volatile uint32_t *)c->sp_hint)[1]);
             }
-            hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0], dim3((uint32_t)gd), dim3(CT_THREADS),
-                               0, s, a, (uint32_t)n_tiles);
+            if (!c->tune_lnt)
+                a.spec_codes = 0;
+            hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0][a.spec_codes ? 1 : 0], dim3((uint32_t)gd),
+                               dim3(CT_THREADS), 0, s, a, (uint32_t)n_tiles);
             if (!a.wl_fold)
                 hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
             if (a.spec_codes) // the coded types, should the passes read them after all
