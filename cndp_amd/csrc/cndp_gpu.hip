@@ -1584,6 +1584,23 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #define CD_NIB 0
 #endif
 #define CD_TAB_WORDS (CD_NIB ? 2 * TAB_POS * 16 : TAB_POS * 256)
+// CD_STAMP 1 (diagnostic builds only): s_memtime stamps around cd_trip's
+// stages, summed per wave into cd_stamps (cndp_gpu_debug_stamps reads them)
+#ifndef CD_STAMP
+#define CD_STAMP 0
+#endif
+#if CD_STAMP
+#define CD_STAMP_WAVES 8192
+__device__ unsigned long long cd_stamps[CD_STAMP_WAVES * 8];
+#define CD_TS(k)                                                                                 \
+    do {                                                                                         \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();                                      \
+        acc[k] += now_ - acc[7];                                                                 \
+        acc[7] = now_;                                                                           \
+    } while (0)
+#else
+#define CD_TS(k) ((void)0)
+#endif
 // CD_HSKIP 1: no Toeplitz in a call that stores neither the hash nor the queue
 #ifndef CD_HSKIP
 #define CD_HSKIP 1
@@ -1611,7 +1628,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
                                         CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
                                         uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig,
-                                        uint32_t *s_mx)
+                                        uint32_t *s_mx, uint64_t *acc)
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
     const uint32_t t = t0 + jt * wstep;
@@ -1646,6 +1663,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             more = more & ((eb & 1u) != 0u) & (rem != 0u);
         }
     }
+    CD_TS(0); // B's chain
     // A: tile c
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1779,6 +1797,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
             tb0 = a.dir16 ? a.dir16 : a.tbl24;
         na.ptf = pt | flags | (1u << 18) | (pe << 19);
     }
+    CD_TS(1); // A's tile, parse, hash
     // (the ablation's stand-in has bit 0 clear: no chain level follows it)
     na.e = (CD_ABL & 4) ? (idx0 & 0xffu) << 1 : tb0[idx0]; // first gather, unconditional
     // offsets one tile further, then the windows of tile c+2 (issued after
@@ -1789,6 +1808,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
         cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
     }
+    CD_TS(2); // gather, offsets and windows issued
     // B's results
     {
         const KAS KArgs &o = kargs_fresh(a);
@@ -1881,6 +1901,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     off.o0 = off.o1;
     off.o1 = off.o2;
     off.o2 = off.o3;
+    CD_TS(3); // B's results stored
 }
 
 // With a.wl_fold, k_cnet_defer ends the way k_classify_cnet<true> does, so
@@ -2010,14 +2031,28 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     sb.ptf = sb.h = sb.e = sb.rx = 0;
     sb.q0 = sb.q1 = sb.q2 = sb.q3 = 0;
     uint32_t last_sig = 0xFFFFFFFFu;
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if CD_STAMP
+    acc[7] = __builtin_amdgcn_s_memtime();
+    acc[6] = acc[7];
+#endif
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {
         cd_trip<LNT, META, CODES, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
-                        last_sig, &s_mx);
+                        last_sig, &s_mx, acc);
         if (jt + 1 < trips)
             cd_trip<LNT, META, CODES, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
-                            count, last_sig, &s_mx);
+                            count, last_sig, &s_mx, acc);
     }
+#if CD_STAMP
+    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES) {
+        unsigned long long *o = cd_stamps + (blockIdx.x * CT_WAVES + wv) * 8u;
+        for (int k = 0; k < 4; k++)
+            o[k] = acc[k];
+        o[4] = acc[7] - acc[6]; // the loop
+        o[5] = trips;
+    }
+#endif
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
         // the wave's non-canonical tiles (its own tile words, its own types)
         __threadfence_block();
@@ -7838,5 +7873,18 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         return -EINVAL;
     }
 }
+
+#if CD_STAMP
+// diagnostic builds: the per-wave stage sums of the last k_cnet_defer launch
+// (8 words a wave: chain, parse, issue, stores, loop, trips)
+extern "C" int cndp_gpu_debug_stamps(unsigned long long *out, uint32_t n)
+{
+    if (n > CD_STAMP_WAVES * 8)
+        n = CD_STAMP_WAVES * 8;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(cd_stamps), (size_t)n * 8));
+    return 0;
+}
+#endif
 
 extern "C" const char *cndp_gpu_version(void) { return CNDP_VERSION; }
