@@ -1875,6 +1875,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                     __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
             }
         }
+        CD_TS(4); // B's speculation words (types, tile word, signature flags)
         if (bf) {
             const uint32_t q = s_reta[sb.h & a.reta_mask];
             if (META && o.ptype)
@@ -2051,6 +2052,7 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
             o[k] = acc[k];
         o[4] = acc[7] - acc[6]; // the loop
         o[5] = trips;
+        o[6] = acc[4];
     }
 #endif
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {

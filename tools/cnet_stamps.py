@@ -17,8 +17,12 @@ import bench  # noqa: E402
 from cndp_amd import native as N  # noqa: E402
 
 dev = torch.device("cuda:0")
-for cfg in sys.argv[1:] or ["c4", "c5"]:
+for arg in sys.argv[1:] or ["c4", "c5"]:
+    cfg, _, opt = arg.partition(":")  # c4:nobins -- no bin counters
     st = bench.build_state(cfg, dev, 0, None)
+    if opt == "nobins":
+        for _, o in st["ring"]:
+            o["bins"] = None
     for k in range(6):
         bench.run_step(st, None, k)
     torch.cuda.synchronize()
@@ -26,10 +30,10 @@ for cfg in sys.argv[1:] or ["c4", "c5"]:
     assert N.lib().cndp_gpu_debug_stamps(buf.ctypes.data_as(__import__("ctypes").c_void_p), buf.size) == 0
     w = buf.reshape(-1, 8).astype(np.float64)
     w = w[w[:, 5] > 0]
-    per = w[:, :5] / w[:, 5:6]
+    per = w[:, [0, 1, 2, 6, 3, 4]] / w[:, 5:6]
     m = per.mean(axis=0)
-    print(f"{cfg}: {len(w)} waves, {w[:, 5].mean():.1f} trips a wave; cycles a trip: chain {m[0]:.0f}, "
-          f"tile+parse+hash {m[1]:.0f}, issue {m[2]:.0f}, stores {m[3]:.0f}; loop {m[4]:.0f} "
-          f"(sum {m[:4].sum():.0f})", flush=True)
+    print(f"{arg}: {len(w)} waves, {w[:, 5].mean():.1f} trips a wave; cycles a trip: chain {m[0]:.0f}, "
+          f"tile+parse+hash {m[1]:.0f}, issue {m[2]:.0f}, speculation words {m[3]:.0f}, result stores "
+          f"{m[4]:.0f}; loop {m[5]:.0f} (sum {m[:5].sum():.0f})", flush=True)
     del st
     torch.cuda.empty_cache()
