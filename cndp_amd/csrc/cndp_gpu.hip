@@ -1614,6 +1614,10 @@ template <class T> __device__ __forceinline__ const GAS T *sgpr_pin(const T *p)
     return g;
 }
 
+struct SigCache { // wave-uniform: 4 signatures already marked, round-robin slot
+    uint32_t s0, s1, s2, s3, next;
+};
+
 // the four packet types a canonical tile holds (spec_canon): Ethernet + IPv4 /
 // IPv6 (0x11 / 0x41) with TCP / UDP (0x100 / 0x200, pktmbuf_ptype.h), coded as
 // IPv6 bit | UDP bit; SPEC_TW_CODES marks a tile whose types went out coded
@@ -1627,7 +1631,7 @@ template <bool LNT, bool META, bool CODES, int P>
 __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
                                         uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
                                         CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
-                                        uint32_t *s_bins, uint32_t *s_sf, bool count, uint32_t &last_sig,
+                                        uint32_t *s_bins, uint32_t *s_sf, bool count, SigCache &sc,
                                         uint32_t *s_mx, uint64_t *acc)
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
@@ -1833,8 +1837,22 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                     __builtin_nontemporal_store((uint16_t)pt, &at16(o.spec_t16, ib));
             }
             const uint32_t sg = ((pt & 0xffu) << 3) | pe; // spec_sig(pt)
-            spec_mark(s_sf, bf && sg != last_sig, sg);
-            last_sig = bf ? sg : last_sig;
+            // sc: signatures this wave already put in the block's flag set
+            // (wave-uniform; the set only grows within a call): only a frame of
+            // another signature marks (IMIX: the first trips only; the mark is
+            // a loop of cross-lane reductions)
+            const bool on = bf && sg != sc.s0 && sg != sc.s1 && sg != sc.s2 && sg != sc.s3;
+            const unsigned long long mo = __ballot(on);
+            if (mo) {
+                spec_mark(s_sf, on, sg);
+                const uint32_t ns = (uint32_t)__builtin_amdgcn_readlane((int)sg, (int)(__ffsll(mo) - 1));
+                const uint32_t k = sc.next & 3u;
+                sc.s0 = k == 0u ? ns : sc.s0;
+                sc.s1 = k == 1u ? ns : sc.s1;
+                sc.s2 = k == 2u ? ns : sc.s2;
+                sc.s3 = k == 3u ? ns : sc.s3;
+                sc.next++;
+            }
             bool codes = false;
             if (o.spec_tile && bv) {
                 // the tile's word for the speculation passes (spec_canon): 1 when
@@ -2031,7 +2049,7 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     CdLane sb;
     sb.ptf = sb.h = sb.e = sb.rx = 0;
     sb.q0 = sb.q1 = sb.q2 = sb.q3 = 0;
-    uint32_t last_sig = 0xFFFFFFFFu;
+    SigCache sig_cache{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u};
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #if CD_STAMP
     acc[7] = __builtin_amdgcn_s_memtime();
@@ -2040,10 +2058,10 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {
         cd_trip<LNT, META, CODES, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
-                        last_sig, &s_mx, acc);
+                        sig_cache, &s_mx, acc);
         if (jt + 1 < trips)
             cd_trip<LNT, META, CODES, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
-                            count, last_sig, &s_mx, acc);
+                            count, sig_cache, &s_mx, acc);
     }
 #if CD_STAMP
     if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES) {
