@@ -1171,6 +1171,31 @@ __device__ __forceinline__ void cnet_lut_fill(uint16_t *lut, uint32_t tid, uint3
     for (uint32_t k = tid; k < CNET_LUT_N / 2; k += nthr) // two entries per 4-B copy
         ((uint32_t *)lut)[k] = ((const uint32_t *)g_cnet_lut.v)[k];
 }
+// the same copy in two halves for 256-thread blocks: the loads at a kernel's
+// start, in flight with its other first loads, the LDS stores later
+struct LutRegs {
+    uint32_t v[3];
+};
+__device__ __forceinline__ LutRegs cnet_lut_load256(uint32_t tid)
+{
+    static_assert(CNET_LUT_N / 2 <= 3 * 256, "three words a thread");
+    LutRegs r;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; j++) {
+        const uint32_t k = tid + 256u * j;
+        r.v[j] = k < CNET_LUT_N / 2 ? ((const uint32_t *)g_cnet_lut.v)[k] : 0u;
+    }
+    return r;
+}
+__device__ __forceinline__ void cnet_lut_store256(uint16_t *lut, uint32_t tid, const LutRegs &r)
+{
+#pragma unroll
+    for (uint32_t j = 0; j < 3; j++) {
+        const uint32_t k = tid + 256u * j;
+        if (k < CNET_LUT_N / 2)
+            ((uint32_t *)lut)[k] = r.v[j];
+    }
+}
 __device__ __forceinline__ uint32_t cnet_lut_x(const uint16_t *lut, uint32_t l)
 {
     const uint32_t h = (l >> 8) & 0xffu;
@@ -1591,7 +1616,16 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #endif
 #if CD_STAMP
 #define CD_STAMP_WAVES 8192
-__device__ unsigned long long cd_stamps[CD_STAMP_WAVES * 8];
+__device__ unsigned long long cd_stamps[CD_STAMP_WAVES * 16];
+// k_spec_local_t per block (start, inputs in, tables filled, end, path) and
+// k_spec_fallback's block 0 (start, end) at [SP_STAMP_BLOCKS * 16]
+#define SP_STAMP_BLOCKS 4096
+__device__ unsigned long long sp_stamps[SP_STAMP_BLOCKS * 16 + 8];
+#define SP_TS(k, v)                                                                              \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < SP_STAMP_BLOCKS)                                    \
+            sp_stamps[blockIdx.x * 16u + (k)] = (v);                                              \
+    } while (0)
 #define CD_TS(k)                                                                                 \
     do {                                                                                         \
         const uint64_t now_ = __builtin_amdgcn_s_memtime();                                      \
@@ -1599,6 +1633,7 @@ __device__ unsigned long long cd_stamps[CD_STAMP_WAVES * 8];
         acc[7] = now_;                                                                           \
     } while (0)
 #else
+#define SP_TS(k, v) ((void)0)
 #define CD_TS(k) ((void)0)
 #endif
 // CD_HSKIP 1: no Toeplitz in a call that stores neither the hash nor the queue
@@ -1956,6 +1991,11 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
         s_last = last;
     }
     __syncthreads();
+#if CD_STAMP
+    if ((threadIdx.x & 63u) == 0 && blockIdx.x * CT_WAVES + (threadIdx.x >> 6) < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * CT_WAVES + (threadIdx.x >> 6)) * 16u + 14u] =
+            __builtin_amdgcn_s_memrealtime() | ((uint64_t)s_last << 63); // ticket taken (bit 63: the last block)
+#endif
     if (!s_last)
         return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -2045,6 +2085,9 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     if (count)
         for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
             s_bins[k] = 0;
+#if CD_STAMP
+    const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime(); // after the prologue's issue
+#endif
     __syncthreads();
     CdLane sb;
     sb.ptf = sb.h = sb.e = sb.rx = 0;
@@ -2054,6 +2097,7 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
 #if CD_STAMP
     acc[7] = __builtin_amdgcn_s_memtime();
     acc[6] = acc[7];
+    const uint64_t rt_loop = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint32_t trips = nt_w ? nt_w + 1 : 0;
     for (uint32_t jt = 0; jt < trips; jt += 2) {
@@ -2065,12 +2109,15 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     }
 #if CD_STAMP
     if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES) {
-        unsigned long long *o = cd_stamps + (blockIdx.x * CT_WAVES + wv) * 8u;
+        unsigned long long *o = cd_stamps + (blockIdx.x * CT_WAVES + wv) * 16u;
         for (int k = 0; k < 4; k++)
             o[k] = acc[k];
         o[4] = acc[7] - acc[6]; // the loop
         o[5] = trips;
         o[6] = acc[4];
+        o[8] = rt_entry; // s_memrealtime (100 MHz): prologue issued, loop start, loop end
+        o[9] = rt_loop;
+        o[10] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
@@ -2086,6 +2133,10 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
             }
         }
     }
+#if CD_STAMP
+    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * CT_WAVES + wv) * 16u + 12u] = __builtin_amdgcn_s_memrealtime(); // odd tiles done
+#endif
     if (count || a.spec_flags || (a.spec_allow & SPEC_ALLOW_LISTS))
         __syncthreads();
     if (count)
@@ -2096,11 +2147,19 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
         atomicOr(&a.spec_flags[tid], s_sf[tid]);
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && tid == 0 && s_mx)
         atomicOr(&a.spec_meta[SPEC_MX], s_mx);
+#if CD_STAMP
+    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * CT_WAVES + wv) * 16u + 13u] = __builtin_amdgcn_s_memrealtime(); // flushes issued
+#endif
     if (a.wl_fold)
         // (the general parse takes the byte tables: from LDS, or global memory
         // when LDS holds the nibble tables)
         cnet_defer_tail<CT_THREADS, 256>(a, (uint32_t *)&s_tile[0][0], CD_NIB ? a.ttab : s_t, s_reta, s_bins, s_sf,
                                          count);
+#if CD_STAMP
+    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * CT_WAVES + wv) * 16u + 11u] = __builtin_amdgcn_s_memrealtime(); // the wave's end
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2141,11 +2200,6 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
 #define SPEC_NOLOCAL 132 // one low byte only: no universal group exists, k_spec_local is skipped
 #define SPEC_UNIF 133 // every type has the entering state's low byte: k_spec_local's uniform pass only
 #define SPEC_ERR 134  // a k_spec_fallback barrier poll expired (diagnostic; sticky)
-// chunks k_spec_local_t leaves to k_spec_fallback (entering state known, types
-// needed): 8 lists, one per block % 8 (the arrivals spread over 8 words, each
-// 128 B from the others and from the meta words every wave reads), list x's
-// count at meta[SPEC_RCNT + 32 x], its entries (chunk, state) at R + x * 2 * nch
-#define SPEC_RCNT 640
 #define SPEC_HINT 900 // the hint words last written to host memory
 #define SPEC_TAIL 16
 // a type another block of the running kernel stored (write-through, agent
@@ -2178,8 +2232,6 @@ __device__ __forceinline__ void spec_classes(uint32_t t, uint32_t *flags, uint8_
     const uint32_t wl_cnt = wl_n ? __hip_atomic_load(wl_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     const uint32_t prev = meta[-1], hint_h0 = meta[SPEC_HINT], hint_h1 = meta[SPEC_HINT + 1];
     const uint32_t f = __hip_atomic_load(&flags[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t < 8)
-        meta[SPEC_RCNT + 32 * t] = 0;
     const uint32_t s_in = prev & 0xffffu, g0 = spec_sig(s_in); // the node state entering the batch
     if (t == 0) {
         meta[SPEC_IN] = s_in;
@@ -2984,6 +3036,7 @@ __device__ __forceinline__ void spec_replay(const KArgs &a, uint32_t B, uint64_t
 {
     uint32_t fm, fe;
     spec_replay_walk<CH>(a, B, c0, c1, s0, lane, st, fm, fe);
+    SP_TS(8, __builtin_amdgcn_s_memrealtime());
     spec_replay_fix<CH>(a, B, c0, lane, st, fm, fe, lbins);
 }
 
@@ -3056,6 +3109,7 @@ __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uin
             }
         }
         s0 = ng ? __shfl(nxt, (int)ng - 1) : s0;
+        SP_TS(10 + (uint32_t)(bb - c0), __builtin_amdgcn_s_memrealtime());
     }
 }
 
@@ -3314,8 +3368,10 @@ __device__ __forceinline__ void spec_chunk_types_v(const KArgs &a, uint32_t B, u
         *(u32x4 *)(st + idx + 4) = (u32x4){o[4], o[5], o[6], o[7]};
     }
     __builtin_amdgcn_wave_barrier();
+    SP_TS(7, __builtin_amdgcn_s_memrealtime());
     if (!spec_chunk_quiet(spec_summary(em & ~(1ull << 63)), s0))
         spec_replay<CH>(a, B, c0, c1, s0, lane, st, lbins);
+    SP_TS(9, __builtin_amdgcn_s_memrealtime());
 }
 
 template <int CH, int WPB>
@@ -3450,18 +3506,47 @@ __device__ __forceinline__ void spec_chunk_pre(const KArgs &a, uint32_t B, uint6
     }
 }
 
+// k_spec_local_t's body: bid / nblk stand for blockIdx.x / gridDim.x; LDS:
+// s_bins (CNDP_BINS_MAX + 2 ints), s_lut (CNET_LUT_N), s_stw (this wave's
+// CH * 256 staged types)
 template <int CH>
-__global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
-                                                      uint8_t *done, uint32_t *R)
+__device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+                                                uint8_t *done, uint32_t bid, uint32_t nblk, int *s_bins,
+                                                uint16_t *s_lut, uint32_t *s_stw)
 {
     static_assert(CH == SPEC_CH, "spec_chunk_pre");
-    __shared__ int s_bins[CNDP_BINS_MAX + 2]; // the uniform pass's / listed chunks' bin moves
-    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
-    __shared__ __attribute__((aligned(16))) uint32_t s_st[4][CH * 256]; // a listed chunk's types
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // wave-uniform in SGPRs (the chunk index and all that derives from it)
-    const uint64_t wid = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wv), W = (uint64_t)gridDim.x * 4;
+    const uint64_t wid = (uint64_t)bid * 4 + __builtin_amdgcn_readfirstlane(wv), W = (uint64_t)nblk * 4;
+    // the prologue's inputs in one round trip: every meta word it decides on,
+    // the chunk list's count and this wave's entry (read past the count and
+    // ignored there), and for wave 0 the batch's last burst (the final state)
+    // -- independent loads, waited for together
+    const LutRegs lr = cnet_lut_load256(threadIdx.x);
     const uint32_t unif = meta[SPEC_UNIF], s_in = meta[SPEC_IN] & 0xffffu;
+    const uint32_t m_stop = meta[SPEC_SKIP] | meta[SPEC_NOLOCAL], mx = meta[SPEC_MX], K = meta[0];
+    const uint32_t sig = lane < SPEC_KMAX ? meta[1 + lane] : 0u;
+    const uint32_t *const cwl = a.spec_cwl ? a.spec_cwl : meta;
+    const uint32_t nl_w = cwl[0], lc_w = a.spec_cwl && wid < nch ? cwl[1 + wid] : 0u;
+    uint32_t fq0 = 0u, fq1 = 0u;
+    if (wid == 0) { // wave-uniform
+        const uint64_t fb0 = (nb - 1) * B;
+        spec_group_regs(a.spec_t16, fb0, (uint32_t)((uint64_t)a.n - fb0 < B ? (uint64_t)a.n - fb0 : B), lane, fq0, fq1);
+    }
+    SP_TS(0, __builtin_amdgcn_s_memrealtime());
+    asm volatile("" ::"s"(unif), "s"(s_in), "s"(m_stop), "s"(mx), "s"(K), "v"(sig), "s"(nl_w), "s"(lc_w));
+    SP_TS(1, __builtin_amdgcn_s_memrealtime());
+    SP_TS(4, unif ? 1u : m_stop ? 2u : 5u);
+    SP_TS(2, 0u);
+    SP_TS(3, 0u);
+    SP_TS(6, 0u);
+    SP_TS(7, 0u);
+    SP_TS(8, 0u);
+    SP_TS(9, 0u);
+    SP_TS(10, 0u);
+    SP_TS(11, 0u);
+    SP_TS(12, 0u);
+    SP_TS(13, 0u);
     if (unif) { // block-uniform
         const uint32_t T = s_in, E = cnet_edge(T);
         const bool tcan = spec_canon(T & 0xffu) == E;
@@ -3508,26 +3593,36 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     // low bytes present), a frame can leave by another edge only inside a
     // chunk the fast kernel listed, so only those are looked at (grid-uniform)
     // (SPEC_UNIF implies no SPEC_SKIP; SPEC_NOLOCAL without it: nothing here)
-    if (meta[SPEC_SKIP] || meta[SPEC_NOLOCAL])
+    if (m_stop)
         return;
     bool lists = false;
     if (a.spec_cwl) {
-        const uint32_t mx = meta[SPEC_MX], M = mx & 0xffu, e_in = cnet_edge(s_in), cn = spec_canon(s_in & 0xffu);
+        const uint32_t M = mx & 0xffu, e_in = cnet_edge(s_in), cn = spec_canon(s_in & 0xffu);
         lists = !(mx >> 8) && (cn == 0xFFu || cn == e_in) && !((M >> e_in) & 1u);
         if (lists) { // a state of another low byte whose edge is in M could take such a 4th type
-            const uint32_t K = meta[0], sig = lane < K && lane < SPEC_KMAX ? meta[1 + lane] : 0u;
-            const bool clash = lane < K && (sig >> 3) != 0x11u && (sig >> 3) != 0x41u && ((M >> (sig & 7u)) & 1u);
+            const bool clash = lane < K && lane < SPEC_KMAX && (sig >> 3) != 0x11u && (sig >> 3) != 0x41u &&
+                               ((M >> (sig & 7u)) & 1u);
             lists = K <= SPEC_KMAX && __ballot(clash) == 0ull;
         }
     }
     // the lists' blocks without a listed chunk (block 0 also walks the final
     // state) leave before the table fill: most of the grid, block-uniform
-    const uint32_t nl = lists ? a.spec_cwl[0] : 0u;
-    if (lists && blockIdx.x != 0 && (uint64_t)blockIdx.x * 4 >= nl)
+    const uint32_t nl = lists ? nl_w : 0u;
+    SP_TS(4, lists ? ((uint64_t)bid * 4 < nl ? 4u : 3u) : 5u);
+    SP_TS(5, nl);
+    if (lists && bid != 0 && (uint64_t)bid * 4 >= nl)
         return;
-    uint32_t tw = 1u, pq0 = 0u, pq1 = 0u;
-    if (!lists)
-        spec_chunk_pre(a, B, nch, wid, lane, tw, pq0, pq1);
+    // without the lists: the first SPEC_LQ chunks' tile words and previous
+    // bursts, all in flight during the table fill (one round trip for the
+    // wave's chunks at the host's grid; a ring of SPEC_LQ at a smaller one)
+    uint32_t tws[SPEC_LQ], q0s[SPEC_LQ], q1s[SPEC_LQ];
+#pragma unroll
+    for (int k = 0; k < SPEC_LQ; k++) {
+        tws[k] = 1u;
+        q0s[k] = q1s[k] = 0u;
+        if (!lists)
+            spec_chunk_pre(a, B, nch, wid + k * W, lane, tws[k], q0s[k], q1s[k]);
+    }
     // lists: the wave's first listed chunk -- its types and the burst before
     // it -- in flight during the table fill
     constexpr uint32_t LR = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
@@ -3536,24 +3631,24 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
     uint32_t lq0 = 0u, lq1 = 0u;
     uint64_t lc = 0;
     if (lists && wid < nl) {
-        lc = a.spec_cwl[1 + wid];
+        lc = lc_w;
         const uint64_t c0 = lc * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
         if (lvec)
             spec_chunk_load<CH>(a, B, c0, c1, lane, lv);
         if (lc > 0)
             spec_group_regs(a.spec_t16, (c0 - 1) * B, B, lane, lq0, lq1);
     }
-    cnet_lut_fill(s_lut, threadIdx.x, 256);
+    cnet_lut_store256(s_lut, threadIdx.x, lr);
     const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
-    if (lists)
-        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
-            s_bins[k] = 0;
+    for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+        s_bins[k] = 0;
     __syncthreads();
+    SP_TS(2, __builtin_amdgcn_s_memrealtime());
     if (lists) {
         if (wid == 0) { // the final node state (meta[-1]): the walk in the last chunk
             const uint64_t l0 = (nch - 1) * CH, l1 = l0 + CH < nb ? l0 + CH : nb;
             uint32_t sf = 0;
-            if (spec_lookback(a.spec_t16, a.n, B, l0, l1, lane, s_lut, sf)) {
+            if (spec_lookback(a.spec_t16, a.n, B, l0, l1, lane, s_lut, sf, true, fq0, fq1)) {
                 if (lane == 0)
                     meta[-1] = sf;
             } else if (lane == 0) {
@@ -3574,7 +3669,9 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
             const bool vec = lvec;
             const u32x4(&v)[LR] = lv;
             uint32_t s0 = s_in;
-            if (c > 0 && !spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, lq0, lq1)) {
+            const bool lb_ok = c == 0 || spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, lq0, lq1);
+            SP_TS(6, __builtin_amdgcn_s_memrealtime());
+            if (!lb_ok) {
                 if (lane == 0) { // left to the full passes (done[] of the others is not read)
                     done[c] = 0;
                     spec_flag_full(meta);
@@ -3582,9 +3679,9 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
                 continue;
             }
             if (vec)
-                spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr, v);
+                spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr, v);
             else
-                spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_st[wv], s_lut, a.bins ? s_bins : nullptr);
+                spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr);
             __builtin_amdgcn_wave_barrier();
             if (lane == 0)
                 done[c] = 1;
@@ -3593,11 +3690,19 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
         for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
             if (s_bins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)(long long)s_bins[k]);
+        SP_TS(3, __builtin_amdgcn_s_memrealtime());
         return;
     }
     for (uint64_t c = wid; c < nch; c += W) {
-        const uint32_t ctw = tw, cq0 = pq0, cq1 = pq1;
-        spec_chunk_pre(a, B, nch, c + W, lane, tw, pq0, pq1); // the next chunk's loads, in flight meanwhile
+        const uint32_t ctw = tws[0], cq0 = q0s[0], cq1 = q1s[0];
+#pragma unroll
+        for (int k = 0; k + 1 < SPEC_LQ; k++) {
+            tws[k] = tws[k + 1];
+            q0s[k] = q0s[k + 1];
+            q1s[k] = q1s[k + 1];
+        }
+        // the ring's next chunk, in flight meanwhile
+        spec_chunk_pre(a, B, nch, c + SPEC_LQ * W, lane, tws[SPEC_LQ - 1], q0s[SPEC_LQ - 1], q1s[SPEC_LQ - 1]);
         const uint64_t c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
         if (c == nch - 1) { // the final node state (meta[-1]; the entering one is meta[SPEC_IN])
             uint32_t sf = 0;
@@ -3619,17 +3724,29 @@ __global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint6
         }
         const uint32_t cn = spec_canon(s0 & 0xffu);
         if (odd || (cn != 0xFFu && cn != cnet_edge_l(s_lut, s0))) {
-            // its types decide: k_spec_fallback reads them (and replays) from
-            // the list, so this kernel carries no replay code (occupancy)
-            if (lane == 0) {
-                const uint32_t x = blockIdx.x & 7u, k = atomicAdd(&meta[SPEC_RCNT + 32 * x], 1u);
-                R[x * 2 * nch + 2 * k] = (uint32_t)c;
-                R[x * 2 * nch + 2 * k + 1] = s0;
-            }
+            // its types decide: read (one more round trip, this wave only) and
+            // replayed here, as k_spec_fallback would from a list
+            spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr);
+            __builtin_amdgcn_wave_barrier();
         }
         if (lane == 0)
             done[c] = 1;
     }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
+        if (s_bins[k])
+            atomicAdd(&a.bins[k], (unsigned long long)(long long)s_bins[k]);
+    SP_TS(3, __builtin_amdgcn_s_memrealtime());
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_local_t(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+                                                      uint8_t *done)
+{
+    __shared__ int s_bins[CNDP_BINS_MAX + 2]; // the uniform pass's / listed chunks' bin moves
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
+    __shared__ __attribute__((aligned(16))) uint32_t s_st[4][CH * 256]; // a listed chunk's types
+    spec_local_body<CH>(a, B, nb, nch, meta, done, blockIdx.x, gridDim.x, s_bins, s_lut, s_st[threadIdx.x >> 6]);
 }
 
 // CNDP_TUNE_SPEC_TYPES: the types of the tiles k_cnet_defer coded
@@ -3669,14 +3786,14 @@ __global__ __launch_bounds__(256) void k_spec_expand(KArgs a, uint32_t n_tiles, 
 // every block is resident; the poll is bounded all the same (meta[SPEC_ERR]
 // records an expiry: a wrong result, not a hung GPU).
 #define SPEC_ERR 134
-__device__ __forceinline__ void spec_grid_sync(uint32_t *bar, uint32_t gen, uint32_t *meta)
+__device__ __forceinline__ void spec_grid_sync(uint32_t *bar, uint32_t gen, uint32_t *meta, uint32_t nblk)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const uint32_t old = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == gen * gridDim.x - 1u) {
+        if (old == gen * nblk - 1u) {
             __hip_atomic_store(&bar[1], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             for (uint32_t it = 0; __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen; it++) {
@@ -3692,37 +3809,33 @@ __device__ __forceinline__ void spec_grid_sync(uint32_t *bar, uint32_t gen, uint
     __syncthreads();
 }
 
-// The general resolution, for what k_spec_local leaves (meta[SPEC_FULL]) or
-// for everything (gated == 0, CNDP_TUNE_SPEC_SCAN forced): one persistent
-// launch, one block of 4 waves per CU, three phases split by grid barriers --
-//   tables  every chunk's map over the signature classes and its summary,
-//   scan    the chunk maps composed (blocks of SPEC_BLK chunks, then block 0
-//           composes the block totals into block start states and the final
-//           node state; more than SPEC_KMAX classes: block 0's thread 0
-//           walks the bursts in order instead),
-//   replay  each chunk k_spec_local did not resolve, from its entering state.
-// With nothing left to resolve it returns at once (one launch of ~256 empty
-// blocks instead of three gated launches).
+// k_spec_fallback's body: bid / nblk stand for blockIdx.x / gridDim.x; LDS: s_m (the scan's rows, which the
+// tables / replay staging reuse), s_carry, s_lut, s_cls.  Block 0 also empties
+// the fast kernel's chunk list for the next call.
 template <int CH>
-__global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
-                                                       const uint8_t *class_id, uint32_t *T, uint32_t *P,
-                                                       uint32_t *Bt, uint32_t *Sblk, uint32_t *S, const uint8_t *done,
-                                                       uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated,
-                                                       const uint32_t *R)
+__device__ __forceinline__ void spec_fallback_body(const KArgs &a, uint32_t B, uint64_t nb, uint64_t nch,
+                                                   uint32_t *meta, const uint8_t *class_id, uint32_t *T, uint32_t *P,
+                                                   uint32_t *Bt, uint32_t *Sblk, uint32_t *S, const uint8_t *done,
+                                                   uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated,
+                                                   uint32_t bid, uint32_t nblk, uint32_t *s_m, uint32_t *s_carry,
+                                                   uint16_t *s_lut, uint8_t *s_cls)
 {
-    // the scan's rows; the tables / replay staging reuse the same bytes
-    __shared__ __attribute__((aligned(16))) uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
-    __shared__ uint32_t s_carry[SPEC_KMAX];
-    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
-    __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
-    // the replays' bin moves, one global atomic per bin and block at the end
-    // (the moves of re-routed frames mostly leave one bin: same-address
-    // device atomics serialize, ~1 µs per hundred)
-    __shared__ int s_lb[CNDP_BINS_MAX + 2];
     static_assert(SPEC_BLK * (SPEC_KMAX + 1) >= 4 * CH * 256, "staging fits the scan rows");
-    if (blockIdx.x == 0 && a.spec_cwl) { // the fast kernel's chunk list and SPEC_MX, empty for the next call
-        const uint32_t nl = a.spec_cwl[0];
-        for (uint32_t k = threadIdx.x; k < nl; k += 256u)
+    // what this launch decides on, in one round trip: SPEC_FULL / SPEC_SKIP
+    // and (block 0) the chunk list's count with its first 256 entries (read
+    // past the count and ignored there)
+#if CD_STAMP
+    if (bid == 0 && threadIdx.x == 0)
+        sp_stamps[SP_STAMP_BLOCKS * 16] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint32_t m_full = meta[SPEC_FULL], m_skip = meta[SPEC_SKIP];
+    const bool clean = bid == 0 && a.spec_cwl;
+    const uint32_t nl = clean ? a.spec_cwl[0] : 0u;
+    const uint32_t e0 = clean && threadIdx.x < nch ? a.spec_cwl[1 + threadIdx.x] : 0u;
+    if (clean) { // the fast kernel's chunk list and SPEC_MX, empty for the next call
+        if (threadIdx.x < nl)
+            a.spec_cflag[e0] = 0u;
+        for (uint32_t k = threadIdx.x + 256u; k < nl; k += 256u)
             a.spec_cflag[a.spec_cwl[1 + k]] = 0u;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -3730,67 +3843,52 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
             meta[SPEC_MX] = 0u;
         }
     }
-    uint32_t rc[8], nrep = 0; // the 8 replay lists (k_spec_local_t)
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-        rc[x] = gated ? meta[SPEC_RCNT + 32 * x] : 0u;
-        nrep += rc[x];
+    const bool full = !gated || m_full;
+    if (bid == 0 && threadIdx.x == 0 && a.spec_hint && gated) {
+        // host hint [2]: whether this call ran the full passes (the next call's
+        // grid: one block while they are not needed -- any grid is correct)
+        const uint32_t h2 = !m_skip && full, old2 = meta[SPEC_HINT + 2];
+        if (h2 != old2) {
+            meta[SPEC_HINT + 2] = h2;
+            __hip_atomic_store(&a.spec_hint[2], h2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
-    const bool full = !gated || meta[SPEC_FULL];
-    if (meta[SPEC_SKIP] || (!full && nrep == 0)) // grid-uniform
+#if CD_STAMP
+    if (bid == 0 && threadIdx.x == 0) {
+        sp_stamps[SP_STAMP_BLOCKS * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+        sp_stamps[SP_STAMP_BLOCKS * 16 + 2] = (uint64_t)full << 32;
+    }
+#endif
+    if (m_skip || !full) // grid-uniform
         return;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t wv = threadIdx.x >> 6;
     const uint32_t K = meta[0];
     uint32_t *st = s_m + wv * (CH * 256);
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
-    const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
-    for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
-        s_lb[k] = 0;
     __syncthreads();
-    const uint64_t W = (uint64_t)gridDim.x * 4, wid = (uint64_t)blockIdx.x * 4 + wv;
-    // the chunks k_spec_local_t listed (their entering states known): types,
-    // then a replay where a frame can move -- before the full passes, which
-    // leave these chunks alone (done[c] = 1)
-    for (uint64_t k = wid; k < nrep; k += W) {
-        uint32_t x = 0, j = (uint32_t)k; // entry j of list x
-        while (j >= rc[x]) // uniform
-            j -= rc[x++];
-        const uint32_t *e = R + x * 2 * nch + 2 * j;
-        const uint64_t c = e[0], c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-        spec_chunk_types<CH>(a, B, c0, c1, e[1], lane, st, s_lut, a.bins ? s_lb : nullptr);
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (nrep) { // block-uniform
-        __syncthreads();
-        for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
-            if (s_lb[k])
-                atomicAdd(&a.bins[k], (unsigned long long)(long long)s_lb[k]);
-    }
-    if (!full)
-        return;
-    __syncthreads(); // the staging rows become the scan's
+    const uint64_t W = (uint64_t)nblk * 4;
     if (K <= SPEC_KMAX)
-        for (uint64_t c = (uint64_t)blockIdx.x * 4 + wv; c < nch; c += W) {
+        for (uint64_t c = (uint64_t)bid * 4 + wv; c < nch; c += W) {
             spec_ctable_chunk<CH>(a.spec_t16, a.n, B, nb, nch, c, K, meta, T, st, s_lut, s_cls);
             __builtin_amdgcn_wave_barrier();
         }
-    spec_grid_sync(bar, 1, meta);
-    const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
-    for (uint64_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+    spec_grid_sync(bar, 1, meta, nblk);
+    const uint64_t nblk_s = (nch + SPEC_BLK - 1) / SPEC_BLK;
+    for (uint64_t vb = bid; vb < nblk_s; vb += nblk) {
         if (K <= kfast)
             spec_scan_a_body<SPEC_KFAST>(s_m, nch, K, T, P, Bt, vb);
         else if (K <= kmax)
             spec_scan_a_body<SPEC_KMAX>(s_m, nch, K, T, P, Bt, vb);
         __syncthreads();
     }
-    spec_grid_sync(bar, 2, meta);
-    if (blockIdx.x == 0) {
+    spec_grid_sync(bar, 2, meta, nblk);
+    if (bid == 0) {
         uint32_t *state = meta - 1;
         if (K <= kfast) {
-            spec_scan_c_body<SPEC_KFAST, SPEC_BLK>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+            spec_scan_c_body<SPEC_KFAST, SPEC_BLK>(s_m, s_carry, nblk_s, K, class_id, Bt, Sblk, state);
         } else if (K <= kmax) {
-            spec_scan_c_body<SPEC_KMAX, SPEC_BLK>(s_m, s_carry, nblk, K, class_id, Bt, Sblk, state);
+            spec_scan_c_body<SPEC_KMAX, SPEC_BLK>(s_m, s_carry, nblk_s, K, class_id, Bt, Sblk, state);
         } else if (threadIdx.x == 0) {
             uint32_t s = meta[SPEC_IN] & 0xffffu;
             for (uint64_t b = 0; b < nb; b++) {
@@ -3804,13 +3902,37 @@ __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint
             *state = s;
         }
     }
-    spec_grid_sync(bar, 3, meta);
+    spec_grid_sync(bar, 3, meta, nblk);
     const bool all = !gated || meta[SPEC_NOLOCAL];
-    for (uint64_t c = (uint64_t)blockIdx.x * 4 + wv; c < nch; c += W) {
+    for (uint64_t c = (uint64_t)bid * 4 + wv; c < nch; c += W) {
         if (all || !done[c])
             spec_cemit_chunk<CH>(a, B, nb, nch, c, meta, P, Sblk, S, T, kfast, kmax, st, s_lut);
         __builtin_amdgcn_wave_barrier();
     }
+}
+
+// The general resolution, for what the local pass leaves (meta[SPEC_FULL]) or
+// for everything (gated == 0, CNDP_TUNE_SPEC_SCAN forced): one persistent
+// launch, one block of 4 waves per CU, three phases split by grid barriers --
+//   tables  every chunk's map over the signature classes and its summary,
+//   scan    the chunk maps composed (blocks of SPEC_BLK chunks, then block 0
+//           composes the block totals into block start states and the final
+//           node state; more than SPEC_KMAX classes: block 0's thread 0
+//           walks the bursts in order instead),
+//   replay  each chunk the local pass did not resolve, from its entering state.
+// With nothing left to resolve it returns at once.
+template <int CH>
+__global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
+                                                       const uint8_t *class_id, uint32_t *T, uint32_t *P,
+                                                       uint32_t *Bt, uint32_t *Sblk, uint32_t *S, const uint8_t *done,
+                                                       uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
+    __shared__ uint32_t s_carry[SPEC_KMAX];
+    __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
+    spec_fallback_body<CH>(a, B, nb, nch, meta, class_id, T, P, Bt, Sblk, S, done, bar, kfast, kmax, gated, blockIdx.x,
+                           gridDim.x, s_m, s_carry, s_lut, s_cls);
 }
 
 // ---------------------------------------------------------------------------
@@ -4072,11 +4194,11 @@ struct cndp_gpu_ctx {
     uint8_t *sp_done;     // per chunk: resolved by k_spec_local
     uint32_t *sp_cwl;     // chunks the fast kernel lists ([0] = count), CNDP_TUNE_SPEC_LISTS
     uint32_t *sp_cflag;   // per chunk: listed this call (cleared by k_spec_fallback)
-    uint32_t *sp_R;       // chunks k_spec_local_t leaves to k_spec_fallback: (chunk, entering state)
     uint8_t *sp_tile;     // per 64-frame tile: the main kernel's canonical-tile word
     uint8_t *sp_c2;       // per 64-frame tile: 16 B of type codes (CNDP_TUNE_SPEC_TYPES)
     int tune_spec_types;  // CNDP_TUNE_SPEC_TYPES: 0 auto, 1 always the types, 2 always codes
-    uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch uniform
+    uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch
+                                   // uniform, [2] the last call ran the full speculation passes
     uint64_t sp_n_cap, sp_b_cap;
     // host-batch pipeline (cndp_gpu_classify_host): device mirrors, grown on demand
     hipStream_t hs[3];    // copy-in, classify, copy-out
@@ -4275,7 +4397,7 @@ extern "C" void cndp_gpu_fini(cndp_gpu_ctx_t *c)
     if (c->d_rw_tbl)
         hipFree(c->d_rw_tbl);
     void *sp[] = {c->sp_small, c->sp_class, c->sp_pt,   c->sp_nh,  c->sp_S,    c->sp_T,
-                  c->sp_U,     c->sp_done,  c->sp_tile, c->sp_R,   c->sp_cwl, c->sp_cflag, c->sp_c2};
+                  c->sp_U,     c->sp_done,  c->sp_tile, c->sp_cwl, c->sp_cflag, c->sp_c2};
     for (void *q : sp)
         if (q)
             hipFree(q);
@@ -5160,13 +5282,11 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
             HIP_TRY(hipFree(c->sp_U));
         if (c->sp_done)
             HIP_TRY(hipFree(c->sp_done));
-        if (c->sp_R)
-            HIP_TRY(hipFree(c->sp_R));
         if (c->sp_cwl)
             HIP_TRY(hipFree(c->sp_cwl));
         if (c->sp_cflag)
             HIP_TRY(hipFree(c->sp_cflag));
-        c->sp_S = c->sp_T = c->sp_U = c->sp_R = c->sp_cwl = c->sp_cflag = nullptr;
+        c->sp_S = c->sp_T = c->sp_U = c->sp_cwl = c->sp_cflag = nullptr;
         c->sp_done = nullptr;
         c->sp_b_cap = 0;
         const uint64_t cap = nb + (nb >> 3) + 64;
@@ -5179,7 +5299,6 @@ static int spec_scratch(cndp_gpu_ctx_t *c, uint64_t n, uint64_t nb)
         HIP_TRY(hipMemset(c->sp_cflag, 0, cap * 4));
         const uint64_t ptrs[2] = {(uint64_t)(uintptr_t)c->sp_cwl, (uint64_t)(uintptr_t)c->sp_cflag};
         HIP_TRY(hipMemcpy(c->sp_small + 1 + SPEC_PTRS, ptrs, sizeof(ptrs), hipMemcpyHostToDevice));
-        HIP_TRY(hipMalloc((void **)&c->sp_R, cap * 16 * 4)); // 8 lists of (chunk, state), chunks <= cap
         HIP_TRY(hipMalloc((void **)&c->sp_T, cap * SPEC_KMAX * 4));
         // inclusive burst prefixes + block totals + block start states
         HIP_TRY(hipMalloc((void **)&c->sp_U, (cap * SPEC_KMAX + (cap / SPEC_BLK + 2) * (SPEC_KMAX + 1)) * 4));
@@ -5393,8 +5512,9 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 const uint64_t nch = (nb + SPEC_CH - 1) / SPEC_CH;
                 // auto mode: the local pass first, the general one only for what it leaves
                 const uint32_t gated = c->tune_spec_scan == 0 ? 1u : 0u;
+                const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
+                uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
                 if (gated && a.spec_tile) { // the main kernel wrote tile words
-                    auto lo = k_spec_local_t<SPEC_CH>;
                     uint32_t gl = (uint32_t)((nch + 4 * SPEC_LQ - 1) / (4 * SPEC_LQ)); // SPEC_LQ chunks per wave
                     // the previous call was a uniform batch: a wave per 64+ tiles
                     // (any grid gives the same results; CNDP_TUNE_SPEC_GRID forces
@@ -5404,19 +5524,20 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                     const uint32_t cap = c->tune_spec_grid == 1 ? 2u : (uint32_t)c->num_cu * 4u;
                     if (shrink && gl > cap)
                         gl = cap;
-                    hipLaunchKernelGGL(lo, dim3(gl), dim3(256), 0, s, a, B, nb, nch, meta, c->sp_done, c->sp_R);
+                    hipLaunchKernelGGL(k_spec_local_t<SPEC_CH>, dim3(gl), dim3(256), 0, s, a, B, nb, nch, meta,
+                                       c->sp_done);
                 } else if (gated) {
                     auto lo = k_spec_local<SPEC_CH, SPEC_WPB>;
                     const uint32_t gl = (uint32_t)((nch + SPEC_WPB - 1) / SPEC_WPB);
                     hipLaunchKernelGGL(lo, dim3(gl), dim3(SPEC_WPB * 64), 0, s, a, B, nb, nch, meta, c->sp_done);
                 }
-                const uint64_t nblk = (nch + SPEC_BLK - 1) / SPEC_BLK;
-                uint32_t *P = c->sp_U, *Bt = c->sp_U + nch * SPEC_KMAX, *Sblk = Bt + nblk * SPEC_KMAX;
-                auto fb = k_spec_fallback<SPEC_CH>;
-                hipLaunchKernelGGL(fb, dim3((uint32_t)c->num_cu), dim3(256), 0, s, a, B, nb, nch, meta,
-                                   (const uint8_t *)c->sp_class, c->sp_T, P, Bt, Sblk, c->sp_S,
-                                   (const uint8_t *)c->sp_done, a.spec_bar, kfast, kmax, gated,
-                                   (const uint32_t *)c->sp_R);
+                // the general resolution: a block a CU when the previous call needed
+                // it (host hint [2]), else one block that mostly returns at once
+                const bool fb_full = !gated || !c->sp_hint || ((volatile uint32_t *)c->sp_hint)[2];
+                hipLaunchKernelGGL(k_spec_fallback<SPEC_CH>, dim3(fb_full ? (uint32_t)c->num_cu : 1u), dim3(256), 0, s,
+                                   a, B, nb, nch,
+                                   meta, (const uint8_t *)c->sp_class, c->sp_T, P, Bt, Sblk, c->sp_S,
+                                   (const uint8_t *)c->sp_done, a.spec_bar, kfast, kmax, gated);
             } else {
                 hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
@@ -7899,10 +8020,19 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
 // (8 words a wave: chain, parse, issue, stores, loop, trips)
 extern "C" int cndp_gpu_debug_stamps(unsigned long long *out, uint32_t n)
 {
-    if (n > CD_STAMP_WAVES * 8)
-        n = CD_STAMP_WAVES * 8;
+    if (n > CD_STAMP_WAVES * 16)
+        n = CD_STAMP_WAVES * 16;
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(cd_stamps), (size_t)n * 8));
+    return 0;
+}
+
+extern "C" int cndp_gpu_debug_spec_stamps(unsigned long long *out, uint32_t n)
+{
+    if (n > SP_STAMP_BLOCKS * 16 + 8)
+        n = SP_STAMP_BLOCKS * 16 + 8;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(sp_stamps), (size_t)n * 8));
     return 0;
 }
 #endif

@@ -26,14 +26,58 @@ for arg in sys.argv[1:] or ["c4", "c5"]:
     for k in range(6):
         bench.run_step(st, None, k)
     torch.cuda.synchronize()
-    buf = np.zeros(8192 * 8, np.uint64)
+    buf = np.zeros(8192 * 16, np.uint64)
     assert N.lib().cndp_gpu_debug_stamps(buf.ctypes.data_as(__import__("ctypes").c_void_p), buf.size) == 0
-    w = buf.reshape(-1, 8).astype(np.float64)
-    w = w[w[:, 5] > 0]
+    raw = buf.reshape(-1, 16)
+    raw = raw[raw[:, 5] > 0]
+    w = raw[:, :8].astype(np.float64)
     per = w[:, [0, 1, 2, 6, 3, 4]] / w[:, 5:6]
     m = per.mean(axis=0)
     print(f"{arg}: {len(w)} waves, {w[:, 5].mean():.1f} trips a wave; cycles a trip: chain {m[0]:.0f}, "
           f"tile+parse+hash {m[1]:.0f}, issue {m[2]:.0f}, speculation words {m[3]:.0f}, result stores "
           f"{m[4]:.0f}; loop {m[5]:.0f} (sum {m[:5].sum():.0f})", flush=True)
+    if raw[:, 8].any():  # s_memrealtime timeline (100 MHz), microseconds from the first wave's prologue
+        t = (raw[:, 8:12].astype(np.int64) - int(raw[:, 8].min())) / 100.0
+        q = lambda c: " / ".join(f"{x:.1f}" for x in np.percentile(t[:, c], [0, 50, 99, 100]))
+        lw = t[:, 2] - t[:, 1]
+        print(f"  us (min / p50 / p99 / max): prologue issued {q(0)}; loop start {q(1)}; loop end {q(2)}; "
+              f"wave end {q(3)}; loop length {lw.min():.1f} / {np.median(lw):.1f} / {lw.max():.1f}; "
+              f"clock {np.median(w[:, 4] / np.maximum(lw, 1e-3)) / 1e3:.2f} GHz", flush=True)
+        if raw[:, 12].any():
+            z = int(raw[:, 8].min())
+            tk = raw[:, 14].astype(np.uint64)
+            last = (tk >> np.uint64(63)) != 0
+            tkt = ((tk & np.uint64((1 << 63) - 1)).astype(np.int64) - z) / 100.0
+            q2 = lambda v: " / ".join(f"{x:.1f}" for x in np.percentile(v, [0, 50, 99, 100]))
+            print(f"  tail us (min / p50 / p99 / max): odd tiles done {q2((raw[:, 12].astype(np.int64) - z) / 100.0)}; "
+                  f"flushes issued {q2((raw[:, 13].astype(np.int64) - z) / 100.0)}; ticket {q2(tkt[raw[:, 14] > 0])}; "
+                  f"last block's ticket {tkt[last].max() if last.any() else 0:.1f}, its end "
+                  f"{((raw[last, 11].astype(np.int64) - z) / 100.0).max() if last.any() else 0:.1f}", flush=True)
+        sp = np.zeros(4096 * 16 + 8, np.uint64)
+        if hasattr(N.lib(), "cndp_gpu_debug_spec_stamps") and \
+                N.lib().cndp_gpu_debug_spec_stamps(sp.ctypes.data_as(__import__("ctypes").c_void_p), sp.size) == 0:
+            kend = int(raw[:, 11].max())
+            b = sp[:4096 * 16].reshape(-1, 16).astype(np.int64)
+            b = b[b[:, 0] >= kend - 200]  # this launch's blocks (from the last cnet wave's end, 2 us slack)
+            if len(b):
+                rel = lambda v: (v - kend) / 100.0
+                paths = {int(k): int(v) for k, v in zip(*np.unique(b[:, 4], return_counts=True))}
+                fill = b[b[:, 2] > 0]
+                endv = np.where(b[:, 3] > 0, b[:, 3], b[:, 1])
+                print(f"  spec (us after the last cnet wave ended): local_t {len(b)} blocks, paths {paths} "
+                      f"(1 unif 2 stop 3 lists-idle 4 lists 5 chunks), list {int(b[:, 5].max())}; first start "
+                      f"{rel(b[:, 0].min()):.1f}, last start {rel(b[:, 0].max()):.1f}, inputs in (p50) "
+                      f"{np.median(rel(b[:, 1])):.1f}, tables filled (p50 / max) "
+                      f"{np.median(rel(fill[:, 2])) if len(fill) else 0:.1f} / {rel(fill[:, 2].max()) if len(fill) else 0:.1f}, "
+                      f"last end {rel(endv.max()):.1f}", flush=True)
+                for k, nm in ((6, "lookback"), (7, "types staged"), (10, "walk burst 0"), (11, "walk burst 1"),
+                              (12, "walk burst 2"), (13, "walk burst 3"), (8, "replay walk"), (9, "replay fixed")):
+                    v = b[b[:, k] > 0][:, k]
+                    if len(v):
+                        print(f"    {nm}: {len(v)} blocks, p50 {np.median(rel(v)):.1f} max {rel(v.max()):.1f}", flush=True)
+                f0, f1, fx = (int(v) for v in sp[4096 * 16:4096 * 16 + 3])
+                if f0 >= kend:
+                    print(f"  fallback block 0: start {rel(f0):.1f}, decided {rel(f1):.1f} (replays {fx & 0xffffffff},"
+                          f" full {fx >> 32})", flush=True)
     del st
     torch.cuda.empty_cache()
