@@ -29,6 +29,8 @@ for arg in sys.argv[1:] or ["c4", "c5"]:
     buf = np.zeros(8192 * 16, np.uint64)
     assert N.lib().cndp_gpu_debug_stamps(buf.ctypes.data_as(__import__("ctypes").c_void_p), buf.size) == 0
     raw = buf.reshape(-1, 16)
+    if os.environ.get("CNET_STAMPS_SAVE"):  # the per-wave rows (wave = block * CT_WAVES + wave in block)
+        np.save(os.path.join(os.environ["CNET_STAMPS_SAVE"], f"stamps_{arg.replace(':', '_')}.npy"), raw)
     raw = raw[raw[:, 5] > 0]
     w = raw[:, :8].astype(np.float64)
     per = w[:, [0, 1, 2, 6, 3, 4]] / w[:, 5:6]

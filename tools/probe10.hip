@@ -54,6 +54,63 @@ struct Seq {
     uint32_t cur, pos, nx_v, done;
 };
 
+// Hybrid (C = 0x100 * R + K): tiles [0, ts) static as C == 0 (ts = nt - nt / R,
+// a multiple of the wave count), then chunks of K tiles of [ts, nt) from eight
+// pools, one per XCD (blockIdx % 8), each with its own counter (128 B apart);
+// a wave whose pool is empty takes from the next one.
+struct HSeq {
+    uint32_t t, step, ts; // static: next tile, stride, end
+    uint32_t pool, tried, cur, pos, K, nt, base, per;
+};
+__device__ __forceinline__ uint32_t hseq_grab(HSeq &h, uint32_t *ctr, uint32_t lane)
+{
+    while (h.tried < 8u) {
+        uint32_t g = 0;
+        if (lane == 0)
+            g = atomicAdd(ctr + 32u * h.pool, 1u);
+        g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+        if (g < h.per) { // chunk g of pool p: tiles base + (g * 8 + p) * K ...
+            const uint32_t t = h.base + (g * 8u + h.pool) * h.K;
+            if (t < h.nt)
+                return t;
+        }
+        h.pool = (h.pool + 1u) & 7u;
+        h.tried++;
+    }
+    return ~0u;
+}
+__device__ __forceinline__ uint32_t hseq_next(HSeq &h, uint32_t *ctr, uint32_t lane)
+{
+    if (h.t < h.ts) {
+        const uint32_t t = h.t;
+        h.t += h.step;
+        return t;
+    }
+    if (h.cur != ~0u && h.pos < h.K && h.cur + h.pos < h.nt)
+        return h.cur + h.pos++;
+    h.cur = hseq_grab(h, ctr, lane);
+    h.pos = 0;
+    if (h.cur == ~0u)
+        return ~0u;
+    return h.cur + h.pos++;
+}
+__device__ __forceinline__ void hseq_init(HSeq &h, uint32_t C, uint32_t gw, uint32_t W, uint32_t nt)
+{
+    const uint32_t R = (C >> 8) & 0xffu;
+    h.K = C & 0xffu;
+    h.nt = nt;
+    uint32_t res = nt / R;
+    h.ts = (nt - res) / W * W; // the static part: whole rounds of the waves
+    h.base = h.ts;
+    h.per = (nt - h.ts + 8u * h.K - 1u) / (8u * h.K); // chunks per pool
+    h.t = gw;
+    h.step = W;
+    h.pool = blockIdx.x & 7u;
+    h.tried = 0;
+    h.cur = ~0u;
+    h.pos = 0;
+}
+
 __device__ __forceinline__ void seq_init(Seq &s, uint32_t C, uint32_t gw, uint32_t nt, uint32_t *ctr, uint32_t lane)
 {
     s.cur = C ? gw * C : gw;
@@ -88,6 +145,17 @@ __device__ __forceinline__ uint32_t seq_next(Seq &s, uint32_t C, uint32_t W, uin
         return ~0u;
     }
     return t;
+}
+
+__device__ __forceinline__ void hseq_fini(uint32_t *ctr, uint32_t lane)
+{
+    if (lane == 0) {
+        __threadfence();
+        const uint32_t W = gridDim.x * (blockDim.x / 64u);
+        if (atomicAdd(ctr + 32u * 8u, 1u) == W - 1u)
+            for (uint32_t k = 0; k < 9; k++)
+                __hip_atomic_store(ctr + 32u * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ void seq_fini(uint32_t C, uint32_t *ctr, uint32_t lane)
@@ -174,6 +242,121 @@ __global__ __launch_bounds__(256) void k_win(const uint8_t *slab, uint64_t strid
     seq_fini(C, ctr, lane);
 }
 
+__global__ __launch_bounds__(256) void k_slots_h(const uint8_t *slab, uint32_t nt, Out o, uint32_t C, uint32_t *ctr)
+{
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[4][256];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint32_t W = gridDim.x * 4u, gw = blockIdx.x * 4u + wv;
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    HSeq h;
+    hseq_init(h, C, gw, W, nt);
+    u32x4 r[2][4];
+    auto issue = [&](u32x4(&d)[4], uint32_t tt) {
+        const uint8_t *g = slab + (uint64_t)(tt < nt ? tt : nt - 1u) * 4096u;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            d[k] = ldnt(g + (64u * k + lane) * 16u);
+    };
+    uint32_t q0 = hseq_next(h, ctr, lane), q1 = hseq_next(h, ctr, lane);
+    issue(r[0], q0);
+    issue(r[1], q1);
+    while (q0 != ~0u) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = r[0][k];
+            r[0][k] = r[1][k];
+        }
+        const uint32_t q2 = q1 == ~0u ? ~0u : hseq_next(h, ctr, lane);
+        issue(r[1], q2);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t f = 16u * k + fr_in_k;
+            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t sw = (lane >> 2) & 3u;
+        const u32x4 p0 = tile[lane * 4u + (0u ^ sw)], p1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+        __builtin_amdgcn_wave_barrier();
+        put(o, (uint64_t)q0 * 64u + lane, p0.w ^ p1.y ^ p1.z ^ p1.w ^ p2.x ^ p2.y);
+        q0 = q1;
+        q1 = q2;
+    }
+    hseq_fini(ctr, lane);
+}
+
+__global__ __launch_bounds__(256) void k_win_h(const uint8_t *slab, uint64_t stride, const uint64_t *offs, uint32_t nt,
+                                               Out o, uint32_t C, uint32_t *ctr)
+{
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t W = gridDim.x * 4u, gw = blockIdx.x * 4u + wv;
+    HSeq h;
+    hseq_init(h, C, gw, W, nt);
+    for (uint32_t g = hseq_next(h, ctr, lane); g != ~0u; g = hseq_next(h, ctr, lane)) {
+        const uint64_t i = (uint64_t)g * 64u + lane;
+        const uint64_t mine = offs ? offs[i] : i * stride;
+        uint32_t res = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t fo = __shfl(mine, 16 * k + (int)(lane >> 2));
+            const u32x4 w = ldnt(slab + fo + (lane & 3u) * 16u);
+            uint32_t x = w.x ^ w.y ^ w.z ^ w.w;
+            x ^= __shfl_xor(x, 1);
+            x ^= __shfl_xor(x, 2);
+            const uint32_t src = __shfl(x, (int)((lane & 15u) * 4u));
+            if ((lane >> 4) == (uint32_t)k)
+                res = src;
+        }
+        put(o, i, res);
+    }
+    hseq_fini(ctr, lane);
+}
+
+// static schedule, PF tiles in flight per wave (C3 shape sweep)
+template <int PF>
+__global__ __launch_bounds__(256) void k_slots_pf(const uint8_t *slab, uint32_t nt, Out o)
+{
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[4][256];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint32_t W = gridDim.x * 4u, t0 = blockIdx.x * 4u + wv;
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    u32x4 r[PF][4];
+    auto issue = [&](u32x4(&d)[4], uint32_t tt) {
+        const uint8_t *g = slab + (uint64_t)(tt < nt ? tt : nt - 1u) * 4096u;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            d[k] = ldnt(g + (64u * k + lane) * 16u);
+    };
+#pragma unroll
+    for (int q = 0; q < PF; q++)
+        issue(r[q], t0 + q * W);
+    for (uint32_t t = t0; t < nt; t += W) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = r[0][k];
+#pragma unroll
+            for (int q = 0; q + 1 < PF; q++)
+                r[q][k] = r[q + 1][k];
+        }
+        issue(r[PF - 1], t + PF * W);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t f = 16u * k + fr_in_k;
+            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t sw = (lane >> 2) & 3u;
+        const u32x4 p0 = tile[lane * 4u + (0u ^ sw)], p1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+        __builtin_amdgcn_wave_barrier();
+        put(o, (uint64_t)t * 64u + lane, p0.w ^ p1.y ^ p1.z ^ p1.w ^ p2.x ^ p2.y);
+    }
+}
+
 template <class F> static float timed(F launch)
 {
     hipEvent_t a, b;
@@ -224,8 +407,8 @@ int main()
     uint32_t *ctr;
     CK(hipMalloc((void **)&slab, bytes));
     CK(hipMalloc((void **)&offs, n4 * 8));
-    CK(hipMalloc((void **)&ctr, 256));
-    CK(hipMemset(ctr, 0, 256));
+    CK(hipMalloc((void **)&ctr, 9 * 128));
+    CK(hipMemset(ctr, 0, 9 * 128));
     CK(hipMemcpy(offs, hoff.data(), n4 * 8, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_fill, dim3(ncu * 16), dim3(256), 0, 0, (uint32_t *)slab, bytes / 4);
     Out full{}, nh{};
@@ -234,36 +417,73 @@ int main()
     CK(hipMalloc((void **)&full.q, n5 * 2));
     nh.a = full.a;
     CK(hipDeviceSynchronize());
-    const uint32_t Cs[] = {0, 1, 2, 4, 8, 16};
+    if (getenv("PROBE10_SHAPES")) { // C3 shape sweep: tiles in flight x blocks a CU, 4 batches in a ring
+        const uint32_t nt = (uint32_t)(n4 / 64);
+        for (int pf : {1, 2, 3, 4}) {
+            printf("slots C3 pf%d:", pf);
+            for (int bpc : {1, 2, 3, 4, 6, 8}) {
+                int k = 0;
+                const float ms = timed([&] {
+                    const uint8_t *sl = slab + (uint64_t)(k++ & 3) * n4 * 64; // a ring of 4 GiB
+                    const dim3 g(ncu * bpc), b(256);
+                    if (pf == 1)
+                        hipLaunchKernelGGL(k_slots_pf<1>, g, b, 0, 0, sl, nt, full);
+                    else if (pf == 2)
+                        hipLaunchKernelGGL(k_slots_pf<2>, g, b, 0, 0, sl, nt, full);
+                    else if (pf == 3)
+                        hipLaunchKernelGGL(k_slots_pf<3>, g, b, 0, 0, sl, nt, full);
+                    else
+                        hipLaunchKernelGGL(k_slots_pf<4>, g, b, 0, 0, sl, nt, full);
+                });
+                printf("  bpc%d %.4f", bpc, ms);
+            }
+            printf(" ms\n");
+            fflush(stdout);
+        }
+        return 0;
+    }
+    // C == 0: static; otherwise hybrid 0x100 * R + K (reserve 1/R, chunks of K)
+    const uint32_t Hs[] = {0x0802, 0x1002, 0x1004, 0x2002};
     for (int bpc : {2, 4}) {
-        printf("slots C3 bpc%d:", bpc);
-        for (uint32_t C : Cs)
-            printf("  C%u %.4f", C, timed([&] {
-                       hipLaunchKernelGGL(k_slots, dim3(ncu * bpc), dim3(256), 0, 0, slab, (uint32_t)(n4 / 64), full, C,
-                                          ctr);
+        printf("slots C3 bpc%d: static %.4f", bpc, timed([&] {
+                   hipLaunchKernelGGL(k_slots, dim3(ncu * bpc), dim3(256), 0, 0, slab, (uint32_t)(n4 / 64), full, 0u, ctr);
+               }));
+        for (uint32_t C : Hs)
+            printf("  h%x %.4f", C, timed([&] {
+                       hipLaunchKernelGGL(k_slots_h, dim3(ncu * bpc), dim3(256), 0, 0, slab, (uint32_t)(n4 / 64), full,
+                                          C, ctr);
                    }));
         printf(" ms\n");
         fflush(stdout);
     }
     for (int bpc : {4, 8}) {
-        printf("win5 C5 bpc%d:", bpc);
-        for (uint32_t C : Cs)
-            printf("  C%u %.4f", C, timed([&] {
-                       hipLaunchKernelGGL(k_win, dim3(ncu * bpc), dim3(256), 0, 0, slab, stride, (const uint64_t *)nullptr,
-                                          (uint32_t)(n5 / 64), nh, C, ctr);
+        printf("win5 C5 bpc%d: static %.4f", bpc, timed([&] {
+                   hipLaunchKernelGGL(k_win, dim3(ncu * bpc), dim3(256), 0, 0, slab, stride, (const uint64_t *)nullptr,
+                                      (uint32_t)(n5 / 64), nh, 0u, ctr);
+               }));
+        for (uint32_t C : Hs)
+            printf("  h%x %.4f", C, timed([&] {
+                       hipLaunchKernelGGL(k_win_h, dim3(ncu * bpc), dim3(256), 0, 0, slab, stride,
+                                          (const uint64_t *)nullptr, (uint32_t)(n5 / 64), nh, C, ctr);
                    }));
         printf(" ms\n");
-        printf("win4 C4 bpc%d:", bpc);
-        for (uint32_t C : Cs)
-            printf("  C%u %.4f", C, timed([&] {
-                       hipLaunchKernelGGL(k_win, dim3(ncu * bpc), dim3(256), 0, 0, slab, (uint64_t)0, offs,
+        printf("win4 C4 bpc%d: static %.4f", bpc, timed([&] {
+                   hipLaunchKernelGGL(k_win, dim3(ncu * bpc), dim3(256), 0, 0, slab, (uint64_t)0, offs,
+                                      (uint32_t)(n4 / 64), full, 0u, ctr);
+               }));
+        for (uint32_t C : Hs)
+            printf("  h%x %.4f", C, timed([&] {
+                       hipLaunchKernelGGL(k_win_h, dim3(ncu * bpc), dim3(256), 0, 0, slab, (uint64_t)0, offs,
                                           (uint32_t)(n4 / 64), full, C, ctr);
                    }));
         printf(" ms\n");
         fflush(stdout);
     }
-    uint32_t hc[2];
-    CK(hipMemcpy(hc, ctr, 8, hipMemcpyDeviceToHost));
-    printf("counters after the runs: %u %u (0 0 = reset by the last wave)\n", hc[0], hc[1]);
+    uint32_t hc[9 * 32];
+    CK(hipMemcpy(hc, ctr, sizeof(hc), hipMemcpyDeviceToHost));
+    uint32_t nz = 0;
+    for (uint32_t k = 0; k < 9; k++)
+        nz += hc[32 * k] != 0;
+    printf("counters left nonzero after the runs: %u (0 = reset by the last wave)\n", nz);
     return 0;
 }
