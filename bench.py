@@ -507,6 +507,7 @@ def probe_ceiling(st, stream, steps: int, kern_ms: float) -> dict:
     P = ctypes.CDLL(os.path.join(ROOT, "cndp_amd", "lib", "libcndp_probe.so"))
     P.cndp_probe_slots.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 3 + \
         [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    P.cndp_probe_slots_bal.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 4
     P.cndp_probe_windows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_uint64] + [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.c_void_p]
     ring = st["ring"]
@@ -540,8 +541,16 @@ def probe_ceiling(st, stream, steps: int, kern_ms: float) -> dict:
                     return P.cndp_probe_slots(fr.slab.data_ptr(), fr.n, ptr(o.get("nh")), ptr(o.get("hash")),
                                               ptr(o.get("queue")), pf, bpc, sid)
                 rows[f"slots_pf{pf}_bpc{bpc}"] = timed(launch)
+
+        def blaunch(k):
+            fr, o = ring[k % len(ring)]
+            return P.cndp_probe_slots_bal(fr.slab.data_ptr(), fr.n, ptr(o.get("nh")), ptr(o.get("hash")),
+                                          ptr(o.get("queue")), sid)
+        rows["slots_balanced_512x1"] = timed(blaunch)
         shape = ("packed 64-B slots: 4 x 1 KiB nt loads per 64-frame wave tile through the LDS tile, the "
-                 "kernel's result stores (nh / hash / queue as allocated), nothing else")
+                 "kernel's result stores (nh / hash / queue as allocated), nothing else; static schedules "
+                 "(1-2 tiles in flight, 2-4 blocks a CU) and the kernel's balanced one (one 512-thread block "
+                 "a CU, tiles shared through an LDS counter)")
     else:
         def wlaunch(bpc, algo_only):
             def launch(k):
@@ -1283,6 +1292,7 @@ def main():
     ap.add_argument("--spec-scan", type=int, default=None)
     ap.add_argument("--spec-lists", type=int, default=None)
     ap.add_argument("--spec-types", type=int, default=None)
+    ap.add_argument("--stream-bal", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--dir16", type=int, default=None)
     ap.add_argument("--nt", type=int, default=None)
@@ -1307,7 +1317,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     cl.set_tuning(nt=args.nt, unroll=args.unroll, blocks_per_cu=args.bpc, tile=args.tile, dir16=args.dir16,
                   load_nt=args.load_nt, cnet_tile=args.cnet_tile, cnet_spec=args.cnet_spec,
-                  spec_scan=args.spec_scan, spec_lists=args.spec_lists, spec_types=args.spec_types)
+                  spec_scan=args.spec_scan, spec_lists=args.spec_lists, spec_types=args.spec_types,
+                  stream_bal=args.stream_bal)
     if args.sweep and rank == 0:
         sweep(st, stream, args.config)
 

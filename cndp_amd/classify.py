@@ -58,10 +58,12 @@ class Classifier:
                    cnet_spec: int | None = None, load_nt: int | None = None,
                    spec_scan: int | None = None, mbuf_hash: int | None = None,
                    cnet_fold: int | None = None, spec_grid: int | None = None,
-                   spec_lists: int | None = None, spec_types: int | None = None):
+                   spec_lists: int | None = None, spec_types: int | None = None,
+                   stream_bal: int | None = None):
         """Kernel variant knobs (cndp_gpu_set_tuning); never change results."""
         for key, v in ((N.CNDP_TUNE_CNET_FOLD, cnet_fold), (N.CNDP_TUNE_SPEC_GRID, spec_grid),
                        (N.CNDP_TUNE_SPEC_LISTS, spec_lists), (N.CNDP_TUNE_SPEC_TYPES, spec_types),
+                       (N.CNDP_TUNE_STREAM_BAL, stream_bal),
                        (N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),
                        (N.CNDP_TUNE_BLOCKS_PER_CU, blocks_per_cu), (N.CNDP_TUNE_TILE, tile),
                        (N.CNDP_TUNE_DIR16, dir16), (N.CNDP_TUNE_CNET_TILE, cnet_tile),

@@ -720,12 +720,13 @@ struct StreamLane { // one lane's packet in flight between stages
     bool sel;     // raw replaces e (resolved by the consumer, not at issue)
 };
 
+// c: tile of stage A, cn: the tile whose frames this trip loads, cd: stage D's
+// tile (its stores only when dD); an index >= n_tiles stands for none
 template <int MODE, bool NTS, bool LNT, int P>
-__device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, uint64_t t0, uint64_t wstep,
-                                            uint64_t nt_w, uint64_t j, uint32_t lane, u32x4 *tile,
-                                            u32x4 (&r)[2][4], StreamLane &sb, StreamLane &sc, StreamLane &sd,
-                                            const uint32_t *s_t, const uint16_t *s_reta, uint32_t *s_bins,
-                                            bool count)
+__device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, uint64_t c, uint64_t cn, uint64_t cd,
+                                            bool dD, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
+                                            StreamLane &sb, StreamLane &sc, StreamLane &sd, const uint32_t *s_t,
+                                            const uint16_t *s_reta, uint32_t *s_bins, bool count)
 {
     // Every load below is issued unconditionally (a safe index when its
     // result is not needed; past the wave's last tile the frame loads re-read
@@ -734,8 +735,6 @@ __device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, ui
     // for what is older than the newest frame tile.
     const uint8_t *base = a.slab + a.data_off;
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const bool dD = j >= 3 && j - 3 < nt_w;
-    const uint64_t c = t0 + j * wstep;
     // D: tile c-3 -- its final entry came back with last trip's gather 3
     uint32_t nhD = CNDP_NH_INVALID;
     const uint32_t etD = sd.et, hsD = sd.hs;
@@ -805,7 +804,6 @@ __device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, ui
         nb.hs = fast_hash<MODE>(a, h, s_t);
     // frame tile c+2 into the register set just consumed
     {
-        const uint64_t cn = c + 2u * wstep;
         const u32x4 *g = (const u32x4 *)(base + (cn < n_tiles ? cn : n_tiles - 1u) * 4096u);
         r[P][0] = ldg4<LNT>((const uint8_t *)(g + lane));
         r[P][1] = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
@@ -814,7 +812,7 @@ __device__ __forceinline__ void stream_trip(const KArgs &a, uint64_t n_tiles, ui
     }
     // D: the stores of tile c-3
     if (dD)
-        fast_emit<MODE, NTS>(a, (c - 3u * wstep) * 64u + lane, etD, nhD, hsD, s_reta, s_bins, count);
+        fast_emit<MODE, NTS>(a, cd * 64u + lane, etD, nhD, hsD, s_reta, s_bins, count);
     sd = nd;
     sc = nc;
     sb = nb;
@@ -858,11 +856,12 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_stream(KArgs a, uint6
     StreamLane sb = {0, 0, 0, 0, 0, false}, sc = sb, sd = sb;
     const uint64_t trips = nt_w ? nt_w + 3 : 0;
     for (uint64_t j = 0; j < trips; j += 2) {
-        stream_trip<MODE, NTS, LNT, 0>(a, n_tiles, t0, wstep, nt_w, j, lane, tile, r, sb, sc, sd, s_t, s_reta,
-                                       s_bins, count);
+        stream_trip<MODE, NTS, LNT, 0>(a, n_tiles, t0 + j * wstep, t0 + (j + 2) * wstep, t0 + (j - 3) * wstep,
+                                       j >= 3 && j - 3 < nt_w, lane, tile, r, sb, sc, sd, s_t, s_reta, s_bins, count);
         if (j + 1 < trips)
-            stream_trip<MODE, NTS, LNT, 1>(a, n_tiles, t0, wstep, nt_w, j + 1, lane, tile, r, sb, sc, sd, s_t,
-                                           s_reta, s_bins, count);
+            stream_trip<MODE, NTS, LNT, 1>(a, n_tiles, t0 + (j + 1) * wstep, t0 + (j + 3) * wstep,
+                                           t0 + (j - 2) * wstep, j >= 2 && j - 2 < nt_w, lane, tile, r, sb, sc, sd,
+                                           s_t, s_reta, s_bins, count);
     }
     // ragged tail (frames past the last whole tile): per-lane path
     const uint64_t done = n_tiles * 64u;
@@ -880,6 +879,113 @@ __global__ __launch_bounds__(FAST_THREADS) void k_classify_stream(KArgs a, uint6
     }
 }
 
+
+// The same stages with the block's tiles (blockIdx + k * gridDim) handed to
+// its BW waves by an LDS counter (CNDP_TUNE_STREAM_BAL): one BW * 64-thread
+// block a CU, so the CU's waves share one pool and the ones the SQ's
+// oldest-first arbitration favours take more tiles -- no wave is left with a
+// static share after the others have finished.  Each wave's first three
+// tiles are static; every trip draws the index it will load two trips
+// later, a trip ahead of its use (the LDS atomic's return is waited for with
+// the trip's other LDS traffic).
+#define STREAM_BW 8
+template <int MODE, bool NTS, bool LNT>
+__global__ __launch_bounds__(STREAM_BW * 64) void k_classify_stream_bal(KArgs a, uint64_t n_tiles)
+{
+    __shared__ uint32_t s_t[TAB4_POS * 256];
+    __shared__ uint16_t s_reta[CNDP_RETA_MAX];
+    __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[STREAM_BW][256];
+    __shared__ uint32_t s_next;
+    constexpr uint32_t NT = STREAM_BW * 64;
+
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < TAB4_POS * 256; k += NT)
+        s_t[k] = a.ttab[k];
+    for (uint32_t k = tid; k <= a.reta_mask; k += NT)
+        s_reta[k] = a.reta[k];
+    const bool count = a.bins != nullptr;
+    if (count)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += NT)
+            s_bins[k] = 0;
+    if (tid == 0)
+        s_next = 3u * STREAM_BW;
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint8_t *base = a.slab + a.data_off;
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    const uint64_t NONE = ~0ull;
+    // the block's tiles, G apart (in the static schedule's round order instead,
+    // k_cnet_defer's BAL mapping, C3 is 1 % slower)
+    const uint64_t nk = b < n_tiles ? (n_tiles - b + G - 1) / G : 0;
+    auto tile_of = [&](uint64_t k) { return k < nk ? b + k * G : NONE; };
+    // the wave's first three tiles, static; two of them loaded now
+    uint64_t q0 = tile_of(wv), q1 = tile_of(wv + STREAM_BW), q2 = tile_of(wv + 2u * STREAM_BW);
+    u32x4 r[2][4];
+#pragma unroll
+    for (uint32_t s = 0; s < 2; s++) {
+        const uint64_t ts = s ? q1 : q0;
+        const u32x4 *g = (const u32x4 *)(base + (ts < n_tiles ? ts : n_tiles - 1u) * 4096u);
+        r[s][0] = ldg4<LNT>((const uint8_t *)(g + lane));
+        r[s][1] = ldg4<LNT>((const uint8_t *)(g + 64 + lane));
+        r[s][2] = ldg4<LNT>((const uint8_t *)(g + 128 + lane));
+        r[s][3] = ldg4<LNT>((const uint8_t *)(g + 192 + lane));
+    }
+    __syncthreads();
+    // the index after q2, drawn a trip ahead (lane 0's LDS atomic)
+    auto draw = [&](uint64_t prev) -> uint32_t {
+        uint32_t v = 0;
+        if (prev != NONE && lane == 0)
+            v = atomicAdd(&s_next, 1u);
+        return v;
+    };
+    uint32_t kv = draw(q2);
+    uint64_t h1 = NONE, h2 = NONE, h3 = NONE; // the tiles of stages B, C, D
+    StreamLane sb = {0, 0, 0, 0, 0, false}, sc = sb, sd = sb;
+    for (;;) {
+        if (q0 == NONE && h1 == NONE && h2 == NONE && h3 == NONE) // wave-uniform
+            break;
+        stream_trip<MODE, NTS, LNT, 0>(a, n_tiles, q0, q2, h3, h3 != NONE, lane, tile, r, sb, sc, sd, s_t, s_reta,
+                                       s_bins, count);
+        {
+            const uint64_t qn = q2 == NONE ? NONE : tile_of(__builtin_amdgcn_readfirstlane(kv));
+            kv = draw(qn);
+            h3 = h2;
+            h2 = h1;
+            h1 = q0;
+            q0 = q1;
+            q1 = q2;
+            q2 = qn;
+        }
+        if (q0 == NONE && h1 == NONE && h2 == NONE && h3 == NONE)
+            break;
+        stream_trip<MODE, NTS, LNT, 1>(a, n_tiles, q0, q2, h3, h3 != NONE, lane, tile, r, sb, sc, sd, s_t, s_reta,
+                                       s_bins, count);
+        {
+            const uint64_t qn = q2 == NONE ? NONE : tile_of(__builtin_amdgcn_readfirstlane(kv));
+            kv = draw(qn);
+            h3 = h2;
+            h2 = h1;
+            h1 = q0;
+            q0 = q1;
+            q1 = q2;
+            q2 = qn;
+        }
+    }
+    // ragged tail (frames past the last whole tile): per-lane path
+    const uint64_t done = n_tiles * 64u;
+    for (uint64_t i = done + (uint64_t)blockIdx.x * NT + tid; i < a.n; i += (uint64_t)gridDim.x * NT) {
+        FastHdr h;
+        fast_load<false>(a, i, h);
+        fast_finish<MODE, false>(a, i, h, s_t, s_reta, s_bins, count);
+    }
+    if (count) {
+        __syncthreads();
+        for (uint32_t k = tid; k < a.n_bins + 2; k += NT)
+            if (s_bins[k])
+                atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
+    }
+}
 
 // ---------------------------------------------------------------------------
 // cnet classify: eth_rx (cne_get_ptype) -> ptype -> ip4_input / ip6_input.
@@ -1662,18 +1768,20 @@ __device__ __forceinline__ bool spec_code_type(uint32_t pt)
     return pt == 0x111u || pt == 0x211u || pt == 0x141u || pt == 0x241u;
 }
 
+// tA: stage A's tile, tB: stage B's (the previous trip's A), tW: the tile
+// whose windows this trip loads, tO: the tile whose offsets it loads;
+// CD_NONE for none
+#define CD_NONE 0xFFFFFFFFu
 template <bool LNT, bool META, bool CODES, int P>
-__device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t wstep, uint32_t n_tiles,
-                                        uint32_t nt_w, uint32_t jt, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4],
-                                        CsOff &off, CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta,
-                                        uint32_t *s_bins, uint32_t *s_sf, bool count, SigCache &sc,
-                                        uint32_t *s_mx, uint64_t *acc)
+__device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t n_tiles, uint32_t tA, uint32_t tB, uint32_t tW,
+                                        uint32_t tO, uint32_t lane, u32x4 *tile, u32x4 (&r)[2][4], CsOff &off,
+                                        CdLane &sb, const uint32_t *s_t, const uint16_t *s_reta, uint32_t *s_bins,
+                                        uint32_t *s_sf, bool count, SigCache &sc, uint32_t *s_mx, uint64_t *acc)
 {
     const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
-    const uint32_t t = t0 + jt * wstep;
     // B: tile c-1 -- the rest of its chain (v4: page / tbl8, v6: tbl8 levels, trie.h:127-134)
-    const bool bv = jt >= 1 && jt - 1 < nt_w;
-    const uint32_t ib = (t - wstep) * 64u + lane;
+    const bool bv = tB != CD_NONE;
+    const uint32_t ib = tB * 64u + lane;
     uint32_t eb = sb.e;
     {
         // one branch-free body for both families: the key bytes stream out of
@@ -1710,8 +1818,8 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
         tile[f * 4u + (part ^ ((f >> 2) & 3u))] = r[P][k];
     }
     __builtin_amdgcn_wave_barrier();
-    const uint32_t i = t * 64u + lane;
-    const bool live = jt < nt_w && i < a.n;
+    const uint32_t i = tA * 64u + lane;
+    const bool live = tA != CD_NONE && i < a.n;
     const uint64_t base = live ? ct_base(a, i, off.o0) : ~0ull;
     const uint32_t sw = (lane >> 2) & 3u;
     uint32_t W[16];
@@ -1843,9 +1951,9 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
     // the first gather: the next trip's wait for the gather leaves them in
     // flight when no lane of the wave needs a further level)
     {
-        const uint32_t t3 = t + 3u * wstep, i3 = t3 * 64u + lane;
-        off.o3 = a.offsets && t3 < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
-        cs_issue<LNT>(a, t + 2u * wstep, n_tiles, off.o2, lane, r[P]);
+        const uint32_t i3 = tO * 64u + lane;
+        off.o3 = a.offsets && tO < n_tiles && i3 < a.n ? a.offsets[i3] : 0;
+        cs_issue<LNT>(a, tW, n_tiles, off.o2, lane, r[P]);
     }
     CD_TS(2); // gather, offsets and windows issued
     // B's results
@@ -1901,17 +2009,17 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t t0, uint32_t ws
                 // passes never read a canonical tile's types) they go out as two
                 // ballots, 16 B a tile, instead of 128 B of types (k_spec_expand
                 // writes the types should this batch need them after all)
-                codes = CODES && om == 0ull && (t - wstep + 1u) * 64u <= a.spec_keep_lo &&
+                codes = CODES && om == 0ull && (tB + 1u) * 64u <= a.spec_keep_lo &&
                         __ballot(ib < a.n && !spec_code_type(pt)) == 0ull;
                 if (codes) {
                     const uint64_t m6 = __ballot((pt & 0xf0u) == 0x40u), mu = __ballot((pt & 0xf00u) == 0x200u);
                     if (lane == 0)
                         __builtin_nontemporal_store((u32x4){(uint32_t)m6, (uint32_t)(m6 >> 32), (uint32_t)mu,
                                                             (uint32_t)(mu >> 32)},
-                                                    (u32x4 *)(a.spec_c2 + 16u * (t - wstep)));
+                                                    (u32x4 *)(a.spec_c2 + 16u * tB));
                 }
                 if (lane == 0)
-                    o.spec_tile[t - wstep] = codes ? (uint8_t)SPEC_TW_CODES : (uint8_t)(om == 0ull);
+                    o.spec_tile[tB] = codes ? (uint8_t)SPEC_TW_CODES : (uint8_t)(om == 0ull);
                 if (om && (a.spec_allow & SPEC_ALLOW_LISTS)) { // wave-uniform, rare
                     // groups (lanes 4q + 3) whose 4th frame was not parsed here, or
                     // is off the common edge beside a 3rd not parsed here (spec_odd_tile)
@@ -2037,8 +2145,13 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
 }
 
 // META: ptype / rxmeta outputs requested (without them the kernel keeps
-// 14 VGPRs and 18 spilled SGPRs fewer)
-template <bool LNT, bool META, bool CODES>
+// 14 VGPRs and 18 spilled SGPRs fewer).  BAL (CNDP_TUNE_STREAM_BAL): the
+// block's tiles are handed to its waves by an LDS counter instead of each
+// wave taking tiles t0, t0 + wstep, ... -- each
+// wave's first four are static, then every trip draws the tile it will
+// read the offsets of next trip (the LDS atomic's return is waited for with
+// the trip's other LDS traffic); the waves the SQ favours take more tiles.
+template <bool LNT, bool META, bool CODES, bool BAL>
 __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
     __shared__ uint32_t s_t[CD_TAB_WORDS];
@@ -2046,21 +2159,44 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
     __shared__ uint32_t s_sf[64];
-    __shared__ uint32_t s_mx; // SPEC_MX bits of this block
+    __shared__ uint32_t s_mx;   // SPEC_MX bits of this block
+    __shared__ uint32_t s_next; // BAL: the block's next tile index
 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     u32x4 *tile = s_tile[wv];
-    const uint32_t wstep = gridDim.x * CT_WAVES;
-    const uint32_t t0 = blockIdx.x * CT_WAVES + wv;
+    const uint32_t G = gridDim.x, bk = blockIdx.x;
+    const uint32_t wstep = G * CT_WAVES;
+    const uint32_t t0 = bk * CT_WAVES + wv;
     const uint32_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
+    // BAL: the block's tiles are the static schedule's tiles of its waves, in
+    // round order -- index k is round k / CT_WAVES, wave k % CT_WAVES -- so the
+    // block's waves work on neighbouring tiles at any time (tiles G apart
+    // instead: C5 11 % slower, the windows of one CU spread over many pages);
+    // they form a prefix of k, nk of them (the waves' static counts)
+    uint32_t nk = 0;
+    if (BAL) {
+        const uint32_t tb0 = bk * CT_WAVES;
+        for (uint32_t w = 0; w < CT_WAVES; w++)
+            nk += tb0 + w < n_tiles ? (n_tiles - tb0 - w + wstep - 1) / wstep : 0;
+    }
+    auto tile_k = [&](uint32_t k) -> uint32_t {
+        return k < nk ? (k / CT_WAVES) * wstep + bk * CT_WAVES + k % CT_WAVES : CD_NONE;
+    };
+    // the wave's k-th tile while its sequence is static
+    auto seq = [&](uint32_t k) -> uint32_t {
+        if (BAL)
+            return tile_k(wv + k * CT_WAVES);
+        return k < nt_w ? t0 + k * wstep : CD_NONE;
+    };
+    uint32_t q0 = seq(0), q1 = seq(1), q2 = seq(2), q3 = seq(3);
     // the first offsets, then the first two frame tiles, in flight while the
     // tables are copied to LDS
     CsOff off{0, 0, 0, 0};
     if (a.offsets) {
 #pragma unroll
         for (uint32_t s = 0; s < 3; s++) {
-            const uint32_t ts = t0 + s * wstep, is = ts * 64u + lane;
+            const uint32_t ts = s == 0 ? q0 : s == 1 ? q1 : q2, is = ts * 64u + lane;
             const uint64_t o = ts < n_tiles && is < a.n ? a.offsets[is] : 0;
             if (s == 0)
                 off.o0 = o;
@@ -2072,13 +2208,15 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     }
     if (tid < 64)
         s_sf[tid] = 0;
-    if (tid == 0)
+    if (tid == 0) {
         s_mx = 0;
+        s_next = 4u * CT_WAVES;
+    }
     for (uint32_t k = tid; k < CD_TAB_WORDS; k += CT_THREADS)
         s_t[k] = a.ttab[(CD_NIB ? TABN_OFF : 0) + k];
     u32x4 r[2][4];
-    cs_issue<LNT>(a, t0, n_tiles, off.o0, lane, r[0]);
-    cs_issue<LNT>(a, t0 + wstep, n_tiles, off.o1, lane, r[1]);
+    cs_issue<LNT>(a, q0, n_tiles, off.o0, lane, r[0]);
+    cs_issue<LNT>(a, q1, n_tiles, off.o1, lane, r[1]);
     for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
         s_reta[k] = a.reta[k];
     const bool count = a.bins != nullptr;
@@ -2089,6 +2227,21 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime(); // after the prologue's issue
 #endif
     __syncthreads();
+    // BAL: the index after q3, drawn by lane 0 a trip ahead
+    uint32_t kv = 0, kst = 4;
+    auto draw = [&]() {
+        if (BAL && q3 != CD_NONE && lane == 0)
+            kv = atomicAdd(&s_next, 1u);
+    };
+    auto next = [&]() -> uint32_t {
+        if (BAL) {
+            if (q3 == CD_NONE)
+                return CD_NONE;
+            return tile_k((uint32_t)__builtin_amdgcn_readfirstlane((int)kv));
+        }
+        return seq(kst++);
+    };
+    draw();
     CdLane sb;
     sb.ptf = sb.h = sb.e = sb.rx = 0;
     sb.q0 = sb.q1 = sb.q2 = sb.q3 = 0;
@@ -2099,14 +2252,38 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     acc[6] = acc[7];
     const uint64_t rt_loop = __builtin_amdgcn_s_memrealtime();
 #endif
-    const uint32_t trips = nt_w ? nt_w + 1 : 0;
-    for (uint32_t jt = 0; jt < trips; jt += 2) {
-        cd_trip<LNT, META, CODES, 0>(a, t0, wstep, n_tiles, nt_w, jt, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf, count,
-                        sig_cache, &s_mx, acc);
-        if (jt + 1 < trips)
-            cd_trip<LNT, META, CODES, 1>(a, t0, wstep, n_tiles, nt_w, jt + 1, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
-                            count, sig_cache, &s_mx, acc);
+    uint32_t tb = CD_NONE, trips = 0; // stage B's tile
+    for (;;) {
+        if (q0 == CD_NONE && tb == CD_NONE) // wave-uniform
+            break;
+        cd_trip<LNT, META, CODES, 0>(a, n_tiles, q0, tb, q2, q3, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
+                                     count, sig_cache, &s_mx, acc);
+        {
+            const uint32_t qn = next();
+            tb = q0;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = qn;
+            draw();
+            trips++;
+        }
+        if (q0 == CD_NONE && tb == CD_NONE)
+            break;
+        cd_trip<LNT, META, CODES, 1>(a, n_tiles, q0, tb, q2, q3, lane, tile, r, off, sb, s_t, s_reta, s_bins, s_sf,
+                                     count, sig_cache, &s_mx, acc);
+        {
+            const uint32_t qn = next();
+            tb = q0;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = qn;
+            draw();
+            trips++;
+        }
     }
+    (void)trips; // (CD_STAMP)
 #if CD_STAMP
     if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES) {
         unsigned long long *o = cd_stamps + (blockIdx.x * CT_WAVES + wv) * 16u;
@@ -2121,15 +2298,25 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     }
 #endif
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && a.spec_tile) {
-        // the wave's non-canonical tiles (its own tile words, its own types)
-        __threadfence_block();
-        for (uint32_t j0 = 0; j0 < nt_w; j0 += 64u) {
+        // the non-canonical tiles: the wave's own (its own tile words and
+        // types), or with BAL a static share of the block's once every wave
+        // of the block is done (workgroup-scope release / acquire)
+        uint32_t ns = nt_w;
+        if (BAL) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            ns = nk > wv ? (nk - wv + CT_WAVES - 1) / CT_WAVES : 0;
+        } else {
+            __threadfence_block();
+        }
+        for (uint32_t j0 = 0; j0 < ns; j0 += 64u) {
             const uint32_t j = j0 + lane;
-            uint64_t om = __ballot(j < nt_w && a.spec_tile[t0 + j * wstep] == 0u);
+            uint64_t om = __ballot(j < ns && a.spec_tile[seq(j)] == 0u);
             while (om) {
                 const uint32_t jj = j0 + (uint32_t)(__ffsll((unsigned long long)om) - 1);
                 om &= om - 1ull;
-                spec_odd_tile(a, t0 + jj * wstep, lane, &s_mx);
+                spec_odd_tile(a, seq(jj), lane, &s_mx);
             }
         }
     }
@@ -4197,6 +4384,7 @@ struct cndp_gpu_ctx {
     uint8_t *sp_tile;     // per 64-frame tile: the main kernel's canonical-tile word
     uint8_t *sp_c2;       // per 64-frame tile: 16 B of type codes (CNDP_TUNE_SPEC_TYPES)
     int tune_spec_types;  // CNDP_TUNE_SPEC_TYPES: 0 auto, 1 always the types, 2 always codes
+    int tune_stream_bal;  // CNDP_TUNE_STREAM_BAL: 1 static, 2 LDS-balanced, 0 auto (balanced l3fwd stream only)
     uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch
                                    // uniform, [2] the last call ran the full speculation passes
     uint64_t sp_n_cap, sp_b_cap;
@@ -5451,10 +5639,14 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             // [load_nt][meta out][codes] (codes with non-temporal loads only: load_nt 0
             // is an A/B knob, and the codes only save stores)
             static void (*const dfns[2][2][2])(KArgs, uint32_t) = {
-                {{k_cnet_defer<false, false, false>, k_cnet_defer<false, false, false>},
-                 {k_cnet_defer<false, true, false>, k_cnet_defer<false, true, false>}},
-                {{k_cnet_defer<true, false, false>, k_cnet_defer<true, false, true>},
-                 {k_cnet_defer<true, true, false>, k_cnet_defer<true, true, true>}}};
+                {{k_cnet_defer<false, false, false, false>, k_cnet_defer<false, false, false, false>},
+                 {k_cnet_defer<false, true, false, false>, k_cnet_defer<false, true, false, false>}},
+                {{k_cnet_defer<true, false, false, false>, k_cnet_defer<true, false, true, false>},
+                 {k_cnet_defer<true, true, false, false>, k_cnet_defer<true, true, true, false>}}};
+            // the LDS-balanced schedule (CNDP_TUNE_STREAM_BAL), non-temporal loads: [meta out][codes]
+            static void (*const bfns[2][2])(KArgs, uint32_t) = {
+                {k_cnet_defer<true, false, false, true>, k_cnet_defer<true, false, true, true>},
+                {k_cnet_defer<true, true, false, true>, k_cnet_defer<true, true, true, true>}};
             const bool meta_out = a.ptype != nullptr || a.rxmeta != nullptr;
             a.spec_tile = B ? c->sp_tile : nullptr; // written by this kernel only
             // chunk lists (CNDP_TUNE_SPEC_LISTS): groups must be lane quads of the
@@ -5489,8 +5681,12 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             }
             if (!c->tune_lnt)
                 a.spec_codes = 0;
-            hipLaunchKernelGGL(dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0][a.spec_codes ? 1 : 0], dim3((uint32_t)gd),
-                               dim3(CT_THREADS), 0, s, a, (uint32_t)n_tiles);
+            // the balanced schedule when asked for (auto keeps the static one here:
+            // C4 0.8 % slower balanced, C5 0.8 % faster)
+            const bool bal = c->tune_lnt && c->tune_stream_bal == 2;
+            hipLaunchKernelGGL(bal ? bfns[meta_out ? 1 : 0][a.spec_codes ? 1 : 0]
+                                   : dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0][a.spec_codes ? 1 : 0],
+                               dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, (uint32_t)n_tiles);
             if (!a.wl_fold)
                 hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
             if (a.spec_codes) // the coded types, should the passes read them after all
@@ -5592,6 +5788,24 @@ static int classify_l3(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, 
                 a.rw_parts = c->tune_rw_wb == 1 ? 4u : c->tune_rw_wb == 2 ? 5u : c->rw_parts;
                 *fused = true;
                 hipLaunchKernelGGL(rfns[nti][li], dim3(gt), dim3(FAST_THREADS), 0, s, a, n_tiles);
+                HIP_TRY(hipGetLastError());
+                return 0;
+            }
+            if (c->tune_stream_bal != 1) {
+                // one STREAM_BW-wave block a CU, the block's tiles shared by an LDS counter
+                static const tile_fn bfns[2][2][2] = {
+                    {{k_classify_stream_bal<CNDP_MODE_L3FWD, false, false>,
+                      k_classify_stream_bal<CNDP_MODE_L3FWD, false, true>},
+                     {k_classify_stream_bal<CNDP_MODE_L3FWD, true, false>,
+                      k_classify_stream_bal<CNDP_MODE_L3FWD, true, true>}},
+                    {{k_classify_stream_bal<CNDP_MODE_HASH, false, false>,
+                      k_classify_stream_bal<CNDP_MODE_HASH, false, true>},
+                     {k_classify_stream_bal<CNDP_MODE_HASH, true, false>,
+                      k_classify_stream_bal<CNDP_MODE_HASH, true, true>}}};
+                uint32_t gb = (uint32_t)c->num_cu * (c->tune_bpc ? (uint32_t)c->tune_bpc : 1u);
+                if ((uint64_t)gb > n_tiles)
+                    gb = (uint32_t)n_tiles;
+                hipLaunchKernelGGL(bfns[mi][nti][li], dim3(gb), dim3(STREAM_BW * 64), 0, s, a, n_tiles);
                 HIP_TRY(hipGetLastError());
                 return 0;
             }
@@ -8004,6 +8218,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 2)
             return -EINVAL;
         c->tune_spec_types = value;
+        return 0;
+    case CNDP_TUNE_STREAM_BAL:
+        if (value < 0 || value > 2)
+            return -EINVAL;
+        c->tune_stream_bal = value;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

@@ -14,6 +14,9 @@
 //                       k_classify_stream), staged through the XOR-swizzled
 //                       LDS tile, `pf` tiles in flight per wave; per frame the
 //                       given 4 / 4 / 2-B outputs stored non-temporal.
+//   cndp_probe_slots_bal  the same with the balanced schedule of
+//                       k_classify_stream_bal (512-thread blocks, one a CU, the
+//                       block's tiles shared by its waves through an LDS counter).
 //   cndp_probe_windows  C4 / C5: the first 64 B of each frame at a stride or
 //                       at u64 offsets, 4 lanes a frame, 16 frames a load
 //                       instruction (as k_cnet_defer's cs_issue), the offsets
@@ -97,6 +100,67 @@ __global__ __launch_bounds__(256) void k_probe_slots(const uint8_t *slab, uint64
     }
 }
 
+// the C2 / C3 kernel's balanced schedule (k_classify_stream_bal): one 512-thread
+// block a CU, the block's tiles (blockIdx + k * gridDim) handed to its 8 waves
+// by an LDS counter, each wave's first three static, the next index drawn a
+// trip before its load; 2 tiles in flight
+__global__ __launch_bounds__(512) void k_probe_slots_bal(const uint8_t *slab, uint64_t n_tiles, ProbeOut o)
+{
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[8][256];
+    __shared__ uint32_t s_next;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint64_t G = gridDim.x, b = blockIdx.x, NONE = ~0ull;
+    const uint64_t nk = b < n_tiles ? (n_tiles - b + G - 1) / G : 0;
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    if (threadIdx.x == 0)
+        s_next = 24u;
+    auto tile_of = [&](uint64_t k) { return k < nk ? b + k * G : NONE; };
+    auto issue = [&](u32x4(&d)[4], uint64_t tt) {
+        const uint8_t *g = slab + (tt < n_tiles ? tt : n_tiles - 1u) * 4096u;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            d[k] = ldnt(g + (64u * k + lane) * 16u);
+    };
+    uint64_t q0 = tile_of(wv), q1 = tile_of(wv + 8u), q2 = tile_of(wv + 16u);
+    u32x4 r[2][4];
+    issue(r[0], q0);
+    issue(r[1], q1);
+    __syncthreads();
+    auto draw = [&](uint64_t prev) -> uint32_t {
+        uint32_t v = 0;
+        if (prev != NONE && lane == 0)
+            v = atomicAdd(&s_next, 1u);
+        return v;
+    };
+    uint32_t kv = draw(q2);
+    while (q0 != NONE) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = r[0][k];
+            r[0][k] = r[1][k];
+        }
+        issue(r[1], q2);
+        const uint64_t qn = q2 == NONE ? NONE : tile_of((uint32_t)__builtin_amdgcn_readfirstlane((int)kv));
+        kv = draw(qn);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t f = 16u * k + fr_in_k;
+            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t sw = (lane >> 2) & 3u;
+        const u32x4 p0 = tile[lane * 4u + (0u ^ sw)], p1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+        __builtin_amdgcn_wave_barrier();
+        probe_store(o, q0 * 64u + lane, p0.w ^ p1.y ^ p1.z ^ p1.w ^ p2.x ^ p2.y);
+        q0 = q1;
+        q1 = q2;
+        q2 = qn;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_probe_windows(const uint8_t *slab, uint64_t stride, const uint64_t *offs,
                                                        uint64_t data_off, uint64_t n, ProbeOut o)
 {
@@ -149,6 +213,18 @@ int cndp_probe_slots(const void *slab, uint64_t n, uint32_t *o_a, uint32_t *o_b,
         hipLaunchKernelGGL(k_probe_slots<1>, grid, blk, 0, (hipStream_t)stream, (const uint8_t *)slab, nt, o);
     else
         hipLaunchKernelGGL(k_probe_slots<2>, grid, blk, 0, (hipStream_t)stream, (const uint8_t *)slab, nt, o);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// C2 / C3 shape with the balanced schedule: one 512-thread block a CU
+int cndp_probe_slots_bal(const void *slab, uint64_t n, uint32_t *o_a, uint32_t *o_b, uint16_t *o_q, void *stream)
+{
+    const uint64_t nt = n / 64u;
+    if (!slab || nt == 0)
+        return -22;
+    const ProbeOut o{o_a, o_b, o_q, nullptr, nullptr};
+    const uint32_t g = (uint64_t)cus() < nt ? (uint32_t)cus() : (uint32_t)nt;
+    hipLaunchKernelGGL(k_probe_slots_bal, dim3(g), dim3(512), 0, (hipStream_t)stream, (const uint8_t *)slab, nt, o);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -363,7 +363,8 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           (wave-tile kernels) (default 1)
  *   CNDP_TUNE_UNROLL        packets per lane per loop trip: 1 (the only value kept)
  *   CNDP_TUNE_BLOCKS_PER_CU grid = CUs x this, grid-stride beyond (default 0 = auto:
- *                           2 for the streamed wave-tile kernel, 4 for the others)
+ *                           1 512-thread block for the balanced streamed wave-tile kernel,
+ *                           2 for the static one, 4 for the others)
  *   CNDP_TUNE_TILE          l3fwd/hash kernel for packed 64-B slots: 1 = streamed wave tile
  *                           (frames two tiles ahead, each FIB gather level one loop trip
  *                           apart; default), 0 = the per-lane kernel every other layout
@@ -417,7 +418,14 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           tile, when the previous call was a uniform batch, whose
  *                           passes read no such type; a batch that needs them after all
  *                           gets them written out by one more launch), 1 = always the
- *                           types, 2 = always codes (tests force all three) */
+ *                           types, 2 = always codes (tests force all three)
+ *   CNDP_TUNE_STREAM_BAL    wave-tile kernels' schedule: 1 = static (wave w takes tiles w,
+ *                           w + W, ...), 2 = balanced (a block's waves share its tiles
+ *                           through an LDS counter; the streamed l3fwd / hash kernel then
+ *                           runs one 512-thread block a CU), 0 = auto: balanced for the
+ *                           streamed l3fwd / hash kernel (2-3 % faster on C3, 1-2 % on C2),
+ *                           static for the cnet kernel (balanced: C4 0.8 % slower, C5 0.8 %
+ *                           faster) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -434,6 +442,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_SPEC_GRID 14
 #define CNDP_TUNE_SPEC_LISTS 15
 #define CNDP_TUNE_SPEC_TYPES 16
+#define CNDP_TUNE_STREAM_BAL 17
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words

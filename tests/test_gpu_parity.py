@@ -128,6 +128,36 @@ def test_cnet_imix_c4_parity(cnet, gpu):
     assert (ref["edge"] == 1).mean() > 0.5
 
 
+def test_cnet_balanced_schedule(cnet, gpu):
+    """CNDP_TUNE_STREAM_BAL 2: k_cnet_defer with the block's tiles shared by
+    its waves through an LDS counter == the oracle (IMIX offsets, 1536-B strided
+    frames, fewer tiles than waves, a ragged end, 1 and 2 blocks a CU, with the
+    speculation model on: its tile words and odd-tile scan come from other waves)"""
+    cl, routes, v6, t4, t6 = cnet
+    cases = [pktgen.imix(1 << 17, v4routes=routes, v6routes=v6, device=gpu, seed=90),
+             pktgen.packed_ipv4(1 << 15, slot=1536, frame_len=1500, routes=routes, device=gpu, seed=91),
+             pktgen.imix(64 * 7 + 5, v4routes=routes, v6routes=v6, device=gpu, seed=92),
+             _sparse_gtp(30000, routes, v6, gpu, seed=93)]
+    try:
+        for fr in cases:
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+            for bal in (1, 2):
+                for bpc in (0, 1):
+                    cl.set_tuning(cnet_tile=1, stream_bal=bal, blocks_per_cu=bpc)
+                    assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
+        cl.set_tuning(cnet_spec=256)  # the speculation model over a chain of calls
+        st = np.zeros(1, np.uint16)
+        for k, fr in enumerate([cases[3], cases[0], cases[3]]):
+            cl.set_tuning(stream_bal=2 if k % 2 == 0 else 1)
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6, spec_burst=256, spec_state=st)
+            o = cl.alloc_outputs(fr.n, 64, device=gpu)
+            cl.classify(fr, N.CNDP_MODE_CNET, out=o)
+            torch.cuda.synchronize()
+            assert_same(o, ref)
+    finally:
+        cl.set_tuning(stream_bal=0, blocks_per_cu=0, cnet_spec=256)
+
+
 @pytest.mark.parametrize("cached", [False, True])
 def test_frame_memory_parity(cnet, l3, gpu, cached):
     """Frames in cndp_gpu_frames_alloc memory (uncached by default: what a
@@ -467,6 +497,29 @@ def test_tuning_variants_identical(l3, gpu, mode):
                         assert_same(run_gpu(cl, fr, mode), ref)
     finally:
         cl.set_tuning(tile=1, nt=1, unroll=1, blocks_per_cu=0, load_nt=1)
+
+
+@pytest.mark.parametrize("mode", [N.CNDP_MODE_L3FWD, N.CNDP_MODE_HASH])
+def test_stream_schedules_identical(l3, gpu, mode):
+    """CNDP_TUNE_STREAM_BAL: the streamed wave-tile kernel with its static schedule
+    and with the block's tiles shared through an LDS counter give the oracle's
+    bits -- fewer tiles than waves, ragged ends, a 16-B data_off, 1 and 2 blocks
+    a CU, fuzz frames (the slow-hash paths)."""
+    cl, fib, t4 = l3
+    cases = [pktgen.packed_ipv4(n, routes=pktgen.l3fwd_routes(), device=gpu, seed=40 + k)
+             for k, n in enumerate((64 * 5, 64 * 300 + 9, 64 * 4096 + 63, 300001))]
+    base = pktgen.packed_ipv4(64 * 1000 + 38, routes=pktgen.l3fwd_routes(), device=gpu, seed=45)
+    cases.append(pktgen.Frames(base.slab, 64 * 1000 + 37, stride=64, data_off=16))
+    cases.append(pktgen.fuzz_frames(64 * 800 + 5, seed=46, slot=64, device=gpu))
+    try:
+        for fr in cases:
+            ref = oracle_classify(mode, fr, tables4=t4)
+            for bal in (1, 2):
+                for bpc in (0, 1, 2):
+                    cl.set_tuning(tile=1, stream_bal=bal, blocks_per_cu=bpc)
+                    assert_same(run_gpu(cl, fr, mode), ref)
+    finally:
+        cl.set_tuning(tile=1, stream_bal=0, blocks_per_cu=0)
 
 
 def test_tile_path_ragged_and_offset(l3, gpu):

@@ -357,6 +357,74 @@ __global__ __launch_bounds__(256) void k_slots_pf(const uint8_t *slab, uint32_t 
     }
 }
 
+// NW-wave blocks; the block's tiles (blockIdx + k * gridDim) handed to its
+// waves by an LDS counter (BAL) or statically (wave w takes k = w, w + NW, ...);
+// 2 tiles in flight, the next index grabbed a trip before it is needed
+template <int NW, bool BAL>
+__global__ __launch_bounds__(NW * 64) void k_slots_bal(const uint8_t *slab, uint32_t nt, Out o)
+{
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[NW][256];
+    __shared__ uint32_t s_ctr;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    u32x4 *tile = s_tile[wv];
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t nk = b < nt ? (nt - b + G - 1u) / G : 0u; // the block's tiles
+    const uint32_t fr_in_k = lane >> 2, part = lane & 3u;
+    if (BAL) {
+        if (threadIdx.x == 0)
+            s_ctr = NW * 3u; // indices < 3 NW are taken statically below
+        __syncthreads();
+    }
+    uint32_t ks = wv; // static: the wave's next k
+    auto grab = [&]() -> uint32_t {
+        uint32_t k;
+        if (BAL && ks >= NW * 3u) {
+            uint32_t v = 0;
+            if (lane == 0)
+                v = atomicAdd(&s_ctr, 1u);
+            k = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        } else {
+            k = ks;
+            ks += NW;
+        }
+        return k < nk ? b + k * G : ~0u;
+    };
+    u32x4 r[2][4];
+    auto issue = [&](u32x4(&d)[4], uint32_t tt) {
+        const uint8_t *g = slab + (uint64_t)(tt < nt ? tt : nt - 1u) * 4096u;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            d[k] = ldnt(g + (64u * k + lane) * 16u);
+    };
+    uint32_t q0 = grab(), q1 = grab(), q2 = grab();
+    issue(r[0], q0);
+    issue(r[1], q1);
+    while (q0 != ~0u) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = r[0][k];
+            r[0][k] = r[1][k];
+        }
+        issue(r[1], q2);
+        const uint32_t q3 = q2 == ~0u ? ~0u : grab();
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t f = 16u * k + fr_in_k;
+            tile[f * 4u + (part ^ ((f >> 2) & 3u))] = v[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t sw = (lane >> 2) & 3u;
+        const u32x4 p0 = tile[lane * 4u + (0u ^ sw)], p1 = tile[lane * 4u + (1u ^ sw)];
+        const u32x4 p2 = tile[lane * 4u + (2u ^ sw)];
+        __builtin_amdgcn_wave_barrier();
+        put(o, (uint64_t)q0 * 64u + lane, p0.w ^ p1.y ^ p1.z ^ p1.w ^ p2.x ^ p2.y);
+        q0 = q1;
+        q1 = q2;
+        q2 = q3;
+    }
+}
+
 template <class F> static float timed(F launch)
 {
     hipEvent_t a, b;
@@ -417,6 +485,26 @@ int main()
     CK(hipMalloc((void **)&full.q, n5 * 2));
     nh.a = full.a;
     CK(hipDeviceSynchronize());
+    if (getenv("PROBE10_BAL")) { // C3 shape: static vs LDS-balanced waves inside big blocks, 4-GiB ring
+        const uint32_t nt = (uint32_t)(n4 / 64);
+        int k = 0;
+        auto ring = [&]() { return slab + (uint64_t)(k++ & 3) * n4 * 64; };
+        printf("slots C3 256-thread blocks x2/CU static %.4f\n", timed([&] {
+                   hipLaunchKernelGGL(k_slots_pf<2>, dim3(ncu * 2), dim3(256), 0, 0, ring(), nt, full);
+               }));
+        for (int rep = 0; rep < 2; rep++) {
+            printf("slots C3 512-thread x2/CU: static %.4f balanced %.4f; 1024-thread x1/CU: static %.4f balanced %.4f; "
+                   "512-thread x1/CU: static %.4f balanced %.4f ms\n",
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<8, false>), dim3(ncu * 2), dim3(512), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<8, true>), dim3(ncu * 2), dim3(512), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<16, false>), dim3(ncu), dim3(1024), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<16, true>), dim3(ncu), dim3(1024), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<8, false>), dim3(ncu), dim3(512), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<8, true>), dim3(ncu), dim3(512), 0, 0, ring(), nt, full); }));
+            fflush(stdout);
+        }
+        return 0;
+    }
     if (getenv("PROBE10_SHAPES")) { // C3 shape sweep: tiles in flight x blocks a CU, 4 batches in a ring
         const uint32_t nt = (uint32_t)(n4 / 64);
         for (int pf : {1, 2, 3, 4}) {
