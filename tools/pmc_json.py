@@ -12,7 +12,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {"c2": "k_classify_stream<2, true, true>", "c3": "k_classify_stream<0, true, true>",
+KERNEL = {"c2": "k_classify_stream_bal<2, true, true>", "c3": "k_classify_stream_bal<0, true, true>",
           "c4": "k_cnet_defer<", "c5": "k_cnet_defer<"}
 PKTS = {"c2": 1 << 24, "c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25}
 ALGO = {"c2": 70, "c3": 74, "c4": 74, "c5": 68}
