@@ -1561,19 +1561,15 @@ __global__ __launch_bounds__(CNET_THREADS) void k_classify_cnet(KArgs a)
 // Frames that are not 16-B aligned or have < 64 bytes before the slab end
 // are staged with bounded byte loads (zero past the end), like Win.
 // ---------------------------------------------------------------------------
+// the balanced k_cnet_defer (CNDP_TUNE_STREAM_BAL): one block of this many
+// threads a CU, all of the CU's waves sharing one LDS counter
+#ifndef CD_BAL_THREADS
+#define CD_BAL_THREADS 1024
+#endif
 #ifndef CT_THREADS
 #define CT_THREADS 512
 #endif
 #define CT_WAVES (CT_THREADS / 64)
-// CD_MINW > 0: ask the compiler for that many waves a SIMD (A/B builds)
-#ifndef CD_MINW
-#define CD_MINW 0
-#endif
-#if CD_MINW
-#define CD_BOUNDS __launch_bounds__(CT_THREADS, CD_MINW)
-#else
-#define CD_BOUNDS __launch_bounds__(CT_THREADS)
-#endif
 
 // frame base (bytes from slab) of packet i, or ~0 when i >= n
 __device__ __forceinline__ uint64_t ct_base(const KArgs &a, uint64_t i, uint64_t off_i)
@@ -2152,10 +2148,11 @@ __device__ __forceinline__ void cnet_defer_tail(const KArgs &a, uint32_t *rows, 
 // read the offsets of next trip (the LDS atomic's return is waited for with
 // the trip's other LDS traffic); the waves the SQ favours take more tiles.
 template <bool LNT, bool META, bool CODES, bool BAL>
-__global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
+__global__ __launch_bounds__(BAL ? CD_BAL_THREADS : CT_THREADS) void k_cnet_defer(KArgs a, uint32_t n_tiles)
 {
+    constexpr uint32_t NTH = BAL ? CD_BAL_THREADS : CT_THREADS, NWV = NTH / 64u;
     __shared__ uint32_t s_t[CD_TAB_WORDS];
-    __shared__ __attribute__((aligned(16))) u32x4 s_tile[CT_WAVES][256];
+    __shared__ __attribute__((aligned(16))) u32x4 s_tile[NWV][256];
     __shared__ uint16_t s_reta[CNDP_RETA_MAX];
     __shared__ uint32_t s_bins[CNDP_BINS_MAX + 2];
     __shared__ uint32_t s_sf[64];
@@ -2166,27 +2163,27 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     u32x4 *tile = s_tile[wv];
     const uint32_t G = gridDim.x, bk = blockIdx.x;
-    const uint32_t wstep = G * CT_WAVES;
-    const uint32_t t0 = bk * CT_WAVES + wv;
+    const uint32_t wstep = G * NWV;
+    const uint32_t t0 = bk * NWV + wv;
     const uint32_t nt_w = t0 < n_tiles ? (n_tiles - t0 + wstep - 1) / wstep : 0;
     // BAL: the block's tiles are the static schedule's tiles of its waves, in
-    // round order -- index k is round k / CT_WAVES, wave k % CT_WAVES -- so the
+    // round order -- index k is round k / NWV, wave k % NWV -- so the
     // block's waves work on neighbouring tiles at any time (tiles G apart
     // instead: C5 11 % slower, the windows of one CU spread over many pages);
     // they form a prefix of k, nk of them (the waves' static counts)
     uint32_t nk = 0;
     if (BAL) {
-        const uint32_t tb0 = bk * CT_WAVES;
-        for (uint32_t w = 0; w < CT_WAVES; w++)
+        const uint32_t tb0 = bk * NWV;
+        for (uint32_t w = 0; w < NWV; w++)
             nk += tb0 + w < n_tiles ? (n_tiles - tb0 - w + wstep - 1) / wstep : 0;
     }
     auto tile_k = [&](uint32_t k) -> uint32_t {
-        return k < nk ? (k / CT_WAVES) * wstep + bk * CT_WAVES + k % CT_WAVES : CD_NONE;
+        return k < nk ? (k / NWV) * wstep + bk * NWV + k % NWV : CD_NONE;
     };
     // the wave's k-th tile while its sequence is static
     auto seq = [&](uint32_t k) -> uint32_t {
         if (BAL)
-            return tile_k(wv + k * CT_WAVES);
+            return tile_k(wv + k * NWV);
         return k < nt_w ? t0 + k * wstep : CD_NONE;
     };
     uint32_t q0 = seq(0), q1 = seq(1), q2 = seq(2), q3 = seq(3);
@@ -2210,18 +2207,18 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
         s_sf[tid] = 0;
     if (tid == 0) {
         s_mx = 0;
-        s_next = 4u * CT_WAVES;
+        s_next = 4u * NWV;
     }
-    for (uint32_t k = tid; k < CD_TAB_WORDS; k += CT_THREADS)
+    for (uint32_t k = tid; k < CD_TAB_WORDS; k += NTH)
         s_t[k] = a.ttab[(CD_NIB ? TABN_OFF : 0) + k];
     u32x4 r[2][4];
     cs_issue<LNT>(a, q0, n_tiles, off.o0, lane, r[0]);
     cs_issue<LNT>(a, q1, n_tiles, off.o1, lane, r[1]);
-    for (uint32_t k = tid; k <= a.reta_mask; k += CT_THREADS)
+    for (uint32_t k = tid; k <= a.reta_mask; k += NTH)
         s_reta[k] = a.reta[k];
     const bool count = a.bins != nullptr;
     if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += NTH)
             s_bins[k] = 0;
 #if CD_STAMP
     const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime(); // after the prologue's issue
@@ -2285,8 +2282,8 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     }
     (void)trips; // (CD_STAMP)
 #if CD_STAMP
-    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES) {
-        unsigned long long *o = cd_stamps + (blockIdx.x * CT_WAVES + wv) * 16u;
+    if (lane == 0 && blockIdx.x * NWV + wv < CD_STAMP_WAVES) {
+        unsigned long long *o = cd_stamps + (blockIdx.x * NWV + wv) * 16u;
         for (int k = 0; k < 4; k++)
             o[k] = acc[k];
         o[4] = acc[7] - acc[6]; // the loop
@@ -2306,7 +2303,7 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __syncthreads();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            ns = nk > wv ? (nk - wv + CT_WAVES - 1) / CT_WAVES : 0;
+            ns = nk > wv ? (nk - wv + NWV - 1) / NWV : 0;
         } else {
             __threadfence_block();
         }
@@ -2321,13 +2318,13 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
         }
     }
 #if CD_STAMP
-    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES)
-        cd_stamps[(blockIdx.x * CT_WAVES + wv) * 16u + 12u] = __builtin_amdgcn_s_memrealtime(); // odd tiles done
+    if (lane == 0 && blockIdx.x * NWV + wv < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * NWV + wv) * 16u + 12u] = __builtin_amdgcn_s_memrealtime(); // odd tiles done
 #endif
     if (count || a.spec_flags || (a.spec_allow & SPEC_ALLOW_LISTS))
         __syncthreads();
     if (count)
-        for (uint32_t k = tid; k < a.n_bins + 2; k += CT_THREADS)
+        for (uint32_t k = tid; k < a.n_bins + 2; k += NTH)
             if (s_bins[k])
                 atomicAdd(&a.bins[k], (unsigned long long)s_bins[k]);
     if (a.spec_flags && tid < 64 && s_sf[tid])
@@ -2335,17 +2332,17 @@ __global__ CD_BOUNDS void k_cnet_defer(KArgs a, uint32_t n_tiles)
     if ((a.spec_allow & SPEC_ALLOW_LISTS) && tid == 0 && s_mx)
         atomicOr(&a.spec_meta[SPEC_MX], s_mx);
 #if CD_STAMP
-    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES)
-        cd_stamps[(blockIdx.x * CT_WAVES + wv) * 16u + 13u] = __builtin_amdgcn_s_memrealtime(); // flushes issued
+    if (lane == 0 && blockIdx.x * NWV + wv < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * NWV + wv) * 16u + 13u] = __builtin_amdgcn_s_memrealtime(); // flushes issued
 #endif
     if (a.wl_fold)
         // (the general parse takes the byte tables: from LDS, or global memory
         // when LDS holds the nibble tables)
-        cnet_defer_tail<CT_THREADS, 256>(a, (uint32_t *)&s_tile[0][0], CD_NIB ? a.ttab : s_t, s_reta, s_bins, s_sf,
+        cnet_defer_tail<NTH, 256>(a, (uint32_t *)&s_tile[0][0], CD_NIB ? a.ttab : s_t, s_reta, s_bins, s_sf,
                                          count);
 #if CD_STAMP
-    if (lane == 0 && blockIdx.x * CT_WAVES + wv < CD_STAMP_WAVES)
-        cd_stamps[(blockIdx.x * CT_WAVES + wv) * 16u + 11u] = __builtin_amdgcn_s_memrealtime(); // the wave's end
+    if (lane == 0 && blockIdx.x * NWV + wv < CD_STAMP_WAVES)
+        cd_stamps[(blockIdx.x * NWV + wv) * 16u + 11u] = __builtin_amdgcn_s_memrealtime(); // the wave's end
 #endif
 }
 
@@ -4384,7 +4381,7 @@ struct cndp_gpu_ctx {
     uint8_t *sp_tile;     // per 64-frame tile: the main kernel's canonical-tile word
     uint8_t *sp_c2;       // per 64-frame tile: 16 B of type codes (CNDP_TUNE_SPEC_TYPES)
     int tune_spec_types;  // CNDP_TUNE_SPEC_TYPES: 0 auto, 1 always the types, 2 always codes
-    int tune_stream_bal;  // CNDP_TUNE_STREAM_BAL: 1 static, 2 LDS-balanced, 0 auto (balanced l3fwd stream only)
+    int tune_stream_bal;  // CNDP_TUNE_STREAM_BAL: 1 static, 2 LDS-balanced, 0 auto
     uint32_t *sp_hint, *sp_hint_d; // pinned, mapped: [0] bit length of the last worklist count, [1] last batch
                                    // uniform, [2] the last call ran the full speculation passes
     uint64_t sp_n_cap, sp_b_cap;
@@ -5632,8 +5629,14 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                 HIP_TRY(hipMemsetAsync(a.wl_n, 0, 4, s));
             c->wl_clean = 0;
             const uint64_t n_tiles = ((uint64_t)b->n + 63u) / 64u;
-            uint64_t gd = (n_tiles + CT_WAVES - 1) / CT_WAVES;
-            const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : 2u;
+            // the schedule (CNDP_TUNE_STREAM_BAL): balanced -- one CD_BAL_THREADS block a
+            // CU, all its waves sharing the block's tiles -- for strided frames (C5 2.5 %
+            // faster), static 512-thread blocks, two a CU, for frames at offsets (IMIX:
+            // C4 0.8-3 % slower balanced)
+            const bool bal = c->tune_lnt && (c->tune_stream_bal == 2 || (c->tune_stream_bal == 0 && !b->offsets));
+            const uint32_t nthr = bal ? CD_BAL_THREADS : CT_THREADS;
+            uint64_t gd = (n_tiles + nthr / 64u - 1) / (nthr / 64u);
+            const uint32_t bpc = c->tune_bpc ? (uint32_t)c->tune_bpc : bal ? 1u : 2u;
             if (gd > (uint64_t)c->num_cu * bpc)
                 gd = (uint64_t)c->num_cu * bpc;
             // [load_nt][meta out][codes] (codes with non-temporal loads only: load_nt 0
@@ -5681,12 +5684,9 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
             }
             if (!c->tune_lnt)
                 a.spec_codes = 0;
-            // the balanced schedule when asked for (auto keeps the static one here:
-            // C4 0.8 % slower balanced, C5 0.8 % faster)
-            const bool bal = c->tune_lnt && c->tune_stream_bal == 2;
             hipLaunchKernelGGL(bal ? bfns[meta_out ? 1 : 0][a.spec_codes ? 1 : 0]
                                    : dfns[c->tune_lnt ? 1 : 0][meta_out ? 1 : 0][a.spec_codes ? 1 : 0],
-                               dim3((uint32_t)gd), dim3(CT_THREADS), 0, s, a, (uint32_t)n_tiles);
+                               dim3((uint32_t)gd), dim3(nthr), 0, s, a, (uint32_t)n_tiles);
             if (!a.wl_fold)
                 hipLaunchKernelGGL(k_classify_cnet<true>, dim3(g), dim3(CNET_THREADS), 0, s, a);
             if (a.spec_codes) // the coded types, should the passes read them after all

@@ -420,12 +420,12 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           gets them written out by one more launch), 1 = always the
  *                           types, 2 = always codes (tests force all three)
  *   CNDP_TUNE_STREAM_BAL    wave-tile kernels' schedule: 1 = static (wave w takes tiles w,
- *                           w + W, ...), 2 = balanced (a block's waves share its tiles
- *                           through an LDS counter; the streamed l3fwd / hash kernel then
- *                           runs one 512-thread block a CU), 0 = auto: balanced for the
- *                           streamed l3fwd / hash kernel (2-3 % faster on C3, 1-2 % on C2),
- *                           static for the cnet kernel (balanced: C4 0.8 % slower, C5 0.8 %
- *                           faster) */
+ *                           w + W, ...), 2 = balanced (one block a CU -- 512 threads for the
+ *                           streamed l3fwd / hash kernel, 1024 for the cnet kernel -- whose
+ *                           waves share its tiles through an LDS counter), 0 = auto:
+ *                           balanced for the l3fwd / hash kernel (C3 2-3 % faster, C2 1-2 %)
+ *                           and for cnet frames at a stride (C5 2.5-3.6 %), static for cnet
+ *                           frames at offsets (IMIX C4: balanced 0.8-3 % slower) */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
