@@ -564,16 +564,18 @@ def probe_ceiling(st, stream, steps: int, kern_ms: float) -> dict:
             return launch
         for bpc in (4, 8):
             rows[f"windows_bpc{bpc}"] = timed(wlaunch(bpc, False))
+        rows["windows_balanced_1024x1"] = timed(wlaunch(0, False))
         shape = ("the first 64 B of each frame (4 lanes a frame, 16 frames a load instruction, nt loads"
                  + (", u64 offsets read coalesced" if fr0.offsets is not None else f", {fr0.stride}-B stride")
                  + "), the kernel's result stores (nh / hash / queue / edge + the 2-B packet type of the "
-                 "speculation model), nothing else")
+                 "speculation model), nothing else; static schedules (4 / 8 blocks a CU) and k_cnet_defer's "
+                 "balanced one (one 1024-thread block a CU, tiles shared through an LDS counter)")
     best = min(rows, key=rows.get)
     res = {"probe_ms": round(rows[best], 5), "kernel_over_probe": round(kern_ms / rows[best], 4),
            "probe_variant": best, "probe_variants_ms": {k: round(v, 5) for k, v in rows.items()},
            "probe_shape": shape}
     if cnet:
-        bpc = int(best.rsplit("bpc", 1)[1])
+        bpc = int(best.rsplit("bpc", 1)[1]) if "bpc" in best else 0  # 0: the balanced probe
         res["probe_nh_only_ms"] = round(timed(wlaunch(bpc, True)), 5)
         res["probe_nh_only_note"] = ("the same windows with only the 4-B next hop stored (SURVEY §8(d)'s "
                                      "algorithmic bytes): probe_ms - this = the cost of the other result bytes")

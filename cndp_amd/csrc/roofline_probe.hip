@@ -17,7 +17,8 @@
 //   cndp_probe_slots_bal  the same with the balanced schedule of
 //                       k_classify_stream_bal (512-thread blocks, one a CU, the
 //                       block's tiles shared by its waves through an LDS counter).
-//   cndp_probe_windows  C4 / C5: the first 64 B of each frame at a stride or
+//   cndp_probe_windows  C4 / C5 (static, or bpc 0: k_cnet_defer's balanced
+//                       schedule): the first 64 B of each frame at a stride or
 //                       at u64 offsets, 4 lanes a frame, 16 frames a load
 //                       instruction (as k_cnet_defer's cs_issue), the offsets
 //                       read coalesced; per frame the given 4 / 4 / 2 / 1 / 2-B
@@ -184,6 +185,50 @@ __global__ __launch_bounds__(256) void k_probe_windows(const uint8_t *slab, uint
     }
 }
 
+// the cnet kernel's balanced schedule (k_cnet_defer with BAL): one 1024-thread
+// block a CU, the block's tiles in the static schedule's round order handed to
+// its 16 waves by an LDS counter (each wave's first tile static, the next
+// drawn a tile ahead)
+__global__ __launch_bounds__(1024) void k_probe_windows_bal(const uint8_t *slab, uint64_t stride, const uint64_t *offs,
+                                                            uint64_t data_off, uint64_t n, ProbeOut o)
+{
+    __shared__ uint32_t s_next;
+    constexpr uint32_t NW = 16;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t tiles = n / 64u, G = gridDim.x, bk = blockIdx.x, ws = G * NW, NONE = ~0ull;
+    uint64_t nk = 0;
+    for (uint32_t w = 0; w < NW; w++)
+        nk += bk * NW + w < tiles ? (tiles - bk * NW - w + ws - 1) / ws : 0;
+    auto tile_k = [&](uint64_t k) { return k < nk ? (k / NW) * ws + bk * NW + k % NW : NONE; };
+    if (threadIdx.x == 0)
+        s_next = NW;
+    __syncthreads();
+    uint64_t g = tile_k(wv);
+    uint32_t kv = 0;
+    if (g != NONE && lane == 0)
+        kv = atomicAdd(&s_next, 1u);
+    while (g != NONE) {
+        const uint64_t gn = tile_k((uint32_t)__builtin_amdgcn_readfirstlane((int)kv));
+        if (gn != NONE && lane == 0)
+            kv = atomicAdd(&s_next, 1u);
+        const uint64_t mine = (offs ? offs[g * 64u + lane] : (g * 64u + lane) * stride) + data_off;
+        uint32_t res = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t fo = __shfl(mine, 16 * k + (int)(lane >> 2));
+            const u32x4 w = ldnt(slab + fo + (lane & 3u) * 16u);
+            uint32_t x = w.x ^ w.y ^ w.z ^ w.w;
+            x ^= __shfl_xor(x, 1);
+            x ^= __shfl_xor(x, 2);
+            const uint32_t src = __shfl(x, (int)((lane & 15u) * 4u));
+            if ((lane >> 4) == (uint32_t)k)
+                res = src;
+        }
+        probe_store(o, g * 64u + lane, res);
+        g = gn;
+    }
+}
+
 static int g_cus;
 
 static int cus()
@@ -230,15 +275,20 @@ int cndp_probe_slots_bal(const void *slab, uint64_t n, uint32_t *o_a, uint32_t *
 
 // C4 / C5 shape: the first 64 B of each of n frames (whole 64-frame tiles),
 // frame i at offs[i] (if offs) or i * stride, plus data_off; the caller keeps
-// every window inside the slab
+// every window inside the slab.  bpc 256-thread blocks a CU, or bpc 0: the
+// balanced schedule (k_probe_windows_bal)
 int cndp_probe_windows(const void *slab, uint64_t stride, const uint64_t *offs, uint64_t data_off, uint64_t n,
                        uint32_t *o_a, uint32_t *o_b, uint16_t *o_q, uint8_t *o_e, uint16_t *o_t, int bpc, void *stream)
 {
-    if (!slab || n < 64 || bpc < 1 || bpc > 8)
+    if (!slab || n < 64 || bpc < 0 || bpc > 8)
         return -22;
     const ProbeOut o{o_a, o_b, o_q, o_e, o_t};
-    hipLaunchKernelGGL(k_probe_windows, dim3((unsigned)(cus() * bpc)), dim3(256), 0, (hipStream_t)stream,
-                       (const uint8_t *)slab, stride, offs, data_off, n, o);
+    if (bpc == 0) // the balanced schedule: one 1024-thread block a CU
+        hipLaunchKernelGGL(k_probe_windows_bal, dim3((unsigned)cus()), dim3(1024), 0, (hipStream_t)stream,
+                           (const uint8_t *)slab, stride, offs, data_off, n, o);
+    else
+        hipLaunchKernelGGL(k_probe_windows, dim3((unsigned)(cus() * bpc)), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t *)slab, stride, offs, data_off, n, o);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 }
