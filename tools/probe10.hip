@@ -493,6 +493,14 @@ int main()
                    hipLaunchKernelGGL(k_slots_pf<2>, dim3(ncu * 2), dim3(256), 0, 0, ring(), nt, full);
                }));
         for (int rep = 0; rep < 2; rep++) {
+            printf("slots C3 balanced x1/CU: 512-thread %.4f  640-thread %.4f  768-thread %.4f  896-thread %.4f ms\n",
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<8, true>), dim3(ncu), dim3(512), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<10, true>), dim3(ncu), dim3(640), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<12, true>), dim3(ncu), dim3(768), 0, 0, ring(), nt, full); }),
+                   timed([&] { hipLaunchKernelGGL((k_slots_bal<14, true>), dim3(ncu), dim3(896), 0, 0, ring(), nt, full); }));
+            fflush(stdout);
+        }
+        for (int rep = 0; rep < 2; rep++) {
             printf("slots C3 512-thread x2/CU: static %.4f balanced %.4f; 1024-thread x1/CU: static %.4f balanced %.4f; "
                    "512-thread x1/CU: static %.4f balanced %.4f ms\n",
                    timed([&] { hipLaunchKernelGGL((k_slots_bal<8, false>), dim3(ncu * 2), dim3(512), 0, 0, ring(), nt, full); }),
