@@ -3260,6 +3260,16 @@ __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uin
             need = !(p0 && p1 && p2 && p3) || ((O & below) >> lu) != 0ull || (!s0p && ub == 0ull) ||
                    lane + 1u == ng;
         }
+#if CD_STAMP
+        if (bb == c0) { // the first burst: the longest walk (groups) and the lanes that walk
+            const unsigned long long bef = sg.U & ((1ull << lane) - 1ull);
+            uint32_t wl = lane < ng && need ? lane - (bef ? 64u - (uint32_t)__clzll(bef) : 0u) : 0u;
+            for (int o = 32; o > 0; o >>= 1)
+                wl = max(wl, (uint32_t)__shfl_xor((int)wl, o));
+            SP_TS(15, (uint64_t)wl | ((uint64_t)__popcll(__ballot(lane < ng && need)) << 32));
+            SP_TS(14, __builtin_amdgcn_s_memrealtime());
+        }
+#endif
         if (lane < ng && need) {
             // the state entering group `lane`
             uint32_t cur = s0, l = low0, e = cnet_edge(s0);
@@ -3281,6 +3291,7 @@ __device__ __forceinline__ void spec_replay_walk(const KArgs &a, uint32_t B, uin
             }
             const u32x4 x = *(const u32x4 *)(sb + 4 * lane);
             const bool quiet = (x.x & 0xffu) == l && (x.y & 0xffu) == l && (x.z & 0xffu) == l && (x.w & 0xffu) == l;
+
             nxt = cur;
             if (!quiet && ((x.z & 0xffffu) == (x.w & 0xffffu) || e == (x.w >> 16)))
                 nxt = x.w & 0xffffu;
@@ -3731,6 +3742,8 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
     SP_TS(11, 0u);
     SP_TS(12, 0u);
     SP_TS(13, 0u);
+    SP_TS(14, 0u);
+    SP_TS(15, 0u);
     if (unif) { // block-uniform
         const uint32_t T = s_in, E = cnet_edge(T);
         const bool tcan = spec_canon(T & 0xffu) == E;

@@ -72,7 +72,11 @@ for arg in sys.argv[1:] or ["c4", "c5"]:
                       f"{np.median(rel(b[:, 1])):.1f}, tables filled (p50 / max) "
                       f"{np.median(rel(fill[:, 2])) if len(fill) else 0:.1f} / {rel(fill[:, 2].max()) if len(fill) else 0:.1f}, "
                       f"last end {rel(endv.max()):.1f}", flush=True)
-                for k, nm in ((6, "lookback"), (7, "types staged"), (10, "walk burst 0"), (11, "walk burst 1"),
+                v15 = b[b[:, 15] > 0][:, 15]
+                if len(v15):
+                    print(f"    first burst: longest walk (groups) p50 {np.median(v15 & 0xffffffff):.0f} max "
+                          f"{(v15 & 0xffffffff).max()}, walking lanes p50 {np.median(v15 >> 32):.0f}", flush=True)
+                for k, nm in ((6, "lookback"), (7, "types staged"), (14, "burst 0 walk set up"), (10, "walk burst 0"), (11, "walk burst 1"),
                               (12, "walk burst 2"), (13, "walk burst 3"), (8, "replay walk"), (9, "replay fixed")):
                     v = b[b[:, k] > 0][:, k]
                     if len(v):
