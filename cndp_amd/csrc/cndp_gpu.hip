@@ -3714,20 +3714,14 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
     // wave-uniform in SGPRs (the chunk index and all that derives from it)
     const uint64_t wid = (uint64_t)bid * 4 + __builtin_amdgcn_readfirstlane(wv), W = (uint64_t)nblk * 4;
     // the prologue's inputs in one round trip: every meta word it decides on,
-    // the chunk list's count and this wave's entry (read past the count and
-    // ignored there), and for wave 0 the batch's last burst (the final state)
-    // -- independent loads, waited for together
+    // the chunk list's count and this block's entry (read past the count and
+    // ignored there) -- independent loads, waited for together
     const LutRegs lr = cnet_lut_load256(threadIdx.x);
     const uint32_t unif = meta[SPEC_UNIF], s_in = meta[SPEC_IN] & 0xffffu;
     const uint32_t m_stop = meta[SPEC_SKIP] | meta[SPEC_NOLOCAL], mx = meta[SPEC_MX], K = meta[0];
     const uint32_t sig = lane < SPEC_KMAX ? meta[1 + lane] : 0u;
     const uint32_t *const cwl = a.spec_cwl ? a.spec_cwl : meta;
-    const uint32_t nl_w = cwl[0], lc_w = a.spec_cwl && wid < nch ? cwl[1 + wid] : 0u;
-    uint32_t fq0 = 0u, fq1 = 0u;
-    if (wid == 0) { // wave-uniform
-        const uint64_t fb0 = (nb - 1) * B;
-        spec_group_regs(a.spec_t16, fb0, (uint32_t)((uint64_t)a.n - fb0 < B ? (uint64_t)a.n - fb0 : B), lane, fq0, fq1);
-    }
+    const uint32_t nl_w = cwl[0], lc_w = a.spec_cwl && bid < nch ? cwl[1 + bid] : 0u;
     SP_TS(0, __builtin_amdgcn_s_memrealtime());
     asm volatile("" ::"s"(unif), "s"(s_in), "s"(m_stop), "s"(mx), "s"(K), "v"(sig), "s"(nl_w), "s"(lc_w));
     SP_TS(1, __builtin_amdgcn_s_memrealtime());
@@ -3802,12 +3796,13 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
             lists = K <= SPEC_KMAX && __ballot(clash) == 0ull;
         }
     }
-    // the lists' blocks without a listed chunk (block 0 also walks the final
-    // state) leave before the table fill: most of the grid, block-uniform
+    // lists: block k < nl takes listed chunk k (one of its bursts a wave),
+    // block nl walks the final state; the others leave before the table fill
+    // (most of the grid, block-uniform)
     const uint32_t nl = lists ? nl_w : 0u;
-    SP_TS(4, lists ? ((uint64_t)bid * 4 < nl ? 4u : 3u) : 5u);
+    SP_TS(4, lists ? (bid <= nl ? 4u : 3u) : 5u);
     SP_TS(5, nl);
-    if (lists && bid != 0 && (uint64_t)bid * 4 >= nl)
+    if (lists && bid > nl)
         return;
     // without the lists: the first SPEC_LQ chunks' tile words and previous
     // bursts, all in flight during the table fill (one round trip for the
@@ -3820,21 +3815,23 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
         if (!lists)
             spec_chunk_pre(a, B, nch, wid + k * W, lane, tws[k], q0s[k], q1s[k]);
     }
-    // lists: the wave's first listed chunk -- its types and the burst before
-    // it -- in flight during the table fill
+    // lists: this wave's burst of the block's chunk -- its types and the groups
+    // of the burst before -- in flight during the table fill
     constexpr uint32_t LR = CH * 256 / 512 > 0 ? CH * 256 / 512 : 1;
     const bool lvec = (B & 7u) == 0;
     u32x4 lv[LR];
     uint32_t lq0 = 0u, lq1 = 0u;
-    uint64_t lc = 0;
-    if (lists && wid < nl) {
-        lc = lc_w;
-        const uint64_t c0 = lc * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-        if (lvec)
-            spec_chunk_load<CH>(a, B, c0, c1, lane, lv);
-        if (lc > 0)
-            spec_group_regs(a.spec_t16, (c0 - 1) * B, B, lane, lq0, lq1);
-    }
+    auto burst_pre = [&](uint64_t lb) {
+        lq0 = lq1 = 0u;
+        if (lb < nb) {
+            if (lvec)
+                spec_chunk_load<CH>(a, B, lb, lb + 1, lane, lv);
+            if (lb > 0)
+                spec_group_regs(a.spec_t16, (lb - 1) * B, B, lane, lq0, lq1);
+        }
+    };
+    if (lists && bid < nl)
+        burst_pre((uint64_t)lc_w * CH + wv);
     cnet_lut_store256(s_lut, threadIdx.x, lr);
     const uint32_t nb2 = a.bins ? a.n_bins + 2u : 0u;
     for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
@@ -3842,46 +3839,52 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
     __syncthreads();
     SP_TS(2, __builtin_amdgcn_s_memrealtime());
     if (lists) {
-        if (wid == 0) { // the final node state (meta[-1]): the walk in the last chunk
-            const uint64_t l0 = (nch - 1) * CH, l1 = l0 + CH < nb ? l0 + CH : nb;
-            uint32_t sf = 0;
-            if (spec_lookback(a.spec_t16, a.n, B, l0, l1, lane, s_lut, sf, true, fq0, fq1)) {
-                if (lane == 0)
-                    meta[-1] = sf;
-            } else if (lane == 0) {
-                spec_flag_full(meta);
+        // every burst of a listed chunk at once: burst b's entering state is the
+        // walk from the last universal group before it (spec_lookback over the
+        // bursts [b - 2 CH, b), the chunk's own earlier ones included: they hold
+        // the same types the node walked), so the chunk's bursts replay side by
+        // side.  A chunk with a burst whose state is not found there is left
+        // whole to the full passes (done[c] = 0), none of it replayed here.
+        for (uint64_t k = bid; k <= nl; k += nblk) {
+            if (k == nl) { // the final node state (meta[-1]): the walk in the last chunk
+                if (wv == 0) {
+                    const uint64_t l0 = (nch - 1) * CH, l1 = l0 + CH < nb ? l0 + CH : nb;
+                    uint32_t sf = 0;
+                    if (spec_lookback(a.spec_t16, a.n, B, l0, l1, lane, s_lut, sf)) {
+                        if (lane == 0)
+                            meta[-1] = sf;
+                    } else if (lane == 0) {
+                        spec_flag_full(meta);
+                    }
+                }
+                continue;
             }
-        }
-        for (uint64_t k = wid; k < nl; k += W) {
-            if (k != wid) { // the chunk's types and the previous burst's groups in one round trip
-                lc = a.spec_cwl[1 + k];
-                const uint64_t d0 = lc * CH, d1 = d0 + CH < nb ? d0 + CH : nb;
-                if (lvec)
-                    spec_chunk_load<CH>(a, B, d0, d1, lane, lv);
-                lq0 = lq1 = 0u;
-                if (lc > 0)
-                    spec_group_regs(a.spec_t16, (d0 - 1) * B, B, lane, lq0, lq1);
-            }
-            const uint64_t c = lc, c0 = c * CH, c1 = c0 + CH < nb ? c0 + CH : nb;
-            const bool vec = lvec;
-            const u32x4(&v)[LR] = lv;
+            const uint64_t c = k == bid ? (uint64_t)lc_w : (uint64_t)a.spec_cwl[1 + k];
+            const uint64_t lb = c * CH + wv;
+            if (k != bid)
+                burst_pre(lb);
             uint32_t s0 = s_in;
-            const bool lb_ok = c == 0 || spec_lookback(a.spec_t16, a.n, B, c0 - CH, c0, lane, s_lut, s0, true, lq0, lq1);
+            bool ok = true;
+            if (lb < nb && lb > 0)
+                ok = spec_lookback(a.spec_t16, a.n, B, lb >= 2 * CH ? lb - 2 * CH : 0, lb, lane, s_lut, s0, true, lq0,
+                                   lq1);
             SP_TS(6, __builtin_amdgcn_s_memrealtime());
-            if (!lb_ok) {
-                if (lane == 0) { // left to the full passes (done[] of the others is not read)
+            if (!__syncthreads_and(ok)) { // block-uniform
+                if (threadIdx.x == 0) { // left to the full passes (done[] of the others is not read)
                     done[c] = 0;
                     spec_flag_full(meta);
                 }
                 continue;
             }
-            if (vec)
-                spec_chunk_types_v<CH>(a, B, c0, c1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr, v);
-            else
-                spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr);
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0)
+            if (threadIdx.x == 0)
                 done[c] = 1;
+            if (lb < nb) {
+                if (lvec)
+                    spec_chunk_types_v<CH>(a, B, lb, lb + 1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr, lv);
+                else
+                    spec_chunk_types<CH>(a, B, lb, lb + 1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr);
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nb2; k += 256u)
