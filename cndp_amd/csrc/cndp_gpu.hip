@@ -1701,7 +1701,8 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #endif
 // timing-only ablations (tools/abbuild.sh -DCD_ABL=<bits>; wrong results,
 // but every index stays in bounds): 1 no Toeplitz, 2 no chain levels, 4 no
-// first gather (and so no chain), 16 no result stores but the edge
+// first gather (and so no chain), 8 at most two IPv6 tbl8 levels, 16 no result
+// stores but the edge
 #ifndef CD_ABL
 #define CD_ABL 0
 #endif
@@ -1783,7 +1784,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t n_tiles, uint32
         // one branch-free body for both families: the key bytes stream out of
         // q0..q3, the level count and the table pair are fixed per lane
         const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
-        uint32_t rem = d6 ? 13u : (a.dir16 ? 2u : 1u);
+        uint32_t rem = d6 ? ((CD_ABL & 8) ? 2u : 13u) : (a.dir16 ? 2u : 1u);
         // the table pointers pinned in SGPRs before the per-lane select:
         // otherwise the select is of their kernarg addresses and the pointer
         // itself a vector load each trip, waited for at the chain's first level
