@@ -3678,12 +3678,18 @@ __global__ __launch_bounds__(WPB * 64) void k_spec_local(KArgs a, uint32_t B, ui
 //                  have spec_canon(T), so when that is E only the other tiles
 //                  are looked at (frame by frame); otherwise every chunk goes
 //                  through spec_uniform_range as without tile words;
+//   chunk lists    (the fast kernel listed the chunks holding a frame off its
+//                  low byte's common edge, and no group can move the state
+//                  off a common edge): a listed chunk a block, a burst a wave,
+//                  each burst's entering state from the look-back over the
+//                  bursts before it, replayed side by side;
 //   otherwise      per chunk: the entering state from the look-back, then
 //                  quiet when every tile is canonical and the state agrees
-//                  with its low byte's common edge (or has another low byte).
-// Any grid is correct (chunks and tiles are strided over the waves): the host
-// sizes it from the previous call's hint -- one chunk per wave, or a small
-// grid when that call was a uniform batch.
+//                  with its low byte's common edge (or has another low byte),
+//                  else replayed by the wave that looked.
+// Any grid is correct (chunks, bursts and tiles are strided over the blocks
+// and waves): the host sizes it from the previous call's hint -- a wave per
+// SPEC_LQ chunks, or a small grid when that call was a uniform batch.
 
 // chunk c's tile words (lane < tiles covering it: <= 17 for B <= 256) and
 // the burst before it (its groups, one per lane)
@@ -3926,7 +3932,7 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
         const uint32_t cn = spec_canon(s0 & 0xffu);
         if (odd || (cn != 0xFFu && cn != cnet_edge_l(s_lut, s0))) {
             // its types decide: read (one more round trip, this wave only) and
-            // replayed here, as k_spec_fallback would from a list
+            // replayed here
             spec_chunk_types<CH>(a, B, c0, c1, s0, lane, s_stw, s_lut, a.bins ? s_bins : nullptr);
             __builtin_amdgcn_wave_barrier();
         }
