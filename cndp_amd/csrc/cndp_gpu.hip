@@ -1701,10 +1701,13 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 #endif
 // timing-only ablations (tools/abbuild.sh -DCD_ABL=<bits>; wrong results,
 // but every index stays in bounds): 1 no Toeplitz, 2 no chain levels, 4 no
-// first gather (and so no chain), 8 at most two IPv6 tbl8 levels, 16 no result
+// first gather (and so no chain), 8 at most CD_V6CAP IPv6 tbl8 levels, 16 no result
 // stores but the edge
 #ifndef CD_ABL
 #define CD_ABL 0
+#endif
+#ifndef CD_V6CAP
+#define CD_V6CAP 2 // CD_ABL bit 8: IPv6 tbl8 levels walked at most
 #endif
 // CD_NIB 1: k_cnet_defer's Toeplitz from the nibble tables (4.5 KiB of LDS,
 // conflict-free reads) instead of the byte tables (36 KiB, random banks)
@@ -1784,7 +1787,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t n_tiles, uint32
         // one branch-free body for both families: the key bytes stream out of
         // q0..q3, the level count and the table pair are fixed per lane
         const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
-        uint32_t rem = d6 ? ((CD_ABL & 8) ? 2u : 13u) : (a.dir16 ? 2u : 1u);
+        uint32_t rem = d6 ? ((CD_ABL & 8) ? (uint32_t)CD_V6CAP : 13u) : (a.dir16 ? 2u : 1u);
         // the table pointers pinned in SGPRs before the per-lane select:
         // otherwise the select is of their kernarg addresses and the pointer
         // itself a vector load each trip, waited for at the chain's first level
