@@ -1702,7 +1702,8 @@ __device__ __forceinline__ const KAS KArgs &kargs_fresh(const KArgs &a)
 // timing-only ablations (tools/abbuild.sh -DCD_ABL=<bits>; wrong results,
 // but every index stays in bounds): 1 no Toeplitz, 2 no chain levels, 4 no
 // first gather (and so no chain), 8 at most CD_V6CAP IPv6 tbl8 levels, 16 no result
-// stores but the edge
+// stores but the edge, 32 five IPv6 levels every lane, all within one line of the
+// first tbl8 group (the walk's dependent latency without its distinct lines)
 #ifndef CD_ABL
 #define CD_ABL 0
 #endif
@@ -1787,7 +1788,8 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t n_tiles, uint32
         // one branch-free body for both families: the key bytes stream out of
         // q0..q3, the level count and the table pair are fixed per lane
         const bool d6 = (sb.ptf & (1u << 17)) != 0u, d4 = (sb.ptf & (1u << 16)) != 0u;
-        uint32_t rem = d6 ? ((CD_ABL & 8) ? (uint32_t)CD_V6CAP : 13u) : (a.dir16 ? 2u : 1u);
+        uint32_t rem = d6 ? ((CD_ABL & 8) ? (uint32_t)CD_V6CAP : (CD_ABL & 32) ? 5u : 13u) : (a.dir16 ? 2u : 1u);
+        const uint32_t g6 = eb >> 1; // (CD_ABL & 32)
         // the table pointers pinned in SGPRs before the per-lane select:
         // otherwise the select is of their kernarg addresses and the pointer
         // itself a vector load each trip, waited for at the chain's first level
@@ -1798,7 +1800,9 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t n_tiles, uint32
         const GAS uint32_t *const tb2 = d6 ? t6 : t8;
         uint32_t q0 = sb.q0, q1 = sb.q1, q2 = sb.q2, q3 = sb.q3;
         while (!(CD_ABL & 2) && __any(more)) {
-            const uint32_t idx = ((eb >> 1) << 8) | (q0 & 0xffu);
+            uint32_t idx = ((eb >> 1) << 8) | (q0 & 0xffu);
+            if (CD_ABL & 32)
+                idx = d6 ? (g6 << 8) | (eb & 7u) : idx;
             if (more)
                 eb = tb[idx];
             tb = tb2;
@@ -1807,7 +1811,7 @@ __device__ __forceinline__ void cd_trip(const KArgs &a, uint32_t n_tiles, uint32
             q2 = alignb(q3, q2, 1);
             q3 >>= 8;
             rem--;
-            more = more & ((eb & 1u) != 0u) & (rem != 0u);
+            more = more & (((eb & 1u) != 0u) | ((CD_ABL & 32) && d6)) & (rem != 0u);
         }
     }
     CD_TS(0); // B's chain
