@@ -222,6 +222,93 @@ def test_cnet_deep_v6_chains(gpu):
     assert np.array_equal(nh[hit] & 0xFFFF, gold[hit])
 
 
+def _v6_dst_frames(n, live, v6, routes, gpu, rng):
+    """IMIX frames whose IPv6 destinations fall under the given (ip, depth)
+    routes (host bits random; a quarter under a random one of the list's
+    prefixes at a shorter depth, so some miss the deepest routes)."""
+    fr = pktgen.imix(n, v4routes=routes, v6routes=v6, device=gpu, v6_frac=0.7, seed=int(rng.integers(1 << 30)))
+    base = fr.offsets + fr.data_off
+    is6 = (fr.slab[base + 12] == 0x86) & (fr.slab[base + 13] == 0xDD)
+    keys = list(live)
+    pick = rng.integers(0, len(keys), n)
+    dst = np.zeros((n, 16), np.uint8)
+    for k in range(n):
+        ip, d = keys[pick[k]]
+        if k % 4 == 3:
+            d = max(1, d - int(rng.integers(1, 17)))
+        v = int.from_bytes(ip, "big")
+        mask = ((1 << 128) - 1) ^ ((1 << (128 - d)) - 1)
+        v = (v & mask) | (int.from_bytes(rng.bytes(16), "big") & ~mask & ((1 << 128) - 1))
+        dst[k] = np.frombuffer(v.to_bytes(16, "big"), np.uint8)
+    pos = (base[is6, None] + 38 + torch.arange(16, device=gpu)).reshape(-1)
+    fr.slab[pos] = torch.as_tensor(dst, device=gpu)[is6].reshape(-1)
+    return fr
+
+
+def test_cnet_v6_route_churn(gpu):
+    """IPv6 routes added / deleted between cnet calls: k_cnet_defer's trie
+    chain (and the general kernel) over the mirror the painter keeps ==
+    the oracle's trie walk of the live routes, every round -- /16-/128
+    routes, C4's /33-/64 shape, whole subtrees deleted (their tbl8 groups
+    freed, then taken again by others), a /24 added over deeper routes and
+    some of those deleted after it."""
+    from cndp_amd.classify import Classifier
+    from cndp_amd.fib import Fib6, node_ip6_add_input
+    from helpers import CNET_DEF
+    rng = np.random.default_rng(2024)
+    fib, _, routes, v6, v4vals, _ = cnet_fibs()
+    fib6 = Fib6("churn6", N.CNE_FIB_TRIE, default_nh=CNET_DEF, max_routes=8192,
+                nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 14)
+    cl = Classifier(0)
+    cl.set_fib(fib, fib6)
+    t4 = O.dir24_8_build(v4vals, CNET_DEF, 256)
+    live = {}
+
+    def rand_route(top):
+        d = int(rng.choice([int(rng.integers(16, 33)), int(rng.integers(33, 65)), int(rng.integers(65, 129))]))
+        v = (top << 96) | int.from_bytes(rng.bytes(12), "big") >> int(rng.integers(0, 40))
+        v &= ((1 << 128) - 1) ^ ((1 << (128 - d)) - 1)
+        return v.to_bytes(16, "big"), d
+
+    def add(ip, d):
+        nh = int(rng.integers(0, 1 << 16))
+        if node_ip6_add_input(fib6, ip, d, nh) == 0:
+            live[(ip, d)] = nh | ((2 if d == 32 else 1) << 24)
+
+    tops = [0x20010db8, 0x20010db9, 0x2a000001, 0xfd000000]
+    for _ in range(700):
+        add(*rand_route(tops[int(rng.integers(0, 4))]))
+    try:
+        for rnd_ in range(6):
+            if rnd_:
+                # a whole subtree out: every route under one /32 of the list
+                gone = tops[rnd_ % 4]
+                for key in [k for k in live if int.from_bytes(k[0][:4], "big") == gone and rng.random() < 0.9]:
+                    assert fib6.delete(*key) == 0
+                    del live[key]
+                for key in list(live):
+                    if rng.random() < 0.1:
+                        assert fib6.delete(*key) == 0
+                        del live[key]
+                for _ in range(150):
+                    add(*rand_route(tops[int(rng.integers(0, 4))]))
+                if rnd_ == 3:  # a /24 over deeper routes, then the deeper ones out
+                    add(bytes.fromhex("20010d") + bytes(13), 24)
+                    for key in [k for k in live if k[0][:3] == bytes.fromhex("20010d") and k[1] > 24][:50]:
+                        assert fib6.delete(*key) == 0
+                        del live[key]
+            t6 = O.trie_build([(ip, d, nh) for (ip, d), nh in live.items()], CNET_DEF, 1 << 14)
+            fr = _v6_dst_frames(20000, live, v6, routes, gpu, rng)
+            ref = oracle_classify(O.MODE_CNET, fr, tables4=t4, tables6=t6)
+            for ct in (CNET_KERNELS if rnd_ % 2 == 0 else (1,)):
+                cl.set_tuning(cnet_tile=ct)
+                assert_same(run_gpu(cl, fr, N.CNDP_MODE_CNET), ref)
+            hit = (ref["nh"] & 0xFFFFFF) != CNET_DEF
+            assert hit.mean() > 0.3
+    finally:
+        cl.set_tuning(cnet_tile=1)
+
+
 def test_cnet_fuzz_parity(cnet, gpu):
     """cne_get_ptype over random structures (parity vs the unpinned restatement)."""
     cl, routes, v6, t4, t6 = cnet
