@@ -1310,6 +1310,10 @@ def main():
     from cndp_amd import dist as D
     world, rank, local = setup_dist()
     dev = torch.device(f"cuda:{local}")
+    if rank == 0:
+        import torch.distributed as tdist
+        if tdist.is_initialized():
+            log(f"[bench] process group: {tdist.get_backend()}, world {tdist.get_world_size()}")
     t0 = time.time()
     st = build_state(args.config, dev, rank, args.packets or None, args.in_route_frac, args.ring)
     torch.cuda.synchronize()
@@ -1451,8 +1455,9 @@ def main():
             "fib_update": fu,
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    import torch.distributed as tdist
+    if tdist.is_initialized():
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

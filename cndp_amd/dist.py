@@ -16,7 +16,10 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    # CNDP_DIST_FORCE=1: a process group (and so the collectives) at one rank
+    # too -- RCCL exercised on a one-GPU box (tests/test_dist.py)
+    force = os.environ.get("CNDP_DIST_FORCE") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -37,13 +40,13 @@ def shard(n_total: int, rank: int, world: int) -> tuple[int, int]:
 
 def final_count_reduce(bins: torch.Tensor) -> torch.Tensor:
     """Sum the per-bin counters of every rank in place (one collective)."""
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.all_reduce(bins, op=dist.ReduceOp.SUM)
     return bins
 
 
 def max_over_ranks(values: list[float], device) -> list[float]:
     t = torch.tensor(values, dtype=torch.float64, device=device)
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t]

@@ -77,3 +77,29 @@ def test_shard_covers_everything():
             assert parts[0][0] == 0 and parts[-1][1] == n
             for (a, b), (c, d) in zip(parts, parts[1:]):
                 assert b == c and a <= b
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_bench():
+    """The bench's distributed path over RCCL ("nccl") on the one GPU a box
+    has: torchrun with one rank and CNDP_DIST_FORCE=1, so the process group
+    exists and the count reduce and the max over ranks are real RCCL
+    all-reduces (identities at one rank).  The bins must still count every
+    frame of every timed step."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n, steps = 1 << 20, 3
+    env = dict(os.environ, CNDP_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--config", "c3",
+           "--packets", str(n), "--steps", str(steps), "--warmup", "1", "--no-e2e", "--no-cpu-baseline",
+           "--no-parity", "--no-imix", "--no-node", "--no-probe", "--ring", "1"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [s for s in r.stdout.splitlines() if s.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
+    assert rec["config"]["bins_total"] == n * steps
+    assert "process group: nccl, world 1" in r.stderr
