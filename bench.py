@@ -58,6 +58,68 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def rank_launch_cmd(n: int, argv: list[str], port: int) -> list[str]:
+    """The torchrun command that runs this script as n ranks on one node (the
+    driver's own form: --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def check_rank_line(line: str, n: int) -> dict:
+    """Rank 0's JSON line from an n-rank run: n_gpus must be n and the all-reduced
+    bin counters must count every packet of every rank's timed steps."""
+    res = json.loads(line)
+    cfg = res.get("config", {})
+    want = n * int(cfg.get("packets_per_gpu", -1)) * int(res.get("steps", -1))
+    if res.get("n_gpus") != n:
+        raise ValueError(f"rank line reports n_gpus {res.get('n_gpus')}, launched {n}")
+    if cfg.get("bins_total") != want:
+        raise ValueError(f"bins_total {cfg.get('bins_total')} != {n} ranks x packets x steps = {want}")
+    return res
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` (N > 1) started without torchrun's environment: run
+    the N ranks as a child torchrun (no exec: this process never touches the
+    GPU; torch.cuda.device_count() does not initialise it on this image), pass
+    their output through, and print rank 0's JSON line once it checks out
+    (check_rank_line).  Returns the exit status."""
+    import socket
+    import subprocess
+    backend = os.environ.get("CNDP_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend != "gloo" and ndev < n:
+        log(f"[bench] --gpus {n}: {ndev} device(s) visible (CNDP_DIST_BACKEND=gloo lets ranks share one)")
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = rank_launch_cmd(n, argv, port)
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in proc.stdout:
+        if ln.startswith("{"):
+            line = ln.strip()
+        else:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+    rc = proc.wait()
+    if rc != 0:
+        log(f"[bench] ranks exited with status {rc}")
+        return rc
+    if line is None:
+        log("[bench] no JSON line from rank 0")
+        return 1
+    try:
+        check_rank_line(line, n)
+    except ValueError as ex:
+        log(f"[bench] {ex}")
+        return 1
+    print(line, flush=True)
+    return 0
+
+
 def setup_dist():
     """One process per GPU (torchrun), RCCL ("nccl") for the one collective.
     CNDP_DIST_BACKEND=gloo rehearses the same multi-rank path on a box with
@@ -1266,7 +1328,8 @@ def load_traffic(cfg: str):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); N > 1 without torchrun's env starts them (launch_ranks)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
@@ -1301,6 +1364,11 @@ def main():
     ap.add_argument("--unroll", type=int, default=None)
     ap.add_argument("--bpc", type=int, default=None)
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and args.gpus is not None and args.gpus != int(env_world):
+        sys.exit(f"--gpus {args.gpus} but torchrun started {env_world} ranks")
     if args.frame_mem != "default":
         for k in FRAME_MEM:
             FRAME_MEM[k] = None if args.frame_mem == "torch" else args.frame_mem
