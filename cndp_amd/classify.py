@@ -59,9 +59,12 @@ class Classifier:
                    spec_scan: int | None = None, mbuf_hash: int | None = None,
                    cnet_fold: int | None = None, spec_grid: int | None = None,
                    spec_lists: int | None = None, spec_types: int | None = None,
-                   stream_bal: int | None = None):
-        """Kernel variant knobs (cndp_gpu_set_tuning); never change results."""
+                   stream_bal: int | None = None, spec_wait: int | None = None):
+        """Kernel variant knobs (cndp_gpu_set_tuning); never change results
+        (spec_wait, the speculation pass's wait bound in us, -1 = fault
+        injection, turns an expired wait into -EIO, never into other edges)."""
         for key, v in ((N.CNDP_TUNE_CNET_FOLD, cnet_fold), (N.CNDP_TUNE_SPEC_GRID, spec_grid),
+                       (N.CNDP_TUNE_SPEC_WAIT, spec_wait),
                        (N.CNDP_TUNE_SPEC_LISTS, spec_lists), (N.CNDP_TUNE_SPEC_TYPES, spec_types),
                        (N.CNDP_TUNE_STREAM_BAL, stream_bal),
                        (N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),
@@ -72,6 +75,11 @@ class Classifier:
                        (N.CNDP_TUNE_SPEC_SCAN, spec_scan), (N.CNDP_TUNE_MBUF_HASH, mbuf_hash)):
             if v is not None:
                 N.check(self._L.cndp_gpu_set_tuning(self.h, key, int(v)), "cndp_gpu_set_tuning")
+
+    def stat(self, key: int) -> int:
+        """cndp_gpu_get_stat (CNDP_STAT_*)."""
+        self._L.cndp_gpu_get_stat.restype = ctypes.c_int64
+        return int(N.check(self._L.cndp_gpu_get_stat(self.h, key), "cndp_gpu_get_stat"))
 
     def set_fib(self, fib4=None, fib6=None):
         N.check(self._L.cndp_gpu_set_fib(self.h, fib4.h if fib4 else None, fib6.h if fib6 else None),

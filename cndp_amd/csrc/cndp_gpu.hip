@@ -2391,7 +2391,7 @@ __global__ __launch_bounds__(BAL ? CD_BAL_THREADS : CT_THREADS) void k_cnet_defe
 #define SPEC_IN 131   // the node state entering this batch (meta[-1] becomes the final one)
 #define SPEC_NOLOCAL 132 // one low byte only: no universal group exists, k_spec_local is skipped
 #define SPEC_UNIF 133 // every type has the entering state's low byte: k_spec_local's uniform pass only
-#define SPEC_ERR 134  // a k_spec_fallback barrier poll expired (diagnostic; sticky)
+#define SPEC_ERR 134  // a k_spec_fallback wait expired (the host reads spec_hint[3])
 #define SPEC_HINT 900 // the hint words last written to host memory
 #define SPEC_TAIL 16
 // a type another block of the running kernel stored (write-through, agent
@@ -2428,8 +2428,7 @@ __device__ __forceinline__ void spec_classes(uint32_t t, uint32_t *flags, uint8_
     if (t == 0) {
         meta[SPEC_IN] = s_in;
         meta[SPEC_FULL] = 0;
-        bar[0] = 0;
-        bar[1] = 0;
+        bar[0] = bar[1] = bar[2] = bar[3] = 0; // k_spec_fallback's ticket and phase counts
     }
     const uint32_t w = f | (t == (g0 >> 5) ? 1u << (g0 & 31u) : 0u), cnt = (uint32_t)__popc(w);
     flags[t] = 0;
@@ -3724,6 +3723,7 @@ __device__ __forceinline__ void spec_local_body(const KArgs &a, uint32_t B, uint
                                                 uint16_t *s_lut, uint32_t *s_stw)
 {
     static_assert(CH == SPEC_CH, "spec_chunk_pre");
+    static_assert(CH == 4, "a listed chunk is replayed a burst a wave by a 4-wave block");
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // wave-uniform in SGPRs (the chunk index and all that derives from it)
     const uint64_t wid = (uint64_t)bid * 4 + __builtin_amdgcn_readfirstlane(wv), W = (uint64_t)nblk * 4;
@@ -3992,47 +3992,74 @@ __global__ __launch_bounds__(256) void k_spec_expand(KArgs a, uint32_t n_tiles, 
     }
 }
 
-// Grid barrier of k_spec_fallback: bar[0] counts arrivals (monotonic within a
-// launch), bar[1] is the generation the last arriver publishes; spec_classes
-// zeroes both every call.  Each wave's stores are drained, then lane 0
-// releases, arrives, polls (relaxed sc1 loads + s_sleep) and acquires
-// (MI355X_MICROARCH.md barrier-counter).  The grid is one block per CU, so
-// every block is resident; the poll is bounded all the same (meta[SPEC_ERR]
-// records an expiry: a wrong result, not a hung GPU).
+// k_spec_fallback's work is handed out in ticket order, so it never assumes
+// that its blocks are co-resident (other kernels, other contexts' queues and
+// other graphs' launches may hold CUs).  bar[0] is the ticket counter; the
+// tickets run tables [0, nT), scan rows [nT, nT + nA), the composition
+// nT + nA, and the replay after it.  A phase's items wait only for the
+// earlier phase's completion count (bar[1..3]), and every ticket of that
+// phase was drawn before any ticket that waits on it -- by a block that is
+// running -- so the waits always end, whatever the grid and whoever else is
+// on the chip (the decoupled-lookback argument).  spec_classes zeroes
+// bar[0..3] every call.  A wait is bounded all the same (wait_ticks of the
+// 100 MHz s_memrealtime clock; 0 = fault injection, every wait expires): an
+// expiry stores meta[SPEC_ERR] and the host-visible hint word [3], the
+// waiting block leaves, and the host reports -EIO (cndp_gpu_classify
+// at the context's next cnet call, cndp_gpu_mq_poll for the batch,
+// CNDP_STAT_SPEC_ERR) -- never silent edges.
 #define SPEC_ERR 134
-__device__ __forceinline__ void spec_grid_sync(uint32_t *bar, uint32_t gen, uint32_t *meta, uint32_t nblk)
+#define SPEC_HINT_ERR 3 // spec_hint[3]: a k_spec_fallback wait expired (sticky until the host takes it)
+
+// the block's completion of one work item: every wave's stores drained, then
+// one release-add on the phase's counter
+__device__ __forceinline__ void spec_item_done(uint32_t *ctr)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const uint32_t old = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == gen * nblk - 1u) {
-            __hip_atomic_store(&bar[1], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            for (uint32_t it = 0; __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen; it++) {
-                if (it == (1u << 22)) { // ~0.2 s
-                    __hip_atomic_store(&meta[SPEC_ERR], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
 }
 
-// k_spec_fallback's body: bid / nblk stand for blockIdx.x / gridDim.x; LDS: s_m (the scan's rows, which the
-// tables / replay staging reuse), s_carry, s_lut, s_cls.  Block 0 also empties
-// the fast kernel's chunk list for the next call.
+// wait until *ctr reaches want (lane 0 polls, relaxed loads + s_sleep, then
+// acquires); false for the whole block when the wait expired (reported)
+__device__ __forceinline__ bool spec_item_wait(const uint32_t *ctr, uint32_t want, uint32_t wait_ticks,
+                                               uint32_t *meta, uint32_t *hint, uint32_t *s_flag)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t ok = wait_ticks != 0u; // 0: fault injection, every wait expires
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (ok && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)wait_ticks) {
+                ok = 0u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) {
+            __hip_atomic_store(&meta[SPEC_ERR], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (hint)
+                __hip_atomic_store(&hint[SPEC_HINT_ERR], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        *s_flag = ok;
+    }
+    __syncthreads();
+    return *s_flag != 0u;
+}
+
+// k_spec_fallback's body: bid stands for blockIdx.x; LDS: s_m (the scan's rows, which the
+// tables / replay staging reuse), s_carry, s_lut, s_cls, s_tk (ticket / wait word).  Block 0
+// also empties the fast kernel's chunk list for the next call.
 template <int CH>
 __device__ __forceinline__ void spec_fallback_body(const KArgs &a, uint32_t B, uint64_t nb, uint64_t nch,
                                                    uint32_t *meta, const uint8_t *class_id, uint32_t *T, uint32_t *P,
                                                    uint32_t *Bt, uint32_t *Sblk, uint32_t *S, const uint8_t *done,
                                                    uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated,
-                                                   uint32_t bid, uint32_t nblk, uint32_t *s_m, uint32_t *s_carry,
-                                                   uint16_t *s_lut, uint8_t *s_cls)
+                                                   uint32_t wait_ticks, uint32_t bid, uint32_t nblk, uint32_t *s_m,
+                                                   uint32_t *s_carry, uint16_t *s_lut, uint8_t *s_cls, uint32_t *s_tk)
 {
     static_assert(SPEC_BLK * (SPEC_KMAX + 1) >= 4 * CH * 256, "staging fits the scan rows");
     // what this launch decides on, in one round trip: SPEC_FULL / SPEC_SKIP
@@ -4058,15 +4085,6 @@ __device__ __forceinline__ void spec_fallback_body(const KArgs &a, uint32_t B, u
         }
     }
     const bool full = !gated || m_full;
-    if (bid == 0 && threadIdx.x == 0 && a.spec_hint && gated) {
-        // host hint [2]: whether this call ran the full passes (the next call's
-        // grid: one block while they are not needed -- any grid is correct)
-        const uint32_t h2 = !m_skip && full, old2 = meta[SPEC_HINT + 2];
-        if (h2 != old2) {
-            meta[SPEC_HINT + 2] = h2;
-            __hip_atomic_store(&a.spec_hint[2], h2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
 #if CD_STAMP
     if (bid == 0 && threadIdx.x == 0) {
         sp_stamps[SP_STAMP_BLOCKS * 16 + 1] = __builtin_amdgcn_s_memrealtime();
@@ -4080,73 +4098,100 @@ __device__ __forceinline__ void spec_fallback_body(const KArgs &a, uint32_t B, u
     uint32_t *st = s_m + wv * (CH * 256);
     cnet_lut_fill(s_lut, threadIdx.x, 256);
     spec_cls_stage(s_cls, class_id, threadIdx.x, 256);
-    __syncthreads();
-    const uint64_t W = (uint64_t)nblk * 4;
-    if (K <= SPEC_KMAX)
-        for (uint64_t c = (uint64_t)bid * 4 + wv; c < nch; c += W) {
-            spec_ctable_chunk<CH>(a.spec_t16, a.n, B, nb, nch, c, K, meta, T, st, s_lut, s_cls);
-            __builtin_amdgcn_wave_barrier();
-        }
-    spec_grid_sync(bar, 1, meta, nblk);
-    const uint64_t nblk_s = (nch + SPEC_BLK - 1) / SPEC_BLK;
-    for (uint64_t vb = bid; vb < nblk_s; vb += nblk) {
-        if (K <= kfast)
-            spec_scan_a_body<SPEC_KFAST>(s_m, nch, K, T, P, Bt, vb);
-        else if (K <= kmax)
-            spec_scan_a_body<SPEC_KMAX>(s_m, nch, K, T, P, Bt, vb);
-        __syncthreads();
-    }
-    spec_grid_sync(bar, 2, meta, nblk);
-    if (bid == 0) {
-        uint32_t *state = meta - 1;
-        if (K <= kfast) {
-            spec_scan_c_body<SPEC_KFAST, SPEC_BLK>(s_m, s_carry, nblk_s, K, class_id, Bt, Sblk, state);
-        } else if (K <= kmax) {
-            spec_scan_c_body<SPEC_KMAX, SPEC_BLK>(s_m, s_carry, nblk_s, K, class_id, Bt, Sblk, state);
-        } else if (threadIdx.x == 0) {
-            uint32_t s = meta[SPEC_IN] & 0xffffu;
-            for (uint64_t b = 0; b < nb; b++) {
-                S[b] = s;
-                const uint64_t b0 = b * B;
-                const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
-                const uint32_t m = spec_burst_map(a.spec_t16, b0, cnt, spec_sig(s), false);
-                if (m != SPEC_UNCH)
-                    s = m;
-            }
-            *state = s;
-        }
-    }
-    spec_grid_sync(bar, 3, meta, nblk);
+    // the items: table / replay rows of 4 chunks (a chunk a wave), item i
+    // takes rows i, i + nT, ...; scan rows of SPEC_BLK chunks likewise
+    const uint64_t nrow = (nch + 3) / 4, nblk_s = (nch + SPEC_BLK - 1) / SPEC_BLK;
+    const uint32_t nT = (uint32_t)(nrow < nblk ? nrow : nblk), nA = (uint32_t)(nblk_s < nblk ? nblk_s : nblk);
+    const uint32_t t_a = nT, t_c = nT + nA, t_e = t_c + 1u, t_end = t_e + nT;
     const bool all = !gated || meta[SPEC_NOLOCAL];
-    for (uint64_t c = (uint64_t)bid * 4 + wv; c < nch; c += W) {
-        if (all || !done[c])
-            spec_cemit_chunk<CH>(a, B, nb, nch, c, meta, P, Sblk, S, T, kfast, kmax, st, s_lut);
-        __builtin_amdgcn_wave_barrier();
+    uint32_t *hint = a.spec_hint;
+    for (;;) {
+        __syncthreads(); // s_tk of the previous item read by every wave
+        if (threadIdx.x == 0)
+            *s_tk = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t tk = *s_tk;
+        if (tk >= t_end)
+            return;
+        if (tk < t_a) { // every chunk's map over the signature classes
+            if (K <= SPEC_KMAX)
+                for (uint64_t r = tk; r < nrow; r += nT) {
+                    const uint64_t c = r * 4 + wv;
+                    if (c < nch)
+                        spec_ctable_chunk<CH>(a.spec_t16, a.n, B, nb, nch, c, K, meta, T, st, s_lut, s_cls);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            spec_item_done(&bar[1]);
+        } else if (tk < t_c) { // the chunk maps composed, a block of SPEC_BLK chunks a row
+            if (!spec_item_wait(&bar[1], nT, wait_ticks, meta, hint, s_tk))
+                return;
+            for (uint64_t vb = tk - t_a; vb < nblk_s; vb += nA) {
+                if (K <= kfast)
+                    spec_scan_a_body<SPEC_KFAST>(s_m, nch, K, T, P, Bt, vb);
+                else if (K <= kmax)
+                    spec_scan_a_body<SPEC_KMAX>(s_m, nch, K, T, P, Bt, vb);
+                __syncthreads();
+            }
+            spec_item_done(&bar[2]);
+        } else if (tk == t_c) { // the block totals into block start states and the final node state
+            if (!spec_item_wait(&bar[2], nA, wait_ticks, meta, hint, s_tk))
+                return;
+            uint32_t *state = meta - 1;
+            if (K <= kfast) {
+                spec_scan_c_body<SPEC_KFAST, SPEC_BLK>(s_m, s_carry, nblk_s, K, class_id, Bt, Sblk, state);
+            } else if (K <= kmax) {
+                spec_scan_c_body<SPEC_KMAX, SPEC_BLK>(s_m, s_carry, nblk_s, K, class_id, Bt, Sblk, state);
+            } else if (threadIdx.x == 0) {
+                uint32_t s = meta[SPEC_IN] & 0xffffu;
+                for (uint64_t b = 0; b < nb; b++) {
+                    S[b] = s;
+                    const uint64_t b0 = b * B;
+                    const uint32_t cnt = (uint32_t)((uint64_t)a.n - b0 < B ? (uint64_t)a.n - b0 : B);
+                    const uint32_t m = spec_burst_map(a.spec_t16, b0, cnt, spec_sig(s), false);
+                    if (m != SPEC_UNCH)
+                        s = m;
+                }
+                *state = s;
+            }
+            spec_item_done(&bar[3]);
+        } else { // replay each chunk the local pass did not resolve, from its entering state
+            if (!spec_item_wait(&bar[3], 1u, wait_ticks, meta, hint, s_tk))
+                return;
+            for (uint64_t r = tk - t_e; r < nrow; r += nT) {
+                const uint64_t c = r * 4 + wv;
+                if (c < nch && (all || !done[c]))
+                    spec_cemit_chunk<CH>(a, B, nb, nch, c, meta, P, Sblk, S, T, kfast, kmax, st, s_lut);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
     }
 }
 
 // The general resolution, for what the local pass leaves (meta[SPEC_FULL]) or
-// for everything (gated == 0, CNDP_TUNE_SPEC_SCAN forced): one persistent
-// launch, one block of 4 waves per CU, three phases split by grid barriers --
+// for everything (gated == 0, CNDP_TUNE_SPEC_SCAN forced): one launch of 4-wave
+// blocks whose work items come in ticket order (above), three phases --
 //   tables  every chunk's map over the signature classes and its summary,
-//   scan    the chunk maps composed (blocks of SPEC_BLK chunks, then block 0
+//   scan    the chunk maps composed (blocks of SPEC_BLK chunks, then one item
 //           composes the block totals into block start states and the final
-//           node state; more than SPEC_KMAX classes: block 0's thread 0
+//           node state; more than SPEC_KMAX classes: that item's thread 0
 //           walks the bursts in order instead),
 //   replay  each chunk the local pass did not resolve, from its entering state.
-// With nothing left to resolve it returns at once.
+// With nothing left to resolve it returns at once.  Any grid gives the same
+// results; the host launches a block per CU.
 template <int CH>
 __global__ __launch_bounds__(256) void k_spec_fallback(KArgs a, uint32_t B, uint64_t nb, uint64_t nch, uint32_t *meta,
                                                        const uint8_t *class_id, uint32_t *T, uint32_t *P,
                                                        uint32_t *Bt, uint32_t *Sblk, uint32_t *S, const uint8_t *done,
-                                                       uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated)
+                                                       uint32_t *bar, uint32_t kfast, uint32_t kmax, uint32_t gated,
+                                                       uint32_t wait_ticks)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_m[SPEC_BLK * (SPEC_KMAX + 1)];
     __shared__ uint32_t s_carry[SPEC_KMAX];
     __shared__ __attribute__((aligned(16))) uint16_t s_lut[CNET_LUT_N];
     __shared__ __attribute__((aligned(16))) uint8_t s_cls[2048];
-    spec_fallback_body<CH>(a, B, nb, nch, meta, class_id, T, P, Bt, Sblk, S, done, bar, kfast, kmax, gated, blockIdx.x,
-                           gridDim.x, s_m, s_carry, s_lut, s_cls);
+    __shared__ uint32_t s_tk;
+    spec_fallback_body<CH>(a, B, nb, nch, meta, class_id, T, P, Bt, Sblk, S, done, bar, kfast, kmax, gated,
+                           wait_ticks, blockIdx.x, gridDim.x, s_m, s_carry, s_lut, s_cls, &s_tk);
 }
 
 // ---------------------------------------------------------------------------
@@ -4377,6 +4422,7 @@ struct cndp_gpu_ctx {
     int tune_spec_scan;   // CNDP_TUNE_SPEC_SCAN
     int tune_cnet_fold;   // CNDP_TUNE_CNET_FOLD: 0 hint, 1 always, 2 never
     int tune_spec_grid;   // CNDP_TUNE_SPEC_GRID: 0 hint, 1 shrunk (2 blocks), 2 full
+    int tune_spec_wait_us; // CNDP_TUNE_SPEC_WAIT: k_spec_fallback wait bound (us), -1 = fault injection
     int tune_spec_lists;  // CNDP_TUNE_SPEC_LISTS: 1 chunk lists from the fast kernel (default), 0 off
     int sf_clean, wl_clean; // signature flags / worklist count known zero (no memset needed)
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
@@ -4559,6 +4605,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_cnet_tile = 1;
     c->tune_lnt = 1;
     c->tune_spec_lists = 1;
+    c->tune_spec_wait_us = 1000000; // 1 s: the waits end by construction, this only bounds a fault
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
     c->tune_rw_wb = 2;
@@ -5757,13 +5804,12 @@ static int classify_cnet(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a
                     const uint32_t gl = (uint32_t)((nch + SPEC_WPB - 1) / SPEC_WPB);
                     hipLaunchKernelGGL(lo, dim3(gl), dim3(SPEC_WPB * 64), 0, s, a, B, nb, nch, meta, c->sp_done);
                 }
-                // the general resolution: a block a CU when the previous call needed
-                // it (host hint [2]), else one block that mostly returns at once
-                const bool fb_full = !gated || !c->sp_hint || ((volatile uint32_t *)c->sp_hint)[2];
-                hipLaunchKernelGGL(k_spec_fallback<SPEC_CH>, dim3(fb_full ? (uint32_t)c->num_cu : 1u), dim3(256), 0, s,
-                                   a, B, nb, nch,
-                                   meta, (const uint8_t *)c->sp_class, c->sp_T, P, Bt, Sblk, c->sp_S,
-                                   (const uint8_t *)c->sp_done, a.spec_bar, kfast, kmax, gated);
+                // the general resolution: a block a CU (ticket-ordered items, so
+                // correct whichever blocks get a CU; mostly it returns at once)
+                hipLaunchKernelGGL(k_spec_fallback<SPEC_CH>, dim3((uint32_t)c->num_cu), dim3(256), 0, s, a, B, nb,
+                                   nch, meta, (const uint8_t *)c->sp_class, c->sp_T, P, Bt, Sblk, c->sp_S,
+                                   (const uint8_t *)c->sp_done, a.spec_bar, kfast, kmax, gated,
+                                   c->tune_spec_wait_us < 0 ? 0u : (uint32_t)c->tune_spec_wait_us * 100u);
             } else {
                 hipLaunchKernelGGL(k_spec_tables, dim3(gw), dim3(256), 0, s, (const uint16_t *)a.spec_t16, b->n, B,
                                    nb, (const uint32_t *)meta, (const uint8_t *)c->sp_class, c->sp_T);
@@ -5858,8 +5904,21 @@ static int classify_l3(cndp_gpu_ctx_t *c, const struct cndp_batch *b, KArgs &a, 
     return 0;
 }
 
+// a k_spec_fallback wait of an earlier call expired (its edges are not the
+// node's): taken once, the node state restarts at 0
+static bool spec_err_take(cndp_gpu_ctx_t *c)
+{
+    if (!c->sp_hint || !__atomic_load_n(&c->sp_hint[SPEC_HINT_ERR], __ATOMIC_ACQUIRE))
+        return false;
+    __atomic_store_n(&c->sp_hint[SPEC_HINT_ERR], 0u, __ATOMIC_RELAXED);
+    c->spec_reset = 1;
+    return true;
+}
+
 extern "C" int cndp_gpu_classify(cndp_gpu_ctx_t *c, const struct cndp_batch *b, void *stream)
 {
+    if (c && b && b->mode == CNDP_MODE_CNET && spec_err_take(c))
+        return -EIO;
     return classify_impl(c, b, stream, nullptr, nullptr);
 }
 
@@ -7705,7 +7764,7 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
             c->spec_burst = saved_B ? sl->run_B[k] : 0u;
             c->mq_iplen = (uint32_t *)(D + q->d_ipl) + i0;
             c->mq_win = a.md ? (u32x4 *)(D + q->d_win) + 4ull * i0 : nullptr;
-            r = cndp_gpu_classify(c, &b, s);
+            r = classify_impl(c, &b, s, nullptr, nullptr); // a speculation error is the poll's (mq_poll)
             c->mq_iplen = nullptr;
             c->mq_win = nullptr;
             i0 += sl->run_n[k];
@@ -8109,6 +8168,16 @@ extern "C" int cndp_gpu_mq_poll(cndp_gpu_mq_t *q, void **mbufs, uint16_t *edges,
                 break;
             sl->state = MQ_DONE;
             q->in_flight--;
+            // a speculation wait of this batch expired (its flag was raised
+            // after k_spec_fallback's error store): its edges are not the
+            // node's, so it comes back like a failed launch
+            if (q->conf.mode == CNDP_MQ_CNET && spec_err_take(q->c)) {
+                sl->failed = 1;
+                uint16_t *ed = (uint16_t *)(sl->h + q->h_edge);
+                for (uint32_t i = 0; i < sl->n; i++)
+                    ed[i] = (uint16_t)MQ_EDGE_NONE;
+                q->err = -EIO;
+            }
         }
         if (sl->state != MQ_DONE)
             break;
@@ -8169,11 +8238,13 @@ extern "C" int cndp_gpu_mq_wait(cndp_gpu_mq_t *q)
 
 extern "C" int64_t cndp_gpu_get_stat(cndp_gpu_ctx_t *c, int key)
 {
-    if (!c || (key != CNDP_STAT_CNET_WORKLIST && key != CNDP_STAT_CNET_UNIFORM))
+    if (!c || (key != CNDP_STAT_CNET_WORKLIST && key != CNDP_STAT_CNET_UNIFORM && key != CNDP_STAT_SPEC_ERR))
         return -EINVAL;
     if (!c->sp_hint)
         return 0;
-    return ((volatile uint32_t *)c->sp_hint)[key == CNDP_STAT_CNET_WORKLIST ? 0 : 1];
+    return ((volatile uint32_t *)c->sp_hint)[key == CNDP_STAT_CNET_WORKLIST ? 0
+                                             : key == CNDP_STAT_CNET_UNIFORM ? 1
+                                                                             : SPEC_HINT_ERR];
 }
 
 extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
@@ -8253,6 +8324,11 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 2)
             return -EINVAL;
         c->tune_stream_bal = value;
+        return 0;
+    case CNDP_TUNE_SPEC_WAIT:
+        if (value == 0 || value < -1 || value > 40000000)
+            return -EINVAL;
+        c->tune_spec_wait_us = value;
         return 0;
     case CNDP_TUNE_HOST_CHUNK:
         if (value < 1024)

@@ -94,16 +94,19 @@ static int rw_alloc(void)
 
 /* one per GPU node module loaded in a process (each registers from its
  * constructor and removes itself from its destructor, so a module unloaded by
- * dlclose leaves no pointer behind) */
+ * dlclose leaves no pointer behind).  hook_lock: ip4_rewrite_set_next calls
+ * the hooks under its read side, and unhook takes the write side, so a
+ * destructor returns only once no call into its module is in flight. */
 #define RW_HOOKS_MAX CNDP_NODE_RW_HOOKS_MAX
 static int (*rw_next_hook[RW_HOOKS_MAX])(uint16_t port_id, uint16_t next_index);
+static pthread_rwlock_t hook_lock = PTHREAD_RWLOCK_INITIALIZER;
 
 int cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_index))
 {
     if (!fn)
         return -EINVAL;
     int r = -ENOSPC, free_k = -1;
-    pthread_mutex_lock(&node_lock);
+    pthread_rwlock_wrlock(&hook_lock);
     for (int k = 0; k < RW_HOOKS_MAX; k++) {
         if (rw_next_hook[k] == fn) {
             r = 0;
@@ -116,20 +119,20 @@ int cndp_node_ip4_rewrite_next_hook(int (*fn)(uint16_t port_id, uint16_t next_in
         rw_next_hook[free_k] = fn;
         r = 0;
     }
-    pthread_mutex_unlock(&node_lock);
+    pthread_rwlock_unlock(&hook_lock);
     return r;
 }
 
 int cndp_node_ip4_rewrite_next_unhook(int (*fn)(uint16_t port_id, uint16_t next_index))
 {
     int r = -ENOENT;
-    pthread_mutex_lock(&node_lock);
+    pthread_rwlock_wrlock(&hook_lock); /* waits for hook calls in flight */
     for (int k = 0; k < RW_HOOKS_MAX && fn; k++)
         if (rw_next_hook[k] == fn) {
             rw_next_hook[k] = NULL;
             r = 0;
         }
-    pthread_mutex_unlock(&node_lock);
+    pthread_rwlock_unlock(&hook_lock);
     return r;
 }
 
@@ -141,15 +144,16 @@ int ip4_rewrite_set_next(uint16_t port_id, uint16_t next_index)
     int r = rw_alloc();
     if (!r)
         ip4_rewrite_nm->next_index[port_id] = next_index;
-    int (*hook[RW_HOOKS_MAX])(uint16_t, uint16_t);
-    memcpy(hook, rw_next_hook, sizeof(hook));
     pthread_mutex_unlock(&node_lock);
     /* pktdev_ctrl.c:81-84 calls this right after adding the port's tx edge to
      * ip4_rewrite: the GPU rewrite node mirrors that edge on its drain node,
-     * the GPU receive node on its own (and its clones') */
+     * the GPU receive node on its own (and its clones'); the hooks run under
+     * the read side of hook_lock (a hook must not hook or unhook) */
+    pthread_rwlock_rdlock(&hook_lock);
     for (int k = 0; k < RW_HOOKS_MAX && !r; k++)
-        if (hook[k])
-            r = hook[k](port_id, next_index);
+        if (rw_next_hook[k])
+            r = rw_next_hook[k](port_id, next_index);
+    pthread_rwlock_unlock(&hook_lock);
     return r;
 }
 

@@ -41,13 +41,14 @@ CNDP_TUNE_RW_WB = 8
 CNDP_TUNE_CNET_SPEC = 9
 CNDP_TUNE_LOAD_NT = 10
 CNDP_TUNE_SPEC_SCAN = 11
-CNDP_STAT_CNET_WORKLIST, CNDP_STAT_CNET_UNIFORM = 1, 2
+CNDP_STAT_CNET_WORKLIST, CNDP_STAT_CNET_UNIFORM, CNDP_STAT_SPEC_ERR = 1, 2, 3
 CNDP_TUNE_MBUF_HASH = 12
 CNDP_TUNE_CNET_FOLD = 13
 CNDP_TUNE_SPEC_GRID = 14
 CNDP_TUNE_SPEC_LISTS = 15
 CNDP_TUNE_SPEC_TYPES = 16
 CNDP_TUNE_STREAM_BAL = 17
+CNDP_TUNE_SPEC_WAIT = 18
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
 CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS, CNDP_MQ_F_RX_PARSE = 1, 2, 4, 8
 CNDP_MQ_F_REWRITE = 16

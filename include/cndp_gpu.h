@@ -425,7 +425,18 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           waves share its tiles through an LDS counter), 0 = auto:
  *                           balanced for the l3fwd / hash kernel (C3 2-3 % faster, C2 1-2 %)
  *                           and for cnet frames at a stride (C5 2.5-3.6 %), static for cnet
- *                           frames at offsets (IMIX C4: balanced 0.8-3 % slower) */
+ *                           frames at offsets (IMIX C4: balanced 0.8-3 % slower)
+ *   CNDP_TUNE_SPEC_WAIT     cnet speculation: bound, in microseconds, on each wait of the
+ *                           general resolution pass for an earlier phase's work items
+ *                           (default 1000000; the waits end by construction -- work is
+ *                           handed out in ticket order, so no co-residency is assumed --
+ *                           the bound only turns a fault into an error).  -1 = fault
+ *                           injection for tests: every such wait expires.  An expired
+ *                           wait is reported, never silent: the context's next
+ *                           cndp_gpu_classify of a cnet batch returns -EIO (and restarts
+ *                           the node state), a node queue's poll returns that batch with
+ *                           every edge CNDP_MQ_EDGE_NONE and its next submit -EIO, and
+ *                           CNDP_STAT_SPEC_ERR reads 1 until then */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -443,6 +454,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_SPEC_LISTS 15
 #define CNDP_TUNE_SPEC_TYPES 16
 #define CNDP_TUNE_STREAM_BAL 17
+#define CNDP_TUNE_SPEC_WAIT 18
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words
@@ -453,9 +465,12 @@ int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
  *                            left to the general parse (0: every frame took
  *                            the fast path)
  *   CNDP_STAT_CNET_UNIFORM   1 when the last call's ptypes all had the entering
- *                            node state's low byte (the uniform speculation pass) */
+ *                            node state's low byte (the uniform speculation pass)
+ *   CNDP_STAT_SPEC_ERR       1 when a speculation pass wait expired and has not been
+ *                            reported yet (CNDP_TUNE_SPEC_WAIT) */
 #define CNDP_STAT_CNET_WORKLIST 1
 #define CNDP_STAT_CNET_UNIFORM 2
+#define CNDP_STAT_SPEC_ERR 3
 int64_t cndp_gpu_get_stat(cndp_gpu_ctx_t *ctx, int key);
 
 /* Version / build info string. */

@@ -5,15 +5,17 @@
  * their process callbacks as cne_graph_walk would (the source node once per
  * walk, ip4_lookup once per burst it is given) and records, per edge name,
  * the objects each node enqueues -- the way graph_test.c (test/testcne) drives
- * fake nodes without a NIC.
+ * fake nodes without a NIC.  Several graphs, one per thread, as the
+ * examples run one per worker lcore (harness_graph_new / _use / _patterns).
  */
+#include <fnmatch.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "cne_graph_worker.h"
 
-#define MAX_REG 12
+#define MAX_REG 16
 #define MAX_OUT (1u << 22)
 
 static const struct cne_node_register *regs[MAX_REG];
@@ -27,30 +29,90 @@ cne_node_t __cne_node_register(const struct cne_node_register *node)
     return (cne_node_t)n_regs++;
 }
 
-static struct cne_graph g;
-static struct cne_node nodes[MAX_REG];
-static int inited[MAX_REG];
-/* objects enqueued per edge name: 0 = "ip4_rewrite", 1 = "pkt_drop", 2 = other */
-static void **out[3];
-static uint32_t n_out[3];
-static uint64_t enqueue_calls;
-/* and per edge name (any node's edges) */
+/* One graph: its node instances (a context each) and what its walks
+ * enqueued.  l3fwd-graph and cnet-graph create one graph per worker lcore
+ * (fwd.c:205-236, cnet-graph.c:360), each walked by its own thread: every
+ * call below acts on the calling thread's graph (harness_graph_use), the
+ * default one unless a test made others (harness_graph_new). */
 #define MAX_NAMES 16
-static char e_name[MAX_NAMES][CNE_NODE_NAMESIZE];
-static void **e_out[MAX_NAMES];
-static uint32_t e_n[MAX_NAMES], n_names;
-static uint64_t n_total;
+#define MAX_EDGES 16
+#define MAX_PATS 8
+struct hgraph {
+    struct cne_graph g; /* first: a graph pointer is its hgraph */
+    struct cne_node nodes[MAX_REG];
+    int inited[MAX_REG];
+    int incl[MAX_REG]; /* the registered nodes this graph holds (harness_graph_patterns) */
+    char pats[MAX_PATS][CNE_NODE_NAMESIZE];
+    int n_pats;
+    /* objects enqueued per edge name: 0 = "ip4_rewrite", 1 = "pkt_drop", 2 = other */
+    void **out[3];
+    uint32_t n_out[3];
+    uint64_t enqueue_calls;
+    /* and per edge name (any node's edges) */
+    char e_name[MAX_NAMES][CNE_NODE_NAMESIZE];
+    void **e_out[MAX_NAMES];
+    uint32_t e_n[MAX_NAMES], n_names;
+    uint64_t n_total;
+    /* the buckets of (registration, edge), looked up once: the per-call cost
+     * stays a copy, as cne_node_enqueue's is (it counts in the node rates) */
+    const struct cne_node_register *slot_reg[MAX_REG];
+    int8_t slot_k[MAX_REG][MAX_EDGES], slot_s[MAX_REG][MAX_EDGES];
+    /* chained walks: per-node streams and the pending circular buffer */
+    void **strm[MAX_REG];
+    uint32_t strm_n[MAX_REG], strm_cap[MAX_REG];
+    int pend[MAX_REG * 4], pend_h, pend_t;
+    double prof_src, prof_proc;
+};
+
+static struct hgraph g_default;
+static __thread struct hgraph *g_cur;
+#define G (g_cur ? g_cur : &g_default)
+
+/* a graph of its own for the calling thread's later calls (NULL: the default) */
+void *harness_graph_new(void) { return calloc(1, sizeof(struct hgraph)); }
+void harness_graph_use(void *h) { g_cur = (struct hgraph *)h; }
+void harness_graph_free(void *h)
+{
+    struct hgraph *x = (struct hgraph *)h;
+    if (!x || x == &g_default)
+        return;
+    for (int k = 0; k < 3; k++)
+        free(x->out[k]);
+    for (uint32_t k = 0; k < x->n_names; k++)
+        free(x->e_out[k]);
+    for (int i = 0; i < MAX_REG; i++)
+        free(x->strm[i]);
+    if (g_cur == x)
+        g_cur = NULL;
+    free(x);
+}
+
+/* the node patterns of the calling thread's next graph create, as
+ * cne_graph_create takes them (fnmatch; l3fwd-graph's "ip4*",
+ * "pktdev_rx-<port>" ..., fwd.c:128-139); none = every registered node */
+int harness_graph_patterns(const char **pats, int n)
+{
+    if (n < 0 || n > MAX_PATS)
+        return -1;
+    for (int i = 0; i < n; i++) {
+        strncpy(G->pats[i], pats[i], CNE_NODE_NAMESIZE - 1);
+        G->pats[i][CNE_NODE_NAMESIZE - 1] = 0;
+    }
+    G->n_pats = n;
+    return 0;
+}
 
 static int name_slot(const char *to)
 {
-    for (uint32_t k = 0; k < n_names; k++)
-        if (strcmp(e_name[k], to) == 0)
+    struct hgraph *h = G;
+    for (uint32_t k = 0; k < h->n_names; k++)
+        if (strcmp(h->e_name[k], to) == 0)
             return (int)k;
-    if (n_names == MAX_NAMES || !(e_out[n_names] = malloc(sizeof(void *) * MAX_OUT)))
+    if (h->n_names == MAX_NAMES || !(h->e_out[h->n_names] = malloc(sizeof(void *) * MAX_OUT)))
         return -1;
-    strncpy(e_name[n_names], to, CNE_NODE_NAMESIZE - 1);
-    e_n[n_names] = 0;
-    return (int)n_names++;
+    strncpy(h->e_name[h->n_names], to, CNE_NODE_NAMESIZE - 1);
+    h->e_n[h->n_names] = 0;
+    return (int)h->n_names++;
 }
 
 static int find(const char *name)
@@ -61,11 +123,9 @@ static int find(const char *name)
     return -1;
 }
 
-/* the buckets of (registration, edge), looked up once: the per-call cost
- * stays a copy, as cne_node_enqueue's is (it counts in the node rates) */
-#define MAX_EDGES 16
-static const struct cne_node_register *slot_reg[MAX_REG];
-static int8_t slot_k[MAX_REG][MAX_EDGES], slot_s[MAX_REG][MAX_EDGES];
+/* registered node i as an instance of the calling thread's graph */
+static int in_graph(int i) { return G->incl[i]; }
+
 
 /* edges set by cne_node_edge_update (cne_graph.h:540), per registration;
  * dyn_n[r] == 0: the registration's own next_nodes */
@@ -118,7 +178,7 @@ cne_edge_t cne_node_edge_update(cne_node_t id, cne_edge_t from, const char **nex
     for (int k = 0; k < nb_edges; k++)
         strncpy(dyn_name[r][f + k], next_nodes[k], CNE_NODE_NAMESIZE - 1);
     dyn_n[r] = f + nb_edges > cnt ? f + nb_edges : cnt;
-    slot_reg[r] = NULL; // re-resolve this registration's edge buckets
+    G->slot_reg[r] = NULL; // re-resolve this registration's edge buckets (edges are set before graphs walk)
     return (cne_edge_t)dyn_n[r];
 }
 
@@ -141,16 +201,17 @@ cne_node_t cne_node_edge_get(cne_node_t id, char *next_nodes[])
 void harness_edges_reset(void)
 {
     memset(dyn_n, 0, sizeof(dyn_n));
-    memset(slot_reg, 0, sizeof(slot_reg));
+    memset(G->slot_reg, 0, sizeof(G->slot_reg));
 }
 
 static void slots_of(int r, const struct cne_node_register *reg)
 {
-    slot_reg[r] = reg;
+    struct hgraph *h = G;
+    h->slot_reg[r] = reg;
     for (int e = 0; e < MAX_EDGES; e++) {
         const char *to = edge_name(r, e);
-        slot_k[r][e] = (int8_t)(strcmp(to, "ip4_rewrite") == 0 ? 0 : strcmp(to, "pkt_drop") == 0 ? 1 : 2);
-        slot_s[r][e] = (int8_t)name_slot(to);
+        h->slot_k[r][e] = (int8_t)(strcmp(to, "ip4_rewrite") == 0 ? 0 : strcmp(to, "pkt_drop") == 0 ? 1 : 2);
+        h->slot_s[r][e] = (int8_t)name_slot(to);
     }
 }
 
@@ -167,53 +228,53 @@ static void put(void **dst, uint32_t *n, void **objs, uint16_t nb)
  * turn -- cne_graph_walk's circular buffer (cne_graph_worker.h:125-170),
  * streams growing past a burst as __cne_node_enqueue_prologue lets them. */
 static int chain_on;
-static void **strm[MAX_REG];
-static uint32_t strm_n[MAX_REG], strm_cap[MAX_REG];
-static int pend[MAX_REG * 4], pend_h, pend_t;
 
 void harness_chain(int on) { chain_on = on; }
 
 static int chain_to(const char *to, void **objs, uint16_t nb)
 {
+    struct hgraph *h = G;
     int t = -1;
     for (int i = 0; i < n_regs; i++)
-        if (strcmp(regs[i]->name, to) == 0 && !(regs[i]->flags & CNE_NODE_SOURCE_F))
+        if (h->incl[i] && strcmp(regs[i]->name, to) == 0 && !(regs[i]->flags & CNE_NODE_SOURCE_F))
             t = i;
     if (t < 0)
         return 0;
-    if (strm_n[t] + nb > strm_cap[t]) {
-        const uint32_t cap = (strm_n[t] + nb) * 2;
-        void **a = realloc(strm[t], cap * sizeof(void *));
+    if (h->strm_n[t] + nb > h->strm_cap[t]) {
+        const uint32_t cap = (h->strm_n[t] + nb) * 2;
+        void **a = realloc(h->strm[t], cap * sizeof(void *));
         if (!a)
             return 0;
-        strm[t] = a;
-        strm_cap[t] = cap;
+        h->strm[t] = a;
+        h->strm_cap[t] = cap;
     }
-    if (strm_n[t] == 0)
-        pend[pend_t++ % (MAX_REG * 4)] = t;
-    memcpy(strm[t] + strm_n[t], objs, nb * sizeof(void *));
-    strm_n[t] += nb;
+    if (h->strm_n[t] == 0)
+        h->pend[h->pend_t++ % (MAX_REG * 4)] = t;
+    memcpy(h->strm[t] + h->strm_n[t], objs, nb * sizeof(void *));
+    h->strm_n[t] += nb;
     return 1;
 }
 
 static void run_pending(void)
 {
-    while (pend_h != pend_t) {
-        const int t = pend[pend_h++ % (MAX_REG * 4)];
-        const uint32_t cnt = strm_n[t];
-        void **objs = strm[t];
-        strm[t] = NULL; // the node's objs for this call; enqueues during it start a new stream
-        strm_n[t] = strm_cap[t] = 0;
+    struct hgraph *h = G;
+    while (h->pend_h != h->pend_t) {
+        const int t = h->pend[h->pend_h++ % (MAX_REG * 4)];
+        const uint32_t cnt = h->strm_n[t];
+        void **objs = h->strm[t];
+        h->strm[t] = NULL; // the node's objs for this call; enqueues during it start a new stream
+        h->strm_n[t] = h->strm_cap[t] = 0;
         if (cnt)
-            regs[t]->process(&g, &nodes[t], objs, (uint16_t)cnt);
+            regs[t]->process(&h->g, &h->nodes[t], objs, (uint16_t)cnt);
         free(objs);
     }
 }
 
 void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16_t nb_objs)
 {
+    struct hgraph *h = G;
     int r = 0;
-    while (r < n_regs && slot_reg[r] != node->reg)
+    while (r < n_regs && h->slot_reg[r] != node->reg)
         r++;
     if (r == n_regs) { // first enqueue from this registration
         for (r = 0; r < n_regs && regs[r] != node->reg; r++)
@@ -225,11 +286,11 @@ void harness_enqueue(struct cne_node *node, cne_edge_t next, void **objs, uint16
     const int e = next < MAX_EDGES ? next : MAX_EDGES - 1;
     if (chain_on && chain_to(edge_name(r, e), objs, nb_objs))
         return;
-    put(out[slot_k[r][e]], &n_out[slot_k[r][e]], objs, nb_objs);
-    if (slot_s[r][e] >= 0)
-        put(e_out[slot_s[r][e]], &e_n[slot_s[r][e]], objs, nb_objs);
-    n_total += nb_objs;
-    enqueue_calls++;
+    put(h->out[h->slot_k[r][e]], &h->n_out[h->slot_k[r][e]], objs, nb_objs);
+    if (h->slot_s[r][e] >= 0)
+        put(h->e_out[h->slot_s[r][e]], &h->e_n[h->slot_s[r][e]], objs, nb_objs);
+    h->n_total += nb_objs;
+    h->enqueue_calls++;
 }
 
 /* node names and flags as registered, for the test to check */
@@ -271,7 +332,7 @@ cne_node_t harness_clone(const char *name, const char *suffix)
 /* forget the clones (back to the registered nodes) */
 void harness_drop_clones(void)
 {
-    memset(slot_reg, 0, sizeof(slot_reg));
+    memset(G->slot_reg, 0, sizeof(G->slot_reg));
     while (n_regs > 0 && regs[n_regs - 1]->parent_id != CNE_NODE_ID_INVALID) {
         free((void *)regs[n_regs - 1]);
         dyn_n[n_regs - 1] = 0;
@@ -279,49 +340,59 @@ void harness_drop_clones(void)
     }
 }
 
-/* graph create: init every registered node (graph id gid) */
+/* graph create: init every node of the graph (graph id gid): the registered
+ * nodes matching its patterns, or all of them */
 int harness_graph_create(int gid)
 {
-    g.id = (cne_graph_t)gid;
-    snprintf(g.name, sizeof(g.name), "worker-%d", gid);
+    struct hgraph *h = G;
+    h->g.id = (cne_graph_t)gid;
+    snprintf(h->g.name, sizeof(h->g.name), "worker-%d", gid);
     for (int k = 0; k < 3; k++) {
-        if (!out[k] && !(out[k] = malloc(sizeof(void *) * MAX_OUT)))
+        if (!h->out[k] && !(h->out[k] = malloc(sizeof(void *) * MAX_OUT)))
             return -12;
-        n_out[k] = 0;
+        h->n_out[k] = 0;
     }
-    for (uint32_t k = 0; k < n_names; k++)
-        e_n[k] = 0;
-    n_total = 0;
+    for (uint32_t k = 0; k < h->n_names; k++)
+        h->e_n[k] = 0;
+    h->n_total = 0;
+    h->pend_h = h->pend_t = 0;
+    memset(h->slot_reg, 0, sizeof(h->slot_reg));
     /* every node laid out before any init runs (graph.c:291-295) */
     for (int i = 0; i < n_regs; i++) {
-        memset(&nodes[i], 0, sizeof(nodes[i]));
-        nodes[i].id = regs[i]->id;
-        nodes[i].reg = regs[i];
-        memcpy(nodes[i].name, regs[i]->name, CNE_NODE_NAMESIZE - 1);
+        memset(&h->nodes[i], 0, sizeof(h->nodes[i]));
+        h->nodes[i].id = regs[i]->id;
+        h->nodes[i].reg = regs[i];
+        memcpy(h->nodes[i].name, regs[i]->name, CNE_NODE_NAMESIZE - 1);
+        h->incl[i] = h->n_pats == 0;
+        for (int p = 0; p < h->n_pats && !h->incl[i]; p++)
+            h->incl[i] = fnmatch(h->pats[p], regs[i]->name, 0) == 0;
     }
     for (int i = 0; i < n_regs; i++) {
-        int r = regs[i]->init ? regs[i]->init(&g, &nodes[i]) : 0;
+        if (!h->incl[i])
+            continue;
+        int r = regs[i]->init ? regs[i]->init(&h->g, &h->nodes[i]) : 0;
         if (r)
             return r;
-        inited[i] = 1;
+        h->inited[i] = 1;
     }
     return 0;
 }
 
 struct cne_node *cne_graph_get_node_by_name(const struct cne_graph *graph, const char *node_name)
 {
-    if (graph != &g)
+    struct hgraph *h = (struct hgraph *)(uintptr_t)graph; /* g is the first member */
+    if (!graph)
         return NULL;
     for (int i = 0; i < n_regs; i++)
-        if (strncmp(nodes[i].name, node_name, CNE_NODE_NAMESIZE) == 0)
-            return &nodes[i];
+        if (h->incl[i] && strncmp(h->nodes[i].name, node_name, CNE_NODE_NAMESIZE) == 0)
+            return &h->nodes[i];
     return NULL;
 }
 
 /* the stats a graph walk keeps for the named node */
 int harness_node_stats(const char *name, uint64_t *calls, uint64_t *objs)
 {
-    struct cne_node *n = cne_graph_get_node_by_name(&g, name);
+    struct cne_node *n = cne_graph_get_node_by_name(&G->g, name);
     if (!n)
         return -1;
     *calls = n->total_calls;
@@ -331,10 +402,11 @@ int harness_node_stats(const char *name, uint64_t *calls, uint64_t *objs)
 
 void harness_graph_destroy(void)
 {
+    struct hgraph *h = G;
     for (int i = 0; i < n_regs; i++)
-        if (inited[i] && regs[i]->fini)
-            regs[i]->fini(&g, &nodes[i]);
-    memset(inited, 0, sizeof(inited));
+        if (h->inited[i] && regs[i]->fini)
+            regs[i]->fini(&h->g, &h->nodes[i]);
+    memset(h->inited, 0, sizeof(h->inited));
 }
 
 /* Receive-driver header writes for the bursts handed to a node's process()
@@ -363,13 +435,13 @@ static void rx_parse(void **pkts, uint16_t n);
 int harness_process(const char *name, void **objs, uint16_t n)
 {
     const int i = find(name);
-    if (i < 0)
+    if (i < 0 || !in_graph(i))
         return -1;
     if (drv_on)
         drv_touch(objs, n);
     if (rx_parse_on)
         rx_parse(objs, n);
-    const int r = regs[i]->process(&g, &nodes[i], objs, n);
+    const int r = regs[i]->process(&G->g, &G->nodes[i], objs, n);
     run_pending();
     return r;
 }
@@ -377,24 +449,25 @@ int harness_process(const char *name, void **objs, uint16_t n)
 /* the source nodes' turn of one cne_graph_walk */
 int harness_walk_sources(void)
 {
+    struct hgraph *h = G;
     int total = 0;
     for (int i = 0; i < n_regs; i++)
-        if (regs[i]->flags & CNE_NODE_SOURCE_F)
-            total += regs[i]->process(&g, &nodes[i], NULL, 0);
+        if (h->incl[i] && (regs[i]->flags & CNE_NODE_SOURCE_F))
+            total += regs[i]->process(&h->g, &h->nodes[i], NULL, 0);
     run_pending();
     return total;
 }
 
 uint32_t harness_take(int k, void **dst, uint32_t max)
 {
-    const uint32_t n = n_out[k] < max ? n_out[k] : max;
-    memcpy(dst, out[k], n * sizeof(void *));
+    const uint32_t n = G->n_out[k] < max ? G->n_out[k] : max;
+    memcpy(dst, G->out[k], n * sizeof(void *));
     return n;
 }
 
-uint32_t harness_count(int k) { return n_out[k]; }
-uint64_t harness_enqueue_calls(void) { return enqueue_calls; }
-uint64_t harness_total(void) { return n_total; }
+uint32_t harness_count(int k) { return G->n_out[k]; }
+uint64_t harness_enqueue_calls(void) { return G->enqueue_calls; }
+uint64_t harness_total(void) { return G->n_total; }
 #ifndef HARNESS_CNET
 extern int node_mbuf_priv1_dynfield_offset;
 int harness_priv1_offset(void) { return node_mbuf_priv1_dynfield_offset; }
@@ -403,10 +476,11 @@ int harness_priv1_offset(void) { return node_mbuf_priv1_dynfield_offset; }
 /* the objects enqueued to the edge named `to`, in enqueue order */
 uint32_t harness_take_edge(const char *to, void **dst, uint32_t max)
 {
-    for (uint32_t k = 0; k < n_names; k++)
-        if (strcmp(e_name[k], to) == 0) {
-            const uint32_t n = e_n[k] < max ? e_n[k] : max;
-            memcpy(dst, e_out[k], n * sizeof(void *));
+    struct hgraph *h = G;
+    for (uint32_t k = 0; k < h->n_names; k++)
+        if (strcmp(h->e_name[k], to) == 0) {
+            const uint32_t n = h->e_n[k] < max ? h->e_n[k] : max;
+            memcpy(dst, h->e_out[k], n * sizeof(void *));
             return n;
         }
     return 0;
@@ -438,12 +512,11 @@ static double now_s(void)
 }
 
 /* time spent in the drives' source turns and process() calls (seconds) */
-static double prof_src, prof_proc;
 void harness_prof(double *src, double *proc)
 {
-    *src = prof_src;
-    *proc = prof_proc;
-    prof_src = prof_proc = 0.0;
+    *src = G->prof_src;
+    *proc = G->prof_proc;
+    G->prof_src = G->prof_proc = 0.0;
 }
 
 /* pktdev_rx's soft parse callback (lib/usr/clib/nodes/pktdev_rx.c:36-101),
@@ -483,13 +556,14 @@ static void rx_parse(void **pkts, uint16_t n)
 
 double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, int passes)
 {
+    struct hgraph *h = G;
     const int i = find(name);
-    if (i < 0 || burst == 0)
+    if (i < 0 || !h->incl[i] || burst == 0)
         return -1.0;
     const double t0 = now_s();
     for (int p = 0; p < passes; p++) {
         for (int k = 0; k < 3; k++)
-            n_out[k] = 0;
+            h->n_out[k] = 0;
         for (uint32_t b = 0; b < n; b += burst) {
             const double a0 = now_s();
             harness_walk_sources();
@@ -499,12 +573,12 @@ double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, 
                 drv_touch(objs + b, c);
             if (rx_parse_on)
                 rx_parse(objs + b, c);
-            regs[i]->process(&g, &nodes[i], objs + b, c);
+            regs[i]->process(&h->g, &h->nodes[i], objs + b, c);
             run_pending();
-            prof_src += a1 - a0;
-            prof_proc += now_s() - a1;
+            h->prof_src += a1 - a0;
+            h->prof_proc += now_s() - a1;
         }
-        for (long spin = 0; n_out[0] + n_out[1] + n_out[2] < n; spin++) {
+        for (long spin = 0; h->n_out[0] + h->n_out[1] + h->n_out[2] < n; spin++) {
             if (spin > 100000000L)
                 return -1.0;
             harness_walk_sources();
@@ -520,7 +594,7 @@ double harness_drive(const char *name, void **objs, uint32_t n, uint16_t burst, 
 double harness_walk_until(uint64_t want)
 {
     const double t0 = now_s();
-    for (long spin = 0; n_total < want; spin++) {
+    for (long spin = 0; G->n_total < want; spin++) {
         if (spin > 100000000L)
             return -1.0;
         harness_walk_sources();
@@ -530,11 +604,12 @@ double harness_walk_until(uint64_t want)
 
 void harness_reset_counts(void)
 {
+    struct hgraph *h = G;
     for (int k = 0; k < 3; k++)
-        n_out[k] = 0;
-    for (uint32_t k = 0; k < n_names; k++)
-        e_n[k] = 0;
-    n_total = 0;
+        h->n_out[k] = 0;
+    for (uint32_t k = 0; k < h->n_names; k++)
+        h->e_n[k] = 0;
+    h->n_total = 0;
 }
 
 /* The asynchronous queue alone, driven by one thread the way a node does:

@@ -364,6 +364,45 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
     assert (want_e == ((N.CNDP_MQ_NODE_PTYPE << 8) | 5)).sum() > 0   # gtpu
 
 
+def test_mq_cnet_spec_wait_expiry(cn, gpu):
+    """A node queue whose batch's speculation pass had a wait expire
+    (CNDP_TUNE_SPEC_WAIT -1, fault injection, with the full passes forced)
+    returns that batch with every edge CNDP_MQ_EDGE_NONE -- each mbuf still
+    has exactly one owner and none leaves on a wrong edge -- and its next
+    submit returns -EIO; with the bound back the same mbufs equal the
+    reference chain from node state 0."""
+    import errno
+    cl, routes, v6, t4, t6 = cn
+    n = 4096
+    pool, orig = cnet_pool(n, routes, v6, False)
+    ptrs = pool.ptrs(np.arange(n))
+    try:
+        cl.set_tuning(cnet_spec=256, spec_scan=1, spec_wait=-1)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=n, depth=2)
+        for b in range(0, n, 256):
+            assert q.submit(ctypes.addressof(ptrs) + b * ctypes.sizeof(ctypes.c_void_p), 256) == 256
+        q.flush()
+        q.wait()
+        addrs, edges = q.poll()
+        assert np.array_equal(pool.index_of(addrs), np.arange(n))
+        assert np.all(edges == N.CNDP_MQ_EDGE_NONE)
+        assert np.array_equal(pool.hdr, orig)   # staged: a failed batch writes nothing back
+        with pytest.raises(OSError) as ex:
+            q.submit(ptrs, 256)
+        assert ex.value.errno == errno.EIO
+        assert cl.stat(N.CNDP_STAT_SPEC_ERR) == 0
+        cl.set_tuning(spec_wait=1000000, spec_scan=0)
+        bursts = _bursts(n, 0, "full")
+        ref = _cnet_expect(pool, np.arange(n), bursts, t4, t6, 0, 0)
+        addrs, edges = q.run(pool, np.arange(n), bursts)
+        q.close()
+    finally:
+        cl.set_tuning(cnet_spec=256, spec_scan=0, spec_wait=1000000)
+    assert np.array_equal(pool.index_of(addrs), np.arange(n))
+    want_e = cnet_check(pool, orig, ref, t4, t6, 0)
+    assert np.array_equal(edges.astype(np.int64), want_e)
+
+
 def test_mq_cnet_device_headers_metadata_hook(cn, gpu):
     """CNDP_MQ_F_DEVICE_HEADERS with a pktmbuf_metadata hook: mbufs of a pool
     whose metadata is the default m + 64 get it from the device, those of a

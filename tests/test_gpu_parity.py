@@ -1217,6 +1217,139 @@ def test_cnet_speculation_fallback_grid(cnet, gpu):
         ccl.set_tuning(cnet_spec=256, spec_scan=0)
 
 
+def _full_pass_mix(n, routes, v6, gpu, seed, ct4, ct6):
+    """A GTP mix (the fix_spec quirk) with single-type runs -- frames aliased
+    to one plain IPv4 UDP frame, no universal group inside -- every ~64K
+    frames, so the local pass leaves chunks to k_spec_fallback's general
+    resolution (tables, scan, replay)."""
+    fr = _gtp_mix(n, routes, v6, gpu, seed=seed)
+    head = pktgen.Frames(fr.slab, 4096, offsets=fr.offsets[:4096].contiguous())
+    pt = oracle_classify(O.MODE_CNET, head, tables4=ct4, tables6=ct6, spec_burst=0)["ptype"]
+    pick = int(np.flatnonzero(pt == 0x0211)[0])
+    off = fr.offsets.clone()
+    for lo in range(3000, n - 4096, 65536):
+        off[lo:lo + 2048 + (lo % 977)] = off[pick]
+    return pktgen.Frames(fr.slab, n, offsets=off)
+
+
+def test_cnet_speculation_wait_expiry_surfaces(cnet, gpu):
+    """An expired wait in the general resolution is reported, never turned
+    into other edges: with CNDP_TUNE_SPEC_WAIT -1 (fault injection, every wait
+    expires) a batch that runs the full passes raises CNDP_STAT_SPEC_ERR, the
+    context's next cnet classify returns -EIO (and restarts the node state),
+    and with the bound back the same batch equals the node loop from state 0.
+    A batch the local pass settles alone never waits, so the injection leaves
+    it exact and silent."""
+    import errno
+    ccl, routes, v6, ct4, ct6 = cnet
+    fr = _full_pass_mix(1 << 18, routes, v6, gpu, 41, ct4, ct6)
+    ref = oracle_classify(O.MODE_CNET, fr, tables4=ct4, tables6=ct6, spec_burst=256)
+    mixed = pktgen.imix(20000, v4routes=routes, v6routes=v6, device=gpu, seed=256)   # the batch shortcut
+    ref_mixed = oracle_classify(O.MODE_CNET, mixed, tables4=ct4, tables6=ct6, spec_burst=256)
+    try:
+        ccl.set_tuning(cnet_spec=256, spec_wait=-1)   # also resets the node state
+        o = ccl.alloc_outputs(mixed.n, 64, device=gpu, meta=True)
+        ccl.classify(mixed, N.CNDP_MODE_CNET, out=o)
+        torch.cuda.synchronize()
+        assert_same(o, ref_mixed, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+        assert ccl.stat(N.CNDP_STAT_SPEC_ERR) == 0
+        ccl.set_tuning(cnet_spec=256, spec_scan=1)   # the full passes run (and wait) in any case
+        ccl.classify(fr, N.CNDP_MODE_CNET, out=ccl.alloc_outputs(fr.n, 64, device=gpu))
+        torch.cuda.synchronize()
+        assert ccl.stat(N.CNDP_STAT_SPEC_ERR) == 1
+        with pytest.raises(OSError) as ex:
+            ccl.classify(fr, N.CNDP_MODE_CNET, out=ccl.alloc_outputs(fr.n, 64, device=gpu))
+        assert ex.value.errno == errno.EIO
+        assert ccl.stat(N.CNDP_STAT_SPEC_ERR) == 0
+        ccl.set_tuning(spec_wait=1000000, spec_scan=0)
+        o = ccl.alloc_outputs(fr.n, 64, device=gpu, meta=True)
+        ccl.classify(fr, N.CNDP_MODE_CNET, out=o)
+        torch.cuda.synchronize()
+        assert_same(o, ref, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+        assert ccl.stat(N.CNDP_STAT_SPEC_ERR) == 0
+    finally:
+        ccl.set_tuning(cnet_spec=256, spec_wait=1000000, spec_scan=0)
+
+
+def test_cnet_contexts_concurrent_on_threads(cnet, gpu):
+    """Two contexts -- two graphs' node state -- classify C4-shaped IMIX GTP
+    mixes on two host threads at once, each on its own stream, three chained
+    calls each whose speculation takes the general resolution (one in auto
+    mode, one with the full passes forced), while a third thread streams
+    l3fwd batches through a third context: k_spec_fallback shares the CUs with
+    whatever else runs, and every call equals the node loop from the state the
+    previous one left."""
+    import threading
+    from cndp_amd.classify import Classifier
+    from helpers import l3fwd_fib, l3fwd_oracle_tables
+    ccl, routes, v6, ct4, ct6 = cnet
+    n, calls = 1 << 19, 3
+    jobs = []
+    for k, scan in enumerate((0, 1)):
+        fr = _full_pass_mix(n, routes, v6, gpu, 60 + k, ct4, ct6)
+        st = np.zeros(1, np.uint16)
+        cuts = [i * n // calls // 256 * 256 for i in range(calls)] + [n]
+        parts, refs = [], []
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            part = pktgen.Frames(fr.slab, hi - lo, offsets=fr.offsets[lo:hi].contiguous())
+            parts.append(part)
+            refs.append(oracle_classify(O.MODE_CNET, part, tables4=ct4, tables6=ct6, spec_burst=256, spec_state=st))
+        cl = Classifier(0)
+        cl.set_fib(ccl.fib4, ccl.fib6)
+        cl.set_tuning(cnet_spec=256, spec_scan=scan)
+        outs = [cl.alloc_outputs(p.n, 64, device=gpu, meta=True) for p in parts]
+        jobs.append((cl, parts, outs, refs, torch.cuda.Stream(device=gpu)))
+    fib, vals = l3fwd_fib()
+    lcl = Classifier(0)
+    lcl.set_fib(fib)
+    lfr = pktgen.packed_ipv4(1 << 22, routes=pktgen.l3fwd_routes(), device=gpu, seed=9)
+    lref = oracle_classify(O.MODE_L3FWD, pktgen.Frames(lfr.slab[:64 << 16], 1 << 16, stride=64),
+                           tables4=l3fwd_oracle_tables(vals))
+    lout = lcl.alloc_outputs(lfr.n, 64, device=gpu)
+    lst = torch.cuda.Stream(device=gpu)
+    torch.cuda.synchronize()
+    errs = []
+    go = threading.Barrier(3)
+
+    def cnet_thread(cl, parts, outs, s):
+        try:
+            go.wait()
+            for p, o in zip(parts, outs):
+                cl.classify(p, N.CNDP_MODE_CNET, out=o, stream=s.cuda_stream)
+            s.synchronize()
+        except Exception as ex:  # reported below
+            errs.append(ex)
+
+    def l3_thread():
+        try:
+            go.wait()
+            for _ in range(8):
+                lout["bins"].zero_()
+                lcl.classify(lfr, N.CNDP_MODE_L3FWD, out=lout, stream=lst.cuda_stream)
+            lst.synchronize()
+        except Exception as ex:
+            errs.append(ex)
+
+    th = [threading.Thread(target=cnet_thread, args=(cl, parts, outs, s)) for cl, parts, outs, _, s in jobs]
+    th.append(threading.Thread(target=l3_thread))
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for cl, parts, outs, refs, s in jobs:
+        for o, r in zip(outs, refs):
+            assert_same(o, r, keys=("nh", "hash", "queue", "edge", "bins", "ptype"))
+        assert cl.stat(N.CNDP_STAT_SPEC_ERR) == 0
+        cl.stream_release(s.cuda_stream)
+        cl.close()
+    got = {k: lout[k][: 1 << 16].cpu().numpy() for k in ("nh", "hash", "queue", "edge")}
+    for k in got:
+        assert np.array_equal(got[k].view(lref[k].dtype), lref[k]), k
+    lcl.close()
+
+
 def test_cnet_speculation_launch_hint(cnet, gpu):
     """The local pass's grid is sized from the previous call's hint (a
     uniform batch shrinks it); a mixed batch right after uniform ones then
