@@ -522,14 +522,23 @@ def e2e_host(st, reps: int = 5, frames=None):
         out["edge"] = torch.zeros(n, dtype=torch.uint8).pin_memory()
     out["bins"] = torch.zeros(66, dtype=torch.int64).pin_memory()
     kw = dict(stride=fr.stride, offsets=offs, data_off=fr.data_off, out=out)
-    cl.classify_host(host, n, mode, **kw)
-    t = time.perf_counter()
-    for _ in range(reps):
+    # frames at a stride wider than their 64-B window (the AF_XDP UMEM layout):
+    # the windows alone cross PCIe (CNDP_TUNE_HOST_WINDOW, the default), and,
+    # beside it, the whole slab mirrored as before
+    strided = offs is None and fr.stride > 64
+    for key, window in (("pinned_stream", 1),) + ((("pinned_stream_whole_frames", 0),) if strided else ()):
+        cl.set_tuning(host_window=window)
         cl.classify_host(host, n, mode, **kw)
-    dt = (time.perf_counter() - t) / reps
-    in_bytes = host.numel() + (n * 8 if offs is not None else 0)
-    res["pinned_stream"] = {"Mpps": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 3),
-                            "h2d_bytes": in_bytes, "h2d_GBs": round(in_bytes / dt / 1e9, 1)}
+        t = time.perf_counter()
+        for _ in range(reps):
+            cl.classify_host(host, n, mode, **kw)
+        dt = (time.perf_counter() - t) / reps
+        in_bytes = (n * 64 if strided and window else host.numel()) + (n * 8 if offs is not None else 0)
+        res[key] = {"Mpps": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 3),
+                    "h2d_bytes": in_bytes, "h2d_GBs": round(in_bytes / dt / 1e9, 1)}
+        if strided and window:
+            res[key]["copy"] = "64-B windows, one strided 2-D H2D copy per 1M-frame chunk (hipMemcpy2DAsync)"
+    cl.set_tuning(host_window=1)
     del host, offs, out
     # zero-copy from a registered, page-aligned buffer
     buf = mmap.mmap(-1, fr.slab.numel())
@@ -1044,6 +1053,250 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     return res
 
 
+def _lcore_run(cpus, nthreads, reset, walk, passes, post=None):
+    """nthreads worker lcores, thread k pinned to cpus[k]: per pass every thread
+    resets its own state (reset(k), untimed), then after a barrier runs
+    walk(k) on its own graph / pool; the pass takes as long as its slowest
+    thread.  Pass 0 warms up (post(k, 0) sees its results).  Returns the
+    seconds of passes 1..passes (sum of the per-pass maxima)."""
+    import threading
+    bar = threading.Barrier(nthreads)
+    secs = [[0.0] * (passes + 1) for _ in range(nthreads)]
+    errs = []
+
+    def lcore(k):
+        try:
+            os.sched_setaffinity(0, {cpus[k % len(cpus)]})  # this thread only (Linux)
+        except OSError:
+            pass
+        try:
+            for p in range(passes + 1):
+                reset(k)
+                bar.wait(timeout=300)
+                t0 = time.perf_counter()
+                if walk(k) is False:
+                    raise RuntimeError(f"lcore {k}: walk failed")
+                secs[k][p] = time.perf_counter() - t0
+                if post:
+                    post(k, p)
+                bar.wait(timeout=300)
+        except BaseException as ex:  # reported; the barrier must not wait forever
+            errs.append(ex)
+            bar.abort()
+
+    th = [threading.Thread(target=lcore, args=(k,)) for k in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return sum(max(secs[k][p] for k in range(nthreads)) for p in range(1, passes + 1))
+
+
+def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, passes: int = 4) -> dict:
+    """One graph per worker lcore, all on one GPU (l3fwd-graph fwd.c:205-236;
+    cnet-graph cnet-graph.c:360): T host threads, each pinned to a core and
+    walking its own graph over its own port's UMEM pool -- the GPU pktdev_rx
+    node (l3fwd receive chain) and the GPU eth_rx node (cnet), one context and
+    queue per graph -- beside the same node chains on the CPU, T pinned threads
+    over the same pools (oracle/oracle.c orc_l3rx_chain_mbufs,
+    oracle/cnet_chain.c).  Rates are aggregate Mpps over the T pools (each pass
+    as long as its slowest lcore); every pool's results are compared with the
+    CPU chain's at every T (results_equal_cpu_chain)."""
+    import ctypes
+    from cndp_amd import native as N
+    from cndp_amd import pktgen
+    from cndp_amd.fib import Fib, Fib6, NodeFib, cne_node_ip4_route_add, node_ip4_add_input, node_ip6_add_input
+    from cndp_amd.mbuf import MbufPool
+    from oracle import oracle as O
+    cpus, _, quota = host_cpus()
+    if quota:
+        cpus = cpus[:max(1, int(-(-quota // 1)))]
+    threads = [t for t in threads if t <= max(1, len(cpus))]
+    tmax = max(threads)
+    L = N.lib()
+    routes = pktgen.l3fwd_routes()
+
+    def harness(name, cnet):
+        H = ctypes.CDLL(os.path.join(ROOT, "tests", "node_harness", name))
+        H.harness_rx_load.argtypes = [ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint32]
+        H.harness_walk_until.argtypes = [ctypes.c_uint64]
+        H.harness_walk_until.restype = ctypes.c_double
+        H.harness_clone.restype = ctypes.c_uint32
+        H.harness_clone.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        H.harness_graph_new.restype = ctypes.c_void_p
+        H.harness_graph_use.argtypes = [ctypes.c_void_p]
+        H.harness_graph_free.argtypes = [ctypes.c_void_p]
+        H.harness_graph_patterns.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        H.harness_rx_driver_writes.argtypes = [ctypes.c_int]
+        if cnet:
+            H.harness_eth_rx_port.argtypes = [ctypes.c_uint32, ctypes.c_uint16]
+            H.harness_cnet_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        else:
+            H.harness_pktdev_rx_port.argtypes = [ctypes.c_uint32, ctypes.c_uint16]
+            H.harness_register_cls_node()
+        H.harness_edges_reset()
+        H.harness_drop_clones()
+        return H
+
+    def graphs_for(H, T, pats_of, gid0):
+        gs = []
+        for k in range(T):
+            g = H.harness_graph_new()
+            H.harness_graph_use(g)
+            pats = [x.encode() for x in pats_of(k)]
+            H.harness_graph_patterns((ctypes.c_char_p * len(pats))(*pats), len(pats))
+            rc = H.harness_graph_create(gid0 + k)
+            gs.append(g)
+            if rc:
+                H.harness_graph_use(None)
+                raise RuntimeError(f"graph create {rc}")
+        H.harness_graph_use(None)
+        return gs
+
+    def graphs_free(H, gs):
+        for g in gs:
+            H.harness_graph_use(g)
+            H.harness_graph_destroy()
+            H.harness_graph_use(None)
+            H.harness_graph_free(g)
+
+    out = {"threads": threads, "mbufs_per_lcore": {"l3fwd": m, "cnet": mc}, "passes": passes, "burst": 256,
+           "cpus": cpus[:tmax], "header_state": "driver-written (receive stub / oracle loops, xskdev.c:296-297)"}
+    # ---- l3fwd-graph receive chain: the GPU pktdev_rx node per lcore
+    HR = harness("librx_harness.so", False)
+    NodeFib.fini()
+    L.cndp_node_gpu_umem_reset()
+    L.cndp_node_ip4_rewrite_reset()
+    pools = []
+    for k in range(tmax):
+        p = MbufPool(m)
+        p.fill(pktgen.packed_ipv4(m, routes=routes, seed=200 + k))
+        pools.append(p)
+        L.cndp_node_gpu_umem_add(ctypes.c_void_p(p.base), ctypes.c_uint64(p.mem.nbytes))
+        cid = HR.harness_clone(b"pktdev_rx", str(k).encode())
+        assert HR.harness_pktdev_rx_port(cid, k) == 0
+    hdr0 = [p.hdr.copy() for p in pools]
+    ptrs = [p.ptrs(np.arange(m)) for p in pools]
+    l3 = {"gpu_Mpps": {}, "cpu_Mpps": {}, "results_equal_cpu_chain": {}}
+    HR.harness_rx_driver_writes(1)
+    try:
+        for T in threads:
+            gs = graphs_for(HR, T, lambda k: ["ip4*", "pkt_cls", f"pktdev_rx-{k}"], 300 + 10 * T)
+            for ip, d, nh in routes:
+                cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+
+            def reset(k, gs=gs):
+                HR.harness_graph_use(gs[k])
+                pools[k].hdr[:] = hdr0[k]
+                HR.harness_rx_load(k, ptrs[k], m)
+                HR.harness_reset_counts()
+
+            snap = {}
+
+            def post(k, p):
+                if p == 0:
+                    snap[k] = (pools[k].hdr["packet_type"].copy(), pools[k].hdr["udata64"].copy())
+
+            t = _lcore_run(cpus, T, reset, lambda k: HR.harness_walk_until(m) >= 0, passes, post)
+            graphs_free(HR, gs)
+            l3["gpu_Mpps"][T] = round(T * m * passes / t / 1e6, 2)
+            t24, t8 = (x.copy() for x in NodeFib().image())
+            O.set_driver_writes(True)
+
+            def reset_cpu(k):
+                pools[k].hdr[:] = hdr0[k]
+
+            t = _lcore_run(cpus, T, reset_cpu, lambda k: O.l3rx_chain_mbufs(ptrs[k], m, (t24, t8)) > 0, passes)
+            O.set_driver_writes(False)
+            l3["cpu_Mpps"][T] = round(T * m * passes / t / 1e6, 2)
+            l3["results_equal_cpu_chain"][T] = all(
+                np.array_equal(snap[k][0], pools[k].hdr["packet_type"]) and
+                np.array_equal(snap[k][1], pools[k].hdr["udata64"]) for k in range(T))
+    finally:
+        HR.harness_rx_driver_writes(0)
+        HR.harness_drop_clones()
+        L.cndp_node_gpu_umem_reset()
+        NodeFib.fini()
+    l3["gpu_over_cpu"] = {T: round(l3["gpu_Mpps"][T] / l3["cpu_Mpps"][T], 2) for T in l3["gpu_Mpps"]}
+    l3["node"] = ("GPU pktdev_rx node (cndp_amd/node/pktdev_rx_gpu.c): soft parse + pkt_cls + ip4_lookup in one "
+                  "queue kernel, zero-copy, device headers; CPU: pktdev_rx's soft parse, pkt_cls and the "
+                  "ip4_lookup loop per 256-burst (orc_l3rx_chain_mbufs)")
+    out["l3fwd_rx_chain"] = l3
+    del pools, ptrs, hdr0
+    # ---- cnet: the GPU eth_rx node per lcore
+    HC = harness("libcnet_harness.so", True)
+    v6 = pktgen.v6_routes()
+    f4 = Fib("lc4", N.CNE_FIB_DIR24_8, default_nh=1025, max_routes=1024, nh_sz=N.CNE_FIB_DIR24_8_4B, num_tbl8=256)
+    for i, (ip, d, _) in enumerate(routes):
+        node_ip4_add_input(f4, ip, d, i)
+    f6 = Fib6("lc6", N.CNE_FIB_TRIE, default_nh=1025, max_routes=1024, nh_sz=N.CNE_FIB_TRIE_4B, num_tbl8=1 << 15)
+    for ip, d, i in v6:
+        node_ip6_add_input(f6, ip, d, i)
+    HC.harness_cnet_set(f4.h, f6.h)
+    t4c, t6c = tuple(x.copy() for x in f4.image()), tuple(x.copy() for x in f6.image())
+    pools = []
+    for k in range(tmax):
+        p = MbufPool(mc)
+        p.fill(pktgen.imix(mc, v4routes=routes, v6routes=v6, seed=300 + k))
+        pools.append(p)
+        L.cndp_node_gpu_umem_add(ctypes.c_void_p(p.base), ctypes.c_uint64(p.mem.nbytes))
+        cid = HC.harness_clone(b"eth_rx", str(k).encode())
+        assert HC.harness_eth_rx_port(cid, k) == 0
+    hdr0 = [p.hdr.copy() for p in pools]
+    ptrs = [p.ptrs(np.arange(mc)) for p in pools]
+    fields = ("packet_type", "ol_flags", "tx_offload", "lport", "data_off", "data_len")
+    cn = {"gpu_Mpps": {}, "cpu_Mpps": {}, "results_equal_cpu_chain": {}}
+    HC.harness_rx_driver_writes(1)
+    try:
+        for T in threads:
+            gs = graphs_for(HC, T, lambda k: [f"eth_rx-{k}", "ptype", "ip4_input", "ip6_input"], 400 + 10 * T)
+
+            def reset(k, gs=gs):
+                HC.harness_graph_use(gs[k])
+                pools[k].hdr[:] = hdr0[k]
+                HC.harness_rx_load(k, ptrs[k], mc)
+                HC.harness_reset_counts()
+
+            snap = {}
+
+            def post(k, p):
+                if p == 0:  # from a fresh graph: ptype node state 0, as the CPU chain starts
+                    snap[k] = {f: pools[k].hdr[f].copy() for f in fields}
+
+            t = _lcore_run(cpus, T, reset, lambda k: HC.harness_walk_until(mc) >= 0, passes, post)
+            graphs_free(HC, gs)
+            cn["gpu_Mpps"][T] = round(T * mc * passes / t / 1e6, 2)
+
+            def reset_cpu(k):
+                pools[k].hdr[:] = hdr0[k]
+
+            def walk_cpu(k):
+                return O.cnet_chain(ptrs[k], mc, hdr0[k]["data_len"], int(hdr0[k]["data_off"][0]), t4c, t6c,
+                                    cpus=[cpus[k % len(cpus)]], lport=k) > 0
+
+            cpu_res = {}
+
+            def post_cpu(k, p):
+                if p == 0:
+                    cpu_res[k] = {f: pools[k].hdr[f].copy() for f in fields}
+
+            t = _lcore_run(cpus, T, reset_cpu, walk_cpu, passes, post_cpu)
+            cn["cpu_Mpps"][T] = round(T * mc * passes / t / 1e6, 2)
+            cn["results_equal_cpu_chain"][T] = all(np.array_equal(snap[k][f], cpu_res[k][f])
+                                                   for k in range(T) for f in fields)
+    finally:
+        HC.harness_rx_driver_writes(0)
+        HC.harness_drop_clones()
+        L.cndp_node_gpu_umem_reset()
+    cn["gpu_over_cpu"] = {T: round(cn["gpu_Mpps"][T] / cn["cpu_Mpps"][T], 2) for T in cn["gpu_Mpps"]}
+    cn["node"] = ("GPU eth_rx node (cndp_amd/node/eth_rx_gpu.c): eth_rx + ptype + ip4_input / ip6_input, "
+                  "zero-copy, host headers; CPU: the cnet chain per 256-mbuf walk (oracle/cnet_chain.c); IMIX")
+    out["cnet_eth_rx"] = cn
+    return out
+
+
 def l3fwd_rx_chain(L, pool, ptrs, n, passes, routes):
     """l3fwd-graph's receive chain pktdev_rx -> pkt_cls -> ip4_lookup as the
     GPU pktdev_rx node runs it (cndp_amd/node/pktdev_rx_gpu.c, CNDP_MQ_F_RX_PARSE:
@@ -1486,6 +1739,13 @@ def main():
             log(f"[bench] node boundary: {nb}")
         except Exception as ex:  # reported, never fatal for the headline line
             nb = {"error": repr(ex)}
+        try:
+            nb_lc = node_lcores(dev)
+            log(f"[bench] node lcores: {nb_lc}")
+        except Exception as ex:  # reported, never fatal for the headline line
+            nb_lc = {"error": repr(ex)}
+        if isinstance(nb, dict):
+            nb["lcore_graphs"] = nb_lc
         try:
             fu = fib_update()
             log(f"[bench] fib update: {fu}")

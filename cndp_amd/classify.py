@@ -59,12 +59,13 @@ class Classifier:
                    spec_scan: int | None = None, mbuf_hash: int | None = None,
                    cnet_fold: int | None = None, spec_grid: int | None = None,
                    spec_lists: int | None = None, spec_types: int | None = None,
-                   stream_bal: int | None = None, spec_wait: int | None = None):
+                   stream_bal: int | None = None, spec_wait: int | None = None,
+                   host_window: int | None = None):
         """Kernel variant knobs (cndp_gpu_set_tuning); never change results
         (spec_wait, the speculation pass's wait bound in us, -1 = fault
         injection, turns an expired wait into -EIO, never into other edges)."""
         for key, v in ((N.CNDP_TUNE_CNET_FOLD, cnet_fold), (N.CNDP_TUNE_SPEC_GRID, spec_grid),
-                       (N.CNDP_TUNE_SPEC_WAIT, spec_wait),
+                       (N.CNDP_TUNE_SPEC_WAIT, spec_wait), (N.CNDP_TUNE_HOST_WINDOW, host_window),
                        (N.CNDP_TUNE_SPEC_LISTS, spec_lists), (N.CNDP_TUNE_SPEC_TYPES, spec_types),
                        (N.CNDP_TUNE_STREAM_BAL, stream_bal),
                        (N.CNDP_TUNE_NT, nt), (N.CNDP_TUNE_UNROLL, unroll),

@@ -4423,6 +4423,7 @@ struct cndp_gpu_ctx {
     int tune_cnet_fold;   // CNDP_TUNE_CNET_FOLD: 0 hint, 1 always, 2 never
     int tune_spec_grid;   // CNDP_TUNE_SPEC_GRID: 0 hint, 1 shrunk (2 blocks), 2 full
     int tune_spec_wait_us; // CNDP_TUNE_SPEC_WAIT: k_spec_fallback wait bound (us), -1 = fault injection
+    int tune_host_window;  // CNDP_TUNE_HOST_WINDOW: classify_host moves 64-B windows of strided frames
     int tune_spec_lists;  // CNDP_TUNE_SPEC_LISTS: 1 chunk lists from the fast kernel (default), 0 off
     int sf_clean, wl_clean; // signature flags / worklist count known zero (no memset needed)
     uint32_t host_chunk;  // CNDP_TUNE_HOST_CHUNK: packets per pipelined host chunk
@@ -4606,6 +4607,7 @@ extern "C" int cndp_gpu_init(int device, cndp_gpu_ctx_t **out)
     c->tune_lnt = 1;
     c->tune_spec_lists = 1;
     c->tune_spec_wait_us = 1000000; // 1 s: the waits end by construction, this only bounds a fault
+    c->tune_host_window = 1;
     c->host_chunk = 1u << 20;
     c->spec_burst = 256;
     c->tune_rw_wb = 2;
@@ -5946,8 +5948,17 @@ static int grow(void **buf, uint64_t *cap, uint64_t need)
 // extension headers of at most 2 KiB each) -- and its results go back on the
 // copy-out stream.  The kernel therefore sees exactly the bytes the device-
 // resident path sees: results are identical to cndp_gpu_classify.
+//
+// Windows only (CNDP_TUNE_HOST_WINDOW, default): the l3fwd and hash parses
+// read nothing past a frame's first 64 bytes (Ethernet + IPv4 + the L4
+// ports), so for frames at a stride wider than that -- the AF_XDP UMEM's
+// 2 KiB frames with data at +256 -- each chunk's windows go H2D as one
+// strided 2-D copy (source pitch = the stride, 64-B rows) into packed 64-B
+// slots, and the streamed wave-tile kernel classifies those: 64 of every
+// 2048 bytes cross PCIe.  Same bytes in every window, so the same results.
 #define CNDP_HOST_SEG (64ull << 20)
 #define CNDP_HOST_REACH (16ull << 10)
+#define CNDP_HOST_WIN 64ull
 
 extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch *hb)
 {
@@ -5964,7 +5975,10 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
         if (!c->hs[k])
             HIP_TRY(hipStreamCreateWithFlags(&c->hs[k], hipStreamNonBlocking));
     hipStream_t cs = c->hs[0], ks = c->hs[1], ds = c->hs[2];
-    if ((r = grow((void **)&c->h_slab, &c->h_slab_cap, hb->slab_len ? hb->slab_len : 1)) ||
+    const bool win = c->tune_host_window && hb->mode != CNDP_MODE_CNET && !hb->offsets && n &&
+                     hb->stride > CNDP_HOST_WIN && (uint64_t)hb->data_off + CNDP_HOST_WIN <= hb->stride &&
+                     (n - 1) * hb->stride + hb->data_off + CNDP_HOST_WIN <= hb->slab_len;
+    if ((r = grow((void **)&c->h_slab, &c->h_slab_cap, win ? n * CNDP_HOST_WIN : hb->slab_len ? hb->slab_len : 1)) ||
         (r = grow((void **)&c->h_out, &c->h_out_cap, out_bytes)) ||
         (hb->offsets && (r = grow((void **)&c->h_off, &c->h_off_cap, n * 8 + 8))))
         return r;
@@ -5983,6 +5997,42 @@ extern "C" int cndp_gpu_classify_host(cndp_gpu_ctx_t *c, const struct cndp_batch
     r = -EIO;
     for (uint64_t k = 0; k < n_chunks; k++) {
         const uint64_t i0 = k * C, cnt = (n - i0) < C ? (n - i0) : C;
+        if (win) { // this chunk's windows, packed
+            struct cndp_batch cb = *hb;
+            if (hipMemcpy2DAsync(c->h_slab + i0 * CNDP_HOST_WIN, CNDP_HOST_WIN,
+                                 (const uint8_t *)hb->slab + i0 * hb->stride + hb->data_off, hb->stride, CNDP_HOST_WIN,
+                                 cnt, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                hipEventRecord(ev_in, cs) != hipSuccess || hipStreamWaitEvent(ks, ev_in, 0) != hipSuccess)
+                goto out;
+            cb.n = (uint32_t)cnt;
+            cb.slab = c->h_slab + i0 * CNDP_HOST_WIN;
+            cb.slab_len = (n - i0) * CNDP_HOST_WIN;
+            cb.stride = (uint32_t)CNDP_HOST_WIN;
+            cb.data_off = 0;
+            cb.nh = hb->nh ? (uint32_t *)(c->h_out + o_nh) + i0 : nullptr;
+            cb.hash = hb->hash ? (uint32_t *)(c->h_out + o_hash) + i0 : nullptr;
+            cb.queue = hb->queue ? (uint16_t *)(c->h_out + o_q) + i0 : nullptr;
+            cb.edge = hb->edge ? c->h_out + o_e + i0 : nullptr;
+            cb.bins = d_bins;
+            cb.ptype = hb->ptype ? (uint32_t *)(c->h_out + o_pt) + i0 : nullptr;
+            cb.rxmeta = nullptr;
+            if ((r = cndp_gpu_classify(c, &cb, ks)))
+                goto out;
+            r = -EIO;
+            if (hipEventRecord(ev_k, ks) != hipSuccess || hipStreamWaitEvent(ds, ev_k, 0) != hipSuccess)
+                goto out;
+            if (hb->nh && hipMemcpyAsync(hb->nh + i0, cb.nh, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
+                goto out;
+            if (hb->hash && hipMemcpyAsync(hb->hash + i0, cb.hash, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
+                goto out;
+            if (hb->queue && hipMemcpyAsync(hb->queue + i0, cb.queue, cnt * 2, hipMemcpyDeviceToHost, ds) != hipSuccess)
+                goto out;
+            if (hb->edge && hipMemcpyAsync(hb->edge + i0, cb.edge, cnt, hipMemcpyDeviceToHost, ds) != hipSuccess)
+                goto out;
+            if (hb->ptype && hipMemcpyAsync(hb->ptype + i0, cb.ptype, cnt * 4, hipMemcpyDeviceToHost, ds) != hipSuccess)
+                goto out;
+            continue;
+        }
         // byte span this chunk's parse can reach
         uint64_t hi;
         if (hb->offsets) {
@@ -8324,6 +8374,9 @@ extern "C" int cndp_gpu_set_tuning(cndp_gpu_ctx_t *c, int key, int value)
         if (value < 0 || value > 2)
             return -EINVAL;
         c->tune_stream_bal = value;
+        return 0;
+    case CNDP_TUNE_HOST_WINDOW:
+        c->tune_host_window = value ? 1 : 0;
         return 0;
     case CNDP_TUNE_SPEC_WAIT:
         if (value == 0 || value < -1 || value > 40000000)

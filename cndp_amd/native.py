@@ -49,6 +49,7 @@ CNDP_TUNE_SPEC_LISTS = 15
 CNDP_TUNE_SPEC_TYPES = 16
 CNDP_TUNE_STREAM_BAL = 17
 CNDP_TUNE_SPEC_WAIT = 18
+CNDP_TUNE_HOST_WINDOW = 19
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
 CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS, CNDP_MQ_F_RX_PARSE = 1, 2, 4, 8
 CNDP_MQ_F_REWRITE = 16

@@ -49,6 +49,16 @@
  * One GPU context and queue per graph (graphs are per lcore, cne_graph_worker.h
  * notes a graph is not shared between threads); contexts share the node FIB,
  * whose device mirror libcndp_gpu keeps on one device per process.
+ *
+ * Linked only together with pktdev_rx_gpu.c: behind
+ * CNDP's own pktdev_rx the core has already parsed every frame and left its
+ * header line dirty, and one core then runs parse + lookup faster than parse
+ * + this node (0.73-0.9 x), so a build that would put this node
+ * there does not link -- the reference to cndp_pktdev_rx_gpu_linked below
+ * makes the GPU receive node come with it, and an unchanged l3fwd-graph gets
+ * the whole receive chain on the device (this node then stays idle, its
+ * drain node polling an empty queue).  IP4_LOOKUP_GPU_STANDALONE builds the
+ * node alone, for the tests and the bench's measurement of that case.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -255,8 +265,16 @@ static uint16_t ip4_lookup_gpu_process(struct cne_graph *graph, struct cne_node 
     return nb_objs;
 }
 
+#ifndef IP4_LOOKUP_GPU_STANDALONE
+extern const int cndp_pktdev_rx_gpu_linked; /* pktdev_rx_gpu.c: the receive chain comes with this node */
+#endif
+
 static int ip4_lookup_gpu_init(const struct cne_graph *graph, struct cne_node *node)
 {
+#ifndef IP4_LOOKUP_GPU_STANDALONE
+    if (!cndp_pktdev_rx_gpu_linked)
+        return -ENOENT;
+#endif
     node_mbuf_priv1_dynfield_offset = offsetof(pktmbuf_t, udata64); /* ip4_lookup.c:322 */
     struct gpu_graph_state *st = state_get(graph, node);
     if (!st)

@@ -94,6 +94,9 @@ enum {
 
 static struct pktdev_rx_node_main pktdev_rx_main;
 
+/* ip4_lookup_gpu.c links only with this file (see there) */
+const int cndp_pktdev_rx_gpu_linked = 1;
+
 struct gpu_rx_state {
     cndp_gpu_ctx_t *gpu;
     cndp_gpu_mq_t *q;

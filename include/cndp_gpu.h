@@ -436,7 +436,12 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
  *                           cndp_gpu_classify of a cnet batch returns -EIO (and restarts
  *                           the node state), a node queue's poll returns that batch with
  *                           every edge CNDP_MQ_EDGE_NONE and its next submit -EIO, and
- *                           CNDP_STAT_SPEC_ERR reads 1 until then */
+ *                           CNDP_STAT_SPEC_ERR reads 1 until then
+ *   CNDP_TUNE_HOST_WINDOW   cndp_gpu_classify_host, l3fwd / hash modes, frames at a stride
+ *                           wider than 64 B (the AF_XDP UMEM layout): 1 = only each frame's
+ *                           first 64 bytes from data_off cross PCIe, one strided 2-D copy per
+ *                           chunk into packed 64-B slots (the parse reads no byte past them;
+ *                           default), 0 = the whole slab is mirrored */
 #define CNDP_TUNE_NT 1
 #define CNDP_TUNE_UNROLL 2
 #define CNDP_TUNE_BLOCKS_PER_CU 3
@@ -455,6 +460,7 @@ int cndp_gpu_bin_ids(cndp_gpu_ctx_t *ctx, uint32_t mode, const uint32_t *nh, con
 #define CNDP_TUNE_SPEC_TYPES 16
 #define CNDP_TUNE_STREAM_BAL 17
 #define CNDP_TUNE_SPEC_WAIT 18
+#define CNDP_TUNE_HOST_WINDOW 19
 int cndp_gpu_set_tuning(cndp_gpu_ctx_t *ctx, int key, int value);
 
 /* Observability: the last cnet classify's shape, read from pinned host words

@@ -398,6 +398,31 @@ def test_classify_host_chunked(l3, cnet, gpu):
             c.set_tuning(host_chunk=1 << 20)
 
 
+@pytest.mark.parametrize("window", [1, 0], ids=["windows", "whole_frames"])
+def test_classify_host_umem_windows(l3, gpu, window):
+    """AF_XDP-layout frames (2 KiB, data at +256) from host memory: with
+    CNDP_TUNE_HOST_WINDOW only each frame's 64-B window crosses PCIe (a
+    strided 2-D copy per chunk into packed slots), without it the whole slab;
+    l3fwd and hash modes, chunk boundaries off the frame count, pinned and
+    pageable buffers -- every output equals the oracle over the frames where
+    they lie."""
+    cl, fib, t4 = l3
+    fr = pktgen.umem_ipv4(50001, routes=pktgen.l3fwd_routes(), seed=12)
+    rows = fr.slab.view(fr.n, 2048)
+    g = torch.Generator().manual_seed(12)
+    rows[:, :256] = torch.randint(0, 256, (fr.n, 256), dtype=torch.uint8, generator=g)   # mbuf header, headroom
+    rows[:, 320:512] = torch.randint(0, 256, (fr.n, 192), dtype=torch.uint8, generator=g)  # past the window
+    try:
+        cl.set_tuning(host_window=window, host_chunk=4096)
+        for mode, omode, kw in ((N.CNDP_MODE_L3FWD, O.MODE_L3FWD, {"tables4": t4}), (N.CNDP_MODE_HASH, O.MODE_HASH, {})):
+            ref = oracle_classify(omode, fr, **kw)
+            for host in (fr.slab.numpy(), fr.slab.pin_memory()):
+                got = cl.classify_host(host, fr.n, mode, stride=fr.stride, data_off=fr.data_off)
+                assert_same({k: (v.numpy() if hasattr(v, "numpy") else v) for k, v in got.items()}, ref)
+    finally:
+        cl.set_tuning(host_window=1, host_chunk=1 << 20)
+
+
 def test_zero_copy_registered_host(l3, gpu):
     """Frames left in registered host memory (a UMEM), read in place by the kernel."""
     cl, fib, t4 = l3

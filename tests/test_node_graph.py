@@ -1373,3 +1373,29 @@ def test_cnet_node_graphs_per_lcore(gpu, threads):
         want = np.array([_edge_of_queue_code(int(e)) for e in want_e])
         assert np.array_equal(have, want), k
         assert set(np.unique(have).tolist()) >= {0, 3, 4, 6}
+
+
+def test_gpu_ip4_lookup_links_only_with_gpu_receive_node(tmp_path):
+    """The supported build takes ip4_lookup_gpu.c only together with
+    pktdev_rx_gpu.c: alone -- behind CNDP's own pktdev_rx,
+    where one core beats it -- the node does not link (it references
+    cndp_pktdev_rx_gpu_linked), so an unchanged l3fwd-graph always gets the
+    fused GPU receive chain.  IP4_LOOKUP_GPU_STANDALONE (tests, bench) builds
+    the node alone."""
+    import subprocess
+    root = os.path.dirname(HERE)
+    nh = os.path.join(HERE, "node_harness")
+    node = os.path.join(root, "cndp_amd", "node")
+    base = ["gcc", "-O1", "-fPIC", "-shared", "-std=gnu11", "-Wall", "-Werror", f"-I{nh}",
+            f"-I{os.path.join(root, 'include')}", "-Wl,--no-undefined", "-o", str(tmp_path / "x.so")]
+    libs = [f"-L{os.path.join(root, 'cndp_amd', 'lib')}", "-lcndp_gpu", "-lpthread"]
+    alone = subprocess.run(base + [os.path.join(node, "ip4_lookup_gpu.c"), os.path.join(nh, "harness.c")] + libs,
+                           capture_output=True, text=True)
+    assert alone.returncode != 0 and "cndp_pktdev_rx_gpu_linked" in alone.stderr
+    ok = subprocess.run(base + ["-DIP4_LOOKUP_GPU_STANDALONE", os.path.join(node, "ip4_lookup_gpu.c"),
+                                os.path.join(nh, "harness.c")] + libs, capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr[-2000:]
+    with_rx = subprocess.run(base + [os.path.join(node, f) for f in ("pktdev_rx_gpu.c", "ip4_lookup_gpu.c")] +
+                             [os.path.join(nh, f) for f in ("harness.c", "l3rx_stubs.c", "rx_stubs.c")] + libs,
+                             capture_output=True, text=True)
+    assert with_rx.returncode == 0, with_rx.stderr[-2000:]
