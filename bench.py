@@ -1204,7 +1204,8 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     HR.harness_rx_driver_writes(1)
     try:
         for T in threads:
-            gs = graphs_for(HR, T, lambda k: ["ip4*", "pkt_cls", f"pktdev_rx-{k}"], 300 + 10 * T)
+            # graph ids < 256: the GPU nodes keep their per-graph state by id (GPU_GRAPHS_MAX)
+            gs = graphs_for(HR, T, lambda k: ["ip4*", "pkt_cls", f"pktdev_rx-{k}"], 100 + 2 * tmax * threads.index(T))
             for ip, d, nh in routes:
                 cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
 
@@ -1272,7 +1273,8 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     HC.harness_rx_driver_writes(1)
     try:
         for T in threads:
-            gs = graphs_for(HC, T, lambda k: [f"eth_rx-{k}", "ptype", "ip4_input", "ip6_input"], 400 + 10 * T)
+            gs = graphs_for(HC, T, lambda k: [f"eth_rx-{k}", "ptype", "ip4_input", "ip6_input"],
+                            170 + 2 * tmax * threads.index(T))
 
             def reset(k, gs=gs):
                 HC.harness_graph_use(gs[k])
