@@ -1122,9 +1122,13 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     node (l3fwd receive chain) and the GPU eth_rx node (cnet), one context and
     queue per graph -- beside the same node chains on the CPU, T pinned threads
     over the same pools (oracle/oracle.c orc_l3rx_chain_mbufs,
-    oracle/cnet_chain.c).  Rates are aggregate Mpps over the T pools (each pass
-    as long as its slowest lcore); every pool's results are compared with the
-    CPU chain's at every T (results_equal_cpu_chain)."""
+    oracle/cnet_chain.c).  The GPU nodes in three forms (the queue's frame and
+    header access, CNDP_GPU_MQ_FLAGS / UMEM registration): device headers (the
+    kernels read header and frame in place), host headers (the host reads the
+    header, the kernel the frame), staged (the host copies the bytes the parse
+    reads into pinned staging).  Rates are aggregate Mpps over the T pools
+    (each pass as long as its slowest lcore); every pool's results are compared
+    with the CPU chain's for every form at every T (results_equal_cpu_chain)."""
     import ctypes
     from cndp_amd import native as N
     from cndp_amd import pktgen
@@ -1138,6 +1142,7 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     tmax = max(threads)
     L = N.lib()
     routes = pktgen.l3fwd_routes()
+    D = N.CNDP_MQ_F_DEVICE_HEADERS
 
     def harness(name, cnet):
         H = ctypes.CDLL(os.path.join(ROOT, "tests", "node_harness", name))
@@ -1172,6 +1177,7 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
             gs.append(g)
             if rc:
                 H.harness_graph_use(None)
+                graphs_free(H, gs)
                 raise RuntimeError(f"graph create {rc}")
         H.harness_graph_use(None)
         return gs
@@ -1183,67 +1189,103 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
             H.harness_graph_use(None)
             H.harness_graph_free(g)
 
+    def umem(pools, on):
+        L.cndp_node_gpu_umem_reset()
+        if on:
+            for p in pools:
+                L.cndp_node_gpu_umem_add(ctypes.c_void_p(p.base), ctypes.c_uint64(p.mem.nbytes))
+
+    def chain(H, pools, hdr0, ptrs, nn, pats_of, gid_base, fields, variants, cpu_walk, after_create=None):
+        """Every GPU form, then the CPU chain, at every T; rates and checks."""
+        res = {"gpu_Mpps": {v: {} for v, _, _ in variants}, "cpu_Mpps": {},
+               "results_equal_cpu_chain": {v: {} for v, _, _ in variants}}
+        for ti, T in enumerate(threads):
+            snaps = {}
+            for vi, (v, flags, zc) in enumerate(variants):
+                umem(pools, zc)
+                os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
+                # graph ids < 256: the GPU nodes keep per-graph state by id (GPU_GRAPHS_MAX)
+                gs = graphs_for(H, T, pats_of, gid_base + (ti * len(variants) + vi) * tmax)
+                os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
+                if after_create:
+                    after_create()
+
+                def reset(k, gs=gs):
+                    H.harness_graph_use(gs[k])
+                    pools[k].hdr[:] = hdr0[k]
+                    H.harness_rx_load(k, ptrs[k], nn)
+                    H.harness_reset_counts()
+
+                snap = snaps.setdefault(v, {})
+
+                def post(k, p, snap=snap):
+                    if p == 0:  # from a fresh graph (node state 0, as the CPU chain starts)
+                        snap[k] = {f: pools[k].hdr[f].copy() for f in fields}
+
+                try:
+                    t = _lcore_run(cpus, T, reset, lambda k: H.harness_walk_until(nn) >= 0, passes, post)
+                finally:
+                    graphs_free(H, gs)
+                res["gpu_Mpps"][v][T] = round(T * nn * passes / t / 1e6, 2)
+            cres = {}
+
+            def reset_cpu(k):
+                pools[k].hdr[:] = hdr0[k]
+
+            def post_cpu(k, p):
+                if p == 0:
+                    cres[k] = {f: pools[k].hdr[f].copy() for f in fields}
+
+            t = _lcore_run(cpus, T, reset_cpu, cpu_walk, passes, post_cpu)
+            res["cpu_Mpps"][T] = round(T * nn * passes / t / 1e6, 2)
+            for v, _, _ in variants:
+                res["results_equal_cpu_chain"][v][T] = all(np.array_equal(snaps[v][k][f], cres[k][f])
+                                                           for k in range(T) for f in fields)
+        best = {T: max(res["gpu_Mpps"][v][T] for v, _, _ in variants) for T in threads}
+        res["gpu_best_Mpps"] = best
+        res["gpu_best_over_cpu"] = {T: round(best[T] / res["cpu_Mpps"][T], 2) for T in threads}
+        return res
+
     out = {"threads": threads, "mbufs_per_lcore": {"l3fwd": m, "cnet": mc}, "passes": passes, "burst": 256,
            "cpus": cpus[:tmax], "header_state": "driver-written (receive stub / oracle loops, xskdev.c:296-297)"}
     # ---- l3fwd-graph receive chain: the GPU pktdev_rx node per lcore
     HR = harness("librx_harness.so", False)
     NodeFib.fini()
-    L.cndp_node_gpu_umem_reset()
     L.cndp_node_ip4_rewrite_reset()
     pools = []
     for k in range(tmax):
         p = MbufPool(m)
         p.fill(pktgen.packed_ipv4(m, routes=routes, seed=200 + k))
         pools.append(p)
-        L.cndp_node_gpu_umem_add(ctypes.c_void_p(p.base), ctypes.c_uint64(p.mem.nbytes))
         cid = HR.harness_clone(b"pktdev_rx", str(k).encode())
         assert HR.harness_pktdev_rx_port(cid, k) == 0
     hdr0 = [p.hdr.copy() for p in pools]
     ptrs = [p.ptrs(np.arange(m)) for p in pools]
-    l3 = {"gpu_Mpps": {}, "cpu_Mpps": {}, "results_equal_cpu_chain": {}}
     HR.harness_rx_driver_writes(1)
+    tabs = []
+
+    def l3_routes():
+        for ip, d, nh in routes:
+            cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
+        if not tabs:
+            tabs.append(tuple(x.copy() for x in NodeFib().image()))
+
+    def l3_cpu(k):
+        O.set_driver_writes(True)
+        return O.l3rx_chain_mbufs(ptrs[k], m, tabs[0]) > 0
+
     try:
-        for T in threads:
-            # graph ids < 256: the GPU nodes keep their per-graph state by id (GPU_GRAPHS_MAX)
-            gs = graphs_for(HR, T, lambda k: ["ip4*", "pkt_cls", f"pktdev_rx-{k}"], 100 + 2 * tmax * threads.index(T))
-            for ip, d, nh in routes:
-                cne_node_ip4_route_add(ip, d, nh, N.IP4_LOOKUP_NEXT_REWRITE)
-
-            def reset(k, gs=gs):
-                HR.harness_graph_use(gs[k])
-                pools[k].hdr[:] = hdr0[k]
-                HR.harness_rx_load(k, ptrs[k], m)
-                HR.harness_reset_counts()
-
-            snap = {}
-
-            def post(k, p):
-                if p == 0:
-                    snap[k] = (pools[k].hdr["packet_type"].copy(), pools[k].hdr["udata64"].copy())
-
-            t = _lcore_run(cpus, T, reset, lambda k: HR.harness_walk_until(m) >= 0, passes, post)
-            graphs_free(HR, gs)
-            l3["gpu_Mpps"][T] = round(T * m * passes / t / 1e6, 2)
-            t24, t8 = (x.copy() for x in NodeFib().image())
-            O.set_driver_writes(True)
-
-            def reset_cpu(k):
-                pools[k].hdr[:] = hdr0[k]
-
-            t = _lcore_run(cpus, T, reset_cpu, lambda k: O.l3rx_chain_mbufs(ptrs[k], m, (t24, t8)) > 0, passes)
-            O.set_driver_writes(False)
-            l3["cpu_Mpps"][T] = round(T * m * passes / t / 1e6, 2)
-            l3["results_equal_cpu_chain"][T] = all(
-                np.array_equal(snap[k][0], pools[k].hdr["packet_type"]) and
-                np.array_equal(snap[k][1], pools[k].hdr["udata64"]) for k in range(T))
+        l3 = chain(HR, pools, hdr0, ptrs, m, lambda k: ["ip4*", "pkt_cls", f"pktdev_rx-{k}"], 20,
+                   ("packet_type", "udata64"),
+                   (("device_headers", D, True), ("host_headers", 0, True), ("staged", 0, False)), l3_cpu, l3_routes)
     finally:
+        O.set_driver_writes(False)
         HR.harness_rx_driver_writes(0)
         HR.harness_drop_clones()
         L.cndp_node_gpu_umem_reset()
         NodeFib.fini()
-    l3["gpu_over_cpu"] = {T: round(l3["gpu_Mpps"][T] / l3["cpu_Mpps"][T], 2) for T in l3["gpu_Mpps"]}
     l3["node"] = ("GPU pktdev_rx node (cndp_amd/node/pktdev_rx_gpu.c): soft parse + pkt_cls + ip4_lookup in one "
-                  "queue kernel, zero-copy, device headers; CPU: pktdev_rx's soft parse, pkt_cls and the "
+                  "queue kernel (device_headers: the node's default); CPU: pktdev_rx's soft parse, pkt_cls and the "
                   "ip4_lookup loop per 256-burst (orc_l3rx_chain_mbufs)")
     out["l3fwd_rx_chain"] = l3
     del pools, ptrs, hdr0
@@ -1263,59 +1305,27 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
         p = MbufPool(mc)
         p.fill(pktgen.imix(mc, v4routes=routes, v6routes=v6, seed=300 + k))
         pools.append(p)
-        L.cndp_node_gpu_umem_add(ctypes.c_void_p(p.base), ctypes.c_uint64(p.mem.nbytes))
         cid = HC.harness_clone(b"eth_rx", str(k).encode())
         assert HC.harness_eth_rx_port(cid, k) == 0
     hdr0 = [p.hdr.copy() for p in pools]
     ptrs = [p.ptrs(np.arange(mc)) for p in pools]
-    fields = ("packet_type", "ol_flags", "tx_offload", "lport", "data_off", "data_len")
-    cn = {"gpu_Mpps": {}, "cpu_Mpps": {}, "results_equal_cpu_chain": {}}
     HC.harness_rx_driver_writes(1)
+
+    def cnet_cpu(k):
+        return O.cnet_chain(ptrs[k], mc, hdr0[k]["data_len"], int(hdr0[k]["data_off"][0]), t4c, t6c,
+                            cpus=[cpus[k % len(cpus)]], lport=k) > 0
+
     try:
-        for T in threads:
-            gs = graphs_for(HC, T, lambda k: [f"eth_rx-{k}", "ptype", "ip4_input", "ip6_input"],
-                            170 + 2 * tmax * threads.index(T))
-
-            def reset(k, gs=gs):
-                HC.harness_graph_use(gs[k])
-                pools[k].hdr[:] = hdr0[k]
-                HC.harness_rx_load(k, ptrs[k], mc)
-                HC.harness_reset_counts()
-
-            snap = {}
-
-            def post(k, p):
-                if p == 0:  # from a fresh graph: ptype node state 0, as the CPU chain starts
-                    snap[k] = {f: pools[k].hdr[f].copy() for f in fields}
-
-            t = _lcore_run(cpus, T, reset, lambda k: HC.harness_walk_until(mc) >= 0, passes, post)
-            graphs_free(HC, gs)
-            cn["gpu_Mpps"][T] = round(T * mc * passes / t / 1e6, 2)
-
-            def reset_cpu(k):
-                pools[k].hdr[:] = hdr0[k]
-
-            def walk_cpu(k):
-                return O.cnet_chain(ptrs[k], mc, hdr0[k]["data_len"], int(hdr0[k]["data_off"][0]), t4c, t6c,
-                                    cpus=[cpus[k % len(cpus)]], lport=k) > 0
-
-            cpu_res = {}
-
-            def post_cpu(k, p):
-                if p == 0:
-                    cpu_res[k] = {f: pools[k].hdr[f].copy() for f in fields}
-
-            t = _lcore_run(cpus, T, reset_cpu, walk_cpu, passes, post_cpu)
-            cn["cpu_Mpps"][T] = round(T * mc * passes / t / 1e6, 2)
-            cn["results_equal_cpu_chain"][T] = all(np.array_equal(snap[k][f], cpu_res[k][f])
-                                                   for k in range(T) for f in fields)
+        cn = chain(HC, pools, hdr0, ptrs, mc, lambda k: [f"eth_rx-{k}", "ptype", "ip4_input", "ip6_input"], 140,
+                   ("packet_type", "ol_flags", "tx_offload", "lport", "data_off", "data_len"),
+                   (("host_headers", 0, True), ("device_headers", D, True), ("staged", 0, False)), cnet_cpu)
     finally:
         HC.harness_rx_driver_writes(0)
         HC.harness_drop_clones()
         L.cndp_node_gpu_umem_reset()
-    cn["gpu_over_cpu"] = {T: round(cn["gpu_Mpps"][T] / cn["cpu_Mpps"][T], 2) for T in cn["gpu_Mpps"]}
-    cn["node"] = ("GPU eth_rx node (cndp_amd/node/eth_rx_gpu.c): eth_rx + ptype + ip4_input / ip6_input, "
-                  "zero-copy, host headers; CPU: the cnet chain per 256-mbuf walk (oracle/cnet_chain.c); IMIX")
+    cn["node"] = ("GPU eth_rx node (cndp_amd/node/eth_rx_gpu.c): eth_rx + ptype + ip4_input / ip6_input "
+                  "(host_headers: the node's default); CPU: the cnet chain per 256-mbuf walk "
+                  "(oracle/cnet_chain.c); IMIX")
     out["cnet_eth_rx"] = cn
     return out
 
