@@ -183,8 +183,8 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
         cl.set_fib(fib, fib6)
         state.update(fib=fib, fib6=fib6, v6routes=v6, mode=N.CNDP_MODE_CNET)
         if cfg == "c4":
-            state["frames"] = family_group(pktgen.imix(n, seed=seed, v4routes=routes, v6routes=v6, device=dev,
-                                                       frame_mem=fm))
+            state["frames"] = pktgen.imix(n, seed=seed, v4routes=routes, v6routes=v6, device=dev, frame_mem=fm,
+                                          family_run=family_run())
         else:
             fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed, device=dev,
                                     frame_mem=fm)
@@ -213,8 +213,8 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
             fr = pktgen.packed_ipv4(n, routes=routes, seed=seed + 1000 * r, device=dev,
                                     in_route_frac=in_route_frac, frame_mem=fm)
         elif cfg == "c4":
-            fr = family_group(pktgen.imix(n, seed=seed + 1000 * r, v4routes=routes, v6routes=state["v6routes"],
-                                          device=dev, frame_mem=fm))
+            fr = pktgen.imix(n, seed=seed + 1000 * r, v4routes=routes, v6routes=state["v6routes"], device=dev,
+                             frame_mem=fm, family_run=family_run())
         else:
             fr = pktgen.packed_ipv4(n, slot=1536, frame_len=1500, routes=routes, seed=seed + 1000 * r, device=dev,
                                     frame_mem=fm)
@@ -234,24 +234,14 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
     return state
 
 
-def family_group(fr):
-    """Measurement of the one-family wave regroup's ceiling (off unless
-    CNDP_BENCH_FAMILY_GROUP=G): the same IMIX frames, their order permuted
-    inside each group of G frames so the IPv4 ones come first -- every wave
-    tile then holds one address family but the few that straddle the split,
-    at no regroup cost, the frames still within G of where they were.  Any
-    order is a valid batch (the full-batch parity check runs on it); only
-    the timing says what a regroup could gain at most."""
-    import torch as _t
-    g = int(os.environ.get("CNDP_BENCH_FAMILY_GROUP", "0"))
-    if g <= 0 or fr.offsets is None:
-        return fr
-    from cndp_amd import pktgen
-    v6 = (fr.slab[fr.offsets + fr.data_off + 12] == 0x86).to(_t.int64)
-    key = (_t.arange(fr.n, device=fr.offsets.device) // g) * 2 + v6
-    perm = _t.sort(key, stable=True).indices
-    return pktgen.Frames(fr.slab, fr.n, offsets=fr.offsets[perm].contiguous(), data_off=fr.data_off,
-                         lengths=fr.lengths[perm].contiguous() if fr.lengths is not None else None)
+def family_run() -> int:
+    """Measurement of the one-family wave regroup's ceiling (0 unless
+    CNDP_BENCH_FAMILY_RUN=R): C4's IMIX with the address family drawn once per
+    run of R frames instead of per frame, so every 64-frame wave tile holds
+    one family (R = 64) at no regroup cost, in the frames' own memory order.
+    A valid batch (the full-batch parity check runs on it); only the timing
+    says what a regroup could gain at most."""
+    return int(os.environ.get("CNDP_BENCH_FAMILY_RUN", "0"))
 
 
 OUTPUTS = {"c2": ("hash", "queue"), "c3": ("nh", "hash", "queue"), "c3rw": ("nh", "hash", "queue"),

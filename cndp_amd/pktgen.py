@@ -283,8 +283,10 @@ IMIX_WEIGHTS = (7, 4, 1)
 
 
 def imix(n: int, seed: int = SEED, v4routes=None, v6routes=None, device="cpu",
-         v6_frac: float = 0.5, frame_mem: str | None = None) -> Frames:
-    """C4: IMIX 64/570/1500 at 7:4:1, IPv4/IPv6 mix, packed at roundup(len, 64)."""
+         v6_frac: float = 0.5, frame_mem: str | None = None, family_run: int = 0) -> Frames:
+    """C4: IMIX 64/570/1500 at 7:4:1, IPv4/IPv6 mix, packed at roundup(len, 64).
+    family_run > 0: the address family drawn once per run of that many frames
+    (measurement of one-family wave tiles; C4 itself draws it per frame)."""
     idx = torch.arange(n, dtype=torch.int64, device=device)
     pick = rnd(seed, idx, 40) % 12
     size = torch.where(pick < 7, torch.full_like(pick, 64),
@@ -295,7 +297,7 @@ def imix(n: int, seed: int = SEED, v4routes=None, v6routes=None, device="cpu",
     slab = _slab(max(total, 64), device, frame_mem)
     rows = slab.view(-1, 64)
     frame_len = size - 4
-    is6 = (rnd(seed, idx, 41) % 1000) < int(round(v6_frac * 1000))
+    is6 = (rnd(seed, idx // family_run if family_run > 0 else idx, 41) % 1000) < int(round(v6_frac * 1000))
     chunk = 1 << 21
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
