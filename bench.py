@@ -1272,6 +1272,7 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
         O.set_driver_writes(False)
         HR.harness_rx_driver_writes(0)
         HR.harness_drop_clones()
+        HR.harness_pktdev_rx_ports_reset()
         L.cndp_node_gpu_umem_reset()
         NodeFib.fini()
     l3["node"] = ("GPU pktdev_rx node (cndp_amd/node/pktdev_rx_gpu.c): soft parse + pkt_cls + ip4_lookup in one "

@@ -46,3 +46,14 @@ void harness_register_cls_node(void)
     stub_cls.parent_id = CNE_NODE_ID_INVALID;
     stub_cls.id = __cne_node_register(&stub_cls);
 }
+
+/* forget every port registration (pktdev_ctrl.c's list back to empty) */
+void harness_pktdev_rx_ports_reset(void)
+{
+    struct pktdev_rx_node_main *m = pktdev_rx_get_node_data_get();
+    while (m->head) {
+        pktdev_rx_node_elem_t *e = m->head;
+        m->head = e->next;
+        free(e);
+    }
+}

@@ -1294,6 +1294,7 @@ def test_rx_node_graphs_per_lcore(gpu, threads):
         os.environ.pop("CNDP_GPU_BATCH", None)
         H.harness_chain(0)
         H.harness_drop_clones()
+        H.harness_pktdev_rx_ports_reset()
         H.harness_edges_reset()
         L.cndp_node_ip4_rewrite_reset()
         L.cndp_node_gpu_umem_reset()
