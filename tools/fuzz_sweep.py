@@ -1,5 +1,7 @@
 """Many-seed parity sweep (diagnostic): random frames through every classify
-mode and kernel variant against the oracle, on one GPU.  Seeds, slot sizes,
+mode, the kernel each layout selects, the CNDP_TUNE_* schedule and
+speculation knobs, and chained cnet calls (the ptype node state carried
+across two calls) against the oracle, on one GPU.  Seeds, slot sizes,
 data offsets and batch lengths vary per round; IMIX and strided C4 / C5
 shapes with random destinations are mixed in.  Prints one line per case and
 a summary; exit status 1 on any mismatch.
@@ -56,10 +58,14 @@ def main():
                                                     routes=routes, device=dev, seed=seed)))
         for name, f in shapes:
             for mode, cl, kw, variants in (
-                    (O.MODE_CNET, cn, dict(tables4=t4, tables6=t6), [dict(cnet_tile=0), dict(cnet_tile=1),
-                                                                     dict(cnet_tile=1, stream_bal=2)]),
-                    (O.MODE_L3FWD, l3, dict(tables4=t43), [dict(tile=0), dict(tile=1)]),
-                    (O.MODE_HASH, l3, {}, [dict(tile=1)])):
+                    (O.MODE_CNET, cn, dict(tables4=t4, tables6=t6),
+                     [dict(cnet_tile=0), dict(cnet_tile=1), dict(cnet_tile=1, stream_bal=2),
+                      dict(cnet_tile=1, stream_bal=1), dict(spec_scan=1), dict(spec_scan=2),
+                      dict(spec_types=1), dict(spec_types=2), dict(spec_lists=0), dict(spec_grid=1),
+                      dict(cnet_fold=1), dict(cnet_fold=2)]),
+                    (O.MODE_L3FWD, l3, dict(tables4=t43), [dict(tile=0), dict(tile=1), dict(tile=1, stream_bal=1),
+                                                          dict(tile=1, stream_bal=2)]),
+                    (O.MODE_HASH, l3, {}, [dict(tile=1), dict(tile=1, stream_bal=1)])):
                 if name != "fuzz" and mode != O.MODE_CNET:
                     continue
                 ref = oracle_classify(mode, f, **kw)
@@ -80,7 +86,32 @@ def main():
                         bad += 1
                         status = f"MISMATCH {ex}"
                     print(f"round {r} {name} n={f.n} mode={mode} {v}: {status}", flush=True)
-                cl.set_tuning(stream_bal=0, tile=1, cnet_tile=1)
+                    cl.set_tuning(stream_bal=0, tile=1, cnet_tile=1, spec_scan=0, spec_types=0, spec_lists=1,
+                                  spec_grid=0, cnet_fold=0)
+                if nmode == N.CNDP_MODE_CNET and f.n > 512:
+                    # chained calls: the ptype node state carried from a first
+                    # call over a burst-aligned head into a second one
+                    cut = (f.n // 2) // 256 * 256
+                    st = np.zeros(1, np.uint16)
+                    cl.set_tuning(cnet_spec=256)
+                    for lo, hi in ((0, cut), (cut, f.n)):
+                        if f.offsets is not None:
+                            part = pktgen.Frames(f.slab, hi - lo, offsets=f.offsets[lo:hi].contiguous(),
+                                                 data_off=f.data_off)
+                        else:
+                            part = pktgen.Frames(f.slab[lo * f.stride:], hi - lo, stride=f.stride,
+                                                 data_off=f.data_off)
+                        r_ = oracle_classify(mode, part, spec_burst=256, spec_state=st, **kw)
+                        out = cl.classify(part, nmode, n_bins=64)
+                        torch.cuda.synchronize()
+                        cases += 1
+                        try:
+                            assert_same({k: v2 for k, v2 in out.items() if k != "n_bins"}, r_)
+                            status = "ok"
+                        except AssertionError as ex:
+                            bad += 1
+                            status = f"MISMATCH {ex}"
+                        print(f"round {r} {name} n={part.n} chained [{lo},{hi}): {status}", flush=True)
     print(f"{cases} cases, {bad} mismatches, {time.time() - t0:.0f} s", flush=True)
     return 1 if bad else 0
 
