@@ -190,9 +190,11 @@ def build_state(cfg: str, dev, rank: int, n_override: int | None, in_route_frac:
                                     frame_mem=fm)
             pktgen.corrupt_cksum(fr, 1024, seed)
             state["frames"] = fr
-    # l3fwd / hash: the graph edge is nh >> 16 (no separate edge stream);
-    # cnet keeps the edge output (its drop/forward/proto edge is not in nh
-    # for packets the ptype node sends elsewhere)
+    # no config stores the edge stream: l3fwd's edge is nh >> 16, and SURVEY
+    # §8(d) counts no edge bytes for cnet either (a cnet frame's edge still
+    # shows in its nh -- a FIB value, or invalid when the ptype node sent it
+    # elsewhere -- and in the bin counters the parity checks compare; the GPU
+    # tests compare the edge stream itself);
     # the per-packet outputs each config's workload asks for, as SURVEY §8(d)
     # counts them: C2 hash + queue (hash mode's nh is a constant), C3 / C4 nh +
     # hash + queue, C5 the verdict / next hop alone (parse + checksum verify +
