@@ -82,8 +82,9 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     """`bench.py --gpus N` (N > 1) started without torchrun's environment: run
     the N ranks as a child torchrun (no exec: this process never touches the
     GPU; torch.cuda.device_count() does not initialise it on this image), pass
-    their output through, and print rank 0's JSON line once it checks out
-    (check_rank_line).  Returns the exit status."""
+    their other output through to stderr, and print rank 0's JSON line -- the
+    one line on stdout -- once it checks out (check_rank_line).  Returns the
+    exit status."""
     import socket
     import subprocess
     backend = os.environ.get("CNDP_DIST_BACKEND", "nccl")
@@ -98,12 +99,12 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
     line = None
-    for ln in proc.stdout:
+    for ln in proc.stdout:  # stdout keeps one line, rank 0's JSON; the rest (gloo / RCCL banners) to stderr
         if ln.startswith("{"):
             line = ln.strip()
         else:
-            sys.stdout.write(ln)
-            sys.stdout.flush()
+            sys.stderr.write(ln)
+            sys.stderr.flush()
     rc = proc.wait()
     if rc != 0:
         log(f"[bench] ranks exited with status {rc}")

@@ -191,9 +191,10 @@ def test_launch_ranks_runs_torchrun_child(monkeypatch, tmp_path, capsys, bins, r
         sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
         "--master-addr=127.0.0.1", f"--master-port={port}", str(script)])
     assert B.launch_ranks(2, []) == rc
-    out = capsys.readouterr().out
-    assert "progress from rank 0" in out
-    assert out.count('"n_gpus": 2') == (1 if rc == 0 else 0)
+    cap = capsys.readouterr()
+    assert "progress from rank 0" in cap.err and "progress" not in cap.out
+    assert cap.out.count('"n_gpus": 2') == (1 if rc == 0 else 0)
+    assert len(cap.out.splitlines()) == (1 if rc == 0 else 0)   # stdout: the JSON line alone
 
 
 @pytest.mark.gpu
@@ -214,8 +215,8 @@ def test_bench_gpus2_launches_two_ranks():
            "--ring", "1"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [s for s in r.stdout.splitlines() if s.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]   # the JSON line alone
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0
     assert rec["config"]["bins_total"] == 2 * n * steps
