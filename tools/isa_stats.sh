@@ -5,7 +5,7 @@
 cd "$(dirname "$0")/.." || exit 1
 pat=${1:-k_cnet_defer}
 out=${TMPDIR:-/tmp}/cndp_isa.s
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only -S -Wno-unused-parameter \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only -S -Wno-unused-parameter $EXTRA \
     -Wno-unused-result -Wno-unused-value -Iinclude -Icndp_amd/csrc cndp_amd/csrc/cndp_gpu.hip -o "$out" || exit 1
 python3 - "$out" "$pat" <<'PY'
 import re, sys, collections
