@@ -1312,7 +1312,8 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     try:
         cn = chain(HC, pools, hdr0, ptrs, mc, lambda k: [f"eth_rx-{k}", "ptype", "ip4_input", "ip6_input"], 140,
                    ("packet_type", "ol_flags", "tx_offload", "lport", "data_off", "data_len"),
-                   (("host_headers", 0, True), ("device_headers", D, True), ("staged", 0, False)), cnet_cpu)
+                   (("host_headers", 0, True), ("device_headers", D, True),
+                    ("host_writeback", N.CNDP_MQ_F_HOST_WRITEBACK, True), ("staged", 0, False)), cnet_cpu)
     finally:
         HC.harness_rx_driver_writes(0)
         HC.harness_drop_clones()

@@ -6826,7 +6826,9 @@ struct MqArgs {
     uint64_t slab_len;
     uint16_t *edges;        // out: next edge per mbuf (pinned host)
     uint64_t *priv1;        // out (staged ip4_lookup): node_mbuf_priv1
-    u32x4 *rec;             // out (staged cnet): {ptype, rxmeta, data_len | edge << 16 | node << 24, hash}
+    u32x4 *rec;             // out (staged cnet, and zc with hostwb): {ptype, rxmeta, data_len | edge << 16 | node << 24, hash}
+    u32x4 *rec_md;          // out (zc cnet, hostwb): per mbuf the source and destination address (2 x 16 B)
+    uint32_t hostwb;        // zc cnet, CNDP_MQ_F_HOST_WRITEBACK: results as records, poll writes the mbufs
     // cnet classify outputs (device)
     const uint32_t *ptype, *rxmeta, *hash;
     const uint8_t *edge8;
@@ -7392,7 +7394,37 @@ __global__ __launch_bounds__(MQ_TPB) void k_mq_cnet_post(MqArgs a)
                 e = mq_input_at(a.slab, a.slab_len, o, v6, a.tb, blen) >> 24;
         }
         const uint32_t h = a.want_hash ? a.hash[i] : 0u;
-        if (a.zc) {
+        if (a.zc && a.hostwb) {
+            // the record staged mode writes, plus the addresses ipv4/ipv6_save_metadata
+            // copy (from the saved window, or the frame when past it)
+            const uint64_t m = a.mb[i];
+            if (m != 0 && fo < a.slab_len) {
+                u32x4 r;
+                r.x = pt;
+                r.y = rm;
+                r.z = dlen | (e << 16) | (node << 24);
+                r.w = h;
+                a.rec[i] = r;
+                if (node != CNDP_MQ_NODE_PTYPE && a.rec_md) {
+                    const uint32_t ip = adj ? l2 : 0u, na = v6 ? 4u : 1u;
+                    const uint32_t s_at = ip + (v6 ? 8u : 12u), d_at = ip + (v6 ? 24u : 16u);
+                    const bool inwin = d_at + 4u * na <= 64u;
+                    const u32x4 *w = a.win + 4ull * i;
+                    const uint8_t *fr = a.slab + fo;
+                    const uint64_t fav = a.slab_len - fo;
+                    uint32_t sa[4] = {0u, 0u, 0u, 0u}, da[4] = {0u, 0u, 0u, 0u};
+                    for (uint32_t k = 0; k < na; k++) {
+                        sa[k] = inwin ? mq_win32(w, s_at + 4 * k) : gld32(fr, fav, s_at + 4 * k);
+                        da[k] = inwin ? mq_win32(w, d_at + 4 * k) : gld32(fr, fav, d_at + 4 * k);
+                    }
+                    a.rec_md[2 * i] = (u32x4){sa[0], sa[1], sa[2], sa[3]};
+                    a.rec_md[2 * i + 1] = (u32x4){da[0], da[1], da[2], da[3]};
+                }
+                a.edges[i] = (uint16_t)((node << 8) | e);
+            } else {
+                a.edges[i] = (uint16_t)MQ_EDGE_NONE;
+            }
+        } else if (a.zc) {
             const uint64_t m = a.mb[i];
             if (m != 0 && fo < a.slab_len) {
                 // data_off, lport, buf_len, data_len, packet_type in one 12-B store
@@ -7462,7 +7494,8 @@ struct cndp_gpu_mq {
     uint32_t *flags, *flags_d;     // pinned completion flags (host / device view)
     uint32_t *tickets;             // device, one per slot
     // byte offsets inside each slot's pinned block (H) and device block (D)
-    uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_stage, h_bst, h_bytes;
+    uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_rmd, h_stage, h_bst, h_bytes;
+    int hostwb;                    // zc cnet with CNDP_MQ_F_HOST_WRITEBACK
     uint64_t d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_win, d_off, d_len, d_md, d_bytes;
     int devhdr;                    // zc with CNDP_MQ_F_DEVICE_HEADERS (ip4_lookup, cnet)
     // cnet device headers: pools seen whose conf.metadata(m) is m + 64 (and
@@ -7520,7 +7553,10 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
         k.mode != CNDP_MQ_IP4_REWRITE)
         return -EINVAL;
     if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_RX_PARSE |
-                    CNDP_MQ_F_REWRITE))
+                    CNDP_MQ_F_REWRITE | CNDP_MQ_F_HOST_WRITEBACK))
+        return -EINVAL;
+    if ((k.flags & CNDP_MQ_F_HOST_WRITEBACK) &&
+        (k.mode != CNDP_MQ_CNET || (k.flags & CNDP_MQ_F_DEVICE_HEADERS)))
         return -EINVAL;
     if ((k.flags & (CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE)) && k.mode != CNDP_MQ_IP4_LOOKUP)
         return -EINVAL;
@@ -7572,8 +7608,10 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->h_len = q->h_off + al64(B * 8);                    // cnet: length fields; rewrite: priv1
     q->h_md = q->h_len + (cnet || rw ? al64(B * 8) : 0);  // cnet zc: metadata addresses
     q->h_edge = q->h_md + (cnet && zc ? al64(B * 8) : 0);
-    q->h_rec = q->h_edge + al64(B * 2);                   // staged: records
-    q->h_stage = q->h_rec + (zc || rw || k.mode == CNDP_MQ_MAC_SWAP ? 0 : al64(B * (cnet ? 16 : 8)));
+    q->hostwb = zc && cnet && (k.flags & CNDP_MQ_F_HOST_WRITEBACK);
+    q->h_rec = q->h_edge + al64(B * 2);                   // staged (and host writeback): records
+    q->h_rmd = q->h_rec + ((zc && !q->hostwb) || rw || k.mode == CNDP_MQ_MAC_SWAP ? 0 : al64(B * (cnet ? 16 : 8)));
+    q->h_stage = q->h_rmd + (q->hostwb ? B * 32 : 0);     // host writeback: metadata addresses
     q->h_bst = q->h_stage + B * q->stage;                 // CNDP_MQ_F_REWRITE: burst starts
     q->h_bytes = q->h_bst + ((k.flags & CNDP_MQ_F_REWRITE) ? al64((B + 1) * 4) : 0);
     q->d_nh = 0;
@@ -7718,6 +7756,8 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
     a.edges = (uint16_t *)(HD + q->h_edge);
     a.priv1 = (uint64_t *)(HD + q->h_rec);
     a.rec = (u32x4 *)(HD + q->h_rec);
+    a.hostwb = (uint32_t)q->hostwb;
+    a.rec_md = q->hostwb && !(q->conf.flags & CNDP_MQ_F_NO_METADATA) ? (u32x4 *)(HD + q->h_rmd) : nullptr;
     a.lport = q->conf.lport;
     a.want_hash = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
     a.ticket = q->tickets + slot_i;
@@ -8097,11 +8137,53 @@ static void mq_save_md_host(uint8_t *md, const uint8_t *ip, bool v6)
 
 // one finished slot's results into its mbufs where the kernels did not
 // write them (staged: every field; zero-copy cnet: metadata the device could
-// not reach)
+// not reach; zero-copy cnet with host writeback: every field, from records)
 static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
 {
     const uint32_t mode = q->conf.mode;
     const uint16_t *ed = (const uint16_t *)(sl->h + q->h_edge);
+    if (q->hostwb) {
+        const uint32_t *rec = (const uint32_t *)(sl->h + q->h_rec);
+        const uint8_t *rmd = sl->h + q->h_rmd;
+        const bool wh = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
+        const bool md_on = !(q->conf.flags & CNDP_MQ_F_NO_METADATA);
+        const uint16_t lport = q->conf.lport;
+        for (uint32_t i = i0; i < i1; i++) {
+            if (i + MQ_PF < i1)
+                __builtin_prefetch(sl->mb[i + MQ_PF], 1);
+            if (ed[i] == MQ_EDGE_NONE) // outside every registered region: untouched
+                continue;
+            uint8_t *m = (uint8_t *)sl->mb[i];
+            const uint32_t pt = rec[4 * i], rm = rec[4 * i + 1], w2 = rec[4 * i + 2];
+            // eth_rx mbuf_update (eth_rx.c:35-63), then the input node's data_len
+            *(uint32_t *)(m + MB_PTYPE) = pt;
+            *(uint64_t *)(m + MB_OL_FLAGS) = (uint64_t)(rm >> 29) << 61;
+            *(uint64_t *)(m + MB_TX_OFFLOAD) = (uint64_t)(rm & 0xffffffu);
+            *(uint16_t *)(m + MB_LPORT) = lport;
+            const uint16_t l2 = (uint16_t)(rm & 0x7fu);
+            uint16_t doff = *(uint16_t *)(m + MB_DATA_OFF);
+            const uint16_t dlen0 = *(uint16_t *)(m + MB_DATA_LEN);
+            const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
+            if (l2 <= dlen0 && (uint32_t)l2 + doff <= blen) // pktmbuf_adj_offset
+                *(uint16_t *)(m + MB_DATA_OFF) = (uint16_t)(doff + l2);
+            *(uint16_t *)(m + MB_DATA_LEN) = (uint16_t)(w2 & 0xffffu);
+            if (wh)
+                *(uint32_t *)(m + MB_HASH) = rec[4 * i + 3];
+            const uint32_t node = w2 >> 24;
+            if (md_on && (node == CNDP_MQ_NODE_IP4 || node == CNDP_MQ_NODE_IP6)) {
+                uint8_t *md = mq_md_host(q, m);
+                if (md) { // ipv4/ipv6_save_metadata (ip4_input.c:33-48, ip6_input.c:32-48)
+                    const bool v6 = node == CNDP_MQ_NODE_IP6;
+                    const uint8_t fam = v6 ? (uint8_t)MQ_AF_INET6 : (uint8_t)MQ_AF_INET, alen = v6 ? 16 : 4;
+                    md[0] = md[20] = fam;
+                    md[1] = md[21] = alen;
+                    memcpy(md + 4, rmd + 32ull * i, alen);
+                    memcpy(md + 24, rmd + 32ull * i + 16, alen);
+                }
+            }
+        }
+        return;
+    }
     if (q->zc) {
         if (mode != CNDP_MQ_CNET || (q->conf.flags & CNDP_MQ_F_NO_METADATA))
             return;

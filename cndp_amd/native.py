@@ -53,6 +53,7 @@ CNDP_TUNE_HOST_WINDOW = 19
 CNDP_MQ_IP4_LOOKUP, CNDP_MQ_CNET, CNDP_MQ_MAC_SWAP, CNDP_MQ_IP4_REWRITE = 0, 1, 2, 3
 CNDP_MQ_F_HASH, CNDP_MQ_F_NO_METADATA, CNDP_MQ_F_DEVICE_HEADERS, CNDP_MQ_F_RX_PARSE = 1, 2, 4, 8
 CNDP_MQ_F_REWRITE = 16
+CNDP_MQ_F_HOST_WRITEBACK = 1 << 5
 CNDP_MQ_EDGE_NONE = 0xFFFF
 CNDP_MQ_EDGE_CLS_DROP = 0xFFFE
 CNDP_MQ_EDGE_LOOKUP_DROP = 0xFFFD

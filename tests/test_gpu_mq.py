@@ -324,11 +324,13 @@ def cnet_check(pool, orig, ref, t4, t6, lport, check_md=True):
     return (node << 8) | np.where(at_input, e_in, e8 & 0x7F)
 
 
-@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers", "host_writeback"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_cnet(cn, gpu, zero_copy, kind):
     """"device_headers": zero-copy with CNDP_MQ_F_DEVICE_HEADERS (k_mq_cnet_hdr
-    reads each mbuf's header on the device)."""
+    reads each mbuf's header on the device); "host_writeback": zero-copy with
+    CNDP_MQ_F_HOST_WRITEBACK (frames read in place, the fields and metadata
+    written by poll from the records)."""
     cl, routes, v6, t4, t6 = cn
     n = 24000
     pool, orig = cnet_pool(n, routes, v6, bool(zero_copy), shift=kind == "shifted")
@@ -336,6 +338,8 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
     flags = N.CNDP_MQ_F_HASH if kind == "ragged" else 0
     if zero_copy == "device_headers":
         flags |= N.CNDP_MQ_F_DEVICE_HEADERS
+    if zero_copy == "host_writeback":
+        flags |= N.CNDP_MQ_F_HOST_WRITEBACK
     if zero_copy:
         cl.host_register(pool.mem)
         umem = pool.base
@@ -362,6 +366,17 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
     # every node and edge kind shows up
     assert {0, 1, 2} <= set(np.unique(node).tolist())
     assert (want_e == ((N.CNDP_MQ_NODE_PTYPE << 8) | 5)).sum() > 0   # gtpu
+
+
+def test_mq_host_writeback_flag_rules(cn, gpu):
+    """CNDP_MQ_F_HOST_WRITEBACK is a cnet-queue flag and excludes device
+    headers (the lcore reads the headers it writes back into)."""
+    cl = cn[0]
+    with pytest.raises(OSError):
+        MbufQueue(cl, N.CNDP_MQ_CNET, flags=N.CNDP_MQ_F_HOST_WRITEBACK | N.CNDP_MQ_F_DEVICE_HEADERS)
+    with pytest.raises(OSError):
+        MbufQueue(cl, N.CNDP_MQ_MAC_SWAP, flags=N.CNDP_MQ_F_HOST_WRITEBACK)
+    MbufQueue(cl, N.CNDP_MQ_CNET, flags=N.CNDP_MQ_F_HOST_WRITEBACK).close()   # staged: writes back anyway
 
 
 def test_mq_cnet_spec_wait_expiry(cn, gpu):
@@ -403,11 +418,13 @@ def test_mq_cnet_spec_wait_expiry(cn, gpu):
     assert np.array_equal(edges.astype(np.int64), want_e)
 
 
-def test_mq_cnet_device_headers_metadata_hook(cn, gpu):
+@pytest.mark.parametrize("flags", ["device_headers", "host_writeback"])
+def test_mq_cnet_device_headers_metadata_hook(cn, gpu, flags):
     """CNDP_MQ_F_DEVICE_HEADERS with a pktmbuf_metadata hook: mbufs of a pool
     whose metadata is the default m + 64 get it from the device, those of a
     pool with a metadata array (pktmbuf.h:1216-1217) from poll through the
-    hook -- both as the host-header path writes them."""
+    hook -- both as the host-header path writes them.  host_writeback
+    (CNDP_MQ_F_HOST_WRITEBACK): poll writes both through the hook."""
     cl, routes, v6, t4, t6 = cn
     n = 6000
     pool, orig = cnet_pool(n, routes, v6, True)
@@ -428,8 +445,8 @@ def test_mq_cnet_device_headers_metadata_hook(cn, gpu):
     cl.host_register(pool.mem)
     try:
         cl.set_tuning(cnet_spec=256)
-        q = MbufQueue(cl, N.CNDP_MQ_CNET, flags=N.CNDP_MQ_F_DEVICE_HEADERS, batch=2048, depth=3,
-                      umem=pool.base, lport=3, metadata=hook)
+        q = MbufQueue(cl, N.CNDP_MQ_CNET, batch=2048, depth=3, umem=pool.base, lport=3, metadata=hook,
+                      flags=N.CNDP_MQ_F_DEVICE_HEADERS if flags == "device_headers" else N.CNDP_MQ_F_HOST_WRITEBACK)
         ref = _cnet_expect(pool, order, bursts, t4, t6, 0, 3)
         addrs, edges = q.run(pool, order, bursts)
         q.close()
