@@ -396,6 +396,42 @@ def host_cpus():
     return cpus, model, quota
 
 
+def spread_cpus(cpus: list[int], k: int) -> list[int]:
+    """k of the allowed CPUs for k pinned worker threads, as a packet-processing
+    deployment places its lcores: one physical core each (no SMT sibling of a
+    core already taken) and spread round-robin over the L3 domains (CCDs), so
+    no two threads share an L3 while another is free; the GPU's NUMA node
+    first.  Falls back to the first k CPUs where sysfs has no topology."""
+    def rd(path):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+    node = rd("/sys/class/drm/card0/device/numa_node") or rd("/sys/class/drm/card1/device/numa_node")
+    groups: dict = {}
+    for c in cpus:
+        l3 = rd(f"/sys/devices/system/cpu/cpu{c}/cache/index3/id")
+        if l3 is None:
+            return cpus[:k]
+        nd = next((n for n in range(8) if os.path.exists(f"/sys/devices/system/cpu/cpu{c}/node{n}")), 0)
+        groups.setdefault((0 if node is None or str(nd) == node else 1, nd, int(l3)), []).append(c)
+    order = [groups[g] for g in sorted(groups)]
+    taken, siblings = [], set()
+    while len(taken) < k and any(order):
+        for g in order:
+            while g and g[0] in siblings:
+                g.pop(0)
+            if g and len(taken) < k:
+                c = g.pop(0)
+                taken.append(c)
+                sib = rd(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") or str(c)
+                for part in sib.split(","):
+                    lo, _, hi = part.partition("-")
+                    siblings.update(range(int(lo), int(hi or lo) + 1))
+    return taken if len(taken) == k else cpus[:k]
+
+
 def cpu_baseline(state, budget_s: float = 10.0):
     """The reference chain on this host's cores (rank 0, N=1), one pinned
     thread per CPU of the process's affinity set, and 1 thread, over a bounded
@@ -425,8 +461,9 @@ def cpu_baseline(state, budget_s: float = 10.0):
         offs = np.arange(n, dtype=np.uint64) * np.uint64(fr.stride) + np.uint64(fr.data_off)
     cpus, model, quota = host_cpus()
     aff = len(cpus)
-    if quota:  # a CPU quota below the affinity set: one pinned thread per CPU of the quota
-        cpus = cpus[:max(1, int(-(-quota // 1)))]
+    # one pinned thread per CPU of the quota (a quota below the affinity set),
+    # on distinct physical cores spread over the L3 domains (spread_cpus)
+    cpus = spread_cpus(cpus, min(len(cpus), max(1, int(-(-quota // 1)))) if quota else len(cpus))
     extra = {}
     if cnet:
         lens = (fr.lengths[:n].cpu().numpy() if fr.lengths is not None
@@ -1129,10 +1166,12 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     from cndp_amd.mbuf import MbufPool
     from oracle import oracle as O
     cpus, _, quota = host_cpus()
-    if quota:
-        cpus = cpus[:max(1, int(-(-quota // 1)))]
-    threads = [t for t in threads if t <= max(1, len(cpus))]
+    n_cpu = min(len(cpus), int(-(-quota // 1))) if quota else len(cpus)  # the CPU quota, in CPUs
+    threads = [t for t in threads if t <= max(1, n_cpu)]
     tmax = max(threads)
+    # lcore k on core cpus[k]: distinct physical cores spread over the L3 domains,
+    # the same cores for the GPU and the CPU legs
+    cpus = spread_cpus(cpus, tmax)
     L = N.lib()
     routes = pktgen.l3fwd_routes()
     D = N.CNDP_MQ_F_DEVICE_HEADERS
