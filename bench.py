@@ -1356,6 +1356,7 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     finally:
         HC.harness_rx_driver_writes(0)
         HC.harness_drop_clones()
+        HC.harness_eth_rx_ports_reset()
         L.cndp_node_gpu_umem_reset()
     cn["node"] = ("GPU eth_rx node (cndp_amd/node/eth_rx_gpu.c): eth_rx + ptype + ip4_input / ip6_input "
                   "(host_headers: the node's default); CPU: the cnet chain per 256-mbuf walk "

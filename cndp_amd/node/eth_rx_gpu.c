@@ -32,7 +32,9 @@
  * flight the node drains and then waits for the oldest batch.
  *
  * Tuning from the environment: CNDP_GPU_DEVICE (0), CNDP_GPU_BATCH (8192),
- * CNDP_GPU_DEPTH (4), CNDP_GPU_DELAY_US (50).  Frames are read in place when
+ * CNDP_GPU_DEPTH (4), CNDP_GPU_DELAY_US (50), CNDP_GPU_MQ_FLAGS (the queue's
+ * header / result form; default host headers, results written back by the
+ * lcores with more than four receive nodes -- see init).  Frames are read in place when
  * the application registered its UMEMs with cndp_node_gpu_umem_add(), else
  * staged.  One GPU context and queue per cloned node (per port and graph).
  *
@@ -66,6 +68,7 @@
 #include "gpu_node_enqueue.h"
 
 #define RX_BURST 256 /* CNE_GRAPH_BURST_SIZE (cne_graph.h:30) */
+#define ETH_RX_HOST_WB_MIN 4
 
 /* ETH_RX_GPU_PROF (diagnostic builds only): where the node's host thread
  * spends its time -- [0] pktdev_rx_burst, [1] cndp_gpu_mq_submit, [2] poll,
@@ -309,8 +312,18 @@ static int eth_rx_gpu_init(const struct cne_graph *graph, struct cne_node *node)
     conf.metadata = rx_metadata;
     /* the host resolves each frame from the mbuf header (measured faster here
      * than the device reading the headers over PCIe: 70-75 against 61 Mpps,
-     * DESIGN.md §6); CNDP_GPU_MQ_FLAGS=4 for CNDP_MQ_F_DEVICE_HEADERS */
-    conf.flags = env_u32("CNDP_GPU_MQ_FLAGS", 0);
+     * DESIGN.md §6); with more than ETH_RX_HOST_WB_MIN receive nodes on the GPU
+     * the results come back as records the lcores write into the mbufs
+     * (CNDP_MQ_F_HOST_WRITEBACK): the device's small PCIe stores bound the
+     * in-place form near 100 Mpps summed over lcores, the records scale with
+     * them (bench node_lcores: 100 against 150 Mpps at 8 lcores, 47 against
+     * 27 at one).  The clones pkt_ctrl.c registered, one per port, are the
+     * receive nodes the application runs.  CNDP_GPU_MQ_FLAGS overrides
+     * (4: CNDP_MQ_F_DEVICE_HEADERS). */
+    uint32_t n_rx = 0;
+    for (eth_rx_node_elem_t *e = eth_rx_main.head; e; e = e->next)
+        n_rx++;
+    conf.flags = env_u32("CNDP_GPU_MQ_FLAGS", n_rx > ETH_RX_HOST_WB_MIN ? CNDP_MQ_F_HOST_WRITEBACK : 0u);
     /* zero-copy: the kernels read the frames in the UMEMs (registration is
      * shared and counted across the per-port contexts) */
     void *umem = NULL;

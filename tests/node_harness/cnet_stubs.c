@@ -92,3 +92,14 @@ void harness_register_input_nodes(void)
         r[i]->id = __cne_node_register(r[i]);
     }
 }
+
+/* forget every port registration (pkt_ctrl.c's list back to empty) */
+void harness_eth_rx_ports_reset(void)
+{
+    struct eth_rx_node_main *m = eth_rx_get_node_data_get();
+    while (m->head) {
+        eth_rx_node_elem_t *e = m->head;
+        m->head = e->next;
+        free(e);
+    }
+}

@@ -1363,6 +1363,7 @@ def test_cnet_node_graphs_per_lcore(gpu, threads):
     finally:
         _destroy_graphs(H, graphs)
         H.harness_drop_clones()
+        H.harness_eth_rx_ports_reset()
         L.cndp_node_gpu_umem_reset()
     for k, (pool, orig, ref) in enumerate(pools):
         have = np.full(n, -1, np.int64)
