@@ -1236,8 +1236,9 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
             for vi, (v, flags, zc) in enumerate(variants):
                 umem(pools, zc)
                 os.environ["CNDP_GPU_MQ_FLAGS"] = str(flags)
-                # graph ids < 256: the GPU nodes keep per-graph state by id (GPU_GRAPHS_MAX)
-                gs = graphs_for(H, T, pats_of, gid_base + (ti * len(variants) + vi) * tmax)
+                # graph ids < 256: the GPU nodes keep per-graph state by id
+                # (GPU_GRAPHS_MAX); a form's graphs are destroyed before the next
+                gs = graphs_for(H, T, pats_of, gid_base + vi * tmax)
                 os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
                 if after_create:
                     after_create()
@@ -1309,7 +1310,9 @@ def node_lcores(dev, threads=(1, 2, 4, 8), m: int = 1 << 18, mc: int = 1 << 17, 
     try:
         l3 = chain(HR, pools, hdr0, ptrs, m, lambda k: ["ip4*", "pkt_cls", f"pktdev_rx-{k}"], 20,
                    ("packet_type", "udata64"),
-                   (("device_headers", D, True), ("host_headers", 0, True), ("staged", 0, False)), l3_cpu, l3_routes)
+                   (("device_headers", D, True), ("host_headers", 0, True),
+                    ("device_headers_host_writeback", D | N.CNDP_MQ_F_HOST_WRITEBACK, True),
+                    ("host_writeback", N.CNDP_MQ_F_HOST_WRITEBACK, True), ("staged", 0, False)), l3_cpu, l3_routes)
     finally:
         O.set_driver_writes(False)
         HR.harness_rx_driver_writes(0)

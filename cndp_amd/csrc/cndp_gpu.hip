@@ -6825,10 +6825,10 @@ struct MqArgs {
     const uint8_t *slab;    // cnet zc: the batch's region (device view); staged: the staging
     uint64_t slab_len;
     uint16_t *edges;        // out: next edge per mbuf (pinned host)
-    uint64_t *priv1;        // out (staged ip4_lookup): node_mbuf_priv1
+    uint64_t *priv1;        // out (staged ip4_lookup, and zc with hostwb): node_mbuf_priv1 (pkt_cls drops: packet_type)
     u32x4 *rec;             // out (staged cnet, and zc with hostwb): {ptype, rxmeta, data_len | edge << 16 | node << 24, hash}
     u32x4 *rec_md;          // out (zc cnet, hostwb): per mbuf the source and destination address (2 x 16 B)
-    uint32_t hostwb;        // zc cnet, CNDP_MQ_F_HOST_WRITEBACK: results as records, poll writes the mbufs
+    uint32_t hostwb;        // zc cnet / ip4_lookup, CNDP_MQ_F_HOST_WRITEBACK: results as records, poll writes the mbufs
     // cnet classify outputs (device)
     const uint32_t *ptype, *rxmeta, *hash;
     const uint8_t *edge8;
@@ -7053,9 +7053,11 @@ __device__ __forceinline__ MqL3 mq_l3_one(const MqArgs &a, uint32_t i)
         const uint8_t *e = p - (MQ_W4_AT - MQ_W4R_AT);
         const uint32_t et = eavail >= 2 ? ((uint32_t)gbyte(e, eavail, 0) << 8) | gbyte(e, eavail, 1) : 0u;
         const uint32_t pt = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
-        if (a.zc)
+        if (a.zc && !a.hostwb)
             *gp((uint32_t *)(m + MB_PTYPE)) = pt;
         if (pt != 0x90u) {
+            if (a.hostwb) // the record of a frame pkt_cls drops carries its packet_type
+                a.priv1[i] = pt;
             r.st = MQ_L3_CLS;
             return r;
         }
@@ -7079,9 +7081,9 @@ __device__ __forceinline__ MqL3 mq_l3_one(const MqArgs &a, uint32_t i)
     }
     r.val = a.tb.d16 ? lpm4d(a.tb.d16, a.tb.pages, a.tb.t8, dip) : lpm4(a.tb.t24, a.tb.t8, dip);
     r.priv1 = (uint64_t)(r.val & 0xffffu) | ((uint64_t)ttl << 16) | ((uint64_t)ck << 32);
-    if (a.zc)
+    if (a.zc && !a.hostwb)
         *gp((uint64_t *)(m + MB_UDATA64)) = r.priv1;
-    else
+    else // staged, or CNDP_MQ_F_HOST_WRITEBACK: a coalesced record poll writes into the mbuf
         a.priv1[i] = r.priv1;
     r.st = MQ_L3_LOOKED;
     return r;
@@ -7495,7 +7497,7 @@ struct cndp_gpu_mq {
     uint32_t *tickets;             // device, one per slot
     // byte offsets inside each slot's pinned block (H) and device block (D)
     uint64_t h_mb, h_off, h_len, h_md, h_edge, h_rec, h_rmd, h_stage, h_bst, h_bytes;
-    int hostwb;                    // zc cnet with CNDP_MQ_F_HOST_WRITEBACK
+    int hostwb;                    // zc cnet / ip4_lookup with CNDP_MQ_F_HOST_WRITEBACK
     uint64_t d_nh, d_edge, d_pt, d_rm, d_hash, d_ipl, d_win, d_off, d_len, d_md, d_bytes;
     int devhdr;                    // zc with CNDP_MQ_F_DEVICE_HEADERS (ip4_lookup, cnet)
     // cnet device headers: pools seen whose conf.metadata(m) is m + 64 (and
@@ -7555,8 +7557,12 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     if (k.flags & ~(CNDP_MQ_F_HASH | CNDP_MQ_F_NO_METADATA | CNDP_MQ_F_DEVICE_HEADERS | CNDP_MQ_F_RX_PARSE |
                     CNDP_MQ_F_REWRITE | CNDP_MQ_F_HOST_WRITEBACK))
         return -EINVAL;
+    // host writeback: cnet and ip4_lookup; cnet's poll reads the header fields
+    // it adjusts, so its headers stay on the host, while ip4_lookup's poll only
+    // stores (packet_type, udata64), so its headers may be the device's
     if ((k.flags & CNDP_MQ_F_HOST_WRITEBACK) &&
-        (k.mode != CNDP_MQ_CNET || (k.flags & CNDP_MQ_F_DEVICE_HEADERS)))
+        ((k.mode != CNDP_MQ_CNET && k.mode != CNDP_MQ_IP4_LOOKUP) ||
+         (k.mode == CNDP_MQ_CNET && (k.flags & CNDP_MQ_F_DEVICE_HEADERS))))
         return -EINVAL;
     if ((k.flags & (CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE)) && k.mode != CNDP_MQ_IP4_LOOKUP)
         return -EINVAL;
@@ -7608,10 +7614,10 @@ extern "C" int cndp_gpu_mq_create(cndp_gpu_ctx_t *c, const struct cndp_mq_conf *
     q->h_len = q->h_off + al64(B * 8);                    // cnet: length fields; rewrite: priv1
     q->h_md = q->h_len + (cnet || rw ? al64(B * 8) : 0);  // cnet zc: metadata addresses
     q->h_edge = q->h_md + (cnet && zc ? al64(B * 8) : 0);
-    q->hostwb = zc && cnet && (k.flags & CNDP_MQ_F_HOST_WRITEBACK);
+    q->hostwb = zc && (k.flags & CNDP_MQ_F_HOST_WRITEBACK);
     q->h_rec = q->h_edge + al64(B * 2);                   // staged (and host writeback): records
     q->h_rmd = q->h_rec + ((zc && !q->hostwb) || rw || k.mode == CNDP_MQ_MAC_SWAP ? 0 : al64(B * (cnet ? 16 : 8)));
-    q->h_stage = q->h_rmd + (q->hostwb ? B * 32 : 0);     // host writeback: metadata addresses
+    q->h_stage = q->h_rmd + (q->hostwb && cnet ? B * 32 : 0); // cnet host writeback: metadata addresses
     q->h_bst = q->h_stage + B * q->stage;                 // CNDP_MQ_F_REWRITE: burst starts
     q->h_bytes = q->h_bst + ((k.flags & CNDP_MQ_F_REWRITE) ? al64((B + 1) * 4) : 0);
     q->d_nh = 0;
@@ -7757,7 +7763,7 @@ static int mq_launch_kernels(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t slot_i)
     a.priv1 = (uint64_t *)(HD + q->h_rec);
     a.rec = (u32x4 *)(HD + q->h_rec);
     a.hostwb = (uint32_t)q->hostwb;
-    a.rec_md = q->hostwb && !(q->conf.flags & CNDP_MQ_F_NO_METADATA) ? (u32x4 *)(HD + q->h_rmd) : nullptr;
+    a.rec_md = q->hostwb && cnet && !(q->conf.flags & CNDP_MQ_F_NO_METADATA) ? (u32x4 *)(HD + q->h_rmd) : nullptr;
     a.lport = q->conf.lport;
     a.want_hash = (q->conf.flags & CNDP_MQ_F_HASH) != 0;
     a.ticket = q->tickets + slot_i;
@@ -8137,11 +8143,42 @@ static void mq_save_md_host(uint8_t *md, const uint8_t *ip, bool v6)
 
 // one finished slot's results into its mbufs where the kernels did not
 // write them (staged: every field; zero-copy cnet: metadata the device could
-// not reach; zero-copy cnet with host writeback: every field, from records)
+// not reach; zero-copy with host writeback: every field, from records)
 static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
 {
     const uint32_t mode = q->conf.mode;
     const uint16_t *ed = (const uint16_t *)(sl->h + q->h_edge);
+    if (mode == CNDP_MQ_IP4_LOOKUP && (q->hostwb || !q->zc)) {
+        // node_mbuf_priv1 (ip4_lookup.c:144-154) and, with the soft parse,
+        // packet_type: staged from the staged ethertype, host writeback from
+        // the record (pkt_cls's drops carry their packet_type there)
+        const uint64_t *priv1 = (const uint64_t *)(sl->h + q->h_rec);
+        const uint64_t *ho = (const uint64_t *)(sl->h + q->h_off);
+        const bool rxp = (q->conf.flags & CNDP_MQ_F_RX_PARSE) != 0;
+        for (uint32_t i = i0; i < i1; i++) {
+            if (i + MQ_PF < i1)
+                __builtin_prefetch((uint8_t *)sl->mb[i + MQ_PF] + MB_UDATA64, 1);
+            if (ed[i] == MQ_EDGE_NONE) // zero-copy: outside every registered region, untouched
+                continue;
+            uint8_t *m = (uint8_t *)sl->mb[i];
+            const bool cls_drop = ed[i] == CNDP_MQ_EDGE_CLS_DROP;
+            if (rxp) {
+                uint32_t pt;
+                if (q->hostwb) {
+                    pt = cls_drop ? (uint32_t)priv1[i] : 0x90u;
+                } else {
+                    const uint8_t *e = sl->h + q->h_stage + ho[i];
+                    const uint32_t et = ((uint32_t)e[0] << 8) | e[1];
+                    pt = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
+                }
+                *(uint32_t *)(m + MB_PTYPE) = pt;
+                if (cls_drop) // pkt_cls dropped it: ip4_lookup never saw it
+                    continue;
+            }
+            *(uint64_t *)(m + MB_UDATA64) = priv1[i];
+        }
+        return;
+    }
     if (q->hostwb) {
         const uint32_t *rec = (const uint32_t *)(sl->h + q->h_rec);
         const uint8_t *rmd = sl->h + q->h_rmd;
@@ -8210,24 +8247,6 @@ static void mq_writeback(cndp_gpu_mq_t *q, MqSlot *sl, uint32_t i0, uint32_t i1)
             const uint16_t blen = *(const uint16_t *)(m + MB_BUF_LEN);
             const uint32_t room = blen > doff ? (uint32_t)(blen - doff) : 0u;
             memcpy(buf + doff, sl->h + q->h_stage + ho[i], room < span ? room : span);
-        }
-        return;
-    }
-    if (mode == CNDP_MQ_IP4_LOOKUP) {
-        const uint64_t *priv1 = (const uint64_t *)R;
-        const bool rxp = (q->conf.flags & CNDP_MQ_F_RX_PARSE) != 0;
-        for (uint32_t i = i0; i < i1; i++) { // node_mbuf_priv1 (ip4_lookup.c:144-154)
-            if (i + MQ_PF < i1)
-                __builtin_prefetch((uint8_t *)sl->mb[i + MQ_PF] + MB_UDATA64, 1);
-            uint8_t *m = (uint8_t *)sl->mb[i];
-            if (rxp) { // the soft parse's packet_type, from the staged ethertype
-                const uint8_t *e = sl->h + q->h_stage + ho[i];
-                const uint32_t et = ((uint32_t)e[0] << 8) | e[1];
-                *(uint32_t *)(m + MB_PTYPE) = et == 0x0800u ? 0x90u : et == 0x86DDu ? 0xE0u : 0u;
-                if (ed[i] == CNDP_MQ_EDGE_CLS_DROP) // pkt_cls dropped it: ip4_lookup never saw it
-                    continue;
-            }
-            *(uint64_t *)(m + MB_UDATA64) = priv1[i];
         }
         return;
     }

@@ -115,8 +115,10 @@ static struct rw_graph_state *rw_state_get(const struct cne_graph *graph)
     conf.max_delay_us = env_u32("CNDP_GPU_DELAY_US", 50);
     /* the kernel reads each mbuf header (buf_addr, data_off, node_mbuf_priv1)
      * itself; CNDP_GPU_RW_MQ_FLAGS (else CNDP_GPU_MQ_FLAGS) = 0 for the
-     * host-header path */
-    conf.flags = env_u32("CNDP_GPU_RW_MQ_FLAGS", env_u32("CNDP_GPU_MQ_FLAGS", CNDP_MQ_F_DEVICE_HEADERS));
+     * host-header path; the receive nodes' result form
+     * (CNDP_MQ_F_HOST_WRITEBACK) is not one of this queue's */
+    conf.flags = env_u32("CNDP_GPU_RW_MQ_FLAGS", env_u32("CNDP_GPU_MQ_FLAGS", CNDP_MQ_F_DEVICE_HEADERS)) &
+                 ~CNDP_MQ_F_HOST_WRITEBACK;
     void *umem = NULL;
     uint64_t ulen = 0;
     for (uint32_t i = 0; cndp_node_gpu_umem_get(i, &umem, &ulen) == 0; i++)

@@ -54,7 +54,8 @@
  * Tuning from the environment: CNDP_GPU_DEVICE (0), CNDP_GPU_BATCH (8192),
  * CNDP_GPU_DEPTH (4), CNDP_GPU_DELAY_US (50), CNDP_GPU_MQ_FLAGS (the
  * queue's flags besides CNDP_MQ_F_RX_PARSE; default CNDP_MQ_F_DEVICE_HEADERS
- * for up to two receive nodes, host headers for more -- see init).  Frames are read in place when the application
+ * for up to two receive nodes, host headers for three or four, host
+ * writeback beyond -- see init).  Frames are read in place when the application
  * registered its UMEMs with cndp_node_gpu_umem_add(), else staged.  One GPU
  * context and queue per cloned node (per port and graph).
  *
@@ -92,6 +93,7 @@ enum {
 };
 #define RX_EDGES_MAX 64 /* GPU_NODE_EDGES_MAX */
 #define RX_DEVICE_HEADERS_MAX 2
+#define RX_HOST_WB_MIN 4
 
 static struct pktdev_rx_node_main pktdev_rx_main;
 
@@ -247,13 +249,18 @@ static int pktdev_rx_gpu_init(const struct cne_graph *graph, struct cne_node *no
      * lcores near 110 Mpps however many there are, while host headers add a
      * header read on each lcore and leave one frame read for the device
      * (bench node_lcores: 60 / 103 / 108 / 110 Mpps at 1 / 2 / 4 / 8 lcores
-     * against 54 / 102 / 150 / 163).  The clones pktdev_ctrl.c registered,
-     * one per port, are the receive nodes the application runs. */
+     * against 54 / 102 / 150 / 163).  Beyond RX_HOST_WB_MIN the results come
+     * back as records the lcores' polls write (CNDP_MQ_F_HOST_WRITEBACK): the
+     * device's reads of the frames are then its only small transactions
+     * (205-209 against 168-169 Mpps at 8 lcores, even at 4).  The clones
+     * pktdev_ctrl.c registered, one per port, are the receive nodes the
+     * application runs. */
     uint32_t n_rx = 0;
     for (pktdev_rx_node_elem_t *e = pktdev_rx_main.head; e; e = e->next)
         n_rx++;
-    conf.flags = CNDP_MQ_F_RX_PARSE |
-                 env_u32("CNDP_GPU_MQ_FLAGS", n_rx > RX_DEVICE_HEADERS_MAX ? 0u : CNDP_MQ_F_DEVICE_HEADERS);
+    conf.flags = CNDP_MQ_F_RX_PARSE | env_u32("CNDP_GPU_MQ_FLAGS", n_rx > RX_HOST_WB_MIN          ? CNDP_MQ_F_HOST_WRITEBACK
+                                                                   : n_rx > RX_DEVICE_HEADERS_MAX ? 0u
+                                                                                                  : CNDP_MQ_F_DEVICE_HEADERS);
     /* zero-copy: the kernels read the frames in the UMEMs (registration is
      * shared and counted across the per-port contexts) */
     void *umem = NULL;

@@ -253,14 +253,18 @@ typedef struct cndp_gpu_mq cndp_gpu_mq_t;
  * hop's tx_node (ip4_rewrite's edge index, 0 pkt_drop); an mbuf ip4_lookup
  * sent elsewhere (pkt_drop) comes back with CNDP_MQ_EDGE_LOOKUP_DROP. */
 #define CNDP_MQ_F_REWRITE (1u << 4)
-/* cnet, zero-copy with host headers: the kernels still read each frame in
- * place, but the results -- the fields eth_rx and the input nodes write and
- * the cnet_metadata addresses -- come back as coalesced records that poll
- * writes into the mbufs on the calling lcore, instead of three to five small
- * posted stores a mbuf from the device.  The device's PCIe transaction rate,
- * which bounds the zero-copy forms summed over lcores, then carries one read
- * a frame; the lcores' writes scale with the lcores.  Same
- * fields, same values; -EINVAL with CNDP_MQ_F_DEVICE_HEADERS. */
+/* cnet and ip4_lookup, zero-copy with host headers: the kernels still read
+ * each frame in place, but the results -- cnet: the fields eth_rx and the
+ * input nodes write and the cnet_metadata addresses; ip4_lookup: udata64 and,
+ * with CNDP_MQ_F_RX_PARSE, packet_type -- come back as coalesced records that
+ * poll writes into the mbufs on the calling lcore, instead of small posted
+ * stores a mbuf from the device (cnet three to five, ip4_lookup one or two).
+ * The device's PCIe transaction rate, which bounds the zero-copy forms summed
+ * over lcores, then carries one read a frame (plus, with CNDP_MQ_F_REWRITE,
+ * the frame's rewrite); the lcores' writes scale with the lcores (DESIGN.md
+ * §6).  Same fields, same values.  cnet: -EINVAL with CNDP_MQ_F_DEVICE_HEADERS
+ * (poll reads the header fields it adjusts); ip4_lookup takes both (the device
+ * reads header and frame, poll only stores). */
 #define CNDP_MQ_F_HOST_WRITEBACK (1u << 5)
 #define CNDP_MQ_EDGE_LOOKUP_DROP 0xFFFDu
 #define CNDP_MQ_NODE_PTYPE 0u

@@ -74,14 +74,22 @@ def _mixed_l3_frames(n, seed):
     return pktgen.Frames(slab.reshape(-1), n, stride=64)
 
 
-@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
+def _l3_flags(zero_copy):
+    return {"device_headers": N.CNDP_MQ_F_DEVICE_HEADERS,
+            "host_writeback": N.CNDP_MQ_F_HOST_WRITEBACK,
+            "device_headers_host_writeback": N.CNDP_MQ_F_DEVICE_HEADERS | N.CNDP_MQ_F_HOST_WRITEBACK}.get(zero_copy, 0)
+
+
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers", "host_writeback", "device_headers_host_writeback"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
     """"shifted": data_off = 256 + (i mod 61), so frames start at every
     alignment and line position (the kernel's one-load and byte-wise reads).
     "device_headers": zero-copy with CNDP_MQ_F_DEVICE_HEADERS (the kernel reads
-    each mbuf header itself)."""
-    flags = N.CNDP_MQ_F_DEVICE_HEADERS if zero_copy == "device_headers" else 0
+    each mbuf header itself); "host_writeback": zero-copy with
+    CNDP_MQ_F_HOST_WRITEBACK (frames read in place, udata64 written by poll
+    from the records), with or without device headers."""
+    flags = _l3_flags(zero_copy)
     cl, fib, t4 = l3
     n = 20000
     pool = MbufPool(n)
@@ -118,15 +126,16 @@ def test_mq_ip4_lookup(l3, gpu, zero_copy, kind):
     assert (edges == 1).sum() > 0 and (edges == 0).sum() > 0
 
 
-@pytest.mark.parametrize("zero_copy", [True, False, "device_headers"])
+@pytest.mark.parametrize("zero_copy", [True, False, "device_headers", "host_writeback", "device_headers_host_writeback"])
 @pytest.mark.parametrize("kind", ["full", "shifted"])
 def test_mq_ip4_lookup_rx_parse(l3, gpu, zero_copy, kind):
     """CNDP_MQ_F_RX_PARSE: the queue also does l3fwd-graph's pktdev_rx soft
     parse (packet_type from the ethertype, pktdev_rx.c:24-34) and pkt_cls
     (only IPv4 goes on to ip4_lookup, pkt_cls.c:19-31) -- against the oracle's
     chain over the same mbufs: packet_type everywhere, priv1 only where
-    ip4_lookup ran, edge CNDP_MQ_EDGE_CLS_DROP where pkt_cls dropped."""
-    flags = N.CNDP_MQ_F_RX_PARSE | (N.CNDP_MQ_F_DEVICE_HEADERS if zero_copy == "device_headers" else 0)
+    ip4_lookup ran, edge CNDP_MQ_EDGE_CLS_DROP where pkt_cls dropped (with
+    host writeback the packet_type of those comes back in the record)."""
+    flags = N.CNDP_MQ_F_RX_PARSE | _l3_flags(zero_copy)
     cl, fib, t4 = l3
     n = 12000
     gp, op = MbufPool(n), MbufPool(n)
@@ -369,14 +378,18 @@ def test_mq_cnet(cn, gpu, zero_copy, kind):
 
 
 def test_mq_host_writeback_flag_rules(cn, gpu):
-    """CNDP_MQ_F_HOST_WRITEBACK is a cnet-queue flag and excludes device
-    headers (the lcore reads the headers it writes back into)."""
+    """CNDP_MQ_F_HOST_WRITEBACK is a cnet / ip4_lookup queue flag; cnet's
+    excludes device headers (its poll reads the header fields it adjusts),
+    ip4_lookup's takes them (its poll only stores)."""
     cl = cn[0]
     with pytest.raises(OSError):
         MbufQueue(cl, N.CNDP_MQ_CNET, flags=N.CNDP_MQ_F_HOST_WRITEBACK | N.CNDP_MQ_F_DEVICE_HEADERS)
-    with pytest.raises(OSError):
-        MbufQueue(cl, N.CNDP_MQ_MAC_SWAP, flags=N.CNDP_MQ_F_HOST_WRITEBACK)
-    MbufQueue(cl, N.CNDP_MQ_CNET, flags=N.CNDP_MQ_F_HOST_WRITEBACK).close()   # staged: writes back anyway
+    MbufQueue(cl, N.CNDP_MQ_IP4_LOOKUP, flags=N.CNDP_MQ_F_HOST_WRITEBACK | N.CNDP_MQ_F_DEVICE_HEADERS).close()
+    for mode in (N.CNDP_MQ_CNET, N.CNDP_MQ_IP4_LOOKUP):
+        MbufQueue(cl, mode, flags=N.CNDP_MQ_F_HOST_WRITEBACK).close()   # staged: writes back anyway
+    for mode in (N.CNDP_MQ_MAC_SWAP, N.CNDP_MQ_IP4_REWRITE):
+        with pytest.raises(OSError):
+            MbufQueue(cl, mode, flags=N.CNDP_MQ_F_HOST_WRITEBACK)
 
 
 def test_mq_cnet_spec_wait_expiry(cn, gpu):
@@ -797,7 +810,7 @@ def test_mq_ip4_rewrite(l3, gpu, zero_copy, kind):
 
 
 @pytest.mark.parametrize("rx_parse", [True, False], ids=["rx_chain", "lookup"])
-@pytest.mark.parametrize("headers", ["host", "device"])
+@pytest.mark.parametrize("headers", ["host", "device", "host_writeback", "device_host_writeback"])
 @pytest.mark.parametrize("kind", ["full", "ragged", "shifted"])
 def test_mq_l3fwd_fused(l3, gpu, headers, kind, rx_parse):
     """CNDP_MQ_F_RX_PARSE | CNDP_MQ_F_REWRITE: l3fwd-graph's pktdev_rx soft
@@ -807,7 +820,9 @@ def test_mq_l3fwd_fused(l3, gpu, headers, kind, rx_parse):
     0xFFFE / 0xFFFF and high-bit cksum words seeded, where the 4-wide and
     tail rules differ), edges = the next hop's tx_node, LOOKUP_DROP, CLS_DROP.
     lookup: CNDP_MQ_F_REWRITE alone (the GPU ip4_lookup node's fused mode):
-    every mbuf through ip4_lookup's loop, packet_type untouched."""
+    every mbuf through ip4_lookup's loop, packet_type untouched.
+    host_writeback: the frames rewritten in place by the device, udata64 and
+    packet_type written by poll."""
     cl, fib, t4 = l3
     tbl = _rewrite_setup(cl, 41)
     n = 12000
@@ -823,7 +838,8 @@ def test_mq_l3fwd_fused(l3, gpu, headers, kind, rx_parse):
             p.mem[d[sel] + 24] = lo
             p.mem[d[sel] + 25] = 0xFF
     flags = ((N.CNDP_MQ_F_RX_PARSE if rx_parse else 0) | N.CNDP_MQ_F_REWRITE |
-             (N.CNDP_MQ_F_DEVICE_HEADERS if headers == "device" else 0))
+             (N.CNDP_MQ_F_DEVICE_HEADERS if headers.startswith("device") else 0) |
+             (N.CNDP_MQ_F_HOST_WRITEBACK if headers.endswith("host_writeback") else 0))
     bursts = _bursts(n, 43, kind)
     order = np.random.default_rng(44).permutation(n)
     cl.host_register(gp.mem)
@@ -867,7 +883,9 @@ def test_mq_l3fwd_fused(l3, gpu, headers, kind, rx_parse):
         assert N.CNDP_MQ_EDGE_CLS_DROP not in set(np.unique(edges).tolist())
 
 
-@pytest.mark.parametrize("flags", [0, N.CNDP_MQ_F_DEVICE_HEADERS], ids=["host_headers", "device_headers"])
+@pytest.mark.parametrize("flags", [0, N.CNDP_MQ_F_DEVICE_HEADERS, N.CNDP_MQ_F_HOST_WRITEBACK,
+                                   N.CNDP_MQ_F_DEVICE_HEADERS | N.CNDP_MQ_F_HOST_WRITEBACK],
+                         ids=["host_headers", "device_headers", "host_writeback", "device_headers_host_writeback"])
 def test_mq_zero_copy_regions(l3, gpu, flags):
     """Zero-copy over several registered regions (a graph's ports with pools
     of their own): mbufs of two registered pools interleaved in one queue get

@@ -919,8 +919,8 @@ def test_rx_node_init_fails_loudly_without_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zero_copy", [True, "host_headers", "no_rewrite", False, "driver_writes",
-                                       "driver_writes_host_headers"])
+@pytest.mark.parametrize("zero_copy", [True, "host_headers", "host_writeback", "device_headers_host_writeback",
+                                       "no_rewrite", False, "driver_writes", "driver_writes_host_headers"])
 def test_rx_node_graph_walk(gpu, zero_copy):
     """Graph walks over the GPU pktdev_rx node: it pulls 256-mbuf bursts from
     its port and every mbuf ends where l3fwd-graph's pktdev_rx -> pkt_cls ->
@@ -937,7 +937,9 @@ def test_rx_node_graph_walk(gpu, zero_copy):
     driver_writes*: the receive stub writes each mbuf's data_len / data_off
     as xskdev's receive does (xskdev.c:296-297), so the node gets header lines
     dirty in the host core's cache, as pktdev_rx.c:107-125 does in a real
-    graph."""
+    graph.  host_writeback (CNDP_GPU_MQ_FLAGS=CNDP_MQ_F_HOST_WRITEBACK, with or
+    without CNDP_MQ_F_DEVICE_HEADERS): the frames read and rewritten in place,
+    packet_type and priv1 written by the node's polls from the queue's records."""
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
     from cndp_amd import pktgen
@@ -969,9 +971,14 @@ def test_rx_node_graph_walk(gpu, zero_copy):
     os.environ["CNDP_GPU_BATCH"] = "4096"
     if zero_copy in ("host_headers", "driver_writes_host_headers"):
         os.environ["CNDP_GPU_MQ_FLAGS"] = "0"
+    if zero_copy == "host_writeback":
+        os.environ["CNDP_GPU_MQ_FLAGS"] = str(N.CNDP_MQ_F_HOST_WRITEBACK)
+    if zero_copy == "device_headers_host_writeback":
+        os.environ["CNDP_GPU_MQ_FLAGS"] = str(N.CNDP_MQ_F_HOST_WRITEBACK | N.CNDP_MQ_F_DEVICE_HEADERS)
     if zero_copy == "no_rewrite":
         os.environ["CNDP_GPU_RX_REWRITE"] = "0"
-    fused = zero_copy in (True, "host_headers", "driver_writes", "driver_writes_host_headers")
+    fused = zero_copy in (True, "host_headers", "host_writeback", "device_headers_host_writeback", "driver_writes",
+                          "driver_writes_host_headers")
     H.harness_rx_driver_writes.argtypes = [ctypes.c_int]
     H.harness_rx_driver_writes(int(str(zero_copy).startswith("driver_writes")))
     routes = pktgen.l3fwd_routes()
@@ -1225,15 +1232,20 @@ def _destroy_graphs(H, graphs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [2, 4])
-def test_rx_node_graphs_per_lcore(gpu, threads):
+@pytest.mark.parametrize("threads,form", [(2, None), (4, None), (6, None), (4, "host_writeback"),
+                                          (4, "device_headers_host_writeback")],
+                         ids=["2", "4", "6", "4-host_writeback", "4-device_headers_host_writeback"])
+def test_rx_node_graphs_per_lcore(gpu, threads, form):
     """`threads` worker lcores, each its own l3fwd-graph graph -- "ip4*",
     "pkt_cls" and its port's pktdev_rx clone (pktdev_ctrl.c:40-64) -- created
     and walked at the same time over disjoint UMEM pools: every mbuf of every
     pool leaves on the edge of the reference chain over that pool
     (pktdev_rx -> pkt_cls -> ip4_lookup -> ip4_rewrite per 256-mbuf burst),
     with its packet_type, priv1 and rewritten frame; each graph's pkt_cls /
-    ip4_lookup / ip4_rewrite get the stats of their own pool."""
+    ip4_lookup / ip4_rewrite get the stats of their own pool.  form: the
+    node's default for that many receive nodes (device headers at 2, host
+    headers at 4, host writeback at 6), or the queues with
+    CNDP_MQ_F_HOST_WRITEBACK (each lcore's polls write its mbufs)."""
     from cndp_amd.fib import NodeFib, cne_node_ip4_route_add
     from cndp_amd.mbuf import MbufPool
     from cndp_amd import pktgen
@@ -1262,6 +1274,9 @@ def test_rx_node_graphs_per_lcore(gpu, threads):
         assert cid != 0xFFFFFFFF and H.harness_pktdev_rx_port(cid, k) == 0
         assert H.harness_rx_load(k, gp.ptrs(np.arange(n)), n) == 0
     os.environ["CNDP_GPU_BATCH"] = "4096"
+    if form:
+        os.environ["CNDP_GPU_MQ_FLAGS"] = str(N.CNDP_MQ_F_HOST_WRITEBACK |
+                                              (N.CNDP_MQ_F_DEVICE_HEADERS if form.startswith("device") else 0))
     routes = pktgen.l3fwd_routes()
     names = [b"pkt_drop"] + [f"pktdev_tx-{p}".encode() for p in ports]
     graphs = []
@@ -1292,6 +1307,7 @@ def test_rx_node_graphs_per_lcore(gpu, threads):
     finally:
         _destroy_graphs(H, graphs)
         os.environ.pop("CNDP_GPU_BATCH", None)
+        os.environ.pop("CNDP_GPU_MQ_FLAGS", None)
         H.harness_chain(0)
         H.harness_drop_clones()
         H.harness_pktdev_rx_ports_reset()
@@ -1322,7 +1338,7 @@ def test_rx_node_graphs_per_lcore(gpu, threads):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [2, 4])
+@pytest.mark.parametrize("threads", [2, 4, 6])
 def test_cnet_node_graphs_per_lcore(gpu, threads):
     """`threads` cnet-graph lcores, each with a graph over its port's eth_rx
     clone (pkt_ctrl.c:55-72), created and walked at the same time over
@@ -1330,7 +1346,8 @@ def test_cnet_node_graphs_per_lcore(gpu, threads):
     gets the fields eth_rx and the input nodes write and leaves on the edge
     the reference's ptype / ip4_input / ip6_input send it to -- the ptype
     node's state is each graph's own, so each pool equals the oracle chain
-    from state 0 over its own bursts."""
+    from state 0 over its own bursts.  At 6 the node's default result form is
+    host writeback (beyond four receive nodes)."""
     from helpers import CNET_DEF, cnet_fibs
     from oracle import oracle as O
     from test_gpu_mq import _bursts, _cnet_expect, cnet_check, cnet_pool
