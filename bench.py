@@ -928,6 +928,9 @@ def node_boundary(dev, n: int = 1 << 20, burst: int = 256, passes: int = 3):
     l3["cpu_chain"] = ("the ip4_lookup node loop over the same mbufs on one core (oracle/oracle.c "
                        "orc_ip4_lookup_mbufs); primary form with the receive driver's header writes and "
                        "pktdev_rx's soft parse before each burst (orc_rx_ip4_lookup_mbufs), as the GPU legs")
+    l3["supported_build"] = ("no: the GPU ip4_lookup node behind CNDP's own pktdev_rx is measured for the "
+                             "record; cndp_amd/node/ip4_lookup_gpu.c links only with pktdev_rx_gpu.c, so an "
+                             "l3fwd-graph build gets l3fwd_rx_chain's node (INTEGRATION.md section 2)")
     NodeFib.fini()
     res["l3fwd_ip4_lookup"] = l3
     # ---- l3fwd: the ip4_lookup + ip4_rewrite node pair, chained as a graph
